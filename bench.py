@@ -1,0 +1,293 @@
+#!/usr/bin/env python3
+"""bench.py -- DQN learn-step throughput (transitions/s) on MI355X through libdqnx.
+
+Workload (BASELINE.json configs[1]): synthetic 1ramp_1x3 state vectors (D=284, A=8),
+MLP(256,128) dueling Q-net, fp32, DuelingDoubleDQNAgent learn step, minibatch 1024 per
+GPU sampled from a GPU-resident replay ring of 1e6 transitions.  One "step" = one
+Agent.learn() + update_target_network() (R:train.py:99-101): sample (bit-exact CPython
+random.sample) -> gather -> online(s'), target(s'), online(s) -> Double-DQN TD target ->
+Huber -> backward -> Adam -> soft target update.
+
+    python bench.py [--gpus N --steps K --warmup W]
+    torchrun --nproc-per-node N bench.py --gpus N ...    (one process per GPU, RCCL)
+
+Data parallel = weak scaling: every rank processes `--batch` transitions per step; all
+ranks draw the same global index set (batch * N) from the same MT19937 state and take
+their shard; gradients are summed with one RCCL all-reduce per step.
+
+Prints ONE JSON line on rank 0 (fields: see the driver contract in DESIGN.md).
+"""
+import argparse
+import ctypes
+import json
+import os
+import random
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.nn as nn
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "multimodal-drl-rmc_amd"))
+
+from dqn import _capi as C  # noqa: E402
+from dqn.engine import LearnEngine, mlp_spec  # noqa: E402
+
+PEAK_FP32_MFMA_TFLOPS = 157.3   # MI355X_MICROARCH.md: F32 matrix, dense
+PEAK_HBM_GBS = 8000.0           # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=200)
+    p.add_argument("--warmup", type=int, default=20)
+    p.add_argument("--batch", type=int, default=1024, help="transitions per GPU per step")
+    p.add_argument("--capacity", type=int, default=1_000_000)
+    p.add_argument("--obs-dim", type=int, default=284)
+    p.add_argument("--actions", type=int, default=8)
+    p.add_argument("--algo", default="DuelingDoubleDQNAgent")
+    p.add_argument("--no-graphs", action="store_true")
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--cpu-seconds", type=float, default=15.0)
+    p.add_argument("--no-kernel-timing", action="store_true")
+    return p.parse_args()
+
+
+def init_params(spec, seed=0):
+    """Random init of the Q-net architecture (torch default Linear init)."""
+    torch.manual_seed(seed)
+    d = spec.obs_dim
+    mods = {}
+    for i, w in enumerate(spec.dense):
+        mods[f"net.{2 * i}"] = nn.Linear(d, w)
+        d = w
+    if spec.head == C.DQNX_HEAD_DUELING:
+        mods["fc_val"] = nn.Linear(d, 1)
+        mods["fc_adv"] = nn.Linear(d, spec.n_actions)
+    else:
+        mods["fc_out"] = nn.Linear(d, spec.n_actions)
+    sd = {}
+    for k, m in mods.items():
+        sd[k + ".weight"] = m.weight.detach()
+        sd[k + ".bias"] = m.bias.detach()
+    return sd
+
+
+def fill_ring(eng, n, D, A, device, seed=0, chunk=1 << 16):
+    """Synthetic 1ramp_1x3-shaped transitions generated on the GPU:
+    macro U[0,1); micro grid occupancy ~ Bernoulli(0.2) with speed U[0,1); action U{0..A-1};
+    reward U[-24,3]; done ~ Bernoulli(1/90)."""
+    g = torch.Generator(device=device)
+    g.manual_seed(seed)
+    macro = min(14, D)
+
+    def obs_block(m):
+        o = torch.empty(m, D, device=device)
+        o[:, :macro] = torch.rand(m, macro, generator=g, device=device)
+        if D > macro:
+            occ = torch.rand(m, D - macro, generator=g, device=device) < 0.2
+            spd = torch.rand(m, D - macro, generator=g, device=device)
+            o[:, macro:] = torch.where(occ, spd, torch.zeros((), device=device))
+        return o
+
+    done_rows = 0
+    while done_rows < n:
+        m = min(chunk, n - done_rows)
+        obs, nobs = obs_block(m), obs_block(m)
+        act = torch.randint(0, A, (m,), generator=g, device=device, dtype=torch.int32)
+        rew = torch.rand(m, generator=g, device=device) * 27.0 - 24.0
+        done = (torch.rand(m, generator=g, device=device) < 1.0 / 90.0).to(torch.uint8)
+        eng.push(obs, act, rew, done, nobs)
+        done_rows += m
+    torch.cuda.synchronize()
+
+
+def cpu_baseline(args):
+    """The oracle's torch-CPU restatement of the same learn step (reference algorithm:
+    deque + random.sample + transitions_to_tensor + 3 forwards + Huber + autograd + Adam +
+    soft update), timed on this host's cores on a bounded sample."""
+    sys.path.insert(0, REPO)
+    from oracle import ref as O
+    spec = O.mlp_spec(args.obs_dim, args.actions, "dueling")
+    L = O.OracleLearner(spec, args.algo, args.batch, args.capacity, seed=0)
+    obs, act, rew, done, nobs = O.synth_transitions(args.capacity, args.obs_dim, args.actions, seed=0)
+    L.replay.replay_buffer.extend(zip(obs, act, rew, done, nobs))
+    random.seed(1234)
+    L.py_state = O.py_state_to_array()
+    for _ in range(2):
+        L.train_step()
+    t0 = time.perf_counter()
+    steps = 0
+    while True:
+        L.train_step()
+        steps += 1
+        el = time.perf_counter() - t0
+        if el >= args.cpu_seconds and steps >= 3:
+            break
+    return {"value": args.batch * steps / el, "unit": "transitions/s", "cores": torch.get_num_threads(),
+            "kind": "port",
+            "sample": f"oracle/ref.py OracleLearner {args.algo} MLP-{args.obs_dim} batch {args.batch}, "
+                      f"deque of {args.capacity} transitions, {steps} learn+soft-update steps in {el:.1f} s, "
+                      f"torch {torch.__version__} CPU, {torch.get_num_threads()} threads"}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.gpus != world and world > 1:
+        log(f"warning: --gpus {args.gpus} != WORLD_SIZE {world}; using WORLD_SIZE")
+    torch.cuda.set_device(local_rank)
+    device = torch.device("cuda", local_rank)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=device)
+
+    spec = mlp_spec(args.obs_dim, args.actions, "dueling" if "Dueling" in args.algo else "linear")
+    Bg = args.batch * world
+    eng = LearnEngine(spec, args.algo, Bg, args.capacity, world_size=world, rank=rank, device=device,
+                      graphs=not args.no_graphs)
+    eng.load_params(init_params(spec, 0))
+    fill_ring(eng, args.capacity, args.obs_dim, args.actions, device, seed=0)
+    random.seed(1234)   # the replay sampler continues CPython's global MT19937 stream
+    eng.set_rng(C.DQNX_RNG_PY, np.array(random.getstate()[1], dtype=np.uint32))
+
+    def step():
+        if world > 1:
+            eng.learn_step(grads_only=True)
+            dist.all_reduce(eng.grads)
+            eng.apply_grads(soft_update=True)
+        else:
+            eng.learn_step(soft_update=True)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    eng.check_device_error()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    if dist:
+        t = torch.tensor([el], device=device, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    eng.check_device_error()
+    loss = eng.loss()
+    ms_per_step = el / args.steps * 1e3
+    value = Bg * args.steps / el
+
+    # ---- dominant-kernel roofline: HIP events around one kernel inside full steps ----
+    roofline = None
+    kernels = []
+    if not args.no_kernel_timing:
+        flags = C.STEP_GRADS_ONLY if world > 1 else C.STEP_SOFT_UPDATE
+        L = C.lib()
+        n = C.I32()
+        C.check(L.dqnx_learn_kernel_count(eng.h, flags, ctypes.byref(n)), "kernel_count")
+        infos = []
+        for i in range(n.value):
+            nm = ctypes.create_string_buffer(64)
+            fl, by = ctypes.c_double(), ctypes.c_double()
+            C.check(L.dqnx_learn_kernel_info(eng.h, flags, i, nm, 64, ctypes.byref(fl), ctypes.byref(by)), "info")
+            infos.append((nm.value.decode(), fl.value, by.value))
+        K = max(args.steps, 20)
+        evs = (ctypes.c_void_p * (2 * K))()
+        C.check(L.dqnx_events_create(2 * K, evs), "events")
+
+        def timed_steps(ki, count):
+            for j in range(count):
+                C.check(L.dqnx_learn_step_timed(eng.h, flags, ki, evs[2 * j], evs[2 * j + 1], eng.stream()),
+                        "timed step")
+                if world > 1:
+                    dist.all_reduce(eng.grads)
+                    eng.apply_grads(soft_update=True)
+            torch.cuda.synchronize()
+            tot = 0.0
+            for j in range(count):
+                ms = ctypes.c_float()
+                C.check(L.dqnx_event_elapsed(evs[2 * j], evs[2 * j + 1], ctypes.byref(ms)), "elapsed")
+                tot += ms.value
+            return tot / count
+
+        for i, (nm, fl, by) in enumerate(infos):
+            kernels.append({"kernel": nm, "avg_us": timed_steps(i, 20) * 1e3, "flops": fl, "bytes": by})
+        dom = max(range(len(kernels)), key=lambda i: kernels[i]["avg_us"])
+        avg_ms = timed_steps(dom, K)
+        kernels[dom]["avg_us"] = avg_ms * 1e3
+        nm, fl, by = infos[dom]
+        intensity = fl / by if by else 0.0
+        ridge = PEAK_FP32_MFMA_TFLOPS * 1e12 / (PEAK_HBM_GBS * 1e9)
+        traffic = None
+        pmc_path = os.path.join(REPO, "profiles", "pmc_traffic.json")
+        if os.path.exists(pmc_path):
+            try:
+                traffic = json.load(open(pmc_path)).get(nm, {}).get("hbm_bytes_per_launch")
+            except Exception:
+                traffic = None
+        if intensity > ridge and fl > 0:
+            ach = fl / (avg_ms * 1e-3) / 1e12
+            roofline = {"bound": "mfma", "achieved": ach, "peak": PEAK_FP32_MFMA_TFLOPS, "unit": "TFLOP/s",
+                        "frac": ach / PEAK_FP32_MFMA_TFLOPS, "traffic": traffic, "kernel": nm,
+                        "avg_us": avg_ms * 1e3, "algorithmic_flops": fl, "algorithmic_bytes": by}
+        else:
+            ach = by / (avg_ms * 1e-3) / 1e9
+            roofline = {"bound": "hbm", "achieved": ach, "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                        "frac": ach / PEAK_HBM_GBS, "traffic": traffic, "kernel": nm,
+                        "avg_us": avg_ms * 1e3, "algorithmic_flops": fl, "algorithmic_bytes": by}
+        C.check(L.dqnx_events_destroy(2 * K, evs), "events_destroy")
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        try:
+            cpu = cpu_baseline(args)
+        except Exception as ex:  # the baseline must never hide the GPU number
+            log(f"cpu baseline failed: {ex!r}")
+
+    if rank == 0:
+        out = {
+            "metric": "DQN learn-steps/sec × batch (transitions/sec) at 1/2/4/8 MI355X",
+            "value": value,
+            "unit": "transitions/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": ms_per_step,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "fp32",
+            "data": "synthetic",
+            "config": {
+                "workload": "configs[1]: synthetic 1ramp_1x3 state vectors, MLP Q-net fp32, GPU replay buffer",
+                "algo": args.algo, "net": f"MLP({args.obs_dim}->256->128, ReLU) + dueling head A={args.actions}",
+                "batch_per_gpu": args.batch, "global_batch": Bg, "replay_capacity": args.capacity,
+                "parallelism": f"dp{world}", "graphs": not args.no_graphs,
+            },
+            "roofline": roofline,
+            "cpu_baseline": cpu,
+            "loss": loss,
+            "kernels": kernels,
+        }
+        print(json.dumps(out), flush=True)
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,240 @@
+/*
+ * dqnx.h -- C ABI of the MI355X-native DQN learn-step engine (libdqnx.so).
+ *
+ * Drop-in boundary for the hot path of youcefMehamlia/Multimodal-DRL-RMC
+ * (R: = /root/reference/).  The reference has no FFI: its "operator API" is the
+ * duck-typed Python of dqn.agent / dqn.network / dqn.replay_memory, which the
+ * Python host shim (multimodal-drl-rmc_amd/dqn/) keeps, calling the entry points
+ * below through ctypes.  Each entry point names the reference interface it
+ * replaces.  Plain C: pointers, sizes, enums; no torch types.  Streams are
+ * hipStream_t passed as void*.  All device work is enqueued on the caller's
+ * stream; nothing here synchronises unless its comment says so.
+ *
+ * Error convention: every function returns int (0 = DQNX_OK, < 0 = invalid
+ * argument/state, > 0 = DQNX_ERR_HIP + hipError_t).  dqnx_last_error() returns a
+ * thread-local message for the last failure.  No C++ exception crosses the ABI.
+ *
+ * Memory: the engine owns no device memory.  The caller allocates ONE device arena
+ * of dqnx_engine_arena_bytes() bytes and binds it; dqnx_engine_buffer() gives the
+ * offset of every region inside it (parameters, Adam moments, replay ring, SumTree,
+ * control block, workspace), so a host framework can view them (the Python shim
+ * makes torch views so state_dict()/load_state_dict() keep working).
+ */
+#ifndef DQNX_H
+#define DQNX_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DQNX_ABI_VERSION 1
+
+/* ---- status codes ---------------------------------------------------------------- */
+#define DQNX_OK 0
+#define DQNX_EINVAL (-1)      /* bad argument */
+#define DQNX_ESTATE (-2)      /* call not valid in the engine's current state (e.g. unbound) */
+#define DQNX_EUNSUPPORTED (-3)/* configuration outside what the engine implements */
+#define DQNX_EDEVICE (-4)     /* device-side sticky error word was set (see dqnx_ctrl.error) */
+#define DQNX_ERR_HIP 1000     /* DQNX_ERR_HIP + hipError_t */
+
+/* ---- enums ------------------------------------------------------------------------- */
+enum dqnx_net_kind { DQNX_NET_MLP = 0, DQNX_NET_TWO_STREAM = 1 };
+enum dqnx_head_kind { DQNX_HEAD_LINEAR = 0, DQNX_HEAD_DUELING = 1 };
+enum dqnx_activation { DQNX_ACT_RELU = 0, DQNX_ACT_ELU = 1 };
+/* Learner algorithm = which Agent.learn() runs:
+ *   DQNX_ALGO_DQN        SimpleAgent.learn          R:dqn/agent.py:166-185  (DQNAgent)
+ *   DQNX_ALGO_DOUBLE     DoubleAgent.learn          R:dqn/agent.py:204-226  (DoubleDQNAgent,
+ *                                                                            DuelingDoubleDQNAgent)
+ *   DQNX_ALGO_PER_DOUBLE PerDoubleAgent.learn       R:dqn/agent.py:245-272  (PerDuelingDoubleDQNAgent) */
+enum dqnx_algo { DQNX_ALGO_DQN = 0, DQNX_ALGO_DOUBLE = 1, DQNX_ALGO_PER_DOUBLE = 2 };
+
+/* ---- network description (replaces nn_conf_func / network_config) ----------------
+ * MLP:        R:env/custom_env/macro with lane/dqn_config.py:58-104
+ *             nn.Sequential(Linear(D,h0), act, Linear(h0,h1), act, ...)
+ * TWO_STREAM: TwoStreamHybridNetwork R:env/dqn_config.py:66-143 (network_config :148-193)
+ * heads:      DeepQNetwork fc_out (R:dqn/network.py:50-65), DuelingDeepQNetwork
+ *             fc_val/fc_adv + aggregate (R:dqn/network.py:77-96). */
+#define DQNX_MAX_DENSE 6
+#define DQNX_MAX_CONV 4
+typedef struct dqnx_net_desc {
+    int32_t kind;              /* dqnx_net_kind */
+    int32_t head;              /* dqnx_head_kind */
+    int32_t activation;        /* dqnx_activation of the body (MLP: ReLU, hybrid: ELU) */
+    int32_t obs_dim;           /* D: length of one flat observation */
+    int32_t n_actions;         /* A */
+    int32_t n_dense;           /* number of body Linear layers (MLP) / dense_stream layers */
+    int32_t dense[DQNX_MAX_DENSE];
+    /* TWO_STREAM only: obs = [macro (macro_len) | micro grid viewed as (c,h,w)] */
+    int32_t macro_len;
+    int32_t micro_c, micro_h, micro_w;
+    int32_t n_conv;
+    int32_t conv_out[DQNX_MAX_CONV], conv_kh[DQNX_MAX_CONV], conv_kw[DQNX_MAX_CONV];
+    int32_t conv_sh[DQNX_MAX_CONV], conv_sw[DQNX_MAX_CONV];
+} dqnx_net_desc;
+
+/* One parameter tensor of the flat parameter vector, in torch named_parameters()
+ * order (= state_dict order, = the order Adam iterates).  Names are the reference's
+ * state_dict keys (e.g. "net.0.weight", "fc_adv.bias"). */
+typedef struct dqnx_param_info {
+    char name[48];
+    int64_t offset;            /* element offset in the flat fp32 vector */
+    int64_t numel;
+    int32_t ndim;
+    int32_t shape[4];
+} dqnx_param_info;
+
+/* Total fp32 parameter count and tensor count of a network (host only, no GPU). */
+int dqnx_net_param_count(const dqnx_net_desc* net, int64_t* n_params, int32_t* n_tensors);
+int dqnx_net_param_info(const dqnx_net_desc* net, int32_t index, dqnx_param_info* out);
+
+/* ---- engine configuration (replaces the Agent constructor kwargs, R:dqn/agent.py:19-52,
+ *      with the hyper-parameters of R:env/dqn_config.py:26-56) -------------------- */
+typedef struct dqnx_config {
+    dqnx_net_desc net;
+    int32_t algo;              /* dqnx_algo */
+    int32_t batch;             /* global minibatch = batch_size (k of random.sample) */
+    int32_t world_size;        /* data-parallel ranks (1 = single GPU) */
+    int32_t rank;              /* this rank: processes samples [rank*batch/world, (rank+1)*batch/world) */
+    int64_t capacity;          /* buffer_size (deque maxlen / SumTree capacity) */
+    float gamma;               /* discount */
+    float lr;                  /* Adam lr */
+    float beta1, beta2, adam_eps;   /* torch.optim.Adam defaults 0.9, 0.999, 1e-8 */
+    float tau;                 /* target_soft_update_tau */
+    int32_t n_env;             /* soft update uses tau*n_env (R:dqn/agent.py:108-109) */
+    int32_t reserved0;
+    /* ReplayMemoryPrioritized constants (R:dqn/replay_memory.py:49-54) */
+    double per_eps, per_alpha, per_max_priority;
+    double per_beta_start, per_beta_end, per_beta_steps;   /* beta = interp(step,[0,steps],[start,end]) */
+} dqnx_config;
+
+/* Fill cfg with the reference's HYPER_PARAMS defaults for the given network. */
+void dqnx_config_defaults(dqnx_config* cfg);
+
+/* ---- device control block (lives in the arena; layout is ABI) ------------------- */
+typedef struct dqnx_ctrl {
+    uint32_t py_mt[625];       /* CPython random state: random.getstate()[1] (624 words + index) */
+    uint32_t np_mt[625];       /* numpy legacy RandomState: get_state()[1] keys + [2] pos */
+    int64_t ring_size;         /* len(replay deque) / SumTree.size */
+    int64_t ring_wptr;         /* next physical write slot (SumTree.data_pointer) */
+    int64_t adam_step;         /* torch Adam state['step'] (same for every tensor) */
+    int64_t agent_step;        /* agent.step * n_env handed to PER sample_transitions */
+    int64_t per_max_idx;       /* SumTree.max_priority_index (tree index) */
+    int64_t per_min_idx;       /* SumTree.min_priority_index (tree index) */
+    float loss;                /* loss of the last learn step (global batch mean) */
+    int32_t error;             /* sticky device error code, 0 = ok */
+    float adam_step_size;      /* -lr / bias_correction1 of the current step (fp32) */
+    float adam_bc2_sqrt;       /* sqrt(bias_correction2) of the current step (fp32) */
+    double per_beta;           /* beta used by the last PER sample */
+    int64_t reserved[8];
+} dqnx_ctrl;
+
+/* device error codes written to dqnx_ctrl.error */
+#define DQNX_DEVERR_SAMPLE_TOO_LARGE 1   /* random.sample: k > n (ValueError) */
+#define DQNX_DEVERR_EMPTY_TREE 2         /* PER sample with total priority 0 */
+
+/* ---- engine lifetime --------------------------------------------------------------- */
+typedef struct dqnx_engine dqnx_engine;
+
+int dqnx_engine_create(const dqnx_config* cfg, dqnx_engine** out);
+int dqnx_engine_destroy(dqnx_engine* e);
+/* Bytes of the single device arena the engine needs (host only). */
+int dqnx_engine_arena_bytes(const dqnx_engine* e, uint64_t* bytes);
+
+/* Arena regions. */
+enum dqnx_buffer {
+    DQNX_BUF_PARAMS = 0,       /* online network flat fp32 params (named_parameters order) */
+    DQNX_BUF_TARGET_PARAMS,    /* target network flat params */
+    DQNX_BUF_GRADS,            /* flat fp32 gradient of the last learn step (all-reduced under DP) */
+    DQNX_BUF_ADAM_M,           /* Adam exp_avg */
+    DQNX_BUF_ADAM_V,           /* Adam exp_avg_sq */
+    DQNX_BUF_CTRL,             /* dqnx_ctrl */
+    DQNX_BUF_RING_OBS,         /* [capacity][obs_stride] fp32 */
+    DQNX_BUF_RING_NEXT_OBS,    /* [capacity][obs_stride] fp32 */
+    DQNX_BUF_RING_ACT,         /* [capacity] int32 */
+    DQNX_BUF_RING_REW,         /* [capacity] fp32 */
+    DQNX_BUF_RING_DONE,        /* [capacity] fp32 (0/1) */
+    DQNX_BUF_SUMTREE,          /* [2*capacity-1] fp64 (PER only, else 0 bytes) */
+    DQNX_BUF_BATCH_IDX,        /* [batch] int32: sampled logical replay positions / tree leaves */
+    DQNX_BUF_Q,                /* [3][batch_local][n_actions] fp32: Q online(s), online(s'), target(s') */
+    DQNX_BUF_TD,               /* [3][batch_local] fp32: targets y, q(s,a), |y - q(s,a)| */
+    DQNX_BUF_IS_WEIGHTS,       /* [batch] fp32 PER importance weights */
+    DQNX_BUF_WORKSPACE,        /* everything else (activations, partial slabs, scratch) */
+    DQNX_BUF_COUNT
+};
+int dqnx_engine_buffer(const dqnx_engine* e, int32_t which, uint64_t* offset, uint64_t* bytes);
+/* Row stride (in floats) of the replay observation rings (>= obs_dim, multiple of 4). */
+int dqnx_engine_obs_stride(const dqnx_engine* e, int32_t* stride);
+/* Bind the caller-allocated arena (device pointer, 256-byte aligned). */
+int dqnx_engine_bind(dqnx_engine* e, void* arena, uint64_t bytes);
+/* Zero Adam moments, ring state, tree, control block (params untouched); stream-ordered. */
+int dqnx_engine_reset(dqnx_engine* e, void* stream);
+/* Use hipGraph capture/replay for learn steps (default on). */
+int dqnx_engine_set_graphs(dqnx_engine* e, int32_t enabled);
+
+/* ---- replay ring: replaces ReplayMemoryNaive/Prioritized.store_transitions
+ *      (R:dqn/replay_memory.py:30-36, :56-67) via Agent.store_transitions (R:dqn/agent.py:80-84).
+ * Appends n transitions (evicting the oldest when full).  Pointers are host memory
+ * (src_on_device = 0; copied with hipMemcpyAsync, caller keeps them alive until the
+ * stream reaches the copy) or device memory (src_on_device = 1).  obs rows are
+ * obs_dim floats, contiguous.  done: 0/1 bytes.  Under PER new leaves get the current
+ * max priority (1.0 when the tree is empty), exactly as the reference. */
+int dqnx_replay_push(dqnx_engine* e, const float* obs, const int32_t* act, const float* rew,
+                     const uint8_t* done, const float* next_obs, int32_t n, int32_t src_on_device,
+                     void* stream);
+
+/* ---- RNG state exchange (Python random / numpy legacy global state) -------------- */
+enum dqnx_rng { DQNX_RNG_PY = 0, DQNX_RNG_NP = 1 };
+/* Upload 625 words (624 + index) into the control block (host pointer; stream-ordered,
+ * the copy is complete when this returns). */
+int dqnx_rng_set(dqnx_engine* e, int32_t which, const uint32_t* state625, void* stream);
+/* Download 625 words; synchronises the stream. */
+int dqnx_rng_get(dqnx_engine* e, int32_t which, uint32_t* state625, void* stream);
+
+/* ---- the learn step: replaces Agent.learn() (R:dqn/agent.py:166-185 / 204-226 /
+ *      245-272) and, with DQNX_STEP_SOFT_UPDATE, the following
+ *      Agent.update_target_network() soft update (R:dqn/agent.py:105-110; caller
+ *      R:train.py:99-101).
+ * Stream-ordered; returns without synchronising.  Reads ring size/RNG/step from the
+ * control block, so consecutive calls need no host round trip. */
+#define DQNX_STEP_SOFT_UPDATE 0x1   /* fuse the tau soft update into the Adam pass */
+#define DQNX_STEP_GIVEN_INDICES 0x2 /* skip sampling: use DQNX_BUF_BATCH_IDX as written by caller */
+#define DQNX_STEP_GRADS_ONLY 0x4    /* stop after writing DQNX_BUF_GRADS (DP: all-reduce, then apply) */
+int dqnx_learn_step(dqnx_engine* e, int32_t flags, void* stream);
+/* Adam (+ optional soft update) from DQNX_BUF_GRADS: second half of a GRADS_ONLY step. */
+int dqnx_apply_grads(dqnx_engine* e, int32_t flags, void* stream);
+/* Agent.update_target_network (R:dqn/agent.py:101-110): soft (tau*n_env) or hard copy. */
+int dqnx_soft_update(dqnx_engine* e, void* stream);
+int dqnx_hard_update(dqnx_engine* e, void* stream);
+
+/* ---- kernel-level timing (bench.py roofline) ---------------------------------------
+ * A learn step is an ordered list of kernel launches (sample, linear_fwd_l1.., head_td_loss,
+ * linear_bwd_lL..l1, adam_fused).  dqnx_learn_step_timed runs one whole step exactly like
+ * dqnx_learn_step but records ev_start/ev_stop (hipEvent_t) around kernel `kernel_index`
+ * on `stream` (the sub-ranges before/after it are graph-replayed separately). */
+int dqnx_learn_kernel_count(dqnx_engine* e, int32_t flags, int32_t* n);
+int dqnx_learn_kernel_info(dqnx_engine* e, int32_t flags, int32_t index, char* name, int32_t name_len,
+                           double* algorithmic_flops, double* algorithmic_bytes);
+int dqnx_learn_step_timed(dqnx_engine* e, int32_t flags, int32_t kernel_index, void* ev_start, void* ev_stop,
+                          void* stream);
+int dqnx_events_create(int32_t n, void** events);      /* hipEventCreate x n */
+int dqnx_events_destroy(int32_t n, void** events);
+int dqnx_event_elapsed(void* start, void* stop, float* ms);   /* synchronises `stop` */
+
+/* ---- sampler (test hook / building block): random.sample positions on device.
+ * R:dqn/replay_memory.py:38-39.  mt625: device uint32[625] (advanced in place);
+ * n: population size; k: sample size; out: device int32[k].  scratch: device buffer of
+ * dqnx_sample_scratch_bytes(n, k) bytes.  err: device int32 (set to 1 if k > n). */
+uint64_t dqnx_sample_scratch_bytes(int64_t n, int32_t k);
+int dqnx_sample_uniform(uint32_t* mt625, int64_t n, int32_t k, int32_t* out, void* scratch,
+                        int32_t* err, void* stream);
+
+/* ---- misc ------------------------------------------------------------------------ */
+const char* dqnx_last_error(void);
+int32_t dqnx_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DQNX_H */

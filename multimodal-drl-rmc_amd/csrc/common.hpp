@@ -1,0 +1,52 @@
+// Shared device/host helpers for libdqnx (gfx950 / CDNA4 only).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/dqnx.h"
+
+namespace dqnx {
+
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+
+constexpr int kWave = 64;
+
+// v_mfma_f32_16x16x4_f32: lane l supplies A[l&15][k=l>>4], B[k=l>>4][l&15];
+// accumulator lane l holds C[(l>>4)*4 + r][l&15], r = 0..3.  Exact fp32 fmaf chain.
+__device__ __forceinline__ floatx4 mfma16x16x4(float a, float b, floatx4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ float relu_f(float x) { return x > 0.f ? x : 0.f; }
+
+// torch CPU ELU (alpha=scale=input_scale=1): x <= 0 ? expm1(x) : x
+__device__ __forceinline__ float elu_f(float x) { return x > 0.f ? x : expm1f(x); }
+
+// activation derivative from the activation OUTPUT h (threshold_backward / elu_backward
+// with is_result=true): relu: h > 0 ? g : 0 ; elu: h > 0 ? g : g * (h + 1)
+template <int ACT>
+__device__ __forceinline__ float act_bwd(float g, float h) {
+    if (ACT == DQNX_ACT_RELU) return h > 0.f ? g : 0.f;
+    return h > 0.f ? g : g * (h + 1.f);
+}
+
+template <int ACT>
+__device__ __forceinline__ float act_fwd(float x) {
+    if (ACT == DQNX_ACT_RELU) return relu_f(x);
+    return elu_f(x);
+}
+
+__device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
+
+}  // namespace dqnx
+
+#define DQNX_HIP_CHECK(expr)                                                    \
+    do {                                                                        \
+        hipError_t _e = (expr);                                                 \
+        if (_e != hipSuccess) return dqnx::set_hip_error(_e, #expr, __FILE__, __LINE__); \
+    } while (0)
+
+namespace dqnx {
+int set_error(int code, const char* fmt, ...);
+int set_hip_error(hipError_t e, const char* expr, const char* file, int line);
+}  // namespace dqnx

@@ -1,0 +1,890 @@
+// libdqnx host side: network planning, arena layout, the C ABI of include/dqnx.h, the
+// learn-step launch sequence and its hipGraph capture/replay.
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <functional>
+#include <map>
+#include <string>
+#include <vector>
+
+#include "learn.hpp"
+
+namespace dqnx {
+
+static thread_local char g_err[512] = "";
+
+int set_error(int code, const char* fmt, ...) {
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(g_err, sizeof(g_err), fmt, ap);
+    va_end(ap);
+    return code;
+}
+
+int set_hip_error(hipError_t e, const char* expr, const char* file, int line) {
+    snprintf(g_err, sizeof(g_err), "%s failed: %s (%s:%d)", expr, hipGetErrorString(e), file, line);
+    return DQNX_ERR_HIP + (int)e;
+}
+
+// ------------------------------------------------------------------------------------
+// network planning (host only)
+// ------------------------------------------------------------------------------------
+struct LayerPlan {
+    int in, out;        // Linear in/out features
+    int64_t off;        // flat offset of the weight ([out][in]); bias follows at off + out*in
+};
+
+struct NetPlan {
+    std::vector<dqnx_param_info> params;
+    std::vector<LayerPlan> dense;   // body Linear layers
+    int F = 0;                      // body output features
+    int NH = 0;                     // head rows (dueling: 1 + A)
+    int64_t head_off = 0, head_params = 0, P = 0;
+};
+
+static void add_param(NetPlan& np, const std::string& name, std::vector<int> shape) {
+    dqnx_param_info pi;
+    memset(&pi, 0, sizeof(pi));
+    snprintf(pi.name, sizeof(pi.name), "%s", name.c_str());
+    pi.offset = np.P;
+    pi.ndim = (int32_t)shape.size();
+    int64_t n = 1;
+    for (size_t i = 0; i < shape.size(); i++) {
+        pi.shape[i] = shape[i];
+        n *= shape[i];
+    }
+    pi.numel = n;
+    np.P += n;
+    np.params.push_back(pi);
+}
+
+static int plan_net(const dqnx_net_desc* d, NetPlan& np) {
+    np = NetPlan();
+    if (!d) return set_error(DQNX_EINVAL, "net desc is null");
+    if (d->obs_dim <= 0 || d->n_actions <= 0) return set_error(DQNX_EINVAL, "obs_dim/n_actions must be > 0");
+    if (d->n_dense < 1 || d->n_dense > DQNX_MAX_DENSE) return set_error(DQNX_EINVAL, "n_dense out of range");
+    if (d->head != DQNX_HEAD_DUELING && d->head != DQNX_HEAD_LINEAR) return set_error(DQNX_EINVAL, "bad head kind");
+    int in;
+    if (d->kind == DQNX_NET_MLP) {
+        in = d->obs_dim;
+        for (int l = 0; l < d->n_dense; l++) {
+            const int out = d->dense[l];
+            if (out <= 0) return set_error(DQNX_EINVAL, "dense width must be > 0");
+            LayerPlan lp{in, out, np.P};
+            add_param(np, "net." + std::to_string(2 * l) + ".weight", {out, in});
+            add_param(np, "net." + std::to_string(2 * l) + ".bias", {out});
+            np.dense.push_back(lp);
+            in = out;
+        }
+    } else if (d->kind == DQNX_NET_TWO_STREAM) {
+        if (d->n_conv < 1 || d->n_conv > DQNX_MAX_CONV) return set_error(DQNX_EINVAL, "n_conv out of range");
+        if (d->macro_len + d->micro_c * d->micro_h * d->micro_w != d->obs_dim)
+            return set_error(DQNX_EINVAL, "obs_dim != macro_len + c*h*w");
+        int c = d->micro_c, h = d->micro_h, w = d->micro_w;
+        for (int l = 0; l < d->n_conv; l++) {
+            const int f = d->conv_out[l], kh = d->conv_kh[l], kw = d->conv_kw[l];
+            add_param(np, "net.cnn_stream." + std::to_string(2 * l) + ".weight", {f, c, kh, kw});
+            add_param(np, "net.cnn_stream." + std::to_string(2 * l) + ".bias", {f});
+            h = (h + 2 * (kh / 2) - kh) / d->conv_sh[l] + 1;
+            w = (w + 2 * (kw / 2) - kw) / d->conv_sw[l] + 1;
+            c = f;
+        }
+        in = c * h * w + d->macro_len;
+        for (int l = 0; l < d->n_dense; l++) {
+            const int out = d->dense[l];
+            LayerPlan lp{in, out, np.P};
+            add_param(np, "net.dense_stream." + std::to_string(2 * l) + ".weight", {out, in});
+            add_param(np, "net.dense_stream." + std::to_string(2 * l) + ".bias", {out});
+            np.dense.push_back(lp);
+            in = out;
+        }
+    } else {
+        return set_error(DQNX_EINVAL, "bad net kind");
+    }
+    np.F = in;
+    np.head_off = np.P;
+    if (d->head == DQNX_HEAD_DUELING) {
+        add_param(np, "fc_val.weight", {1, in});
+        add_param(np, "fc_val.bias", {1});
+        add_param(np, "fc_adv.weight", {d->n_actions, in});
+        add_param(np, "fc_adv.bias", {d->n_actions});
+        np.NH = 1 + d->n_actions;
+    } else {
+        add_param(np, "fc_out.weight", {d->n_actions, in});
+        add_param(np, "fc_out.bias", {d->n_actions});
+        np.NH = d->n_actions;
+    }
+    np.head_params = np.P - np.head_off;
+    return DQNX_OK;
+}
+
+static inline uint64_t align_up(uint64_t x, uint64_t a) { return (x + a - 1) / a * a; }
+
+struct KStep {
+    std::string name;
+    double flops = 0, bytes = 0;
+    std::function<int(hipStream_t)> run;
+};
+
+}  // namespace dqnx
+
+using namespace dqnx;
+
+struct dqnx_engine {
+    dqnx_config cfg;
+    NetPlan np;
+    int Bg = 0, Bl = 0, shard_begin = 0, stride = 0, tiles = 0;
+    int64_t setsize = 0;
+    std::vector<int> slices;          // split-K slabs per dense layer
+    std::vector<int> kslice;
+    uint64_t off[DQNX_BUF_COUNT] = {0}, bytes[DQNX_BUF_COUNT] = {0};
+    uint64_t total = 0;
+    // workspace sub-regions (byte offsets from the arena base)
+    uint64_t ws_phys = 0, ws_pool = 0, ws_xobs = 0, ws_head_part = 0, ws_loss_part = 0, ws_stage = 0;
+    std::vector<uint64_t> ws_H, ws_dZ, ws_part;
+    int stage_rows = 0;
+    char* arena = nullptr;
+    int64_t ring_size = 0, ring_wptr = 0;   // host mirror of the ring state (pushes are host-driven)
+    bool graphs = true;
+    std::map<int, hipGraphExec_t> graph_cache;
+    hipStream_t capture_stream = nullptr;
+    std::map<int, std::vector<KStep>> steps_cache;
+};
+
+namespace {
+
+template <class T>
+T* at(dqnx_engine* e, uint64_t byte_off) {
+    return reinterpret_cast<T*>(e->arena + byte_off);
+}
+
+dqnx_ctrl* ctrl_of(dqnx_engine* e) { return at<dqnx_ctrl>(e, e->off[DQNX_BUF_CTRL]); }
+
+int layout(dqnx_engine* e) {
+    const dqnx_config& c = e->cfg;
+    const NetPlan& np = e->np;
+    const int L = (int)np.dense.size();
+    const int A = c.net.n_actions;
+    const int64_t P = np.P;
+    uint64_t cur = 0;
+    auto region = [&](int which, uint64_t nbytes) {
+        cur = align_up(cur, 256);
+        e->off[which] = cur;
+        e->bytes[which] = nbytes;
+        cur += nbytes;
+    };
+    region(DQNX_BUF_PARAMS, P * 4);
+    region(DQNX_BUF_TARGET_PARAMS, P * 4);
+    region(DQNX_BUF_GRADS, (P + 1) * 4);
+    region(DQNX_BUF_ADAM_M, P * 4);
+    region(DQNX_BUF_ADAM_V, P * 4);
+    region(DQNX_BUF_CTRL, sizeof(dqnx_ctrl));
+    const uint64_t cap = (uint64_t)c.capacity;
+    region(DQNX_BUF_RING_OBS, cap * e->stride * 4);
+    region(DQNX_BUF_RING_NEXT_OBS, cap * e->stride * 4);
+    region(DQNX_BUF_RING_ACT, cap * 4);
+    region(DQNX_BUF_RING_REW, cap * 4);
+    region(DQNX_BUF_RING_DONE, cap * 4);
+    region(DQNX_BUF_SUMTREE, c.algo == DQNX_ALGO_PER_DOUBLE ? (2 * cap - 1) * 8 : 0);
+    region(DQNX_BUF_BATCH_IDX, (uint64_t)e->Bg * 4);
+    region(DQNX_BUF_Q, (uint64_t)3 * e->Bl * A * 4);
+    region(DQNX_BUF_TD, (uint64_t)3 * e->Bl * 4);
+    region(DQNX_BUF_IS_WEIGHTS, (uint64_t)e->Bg * 4);
+    // workspace
+    cur = align_up(cur, 256);
+    e->off[DQNX_BUF_WORKSPACE] = cur;
+    auto sub = [&](uint64_t nbytes) {
+        cur = align_up(cur, 256);
+        uint64_t o = cur;
+        cur += nbytes;
+        return o;
+    };
+    e->ws_phys = sub((uint64_t)e->Bl * 4);
+    e->ws_pool = sub((uint64_t)(e->setsize + 64) * 4);
+    e->ws_xobs = sub((uint64_t)e->Bl * e->stride * 4);
+    e->ws_H.assign(L, 0);
+    e->ws_dZ.assign(L, 0);
+    e->ws_part.assign(L, 0);
+    for (int l = 0; l < L; l++) {
+        const int w = np.dense[l].out;
+        e->ws_H[l] = sub((uint64_t)3 * e->Bl * w * 4);
+        e->ws_dZ[l] = sub((uint64_t)e->Bl * w * 4);
+        const uint64_t lp = (uint64_t)np.dense[l].out * np.dense[l].in + np.dense[l].out;
+        e->ws_part[l] = sub((uint64_t)e->slices[l] * lp * 4);
+    }
+    e->ws_head_part = sub((uint64_t)e->tiles * np.head_params * 4);
+    e->ws_loss_part = sub((uint64_t)e->tiles * 4);
+    e->stage_rows = 1024;
+    e->ws_stage = sub((uint64_t)e->stage_rows * (2 * (uint64_t)c.net.obs_dim + 3) * 4 + 256);
+    cur = align_up(cur, 256);
+    e->bytes[DQNX_BUF_WORKSPACE] = cur - e->off[DQNX_BUF_WORKSPACE];
+    e->total = cur;
+    return DQNX_OK;
+}
+
+int check_bound(const dqnx_engine* e) {
+    if (!e) return set_error(DQNX_EINVAL, "engine is null");
+    if (!e->arena) return set_error(DQNX_ESTATE, "engine arena not bound");
+    return DQNX_OK;
+}
+
+// ---- the learn-step launch sequence ----------------------------------------------------
+// One learn step = an ordered list of kernel launches.  Each entry carries its name and
+// algorithmic FLOPs / bytes (for the roofline of DESIGN.md) so a sub-range can be captured
+// and timed on its own (dqnx_learn_step_timed).
+
+
+std::vector<KStep> build_learn_steps(dqnx_engine* e, int flags) {
+    std::vector<KStep> ks;
+    const dqnx_config& c = e->cfg;
+    const NetPlan& np = e->np;
+    const int L = (int)np.dense.size();
+    const int A = c.net.n_actions;
+    const int act = c.net.activation;
+    dqnx_ctrl* ctrl = ctrl_of(e);
+    float* params = at<float>(e, e->off[DQNX_BUF_PARAMS]);
+    float* tparams = at<float>(e, e->off[DQNX_BUF_TARGET_PARAMS]);
+    int32_t* idx = at<int32_t>(e, e->off[DQNX_BUF_BATCH_IDX]);
+    int32_t* phys = at<int32_t>(e, e->ws_phys);
+    const double Bl = e->Bl;
+
+    // 1. sample (R:dqn/replay_memory.py:38-39)
+    if (flags & DQNX_STEP_GIVEN_INDICES) {
+        KStep k;
+        k.name = "idx_to_phys";
+        k.bytes = 8.0 * Bl;
+        k.run = [=](hipStream_t s) { return launch_idx_to_phys(idx, phys, e->shard_begin, e->Bl, ctrl, c.capacity, s); };
+        ks.push_back(k);
+    } else {
+        SampleArgs sa;
+        memset(&sa, 0, sizeof(sa));
+        sa.state = ctrl->py_mt;
+        sa.n_dev = &ctrl->ring_size;
+        sa.k = e->Bg;
+        sa.setsize = e->setsize;
+        sa.out = idx;
+        sa.err = &ctrl->error;
+        sa.pool = at<int32_t>(e, e->ws_pool);
+        sa.phys_out = phys;
+        sa.shard_begin = e->shard_begin;
+        sa.shard_len = e->Bl;
+        sa.wptr_dev = &ctrl->ring_wptr;
+        sa.capacity = c.capacity;
+        KStep k;
+        k.name = "sample_uniform";
+        k.bytes = 2.0 * 625 * 4 + 4.0 * e->Bg + 4.0 * Bl;
+        k.run = [=](hipStream_t s) { return launch_sample_uniform(sa, s); };
+        ks.push_back(k);
+    }
+
+    // 2. forward layers: streams 0 online(obs), 1 online(next) [double], 2 target(next)
+    const bool dbl = c.algo != DQNX_ALGO_DQN;
+    const int nstreams = dbl ? 3 : 2;
+    for (int l = 0; l < L; l++) {
+        const LayerPlan lp = np.dense[l];
+        FwdArgs fa;
+        memset(&fa, 0, sizeof(fa));
+        fa.M = e->Bl;
+        fa.N = lp.out;
+        fa.K = lp.in;
+        fa.ldc = lp.out;
+        float* H = at<float>(e, e->ws_H[l]);
+        int np_ = 0;
+        for (int st = 0; st < 3; st++) {
+            if (st == 1 && !dbl) continue;
+            FwdProblem& p = fa.p[np_++];
+            const bool tgt = st == 2;
+            p.W = (tgt ? tparams : params) + lp.off;
+            p.bias = p.W + (int64_t)lp.out * lp.in;
+            p.C = H + (int64_t)st * e->Bl * lp.out;
+            if (l == 0) {
+                p.A = at<float>(e, e->off[st == 0 ? DQNX_BUF_RING_OBS : DQNX_BUF_RING_NEXT_OBS]);
+                p.lda = e->stride;
+                p.phys = phys;
+                p.xcopy = (st == 0) ? at<float>(e, e->ws_xobs) : nullptr;
+            } else {
+                const int w = np.dense[l - 1].out;
+                p.A = at<float>(e, e->ws_H[l - 1]) + (int64_t)st * e->Bl * w;
+                p.lda = w;
+            }
+        }
+        KStep k;
+        k.name = "linear_fwd_l" + std::to_string(l + 1);
+        k.flops = 2.0 * nstreams * Bl * lp.out * lp.in;
+        // unique bytes: input rows, weights (online + target), outputs (+ layer-1 row copy)
+        k.bytes = 4.0 * (nstreams * Bl * lp.in + 2.0 * (lp.out * (double)lp.in + lp.out) + nstreams * Bl * lp.out
+                         + (l == 0 ? Bl * lp.in : 0.0));
+        const bool vecb = (lp.in % 4) == 0;
+        k.run = [=](hipStream_t s) { return launch_linear_fwd(fa, np_, act, vecb, s); };
+        ks.push_back(k);
+    }
+
+    // 3. head + TD + Huber + head backward (R:dqn/agent.py:209-221, R:dqn/network.py:90-96)
+    {
+        HeadArgs ha;
+        memset(&ha, 0, sizeof(ha));
+        ha.Bl = e->Bl;
+        ha.F = np.F;
+        ha.A = A;
+        ha.NH = np.NH;
+        ha.head_kind = c.net.head;
+        ha.algo = c.algo;
+        ha.head_params = (int)np.head_params;
+        ha.inv_bg = (float)(1.0 / (double)e->Bg);
+        ha.gamma = c.gamma;
+        ha.H = at<float>(e, e->ws_H[L - 1]);
+        ha.Wo = params + np.head_off;
+        ha.Wt = tparams + np.head_off;
+        ha.phys = phys;
+        ha.act = at<int32_t>(e, e->off[DQNX_BUF_RING_ACT]);
+        ha.rew = at<float>(e, e->off[DQNX_BUF_RING_REW]);
+        ha.done = at<float>(e, e->off[DQNX_BUF_RING_DONE]);
+        ha.isw = (c.algo == DQNX_ALGO_PER_DOUBLE) ? at<float>(e, e->off[DQNX_BUF_IS_WEIGHTS]) + e->shard_begin : nullptr;
+        ha.Q = at<float>(e, e->off[DQNX_BUF_Q]);
+        ha.td = at<float>(e, e->off[DQNX_BUF_TD]);
+        ha.dZ = at<float>(e, e->ws_dZ[L - 1]);
+        ha.head_partial = at<float>(e, e->ws_head_part);
+        ha.loss_partial = at<float>(e, e->ws_loss_part);
+        ha.ctrl = ctrl;
+        ha.beta1 = c.beta1;
+        ha.beta2 = c.beta2;
+        ha.lr = c.lr;
+        KStep k;
+        k.name = "head_td_loss";
+        const double F = np.F, NH = np.NH;
+        k.flops = 2.0 * Bl * NH * F * (nstreams + 2.0);
+        k.bytes = 4.0 * (nstreams * Bl * F + 2.0 * np.head_params + Bl * F + e->tiles * (double)np.head_params
+                         + 3.0 * Bl * A + 6.0 * Bl);
+        k.run = [=](hipStream_t s) { return launch_head(ha, act, s); };
+        ks.push_back(k);
+    }
+
+    // 4. backward levels L..1: dX of the level below + split-K dW of this level
+    for (int l = L - 1; l >= 0; l--) {
+        const LayerPlan lp = np.dense[l];
+        BwdArgs ba;
+        memset(&ba, 0, sizeof(ba));
+        ba.dZ = at<float>(e, e->ws_dZ[l]);
+        ba.Bl = e->Bl;
+        ba.in = lp.in;
+        ba.out = lp.out;
+        ba.W = params + lp.off;
+        if (l > 0) {
+            ba.Hprev = at<float>(e, e->ws_H[l - 1]);   // stream 0 rows
+            ba.ldh = lp.in;
+            ba.dZprev = at<float>(e, e->ws_dZ[l - 1]);
+            ba.X = ba.Hprev;
+            ba.ldx = lp.in;
+        } else {
+            ba.X = at<float>(e, e->ws_xobs);
+            ba.ldx = e->stride;
+        }
+        ba.partial = at<float>(e, e->ws_part[l]);
+        ba.pstride = (int64_t)lp.out * lp.in + lp.out;
+        ba.kslice = e->kslice[l];
+        bwd_level_grid(ba);
+        const int S = e->slices[l];
+        KStep k;
+        k.name = "linear_bwd_l" + std::to_string(l + 1);
+        k.flops = 2.0 * Bl * lp.out * (lp.in + 1.0) + (l > 0 ? 2.0 * Bl * lp.out * lp.in : 0.0);
+        k.bytes = 4.0 * (Bl * lp.out + Bl * lp.in + S * (lp.out * (lp.in + 1.0))
+                         + (l > 0 ? lp.out * (double)lp.in + 2.0 * Bl * lp.in : 0.0));
+        k.run = [=](hipStream_t s) { return launch_bwd_level(ba, S, act, s); };
+        ks.push_back(k);
+    }
+
+    // 5. gradient reduction + Adam (+ soft update)
+    {
+        AdamArgs aa;
+        memset(&aa, 0, sizeof(aa));
+        aa.nseg = 0;
+        double part_elems = 0;
+        for (int l = 0; l < L; l++) {
+            AdamSegment& sg = aa.seg[aa.nseg++];
+            sg.off = np.dense[l].off;
+            sg.partial = at<float>(e, e->ws_part[l]);
+            sg.pstride = (int64_t)np.dense[l].out * np.dense[l].in + np.dense[l].out;
+            sg.S = e->slices[l];
+            part_elems += (double)sg.S * sg.pstride;
+        }
+        {
+            AdamSegment& sg = aa.seg[aa.nseg++];
+            sg.off = np.head_off;
+            sg.partial = at<float>(e, e->ws_head_part);
+            sg.pstride = np.head_params;
+            sg.S = e->tiles;
+            part_elems += (double)sg.S * sg.pstride;
+        }
+        aa.mode = (flags & DQNX_STEP_GRADS_ONLY) ? 0 : 1;
+        aa.soft = (flags & DQNX_STEP_SOFT_UPDATE) ? 1 : 0;
+        aa.n_params = np.P;
+        aa.p = params;
+        aa.m = at<float>(e, e->off[DQNX_BUF_ADAM_M]);
+        aa.v = at<float>(e, e->off[DQNX_BUF_ADAM_V]);
+        aa.grads = at<float>(e, e->off[DQNX_BUF_GRADS]);
+        aa.target = tparams;
+        aa.ctrl = ctrl;
+        aa.w1 = (float)(1.0 - (double)c.beta1);
+        aa.beta2 = c.beta2;
+        aa.c2 = (float)(1.0 - (double)c.beta2);
+        aa.eps = c.adam_eps;
+        aa.tau = (float)((double)c.tau * c.n_env);
+        aa.one_minus_tau = (float)(1.0 - (double)c.tau * c.n_env);
+        aa.loss_partial = at<float>(e, e->ws_loss_part);
+        aa.n_loss_partial = e->tiles;
+        aa.batch_global = e->Bg;
+        KStep k;
+        k.name = aa.mode ? "adam_fused" : "grad_reduce";
+        const double P = (double)np.P;
+        // read partials; write g; Adam: read p,m,v (+target), write p,m,v (+target)
+        k.bytes = 4.0 * (part_elems + P + (aa.mode ? 6.0 * P + (aa.soft ? 2.0 * P : 0.0) : 0.0));
+        k.flops = aa.mode ? 12.0 * P : 0.0;
+        k.run = [=](hipStream_t s) { return launch_adam(aa, s); };
+        ks.push_back(k);
+    }
+    return ks;
+}
+
+int enqueue_range(const std::vector<KStep>& ks, int a, int b, hipStream_t s) {
+    for (int i = a; i < b; i++) {
+        int rc = ks[i].run(s);
+        if (rc) return rc;
+    }
+    return DQNX_OK;
+}
+
+int enqueue_apply(dqnx_engine* e, int flags, hipStream_t s) {
+    const dqnx_config& c = e->cfg;
+    AdamArgs aa;
+    memset(&aa, 0, sizeof(aa));
+    aa.nseg = 0;
+    aa.mode = 2;
+    aa.soft = (flags & DQNX_STEP_SOFT_UPDATE) ? 1 : 0;
+    aa.n_params = e->np.P;
+    aa.p = at<float>(e, e->off[DQNX_BUF_PARAMS]);
+    aa.m = at<float>(e, e->off[DQNX_BUF_ADAM_M]);
+    aa.v = at<float>(e, e->off[DQNX_BUF_ADAM_V]);
+    aa.grads = at<float>(e, e->off[DQNX_BUF_GRADS]);
+    aa.target = at<float>(e, e->off[DQNX_BUF_TARGET_PARAMS]);
+    aa.ctrl = ctrl_of(e);
+    aa.w1 = (float)(1.0 - (double)c.beta1);
+    aa.beta2 = c.beta2;
+    aa.c2 = (float)(1.0 - (double)c.beta2);
+    aa.eps = c.adam_eps;
+    aa.tau = (float)((double)c.tau * c.n_env);
+    aa.one_minus_tau = (float)(1.0 - (double)c.tau * c.n_env);
+    aa.batch_global = e->Bg;
+    return launch_adam(aa, s);
+}
+
+// Capture `fn` into a graph once per key, then replay on the caller's stream.
+template <class Fn>
+int run_graphed(dqnx_engine* e, int key, hipStream_t s, Fn fn) {
+    if (!e->graphs) return fn(s);
+    auto it = e->graph_cache.find(key);
+    if (it == e->graph_cache.end()) {
+        if (!e->capture_stream) DQNX_HIP_CHECK(hipStreamCreateWithFlags(&e->capture_stream, hipStreamNonBlocking));
+        DQNX_HIP_CHECK(hipStreamBeginCapture(e->capture_stream, hipStreamCaptureModeThreadLocal));
+        int rc = fn(e->capture_stream);
+        hipGraph_t graph = nullptr;
+        hipError_t ce = hipStreamEndCapture(e->capture_stream, &graph);
+        if (rc) {
+            if (graph) (void)hipGraphDestroy(graph);
+            return rc;
+        }
+        if (ce != hipSuccess) return set_hip_error(ce, "hipStreamEndCapture", __FILE__, __LINE__);
+        hipGraphExec_t exec = nullptr;
+        hipError_t ie = hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0);
+        (void)hipGraphDestroy(graph);
+        if (ie != hipSuccess) return set_hip_error(ie, "hipGraphInstantiate", __FILE__, __LINE__);
+        it = e->graph_cache.emplace(key, exec).first;
+    }
+    DQNX_HIP_CHECK(hipGraphLaunch(it->second, s));
+    return DQNX_OK;
+}
+
+void drop_graphs(dqnx_engine* e) {
+    for (auto& kv : e->graph_cache) (void)hipGraphExecDestroy(kv.second);
+    e->graph_cache.clear();
+    e->steps_cache.clear();
+}
+
+const std::vector<KStep>& steps_for(dqnx_engine* e, int key) {
+    auto it = e->steps_cache.find(key);
+    if (it == e->steps_cache.end()) it = e->steps_cache.emplace(key, build_learn_steps(e, key)).first;
+    return it->second;
+}
+
+}  // namespace
+
+// ======================================================================================
+// C ABI
+// ======================================================================================
+extern "C" {
+
+const char* dqnx_last_error(void) { return g_err; }
+int32_t dqnx_abi_version(void) { return DQNX_ABI_VERSION; }
+
+int dqnx_net_param_count(const dqnx_net_desc* net, int64_t* n_params, int32_t* n_tensors) {
+    NetPlan np;
+    int rc = plan_net(net, np);
+    if (rc) return rc;
+    if (n_params) *n_params = np.P;
+    if (n_tensors) *n_tensors = (int32_t)np.params.size();
+    return DQNX_OK;
+}
+
+int dqnx_net_param_info(const dqnx_net_desc* net, int32_t index, dqnx_param_info* out) {
+    NetPlan np;
+    int rc = plan_net(net, np);
+    if (rc) return rc;
+    if (!out || index < 0 || index >= (int32_t)np.params.size())
+        return set_error(DQNX_EINVAL, "param index %d out of range", index);
+    *out = np.params[index];
+    return DQNX_OK;
+}
+
+void dqnx_config_defaults(dqnx_config* c) {
+    if (!c) return;
+    const dqnx_net_desc keep = c->net;
+    memset(c, 0, sizeof(*c));
+    c->net = keep;
+    c->algo = DQNX_ALGO_DOUBLE;
+    c->batch = 32;
+    c->world_size = 1;
+    c->rank = 0;
+    c->capacity = 1000000;
+    c->gamma = 0.99f;
+    c->lr = 1e-4f;
+    c->beta1 = 0.9f;
+    c->beta2 = 0.999f;
+    c->adam_eps = 1e-8f;
+    c->tau = 1e-3f;
+    c->n_env = 1;
+    c->per_eps = 1e-4;
+    c->per_alpha = 0.6;
+    c->per_max_priority = 1.0;
+    c->per_beta_start = 0.4;
+    c->per_beta_end = 1.0;
+    c->per_beta_steps = 2e6;
+}
+
+int dqnx_engine_create(const dqnx_config* cfg, dqnx_engine** out) {
+    if (!cfg || !out) return set_error(DQNX_EINVAL, "null argument");
+    *out = nullptr;
+    dqnx_engine* e = new dqnx_engine();
+    e->cfg = *cfg;
+    int rc = plan_net(&cfg->net, e->np);
+    if (rc) { delete e; return rc; }
+    const dqnx_config& c = e->cfg;
+    if (c.net.kind != DQNX_NET_MLP) { delete e; return set_error(DQNX_EUNSUPPORTED, "two-stream network not built yet"); }
+    if (c.algo < DQNX_ALGO_DQN || c.algo > DQNX_ALGO_PER_DOUBLE) { delete e; return set_error(DQNX_EINVAL, "bad algo"); }
+    if (c.algo == DQNX_ALGO_PER_DOUBLE) { delete e; return set_error(DQNX_EUNSUPPORTED, "PER learn step not built yet"); }
+    if (c.batch <= 0 || c.world_size <= 0 || c.rank < 0 || c.rank >= c.world_size || c.batch % c.world_size)
+        { delete e; return set_error(DQNX_EINVAL, "batch must be a positive multiple of world_size"); }
+    if (c.capacity <= 0 || c.capacity >= ((int64_t)1 << 31)) { delete e; return set_error(DQNX_EINVAL, "capacity out of range"); }
+    if (e->np.NH > 16) { delete e; return set_error(DQNX_EUNSUPPORTED, "head with more than 16 outputs"); }
+    for (size_t l = 0; l < e->np.dense.size(); l++)
+        if (e->np.dense[l].out % 4) { delete e; return set_error(DQNX_EUNSUPPORTED, "hidden widths must be multiples of 4"); }
+    if (sample_hash_slots(c.batch) < 0) { delete e; return set_error(DQNX_EUNSUPPORTED, "batch too large for the sampler"); }
+    e->Bg = c.batch;
+    e->Bl = c.batch / c.world_size;
+    e->shard_begin = c.rank * e->Bl;
+    e->stride = (int)align_up((uint64_t)c.net.obs_dim, 4);
+    e->tiles = (e->Bl + 15) / 16;
+    e->setsize = sample_setsize(e->Bg);
+    const int L = (int)e->np.dense.size();
+    e->slices.assign(L, 1);
+    e->kslice.assign(L, e->Bl);
+    for (int l = 0; l < L; l++) {
+        int S = e->Bl / 128;
+        if (S < 1) S = 1;
+        if (S > 32) S = 32;
+        int ks = (int)align_up((uint64_t)((e->Bl + S - 1) / S), 16);
+        S = (e->Bl + ks - 1) / ks;
+        e->slices[l] = S;
+        e->kslice[l] = ks;
+    }
+    layout(e);
+    *out = e;
+    return DQNX_OK;
+}
+
+int dqnx_engine_destroy(dqnx_engine* e) {
+    if (!e) return DQNX_OK;
+    drop_graphs(e);
+    if (e->capture_stream) (void)hipStreamDestroy(e->capture_stream);
+    delete e;
+    return DQNX_OK;
+}
+
+int dqnx_engine_arena_bytes(const dqnx_engine* e, uint64_t* bytes) {
+    if (!e || !bytes) return set_error(DQNX_EINVAL, "null argument");
+    *bytes = e->total;
+    return DQNX_OK;
+}
+
+int dqnx_engine_buffer(const dqnx_engine* e, int32_t which, uint64_t* offset, uint64_t* bytes) {
+    if (!e || which < 0 || which >= DQNX_BUF_COUNT) return set_error(DQNX_EINVAL, "bad buffer id %d", which);
+    if (offset) *offset = e->off[which];
+    if (bytes) *bytes = e->bytes[which];
+    return DQNX_OK;
+}
+
+int dqnx_engine_obs_stride(const dqnx_engine* e, int32_t* stride) {
+    if (!e || !stride) return set_error(DQNX_EINVAL, "null argument");
+    *stride = e->stride;
+    return DQNX_OK;
+}
+
+int dqnx_engine_bind(dqnx_engine* e, void* arena, uint64_t bytes) {
+    if (!e || !arena) return set_error(DQNX_EINVAL, "null argument");
+    if (bytes < e->total) return set_error(DQNX_EINVAL, "arena too small: %llu < %llu", (unsigned long long)bytes,
+                                           (unsigned long long)e->total);
+    if (((uintptr_t)arena) % 256) return set_error(DQNX_EINVAL, "arena must be 256-byte aligned");
+    drop_graphs(e);
+    e->arena = (char*)arena;
+    return DQNX_OK;
+}
+
+int dqnx_engine_set_graphs(dqnx_engine* e, int32_t enabled) {
+    if (!e) return set_error(DQNX_EINVAL, "null engine");
+    e->graphs = enabled != 0;
+    if (!e->graphs) drop_graphs(e);
+    return DQNX_OK;
+}
+
+int dqnx_engine_reset(dqnx_engine* e, void* stream) {
+    int rc = check_bound(e);
+    if (rc) return rc;
+    hipStream_t s = (hipStream_t)stream;
+    const int ids[] = {DQNX_BUF_GRADS, DQNX_BUF_ADAM_M, DQNX_BUF_ADAM_V, DQNX_BUF_CTRL, DQNX_BUF_RING_OBS,
+                       DQNX_BUF_RING_NEXT_OBS, DQNX_BUF_RING_ACT, DQNX_BUF_RING_REW, DQNX_BUF_RING_DONE,
+                       DQNX_BUF_SUMTREE, DQNX_BUF_BATCH_IDX, DQNX_BUF_Q, DQNX_BUF_TD, DQNX_BUF_IS_WEIGHTS,
+                       DQNX_BUF_WORKSPACE};
+    for (int id : ids)
+        if (e->bytes[id]) DQNX_HIP_CHECK(hipMemsetAsync(e->arena + e->off[id], 0, e->bytes[id], s));
+    // SumTree.max/min_priority_index start at capacity - 1 (R:dqn/utils/sum_tree.py:12-13)
+    dqnx_ctrl init;
+    memset(&init, 0, sizeof(init));
+    init.per_max_idx = e->cfg.capacity - 1;
+    init.per_min_idx = e->cfg.capacity - 1;
+    DQNX_HIP_CHECK(hipMemcpyAsync(&ctrl_of(e)->per_max_idx, &init.per_max_idx, 2 * sizeof(int64_t),
+                                  hipMemcpyHostToDevice, s));
+    DQNX_HIP_CHECK(hipStreamSynchronize(s));
+    e->ring_size = 0;
+    e->ring_wptr = 0;
+    return DQNX_OK;
+}
+
+int dqnx_replay_push(dqnx_engine* e, const float* obs, const int32_t* act, const float* rew, const uint8_t* done,
+                     const float* next_obs, int32_t n, int32_t src_on_device, void* stream) {
+    int rc = check_bound(e);
+    if (rc) return rc;
+    if (n < 0 || (n > 0 && (!obs || !act || !rew || !done || !next_obs)))
+        return set_error(DQNX_EINVAL, "dqnx_replay_push: bad argument");
+    if (e->cfg.algo == DQNX_ALGO_PER_DOUBLE) return set_error(DQNX_EUNSUPPORTED, "PER push not built yet");
+    hipStream_t s = (hipStream_t)stream;
+    const int D = e->cfg.net.obs_dim;
+    int done_rows = 0;
+    while (done_rows < n) {
+        const int m = src_on_device ? n - done_rows : std::min(n - done_rows, e->stage_rows);
+        PushArgs pa;
+        memset(&pa, 0, sizeof(pa));
+        if (src_on_device) {
+            pa.obs = obs + (int64_t)done_rows * D;
+            pa.next_obs = next_obs + (int64_t)done_rows * D;
+            pa.act = act + done_rows;
+            pa.rew = rew + done_rows;
+            pa.done = done + done_rows;
+        } else {
+            char* st = e->arena + e->ws_stage;
+            float* so = (float*)st;
+            float* sn = so + (int64_t)e->stage_rows * D;
+            int32_t* sa = (int32_t*)(sn + (int64_t)e->stage_rows * D);
+            float* sr = (float*)(sa + e->stage_rows);
+            uint8_t* sd = (uint8_t*)(sr + e->stage_rows);
+            DQNX_HIP_CHECK(hipMemcpyAsync(so, obs + (int64_t)done_rows * D, (size_t)m * D * 4, hipMemcpyHostToDevice, s));
+            DQNX_HIP_CHECK(hipMemcpyAsync(sn, next_obs + (int64_t)done_rows * D, (size_t)m * D * 4, hipMemcpyHostToDevice, s));
+            DQNX_HIP_CHECK(hipMemcpyAsync(sa, act + done_rows, (size_t)m * 4, hipMemcpyHostToDevice, s));
+            DQNX_HIP_CHECK(hipMemcpyAsync(sr, rew + done_rows, (size_t)m * 4, hipMemcpyHostToDevice, s));
+            DQNX_HIP_CHECK(hipMemcpyAsync(sd, done + done_rows, (size_t)m, hipMemcpyHostToDevice, s));
+            pa.obs = so;
+            pa.next_obs = sn;
+            pa.act = sa;
+            pa.rew = sr;
+            pa.done = sd;
+        }
+        const int64_t cap = e->cfg.capacity;
+        pa.n = m;
+        pa.obs_dim = D;
+        pa.stride = e->stride;
+        pa.wptr = e->ring_wptr;
+        pa.capacity = cap;
+        pa.new_wptr = (e->ring_wptr + m) % cap;
+        pa.new_size = std::min<int64_t>(e->ring_size + m, cap);
+        pa.ring_obs = at<float>(e, e->off[DQNX_BUF_RING_OBS]);
+        pa.ring_next = at<float>(e, e->off[DQNX_BUF_RING_NEXT_OBS]);
+        pa.ring_act = at<int32_t>(e, e->off[DQNX_BUF_RING_ACT]);
+        pa.ring_rew = at<float>(e, e->off[DQNX_BUF_RING_REW]);
+        pa.ring_done = at<float>(e, e->off[DQNX_BUF_RING_DONE]);
+        pa.ctrl = ctrl_of(e);
+        if (m > cap) {
+            // only the last `cap` rows survive; push them alone
+            const int skip = (int)(m - cap);
+            e->ring_wptr = (e->ring_wptr + skip) % cap;
+            e->ring_size = std::min<int64_t>(e->ring_size + skip, cap);
+            pa.obs += (int64_t)skip * D;
+            pa.next_obs += (int64_t)skip * D;
+            pa.act += skip;
+            pa.rew += skip;
+            pa.done += skip;
+            pa.n = (int)cap;
+            pa.wptr = e->ring_wptr;
+            pa.new_wptr = (e->ring_wptr + cap) % cap;
+            pa.new_size = cap;
+        }
+        rc = launch_replay_push(pa, s);
+        if (rc) return rc;
+        e->ring_wptr = pa.new_wptr;
+        e->ring_size = pa.new_size;
+        done_rows += m;
+        if (!src_on_device) DQNX_HIP_CHECK(hipStreamSynchronize(s));  // staging buffer reuse
+    }
+    return DQNX_OK;
+}
+
+int dqnx_rng_set(dqnx_engine* e, int32_t which, const uint32_t* state625, void* stream) {
+    int rc = check_bound(e);
+    if (rc) return rc;
+    if (!state625 || (which != DQNX_RNG_PY && which != DQNX_RNG_NP)) return set_error(DQNX_EINVAL, "bad argument");
+    if (state625[624] > 624) return set_error(DQNX_EINVAL, "MT index must be <= 624");
+    hipStream_t s = (hipStream_t)stream;
+    uint32_t* dst = which == DQNX_RNG_PY ? ctrl_of(e)->py_mt : ctrl_of(e)->np_mt;
+    DQNX_HIP_CHECK(hipMemcpyAsync(dst, state625, 625 * 4, hipMemcpyHostToDevice, s));
+    DQNX_HIP_CHECK(hipStreamSynchronize(s));
+    return DQNX_OK;
+}
+
+int dqnx_rng_get(dqnx_engine* e, int32_t which, uint32_t* state625, void* stream) {
+    int rc = check_bound(e);
+    if (rc) return rc;
+    if (!state625 || (which != DQNX_RNG_PY && which != DQNX_RNG_NP)) return set_error(DQNX_EINVAL, "bad argument");
+    hipStream_t s = (hipStream_t)stream;
+    const uint32_t* src = which == DQNX_RNG_PY ? ctrl_of(e)->py_mt : ctrl_of(e)->np_mt;
+    DQNX_HIP_CHECK(hipMemcpyAsync(state625, src, 625 * 4, hipMemcpyDeviceToHost, s));
+    DQNX_HIP_CHECK(hipStreamSynchronize(s));
+    return DQNX_OK;
+}
+
+int dqnx_learn_step(dqnx_engine* e, int32_t flags, void* stream) {
+    int rc = check_bound(e);
+    if (rc) return rc;
+    if (e->ring_size < e->Bg && !(flags & DQNX_STEP_GIVEN_INDICES))
+        return set_error(DQNX_EINVAL, "Sample larger than population: %lld < %d", (long long)e->ring_size, e->Bg);
+    const int key = flags & (DQNX_STEP_SOFT_UPDATE | DQNX_STEP_GIVEN_INDICES | DQNX_STEP_GRADS_ONLY);
+    const std::vector<KStep>& ks = steps_for(e, key);
+    return run_graphed(e, key, (hipStream_t)stream,
+                       [&](hipStream_t s) { return enqueue_range(ks, 0, (int)ks.size(), s); });
+}
+
+int dqnx_learn_kernel_count(dqnx_engine* e, int32_t flags, int32_t* n) {
+    int rc = check_bound(e);
+    if (rc) return rc;
+    if (!n) return set_error(DQNX_EINVAL, "null argument");
+    *n = (int32_t)steps_for(e, flags & 7).size();
+    return DQNX_OK;
+}
+
+int dqnx_learn_kernel_info(dqnx_engine* e, int32_t flags, int32_t i, char* name, int32_t name_len, double* flops,
+                           double* bytes) {
+    int rc = check_bound(e);
+    if (rc) return rc;
+    const std::vector<KStep>& ks = steps_for(e, flags & 7);
+    if (i < 0 || i >= (int32_t)ks.size()) return set_error(DQNX_EINVAL, "kernel index %d out of range", i);
+    if (name && name_len > 0) snprintf(name, (size_t)name_len, "%s", ks[i].name.c_str());
+    if (flops) *flops = ks[i].flops;
+    if (bytes) *bytes = ks[i].bytes;
+    return DQNX_OK;
+}
+
+int dqnx_learn_step_timed(dqnx_engine* e, int32_t flags, int32_t kernel_index, void* ev_start, void* ev_stop,
+                          void* stream) {
+    int rc = check_bound(e);
+    if (rc) return rc;
+    if (!ev_start || !ev_stop) return set_error(DQNX_EINVAL, "null event");
+    if (e->ring_size < e->Bg && !(flags & DQNX_STEP_GIVEN_INDICES))
+        return set_error(DQNX_EINVAL, "Sample larger than population: %lld < %d", (long long)e->ring_size, e->Bg);
+    const int key = flags & 7;
+    const std::vector<KStep>& ks = steps_for(e, key);
+    const int n = (int)ks.size();
+    if (kernel_index < 0 || kernel_index >= n) return set_error(DQNX_EINVAL, "kernel index out of range");
+    hipStream_t s = (hipStream_t)stream;
+    const int base = key | (kernel_index << 12);
+    if (kernel_index > 0) {
+        rc = run_graphed(e, base | (1 << 8), s, [&](hipStream_t cs) { return enqueue_range(ks, 0, kernel_index, cs); });
+        if (rc) return rc;
+    }
+    DQNX_HIP_CHECK(hipEventRecord((hipEvent_t)ev_start, s));
+    rc = run_graphed(e, base | (2 << 8), s,
+                     [&](hipStream_t cs) { return enqueue_range(ks, kernel_index, kernel_index + 1, cs); });
+    if (rc) return rc;
+    DQNX_HIP_CHECK(hipEventRecord((hipEvent_t)ev_stop, s));
+    if (kernel_index + 1 < n)
+        rc = run_graphed(e, base | (3 << 8), s,
+                         [&](hipStream_t cs) { return enqueue_range(ks, kernel_index + 1, n, cs); });
+    return rc;
+}
+
+int dqnx_events_create(int32_t n, void** events) {
+    if (n < 0 || (n && !events)) return set_error(DQNX_EINVAL, "bad argument");
+    for (int i = 0; i < n; i++) {
+        hipEvent_t ev;
+        DQNX_HIP_CHECK(hipEventCreate(&ev));
+        events[i] = (void*)ev;
+    }
+    return DQNX_OK;
+}
+
+int dqnx_events_destroy(int32_t n, void** events) {
+    for (int i = 0; i < n; i++)
+        if (events && events[i]) (void)hipEventDestroy((hipEvent_t)events[i]);
+    return DQNX_OK;
+}
+
+int dqnx_event_elapsed(void* start, void* stop, float* ms) {
+    if (!start || !stop || !ms) return set_error(DQNX_EINVAL, "null argument");
+    DQNX_HIP_CHECK(hipEventSynchronize((hipEvent_t)stop));
+    DQNX_HIP_CHECK(hipEventElapsedTime(ms, (hipEvent_t)start, (hipEvent_t)stop));
+    return DQNX_OK;
+}
+
+int dqnx_apply_grads(dqnx_engine* e, int32_t flags, void* stream) {
+    int rc = check_bound(e);
+    if (rc) return rc;
+    const int key = 0x100 | (flags & DQNX_STEP_SOFT_UPDATE);
+    return run_graphed(e, key, (hipStream_t)stream, [&](hipStream_t s) { return enqueue_apply(e, key, s); });
+}
+
+int dqnx_soft_update(dqnx_engine* e, void* stream) {
+    int rc = check_bound(e);
+    if (rc) return rc;
+    const float tau = (float)((double)e->cfg.tau * e->cfg.n_env);
+    const float omt = (float)(1.0 - (double)e->cfg.tau * e->cfg.n_env);
+    return launch_soft_update(at<float>(e, e->off[DQNX_BUF_TARGET_PARAMS]), at<float>(e, e->off[DQNX_BUF_PARAMS]),
+                              e->np.P, tau, omt, (hipStream_t)stream);
+}
+
+int dqnx_hard_update(dqnx_engine* e, void* stream) {
+    int rc = check_bound(e);
+    if (rc) return rc;
+    DQNX_HIP_CHECK(hipMemcpyAsync(e->arena + e->off[DQNX_BUF_TARGET_PARAMS], e->arena + e->off[DQNX_BUF_PARAMS],
+                                  (size_t)e->np.P * 4, hipMemcpyDeviceToDevice, (hipStream_t)stream));
+    return DQNX_OK;
+}
+
+}  // extern "C"

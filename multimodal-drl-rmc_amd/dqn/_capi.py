@@ -1,0 +1,144 @@
+"""ctypes binding of include/dqnx.h (libdqnx.so, the gfx950 HIP engine).
+
+The library is built in-tree (``multimodal-drl-rmc_amd/dqn/_lib/libdqnx.so``, see the
+package Makefile / ``__graft_entry__.build()``).  There is no fallback: if the library
+is missing this module raises, and every engine entry point that touches the GPU
+raises ``RuntimeError`` with ``dqnx_last_error()``.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "_lib", "libdqnx.so")
+
+# ---- constants (mirror dqnx.h) --------------------------------------------------------
+DQNX_OK = 0
+DQNX_NET_MLP, DQNX_NET_TWO_STREAM = 0, 1
+DQNX_HEAD_LINEAR, DQNX_HEAD_DUELING = 0, 1
+DQNX_ACT_RELU, DQNX_ACT_ELU = 0, 1
+DQNX_ALGO_DQN, DQNX_ALGO_DOUBLE, DQNX_ALGO_PER_DOUBLE = 0, 1, 2
+DQNX_MAX_DENSE, DQNX_MAX_CONV = 6, 4
+(BUF_PARAMS, BUF_TARGET_PARAMS, BUF_GRADS, BUF_ADAM_M, BUF_ADAM_V, BUF_CTRL, BUF_RING_OBS,
+ BUF_RING_NEXT_OBS, BUF_RING_ACT, BUF_RING_REW, BUF_RING_DONE, BUF_SUMTREE, BUF_BATCH_IDX, BUF_Q,
+ BUF_TD, BUF_IS_WEIGHTS, BUF_WORKSPACE, BUF_COUNT) = range(18)
+DQNX_RNG_PY, DQNX_RNG_NP = 0, 1
+STEP_SOFT_UPDATE = 0x1
+STEP_GIVEN_INDICES = 0x2
+STEP_GRADS_ONLY = 0x4
+DEVERR_SAMPLE_TOO_LARGE = 1
+DEVERR_EMPTY_TREE = 2
+
+I32 = ctypes.c_int32
+I64 = ctypes.c_int64
+
+
+class NetDesc(ctypes.Structure):
+    _fields_ = [
+        ("kind", I32), ("head", I32), ("activation", I32), ("obs_dim", I32), ("n_actions", I32),
+        ("n_dense", I32), ("dense", I32 * DQNX_MAX_DENSE),
+        ("macro_len", I32), ("micro_c", I32), ("micro_h", I32), ("micro_w", I32), ("n_conv", I32),
+        ("conv_out", I32 * DQNX_MAX_CONV), ("conv_kh", I32 * DQNX_MAX_CONV), ("conv_kw", I32 * DQNX_MAX_CONV),
+        ("conv_sh", I32 * DQNX_MAX_CONV), ("conv_sw", I32 * DQNX_MAX_CONV),
+    ]
+
+
+class ParamInfo(ctypes.Structure):
+    _fields_ = [("name", ctypes.c_char * 48), ("offset", I64), ("numel", I64), ("ndim", I32),
+                ("shape", I32 * 4)]
+
+
+class Config(ctypes.Structure):
+    _fields_ = [
+        ("net", NetDesc), ("algo", I32), ("batch", I32), ("world_size", I32), ("rank", I32),
+        ("capacity", I64), ("gamma", ctypes.c_float), ("lr", ctypes.c_float), ("beta1", ctypes.c_float),
+        ("beta2", ctypes.c_float), ("adam_eps", ctypes.c_float), ("tau", ctypes.c_float), ("n_env", I32),
+        ("reserved0", I32), ("per_eps", ctypes.c_double), ("per_alpha", ctypes.c_double),
+        ("per_max_priority", ctypes.c_double), ("per_beta_start", ctypes.c_double),
+        ("per_beta_end", ctypes.c_double), ("per_beta_steps", ctypes.c_double),
+    ]
+
+
+class Ctrl(ctypes.Structure):
+    _fields_ = [
+        ("py_mt", ctypes.c_uint32 * 625), ("np_mt", ctypes.c_uint32 * 625), ("ring_size", I64),
+        ("ring_wptr", I64), ("adam_step", I64), ("agent_step", I64), ("per_max_idx", I64),
+        ("per_min_idx", I64), ("loss", ctypes.c_float), ("error", I32), ("adam_step_size", ctypes.c_float),
+        ("adam_bc2_sqrt", ctypes.c_float), ("per_beta", ctypes.c_double), ("reserved", I64 * 8),
+    ]
+
+
+# every symbol the header declares (checked by tests/test_capi.py)
+EXPORTS = [
+    "dqnx_net_param_count", "dqnx_net_param_info", "dqnx_config_defaults", "dqnx_engine_create",
+    "dqnx_engine_destroy", "dqnx_engine_arena_bytes", "dqnx_engine_buffer", "dqnx_engine_obs_stride",
+    "dqnx_engine_bind", "dqnx_engine_reset", "dqnx_engine_set_graphs", "dqnx_replay_push", "dqnx_rng_set",
+    "dqnx_rng_get", "dqnx_learn_step", "dqnx_apply_grads", "dqnx_soft_update", "dqnx_hard_update",
+    "dqnx_sample_scratch_bytes", "dqnx_sample_uniform", "dqnx_last_error", "dqnx_abi_version",
+    "dqnx_learn_kernel_count", "dqnx_learn_kernel_info", "dqnx_learn_step_timed", "dqnx_events_create",
+    "dqnx_events_destroy", "dqnx_event_elapsed",
+]
+
+_lib = None
+
+
+class DqnxError(RuntimeError):
+    pass
+
+
+def lib():
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(
+            f"libdqnx.so not built ({LIB_PATH}); run `make -C multimodal-drl-rmc_amd` or "
+            "__graft_entry__.build().  There is no CPU fallback.")
+    L = ctypes.CDLL(LIB_PATH)
+    vp = ctypes.c_void_p
+    P = ctypes.POINTER
+    sig = {
+        "dqnx_net_param_count": ([P(NetDesc), P(I64), P(I32)], ctypes.c_int),
+        "dqnx_net_param_info": ([P(NetDesc), I32, P(ParamInfo)], ctypes.c_int),
+        "dqnx_config_defaults": ([P(Config)], None),
+        "dqnx_engine_create": ([P(Config), P(vp)], ctypes.c_int),
+        "dqnx_engine_destroy": ([vp], ctypes.c_int),
+        "dqnx_engine_arena_bytes": ([vp, P(ctypes.c_uint64)], ctypes.c_int),
+        "dqnx_engine_buffer": ([vp, I32, P(ctypes.c_uint64), P(ctypes.c_uint64)], ctypes.c_int),
+        "dqnx_engine_obs_stride": ([vp, P(I32)], ctypes.c_int),
+        "dqnx_engine_bind": ([vp, vp, ctypes.c_uint64], ctypes.c_int),
+        "dqnx_engine_reset": ([vp, vp], ctypes.c_int),
+        "dqnx_engine_set_graphs": ([vp, I32], ctypes.c_int),
+        "dqnx_replay_push": ([vp, vp, vp, vp, vp, vp, I32, I32, vp], ctypes.c_int),
+        "dqnx_rng_set": ([vp, I32, P(ctypes.c_uint32), vp], ctypes.c_int),
+        "dqnx_rng_get": ([vp, I32, P(ctypes.c_uint32), vp], ctypes.c_int),
+        "dqnx_learn_step": ([vp, I32, vp], ctypes.c_int),
+        "dqnx_apply_grads": ([vp, I32, vp], ctypes.c_int),
+        "dqnx_soft_update": ([vp, vp], ctypes.c_int),
+        "dqnx_hard_update": ([vp, vp], ctypes.c_int),
+        "dqnx_sample_scratch_bytes": ([I64, I32], ctypes.c_uint64),
+        "dqnx_sample_uniform": ([vp, I64, I32, vp, vp, vp, vp], ctypes.c_int),
+        "dqnx_last_error": ([], ctypes.c_char_p),
+        "dqnx_learn_kernel_count": ([vp, I32, P(I32)], ctypes.c_int),
+        "dqnx_learn_kernel_info": ([vp, I32, I32, ctypes.c_char_p, I32, P(ctypes.c_double), P(ctypes.c_double)],
+                                   ctypes.c_int),
+        "dqnx_learn_step_timed": ([vp, I32, I32, vp, vp, vp], ctypes.c_int),
+        "dqnx_events_create": ([I32, P(vp)], ctypes.c_int),
+        "dqnx_events_destroy": ([I32, P(vp)], ctypes.c_int),
+        "dqnx_event_elapsed": ([vp, vp, P(ctypes.c_float)], ctypes.c_int),
+        "dqnx_abi_version": ([], I32),
+    }
+    for name, (args, res) in sig.items():
+        f = getattr(L, name)
+        f.argtypes = args
+        f.restype = res
+    _lib = L
+    return L
+
+
+def check(rc: int, what: str = ""):
+    if rc != DQNX_OK:
+        msg = lib().dqnx_last_error().decode(errors="replace")
+        raise DqnxError(f"{what}: dqnx error {rc}: {msg}")
+    return rc

@@ -1,0 +1,280 @@
+"""LearnEngine: the Python face of libdqnx (one engine = one agent's learn-step state).
+
+The engine's whole device state lives in ONE torch-allocated HBM arena (parameters,
+target parameters, gradient, Adam moments, control block, replay ring, workspace);
+libdqnx only borrows it.  ``LearnEngine`` exposes torch views of every region so the
+host shim can keep the reference's ``state_dict()`` / checkpoint behaviour.
+
+No CPU fallback: constructing an engine without a GPU or without libdqnx.so raises.
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+from typing import Optional, Sequence, Tuple
+
+import numpy as np
+import torch
+import torch.nn as nn
+
+from . import _capi as C
+
+ALGO_IDS = {"DQNAgent": C.DQNX_ALGO_DQN, "DoubleDQNAgent": C.DQNX_ALGO_DOUBLE,
+            "DuelingDoubleDQNAgent": C.DQNX_ALGO_DOUBLE, "PerDuelingDoubleDQNAgent": C.DQNX_ALGO_PER_DOUBLE}
+
+
+# ----------------------------------------------------------------------------------------
+# network description
+# ----------------------------------------------------------------------------------------
+@dataclass
+class NetSpec:
+    """What libdqnx needs to know about a Q-network (mirrors dqnx_net_desc)."""
+    kind: int = C.DQNX_NET_MLP
+    head: int = C.DQNX_HEAD_DUELING
+    activation: int = C.DQNX_ACT_RELU
+    obs_dim: int = 284
+    n_actions: int = 8
+    dense: Tuple[int, ...] = (256, 128)
+    macro_len: int = 0
+    micro_chw: Tuple[int, int, int] = (0, 0, 0)
+    conv: Tuple[Tuple[int, Tuple[int, int], Tuple[int, int]], ...] = ()
+
+    def to_c(self) -> C.NetDesc:
+        d = C.NetDesc()
+        d.kind, d.head, d.activation = self.kind, self.head, self.activation
+        d.obs_dim, d.n_actions = self.obs_dim, self.n_actions
+        d.n_dense = len(self.dense)
+        for i, w in enumerate(self.dense):
+            d.dense[i] = w
+        d.macro_len = self.macro_len
+        d.micro_c, d.micro_h, d.micro_w = self.micro_chw
+        d.n_conv = len(self.conv)
+        for i, (f, (kh, kw), (sh, sw)) in enumerate(self.conv):
+            d.conv_out[i], d.conv_kh[i], d.conv_kw[i], d.conv_sh[i], d.conv_sw[i] = f, kh, kw, sh, sw
+        return d
+
+    def param_infos(self):
+        L = C.lib()
+        d = self.to_c()
+        n = C.I64()
+        nt = C.I32()
+        C.check(L.dqnx_net_param_count(ctypes.byref(d), ctypes.byref(n), ctypes.byref(nt)), "param_count")
+        out = []
+        for i in range(nt.value):
+            pi = C.ParamInfo()
+            C.check(L.dqnx_net_param_info(ctypes.byref(d), i, ctypes.byref(pi)), "param_info")
+            out.append((pi.name.decode(), int(pi.offset), tuple(pi.shape[:pi.ndim])))
+        return int(n.value), out
+
+
+def mlp_spec(obs_dim=284, n_actions=8, head="dueling", hidden=(256, 128)) -> NetSpec:
+    return NetSpec(kind=C.DQNX_NET_MLP, head=C.DQNX_HEAD_DUELING if head == "dueling" else C.DQNX_HEAD_LINEAR,
+                   activation=C.DQNX_ACT_RELU, obs_dim=obs_dim, n_actions=n_actions, dense=tuple(hidden))
+
+
+def spec_from_body(net: nn.Module, obs_dim: int, n_actions: int, dueling: bool) -> NetSpec:
+    """Recognise the two body families the reference ships (SURVEY §7 hard part 6) and
+    refuse anything else:
+      * nn.Sequential(Linear, ReLU|ELU, Linear, ReLU|ELU, ...)
+        (R:env/custom_env/macro with lane/dqn_config.py:76-84)
+      * TwoStreamHybridNetwork (R:env/dqn_config.py:66-143)."""
+    head = C.DQNX_HEAD_DUELING if dueling else C.DQNX_HEAD_LINEAR
+    if isinstance(net, nn.Sequential):
+        mods = list(net)
+        if len(mods) % 2 or len(mods) == 0:
+            raise NotImplementedError("libdqnx: MLP body must alternate Linear and activation")
+        dense, act = [], None
+        d = obs_dim
+        for i in range(0, len(mods), 2):
+            lin, a = mods[i], mods[i + 1]
+            if not isinstance(lin, nn.Linear) or lin.in_features != d or lin.bias is None:
+                raise NotImplementedError(f"libdqnx: unsupported MLP layer {lin!r}")
+            k = C.DQNX_ACT_RELU if isinstance(a, nn.ReLU) else (C.DQNX_ACT_ELU if isinstance(a, nn.ELU) else None)
+            if k is None or (act is not None and k != act):
+                raise NotImplementedError(f"libdqnx: unsupported activation {a!r}")
+            if isinstance(a, nn.ELU) and a.alpha != 1.0:
+                raise NotImplementedError("libdqnx: ELU alpha must be 1")
+            act = k
+            dense.append(lin.out_features)
+            d = lin.out_features
+        return NetSpec(kind=C.DQNX_NET_MLP, head=head, activation=act, obs_dim=obs_dim, n_actions=n_actions,
+                       dense=tuple(dense))
+    if hasattr(net, "cnn_stream") and hasattr(net, "dense_stream") and hasattr(net, "micro_shape"):
+        conv = []
+        mods = list(net.cnn_stream)
+        for i in range(0, len(mods), 2):
+            cv = mods[i]
+            if not isinstance(cv, nn.Conv2d) or cv.padding != (cv.kernel_size[0] // 2, cv.kernel_size[1] // 2):
+                raise NotImplementedError(f"libdqnx: unsupported conv {cv!r}")
+            conv.append((cv.out_channels, tuple(cv.kernel_size), tuple(cv.stride)))
+        dense = [m.out_features for m in net.dense_stream if isinstance(m, nn.Linear)]
+        acts = [m for m in list(net.cnn_stream) + list(net.dense_stream) if not isinstance(m, (nn.Linear, nn.Conv2d))]
+        if not all(isinstance(a, nn.ELU) and a.alpha == 1.0 for a in acts):
+            raise NotImplementedError("libdqnx: two-stream net must use ELU(alpha=1)")
+        return NetSpec(kind=C.DQNX_NET_TWO_STREAM, head=head, activation=C.DQNX_ACT_ELU, obs_dim=obs_dim,
+                       n_actions=n_actions, dense=tuple(dense), macro_len=int(net.macro_len),
+                       micro_chw=tuple(int(x) for x in net.micro_shape), conv=tuple(conv))
+    raise NotImplementedError(f"libdqnx: unsupported Q-network body {type(net).__name__}")
+
+
+# ----------------------------------------------------------------------------------------
+# engine
+# ----------------------------------------------------------------------------------------
+class LearnEngine:
+    """One agent's learn-step engine on one GPU (one process per GPU under DP)."""
+
+    def __init__(self, spec: NetSpec, algo: str, batch: int, capacity: int, gamma=0.99, lr=1e-4,
+                 tau=1e-3, n_env=1, world_size=1, rank=0, device=None, graphs=True, eps_dec=2e6):
+        if not torch.cuda.is_available():
+            raise RuntimeError("libdqnx needs a ROCm GPU (MI355X / gfx950); there is no CPU fallback")
+        self.L = C.lib()
+        self.spec = spec
+        self.algo = algo
+        self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+        cfg = C.Config()
+        cfg.net = spec.to_c()
+        self.L.dqnx_config_defaults(ctypes.byref(cfg))
+        cfg.algo = ALGO_IDS[algo] if isinstance(algo, str) else int(algo)
+        cfg.batch, cfg.world_size, cfg.rank, cfg.capacity = batch, world_size, rank, capacity
+        cfg.gamma, cfg.lr, cfg.tau, cfg.n_env = gamma, lr, tau, n_env
+        cfg.per_beta_steps = eps_dec
+        self.cfg = cfg
+        h = ctypes.c_void_p()
+        C.check(self.L.dqnx_engine_create(ctypes.byref(cfg), ctypes.byref(h)), "dqnx_engine_create")
+        self.h = h
+        nbytes = ctypes.c_uint64()
+        C.check(self.L.dqnx_engine_arena_bytes(h, ctypes.byref(nbytes)), "arena_bytes")
+        self.arena = torch.zeros(int(nbytes.value), dtype=torch.uint8, device=self.device)
+        C.check(self.L.dqnx_engine_bind(h, ctypes.c_void_p(self.arena.data_ptr()), nbytes.value), "bind")
+        C.check(self.L.dqnx_engine_set_graphs(h, 1 if graphs else 0), "set_graphs")
+        st = C.I32()
+        C.check(self.L.dqnx_engine_obs_stride(h, ctypes.byref(st)), "obs_stride")
+        self.obs_stride = st.value
+        self.batch, self.capacity, self.world_size, self.rank = batch, capacity, world_size, rank
+        self.batch_local = batch // world_size
+        self.n_params, self.param_layout = spec.param_infos()
+        self.reset()
+        self.params = self.view(C.BUF_PARAMS, torch.float32)
+        self.target_params = self.view(C.BUF_TARGET_PARAMS, torch.float32)
+        self.grads = self.view(C.BUF_GRADS, torch.float32)          # [P + 1], last = loss
+        self.adam_m = self.view(C.BUF_ADAM_M, torch.float32)
+        self.adam_v = self.view(C.BUF_ADAM_V, torch.float32)
+        self.ctrl_bytes = self.view(C.BUF_CTRL, torch.uint8)
+        self.batch_idx = self.view(C.BUF_BATCH_IDX, torch.int32)
+        self.q = self.view(C.BUF_Q, torch.float32).view(3, self.batch_local, spec.n_actions)
+        self.td = self.view(C.BUF_TD, torch.float32).view(3, self.batch_local)
+        self.is_weights = self.view(C.BUF_IS_WEIGHTS, torch.float32)
+        self.ring_obs = self.view(C.BUF_RING_OBS, torch.float32).view(capacity, self.obs_stride)
+        self.ring_next_obs = self.view(C.BUF_RING_NEXT_OBS, torch.float32).view(capacity, self.obs_stride)
+        self.ring_act = self.view(C.BUF_RING_ACT, torch.int32)
+        self.ring_rew = self.view(C.BUF_RING_REW, torch.float32)
+        self.ring_done = self.view(C.BUF_RING_DONE, torch.float32)
+        self.ring_size = 0
+        self.ring_wptr = 0
+
+    # ---- plumbing ------------------------------------------------------------------
+    def buffer(self, which) -> Tuple[int, int]:
+        o, b = ctypes.c_uint64(), ctypes.c_uint64()
+        C.check(self.L.dqnx_engine_buffer(self.h, which, ctypes.byref(o), ctypes.byref(b)), "buffer")
+        return int(o.value), int(b.value)
+
+    def view(self, which, dtype):
+        o, b = self.buffer(which)
+        t = self.arena[o:o + b]
+        return t.view(dtype) if b else t.view(dtype)
+
+    def stream(self):
+        return ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+
+    def __del__(self):
+        try:
+            if getattr(self, "h", None):
+                self.L.dqnx_engine_destroy(self.h)
+                self.h = None
+        except Exception:
+            pass
+
+    def reset(self):
+        C.check(self.L.dqnx_engine_reset(self.h, self.stream()), "reset")
+        self.ring_size = 0
+        self.ring_wptr = 0
+
+    def param_views(self, flat: torch.Tensor):
+        """name -> view into a flat parameter vector, in state_dict order."""
+        return {name: flat[off:off + int(np.prod(shape))].view(*shape) for name, off, shape in self.param_layout}
+
+    def load_params(self, state: dict, target: Optional[dict] = None):
+        for name, v in self.param_views(self.params).items():
+            v.copy_(state[name].to(self.device, torch.float32))
+        tsrc = state if target is None else target
+        for name, v in self.param_views(self.target_params).items():
+            v.copy_(tsrc[name].to(self.device, torch.float32))
+
+    # ---- replay ----------------------------------------------------------------------
+    def push(self, obs, act, rew, done, next_obs):
+        """Append transitions (numpy arrays or CUDA tensors)."""
+        if isinstance(obs, torch.Tensor) and obs.is_cuda:
+            obs = obs.contiguous().float()
+            next_obs = next_obs.contiguous().float()
+            act = act.to(torch.int32).contiguous()
+            rew = rew.float().contiguous()
+            done = done.to(torch.uint8).contiguous()
+            n = obs.shape[0]
+            C.check(self.L.dqnx_replay_push(self.h, obs.data_ptr(), act.data_ptr(), rew.data_ptr(), done.data_ptr(),
+                                            next_obs.data_ptr(), n, 1, self.stream()), "replay_push")
+        else:
+            obs = np.ascontiguousarray(obs, dtype=np.float32).reshape(-1, self.spec.obs_dim)
+            next_obs = np.ascontiguousarray(next_obs, dtype=np.float32).reshape(-1, self.spec.obs_dim)
+            act = np.ascontiguousarray(act, dtype=np.int32).reshape(-1)
+            rew = np.ascontiguousarray(rew, dtype=np.float32).reshape(-1)
+            done = np.ascontiguousarray(np.asarray(done).astype(bool), dtype=np.uint8).reshape(-1)
+            n = obs.shape[0]
+            C.check(self.L.dqnx_replay_push(self.h, obs.ctypes.data, act.ctypes.data, rew.ctypes.data,
+                                            done.ctypes.data, next_obs.ctypes.data, n, 0, self.stream()),
+                    "replay_push")
+        self.ring_wptr = (self.ring_wptr + n) % self.capacity
+        self.ring_size = min(self.ring_size + n, self.capacity)
+
+    # ---- RNG -------------------------------------------------------------------------
+    def set_rng(self, which: int, state625: np.ndarray):
+        a = np.ascontiguousarray(state625, dtype=np.uint32)
+        assert a.shape == (625,)
+        C.check(self.L.dqnx_rng_set(self.h, which, a.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)),
+                                    self.stream()), "rng_set")
+
+    def get_rng(self, which: int) -> np.ndarray:
+        a = np.empty(625, dtype=np.uint32)
+        C.check(self.L.dqnx_rng_get(self.h, which, a.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)),
+                                    self.stream()), "rng_get")
+        return a
+
+    # ---- steps -----------------------------------------------------------------------
+    def learn_step(self, soft_update=False, given_indices=False, grads_only=False):
+        flags = (C.STEP_SOFT_UPDATE if soft_update else 0) | (C.STEP_GIVEN_INDICES if given_indices else 0) \
+            | (C.STEP_GRADS_ONLY if grads_only else 0)
+        C.check(self.L.dqnx_learn_step(self.h, flags, self.stream()), "learn_step")
+
+    def apply_grads(self, soft_update=False):
+        C.check(self.L.dqnx_apply_grads(self.h, C.STEP_SOFT_UPDATE if soft_update else 0, self.stream()),
+                "apply_grads")
+
+    def soft_update(self):
+        C.check(self.L.dqnx_soft_update(self.h, self.stream()), "soft_update")
+
+    def hard_update(self):
+        C.check(self.L.dqnx_hard_update(self.h, self.stream()), "hard_update")
+
+    def ctrl(self) -> C.Ctrl:
+        """Snapshot of the device control block (synchronises)."""
+        raw = self.ctrl_bytes.cpu().numpy().tobytes()
+        return C.Ctrl.from_buffer_copy(raw[:ctypes.sizeof(C.Ctrl)])
+
+    def loss(self) -> float:
+        return float(self.ctrl().loss)
+
+    def check_device_error(self):
+        err = self.ctrl().error
+        if err == C.DEVERR_SAMPLE_TOO_LARGE:
+            raise ValueError("Sample larger than population or is negative")
+        if err:
+            raise RuntimeError(f"libdqnx device error {err}")

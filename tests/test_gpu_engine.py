@@ -1,0 +1,181 @@
+"""GPU parity: libdqnx (through its C ABI) against the oracle on seeded inputs."""
+import ctypes
+import os
+import random
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import ref as O
+
+pytestmark = pytest.mark.gpu
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def _engine_mod():
+    from dqn import engine as E
+    return E
+
+
+def test_gpu_sampler_matches_oracle():
+    from dqn import _capi as C
+    L = C.lib()
+    dev = torch.device("cuda")
+    cases = [(50, 32), (200, 32), (4117, 1024), (4118, 1024), (10000, 1024), (100000, 4096),
+             (1000000, 1024), (1000000, 8192), (16405, 4096), (16406, 4096), (7, 5), (6, 6), (1, 1),
+             (3000, 0), (999, 999)]
+    for j, (n, k) in enumerate(cases):
+        random.seed(1000 + j)
+        st = O.py_state_to_array()
+        for rep in range(3):   # consecutive calls continue the same stream
+            want_state = st.copy()
+            want = O.sample_positions(want_state, n, k)
+            d_state = torch.from_numpy(st.view(np.int32).copy()).to(dev)
+            out = torch.zeros(max(k, 1), dtype=torch.int32, device=dev)
+            err = torch.zeros(1, dtype=torch.int32, device=dev)
+            scratch = torch.zeros(int(L.dqnx_sample_scratch_bytes(n, k)) + 16, dtype=torch.uint8, device=dev)
+            C.check(L.dqnx_sample_uniform(d_state.data_ptr(), n, k, out.data_ptr(), scratch.data_ptr(),
+                                          err.data_ptr(), torch.cuda.current_stream().cuda_stream), "sample")
+            torch.cuda.synchronize()
+            assert int(err.item()) == 0
+            got = out.cpu().numpy()[:k].astype(np.int64)
+            assert np.array_equal(got, want), (n, k, rep)
+            new_state = d_state.cpu().numpy().view(np.uint32)
+            assert np.array_equal(new_state, want_state), (n, k, rep)
+            st = want_state
+
+
+def test_gpu_sampler_golden():
+    from dqn import _capi as C
+    L = C.lib()
+    z = np.load(os.path.join(GOLDEN, "sampler.npz"))
+    for j in range(int(z["count"])):
+        n, k = int(z[f"c{j}_n"]), int(z[f"c{j}_k"])
+        d_state = torch.from_numpy(z[f"c{j}_state_in"].view(np.int32).copy()).cuda()
+        out = torch.zeros(k, dtype=torch.int32, device="cuda")
+        err = torch.zeros(1, dtype=torch.int32, device="cuda")
+        scratch = torch.zeros(int(L.dqnx_sample_scratch_bytes(n, k)) + 16, dtype=torch.uint8, device="cuda")
+        C.check(L.dqnx_sample_uniform(d_state.data_ptr(), n, k, out.data_ptr(), scratch.data_ptr(),
+                                      err.data_ptr(), torch.cuda.current_stream().cuda_stream), "sample")
+        torch.cuda.synchronize()
+        assert np.array_equal(out.cpu().numpy().astype(np.int64), z[f"c{j}_idx"]), j
+        assert np.array_equal(d_state.cpu().numpy().view(np.uint32), z[f"c{j}_state_out"]), j
+
+
+def test_gpu_sampler_k_larger_than_n_sets_error():
+    from dqn import _capi as C
+    L = C.lib()
+    d_state = torch.from_numpy(O.py_state_to_array().view(np.int32).copy()).cuda()
+    before = d_state.clone()
+    out = torch.zeros(8, dtype=torch.int32, device="cuda")
+    err = torch.zeros(1, dtype=torch.int32, device="cuda")
+    scratch = torch.zeros(1024, dtype=torch.uint8, device="cuda")
+    C.check(L.dqnx_sample_uniform(d_state.data_ptr(), 5, 8, out.data_ptr(), scratch.data_ptr(), err.data_ptr(),
+                                  torch.cuda.current_stream().cuda_stream), "sample")
+    torch.cuda.synchronize()
+    assert int(err.item()) == C.DEVERR_SAMPLE_TOO_LARGE
+    assert torch.equal(before, d_state)   # ValueError consumes nothing
+
+
+def make_pair(algo, obs_dim, batch, capacity, n_fill, seed, graphs=True):
+    E = _engine_mod()
+    head = O.algo_spec_head(algo)
+    ospec = O.mlp_spec(obs_dim, 8, head)
+    init = O.reference_init(ospec, seed)
+    oracle = O.OracleLearner(ospec, algo, batch, capacity, seed=seed, params=init)
+    data = O.synth_transitions(n_fill, obs_dim, 8, seed=seed + 100)
+    O.fill_replay(oracle, *data)
+    eng = E.LearnEngine(E.mlp_spec(obs_dim, 8, head), algo, batch, capacity, graphs=graphs)
+    eng.load_params(init)
+    obs, act, rew, done, new_obs = data
+    eng.push(obs, act, rew, done, new_obs)
+    random.seed(seed + 7)
+    st = O.py_state_to_array()
+    oracle.py_state = st.copy()
+    eng.set_rng(0, st)
+    return oracle, eng
+
+
+def compare_state(oracle, eng, atol=1e-5):
+    views = {"online": eng.param_views(eng.params), "target": eng.param_views(eng.target_params),
+             "m": eng.param_views(eng.adam_m), "v": eng.param_views(eng.adam_v)}
+    worst = {}
+    for nm, src in (("online", oracle.online), ("target", oracle.target), ("m", oracle.m), ("v", oracle.v)):
+        for k, ref in src.items():
+            got = views[nm][k].detach().cpu()
+            d = float((got - ref).abs().max())
+            worst[nm] = max(worst.get(nm, 0.0), d)
+    assert worst["online"] <= atol and worst["target"] <= atol, worst
+    assert worst["m"] <= 1e-6 and worst["v"] <= 1e-7, worst
+    return worst
+
+
+@pytest.mark.parametrize("algo,obs_dim,batch,capacity,n_fill,seed", [
+    ("DQNAgent", 14, 32, 500, 300, 3),
+    ("DoubleDQNAgent", 14, 32, 500, 300, 4),
+    ("DuelingDoubleDQNAgent", 14, 32, 500, 300, 5),
+    ("DuelingDoubleDQNAgent", 284, 256, 5000, 3000, 6),
+    ("DuelingDoubleDQNAgent", 284, 1024, 20000, 20000, 7),
+    ("DoubleDQNAgent", 284, 100, 700, 650, 8),
+])
+def test_gpu_learn_matches_oracle(algo, obs_dim, batch, capacity, n_fill, seed):
+    oracle, eng = make_pair(algo, obs_dim, batch, capacity, n_fill, seed)
+    for step in range(3):
+        rec = oracle.train_step()
+        eng.learn_step(soft_update=True)
+        torch.cuda.synchronize()
+        eng.check_device_error()
+        idx = eng.batch_idx.cpu().numpy().astype(np.int64)
+        assert np.array_equal(idx, rec.positions), f"step {step}: sampled indices differ"
+        q = eng.q.cpu()
+        np.testing.assert_allclose(q[0].numpy(), rec.q_online.numpy(), atol=1e-5, rtol=0)
+        np.testing.assert_allclose(q[2].numpy(), rec.q_target_next.numpy(), atol=1e-5, rtol=0)
+        if rec.q_online_next is not None:
+            np.testing.assert_allclose(q[1].numpy(), rec.q_online_next.numpy(), atol=1e-5, rtol=0)
+        np.testing.assert_allclose(eng.td[0].cpu().numpy(), rec.targets.view(-1).numpy(), atol=1e-5, rtol=0)
+        assert abs(eng.loss() - rec.loss) <= 1e-5 * max(1.0, abs(rec.loss))
+        g = eng.param_views(eng.grads[:-1])
+        for k, ref in rec.grads.items():
+            np.testing.assert_allclose(g[k].cpu().numpy(), ref.numpy(), atol=2e-6, rtol=1e-4, err_msg=k)
+        compare_state(oracle, eng)
+    assert np.array_equal(eng.get_rng(0), oracle.py_state)
+
+
+def test_gpu_learn_graph_and_eager_identical():
+    o1, e1 = make_pair("DuelingDoubleDQNAgent", 284, 512, 4000, 4000, 11, graphs=True)
+    o2, e2 = make_pair("DuelingDoubleDQNAgent", 284, 512, 4000, 4000, 11, graphs=False)
+    for _ in range(4):
+        e1.learn_step(soft_update=True)
+        e2.learn_step(soft_update=True)
+    torch.cuda.synchronize()
+    assert torch.equal(e1.params, e2.params)
+    assert torch.equal(e1.target_params, e2.target_params)
+
+
+@pytest.mark.parametrize("golden", ["learn_mlp14_DQNAgent", "learn_mlp14_DoubleDQNAgent",
+                                    "learn_mlp14_DuelingDoubleDQNAgent", "learn_mlp284_DuelingDoubleDQNAgent"])
+def test_gpu_learn_golden(golden):
+    """Engine against the reference's own outputs (tests/golden, made by make_golden.py)."""
+    E = _engine_mod()
+    z = np.load(os.path.join(GOLDEN, golden + ".npz"))
+    algo = str(z["algo"])
+    obs_dim = int(z["obs_dim"])
+    head = O.algo_spec_head(algo)
+    init = O.reference_init(O.mlp_spec(obs_dim, 8, head), int(z["seed"]))
+    eng = E.LearnEngine(E.mlp_spec(obs_dim, 8, head), algo, int(z["batch"]), int(z["buffer"]))
+    eng.load_params(init)
+    eng.push(*O.synth_transitions(int(z["n_fill"]), obs_dim, 8, seed=int(z["seed"]) + 100))
+    eng.set_rng(0, z["py_state_in"])
+    for s in range(int(z["steps"])):
+        eng.learn_step(soft_update=True)
+        torch.cuda.synchronize()
+        assert np.array_equal(eng.batch_idx.cpu().numpy().astype(np.int64), z["pos"][s])
+        assert abs(eng.loss() - z["loss"][s]) <= 1e-5 * max(1.0, abs(z["loss"][s]))
+    assert np.array_equal(eng.get_rng(0), z["py_state_out"])
+    keys = [str(k) for k in z["keys"]]
+    on, tg = eng.param_views(eng.params), eng.param_views(eng.target_params)
+    for i, k in enumerate(keys):
+        np.testing.assert_allclose(on[k].cpu().numpy().reshape(-1), z[f"online_{i}"], atol=1e-5, rtol=0)
+        np.testing.assert_allclose(tg[k].cpu().numpy().reshape(-1), z[f"target_{i}"], atol=1e-5, rtol=0)
