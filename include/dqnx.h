@@ -98,10 +98,12 @@ typedef struct dqnx_config {
     int32_t world_size;        /* data-parallel ranks (1 = single GPU) */
     int32_t rank;              /* this rank: processes samples [rank*batch/world, (rank+1)*batch/world) */
     int64_t capacity;          /* buffer_size (deque maxlen / SumTree capacity) */
-    float gamma;               /* discount */
-    float lr;                  /* Adam lr */
-    float beta1, beta2, adam_eps;   /* torch.optim.Adam defaults 0.9, 0.999, 1e-8 */
-    float tau;                 /* target_soft_update_tau */
+    /* hyper-parameters are doubles, like the reference's Python floats; the engine casts
+     * them to fp32 exactly where torch does (tensor * Python float). */
+    double gamma;              /* discount */
+    double lr;                 /* Adam lr */
+    double beta1, beta2, adam_eps;  /* torch.optim.Adam defaults 0.9, 0.999, 1e-8 */
+    double tau;                /* target_soft_update_tau */
     int32_t n_env;             /* soft update uses tau*n_env (R:dqn/agent.py:108-109) */
     int32_t reserved0;
     /* ReplayMemoryPrioritized constants (R:dqn/replay_memory.py:49-54) */
@@ -233,6 +235,10 @@ int dqnx_sample_uniform(uint32_t* mt625, int64_t n, int32_t k, int32_t* out, voi
 /* ---- misc ------------------------------------------------------------------------ */
 const char* dqnx_last_error(void);
 int32_t dqnx_abi_version(void);
+/* Diagnostic builds only (-DDQNX_STAMPS): copy the 64 s_memtime phase stamps written by
+ * block 0 of the sampler / head kernels (synchronises).  Returns DQNX_EUNSUPPORTED in
+ * production builds. */
+int dqnx_debug_stamps(dqnx_engine* e, int64_t* out64, void* stream);
 
 #ifdef __cplusplus
 }

@@ -38,6 +38,24 @@ __device__ __forceinline__ float act_fwd(float x) {
 
 __device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
 
+// XCD-aware block remap (CDNA guide T1): blocks are dealt round-robin over the 8 XCDs, so
+// hand XCD x a CONTIGUOUS range of tiles (bijective for any total).  Speed only: placement
+// never affects results.
+__device__ __forceinline__ int xcd_remap(int L, int total) {
+    const int per = total >> 3, rem = total & 7;
+    const int x = L & 7, local = L >> 3;
+    return x * per + (x < rem ? x : rem) + local;
+}
+
+#ifdef DQNX_STAMPS
+#define DQNX_STAMP(ptr, i)                                                            \
+    do {                                                                             \
+        if ((ptr) && blockIdx.x == 0 && threadIdx.x == 0) (ptr)[i] = (int64_t)__builtin_amdgcn_s_memtime(); \
+    } while (0)
+#else
+#define DQNX_STAMP(ptr, i) do { } while (0)
+#endif
+
 }  // namespace dqnx
 
 #define DQNX_HIP_CHECK(expr)                                                    \

@@ -6,6 +6,7 @@
 #include <stdio.h>
 #include <string.h>
 
+#include <cmath>
 #include <functional>
 #include <map>
 #include <string>
@@ -145,6 +146,7 @@ struct dqnx_engine {
     uint64_t total = 0;
     // workspace sub-regions (byte offsets from the arena base)
     uint64_t ws_phys = 0, ws_pool = 0, ws_xobs = 0, ws_head_part = 0, ws_loss_part = 0, ws_stage = 0;
+    uint64_t ws_adam_tab = 0, ws_stamps = 0, ws_dhead = 0;
     std::vector<uint64_t> ws_H, ws_dZ, ws_part;
     int stage_rows = 0;
     char* arena = nullptr;
@@ -216,7 +218,10 @@ int layout(dqnx_engine* e) {
         const uint64_t lp = (uint64_t)np.dense[l].out * np.dense[l].in + np.dense[l].out;
         e->ws_part[l] = sub((uint64_t)e->slices[l] * lp * 4);
     }
-    e->ws_head_part = sub((uint64_t)e->tiles * np.head_params * 4);
+    e->ws_head_part = sub((uint64_t)e->slices[L - 1] * np.head_params * 4);
+    e->ws_dhead = sub((uint64_t)e->Bl * 16 * 4);
+    e->ws_adam_tab = sub((uint64_t)kAdamTable * 2 * 4);
+    e->ws_stamps = sub(64 * 8);
     e->ws_loss_part = sub((uint64_t)e->tiles * 4);
     e->stage_rows = 1024;
     e->ws_stage = sub((uint64_t)e->stage_rows * (2 * (uint64_t)c.net.obs_dim + 3) * 4 + 256);
@@ -274,6 +279,7 @@ std::vector<KStep> build_learn_steps(dqnx_engine* e, int flags) {
         sa.shard_len = e->Bl;
         sa.wptr_dev = &ctrl->ring_wptr;
         sa.capacity = c.capacity;
+        sa.stamps = at<int64_t>(e, e->ws_stamps);
         KStep k;
         k.name = "sample_uniform";
         k.bytes = 2.0 * 625 * 4 + 4.0 * e->Bg + 4.0 * Bl;
@@ -335,7 +341,7 @@ std::vector<KStep> build_learn_steps(dqnx_engine* e, int flags) {
         ha.algo = c.algo;
         ha.head_params = (int)np.head_params;
         ha.inv_bg = (float)(1.0 / (double)e->Bg);
-        ha.gamma = c.gamma;
+        ha.gamma = (float)c.gamma;
         ha.H = at<float>(e, e->ws_H[L - 1]);
         ha.Wo = params + np.head_off;
         ha.Wt = tparams + np.head_off;
@@ -347,12 +353,13 @@ std::vector<KStep> build_learn_steps(dqnx_engine* e, int flags) {
         ha.Q = at<float>(e, e->off[DQNX_BUF_Q]);
         ha.td = at<float>(e, e->off[DQNX_BUF_TD]);
         ha.dZ = at<float>(e, e->ws_dZ[L - 1]);
-        ha.head_partial = at<float>(e, e->ws_head_part);
+        ha.dhead = at<float>(e, e->ws_dhead);
         ha.loss_partial = at<float>(e, e->ws_loss_part);
         ha.ctrl = ctrl;
-        ha.beta1 = c.beta1;
-        ha.beta2 = c.beta2;
-        ha.lr = c.lr;
+        ha.beta1 = (float)c.beta1;
+        ha.beta2 = (float)c.beta2;
+        ha.lr = (float)c.lr;
+        ha.stamps = at<int64_t>(e, e->ws_stamps);
         KStep k;
         k.name = "head_td_loss";
         const double F = np.F, NH = np.NH;
@@ -364,6 +371,7 @@ std::vector<KStep> build_learn_steps(dqnx_engine* e, int flags) {
     }
 
     // 4. backward levels L..1: dX of the level below + split-K dW of this level
+    //    (level L also computes the head-weight gradient from the head kernel's dHead)
     for (int l = L - 1; l >= 0; l--) {
         const LayerPlan lp = np.dense[l];
         BwdArgs ba;
@@ -373,27 +381,50 @@ std::vector<KStep> build_learn_steps(dqnx_engine* e, int flags) {
         ba.in = lp.in;
         ba.out = lp.out;
         ba.W = params + lp.off;
+        ba.kslice = e->kslice[l];
+        ba.dw_slices = e->slices[l];
+        DwProblem& d = ba.dw[ba.ndw++];
+        d.dZ = ba.dZ;
+        d.ldz = lp.out;
+        d.in = lp.in;
+        d.out = lp.out;
+        d.head_kind = -1;
         if (l > 0) {
             ba.Hprev = at<float>(e, e->ws_H[l - 1]);   // stream 0 rows
             ba.ldh = lp.in;
             ba.dZprev = at<float>(e, e->ws_dZ[l - 1]);
-            ba.X = ba.Hprev;
-            ba.ldx = lp.in;
+            d.X = ba.Hprev;
+            d.ldx = lp.in;
         } else {
-            ba.X = at<float>(e, e->ws_xobs);
-            ba.ldx = e->stride;
+            d.X = at<float>(e, e->ws_xobs);
+            d.ldx = e->stride;
         }
-        ba.partial = at<float>(e, e->ws_part[l]);
-        ba.pstride = (int64_t)lp.out * lp.in + lp.out;
-        ba.kslice = e->kslice[l];
+        d.partial = at<float>(e, e->ws_part[l]);
+        d.pstride = (int64_t)lp.out * lp.in + lp.out;
+        double flops = 2.0 * Bl * lp.out * (lp.in + 1.0) + (l > 0 ? 2.0 * Bl * lp.out * lp.in : 0.0);
+        double bytes = 4.0 * (Bl * lp.out + Bl * lp.in + ba.dw_slices * (lp.out * (lp.in + 1.0))
+                              + (l > 0 ? lp.out * (double)lp.in + 2.0 * Bl * lp.in : 0.0));
+        if (l == L - 1) {   // head weight gradient: dHead^T [H_L | 1]
+            DwProblem& h = ba.dw[ba.ndw++];
+            h.dZ = at<float>(e, e->ws_dhead);
+            h.ldz = 16;
+            h.X = at<float>(e, e->ws_H[L - 1]);
+            h.ldx = np.F;
+            h.in = np.F;
+            h.out = np.NH;
+            h.partial = at<float>(e, e->ws_head_part);
+            h.pstride = np.head_params;
+            h.head_kind = c.net.head;
+            h.A = A;
+            flops += 2.0 * Bl * np.NH * (np.F + 1.0);
+            bytes += 4.0 * (16.0 * Bl + ba.dw_slices * (double)np.head_params);
+        }
         bwd_level_grid(ba);
-        const int S = e->slices[l];
         KStep k;
         k.name = "linear_bwd_l" + std::to_string(l + 1);
-        k.flops = 2.0 * Bl * lp.out * (lp.in + 1.0) + (l > 0 ? 2.0 * Bl * lp.out * lp.in : 0.0);
-        k.bytes = 4.0 * (Bl * lp.out + Bl * lp.in + S * (lp.out * (lp.in + 1.0))
-                         + (l > 0 ? lp.out * (double)lp.in + 2.0 * Bl * lp.in : 0.0));
-        k.run = [=](hipStream_t s) { return launch_bwd_level(ba, S, act, s); };
+        k.flops = flops;
+        k.bytes = bytes;
+        k.run = [=](hipStream_t s) { return launch_bwd_level(ba, act, s); };
         ks.push_back(k);
     }
 
@@ -416,7 +447,7 @@ std::vector<KStep> build_learn_steps(dqnx_engine* e, int flags) {
             sg.off = np.head_off;
             sg.partial = at<float>(e, e->ws_head_part);
             sg.pstride = np.head_params;
-            sg.S = e->tiles;
+            sg.S = e->slices[L - 1];
             part_elems += (double)sg.S * sg.pstride;
         }
         aa.mode = (flags & DQNX_STEP_GRADS_ONLY) ? 0 : 1;
@@ -428,12 +459,17 @@ std::vector<KStep> build_learn_steps(dqnx_engine* e, int flags) {
         aa.grads = at<float>(e, e->off[DQNX_BUF_GRADS]);
         aa.target = tparams;
         aa.ctrl = ctrl;
-        aa.w1 = (float)(1.0 - (double)c.beta1);
-        aa.beta2 = c.beta2;
-        aa.c2 = (float)(1.0 - (double)c.beta2);
-        aa.eps = c.adam_eps;
-        aa.tau = (float)((double)c.tau * c.n_env);
-        aa.one_minus_tau = (float)(1.0 - (double)c.tau * c.n_env);
+        aa.w1 = (float)(1.0 - c.beta1);          // Python: exp_avg.lerp_(grad, 1 - beta1)
+        aa.beta2 = (float)c.beta2;
+        aa.c2 = (float)(1.0 - c.beta2);
+        aa.eps = (float)c.adam_eps;
+        aa.tau = (float)(c.tau * c.n_env);      // (tau * n_env) * online + (1 - tau * n_env) * target
+        aa.one_minus_tau = (float)(1.0 - c.tau * c.n_env);
+        aa.adam_table = at<float>(e, e->ws_adam_tab);
+        aa.adam_table_len = kAdamTable;
+        aa.beta1d = c.beta1;
+        aa.beta2d = c.beta2;
+        aa.lrd = c.lr;
         aa.loss_partial = at<float>(e, e->ws_loss_part);
         aa.n_loss_partial = e->tiles;
         aa.batch_global = e->Bg;
@@ -471,12 +507,17 @@ int enqueue_apply(dqnx_engine* e, int flags, hipStream_t s) {
     aa.grads = at<float>(e, e->off[DQNX_BUF_GRADS]);
     aa.target = at<float>(e, e->off[DQNX_BUF_TARGET_PARAMS]);
     aa.ctrl = ctrl_of(e);
-    aa.w1 = (float)(1.0 - (double)c.beta1);
-    aa.beta2 = c.beta2;
-    aa.c2 = (float)(1.0 - (double)c.beta2);
-    aa.eps = c.adam_eps;
-    aa.tau = (float)((double)c.tau * c.n_env);
-    aa.one_minus_tau = (float)(1.0 - (double)c.tau * c.n_env);
+    aa.w1 = (float)(1.0 - c.beta1);          // Python: exp_avg.lerp_(grad, 1 - beta1)
+    aa.beta2 = (float)c.beta2;
+    aa.c2 = (float)(1.0 - c.beta2);
+    aa.eps = (float)c.adam_eps;
+    aa.tau = (float)(c.tau * c.n_env);      // (tau * n_env) * online + (1 - tau * n_env) * target
+    aa.one_minus_tau = (float)(1.0 - c.tau * c.n_env);
+    aa.adam_table = at<float>(e, e->ws_adam_tab);
+    aa.adam_table_len = kAdamTable;
+    aa.beta1d = c.beta1;
+    aa.beta2d = c.beta2;
+    aa.lrd = c.lr;
     aa.batch_global = e->Bg;
     return launch_adam(aa, s);
 }
@@ -558,12 +599,12 @@ void dqnx_config_defaults(dqnx_config* c) {
     c->world_size = 1;
     c->rank = 0;
     c->capacity = 1000000;
-    c->gamma = 0.99f;
-    c->lr = 1e-4f;
-    c->beta1 = 0.9f;
-    c->beta2 = 0.999f;
-    c->adam_eps = 1e-8f;
-    c->tau = 1e-3f;
+    c->gamma = 0.99;
+    c->lr = 1e-4;
+    c->beta1 = 0.9;
+    c->beta2 = 0.999;
+    c->adam_eps = 1e-8;
+    c->tau = 1e-3;
     c->n_env = 1;
     c->per_eps = 1e-4;
     c->per_alpha = 0.6;
@@ -588,6 +629,7 @@ int dqnx_engine_create(const dqnx_config* cfg, dqnx_engine** out) {
         { delete e; return set_error(DQNX_EINVAL, "batch must be a positive multiple of world_size"); }
     if (c.capacity <= 0 || c.capacity >= ((int64_t)1 << 31)) { delete e; return set_error(DQNX_EINVAL, "capacity out of range"); }
     if (e->np.NH > 16) { delete e; return set_error(DQNX_EUNSUPPORTED, "head with more than 16 outputs"); }
+    if (!head_supported(e->np.F)) { delete e; return set_error(DQNX_EUNSUPPORTED, "head input width %d not in {64,128,256}", e->np.F); }
     for (size_t l = 0; l < e->np.dense.size(); l++)
         if (e->np.dense[l].out % 4) { delete e; return set_error(DQNX_EUNSUPPORTED, "hidden widths must be multiples of 4"); }
     if (sample_hash_slots(c.batch) < 0) { delete e; return set_error(DQNX_EUNSUPPORTED, "batch too large for the sampler"); }
@@ -601,7 +643,7 @@ int dqnx_engine_create(const dqnx_config* cfg, dqnx_engine** out) {
     e->slices.assign(L, 1);
     e->kslice.assign(L, e->Bl);
     for (int l = 0; l < L; l++) {
-        int S = e->Bl / 128;
+        int S = e->Bl / 256;
         if (S < 1) S = 1;
         if (S > 32) S = 32;
         int ks = (int)align_up((uint64_t)((e->Bl + S - 1) / S), 16);
@@ -675,7 +717,20 @@ int dqnx_engine_reset(dqnx_engine* e, void* stream) {
     init.per_min_idx = e->cfg.capacity - 1;
     DQNX_HIP_CHECK(hipMemcpyAsync(&ctrl_of(e)->per_max_idx, &init.per_max_idx, 2 * sizeof(int64_t),
                                   hipMemcpyHostToDevice, s));
-    DQNX_HIP_CHECK(hipStreamSynchronize(s));
+    // Adam bias corrections, computed like torch's _single_tensor_adam does on the host:
+    // step_size = lr / (1 - beta1**t), bias_correction2**0.5 (Python float pow = libm pow)
+    {
+        std::vector<float> tab((size_t)kAdamTable * 2);
+        const dqnx_config& c = e->cfg;
+        for (int t = 1; t <= kAdamTable; t++) {
+            const double bc1 = 1.0 - std::pow(c.beta1, (double)t);
+            const double bc2 = 1.0 - std::pow(c.beta2, (double)t);
+            tab[2 * (t - 1)] = (float)(-(c.lr / bc1));
+            tab[2 * (t - 1) + 1] = (float)std::pow(bc2, 0.5);
+        }
+        DQNX_HIP_CHECK(hipMemcpyAsync(e->arena + e->ws_adam_tab, tab.data(), tab.size() * 4, hipMemcpyHostToDevice, s));
+        DQNX_HIP_CHECK(hipStreamSynchronize(s));
+    }
     e->ring_size = 0;
     e->ring_wptr = 0;
     return DQNX_OK;
@@ -885,6 +940,20 @@ int dqnx_hard_update(dqnx_engine* e, void* stream) {
     DQNX_HIP_CHECK(hipMemcpyAsync(e->arena + e->off[DQNX_BUF_TARGET_PARAMS], e->arena + e->off[DQNX_BUF_PARAMS],
                                   (size_t)e->np.P * 4, hipMemcpyDeviceToDevice, (hipStream_t)stream));
     return DQNX_OK;
+}
+
+int dqnx_debug_stamps(dqnx_engine* e, int64_t* out64, void* stream) {
+#ifdef DQNX_STAMPS
+    int rc = check_bound(e);
+    if (rc) return rc;
+    DQNX_HIP_CHECK(hipMemcpyAsync(out64, e->arena + e->ws_stamps, 64 * 8, hipMemcpyDeviceToHost, (hipStream_t)stream));
+    DQNX_HIP_CHECK(hipMemsetAsync(e->arena + e->ws_stamps, 0, 64 * 8, (hipStream_t)stream));
+    DQNX_HIP_CHECK(hipStreamSynchronize((hipStream_t)stream));
+    return DQNX_OK;
+#else
+    (void)e; (void)out64; (void)stream;
+    return set_error(DQNX_EUNSUPPORTED, "not a -DDQNX_STAMPS build");
+#endif
 }
 
 }  // extern "C"

@@ -1,0 +1,199 @@
+// LDS-staged fp32 MFMA GEMM tiles for the learn step's small GEMMs (gfx950).
+//
+// A 256-thread workgroup stages a K pass of its A and B tiles in LDS with every lane's
+// float4 loads issued before the first wait (full-line, lane-contiguous loads: one
+// round trip per pass), prefetches the next pass into registers while the current one is
+// multiplied, and reads MFMA fragments from LDS:
+//   ROWS_K image [rows][KT+8]  (K contiguous)  -> one ds_read_b128 per fragment
+//   K_ROWS image [KT][cols+4]  (K strided)     -> four ds_read_b32 per fragment
+// (paddings chosen conflict-free for the b128 / b32 lane groups of MI355X_MICROARCH §LDS).
+// MFMA jj of a 16-deep chunk consumes k = kk + 4*(lane>>4) + jj for both operands.
+// Measured against the wave-split-K engine (gemm_sk.hpp) in profiles/r01_*: this one is
+// faster for every GEMM of the MLP learn step (fragment-shaped global loads cost more
+// than the LDS round trip).
+#pragma once
+#include "gemm_common.hpp"
+
+namespace dqnx {
+
+template <int R, int KT, bool VEC>
+struct StageRowsK {
+    static constexpr int S = KT + 8;                 // LDS row stride (floats)
+    static constexpr int Q4 = KT / 4;                // float4 per row
+    static constexpr int NQ = (R * Q4 + 255) / 256;  // float4 slots per thread
+    static constexpr int LDS_FLOATS = R * S;
+    float4 v[NQ];
+
+    __device__ __forceinline__ void load(const Operand& o, int r0, int kb) {
+        const int tid = threadIdx.x;
+#pragma unroll
+        for (int j = 0; j < NQ; j++) {
+            const int q = tid + 256 * j;
+            float4 x = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (q < R * Q4) {
+                const int r = q / Q4, k = kb + 4 * (q - r * Q4);
+                const int gr = r0 + r;
+                if (gr < o.nrows && k < o.K) {
+                    const int64_t row = o.gather ? (int64_t)o.gather[gr] : (int64_t)gr;
+                    const float* p = o.base + row * o.ld + k;
+                    if (VEC) {
+                        x = ld4(p);
+                    } else {
+                        x.x = p[0];
+                        x.y = (k + 1 < o.K) ? p[1] : 0.f;
+                        x.z = (k + 2 < o.K) ? p[2] : 0.f;
+                        x.w = (k + 3 < o.K) ? p[3] : 0.f;
+                    }
+                }
+            }
+            v[j] = x;
+        }
+    }
+    __device__ __forceinline__ void store(float* lds, const Operand& o, int r0, int kb) const {
+        const int tid = threadIdx.x;
+#pragma unroll
+        for (int j = 0; j < NQ; j++) {
+            const int q = tid + 256 * j;
+            if (q < R * Q4) {
+                const int r = q / Q4, c = 4 * (q - r * Q4);
+                *reinterpret_cast<float4*>(lds + r * S + c) = v[j];
+                if (o.copy && r0 + r < o.nrows && kb + c < o.K)
+                    *reinterpret_cast<float4*>(o.copy + (int64_t)(r0 + r) * o.ldcopy + kb + c) = v[j];
+            }
+        }
+    }
+    __device__ __forceinline__ void frag(const float* lds, int rw, int kk, float (&f)[4]) const {
+        const int lane = threadIdx.x & 63;
+        const float4 x = *reinterpret_cast<const float4*>(lds + (rw + (lane & 15)) * S + kk + 4 * (lane >> 4));
+        f[0] = x.x; f[1] = x.y; f[2] = x.z; f[3] = x.w;
+    }
+};
+
+template <int C, int KT>
+struct StageKRows {
+    static constexpr int S = C + 4;
+    static constexpr int C4 = C / 4;
+    static constexpr int NQ = (KT * C4 + 255) / 256;
+    static constexpr int LDS_FLOATS = KT * S;
+    float4 v[NQ];
+
+    __device__ __forceinline__ void load(const Operand& o, int c0, int kb) {
+        const int tid = threadIdx.x;
+#pragma unroll
+        for (int j = 0; j < NQ; j++) {
+            const int q = tid + 256 * j;
+            float4 x = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (q < KT * C4) {
+                const int kr = q / C4, c = c0 + 4 * (q - kr * C4);
+                const int k = kb + kr;
+                if (k < o.K && c < o.nrows) x = ld4(o.base + (int64_t)k * o.ld + c);
+            }
+            v[j] = x;
+        }
+    }
+    __device__ __forceinline__ void store(float* lds, const Operand&, int, int) const {
+        const int tid = threadIdx.x;
+#pragma unroll
+        for (int j = 0; j < NQ; j++) {
+            const int q = tid + 256 * j;
+            if (q < KT * C4) {
+                const int kr = q / C4, c = 4 * (q - kr * C4);
+                *reinterpret_cast<float4*>(lds + kr * S + c) = v[j];
+            }
+        }
+    }
+    __device__ __forceinline__ void frag(const float* lds, int cw, int kk, float (&f)[4], int col_abs, int aug) const {
+        const int lane = threadIdx.x & 63;
+        const float* p = lds + (kk + 4 * (lane >> 4)) * S + cw + (lane & 15);
+        if (col_abs == aug) {
+            f[0] = f[1] = f[2] = f[3] = 1.f;
+        } else {
+            f[0] = p[0]; f[1] = p[S]; f[2] = p[2 * S]; f[3] = p[3 * S];
+        }
+    }
+};
+
+template <int LAYOUT, int R, int KT, bool VEC>
+struct Stage;
+template <int R, int KT, bool VEC>
+struct Stage<L_ROWS_K, R, KT, VEC> : StageRowsK<R, KT, VEC> {
+    __device__ __forceinline__ void fragx(const float* lds, int rw, int kk, float (&f)[4], int, int) const {
+        this->frag(lds, rw, kk, f);
+    }
+};
+template <int R, int KT, bool VEC>
+struct Stage<L_K_ROWS, R, KT, VEC> : StageKRows<R, KT> {
+    __device__ __forceinline__ void fragx(const float* lds, int rw, int kk, float (&f)[4], int col_abs,
+                                          int aug) const {
+        this->frag(lds, rw, kk, f, col_abs, aug);
+    }
+};
+
+// Workgroup tile: BM x BN outputs, 4 waves as WM x WN, each wave TM x TN 16x16 sub-tiles,
+// K range [kbeg, kend) in passes of KT.  acc[tm][tn] lane l holds
+// C[m0 + (wm*TM + tm)*16 + 4*(l>>4) + r][n0 + (wn*TN + tn)*16 + (l&15)], r = 0..3.
+template <int BM, int BN, int KT, int WM, int WN, int LA, int LB, bool VA, bool VB>
+struct TileGemm {
+    static constexpr int TM = BM / (WM * 16), TN = BN / (WN * 16);
+    static_assert(WM * WN == 4, "4 waves per workgroup");
+    static_assert(TM * 16 * WM == BM && TN * 16 * WN == BN, "tile shape");
+    static_assert(KT % 16 == 0, "KT multiple of 16");
+    using SA = Stage<LA, BM, KT, VA>;
+    using SB = Stage<LB, BN, KT, VB>;
+    static constexpr int LDS_FLOATS = SA::LDS_FLOATS + SB::LDS_FLOATS;
+
+    __device__ __forceinline__ static void run(float* lds, const Operand& A, const Operand& B, int m0, int n0,
+                                               int kbeg, int kend, floatx4 (&acc)[TM][TN]) {
+        const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+        const int wm = wid / WN, wn = wid % WN;
+        float* la = lds;
+        float* lb = lds + SA::LDS_FLOATS;
+#pragma unroll
+        for (int tm = 0; tm < TM; tm++)
+#pragma unroll
+            for (int tn = 0; tn < TN; tn++) acc[tm][tn] = floatx4{0.f, 0.f, 0.f, 0.f};
+        SA sa;
+        SB sb;
+        int kb = kbeg;
+        if (kb >= kend) return;
+        sa.load(A, m0, kb);
+        sb.load(B, n0, kb);
+        sa.store(la, A, m0, kb);
+        sb.store(lb, B, n0, kb);
+        __syncthreads();
+        while (true) {
+            const int klen = min(KT, kend - kb);
+            const int kn = kb + KT;
+            const bool more = kn < kend;
+            if (more) {   // next pass in flight while this one is multiplied
+                sa.load(A, m0, kn);
+                sb.load(B, n0, kn);
+            }
+            for (int kk = 0; kk < klen; kk += 16) {
+                float a[TM][4], b[TN][4];
+#pragma unroll
+                for (int tm = 0; tm < TM; tm++) sa.fragx(la, (wm * TM + tm) * 16, kk, a[tm], -1, -2);
+#pragma unroll
+                for (int tn = 0; tn < TN; tn++) {
+                    const int cw = (wn * TN + tn) * 16;
+                    sb.fragx(lb, cw, kk, b[tn], n0 + cw + (lane & 15), B.aug);
+                }
+#pragma unroll
+                for (int jj = 0; jj < 4; jj++)
+#pragma unroll
+                    for (int tm = 0; tm < TM; tm++)
+#pragma unroll
+                        for (int tn = 0; tn < TN; tn++)
+                            acc[tm][tn] = mfma16x16x4(a[tm][jj], b[tn][jj], acc[tm][tn]);
+            }
+            if (!more) break;
+            __syncthreads();
+            sa.store(la, A, m0, kn);
+            sb.store(lb, B, n0, kn);
+            __syncthreads();
+            kb = kn;
+        }
+    }
+};
+
+}  // namespace dqnx

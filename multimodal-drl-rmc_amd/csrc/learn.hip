@@ -12,7 +12,8 @@
 //   MLP body               R:env/custom_env/macro with lane/dqn_config.py:76-84
 //   Adam                   torch.optim.Adam single-tensor step (R:env/dqn_config.py:176)
 //   soft target update     R:dqn/agent.py:105-110
-#include "gemm.hpp"
+#include "gemm_lds.hpp"
+#include "gemm_sk.hpp"
 #include "learn.hpp"
 
 namespace dqnx {
@@ -21,132 +22,39 @@ namespace dqnx {
 // Forward Linear: C[s] = act(A[s] W[s]^T + b[s]) for up to 3 "streams" (blockIdx.z):
 // online(obs), online(next_obs), target(next_obs).  Layer 1 gathers A rows from the
 // replay ring through the sampled physical slots (no materialised minibatch), and
-// stream 0 also writes the gathered rows to `xcopy` for the dW of layer 1.
+// stream 0's first column tile also writes the gathered rows to `xcopy` for layer-1 dW.
 // =====================================================================================
-template <int TM, int TN, int WM, int WN, int ACT, bool VECB>
-__global__ __launch_bounds__(256) void k_linear_fwd(FwdArgs args) {
-    const FwdProblem& P = args.p[blockIdx.z];
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    const int wm = wid / WN, wn = wid % WN;
-    const int i = lane & 15, g = lane >> 4;
-    const int m0 = blockIdx.y * (WM * TM * 16) + wm * TM * 16;
-    const int n0 = blockIdx.x * (WN * TN * 16) + wn * TN * 16;
-    const int M = args.M, N = args.N, K = args.K;
+// Tile engine: DQNX_GEMM_SK=1 selects the wave-split-K engine (gemm_sk.hpp), default the
+// LDS-staged engine (gemm_lds.hpp).  Configs are compile-time (tools/variants_*.txt sweeps).
+#ifndef DQNX_GEMM_SK
+#define DQNX_GEMM_SK 0
+#endif
+#ifndef DQNX_FWD_BM
+#define DQNX_FWD_BM 16
+#endif
+#ifndef DQNX_FWD_BN
+#define DQNX_FWD_BN 64
+#endif
+#ifndef DQNX_FWD_KT
+#define DQNX_FWD_KT 128
+#endif
+#ifndef DQNX_FWD_WM
+#define DQNX_FWD_WM 1
+#endif
+#ifndef DQNX_BWD_BM
+#define DQNX_BWD_BM 32
+#endif
+#ifndef DQNX_BWD_BN
+#define DQNX_BWD_BN 32
+#endif
+#ifndef DQNX_BWD_KT
+#define DQNX_BWD_KT 128
+#endif
+#ifndef DQNX_BWD_WM
+#define DQNX_BWD_WM 2
+#endif
+constexpr int FWD_BM = DQNX_FWD_BM, FWD_BN = DQNX_FWD_BN, BWD_BM = DQNX_BWD_BM, BWD_BN = DQNX_BWD_BN;
 
-    RowsK<TM, true> A;
-    if (P.phys) {
-        A.K = K;
-#pragma unroll
-        for (int t = 0; t < TM; t++) {
-            const int r = m0 + t * 16 + i;
-            A.ptr[t] = (r < M) ? P.A + (int64_t)P.phys[r] * P.lda : nullptr;
-            A.cpy[t] = (P.xcopy && blockIdx.x == 0 && wn == 0 && r < M) ? P.xcopy + (int64_t)r * P.lda : nullptr;
-        }
-    } else {
-        A.set_dense(P.A, P.lda, m0, M, K);
-    }
-    RowsK<TN, VECB> B;
-    B.set_dense(P.W, K, n0, N, K);
-
-    floatx4 acc[TM][TN];
-    zero_acc<TM, TN>(acc);
-    mfma_loop<TM, TN>(A, B, 0, K, acc);
-
-#pragma unroll
-    for (int tn = 0; tn < TN; tn++) {
-        const int col = n0 + tn * 16 + i;
-        if (col >= N) continue;
-        const float bias = P.bias[col];
-#pragma unroll
-        for (int tm = 0; tm < TM; tm++)
-#pragma unroll
-            for (int r = 0; r < 4; r++) {
-                const int row = m0 + tm * 16 + 4 * g + r;
-                if (row < M) P.C[(int64_t)row * args.ldc + col] = act_fwd<ACT>(acc[tm][tn][r] + bias);
-            }
-    }
-}
-
-// =====================================================================================
-// Backward level: two independent GEMMs in one launch.
-//   dx role:  dZprev = (dZ W) (.) act'(Hprev)      [Bl x in], K = out
-//   dw role:  partial[s] = dZ^T [Xprev | 1]        [out x (in+1)], K = samples of slice s
-// =====================================================================================
-template <int ACT>
-__global__ __launch_bounds__(256) void k_bwd_level(BwdArgs a) {
-    constexpr int TM = 1, TN = 2, WM = 2, WN = 2;
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    const int wm = wid / WN, wn = wid % WN;
-    const int i = lane & 15, g = lane >> 4;
-    int b = blockIdx.x;
-    if (b < a.dx_blocks) {
-        const int bx = b % a.dx_grid_x, by = b / a.dx_grid_x;
-        const int m0 = by * (WM * TM * 16) + wm * TM * 16;
-        const int n0 = bx * (WN * TN * 16) + wn * TN * 16;
-        RowsK<TM, true> A;
-        A.set_dense(a.dZ, a.out, m0, a.Bl, a.out);
-        StridedK<TN> B;
-        B.set(a.W, a.in, a.out, n0, a.in, -1);
-        floatx4 acc[TM][TN];
-        zero_acc<TM, TN>(acc);
-        mfma_loop<TM, TN>(A, B, 0, a.out, acc);
-#pragma unroll
-        for (int tn = 0; tn < TN; tn++) {
-            const int col = n0 + tn * 16 + i;
-            if (col >= a.in) continue;
-#pragma unroll
-            for (int tm = 0; tm < TM; tm++)
-#pragma unroll
-                for (int r = 0; r < 4; r++) {
-                    const int row = m0 + tm * 16 + 4 * g + r;
-                    if (row < a.Bl)
-                        a.dZprev[(int64_t)row * a.in + col] =
-                            act_bwd<ACT>(acc[tm][tn][r], a.Hprev[(int64_t)row * a.ldh + col]);
-                }
-        }
-        return;
-    }
-    b -= a.dx_blocks;
-    const int bx = b % a.dw_grid_x;
-    const int t2 = b / a.dw_grid_x;
-    const int by = t2 % a.dw_grid_y, bz = t2 / a.dw_grid_y;
-    const int m0 = by * (WM * TM * 16) + wm * TM * 16;   // out rows
-    const int n0 = bx * (WN * TN * 16) + wn * TN * 16;   // in cols (+ ones column)
-    const int kb = bz * a.kslice;
-    const int ke = min(a.Bl, kb + a.kslice);
-    StridedK<TM> A;
-    A.set(a.dZ, a.out, ke, m0, a.out, -1);
-    StridedK<TN> B;
-    B.set(a.X, a.ldx, ke, n0, a.in, a.in);
-    floatx4 acc[TM][TN];
-    zero_acc<TM, TN>(acc);
-    mfma_loop<TM, TN>(A, B, kb, ke, acc);
-    float* part = a.partial + (int64_t)bz * a.pstride;
-#pragma unroll
-    for (int tn = 0; tn < TN; tn++) {
-        const int col = n0 + tn * 16 + i;
-        if (col > a.in) continue;
-#pragma unroll
-        for (int tm = 0; tm < TM; tm++)
-#pragma unroll
-            for (int r = 0; r < 4; r++) {
-                const int row = m0 + tm * 16 + 4 * g + r;
-                if (row >= a.out) continue;
-                const int64_t o = (col < a.in) ? (int64_t)row * a.in + col : (int64_t)a.out * a.in + row;
-                part[o] = acc[tm][tn][r];
-            }
-    }
-}
-
-// =====================================================================================
-// Fused head kernel: one workgroup = 16 samples.
-//   (1) head Linear(s) for the 3 streams on MFMA (waves 0..2)
-//   (2) per sample: dueling aggregate, Double-DQN argmax / DQN max, TD target
-//       y = r + ((1-d)*gamma)*q', q(s,a), Huber (beta=1) value and gradient (mean or
-//       IS-weighted 'none' reduction), dQ -> d(head outputs)
-//   (3) dH = dHead . W_head, dZ_L = dH (.) act'(H_L); head-weight gradient partial of the
-//       16 samples; loss partial.
-// =====================================================================================
 __device__ __forceinline__ int head_w_off(int kind, int o, int F) {
     // dueling: [fc_val.w (F) | fc_val.b | fc_adv.w (A*F) | fc_adv.b (A)], o = 0 val, 1..A adv
     // linear:  [fc_out.w (A*F) | fc_out.b (A)]
@@ -156,171 +64,371 @@ __device__ __forceinline__ int head_b_off(int kind, int o, int F, int A) {
     return kind == DQNX_HEAD_DUELING ? (o == 0 ? F : F + 1 + A * F + (o - 1)) : A * F + o;
 }
 
+// Engine adapter: G::run leaves tile element rows [ro + tm*16 + 4g + r], cols [co + tn*16 + i]
+// in acc[tm][tn][r] of the waves for which owner() is true.
+template <int BM, int BN, int KT, int WM, int LA, int LB, bool VA, bool VB>
+struct Engine {
+#if DQNX_GEMM_SK
+    using G = TileGemmSK<BM, BN, 4, (KT < 64 ? KT : 64), LA, LB, VA, VB>;
+    __device__ __forceinline__ static int ro() { return 0; }
+    __device__ __forceinline__ static int co() { return 0; }
+    __device__ __forceinline__ static bool owner() { return (threadIdx.x >> 6) == 0; }
+#else
+    using G = TileGemm<BM, BN, KT, WM, 4 / WM, LA, LB, VA, VB>;
+    __device__ __forceinline__ static int ro() { return ((threadIdx.x >> 6) / (4 / WM)) * G::TM * 16; }
+    __device__ __forceinline__ static int co() { return ((threadIdx.x >> 6) % (4 / WM)) * G::TN * 16; }
+    __device__ __forceinline__ static bool owner() { return true; }
+#endif
+    static constexpr int TM = G::TM, TN = G::TN, LDS_FLOATS = G::LDS_FLOATS > 0 ? G::LDS_FLOATS : 1;
+};
+
+// =====================================================================================
+// Forward Linear: C[s] = act(A[s] W[s]^T + b[s]) for up to 3 "streams":
+// online(obs), online(next_obs), target(next_obs).  Layer 1 gathers A rows from the
+// replay ring through the sampled physical slots (no materialised minibatch), and
+// stream 0's first column tile also writes the gathered rows to `xcopy` for layer-1 dW.
+// =====================================================================================
+template <int ACT, bool VECB>
+__global__ __launch_bounds__(256) void k_linear_fwd(FwdArgs args) {
+    using E = Engine<FWD_BM, FWD_BN, DQNX_FWD_KT, DQNX_FWD_WM, L_ROWS_K, L_ROWS_K, true, VECB>;
+    constexpr int TM = E::TM, TN = E::TN;
+    __shared__ __attribute__((aligned(16))) float lds[E::LDS_FLOATS];
+    // tiles ordered (stream, m-tile, n-tile) with n fastest; each XCD gets a contiguous
+    // range, so the n-tiles that re-read one m-tile's gathered rows share an L2.
+    const int ntn = (args.N + FWD_BN - 1) / FWD_BN, ntm = (args.M + FWD_BM - 1) / FWD_BM;
+    const int T = xcd_remap(blockIdx.x, ntn * ntm * args.nprob);
+    const int z = T / (ntn * ntm), rem = T - z * ntn * ntm;
+    const int tm_ = rem / ntn, tn_ = rem - tm_ * ntn;
+    const FwdProblem& P = args.p[z];
+    const int lane = threadIdx.x & 63;
+    const int i = lane & 15, g = lane >> 4;
+    const int m0 = tm_ * FWD_BM, n0 = tn_ * FWD_BN;
+    const int M = args.M, N = args.N, K = args.K;
+    const int Kpad = (K + 3) & ~3;   // ring / activation rows are zero padded to a multiple of 4
+    float bias[TN];                  // epilogue operands fetched before the main loop
+#pragma unroll
+    for (int tn = 0; tn < TN; tn++) {
+        const int col = n0 + E::co() + tn * 16 + i;
+        bias[tn] = col < N ? P.bias[col] : 0.f;
+    }
+    Operand A{P.A, P.lda, P.phys, M, Kpad, -1, (P.xcopy && tn_ == 0) ? P.xcopy : nullptr, P.lda};
+    Operand B{P.W, K, nullptr, N, K, -1, nullptr, 0};
+    floatx4 acc[TM][TN];
+    E::G::run(lds, A, B, m0, n0, 0, Kpad, acc);
+    if (!E::owner()) return;
+#pragma unroll
+    for (int tn = 0; tn < TN; tn++) {
+        const int col = n0 + E::co() + tn * 16 + i;
+        if (col >= N) continue;
+#pragma unroll
+        for (int tm = 0; tm < TM; tm++)
+#pragma unroll
+            for (int r = 0; r < 4; r++) {
+                const int row = m0 + E::ro() + tm * 16 + 4 * g + r;
+                if (row < M) P.C[(int64_t)row * args.ldc + col] = act_fwd<ACT>(acc[tm][tn][r] + bias[tn]);
+            }
+    }
+}
+
+// =====================================================================================
+// Backward level: independent GEMMs in one launch.
+//   dx role:  dZprev = (dZ W) (.) act'(Hprev)      [Bl x in], K = out
+//   dw role:  partial[s] = dZ^T [Xprev | 1]        [out x (in+1)], K = samples of slice s
+// =====================================================================================
 template <int ACT>
+__global__ __launch_bounds__(256) void k_bwd_level(BwdArgs a) {
+    using EX = Engine<BWD_BM, BWD_BN, DQNX_BWD_KT, DQNX_BWD_WM, L_ROWS_K, L_K_ROWS, true, true>;
+    using EW = Engine<BWD_BM, BWD_BN, DQNX_BWD_KT, DQNX_BWD_WM, L_K_ROWS, L_K_ROWS, true, true>;
+    constexpr int TM = EX::TM, TN = EX::TN;
+    constexpr int LF = EX::LDS_FLOATS > EW::LDS_FLOATS ? EX::LDS_FLOATS : EW::LDS_FLOATS;
+    __shared__ __attribute__((aligned(16))) float lds[LF];
+    const int lane = threadIdx.x & 63;
+    const int i = lane & 15, g = lane >> 4;
+    int b = blockIdx.x;
+    floatx4 acc[TM][TN];
+    if (b < a.dx_blocks) {
+        const int T = xcd_remap(b, a.dx_blocks);
+        const int bx = T % a.dx_grid_x, by = T / a.dx_grid_x;
+        const int m0 = by * BWD_BM, n0 = bx * BWD_BN;
+        float hm[TM][TN][4];   // activation values for the mask, fetched before the main loop
+#pragma unroll
+        for (int tn = 0; tn < TN; tn++)
+#pragma unroll
+            for (int tm = 0; tm < TM; tm++)
+#pragma unroll
+                for (int r = 0; r < 4; r++) {
+                    const int col = n0 + EX::co() + tn * 16 + i, row = m0 + EX::ro() + tm * 16 + 4 * g + r;
+                    hm[tm][tn][r] = (col < a.in && row < a.Bl) ? a.Hprev[(int64_t)row * a.ldh + col] : 0.f;
+                }
+        Operand A{a.dZ, a.out, nullptr, a.Bl, a.out, -1, nullptr, 0};
+        Operand B{a.W, a.in, nullptr, a.in, a.out, -1, nullptr, 0};
+        EX::G::run(lds, A, B, m0, n0, 0, a.out, acc);
+        if (!EX::owner()) return;
+#pragma unroll
+        for (int tn = 0; tn < TN; tn++) {
+            const int col = n0 + EX::co() + tn * 16 + i;
+            if (col >= a.in) continue;
+#pragma unroll
+            for (int tm = 0; tm < TM; tm++)
+#pragma unroll
+                for (int r = 0; r < 4; r++) {
+                    const int row = m0 + EX::ro() + tm * 16 + 4 * g + r;
+                    if (row < a.Bl) a.dZprev[(int64_t)row * a.in + col] = act_bwd<ACT>(acc[tm][tn][r], hm[tm][tn][r]);
+                }
+        }
+        return;
+    }
+    b -= a.dx_blocks;
+    const int p = (a.ndw > 1 && b >= a.dw[0].blocks) ? 1 : 0;
+    if (p) b -= a.dw[0].blocks;
+    const DwProblem& d = a.dw[p];
+    // dW tiles ordered (slice, m, n) so one XCD re-reads one slice of dZ / X rows
+    b = xcd_remap(b, d.blocks);
+    const int bx = b % d.grid_x;
+    const int t2 = b / d.grid_x;
+    const int by = t2 % d.grid_y, bz = t2 / d.grid_y;
+    const int m0 = by * BWD_BM, n0 = bx * BWD_BN;
+    const int kb = bz * a.kslice;
+    const int ke = min(a.Bl, kb + a.kslice);
+    Operand A{d.dZ, d.ldz, nullptr, d.out, a.Bl, -1, nullptr, 0};
+    Operand B{d.X, d.ldx, nullptr, d.in, a.Bl, d.in, nullptr, 0};
+    EW::G::run(lds, A, B, m0, n0, kb, ke, acc);
+    if (!EW::owner()) return;
+    float* part = d.partial + (int64_t)bz * d.pstride;
+#pragma unroll
+    for (int tn = 0; tn < TN; tn++) {
+        const int col = n0 + EW::co() + tn * 16 + i;
+        if (col > d.in) continue;
+#pragma unroll
+        for (int tm = 0; tm < TM; tm++)
+#pragma unroll
+            for (int r = 0; r < 4; r++) {
+                const int row = m0 + EW::ro() + tm * 16 + 4 * g + r;
+                if (row >= d.out) continue;
+                int64_t o;
+                if (d.head_kind < 0) o = (col < d.in) ? (int64_t)row * d.in + col : (int64_t)d.out * d.in + row;
+                else o = (col < d.in) ? head_w_off(d.head_kind, row, d.in) + col : head_b_off(d.head_kind, row, d.in, d.A);
+                part[o] = acc[tm][tn][r];
+            }
+    }
+}
+
+// =====================================================================================
+// Fused head kernel: one workgroup = 16 samples, 256 threads.
+//   (0) stage H_L of the 3 streams and both heads' weights in LDS (one round trip)
+//   (1) head Linear for the 3 streams on MFMA (waves 0..2)
+//   (2) thread (b, j): Q[s][b][j] (dueling aggregate V + (A - mean A))
+//   (3) thread (b, 0): Double-DQN argmax / DQN max, TD target y = r + ((1-d)*gamma)*q',
+//       q(s,a), Huber (beta=1) value and gradient (mean or IS-weighted 'none' reduction)
+//   (4) thread (b, o): d(head outputs)
+//   (5) MFMA: dH = dHead . W_head -> dZ_L = dH (.) act'(H_L);  dW_head partial = dHead^T H_L;
+//       bias and loss partials in fixed order.
+// =====================================================================================
+template <int ACT, int F>
 __global__ __launch_bounds__(256) void k_head(HeadArgs a) {
-    constexpr int TS = 16;
-    __shared__ float raw[3][TS][17];
-    __shared__ float dh[TS][17];
-    __shared__ float lossv[TS];
-    extern __shared__ __attribute__((aligned(16))) float dyn[];
-    float* Hl = dyn;                       // [TS][F]   last hidden of stream 0 (online, obs)
-    float* Wl = dyn + TS * a.F;            // [NH][F]   online head weights
+    constexpr int TS = 16, QS = 17;
+    constexpr int SF = F + 8, F4 = F / 4;
+    constexpr int NHQ = 3 * TS * F4, NWQ = 2 * 16 * F4, NQ = (NHQ + NWQ + 255) / 256;
+    __shared__ __attribute__((aligned(16))) float dyn[5 * 16 * SF];
+    __shared__ float raw[3][TS][QS];
+    __shared__ float qv[3][TS][QS];
+    __shared__ float dh[TS][20];
+    __shared__ float gsh[TS], lossv[TS], rsh[TS], dsh[TS], wsh[TS];
+    __shared__ int ash[TS];
 
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int i = lane & 15, g = lane >> 4;
     const int b0 = blockIdx.x * TS;
-    const int F = a.F, A = a.A, NH = a.NH, Bl = a.Bl;
+    const int A = a.A, NH = a.NH, Bl = a.Bl;
     const int nb = min(TS, Bl - b0);
+    const bool use1 = a.algo != DQNX_ALGO_DQN;
+    float* Hs = dyn;                    // [3][TS][SF]
+    float* Wh = dyn + 3 * TS * SF;      // [2][16][SF] online, target (rows >= NH zero)
+    DQNX_STAMP(a.stamps, 16);
 
-    // stage H_L(stream 0) tile and the online head weights into LDS
-    for (int idx = tid; idx < TS * F; idx += 256) {
-        const int b = idx / F, f = idx - b * F;
-        Hl[idx] = (b < nb) ? a.H[(int64_t)(b0 + b) * F + f] : 0.f;
+    // (0) stage: every load issued before the first wait
+    {
+        float4 v[NQ];
+#pragma unroll
+        for (int j = 0; j < NQ; j++) {
+            const int q = tid + 256 * j;
+            float4 x = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (q < NHQ) {
+                const int s = q / (TS * F4), rem = q - s * TS * F4, b = rem / F4, c = 4 * (rem - b * F4);
+                if (b < nb && (s != 1 || use1)) x = ld4(a.H + ((int64_t)s * Bl + b0 + b) * F + c);
+            } else if (q < NHQ + NWQ) {
+                const int q2 = q - NHQ;
+                const int w = q2 / (16 * F4), rem = q2 - w * 16 * F4, o = rem / F4, c = 4 * (rem - o * F4);
+                if (o < NH) x = ld4((w ? a.Wt : a.Wo) + head_w_off(a.head_kind, o, F) + c);
+            }
+            v[j] = x;
+        }
+#pragma unroll
+        for (int j = 0; j < NQ; j++) {
+            const int q = tid + 256 * j;
+            if (q < NHQ) {
+                const int s = q / (TS * F4), rem = q - s * TS * F4, b = rem / F4, c = 4 * (rem - b * F4);
+                *reinterpret_cast<float4*>(Hs + (s * TS + b) * SF + c) = v[j];
+            } else if (q < NHQ + NWQ) {
+                const int q2 = q - NHQ;
+                const int w = q2 / (16 * F4), rem = q2 - w * 16 * F4, o = rem / F4, c = 4 * (rem - o * F4);
+                *reinterpret_cast<float4*>(Wh + (w * 16 + o) * SF + c) = v[j];
+            }
+        }
+        if (tid < TS) {
+            const int b = tid;
+            int act = 0;
+            float rew = 0.f, done = 0.f, w = 1.f;
+            if (b < nb) {
+                const int slot = a.phys[b0 + b];
+                act = a.act[slot];
+                rew = a.rew[slot];
+                done = a.done[slot];
+                if (a.isw) w = a.isw[b0 + b];
+                if (act < 0 || act >= A) act = 0;
+            }
+            ash[b] = act;
+            rsh[b] = rew;
+            dsh[b] = done;
+            wsh[b] = w;
+        }
     }
-    for (int idx = tid; idx < NH * F; idx += 256) {
-        const int o = idx / F, f = idx - o * F;
-        Wl[idx] = a.Wo[head_w_off(a.head_kind, o, F) + f];
-    }
+    __syncthreads();
+    DQNX_STAMP(a.stamps, 17);
 
-    // (1) head outputs for the streams this algorithm needs
-    if (wid < 3 && !(wid == 1 && a.algo == DQNX_ALGO_DQN)) {
+    // (1) head outputs per stream: raw[s] = H_s . W^T + b
+    if (wid < 3 && (wid != 1 || use1)) {
         const int s = wid;
-        const float* W = (s == 2) ? a.Wt : a.Wo;
-        const float* Hs = a.H + (int64_t)s * Bl * F;
-        const int row = b0 + i;
-        const float* arow = (row < Bl) ? Hs + (int64_t)row * F : nullptr;
-        const float* brow = (i < NH) ? W + head_w_off(a.head_kind, i, F) : nullptr;
+        const float* hs = Hs + s * TS * SF;
+        const float* wh = Wh + (s == 2 ? 16 : 0) * SF;
         floatx4 acc = {0.f, 0.f, 0.f, 0.f};
-        for (int k0 = 0; k0 < F; k0 += 16) {
-            const int k = k0 + 4 * g;
-            float4 av = make_float4(0.f, 0.f, 0.f, 0.f), bv = av;
-            if (arow && k < F) av = ld4(arow + k);
-            if (brow && k < F) bv = ld4(brow + k);
+        for (int kk = 0; kk < F; kk += 16) {
+            const float4 av = *reinterpret_cast<const float4*>(hs + i * SF + kk + 4 * g);
+            const float4 bv = *reinterpret_cast<const float4*>(wh + i * SF + kk + 4 * g);
             acc = mfma16x16x4(av.x, bv.x, acc);
             acc = mfma16x16x4(av.y, bv.y, acc);
             acc = mfma16x16x4(av.z, bv.z, acc);
             acc = mfma16x16x4(av.w, bv.w, acc);
         }
+        const float* W = (s == 2) ? a.Wt : a.Wo;
         const float bias = (i < NH) ? W[head_b_off(a.head_kind, i, F, A)] : 0.f;
 #pragma unroll
         for (int r = 0; r < 4; r++) raw[s][4 * g + r][i] = acc[r] + bias;
     }
     __syncthreads();
 
-    // (2) per-sample TD / loss / head gradient
+    // (2) Q values, thread (b, j)
+    {
+        const int b = tid >> 4, j = tid & 15;
+        for (int s = 0; s < 3; s++) {
+            if (s == 1 && !use1) continue;
+            float q = 0.f;
+            if (a.head_kind == DQNX_HEAD_DUELING) {
+                float sum = 0.f;
+                for (int jj = 0; jj < A; jj++) sum += raw[s][b][1 + jj];
+                const float mean = sum / (float)A;
+                if (j < A) q = raw[s][b][0] + (raw[s][b][1 + j] - mean);
+            } else if (j < A) {
+                q = raw[s][b][j];
+            }
+            qv[s][b][j] = q;
+            if (j < A && b < nb) a.Q[((int64_t)s * Bl + b0 + b) * A + j] = q;
+        }
+    }
+    __syncthreads();
+    DQNX_STAMP(a.stamps, 18);
+
+    // (3) per-sample TD target / Huber, thread (b, 0)
     if (tid < TS) {
         const int b = tid;
-        float dho[17];
-        float lb = 0.f;
+        float gq = 0.f, lb = 0.f;
         if (b < nb) {
-            const int gb = b0 + b;
-            const int slot = a.phys[gb];
-            const int act = a.act[slot];
-            const float rew = a.rew[slot], done = a.done[slot];
-            float q[3][16];
-            for (int s = 0; s < 3; s++) {
-                if (s == 1 && a.algo == DQNX_ALGO_DQN) continue;
-                if (a.head_kind == DQNX_HEAD_DUELING) {
-                    const float v = raw[s][b][0];
-                    float sum = 0.f;
-                    for (int j = 0; j < A; j++) sum += raw[s][b][1 + j];
-                    const float mean = sum / (float)A;
-                    for (int j = 0; j < A; j++) q[s][j] = v + (raw[s][b][1 + j] - mean);
-                } else {
-                    for (int j = 0; j < A; j++) q[s][j] = raw[s][b][j];
-                }
-                for (int j = 0; j < A; j++) a.Q[((int64_t)s * Bl + gb) * A + j] = q[s][j];
-            }
             float qn;
-            if (a.algo == DQNX_ALGO_DQN) {        // target(s').max(1)  (R:dqn/agent.py:172-173)
-                qn = q[2][0];
-                for (int j = 1; j < A; j++) qn = q[2][j] > qn ? q[2][j] : qn;
-            } else {                               // argmax online(s'), gather target(s') (:210-214)
+            if (!use1) {                                   // target(s').max(1) (R:dqn/agent.py:172-173)
+                qn = qv[2][b][0];
+                for (int j = 1; j < A; j++) qn = qv[2][b][j] > qn ? qv[2][b][j] : qn;
+            } else {                                       // argmax online(s'), gather target(s') (:210-214)
                 int best = 0;
-                float bq = q[1][0];
+                float bq = qv[1][b][0];
                 for (int j = 1; j < A; j++)
-                    if (q[1][j] > bq) { bq = q[1][j]; best = j; }
-                qn = q[2][best];
+                    if (qv[1][b][j] > bq) { bq = qv[1][b][j]; best = j; }
+                qn = qv[2][b][best];
             }
-            // targets = rews + (1 - dones) * gamma * q'    (R:dqn/agent.py:216)
-            const float t1 = 1.f - done;
+            // targets = rews + (1 - dones) * gamma * q'   (R:dqn/agent.py:216)
+            const float t1 = 1.f - dsh[b];
             const float t2 = t1 * a.gamma;
             const float t3 = t2 * qn;
-            const float y = rew + t3;
-            const float qa = q[0][act];
-            const float x = qa - y;               // smooth_l1: input - target
+            const float y = rsh[b] + t3;
+            const float qa = qv[0][b][ash[b]];
+            const float x = qa - y;                        // smooth_l1: input - target
             const float z = fabsf(x);
             const float l = z < 1.f ? (0.5f * z) * z / 1.f : z - 0.5f;
-            float gq;
-            if (a.isw) {                          // PER: mean(w * huber_none)  (R:dqn/agent.py:267)
-                const float w = a.isw[gb];
-                const float go = a.inv_bg * w;    // MeanBackward (1/B) then MulBackward (* w)
+            if (a.isw) {                                   // PER: mean(w * huber_none) (R:dqn/agent.py:267)
+                const float go = a.inv_bg * wsh[b];
                 gq = x <= -1.f ? -go : (x >= 1.f ? go : (x * go) / 1.f);
-                lb = w * l;
-            } else {                              // SmoothL1Loss(mean): norm = 1/B
+                lb = wsh[b] * l;
+            } else {                                       // SmoothL1Loss(mean): norm = 1/B
                 gq = x <= -1.f ? -a.inv_bg : (x >= 1.f ? a.inv_bg : (a.inv_bg * x) / 1.f);
                 lb = l;
             }
+            const int gb = b0 + b;
             a.td[gb] = y;
             a.td[Bl + gb] = qa;
             a.td[2 * Bl + gb] = z;
-            if (a.head_kind == DQNX_HEAD_DUELING) {
-                const float nm = (-gq) / (float)A;    // mean backward of -sum(dQ)
-                dho[0] = gq;                          // dV = sum_a dQ
-                for (int j = 0; j < A; j++) dho[1 + j] = (j == act ? gq : 0.f) + nm;
-            } else {
-                for (int j = 0; j < A; j++) dho[j] = (j == act) ? gq : 0.f;
-            }
-        } else {
-            for (int o = 0; o < NH; o++) dho[o] = 0.f;
         }
-        for (int o = 0; o < NH; o++) dh[b][o] = dho[o];
+        gsh[b] = gq;
         lossv[b] = lb;
     }
     __syncthreads();
 
-    // (3a) loss partial (fixed order)
-    if (tid == 0) {
+    // (4) d(head outputs), thread (b, o)
+    {
+        const int b = tid >> 4, o = tid & 15;
+        const float gq = gsh[b];
+        const int act = ash[b];
+        float d = 0.f;
+        if (o < NH) {
+            if (a.head_kind == DQNX_HEAD_DUELING)
+                d = (o == 0) ? gq : ((o - 1 == act ? gq : 0.f) + (-gq) / (float)A);   // V / A - mean(A) bwd
+            else
+                d = (o == act) ? gq : 0.f;
+        }
+        dh[b][o] = d;
+    }
+    __syncthreads();
+    DQNX_STAMP(a.stamps, 19);
+
+    // (5) dH = dHead . W_head (online), dZ_L = dH (.) act'(H_L)   [TS x F], K = 16 head rows;
+    //     dHead rows go to global for the head-weight gradient (bwd level L)
+    if (tid < TS * 4) {
+        const int b = tid >> 2, q = tid & 3;
+        if (b < nb)
+            *reinterpret_cast<float4*>(a.dhead + (int64_t)(b0 + b) * 16 + 4 * q) =
+                make_float4(dh[b][4 * q], dh[b][4 * q + 1], dh[b][4 * q + 2], dh[b][4 * q + 3]);
+    }
+    constexpr int ftiles = F / 16;
+    for (int t = wid; t < ftiles; t += 4) {
+        const int f0 = t * 16;
+        floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int jj = 0; jj < 4; jj++) {   // A[b][o] = dh[b][o]; B[o][f] = Wh_online[o][f]
+            const int o = 4 * g + jj;
+            acc = mfma16x16x4(dh[i][o], Wh[o * SF + f0 + i], acc);
+        }
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+            const int b = 4 * g + r;
+            if (b < nb) a.dZ[(int64_t)(b0 + b) * F + f0 + i] = act_bwd<ACT>(acc[r], Hs[b * SF + f0 + i]);
+        }
+    }
+    if (tid == 64) {
         float s = 0.f;
         for (int b = 0; b < TS; b++) s += lossv[b];
         a.loss_partial[blockIdx.x] = s;
     }
-    // (3b) dH_L and dZ_L = dH_L (.) act'(H_L)
-    for (int idx = tid; idx < TS * F; idx += 256) {
-        const int b = idx / F, f = idx - b * F;
-        if (b >= nb) continue;
-        float s = 0.f;
-        if (a.head_kind == DQNX_HEAD_DUELING) {
-            for (int o = 1; o < NH; o++) s += dh[b][o] * Wl[o * F + f];
-            s = dh[b][0] * Wl[f] + s;
-        } else {
-            for (int o = 0; o < NH; o++) s += dh[b][o] * Wl[o * F + f];
-        }
-        a.dZ[(int64_t)(b0 + b) * F + f] = act_bwd<ACT>(s, Hl[idx]);
-    }
-    // (3c) head weight / bias gradient partial of this tile
-    float* part = a.head_partial + (int64_t)blockIdx.x * a.head_params;
-    for (int idx = tid; idx < NH * F; idx += 256) {
-        const int o = idx / F, f = idx - o * F;
-        float s = 0.f;
-        for (int b = 0; b < TS; b++) s += dh[b][o] * Hl[b * F + f];
-        part[head_w_off(a.head_kind, o, F) + f] = s;
-    }
-    if (tid < NH) {
-        float s = 0.f;
-        for (int b = 0; b < TS; b++) s += dh[b][tid];
-        part[head_b_off(a.head_kind, tid, F, A)] = s;
-    }
-    // Adam scalars of this step (read by the Adam pass, a later launch)
-    if (blockIdx.x == 0 && tid == 0 && a.ctrl) {
-        const int64_t t = a.ctrl->adam_step + 1;
-        a.ctrl->adam_step = t;
-        const double bc1 = 1.0 - pow((double)a.beta1, (double)t);
-        const double bc2 = 1.0 - pow((double)a.beta2, (double)t);
-        const double step_size = (double)a.lr / bc1;
-        a.ctrl->adam_step_size = (float)(-step_size);
-        a.ctrl->adam_bc2_sqrt = (float)sqrt(bc2);
-    }
+    // Adam step counter of this learn step (read by the Adam pass, a later launch)
+    if (blockIdx.x == 0 && tid == 128 && a.ctrl) a.ctrl->adam_step = a.ctrl->adam_step + 1;
+    DQNX_STAMP(a.stamps, 20);
 }
 
 // =====================================================================================
@@ -346,14 +454,28 @@ __global__ __launch_bounds__(256) void k_adam(AdamArgs a) {
                 if (e >= a.seg[q].off) sgi = q;
             const AdamSegment sg = a.seg[sgi];
             const float* pp = sg.partial + (e - sg.off);
-            gsum = pp[0];
-#pragma unroll 1
-            for (int s = 1; s < sg.S; s++) gsum += pp[(int64_t)s * sg.pstride];
+            // fixed-order sum of the slabs; loads issued 8 at a time before the adds
+            gsum = 0.f;
+            for (int s0 = 0; s0 < sg.S; s0 += 8) {
+                float v[8];
+#pragma unroll
+                for (int u = 0; u < 8; u++) v[u] = (s0 + u < sg.S) ? pp[(int64_t)(s0 + u) * sg.pstride] : 0.f;
+#pragma unroll
+                for (int u = 0; u < 8; u++)
+                    if (s0 + u < sg.S) gsum = (s0 + u == 0) ? v[u] : gsum + v[u];
+            }
             a.grads[e] = gsum;
         }
         if (a.mode == 0) continue;
-        const float step_size = a.ctrl->adam_step_size;
-        const float bc2s = a.ctrl->adam_bc2_sqrt;
+        const int64_t t = a.ctrl->adam_step;
+        float step_size, bc2s;
+        if (t >= 1 && t <= a.adam_table_len) {
+            step_size = a.adam_table[2 * (t - 1)];
+            bc2s = a.adam_table[2 * (t - 1) + 1];
+        } else {   // beyond the precomputed range: device libm (may differ in the last bit)
+            step_size = (float)(-(a.lrd / (1.0 - pow(a.beta1d, (double)t))));
+            bc2s = (float)pow(1.0 - pow(a.beta2d, (double)t), 0.5);
+        }
         float m = a.m[e], v = a.v[e], p = a.p[e];
         m = fmaf(a.w1, gsum - m, m);
         v = v * a.beta2;
@@ -410,21 +532,22 @@ __global__ void k_replay_push(PushArgs a) {
 // host-side launchers
 // =====================================================================================
 int launch_linear_fwd(const FwdArgs& args, int nprob, int act, bool vecb, hipStream_t s) {
-    constexpr int TM = 1, TN = 2, WM = 2, WN = 2;
-    dim3 grid((args.N + WN * TN * 16 - 1) / (WN * TN * 16), (args.M + WM * TM * 16 - 1) / (WM * TM * 16), nprob);
+    FwdArgs a2 = args;
+    a2.nprob = nprob;
+    dim3 grid(((args.N + FWD_BN - 1) / FWD_BN) * ((args.M + FWD_BM - 1) / FWD_BM) * nprob);
     if (act == DQNX_ACT_RELU) {
-        if (vecb) hipLaunchKernelGGL((k_linear_fwd<TM, TN, WM, WN, DQNX_ACT_RELU, true>), grid, dim3(256), 0, s, args);
-        else hipLaunchKernelGGL((k_linear_fwd<TM, TN, WM, WN, DQNX_ACT_RELU, false>), grid, dim3(256), 0, s, args);
+        if (vecb) hipLaunchKernelGGL((k_linear_fwd<DQNX_ACT_RELU, true>), grid, dim3(256), 0, s, a2);
+        else hipLaunchKernelGGL((k_linear_fwd<DQNX_ACT_RELU, false>), grid, dim3(256), 0, s, a2);
     } else {
-        if (vecb) hipLaunchKernelGGL((k_linear_fwd<TM, TN, WM, WN, DQNX_ACT_ELU, true>), grid, dim3(256), 0, s, args);
-        else hipLaunchKernelGGL((k_linear_fwd<TM, TN, WM, WN, DQNX_ACT_ELU, false>), grid, dim3(256), 0, s, args);
+        if (vecb) hipLaunchKernelGGL((k_linear_fwd<DQNX_ACT_ELU, true>), grid, dim3(256), 0, s, a2);
+        else hipLaunchKernelGGL((k_linear_fwd<DQNX_ACT_ELU, false>), grid, dim3(256), 0, s, a2);
     }
     DQNX_HIP_CHECK(hipGetLastError());
     return DQNX_OK;
 }
 
 void bwd_level_grid(BwdArgs& a) {
-    constexpr int BM = 32, BN = 64;
+    constexpr int BM = BWD_BM, BN = BWD_BN;
     if (a.dZprev) {
         a.dx_grid_x = (a.in + BN - 1) / BN;
         a.dx_blocks = a.dx_grid_x * ((a.Bl + BM - 1) / BM);
@@ -432,23 +555,39 @@ void bwd_level_grid(BwdArgs& a) {
         a.dx_grid_x = 1;
         a.dx_blocks = 0;
     }
-    a.dw_grid_x = (a.in + 1 + BN - 1) / BN;
-    a.dw_grid_y = (a.out + BM - 1) / BM;
+    for (int p = 0; p < a.ndw; p++) {
+        DwProblem& d = a.dw[p];
+        d.grid_x = (d.in + 1 + BN - 1) / BN;
+        d.grid_y = (d.out + BM - 1) / BM;
+        d.blocks = d.grid_x * d.grid_y * a.dw_slices;
+    }
 }
 
-int launch_bwd_level(const BwdArgs& a, int nslices, int act, hipStream_t s) {
-    const int blocks = a.dx_blocks + a.dw_grid_x * a.dw_grid_y * nslices;
+int launch_bwd_level(const BwdArgs& a, int act, hipStream_t s) {
+    int blocks = a.dx_blocks;
+    for (int p = 0; p < a.ndw; p++) blocks += a.dw[p].blocks;
     if (act == DQNX_ACT_RELU) hipLaunchKernelGGL(k_bwd_level<DQNX_ACT_RELU>, dim3(blocks), dim3(256), 0, s, a);
     else hipLaunchKernelGGL(k_bwd_level<DQNX_ACT_ELU>, dim3(blocks), dim3(256), 0, s, a);
     DQNX_HIP_CHECK(hipGetLastError());
     return DQNX_OK;
 }
 
+template <int F>
+static void launch_head_f(const HeadArgs& a, int act, int tiles, hipStream_t s) {
+    if (act == DQNX_ACT_RELU) hipLaunchKernelGGL((k_head<DQNX_ACT_RELU, F>), dim3(tiles), dim3(256), 0, s, a);
+    else hipLaunchKernelGGL((k_head<DQNX_ACT_ELU, F>), dim3(tiles), dim3(256), 0, s, a);
+}
+
+bool head_supported(int F) { return F == 64 || F == 128 || F == 256; }
+
 int launch_head(const HeadArgs& a, int act, hipStream_t s) {
     const int tiles = (a.Bl + 15) / 16;
-    const size_t lds = (size_t)(16 + a.NH) * a.F * sizeof(float);
-    if (act == DQNX_ACT_RELU) hipLaunchKernelGGL(k_head<DQNX_ACT_RELU>, dim3(tiles), dim3(256), lds, s, a);
-    else hipLaunchKernelGGL(k_head<DQNX_ACT_ELU>, dim3(tiles), dim3(256), lds, s, a);
+    switch (a.F) {
+        case 64: launch_head_f<64>(a, act, tiles, s); break;
+        case 128: launch_head_f<128>(a, act, tiles, s); break;
+        case 256: launch_head_f<256>(a, act, tiles, s); break;
+        default: return set_error(DQNX_EUNSUPPORTED, "head input width %d not in {64,128,256}", a.F);
+    }
     DQNX_HIP_CHECK(hipGetLastError());
     return DQNX_OK;
 }

@@ -16,25 +16,38 @@ struct FwdProblem {
 struct FwdArgs {
     FwdProblem p[3];
     int M, N, K, ldc;
+    int nprob;
 };
 
+// One split-K weight-gradient GEMM: partial[s] = dZ^T [X | 1] over the samples of slice s.
+// Partials are written in the flat parameter layout of the layer: plain Linear
+// ([W (out x in) | b (out)]) or, for head_kind >= 0, the Q-head layout
+// ([fc_val.w | fc_val.b | fc_adv.w | fc_adv.b] or [fc_out.w | fc_out.b]).
+struct DwProblem {
+    const float* dZ;       // [Bl][ldz]
+    int ldz;
+    const float* X;        // [Bl][ldx] layer input rows (stream 0)
+    int ldx;
+    int in, out;
+    float* partial;        // [slices][pstride]
+    int64_t pstride;
+    int head_kind;         // -1 plain Linear layout, else dqnx_head_kind
+    int A;                 // actions (head layout)
+    int grid_x, grid_y, blocks;   // filled by bwd_level_grid
+};
 struct BwdArgs {
-    // dx role (skipped when dZprev == null)
+    // dx role (skipped when dZprev == null): dZprev = (dZ W) (.) act'(Hprev)
+    const float* dZ;       // [Bl][out]
     const float* W;        // [out][in]
-    const float* Hprev;    // activations of the previous layer, stream 0 [Bl][ldh]
+    const float* Hprev;    // [Bl][ldh]
     int ldh;
     float* dZprev;         // [Bl][in]
-    // dw role
-    const float* X;        // layer input rows [Bl][ldx] (stream 0)
-    int ldx;
-    float* partial;        // [slices][out*in + out]
-    int64_t pstride;
-    int kslice;
-    // shared
-    const float* dZ;       // [Bl][out]
-    int Bl, in, out;
-    // grid bookkeeping (bwd_level_grid)
-    int dx_blocks, dx_grid_x, dw_grid_x, dw_grid_y;
+    int in, out;
+    // dw roles
+    DwProblem dw[2];
+    int ndw;
+    int Bl, kslice, dw_slices;
+    int dx_blocks, dx_grid_x;
 };
 
 struct HeadArgs {
@@ -52,13 +65,15 @@ struct HeadArgs {
     float* Q;              // [3][Bl][A]
     float* td;             // [3][Bl]: y, q(s,a), |y - q(s,a)|
     float* dZ;             // [Bl][F]
-    float* head_partial;   // [tiles][head_params]
+    float* dhead;          // [Bl][16] d(head outputs), consumed by the head dW in the bwd level
     float* loss_partial;   // [tiles]
     dqnx_ctrl* ctrl;       // Adam step bookkeeping (block 0) or null
     float beta1, beta2, lr;
+    int64_t* stamps;       // diagnostic builds (-DDQNX_STAMPS)
 };
 
 constexpr int kMaxSeg = 10;
+constexpr int kAdamTable = 1 << 20;   // precomputed Adam bias corrections (steps 1..2^20)
 struct AdamSegment {
     int64_t off;           // first flat element of the segment
     const float* partial;  // slab 0 of the segment's partials
@@ -81,6 +96,9 @@ struct AdamArgs {
     const float* loss_partial;
     int n_loss_partial;
     int batch_global;
+    const float* adam_table;   // [t-1] = {-lr/bc1, bc2**0.5} for t <= adam_table_len (host libm)
+    int adam_table_len;
+    double beta1d, beta2d, lrd;
 };
 
 struct PushArgs {
@@ -113,12 +131,14 @@ struct SampleArgs {
     int32_t shard_begin, shard_len;
     const int64_t* wptr_dev;
     int64_t capacity;
+    int64_t* stamps;          // diagnostic builds (-DDQNX_STAMPS)
 };
 
 int launch_linear_fwd(const FwdArgs& args, int nprob, int act, bool vecb, hipStream_t s);
 void bwd_level_grid(BwdArgs& a);
-int launch_bwd_level(const BwdArgs& a, int nslices, int act, hipStream_t s);
+int launch_bwd_level(const BwdArgs& a, int act, hipStream_t s);
 int launch_head(const HeadArgs& a, int act, hipStream_t s);
+bool head_supported(int F);
 int launch_adam(const AdamArgs& a, hipStream_t s);
 int launch_soft_update(float* target, const float* p, int64_t n, float tau, float omt, hipStream_t s);
 int launch_replay_push(const PushArgs& a, hipStream_t s);

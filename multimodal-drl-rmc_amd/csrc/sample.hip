@@ -35,20 +35,6 @@ __device__ __forceinline__ uint32_t mt_mix(uint32_t a, uint32_t b) {
     return (y >> 1) ^ ((y & 1u) ? MT_A : 0u);
 }
 
-// Parallel twist of mt[624] (LDS); old copy in tmp.  All threads of the block call it.
-__device__ void mt_twist_block(uint32_t* mt, uint32_t* tmp) {
-    const int tid = threadIdx.x, nt = blockDim.x;
-    for (int i = tid; i < 624; i += nt) tmp[i] = mt[i];
-    __syncthreads();
-    for (int i = tid; i < 227; i += nt) mt[i] = tmp[i + 397] ^ mt_mix(tmp[i], tmp[i + 1]);
-    __syncthreads();
-    for (int i = 227 + tid; i < 454; i += nt) mt[i] = mt[i - 227] ^ mt_mix(tmp[i], tmp[i + 1]);
-    __syncthreads();
-    for (int i = 454 + tid; i < 623; i += nt) mt[i] = mt[i - 227] ^ mt_mix(tmp[i], tmp[i + 1]);
-    if (tid == 0) mt[623] = mt[396] ^ mt_mix(tmp[623], mt[0]);
-    __syncthreads();
-}
-
 // Serial genrand_uint32 on one lane (pool branch).
 __device__ uint32_t mt_next_serial(uint32_t* mt, uint32_t& pos) {
     if (pos >= 624) {
@@ -70,17 +56,20 @@ __device__ __forceinline__ uint32_t hash_u32(uint32_t x) {
 
 
 
+constexpr int SAMPLE_NT = 1024;   // threads of the sampler workgroup (>= 624: one MT word per lane)
+
 template <int HS>  // hash slots (power of two)
-__global__ __launch_bounds__(1024) void k_sample_uniform(SampleArgs a) {
+__global__ __launch_bounds__(SAMPLE_NT) void k_sample_uniform(SampleArgs a) {
+    constexpr int NT = SAMPLE_NT, NW = NT / 64;
     __shared__ unsigned long long tab[HS];
     __shared__ uint32_t mt[624];
     __shared__ uint32_t tmp[624];
-    __shared__ int wave_cnt[16];
+    __shared__ int wave_cnt[NW];
     __shared__ int s_newpos;
-    __shared__ int s_done;
 
-    const int tid = threadIdx.x, nt = blockDim.x;
-    const int lane = tid & 63, wid = tid >> 6, nwaves = nt >> 6;
+    const int tid = threadIdx.x;
+    const int lane = tid & 63, wid = tid >> 6;
+    DQNX_STAMP(a.stamps, 0);
     const int64_t n = a.n_dev ? *a.n_dev : a.n_val;
     const int k = a.k;
     if (k < 0 || (int64_t)k > n) {
@@ -91,13 +80,14 @@ __global__ __launch_bounds__(1024) void k_sample_uniform(SampleArgs a) {
     int64_t phys_base = 0;
     if (a.phys_out) {
         const int64_t wptr = *a.wptr_dev;
-        phys_base = ((wptr - n) % a.capacity + a.capacity) % a.capacity;
+        phys_base = wptr - n;
+        if (phys_base < 0) phys_base += a.capacity;
     }
-    for (int i = tid; i < 624; i += nt) mt[i] = a.state[i];
+    if (tid < 624) mt[tid] = a.state[tid];
     uint32_t pos = a.state[624];
 
     if (n <= a.setsize) {
-        // ---- pool branch: one lane, CPython order ----
+        // ---- pool branch: one lane, CPython order (only while the buffer is tiny) ----
         __syncthreads();
         if (tid == 0) {
             int32_t* pool = a.pool;
@@ -109,8 +99,11 @@ __global__ __launch_bounds__(1024) void k_sample_uniform(SampleArgs a) {
                 do { r = mt_next_serial(mt, pos) >> (32 - bits); } while (r >= m);
                 const int32_t j = pool[r];
                 a.out[i] = j;
-                if (a.phys_out && i >= a.shard_begin && i < a.shard_begin + a.shard_len)
-                    a.phys_out[i - a.shard_begin] = (int32_t)((phys_base + j) % a.capacity);
+                if (a.phys_out && i >= a.shard_begin && i < a.shard_begin + a.shard_len) {
+                    int64_t ps = phys_base + j;
+                    if (ps >= a.capacity) ps -= a.capacity;
+                    a.phys_out[i - a.shard_begin] = (int32_t)ps;
+                }
                 pool[r] = pool[n - i - 1];
             }
             for (int i = 0; i < 624; i++) a.state[i] = mt[i];
@@ -120,55 +113,58 @@ __global__ __launch_bounds__(1024) void k_sample_uniform(SampleArgs a) {
     }
 
     // ---- set branch ----
-    for (int i = tid; i < HS; i += nt) tab[i] = ~0ull;
-    const int bits = bit_length64((uint64_t)n);
-    const uint32_t shift = 32u - (uint32_t)bits;
+    DQNX_STAMP(a.stamps, 1);
+#pragma unroll
+    for (int i = 0; i < HS / NT; i++) tab[tid + i * NT] = ~0ull;
+    const uint32_t shift = 32u - (uint32_t)bit_length64((uint64_t)n);
     int accepted = 0;
-    uint32_t consumed = 0;  // words consumed before the current block (stream position base)
+    uint32_t consumed = 0;   // words consumed before the current MT block (stream position base)
     bool twisted = false;
+    int iter = 0;
     __syncthreads();
     while (true) {
-        if (pos >= 624) {
-            mt_twist_block(mt, tmp);
+        if (pos >= 624) {   // parallel twist: 3 dependency phases (CPython genrand_uint32)
+            if (tid < 624) tmp[tid] = mt[tid];
+            __syncthreads();
+            if (tid < 227) mt[tid] = tmp[tid + 397] ^ mt_mix(tmp[tid], tmp[tid + 1]);
+            __syncthreads();
+            if (tid >= 227 && tid < 454) mt[tid] = mt[tid - 227] ^ mt_mix(tmp[tid], tmp[tid + 1]);
+            __syncthreads();
+            if (tid >= 454 && tid < 623) mt[tid] = mt[tid - 227] ^ mt_mix(tmp[tid], tmp[tid + 1]);
+            if (tid == 623) mt[623] = mt[396] ^ mt_mix(tmp[623], mt[0]);
+            __syncthreads();
             pos = 0;
             twisted = true;
         }
         const int avail = 624 - (int)pos;
         bool valid = false, first = false;
-        uint32_t c = 0, sp = 0;
+        uint32_t c = 0, sp = 0, h = 0;
         if (tid < avail) {
             c = mt_temper(mt[pos + tid]) >> shift;
             sp = consumed + (uint32_t)tid;
             valid = (int64_t)c < n;
-            if (valid) {
+            if (valid) {   // insert (value, stream position); keep the earliest position per value
                 const unsigned long long key = ((unsigned long long)c << 32) | sp;
-                uint32_t h = hash_u32(c) & (HS - 1);
+                h = hash_u32(c) & (HS - 1);
                 while (true) {
-                    unsigned long long cur = tab[h];
-                    if (cur == ~0ull) {
-                        unsigned long long prev = atomicCAS(&tab[h], ~0ull, key);
-                        if (prev == ~0ull) break;
-                        cur = prev;
-                    }
-                    if ((uint32_t)(cur >> 32) == c) { atomicMin(&tab[h], key); break; }
+                    const unsigned long long prev = atomicCAS(&tab[h], ~0ull, key);
+                    if (prev == ~0ull) break;
+                    if ((uint32_t)(prev >> 32) == c) { atomicMin(&tab[h], key); break; }
                     h = (h + 1) & (HS - 1);
                 }
             }
         }
-        if (tid == 0) { s_newpos = -1; }
+        if (tid == 0) s_newpos = -1;
         __syncthreads();
-        if (valid) {
-            uint32_t h = hash_u32(c) & (HS - 1);
-            while ((uint32_t)(tab[h] >> 32) != c) h = (h + 1) & (HS - 1);
-            first = (uint32_t)(tab[h] & 0xffffffffull) == sp;
-        }
+        if (valid) first = (uint32_t)(tab[h] & 0xffffffffull) == sp;   // h = the value's slot
         // block-wide exclusive scan of `first` in thread (= stream) order
         const unsigned long long bal = __ballot(first);
         const int wprefix = __popcll(bal & ((1ull << lane) - 1ull));
         if (lane == 0) wave_cnt[wid] = __popcll(bal);
         __syncthreads();
         int before = 0, total = 0;
-        for (int w = 0; w < nwaves; w++) {
+#pragma unroll
+        for (int w = 0; w < NW; w++) {
             const int cw = wave_cnt[w];
             before += (w < wid) ? cw : 0;
             total += cw;
@@ -177,12 +173,17 @@ __global__ __launch_bounds__(1024) void k_sample_uniform(SampleArgs a) {
             const int r = accepted + before + wprefix;
             if (r < k) {
                 a.out[r] = (int32_t)c;
-                if (a.phys_out && r >= a.shard_begin && r < a.shard_begin + a.shard_len)
-                    a.phys_out[r - a.shard_begin] = (int32_t)((phys_base + (int64_t)c) % a.capacity);
+                if (a.phys_out && r >= a.shard_begin && r < a.shard_begin + a.shard_len) {
+                    int64_t ps = phys_base + (int64_t)c;
+                    if (ps >= a.capacity) ps -= a.capacity;
+                    a.phys_out[r - a.shard_begin] = (int32_t)ps;
+                }
                 if (r == k - 1) s_newpos = (int)pos + tid + 1;
             }
         }
         __syncthreads();
+        DQNX_STAMP(a.stamps, 2 + (iter < 12 ? iter : 12));
+        iter++;
         accepted += total;
         if (accepted >= k) {
             pos = (uint32_t)s_newpos;
@@ -191,10 +192,10 @@ __global__ __launch_bounds__(1024) void k_sample_uniform(SampleArgs a) {
         consumed += (uint32_t)avail;
         pos = 624;
     }
-    if (twisted)
-        for (int i = tid; i < 624; i += nt) a.state[i] = mt[i];
+    (void)iter;
+    if (twisted && tid < 624) a.state[tid] = mt[tid];
     if (tid == 0) a.state[624] = pos;
-    (void)s_done;
+    DQNX_STAMP(a.stamps, 15);
 }
 
 // Logical positions (given by the caller) -> physical ring slots of the local shard.
@@ -238,10 +239,10 @@ int launch_sample_uniform(const SampleArgs& a, hipStream_t s) {
     const int hs = sample_hash_slots(a.k);
     if (hs < 0) return set_error(DQNX_EUNSUPPORTED, "sample: k=%d too large for the LDS table", a.k);
     switch (hs) {
-        case 2048: hipLaunchKernelGGL(k_sample_uniform<2048>, dim3(1), dim3(1024), 0, s, a); break;
-        case 4096: hipLaunchKernelGGL(k_sample_uniform<4096>, dim3(1), dim3(1024), 0, s, a); break;
-        case 8192: hipLaunchKernelGGL(k_sample_uniform<8192>, dim3(1), dim3(1024), 0, s, a); break;
-        default: hipLaunchKernelGGL(k_sample_uniform<16384>, dim3(1), dim3(1024), 0, s, a); break;
+        case 2048: hipLaunchKernelGGL(k_sample_uniform<2048>, dim3(1), dim3(SAMPLE_NT), 0, s, a); break;
+        case 4096: hipLaunchKernelGGL(k_sample_uniform<4096>, dim3(1), dim3(SAMPLE_NT), 0, s, a); break;
+        case 8192: hipLaunchKernelGGL(k_sample_uniform<8192>, dim3(1), dim3(SAMPLE_NT), 0, s, a); break;
+        default: hipLaunchKernelGGL(k_sample_uniform<16384>, dim3(1), dim3(SAMPLE_NT), 0, s, a); break;
     }
     DQNX_HIP_CHECK(hipGetLastError());
     return DQNX_OK;

@@ -11,7 +11,8 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "_lib", "libdqnx.so")
+# DQNX_LIB may point at a diagnostic build (e.g. _lib/libdqnx_stamps.so); default: in-tree build.
+LIB_PATH = os.environ.get("DQNX_LIB") or os.path.join(_HERE, "_lib", "libdqnx.so")
 
 # ---- constants (mirror dqnx.h) --------------------------------------------------------
 DQNX_OK = 0
@@ -52,8 +53,8 @@ class ParamInfo(ctypes.Structure):
 class Config(ctypes.Structure):
     _fields_ = [
         ("net", NetDesc), ("algo", I32), ("batch", I32), ("world_size", I32), ("rank", I32),
-        ("capacity", I64), ("gamma", ctypes.c_float), ("lr", ctypes.c_float), ("beta1", ctypes.c_float),
-        ("beta2", ctypes.c_float), ("adam_eps", ctypes.c_float), ("tau", ctypes.c_float), ("n_env", I32),
+        ("capacity", I64), ("gamma", ctypes.c_double), ("lr", ctypes.c_double), ("beta1", ctypes.c_double),
+        ("beta2", ctypes.c_double), ("adam_eps", ctypes.c_double), ("tau", ctypes.c_double), ("n_env", I32),
         ("reserved0", I32), ("per_eps", ctypes.c_double), ("per_alpha", ctypes.c_double),
         ("per_max_priority", ctypes.c_double), ("per_beta_start", ctypes.c_double),
         ("per_beta_end", ctypes.c_double), ("per_beta_steps", ctypes.c_double),
@@ -77,7 +78,7 @@ EXPORTS = [
     "dqnx_rng_get", "dqnx_learn_step", "dqnx_apply_grads", "dqnx_soft_update", "dqnx_hard_update",
     "dqnx_sample_scratch_bytes", "dqnx_sample_uniform", "dqnx_last_error", "dqnx_abi_version",
     "dqnx_learn_kernel_count", "dqnx_learn_kernel_info", "dqnx_learn_step_timed", "dqnx_events_create",
-    "dqnx_events_destroy", "dqnx_event_elapsed",
+    "dqnx_events_destroy", "dqnx_event_elapsed", "dqnx_debug_stamps",
 ]
 
 _lib = None
@@ -128,6 +129,7 @@ def lib():
         "dqnx_events_destroy": ([I32, P(vp)], ctypes.c_int),
         "dqnx_event_elapsed": ([vp, vp, P(ctypes.c_float)], ctypes.c_int),
         "dqnx_abi_version": ([], I32),
+        "dqnx_debug_stamps": ([vp, P(I64), vp], ctypes.c_int),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)
