@@ -57,6 +57,9 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=15.0)
     p.add_argument("--no-kernel-timing", action="store_true")
+    p.add_argument("--prefetch", action="store_true",
+                   help="overlap the next step's replay sampling with this step's compute on a "
+                        "side stream (measured slower at batch 1024: cross-stream event waits)")
     return p.parse_args()
 
 
@@ -161,13 +164,15 @@ def main():
     random.seed(1234)   # the replay sampler continues CPython's global MT19937 stream
     eng.set_rng(C.DQNX_RNG_PY, np.array(random.getstate()[1], dtype=np.uint32))
 
+    prefetch = args.prefetch
+
     def step():
         if world > 1:
-            eng.learn_step(grads_only=True)
+            eng.learn_step(grads_only=True, prefetch=prefetch)
             dist.all_reduce(eng.grads)
             eng.apply_grads(soft_update=True)
         else:
-            eng.learn_step(soft_update=True)
+            eng.learn_step(soft_update=True, prefetch=prefetch)
 
     for _ in range(args.warmup):
         step()
@@ -192,7 +197,7 @@ def main():
     ms_per_step = el / args.steps * 1e3
     value = Bg * args.steps / el
 
-    # ---- dominant-kernel roofline: HIP events around one kernel inside full steps ----
+    # ---- dominant-kernel roofline: HIP-event-timed graph steps with / without each kernel ----
     roofline = None
     kernels = []
     if not args.no_kernel_timing:
@@ -206,29 +211,42 @@ def main():
             fl, by = ctypes.c_double(), ctypes.c_double()
             C.check(L.dqnx_learn_kernel_info(eng.h, flags, i, nm, 64, ctypes.byref(fl), ctypes.byref(by)), "info")
             infos.append((nm.value.decode(), fl.value, by.value))
-        K = max(args.steps, 20)
-        evs = (ctypes.c_void_p * (2 * K))()
-        C.check(L.dqnx_events_create(2 * K, evs), "events")
+        # consume a pending prefetched minibatch so the timing steps sample themselves
+        if world > 1:
+            eng.learn_step(grads_only=True)
+            dist.all_reduce(eng.grads)
+            eng.apply_grads(soft_update=True)
+        else:
+            eng.learn_step(soft_update=True)
+        K = max(args.steps, 50)
+        stream = eng.stream()
 
-        def timed_steps(ki, count):
-            for j in range(count):
-                C.check(L.dqnx_learn_step_timed(eng.h, flags, ki, evs[2 * j], evs[2 * j + 1], eng.stream()),
-                        "timed step")
-                if world > 1:
-                    dist.all_reduce(eng.grads)
-                    eng.apply_grads(soft_update=True)
+        def graph_steps_ms(omit, count):
+            """`count` graph-launched learn steps with kernel `omit` left out (-1: none),
+            bracketed by HIP events on the engine's stream; ms per step."""
+            C.check(L.dqnx_learn_step_omit(eng.h, flags, omit, stream), "omit step")   # capture
+            t0, t1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             torch.cuda.synchronize()
-            tot = 0.0
-            for j in range(count):
-                ms = ctypes.c_float()
-                C.check(L.dqnx_event_elapsed(evs[2 * j], evs[2 * j + 1], ctypes.byref(ms)), "elapsed")
-                tot += ms.value
-            return tot / count
+            t0.record()
+            for _ in range(count):
+                C.check(L.dqnx_learn_step_omit(eng.h, flags, omit, stream), "omit step")
+            t1.record()
+            t1.synchronize()
+            return t0.elapsed_time(t1) / count
+
+        # a kernel's in-context time per launch = step time with it - step time without it;
+        # full and omitted runs are interleaved and the median of `reps` pairs is kept
+        def kernel_ms(i, count, reps):
+            d = []
+            for _ in range(reps):
+                d.append(graph_steps_ms(-1, count) - graph_steps_ms(i, count))
+            d.sort()
+            return d[len(d) // 2]
 
         for i, (nm, fl, by) in enumerate(infos):
-            kernels.append({"kernel": nm, "avg_us": timed_steps(i, 20) * 1e3, "flops": fl, "bytes": by})
+            kernels.append({"kernel": nm, "avg_us": kernel_ms(i, 50, 3) * 1e3, "flops": fl, "bytes": by})
         dom = max(range(len(kernels)), key=lambda i: kernels[i]["avg_us"])
-        avg_ms = timed_steps(dom, K)
+        avg_ms = kernel_ms(dom, K, 5)
         kernels[dom]["avg_us"] = avg_ms * 1e3
         nm, fl, by = infos[dom]
         intensity = fl / by if by else 0.0
@@ -250,7 +268,6 @@ def main():
             roofline = {"bound": "hbm", "achieved": ach, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                         "frac": ach / PEAK_HBM_GBS, "traffic": traffic, "kernel": nm,
                         "avg_us": avg_ms * 1e3, "algorithmic_flops": fl, "algorithmic_bytes": by}
-        C.check(L.dqnx_events_destroy(2 * K, evs), "events_destroy")
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -277,7 +294,7 @@ def main():
                 "workload": "configs[1]: synthetic 1ramp_1x3 state vectors, MLP Q-net fp32, GPU replay buffer",
                 "algo": args.algo, "net": f"MLP({args.obs_dim}->256->128, ReLU) + dueling head A={args.actions}",
                 "batch_per_gpu": args.batch, "global_batch": Bg, "replay_capacity": args.capacity,
-                "parallelism": f"dp{world}", "graphs": not args.no_graphs,
+                "parallelism": f"dp{world}", "graphs": not args.no_graphs, "prefetch_sampling": prefetch,
             },
             "roofline": roofline,
             "cpu_baseline": cpu,

@@ -158,7 +158,8 @@ enum dqnx_buffer {
     DQNX_BUF_RING_REW,         /* [capacity] fp32 */
     DQNX_BUF_RING_DONE,        /* [capacity] fp32 (0/1) */
     DQNX_BUF_SUMTREE,          /* [2*capacity-1] fp64 (PER only, else 0 bytes) */
-    DQNX_BUF_BATCH_IDX,        /* [batch] int32: sampled logical replay positions / tree leaves */
+    DQNX_BUF_BATCH_IDX,        /* [2][batch] int32: sampled logical replay positions / tree leaves;
+                                  slot 0 unless DQNX_STEP_PREFETCH alternates the slots */
     DQNX_BUF_Q,                /* [3][batch_local][n_actions] fp32: Q online(s), online(s'), target(s') */
     DQNX_BUF_TD,               /* [3][batch_local] fp32: targets y, q(s,a), |y - q(s,a)| */
     DQNX_BUF_IS_WEIGHTS,       /* [batch] fp32 PER importance weights */
@@ -203,6 +204,13 @@ int dqnx_rng_get(dqnx_engine* e, int32_t which, uint32_t* state625, void* stream
 #define DQNX_STEP_SOFT_UPDATE 0x1   /* fuse the tau soft update into the Adam pass */
 #define DQNX_STEP_GIVEN_INDICES 0x2 /* skip sampling: use DQNX_BUF_BATCH_IDX as written by caller */
 #define DQNX_STEP_GRADS_ONLY 0x4    /* stop after writing DQNX_BUF_GRADS (DP: all-reduce, then apply) */
+#define DQNX_STEP_PREFETCH 0x8      /* pure learning loops: also draw the NEXT step's minibatch on a
+                                       forked graph branch, overlapped with this step's compute.
+                                       Results are bit-identical to sequential steps; while a
+                                       prefetched minibatch is pending, dqnx_replay_push and
+                                       dqnx_rng_set return DQNX_ESTATE and dqnx_rng_get already
+                                       reflects the prefetched draw.  A step without the flag
+                                       consumes the pending minibatch. */
 int dqnx_learn_step(dqnx_engine* e, int32_t flags, void* stream);
 /* Adam (+ optional soft update) from DQNX_BUF_GRADS: second half of a GRADS_ONLY step. */
 int dqnx_apply_grads(dqnx_engine* e, int32_t flags, void* stream);
@@ -220,6 +228,11 @@ int dqnx_learn_kernel_info(dqnx_engine* e, int32_t flags, int32_t index, char* n
                            double* algorithmic_flops, double* algorithmic_bytes);
 int dqnx_learn_step_timed(dqnx_engine* e, int32_t flags, int32_t kernel_index, void* ev_start, void* ev_stop,
                           void* stream);
+/* Timing aid (bench.py roofline): one learn step, graph-launched, with kernel
+ * `omit_index` (as numbered by dqnx_learn_kernel_info; -1 = none) left out.  Engine state
+ * afterwards is meant for timing only. */
+int dqnx_learn_step_omit(dqnx_engine* e, int32_t flags, int32_t omit_index, void* stream);
+
 int dqnx_events_create(int32_t n, void** events);      /* hipEventCreate x n */
 int dqnx_events_destroy(int32_t n, void** events);
 int dqnx_event_elapsed(void* start, void* stop, float* ms);   /* synchronises `stop` */

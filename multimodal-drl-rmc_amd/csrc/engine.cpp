@@ -4,11 +4,13 @@
 #include <math.h>
 #include <stdarg.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <cmath>
 #include <functional>
 #include <map>
+#include <tuple>
 #include <string>
 #include <vector>
 
@@ -155,6 +157,16 @@ struct dqnx_engine {
     std::map<int, hipGraphExec_t> graph_cache;
     hipStream_t capture_stream = nullptr;
     std::map<int, std::vector<KStep>> steps_cache;
+    std::map<std::tuple<int, int, void*, void*>, hipGraphExec_t> timed_cache;
+    hipStream_t side_stream = nullptr;
+    hipEvent_t fork_ev = nullptr, join_ev = nullptr;
+    hipEvent_t ev_sampled[2] = {nullptr, nullptr}, ev_computed[2] = {nullptr, nullptr};
+    bool pf_computed_valid[2] = {false, false};
+    // backward plan: 0 = split-K backward levels + Adam pass (default, fastest measured at
+    // batch 1024); 1 = head kernel also makes dZ_{L-1}, one full-K dW + Adam launch
+    int bwd_plan = 0;
+    bool pf_valid = false;   // a prefetched minibatch for the next step sits in slot pf_slot
+    int pf_slot = 0;
 };
 
 namespace {
@@ -192,7 +204,7 @@ int layout(dqnx_engine* e) {
     region(DQNX_BUF_RING_REW, cap * 4);
     region(DQNX_BUF_RING_DONE, cap * 4);
     region(DQNX_BUF_SUMTREE, c.algo == DQNX_ALGO_PER_DOUBLE ? (2 * cap - 1) * 8 : 0);
-    region(DQNX_BUF_BATCH_IDX, (uint64_t)e->Bg * 4);
+    region(DQNX_BUF_BATCH_IDX, (uint64_t)2 * e->Bg * 4);   // [slot][Bg]: slot 1 is the prefetch buffer
     region(DQNX_BUF_Q, (uint64_t)3 * e->Bl * A * 4);
     region(DQNX_BUF_TD, (uint64_t)3 * e->Bl * 4);
     region(DQNX_BUF_IS_WEIGHTS, (uint64_t)e->Bg * 4);
@@ -205,7 +217,7 @@ int layout(dqnx_engine* e) {
         cur += nbytes;
         return o;
     };
-    e->ws_phys = sub((uint64_t)e->Bl * 4);
+    e->ws_phys = sub((uint64_t)2 * e->Bl * 4);
     e->ws_pool = sub((uint64_t)(e->setsize + 64) * 4);
     e->ws_xobs = sub((uint64_t)e->Bl * e->stride * 4);
     e->ws_H.assign(L, 0);
@@ -243,7 +255,10 @@ int check_bound(const dqnx_engine* e) {
 // and timed on its own (dqnx_learn_step_timed).
 
 
-std::vector<KStep> build_learn_steps(dqnx_engine* e, int flags) {
+// key = flags | (slot << 8): `slot` selects the (sampled indices, physical rows) buffer pair.
+std::vector<KStep> build_learn_steps(dqnx_engine* e, int key) {
+    const int flags = key & 0xff;
+    const int slot = (key >> 8) & 1;
     std::vector<KStep> ks;
     const dqnx_config& c = e->cfg;
     const NetPlan& np = e->np;
@@ -253,8 +268,8 @@ std::vector<KStep> build_learn_steps(dqnx_engine* e, int flags) {
     dqnx_ctrl* ctrl = ctrl_of(e);
     float* params = at<float>(e, e->off[DQNX_BUF_PARAMS]);
     float* tparams = at<float>(e, e->off[DQNX_BUF_TARGET_PARAMS]);
-    int32_t* idx = at<int32_t>(e, e->off[DQNX_BUF_BATCH_IDX]);
-    int32_t* phys = at<int32_t>(e, e->ws_phys);
+    int32_t* idx = at<int32_t>(e, e->off[DQNX_BUF_BATCH_IDX]) + (size_t)slot * e->Bg;
+    int32_t* phys = at<int32_t>(e, e->ws_phys) + (size_t)slot * e->Bl;
     const double Bl = e->Bl;
 
     // 1. sample (R:dqn/replay_memory.py:38-39)
@@ -354,6 +369,12 @@ std::vector<KStep> build_learn_steps(dqnx_engine* e, int flags) {
         ha.td = at<float>(e, e->off[DQNX_BUF_TD]);
         ha.dZ = at<float>(e, e->ws_dZ[L - 1]);
         ha.dhead = at<float>(e, e->ws_dhead);
+        if (L >= 2 && e->bwd_plan == 1) {
+            ha.W_last = params + np.dense[L - 1].off;
+            ha.Hprev = at<float>(e, e->ws_H[L - 2]);
+            ha.dZprev = at<float>(e, e->ws_dZ[L - 2]);
+            ha.in_prev = np.dense[L - 1].in;
+        }
         ha.loss_partial = at<float>(e, e->ws_loss_part);
         ha.ctrl = ctrl;
         ha.beta1 = (float)c.beta1;
@@ -370,6 +391,7 @@ std::vector<KStep> build_learn_steps(dqnx_engine* e, int flags) {
         ks.push_back(k);
     }
 
+    if (e->bwd_plan == 0) {
     // 4. backward levels L..1: dX of the level below + split-K dW of this level
     //    (level L also computes the head-weight gradient from the head kernel's dHead)
     for (int l = L - 1; l >= 0; l--) {
@@ -482,6 +504,106 @@ std::vector<KStep> build_learn_steps(dqnx_engine* e, int flags) {
         k.run = [=](hipStream_t s) { return launch_adam(aa, s); };
         ks.push_back(k);
     }
+    } else {
+    // 4. dZ of levels below L-1 (deeper MLPs only; the head kernel produced dZ_L and dZ_{L-1})
+    for (int l = L - 2; l >= 1; l--) {
+        const LayerPlan lp = np.dense[l];
+        BwdArgs ba;
+        memset(&ba, 0, sizeof(ba));
+        ba.dZ = at<float>(e, e->ws_dZ[l]);
+        ba.Bl = e->Bl;
+        ba.in = lp.in;
+        ba.out = lp.out;
+        ba.W = params + lp.off;
+        ba.Hprev = at<float>(e, e->ws_H[l - 1]);
+        ba.ldh = lp.in;
+        ba.dZprev = at<float>(e, e->ws_dZ[l - 1]);
+        ba.ndw = 0;
+        ba.dw_slices = 1;
+        ba.kslice = e->Bl;
+        bwd_level_grid(ba);
+        KStep k;
+        k.name = "linear_dx_l" + std::to_string(l + 1);
+        k.flops = 2.0 * Bl * lp.out * lp.in;
+        k.bytes = 4.0 * (Bl * lp.out + lp.out * (double)lp.in + 2.0 * Bl * lp.in);
+        k.run = [=](hipStream_t s) { return launch_bwd_level(ba, act, s); };
+        ks.push_back(k);
+    }
+
+    // 5. all weight gradients (full minibatch per tile) + Adam (+ soft update) in one launch
+    {
+        DwAdamArgs da;
+        memset(&da, 0, sizeof(da));
+        double flops = 0, bytes = 0;
+        for (int l = 0; l < L; l++) {
+            const LayerPlan lp = np.dense[l];
+            DwAdamProblem& d = da.pr[da.npr++];
+            d.dZ = at<float>(e, e->ws_dZ[l]);
+            d.ldz = lp.out;
+            if (l > 0) {
+                d.X = at<float>(e, e->ws_H[l - 1]);   // stream 0 rows
+                d.ldx = lp.in;
+            } else {
+                d.X = at<float>(e, e->ws_xobs);
+                d.ldx = e->stride;
+            }
+            d.in = lp.in;
+            d.out = lp.out;
+            d.poff = lp.off;
+            d.head_kind = -1;
+            flops += 2.0 * Bl * lp.out * (lp.in + 1.0);
+            bytes += 4.0 * Bl * (lp.out + lp.in);
+        }
+        {
+            DwAdamProblem& d = da.pr[da.npr++];
+            d.dZ = at<float>(e, e->ws_dhead);
+            d.ldz = 16;
+            d.X = at<float>(e, e->ws_H[L - 1]);
+            d.ldx = np.F;
+            d.in = np.F;
+            d.out = np.NH;
+            d.poff = np.head_off;
+            d.head_kind = c.net.head;
+            d.A = A;
+            flops += 2.0 * Bl * np.NH * (np.F + 1.0);
+            bytes += 4.0 * Bl * (16.0 + np.F);
+        }
+        dw_adam_grid(da);
+        da.Bl = e->Bl;
+        da.mode = (flags & DQNX_STEP_GRADS_ONLY) ? 0 : 1;
+        da.soft = (flags & DQNX_STEP_SOFT_UPDATE) ? 1 : 0;
+        da.n_params = np.P;
+        da.p = params;
+        da.m = at<float>(e, e->off[DQNX_BUF_ADAM_M]);
+        da.v = at<float>(e, e->off[DQNX_BUF_ADAM_V]);
+        da.grads = at<float>(e, e->off[DQNX_BUF_GRADS]);
+        da.target = tparams;
+        da.ctrl = ctrl;
+        da.w1 = (float)(1.0 - c.beta1);          // Python: exp_avg.lerp_(grad, 1 - beta1)
+        da.beta2 = (float)c.beta2;
+        da.c2 = (float)(1.0 - c.beta2);
+        da.eps = (float)c.adam_eps;
+        da.tau = (float)(c.tau * c.n_env);
+        da.one_minus_tau = (float)(1.0 - c.tau * c.n_env);
+        da.adam_table = at<float>(e, e->ws_adam_tab);
+        da.adam_table_len = kAdamTable;
+        da.beta1d = c.beta1;
+        da.beta2d = c.beta2;
+        da.lrd = c.lr;
+        da.loss_partial = at<float>(e, e->ws_loss_part);
+        da.n_loss_partial = e->tiles;
+        da.batch_global = e->Bg;
+        const double P = (double)np.P;
+        bytes += 4.0 * (P + (da.mode ? 6.0 * P + (da.soft ? 2.0 * P : 0.0) : 0.0));
+        flops += da.mode ? 12.0 * P : 0.0;
+        KStep k;
+        k.name = da.mode ? "dw_adam" : "dw_grads";
+        k.flops = flops;
+        k.bytes = bytes;
+        k.run = [=](hipStream_t s) { return launch_dw_adam(da, s); };
+        ks.push_back(k);
+    }
+    }
     return ks;
 }
 
@@ -522,26 +644,34 @@ int enqueue_apply(dqnx_engine* e, int flags, hipStream_t s) {
     return launch_adam(aa, s);
 }
 
+// Capture `fn` (enqueueing on the given stream) into an executable graph.
+template <class Fn>
+int capture(dqnx_engine* e, Fn fn, hipGraphExec_t* out) {
+    if (!e->capture_stream) DQNX_HIP_CHECK(hipStreamCreateWithFlags(&e->capture_stream, hipStreamNonBlocking));
+    DQNX_HIP_CHECK(hipStreamBeginCapture(e->capture_stream, hipStreamCaptureModeThreadLocal));
+    int rc = fn(e->capture_stream);
+    hipGraph_t graph = nullptr;
+    hipError_t ce = hipStreamEndCapture(e->capture_stream, &graph);
+    if (rc) {
+        if (graph) (void)hipGraphDestroy(graph);
+        return rc;
+    }
+    if (ce != hipSuccess) return set_hip_error(ce, "hipStreamEndCapture", __FILE__, __LINE__);
+    hipError_t ie = hipGraphInstantiate(out, graph, nullptr, nullptr, 0);
+    (void)hipGraphDestroy(graph);
+    if (ie != hipSuccess) return set_hip_error(ie, "hipGraphInstantiate", __FILE__, __LINE__);
+    return DQNX_OK;
+}
+
 // Capture `fn` into a graph once per key, then replay on the caller's stream.
 template <class Fn>
 int run_graphed(dqnx_engine* e, int key, hipStream_t s, Fn fn) {
     if (!e->graphs) return fn(s);
     auto it = e->graph_cache.find(key);
     if (it == e->graph_cache.end()) {
-        if (!e->capture_stream) DQNX_HIP_CHECK(hipStreamCreateWithFlags(&e->capture_stream, hipStreamNonBlocking));
-        DQNX_HIP_CHECK(hipStreamBeginCapture(e->capture_stream, hipStreamCaptureModeThreadLocal));
-        int rc = fn(e->capture_stream);
-        hipGraph_t graph = nullptr;
-        hipError_t ce = hipStreamEndCapture(e->capture_stream, &graph);
-        if (rc) {
-            if (graph) (void)hipGraphDestroy(graph);
-            return rc;
-        }
-        if (ce != hipSuccess) return set_hip_error(ce, "hipStreamEndCapture", __FILE__, __LINE__);
         hipGraphExec_t exec = nullptr;
-        hipError_t ie = hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0);
-        (void)hipGraphDestroy(graph);
-        if (ie != hipSuccess) return set_hip_error(ie, "hipGraphInstantiate", __FILE__, __LINE__);
+        int rc = capture(e, fn, &exec);
+        if (rc) return rc;
         it = e->graph_cache.emplace(key, exec).first;
     }
     DQNX_HIP_CHECK(hipGraphLaunch(it->second, s));
@@ -551,6 +681,8 @@ int run_graphed(dqnx_engine* e, int key, hipStream_t s, Fn fn) {
 void drop_graphs(dqnx_engine* e) {
     for (auto& kv : e->graph_cache) (void)hipGraphExecDestroy(kv.second);
     e->graph_cache.clear();
+    for (auto& kv : e->timed_cache) (void)hipGraphExecDestroy(kv.second);
+    e->timed_cache.clear();
     e->steps_cache.clear();
 }
 
@@ -633,6 +765,7 @@ int dqnx_engine_create(const dqnx_config* cfg, dqnx_engine** out) {
     for (size_t l = 0; l < e->np.dense.size(); l++)
         if (e->np.dense[l].out % 4) { delete e; return set_error(DQNX_EUNSUPPORTED, "hidden widths must be multiples of 4"); }
     if (sample_hash_slots(c.batch) < 0) { delete e; return set_error(DQNX_EUNSUPPORTED, "batch too large for the sampler"); }
+    if (const char* bp = getenv("DQNX_BWD_PLAN")) e->bwd_plan = atoi(bp) == 1 ? 1 : 0;
     e->Bg = c.batch;
     e->Bl = c.batch / c.world_size;
     e->shard_begin = c.rank * e->Bl;
@@ -660,6 +793,16 @@ int dqnx_engine_destroy(dqnx_engine* e) {
     if (!e) return DQNX_OK;
     drop_graphs(e);
     if (e->capture_stream) (void)hipStreamDestroy(e->capture_stream);
+    if (e->side_stream) {
+        (void)hipStreamSynchronize(e->side_stream);
+        (void)hipStreamDestroy(e->side_stream);
+    }
+    for (int i = 0; i < 2; i++) {
+        if (e->ev_sampled[i]) (void)hipEventDestroy(e->ev_sampled[i]);
+        if (e->ev_computed[i]) (void)hipEventDestroy(e->ev_computed[i]);
+    }
+    if (e->fork_ev) (void)hipEventDestroy(e->fork_ev);
+    if (e->join_ev) (void)hipEventDestroy(e->join_ev);
     delete e;
     return DQNX_OK;
 }
@@ -733,6 +876,7 @@ int dqnx_engine_reset(dqnx_engine* e, void* stream) {
     }
     e->ring_size = 0;
     e->ring_wptr = 0;
+    e->pf_valid = false;
     return DQNX_OK;
 }
 
@@ -743,6 +887,7 @@ int dqnx_replay_push(dqnx_engine* e, const float* obs, const int32_t* act, const
     if (n < 0 || (n > 0 && (!obs || !act || !rew || !done || !next_obs)))
         return set_error(DQNX_EINVAL, "dqnx_replay_push: bad argument");
     if (e->cfg.algo == DQNX_ALGO_PER_DOUBLE) return set_error(DQNX_EUNSUPPORTED, "PER push not built yet");
+    if (e->pf_valid) return set_error(DQNX_ESTATE, "replay push while a prefetched minibatch is pending");
     hipStream_t s = (hipStream_t)stream;
     const int D = e->cfg.net.obs_dim;
     int done_rows = 0;
@@ -818,6 +963,7 @@ int dqnx_rng_set(dqnx_engine* e, int32_t which, const uint32_t* state625, void* 
     if (rc) return rc;
     if (!state625 || (which != DQNX_RNG_PY && which != DQNX_RNG_NP)) return set_error(DQNX_EINVAL, "bad argument");
     if (state625[624] > 624) return set_error(DQNX_EINVAL, "MT index must be <= 624");
+    if (e->pf_valid) return set_error(DQNX_ESTATE, "rng_set while a prefetched minibatch is pending");
     hipStream_t s = (hipStream_t)stream;
     uint32_t* dst = which == DQNX_RNG_PY ? ctrl_of(e)->py_mt : ctrl_of(e)->np_mt;
     DQNX_HIP_CHECK(hipMemcpyAsync(dst, state625, 625 * 4, hipMemcpyHostToDevice, s));
@@ -831,20 +977,78 @@ int dqnx_rng_get(dqnx_engine* e, int32_t which, uint32_t* state625, void* stream
     if (!state625 || (which != DQNX_RNG_PY && which != DQNX_RNG_NP)) return set_error(DQNX_EINVAL, "bad argument");
     hipStream_t s = (hipStream_t)stream;
     const uint32_t* src = which == DQNX_RNG_PY ? ctrl_of(e)->py_mt : ctrl_of(e)->np_mt;
+    if (e->pf_valid) DQNX_HIP_CHECK(hipStreamWaitEvent(s, e->ev_sampled[e->pf_slot], 0));
     DQNX_HIP_CHECK(hipMemcpyAsync(state625, src, 625 * 4, hipMemcpyDeviceToHost, s));
     DQNX_HIP_CHECK(hipStreamSynchronize(s));
     return DQNX_OK;
 }
 
+// Prefetch pipeline (DQNX_STEP_PREFETCH): the sampler runs on the engine's side stream,
+// one step ahead, into the other (idx, phys) slot.  Ordering, all by events:
+//   side: wait computed[nxt] (step t-1 read slot nxt) -> sample(t+1) into nxt -> sampled[nxt]
+//   main: wait sampled[cur] -> compute(t) on slot cur -> computed[cur]
+// The sampler is the only writer of ctrl->py_mt and the slots, so results are bit-identical
+// to sequential steps.
+static int pf_events(dqnx_engine* e) {
+    if (!e->side_stream) DQNX_HIP_CHECK(hipStreamCreateWithFlags(&e->side_stream, hipStreamNonBlocking));
+    for (int i = 0; i < 2; i++) {
+        if (!e->ev_sampled[i]) DQNX_HIP_CHECK(hipEventCreateWithFlags(&e->ev_sampled[i], hipEventDisableTiming));
+        if (!e->ev_computed[i]) DQNX_HIP_CHECK(hipEventCreateWithFlags(&e->ev_computed[i], hipEventDisableTiming));
+    }
+    if (!e->fork_ev) DQNX_HIP_CHECK(hipEventCreateWithFlags(&e->fork_ev, hipEventDisableTiming));
+    return DQNX_OK;
+}
+
+static int pf_sample(dqnx_engine* e, int base, int slot) {
+    const std::vector<KStep>& ks = steps_for(e, base | (slot << 8));
+    return run_graphed(e, 0x10000 | (slot << 8), e->side_stream,
+                       [&](hipStream_t cs) { return enqueue_range(ks, 0, 1, cs); });
+}
+
 int dqnx_learn_step(dqnx_engine* e, int32_t flags, void* stream) {
     int rc = check_bound(e);
     if (rc) return rc;
-    if (e->ring_size < e->Bg && !(flags & DQNX_STEP_GIVEN_INDICES))
+    hipStream_t s = (hipStream_t)stream;
+    const bool prefetch = (flags & DQNX_STEP_PREFETCH) && !(flags & DQNX_STEP_GIVEN_INDICES);
+    if (e->ring_size < e->Bg && !(flags & DQNX_STEP_GIVEN_INDICES) && !e->pf_valid)
         return set_error(DQNX_EINVAL, "Sample larger than population: %lld < %d", (long long)e->ring_size, e->Bg);
-    const int key = flags & (DQNX_STEP_SOFT_UPDATE | DQNX_STEP_GIVEN_INDICES | DQNX_STEP_GRADS_ONLY);
-    const std::vector<KStep>& ks = steps_for(e, key);
-    return run_graphed(e, key, (hipStream_t)stream,
-                       [&](hipStream_t s) { return enqueue_range(ks, 0, (int)ks.size(), s); });
+    const int base = flags & (DQNX_STEP_SOFT_UPDATE | DQNX_STEP_GIVEN_INDICES | DQNX_STEP_GRADS_ONLY);
+    if (!prefetch && !e->pf_valid) {
+        const std::vector<KStep>& ks = steps_for(e, base);
+        return run_graphed(e, base, s, [&](hipStream_t cs) { return enqueue_range(ks, 0, (int)ks.size(), cs); });
+    }
+    rc = pf_events(e);
+    if (rc) return rc;
+    if (!e->pf_valid) {   // prologue: this step's minibatch, ordered after everything on s
+        DQNX_HIP_CHECK(hipEventRecord(e->fork_ev, s));
+        DQNX_HIP_CHECK(hipStreamWaitEvent(e->side_stream, e->fork_ev, 0));
+        rc = pf_sample(e, base, 0);
+        if (rc) return rc;
+        DQNX_HIP_CHECK(hipEventRecord(e->ev_sampled[0], e->side_stream));
+        e->pf_slot = 0;
+        e->pf_valid = true;
+        e->pf_computed_valid[0] = e->pf_computed_valid[1] = false;
+    }
+    const int cur = e->pf_slot, nxt = cur ^ 1;
+    // compute this step on slot `cur`
+    DQNX_HIP_CHECK(hipStreamWaitEvent(s, e->ev_sampled[cur], 0));
+    const std::vector<KStep>& ks = steps_for(e, base | (cur << 8));
+    rc = run_graphed(e, base | (cur << 8) | 0x20000, s,
+                     [&](hipStream_t cs) { return enqueue_range(ks, 1, (int)ks.size(), cs); });
+    if (rc) return rc;
+    DQNX_HIP_CHECK(hipEventRecord(e->ev_computed[cur], s));
+    e->pf_computed_valid[cur] = true;
+    if (!prefetch) {   // consumed the pending minibatch; nothing drawn ahead
+        e->pf_valid = false;
+        return DQNX_OK;
+    }
+    // draw the next step's minibatch into slot `nxt` once step t-1 no longer reads it
+    if (e->pf_computed_valid[nxt]) DQNX_HIP_CHECK(hipStreamWaitEvent(e->side_stream, e->ev_computed[nxt], 0));
+    rc = pf_sample(e, base, nxt);
+    if (rc) return rc;
+    DQNX_HIP_CHECK(hipEventRecord(e->ev_sampled[nxt], e->side_stream));
+    e->pf_slot = nxt;
+    return DQNX_OK;
 }
 
 int dqnx_learn_kernel_count(dqnx_engine* e, int32_t flags, int32_t* n) {
@@ -872,6 +1076,7 @@ int dqnx_learn_step_timed(dqnx_engine* e, int32_t flags, int32_t kernel_index, v
     int rc = check_bound(e);
     if (rc) return rc;
     if (!ev_start || !ev_stop) return set_error(DQNX_EINVAL, "null event");
+    if (e->pf_valid) return set_error(DQNX_ESTATE, "timed step with a prefetched minibatch pending");
     if (e->ring_size < e->Bg && !(flags & DQNX_STEP_GIVEN_INDICES))
         return set_error(DQNX_EINVAL, "Sample larger than population: %lld < %d", (long long)e->ring_size, e->Bg);
     const int key = flags & 7;
@@ -879,20 +1084,40 @@ int dqnx_learn_step_timed(dqnx_engine* e, int32_t flags, int32_t kernel_index, v
     const int n = (int)ks.size();
     if (kernel_index < 0 || kernel_index >= n) return set_error(DQNX_EINVAL, "kernel index out of range");
     hipStream_t s = (hipStream_t)stream;
-    const int base = key | (kernel_index << 12);
-    if (kernel_index > 0) {
-        rc = run_graphed(e, base | (1 << 8), s, [&](hipStream_t cs) { return enqueue_range(ks, 0, kernel_index, cs); });
-        if (rc) return rc;
-    }
+    // eager launches (HIP cannot time events recorded inside a graph); the caller enqueues
+    // many steps before reading the events, so the host runs ahead of the GPU and the event
+    // pair brackets the kernel alone
+    rc = enqueue_range(ks, 0, kernel_index, s);
+    if (rc) return rc;
     DQNX_HIP_CHECK(hipEventRecord((hipEvent_t)ev_start, s));
-    rc = run_graphed(e, base | (2 << 8), s,
-                     [&](hipStream_t cs) { return enqueue_range(ks, kernel_index, kernel_index + 1, cs); });
+    rc = enqueue_range(ks, kernel_index, kernel_index + 1, s);
     if (rc) return rc;
     DQNX_HIP_CHECK(hipEventRecord((hipEvent_t)ev_stop, s));
-    if (kernel_index + 1 < n)
-        rc = run_graphed(e, base | (3 << 8), s,
-                         [&](hipStream_t cs) { return enqueue_range(ks, kernel_index + 1, n, cs); });
-    return rc;
+    return enqueue_range(ks, kernel_index + 1, n, s);
+}
+
+// Timing aid: one learn step as a graph with kernel `omit_index` left out (-1: none).  The
+// difference of event-timed runs with and without a kernel is that kernel's in-context
+// cost per launch (bench.py roofline).  The omitted kernel's outputs are stale, so the
+// engine state afterwards is for timing only.
+int dqnx_learn_step_omit(dqnx_engine* e, int32_t flags, int32_t omit_index, void* stream) {
+    int rc = check_bound(e);
+    if (rc) return rc;
+    if (e->pf_valid) return set_error(DQNX_ESTATE, "timing step with a prefetched minibatch pending");
+    if (e->ring_size < e->Bg && !(flags & DQNX_STEP_GIVEN_INDICES))
+        return set_error(DQNX_EINVAL, "Sample larger than population: %lld < %d", (long long)e->ring_size, e->Bg);
+    const int base = flags & 7;
+    const std::vector<KStep>& ks = steps_for(e, base);
+    const int n = (int)ks.size();
+    if (omit_index < -1 || omit_index >= n) return set_error(DQNX_EINVAL, "kernel index out of range");
+    return run_graphed(e, base | 0x40000 | ((omit_index + 1) << 20), (hipStream_t)stream, [&](hipStream_t cs) {
+        for (int i = 0; i < n; i++) {
+            if (i == omit_index) continue;
+            int r = ks[i].run(cs);
+            if (r) return r;
+        }
+        return (int)DQNX_OK;
+    });
 }
 
 int dqnx_events_create(int32_t n, void** events) {

@@ -88,7 +88,9 @@ struct Engine {
 // replay ring through the sampled physical slots (no materialised minibatch), and
 // stream 0's first column tile also writes the gathered rows to `xcopy` for layer-1 dW.
 // =====================================================================================
-template <int ACT, bool VECB>
+// GATHER: first layer (operand rows gathered from the replay ring through the sampled
+// physical rows); hidden layers read the previous activation rows in order.
+template <int ACT, bool VECB, bool GATHER>
 __global__ __launch_bounds__(256) void k_linear_fwd(FwdArgs args) {
     using E = Engine<FWD_BM, FWD_BN, DQNX_FWD_KT, DQNX_FWD_WM, L_ROWS_K, L_ROWS_K, true, VECB>;
     constexpr int TM = E::TM, TN = E::TN;
@@ -111,7 +113,7 @@ __global__ __launch_bounds__(256) void k_linear_fwd(FwdArgs args) {
         const int col = n0 + E::co() + tn * 16 + i;
         bias[tn] = col < N ? P.bias[col] : 0.f;
     }
-    Operand A{P.A, P.lda, P.phys, M, Kpad, -1, (P.xcopy && tn_ == 0) ? P.xcopy : nullptr, P.lda};
+    Operand A{P.A, P.lda, GATHER ? P.phys : nullptr, M, Kpad, -1, (GATHER && P.xcopy && tn_ == 0) ? P.xcopy : nullptr, P.lda};
     Operand B{P.W, K, nullptr, N, K, -1, nullptr, 0};
     floatx4 acc[TM][TN];
     E::G::run(lds, A, B, m0, n0, 0, Kpad, acc);
@@ -426,6 +428,41 @@ __global__ __launch_bounds__(256) void k_head(HeadArgs a) {
         for (int b = 0; b < TS; b++) s += lossv[b];
         a.loss_partial[blockIdx.x] = s;
     }
+    // (6) dZ_{L-1} = (dZ_L W_L) (.) act'(H_{L-1}) for this tile's samples: [TS x in_prev], K = F.
+    //     The tile's dZ_L rows were just stored by this workgroup (never cached before: no
+    //     stale L1 lines); the block fence + barrier order them before the reads.
+    if (a.dZprev) {
+        using GP = TileGemm<16, 256, 32, 1, 4, L_ROWS_K, L_K_ROWS, true, true>;
+        __shared__ __attribute__((aligned(16))) float lds2[GP::LDS_FLOATS];
+        __threadfence_block();
+        __syncthreads();
+        Operand Ao{a.dZ, F, nullptr, Bl, F, -1, nullptr, 0};
+        Operand Bo{a.W_last, a.in_prev, nullptr, a.in_prev, F, -1, nullptr, 0};
+        for (int n0 = 0; n0 < a.in_prev; n0 += 256) {
+            float hm[GP::TN][4];   // mask operands fetched before the GEMM
+#pragma unroll
+            for (int tn = 0; tn < GP::TN; tn++)
+#pragma unroll
+                for (int r = 0; r < 4; r++) {
+                    const int col = n0 + (wid * GP::TN + tn) * 16 + i, b = 4 * g + r;
+                    hm[tn][r] = (col < a.in_prev && b < nb) ? a.Hprev[(int64_t)(b0 + b) * a.in_prev + col] : 0.f;
+                }
+            floatx4 acc2[GP::TM][GP::TN];
+            GP::run(lds2, Ao, Bo, b0, n0, 0, F, acc2);
+#pragma unroll
+            for (int tn = 0; tn < GP::TN; tn++) {
+                const int col = n0 + (wid * GP::TN + tn) * 16 + i;
+                if (col >= a.in_prev) continue;
+#pragma unroll
+                for (int r = 0; r < 4; r++) {
+                    const int b = 4 * g + r;
+                    if (b < nb)
+                        a.dZprev[(int64_t)(b0 + b) * a.in_prev + col] = act_bwd<ACT>(acc2[0][tn][r], hm[tn][r]);
+                }
+            }
+            __syncthreads();
+        }
+    }
     // Adam step counter of this learn step (read by the Adam pass, a later launch)
     if (blockIdx.x == 0 && tid == 128 && a.ctrl) a.ctrl->adam_step = a.ctrl->adam_step + 1;
     DQNX_STAMP(a.stamps, 20);
@@ -443,32 +480,9 @@ __global__ __launch_bounds__(256) void k_head(HeadArgs a) {
 __global__ __launch_bounds__(256) void k_adam(AdamArgs a) {
     const int64_t P = a.n_params;
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < P; e += stride) {
-        float gsum;
-        if (a.mode == 2) {
-            gsum = a.grads[e];
-        } else {
-            int sgi = 0;
-#pragma unroll 1
-            for (int q = 1; q < a.nseg; q++)
-                if (e >= a.seg[q].off) sgi = q;
-            const AdamSegment sg = a.seg[sgi];
-            const float* pp = sg.partial + (e - sg.off);
-            // fixed-order sum of the slabs; loads issued 8 at a time before the adds
-            gsum = 0.f;
-            for (int s0 = 0; s0 < sg.S; s0 += 8) {
-                float v[8];
-#pragma unroll
-                for (int u = 0; u < 8; u++) v[u] = (s0 + u < sg.S) ? pp[(int64_t)(s0 + u) * sg.pstride] : 0.f;
-#pragma unroll
-                for (int u = 0; u < 8; u++)
-                    if (s0 + u < sg.S) gsum = (s0 + u == 0) ? v[u] : gsum + v[u];
-            }
-            a.grads[e] = gsum;
-        }
-        if (a.mode == 0) continue;
+    float step_size = 0.f, bc2s = 1.f;
+    if (a.mode != 0) {
         const int64_t t = a.ctrl->adam_step;
-        float step_size, bc2s;
         if (t >= 1 && t <= a.adam_table_len) {
             step_size = a.adam_table[2 * (t - 1)];
             bc2s = a.adam_table[2 * (t - 1) + 1];
@@ -476,7 +490,37 @@ __global__ __launch_bounds__(256) void k_adam(AdamArgs a) {
             step_size = (float)(-(a.lrd / (1.0 - pow(a.beta1d, (double)t))));
             bc2s = (float)pow(1.0 - pow(a.beta2d, (double)t), 0.5);
         }
-        float m = a.m[e], v = a.v[e], p = a.p[e];
+    }
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < P; e += stride) {
+        // every load of this element is issued before the first use (one round trip)
+        float m = 0.f, v = 0.f, p = 0.f, tg = 0.f;
+        if (a.mode != 0) {
+            m = a.m[e];
+            v = a.v[e];
+            p = a.p[e];
+            if (a.soft) tg = a.target[e];
+        }
+        float gsum;
+        if (a.mode == 2) {
+            gsum = a.grads[e];
+        } else {
+            int sgi = 0;
+#pragma unroll
+            for (int q = 1; q < kMaxSeg; q++)
+                if (q < a.nseg && e >= a.seg[q].off) sgi = q;
+            const AdamSegment sg = a.seg[sgi];
+            const float* pp = sg.partial + (e - sg.off);
+            float pv[8];
+#pragma unroll
+            for (int u = 0; u < 8; u++) pv[u] = (u < sg.S) ? pp[(int64_t)u * sg.pstride] : 0.f;
+            gsum = pv[0];                               // fixed-order sum of the slabs
+#pragma unroll
+            for (int u = 1; u < 8; u++)
+                if (u < sg.S) gsum += pv[u];
+            for (int u = 8; u < sg.S; u++) gsum += pp[(int64_t)u * sg.pstride];
+            a.grads[e] = gsum;
+        }
+        if (a.mode == 0) continue;
         m = fmaf(a.w1, gsum - m, m);
         v = v * a.beta2;
         v = v + (a.c2 * gsum) * gsum;
@@ -485,7 +529,7 @@ __global__ __launch_bounds__(256) void k_adam(AdamArgs a) {
         a.m[e] = m;
         a.v[e] = v;
         a.p[e] = p;
-        if (a.soft) a.target[e] = a.tau * p + a.one_minus_tau * a.target[e];
+        if (a.soft) a.target[e] = a.tau * p + a.one_minus_tau * tg;
     }
     if (a.mode != 2 && blockIdx.x == 0 && threadIdx.x == 0 && a.loss_partial) {
         float s = 0.f;
@@ -531,16 +575,22 @@ __global__ void k_replay_push(PushArgs a) {
 // =====================================================================================
 // host-side launchers
 // =====================================================================================
+template <int ACT, bool VECB>
+static void launch_fwd_gather(const FwdArgs& a, dim3 grid, hipStream_t s) {
+    if (a.p[0].phys) hipLaunchKernelGGL((k_linear_fwd<ACT, VECB, true>), grid, dim3(256), 0, s, a);
+    else hipLaunchKernelGGL((k_linear_fwd<ACT, VECB, false>), grid, dim3(256), 0, s, a);
+}
+
 int launch_linear_fwd(const FwdArgs& args, int nprob, int act, bool vecb, hipStream_t s) {
     FwdArgs a2 = args;
     a2.nprob = nprob;
     dim3 grid(((args.N + FWD_BN - 1) / FWD_BN) * ((args.M + FWD_BM - 1) / FWD_BM) * nprob);
     if (act == DQNX_ACT_RELU) {
-        if (vecb) hipLaunchKernelGGL((k_linear_fwd<DQNX_ACT_RELU, true>), grid, dim3(256), 0, s, a2);
-        else hipLaunchKernelGGL((k_linear_fwd<DQNX_ACT_RELU, false>), grid, dim3(256), 0, s, a2);
+        if (vecb) launch_fwd_gather<DQNX_ACT_RELU, true>(a2, grid, s);
+        else launch_fwd_gather<DQNX_ACT_RELU, false>(a2, grid, s);
     } else {
-        if (vecb) hipLaunchKernelGGL((k_linear_fwd<DQNX_ACT_ELU, true>), grid, dim3(256), 0, s, a2);
-        else hipLaunchKernelGGL((k_linear_fwd<DQNX_ACT_ELU, false>), grid, dim3(256), 0, s, a2);
+        if (vecb) launch_fwd_gather<DQNX_ACT_ELU, true>(a2, grid, s);
+        else launch_fwd_gather<DQNX_ACT_ELU, false>(a2, grid, s);
     }
     DQNX_HIP_CHECK(hipGetLastError());
     return DQNX_OK;

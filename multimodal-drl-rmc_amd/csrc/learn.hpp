@@ -65,7 +65,12 @@ struct HeadArgs {
     float* Q;              // [3][Bl][A]
     float* td;             // [3][Bl]: y, q(s,a), |y - q(s,a)|
     float* dZ;             // [Bl][F]
-    float* dhead;          // [Bl][16] d(head outputs), consumed by the head dW in the bwd level
+    float* dhead;          // [Bl][16] d(head outputs), consumed by the head dW
+    // dZ of the layer below the last hidden layer (L >= 2): dZprev = (dZ_L W_L) (.) act'(H_{L-1})
+    const float* W_last;   // W_L [F][in_prev]
+    const float* Hprev;    // H_{L-1} stream 0 [Bl][in_prev]
+    float* dZprev;         // [Bl][in_prev] or null (L == 1)
+    int in_prev;
     float* loss_partial;   // [tiles]
     dqnx_ctrl* ctrl;       // Adam step bookkeeping (block 0) or null
     float beta1, beta2, lr;
@@ -97,6 +102,40 @@ struct AdamArgs {
     int n_loss_partial;
     int batch_global;
     const float* adam_table;   // [t-1] = {-lr/bc1, bc2**0.5} for t <= adam_table_len (host libm)
+    int adam_table_len;
+    double beta1d, beta2d, lrd;
+};
+
+// Full-K weight gradients of every layer + Adam (+ soft update) in one launch.
+struct DwAdamProblem {
+    const float* dZ;       // [Bl][ldz]
+    int ldz;
+    const float* X;        // [Bl][ldx]
+    int ldx;
+    int in, out;           // gradient tile space: out x (in + 1 ones column)
+    int64_t poff;          // flat offset of this layer's parameters
+    int head_kind;         // -1 plain Linear layout, else dqnx_head_kind
+    int A;
+    int grid_x, blocks;
+};
+struct DwAdamArgs {
+    DwAdamProblem pr[DQNX_MAX_DENSE + 1];
+    int npr;
+    int Bl;
+    int mode;              // 0: write grads only (DP all-reduce follows), 1: grads + Adam
+    int soft;
+    int64_t n_params;
+    float* p;
+    float* m;
+    float* v;
+    float* grads;          // [n_params + 1] (last = loss)
+    float* target;
+    dqnx_ctrl* ctrl;
+    float w1, beta2, c2, eps, tau, one_minus_tau;
+    const float* loss_partial;
+    int n_loss_partial;
+    int batch_global;
+    const float* adam_table;
     int adam_table_len;
     double beta1d, beta2d, lrd;
 };
@@ -140,6 +179,8 @@ int launch_bwd_level(const BwdArgs& a, int act, hipStream_t s);
 int launch_head(const HeadArgs& a, int act, hipStream_t s);
 bool head_supported(int F);
 int launch_adam(const AdamArgs& a, hipStream_t s);
+void dw_adam_grid(DwAdamArgs& a);
+int launch_dw_adam(const DwAdamArgs& a, hipStream_t s);
 int launch_soft_update(float* target, const float* p, int64_t n, float tau, float omt, hipStream_t s);
 int launch_replay_push(const PushArgs& a, hipStream_t s);
 

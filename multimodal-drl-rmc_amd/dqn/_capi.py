@@ -28,6 +28,7 @@ DQNX_RNG_PY, DQNX_RNG_NP = 0, 1
 STEP_SOFT_UPDATE = 0x1
 STEP_GIVEN_INDICES = 0x2
 STEP_GRADS_ONLY = 0x4
+STEP_PREFETCH = 0x8
 DEVERR_SAMPLE_TOO_LARGE = 1
 DEVERR_EMPTY_TREE = 2
 
@@ -77,7 +78,7 @@ EXPORTS = [
     "dqnx_engine_bind", "dqnx_engine_reset", "dqnx_engine_set_graphs", "dqnx_replay_push", "dqnx_rng_set",
     "dqnx_rng_get", "dqnx_learn_step", "dqnx_apply_grads", "dqnx_soft_update", "dqnx_hard_update",
     "dqnx_sample_scratch_bytes", "dqnx_sample_uniform", "dqnx_last_error", "dqnx_abi_version",
-    "dqnx_learn_kernel_count", "dqnx_learn_kernel_info", "dqnx_learn_step_timed", "dqnx_events_create",
+    "dqnx_learn_kernel_count", "dqnx_learn_kernel_info", "dqnx_learn_step_timed", "dqnx_learn_step_omit", "dqnx_events_create",
     "dqnx_events_destroy", "dqnx_event_elapsed", "dqnx_debug_stamps",
 ]
 
@@ -125,6 +126,7 @@ def lib():
         "dqnx_learn_kernel_info": ([vp, I32, I32, ctypes.c_char_p, I32, P(ctypes.c_double), P(ctypes.c_double)],
                                    ctypes.c_int),
         "dqnx_learn_step_timed": ([vp, I32, I32, vp, vp, vp], ctypes.c_int),
+        "dqnx_learn_step_omit": ([vp, I32, I32, vp], ctypes.c_int),
         "dqnx_events_create": ([I32, P(vp)], ctypes.c_int),
         "dqnx_events_destroy": ([I32, P(vp)], ctypes.c_int),
         "dqnx_event_elapsed": ([vp, vp, P(ctypes.c_float)], ctypes.c_int),

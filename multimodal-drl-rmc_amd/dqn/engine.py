@@ -160,7 +160,8 @@ class LearnEngine:
         self.adam_m = self.view(C.BUF_ADAM_M, torch.float32)
         self.adam_v = self.view(C.BUF_ADAM_V, torch.float32)
         self.ctrl_bytes = self.view(C.BUF_CTRL, torch.uint8)
-        self.batch_idx = self.view(C.BUF_BATCH_IDX, torch.int32)
+        self.batch_idx_slots = self.view(C.BUF_BATCH_IDX, torch.int32).view(2, batch)
+        self.batch_idx = self.batch_idx_slots[0]
         self.q = self.view(C.BUF_Q, torch.float32).view(3, self.batch_local, spec.n_actions)
         self.td = self.view(C.BUF_TD, torch.float32).view(3, self.batch_local)
         self.is_weights = self.view(C.BUF_IS_WEIGHTS, torch.float32)
@@ -249,9 +250,11 @@ class LearnEngine:
         return a
 
     # ---- steps -----------------------------------------------------------------------
-    def learn_step(self, soft_update=False, given_indices=False, grads_only=False):
+    def learn_step(self, soft_update=False, given_indices=False, grads_only=False, prefetch=False):
+        """One learn step (+ fused soft update).  prefetch=True also draws the next step's
+        minibatch on a forked graph branch (pure learning loops; see DQNX_STEP_PREFETCH)."""
         flags = (C.STEP_SOFT_UPDATE if soft_update else 0) | (C.STEP_GIVEN_INDICES if given_indices else 0) \
-            | (C.STEP_GRADS_ONLY if grads_only else 0)
+            | (C.STEP_GRADS_ONLY if grads_only else 0) | (C.STEP_PREFETCH if prefetch else 0)
         C.check(self.L.dqnx_learn_step(self.h, flags, self.stream()), "learn_step")
 
     def apply_grads(self, soft_update=False):

@@ -121,7 +121,20 @@ def compare_state(oracle, eng, atol=1e-5):
     ("DoubleDQNAgent", 284, 100, 700, 650, 8),
 ])
 def test_gpu_learn_matches_oracle(algo, obs_dim, batch, capacity, n_fill, seed):
-    oracle, eng = make_pair(algo, obs_dim, batch, capacity, n_fill, seed)
+    _check_learn(*make_pair(algo, obs_dim, batch, capacity, n_fill, seed))
+
+
+@pytest.mark.parametrize("algo,obs_dim,batch,capacity,n_fill,seed", [
+    ("DQNAgent", 14, 32, 500, 300, 13),
+    ("DuelingDoubleDQNAgent", 284, 1024, 20000, 20000, 17),
+])
+def test_gpu_learn_fused_backward_plan_matches_oracle(monkeypatch, algo, obs_dim, batch, capacity, n_fill, seed):
+    """Backward plan 1 (head kernel makes dZ_{L-1}; one full-K dW + Adam launch)."""
+    monkeypatch.setenv("DQNX_BWD_PLAN", "1")
+    _check_learn(*make_pair(algo, obs_dim, batch, capacity, n_fill, seed))
+
+
+def _check_learn(oracle, eng):
     for step in range(3):
         rec = oracle.train_step()
         eng.learn_step(soft_update=True)
@@ -179,3 +192,30 @@ def test_gpu_learn_golden(golden):
     for i, k in enumerate(keys):
         np.testing.assert_allclose(on[k].cpu().numpy().reshape(-1), z[f"online_{i}"], atol=1e-5, rtol=0)
         np.testing.assert_allclose(tg[k].cpu().numpy().reshape(-1), z[f"target_{i}"], atol=1e-5, rtol=0)
+
+
+def test_gpu_prefetch_mode_bit_identical():
+    """DQNX_STEP_PREFETCH draws step t+1's minibatch during step t: same results, bitwise."""
+    o1, e1 = make_pair("DuelingDoubleDQNAgent", 284, 256, 3000, 3000, 21)
+    o2, e2 = make_pair("DuelingDoubleDQNAgent", 284, 256, 3000, 3000, 21)
+    for _ in range(5):
+        e1.learn_step(soft_update=True)
+    for _ in range(4):
+        e2.learn_step(soft_update=True, prefetch=True)
+    e2.learn_step(soft_update=True)     # consumes the pending minibatch
+    torch.cuda.synchronize()
+    assert torch.equal(e1.params, e2.params)
+    assert torch.equal(e1.target_params, e2.target_params)
+    assert np.array_equal(e1.get_rng(0), e2.get_rng(0))
+    # after the flush, pushes are allowed again
+    e2.push(*O.synth_transitions(4, 284, 8, seed=3))
+
+
+def test_gpu_push_refused_with_pending_prefetch():
+    from dqn import _capi as C
+    o, e = make_pair("DuelingDoubleDQNAgent", 14, 32, 500, 300, 22)
+    e.learn_step(prefetch=True)
+    with pytest.raises(C.DqnxError):
+        e.push(*O.synth_transitions(2, 14, 8, seed=1))
+    e.learn_step()
+    torch.cuda.synchronize()
