@@ -164,6 +164,9 @@ enum dqnx_buffer {
     DQNX_BUF_TD,               /* [3][batch_local] fp32: targets y, q(s,a), |y - q(s,a)| */
     DQNX_BUF_IS_WEIGHTS,       /* [batch] fp32 PER importance weights */
     DQNX_BUF_WORKSPACE,        /* everything else (activations, partial slabs, scratch) */
+    DQNX_BUF_PER_ABS_TD,       /* [batch] fp32 |targets - q(s,a)| of the GLOBAL minibatch (PER only):
+                                  each rank's learn step writes its shard; under DP the caller
+                                  all-gathers it in place before dqnx_apply_grads */
     DQNX_BUF_COUNT
 };
 int dqnx_engine_buffer(const dqnx_engine* e, int32_t which, uint64_t* offset, uint64_t* bytes);
@@ -186,6 +189,22 @@ int dqnx_engine_set_graphs(dqnx_engine* e, int32_t enabled);
 int dqnx_replay_push(dqnx_engine* e, const float* obs, const int32_t* act, const float* rew,
                      const uint8_t* done, const float* next_obs, int32_t n, int32_t src_on_device,
                      void* stream);
+
+/* ---- prioritised replay (DQNX_ALGO_PER_DOUBLE) ------------------------------------
+ * The SumTree lives in DQNX_BUF_SUMTREE with the reference's layout (leaf of ring slot s
+ * = tree index s + capacity - 1); its max/min priority indices in dqnx_ctrl.
+ * dqnx_per_sample: ReplayMemoryPrioritized.sample_transitions(step) (R:dqn/replay_memory.py:69-92)
+ *   -> ring slots into DQNX_BUF_BATCH_IDX slot 0, IS weights into DQNX_BUF_IS_WEIGHTS; consumes
+ *   numpy global-state words from dqnx_ctrl.np_mt and advances dqnx_ctrl.agent_step by n_env.
+ *   A PER learn step does this itself.
+ * dqnx_per_update_priorities: update_batch_priorities(tree_indices, abs_td_errors)
+ *   (R:dqn/replay_memory.py:94-98) for n (ring slot, |delta|) pairs in device memory, in order.
+ *   A PER learn step does this itself (after the all-gather under DP: dqnx_apply_grads).
+ * dqnx_set_agent_step: the `self.step * self.n_env` the next PER sample interpolates beta from
+ *   (R:dqn/agent.py:247). */
+int dqnx_per_sample(dqnx_engine* e, void* stream);
+int dqnx_per_update_priorities(dqnx_engine* e, const int32_t* slots, const float* abs_td, int32_t n, void* stream);
+int dqnx_set_agent_step(dqnx_engine* e, int64_t step_times_n_env, void* stream);
 
 /* ---- RNG state exchange (Python random / numpy legacy global state) -------------- */
 enum dqnx_rng { DQNX_RNG_PY = 0, DQNX_RNG_NP = 1 };

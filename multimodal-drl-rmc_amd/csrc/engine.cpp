@@ -208,6 +208,7 @@ int layout(dqnx_engine* e) {
     region(DQNX_BUF_Q, (uint64_t)3 * e->Bl * A * 4);
     region(DQNX_BUF_TD, (uint64_t)3 * e->Bl * 4);
     region(DQNX_BUF_IS_WEIGHTS, (uint64_t)e->Bg * 4);
+    region(DQNX_BUF_PER_ABS_TD, c.algo == DQNX_ALGO_PER_DOUBLE ? (uint64_t)e->Bg * 4 : 0);
     // workspace
     cur = align_up(cur, 256);
     e->off[DQNX_BUF_WORKSPACE] = cur;
@@ -255,6 +256,58 @@ int check_bound(const dqnx_engine* e) {
 // and timed on its own (dqnx_learn_step_timed).
 
 
+PerSampleArgs per_sample_args(dqnx_engine* e, int32_t* idx, int32_t* phys) {
+    const dqnx_config& c = e->cfg;
+    PerSampleArgs pa;
+    memset(&pa, 0, sizeof(pa));
+    pa.tree = at<double>(e, e->off[DQNX_BUF_SUMTREE]);
+    pa.cap = c.capacity;
+    pa.ctrl = ctrl_of(e);
+    pa.Bg = e->Bg;
+    pa.shard_begin = e->shard_begin;
+    pa.shard_len = e->Bl;
+    pa.out_idx = idx;
+    pa.phys_out = phys;
+    pa.isw = at<float>(e, e->off[DQNX_BUF_IS_WEIGHTS]);
+    pa.beta_start = c.per_beta_start;
+    pa.beta_end = c.per_beta_end;
+    pa.beta_steps = c.per_beta_steps;
+    pa.n_env = c.n_env;
+    return pa;
+}
+
+PerUpdateArgs per_update_args(dqnx_engine* e) {
+    const dqnx_config& c = e->cfg;
+    PerUpdateArgs ua;
+    memset(&ua, 0, sizeof(ua));
+    ua.tree = at<double>(e, e->off[DQNX_BUF_SUMTREE]);
+    ua.cap = c.capacity;
+    ua.ctrl = ctrl_of(e);
+    ua.eps = (float)c.per_eps;
+    ua.alpha = (float)c.per_alpha;
+    ua.pmax = (float)c.per_max_priority;
+    return ua;
+}
+
+// update_batch_priorities over n (slot, |delta|) pairs in order, in PER_CHUNK launches.
+// size: the ring size at the time (the rescan range); read from the host mirror.
+int enqueue_per_update_pairs(dqnx_engine* e, const int32_t* slots, const float* abs_td, int n, hipStream_t s) {
+    for (int o = 0; o < n; o += PER_CHUNK) {
+        PerUpdateArgs ua = per_update_args(e);
+        ua.mode = 0;
+        ua.n = std::min(PER_CHUNK, n - o);
+        ua.slots = slots + o;
+        ua.abs_td = abs_td + o;
+        int rc = launch_per_update(ua, s);   // mode 0 reads the ring size on the device
+        if (rc) return rc;
+    }
+    return DQNX_OK;
+}
+
+int enqueue_per_update(dqnx_engine* e, const int32_t* idx, hipStream_t s) {
+    return enqueue_per_update_pairs(e, idx, at<float>(e, e->off[DQNX_BUF_PER_ABS_TD]), e->Bg, s);
+}
+
 // key = flags | (slot << 8): `slot` selects the (sampled indices, physical rows) buffer pair.
 std::vector<KStep> build_learn_steps(dqnx_engine* e, int key) {
     const int flags = key & 0xff;
@@ -271,9 +324,17 @@ std::vector<KStep> build_learn_steps(dqnx_engine* e, int key) {
     int32_t* idx = at<int32_t>(e, e->off[DQNX_BUF_BATCH_IDX]) + (size_t)slot * e->Bg;
     int32_t* phys = at<int32_t>(e, e->ws_phys) + (size_t)slot * e->Bl;
     const double Bl = e->Bl;
+    const double Bg_ = e->Bg;
 
-    // 1. sample (R:dqn/replay_memory.py:38-39)
-    if (flags & DQNX_STEP_GIVEN_INDICES) {
+    // 1. sample (R:dqn/replay_memory.py:38-39; PER :69-92)
+    if (c.algo == DQNX_ALGO_PER_DOUBLE) {
+        const PerSampleArgs pa = per_sample_args(e, idx, phys);
+        KStep k;
+        k.name = "per_sample";
+        k.bytes = 2.0 * 625 * 4 + 8.0 * Bg_ * 22 + 8.0 * e->Bg + 4.0 * Bl;
+        k.run = [=](hipStream_t s) { return launch_per_sample(pa, s); };
+        ks.push_back(k);
+    } else if (flags & DQNX_STEP_GIVEN_INDICES) {
         KStep k;
         k.name = "idx_to_phys";
         k.bytes = 8.0 * Bl;
@@ -365,6 +426,8 @@ std::vector<KStep> build_learn_steps(dqnx_engine* e, int key) {
         ha.rew = at<float>(e, e->off[DQNX_BUF_RING_REW]);
         ha.done = at<float>(e, e->off[DQNX_BUF_RING_DONE]);
         ha.isw = (c.algo == DQNX_ALGO_PER_DOUBLE) ? at<float>(e, e->off[DQNX_BUF_IS_WEIGHTS]) + e->shard_begin : nullptr;
+        ha.abs_td_out = (c.algo == DQNX_ALGO_PER_DOUBLE) ? at<float>(e, e->off[DQNX_BUF_PER_ABS_TD]) + e->shard_begin
+                                                         : nullptr;
         ha.Q = at<float>(e, e->off[DQNX_BUF_Q]);
         ha.td = at<float>(e, e->off[DQNX_BUF_TD]);
         ha.dZ = at<float>(e, e->ws_dZ[L - 1]);
@@ -388,6 +451,16 @@ std::vector<KStep> build_learn_steps(dqnx_engine* e, int key) {
         k.bytes = 4.0 * (nstreams * Bl * F + 2.0 * np.head_params + Bl * F + e->tiles * (double)np.head_params
                          + 3.0 * Bl * A + 6.0 * Bl);
         k.run = [=](hipStream_t s) { return launch_head(ha, act, s); };
+        ks.push_back(k);
+    }
+
+    // 3b. PER priorities (R:dqn/agent.py:263-265): single GPU here; under DP after the
+    //     all-gather of |delta|, in dqnx_apply_grads
+    if (c.algo == DQNX_ALGO_PER_DOUBLE && !(flags & DQNX_STEP_GRADS_ONLY)) {
+        KStep k;
+        k.name = "per_update";
+        k.bytes = Bg_ * (4.0 + 4.0 + 8.0 * 2.0 * 21.0);
+        k.run = [=](hipStream_t s) { return enqueue_per_update(e, idx, s); };
         ks.push_back(k);
     }
 
@@ -617,6 +690,10 @@ int enqueue_range(const std::vector<KStep>& ks, int a, int b, hipStream_t s) {
 
 int enqueue_apply(dqnx_engine* e, int flags, hipStream_t s) {
     const dqnx_config& c = e->cfg;
+    if (c.algo == DQNX_ALGO_PER_DOUBLE) {   // priorities from the all-gathered |delta| (DP)
+        int rc = enqueue_per_update(e, at<int32_t>(e, e->off[DQNX_BUF_BATCH_IDX]), s);
+        if (rc) return rc;
+    }
     AdamArgs aa;
     memset(&aa, 0, sizeof(aa));
     aa.nseg = 0;
@@ -756,7 +833,11 @@ int dqnx_engine_create(const dqnx_config* cfg, dqnx_engine** out) {
     const dqnx_config& c = e->cfg;
     if (c.net.kind != DQNX_NET_MLP) { delete e; return set_error(DQNX_EUNSUPPORTED, "two-stream network not built yet"); }
     if (c.algo < DQNX_ALGO_DQN || c.algo > DQNX_ALGO_PER_DOUBLE) { delete e; return set_error(DQNX_EINVAL, "bad algo"); }
-    if (c.algo == DQNX_ALGO_PER_DOUBLE) { delete e; return set_error(DQNX_EUNSUPPORTED, "PER learn step not built yet"); }
+    if (c.algo == DQNX_ALGO_PER_DOUBLE) {
+        // exact float64 tree sums need cap <= 2^20 (see per.hip); one sampler workgroup <= PER_MAX_B
+        if (c.capacity > ((int64_t)1 << 20)) { delete e; return set_error(DQNX_EUNSUPPORTED, "PER capacity > 2^20"); }
+        if (c.batch > PER_MAX_B) { delete e; return set_error(DQNX_EUNSUPPORTED, "PER batch > %d", PER_MAX_B); }
+    }
     if (c.batch <= 0 || c.world_size <= 0 || c.rank < 0 || c.rank >= c.world_size || c.batch % c.world_size)
         { delete e; return set_error(DQNX_EINVAL, "batch must be a positive multiple of world_size"); }
     if (c.capacity <= 0 || c.capacity >= ((int64_t)1 << 31)) { delete e; return set_error(DQNX_EINVAL, "capacity out of range"); }
@@ -850,7 +931,7 @@ int dqnx_engine_reset(dqnx_engine* e, void* stream) {
     const int ids[] = {DQNX_BUF_GRADS, DQNX_BUF_ADAM_M, DQNX_BUF_ADAM_V, DQNX_BUF_CTRL, DQNX_BUF_RING_OBS,
                        DQNX_BUF_RING_NEXT_OBS, DQNX_BUF_RING_ACT, DQNX_BUF_RING_REW, DQNX_BUF_RING_DONE,
                        DQNX_BUF_SUMTREE, DQNX_BUF_BATCH_IDX, DQNX_BUF_Q, DQNX_BUF_TD, DQNX_BUF_IS_WEIGHTS,
-                       DQNX_BUF_WORKSPACE};
+                       DQNX_BUF_WORKSPACE, DQNX_BUF_PER_ABS_TD};
     for (int id : ids)
         if (e->bytes[id]) DQNX_HIP_CHECK(hipMemsetAsync(e->arena + e->off[id], 0, e->bytes[id], s));
     // SumTree.max/min_priority_index start at capacity - 1 (R:dqn/utils/sum_tree.py:12-13)
@@ -886,13 +967,15 @@ int dqnx_replay_push(dqnx_engine* e, const float* obs, const int32_t* act, const
     if (rc) return rc;
     if (n < 0 || (n > 0 && (!obs || !act || !rew || !done || !next_obs)))
         return set_error(DQNX_EINVAL, "dqnx_replay_push: bad argument");
-    if (e->cfg.algo == DQNX_ALGO_PER_DOUBLE) return set_error(DQNX_EUNSUPPORTED, "PER push not built yet");
     if (e->pf_valid) return set_error(DQNX_ESTATE, "replay push while a prefetched minibatch is pending");
     hipStream_t s = (hipStream_t)stream;
     const int D = e->cfg.net.obs_dim;
     int done_rows = 0;
     while (done_rows < n) {
-        const int m = src_on_device ? n - done_rows : std::min(n - done_rows, e->stage_rows);
+        const bool per = e->cfg.algo == DQNX_ALGO_PER_DOUBLE;
+        int m = src_on_device ? n - done_rows : std::min(n - done_rows, e->stage_rows);
+        // PER: every add is a SumTree.update in order; chunks never wrap onto themselves
+        if (per) m = (int)std::min<int64_t>(std::min(m, PER_CHUNK), e->cfg.capacity);
         PushArgs pa;
         memset(&pa, 0, sizeof(pa));
         if (src_on_device) {
@@ -947,6 +1030,15 @@ int dqnx_replay_push(dqnx_engine* e, const float* obs, const int32_t* act, const
             pa.wptr = e->ring_wptr;
             pa.new_wptr = (e->ring_wptr + cap) % cap;
             pa.new_size = cap;
+        }
+        if (per) {   // Agent.store_transitions -> SumTree.add(max_priority) x m (R:dqn/replay_memory.py:56-67)
+            PerUpdateArgs ua = per_update_args(e);
+            ua.mode = 1;
+            ua.n = pa.n;
+            ua.wptr = pa.wptr;
+            ua.size = e->ring_size;
+            rc = launch_per_update(ua, s);
+            if (rc) return rc;
         }
         rc = launch_replay_push(pa, s);
         if (rc) return rc;
@@ -1009,7 +1101,11 @@ int dqnx_learn_step(dqnx_engine* e, int32_t flags, void* stream) {
     int rc = check_bound(e);
     if (rc) return rc;
     hipStream_t s = (hipStream_t)stream;
-    const bool prefetch = (flags & DQNX_STEP_PREFETCH) && !(flags & DQNX_STEP_GIVEN_INDICES);
+    if (e->cfg.algo == DQNX_ALGO_PER_DOUBLE && (flags & DQNX_STEP_GIVEN_INDICES))
+        return set_error(DQNX_EUNSUPPORTED, "PER learn step samples its own minibatch");
+    // PER: step t+1's sample depends on step t's priority update, so nothing is drawn ahead
+    const bool prefetch = (flags & DQNX_STEP_PREFETCH) && !(flags & DQNX_STEP_GIVEN_INDICES) &&
+                          e->cfg.algo != DQNX_ALGO_PER_DOUBLE;
     if (e->ring_size < e->Bg && !(flags & DQNX_STEP_GIVEN_INDICES) && !e->pf_valid)
         return set_error(DQNX_EINVAL, "Sample larger than population: %lld < %d", (long long)e->ring_size, e->Bg);
     const int base = flags & (DQNX_STEP_SOFT_UPDATE | DQNX_STEP_GIVEN_INDICES | DQNX_STEP_GRADS_ONLY);
@@ -1118,6 +1214,31 @@ int dqnx_learn_step_omit(dqnx_engine* e, int32_t flags, int32_t omit_index, void
         }
         return (int)DQNX_OK;
     });
+}
+
+int dqnx_per_sample(dqnx_engine* e, void* stream) {
+    int rc = check_bound(e);
+    if (rc) return rc;
+    if (e->cfg.algo != DQNX_ALGO_PER_DOUBLE) return set_error(DQNX_ESTATE, "engine is not PER");
+    const PerSampleArgs pa = per_sample_args(e, at<int32_t>(e, e->off[DQNX_BUF_BATCH_IDX]), at<int32_t>(e, e->ws_phys));
+    return launch_per_sample(pa, (hipStream_t)stream);
+}
+
+int dqnx_per_update_priorities(dqnx_engine* e, const int32_t* slots, const float* abs_td, int32_t n, void* stream) {
+    int rc = check_bound(e);
+    if (rc) return rc;
+    if (e->cfg.algo != DQNX_ALGO_PER_DOUBLE) return set_error(DQNX_ESTATE, "engine is not PER");
+    if (n < 0 || (n && (!slots || !abs_td))) return set_error(DQNX_EINVAL, "bad argument");
+    return enqueue_per_update_pairs(e, slots, abs_td, n, (hipStream_t)stream);
+}
+
+int dqnx_set_agent_step(dqnx_engine* e, int64_t step_times_n_env, void* stream) {
+    int rc = check_bound(e);
+    if (rc) return rc;
+    const int64_t v = step_times_n_env;
+    DQNX_HIP_CHECK(hipMemcpyAsync(&ctrl_of(e)->agent_step, &v, sizeof(v), hipMemcpyHostToDevice, (hipStream_t)stream));
+    DQNX_HIP_CHECK(hipStreamSynchronize((hipStream_t)stream));   // `v` is on this stack frame
+    return DQNX_OK;
 }
 
 int dqnx_events_create(int32_t n, void** events) {

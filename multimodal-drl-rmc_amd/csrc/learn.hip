@@ -377,6 +377,7 @@ __global__ __launch_bounds__(256) void k_head(HeadArgs a) {
             a.td[gb] = y;
             a.td[Bl + gb] = qa;
             a.td[2 * Bl + gb] = z;
+            if (a.abs_td_out) a.abs_td_out[gb] = z;
         }
         gsh[b] = gq;
         lossv[b] = lb;

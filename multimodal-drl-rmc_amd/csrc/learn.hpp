@@ -62,6 +62,7 @@ struct HeadArgs {
     const float* rew;
     const float* done;
     const float* isw;      // [Bl] PER IS weights of the local shard or null
+    float* abs_td_out;     // PER: [Bl] |targets - q(s,a)| into the global [Bg] array (shard offset) or null
     float* Q;              // [3][Bl][A]
     float* td;             // [3][Bl]: y, q(s,a), |y - q(s,a)|
     float* dZ;             // [Bl][F]
@@ -172,6 +173,40 @@ struct SampleArgs {
     int64_t capacity;
     int64_t* stamps;          // diagnostic builds (-DDQNX_STAMPS)
 };
+
+// PER sampling: ReplayMemoryPrioritized.sample_transitions (R:dqn/replay_memory.py:69-92)
+constexpr int PER_MAX_B = 8192;     // largest global minibatch k_per_sample handles
+constexpr int PER_CHUNK = 4096;     // priority updates per k_per_update launch
+struct PerSampleArgs {
+    const double* tree;       // [2*cap-1] SumTree (R:dqn/utils/sum_tree.py)
+    int64_t cap;
+    dqnx_ctrl* ctrl;          // np_mt (advanced), ring_size, per_min_idx, agent_step (read, += n_env)
+    int32_t Bg;               // global minibatch
+    int32_t shard_begin, shard_len;
+    int32_t* out_idx;         // [Bg] sampled data indices (= ring slots = leaf - (cap-1))
+    int32_t* phys_out;        // [shard_len] ring slots of this rank's shard
+    float* isw;               // [Bg] importance weights (float32, like T.as_tensor(..., float32))
+    double beta_start, beta_end, beta_steps;
+    int32_t n_env;
+};
+
+// PER priority writes with SumTree.update's sequential semantics (R:dqn/utils/sum_tree.py:15-32):
+// mode 0 = update_batch_priorities (R:dqn/replay_memory.py:94-98),
+// mode 1 = store_transitions' adds at the current max priority (R:dqn/replay_memory.py:56-67).
+struct PerUpdateArgs {
+    double* tree;
+    int64_t cap;
+    dqnx_ctrl* ctrl;          // per_max_idx / per_min_idx (read + written)
+    int32_t mode;
+    int32_t n;                // updates in this launch (<= PER_CHUNK)
+    const int32_t* slots;     // mode 0: [n] ring slots, in batch order
+    const float* abs_td;      // mode 0: [n] |targets - q(s,a)|
+    int64_t wptr, size;       // mode 1: ring write pointer / size before this chunk (mode 0 reads ctrl)
+    float eps, alpha, pmax;   // numpy float32 arithmetic on the python-float constants
+};
+
+int launch_per_sample(const PerSampleArgs& a, hipStream_t s);
+int launch_per_update(const PerUpdateArgs& a, hipStream_t s);
 
 int launch_linear_fwd(const FwdArgs& args, int nprob, int act, bool vecb, hipStream_t s);
 void bwd_level_grid(BwdArgs& a);

@@ -1,0 +1,39 @@
+// MT19937 pieces shared by the replay samplers (CPython random and numpy's legacy
+// RandomState use the same generator, state layout (624 words + index) and tempering).
+#pragma once
+#include <stdint.h>
+
+namespace dqnx {
+
+constexpr uint32_t MT_UPPER = 0x80000000u, MT_LOWER = 0x7fffffffu, MT_A = 0x9908b0dfu;
+
+__device__ __forceinline__ uint32_t mt_temper(uint32_t y) {
+    y ^= (y >> 11);
+    y ^= (y << 7) & 0x9d2c5680u;
+    y ^= (y << 15) & 0xefc60000u;
+    y ^= (y >> 18);
+    return y;
+}
+
+__device__ __forceinline__ uint32_t mt_mix(uint32_t a, uint32_t b) {
+    uint32_t y = (a & MT_UPPER) | (b & MT_LOWER);
+    return (y >> 1) ^ ((y & 1u) ? MT_A : 0u);
+}
+
+// Block-parallel twist of the 624-word state in LDS (blockDim >= 624): the recurrence
+// mt[k] = mt[k+397 or k-227] ^ mix(mt[k], mt[k+1]) has three dependency phases.
+// Every thread of the block must call it.
+__device__ __forceinline__ void mt_twist_block(uint32_t* mt, uint32_t* tmp) {
+    const int tid = threadIdx.x;
+    if (tid < 624) tmp[tid] = mt[tid];
+    __syncthreads();
+    if (tid < 227) mt[tid] = tmp[tid + 397] ^ mt_mix(tmp[tid], tmp[tid + 1]);
+    __syncthreads();
+    if (tid >= 227 && tid < 454) mt[tid] = mt[tid - 227] ^ mt_mix(tmp[tid], tmp[tid + 1]);
+    __syncthreads();
+    if (tid >= 454 && tid < 623) mt[tid] = mt[tid - 227] ^ mt_mix(tmp[tid], tmp[tid + 1]);
+    if (tid == 623) mt[623] = mt[396] ^ mt_mix(tmp[623], mt[0]);
+    __syncthreads();
+}
+
+}  // namespace dqnx

@@ -17,23 +17,9 @@
 //
 // Pool branch (n <= setsize, only while the buffer is tiny): sequential on one lane.
 #include "learn.hpp"
+#include "mt.hpp"
 
 namespace dqnx {
-
-constexpr uint32_t MT_UPPER = 0x80000000u, MT_LOWER = 0x7fffffffu, MT_A = 0x9908b0dfu;
-
-__device__ __forceinline__ uint32_t mt_temper(uint32_t y) {
-    y ^= (y >> 11);
-    y ^= (y << 7) & 0x9d2c5680u;
-    y ^= (y << 15) & 0xefc60000u;
-    y ^= (y >> 18);
-    return y;
-}
-
-__device__ __forceinline__ uint32_t mt_mix(uint32_t a, uint32_t b) {
-    uint32_t y = (a & MT_UPPER) | (b & MT_LOWER);
-    return (y >> 1) ^ ((y & 1u) ? MT_A : 0u);
-}
 
 // Serial genrand_uint32 on one lane (pool branch).
 __device__ uint32_t mt_next_serial(uint32_t* mt, uint32_t& pos) {
@@ -124,15 +110,7 @@ __global__ __launch_bounds__(SAMPLE_NT) void k_sample_uniform(SampleArgs a) {
     __syncthreads();
     while (true) {
         if (pos >= 624) {   // parallel twist: 3 dependency phases (CPython genrand_uint32)
-            if (tid < 624) tmp[tid] = mt[tid];
-            __syncthreads();
-            if (tid < 227) mt[tid] = tmp[tid + 397] ^ mt_mix(tmp[tid], tmp[tid + 1]);
-            __syncthreads();
-            if (tid >= 227 && tid < 454) mt[tid] = mt[tid - 227] ^ mt_mix(tmp[tid], tmp[tid + 1]);
-            __syncthreads();
-            if (tid >= 454 && tid < 623) mt[tid] = mt[tid - 227] ^ mt_mix(tmp[tid], tmp[tid + 1]);
-            if (tid == 623) mt[623] = mt[396] ^ mt_mix(tmp[623], mt[0]);
-            __syncthreads();
+            mt_twist_block(mt, tmp);
             pos = 0;
             twisted = true;
         }

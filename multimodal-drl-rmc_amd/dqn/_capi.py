@@ -23,7 +23,7 @@ DQNX_ALGO_DQN, DQNX_ALGO_DOUBLE, DQNX_ALGO_PER_DOUBLE = 0, 1, 2
 DQNX_MAX_DENSE, DQNX_MAX_CONV = 6, 4
 (BUF_PARAMS, BUF_TARGET_PARAMS, BUF_GRADS, BUF_ADAM_M, BUF_ADAM_V, BUF_CTRL, BUF_RING_OBS,
  BUF_RING_NEXT_OBS, BUF_RING_ACT, BUF_RING_REW, BUF_RING_DONE, BUF_SUMTREE, BUF_BATCH_IDX, BUF_Q,
- BUF_TD, BUF_IS_WEIGHTS, BUF_WORKSPACE, BUF_COUNT) = range(18)
+ BUF_TD, BUF_IS_WEIGHTS, BUF_WORKSPACE, BUF_PER_ABS_TD, BUF_COUNT) = range(19)
 DQNX_RNG_PY, DQNX_RNG_NP = 0, 1
 STEP_SOFT_UPDATE = 0x1
 STEP_GIVEN_INDICES = 0x2
@@ -80,6 +80,7 @@ EXPORTS = [
     "dqnx_sample_scratch_bytes", "dqnx_sample_uniform", "dqnx_last_error", "dqnx_abi_version",
     "dqnx_learn_kernel_count", "dqnx_learn_kernel_info", "dqnx_learn_step_timed", "dqnx_learn_step_omit", "dqnx_events_create",
     "dqnx_events_destroy", "dqnx_event_elapsed", "dqnx_debug_stamps",
+    "dqnx_per_sample", "dqnx_per_update_priorities", "dqnx_set_agent_step",
 ]
 
 _lib = None
@@ -132,6 +133,9 @@ def lib():
         "dqnx_event_elapsed": ([vp, vp, P(ctypes.c_float)], ctypes.c_int),
         "dqnx_abi_version": ([], I32),
         "dqnx_debug_stamps": ([vp, P(I64), vp], ctypes.c_int),
+        "dqnx_per_sample": ([vp, vp], ctypes.c_int),
+        "dqnx_per_update_priorities": ([vp, vp, vp, I32, vp], ctypes.c_int),
+        "dqnx_set_agent_step": ([vp, I64, vp], ctypes.c_int),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)

@@ -170,6 +170,8 @@ class LearnEngine:
         self.ring_act = self.view(C.BUF_RING_ACT, torch.int32)
         self.ring_rew = self.view(C.BUF_RING_REW, torch.float32)
         self.ring_done = self.view(C.BUF_RING_DONE, torch.float32)
+        self.sumtree = self.view(C.BUF_SUMTREE, torch.float64)      # [2*cap-1] (PER), else empty
+        self.per_abs_td = self.view(C.BUF_PER_ABS_TD, torch.float32)  # [batch] (PER), else empty
         self.ring_size = 0
         self.ring_wptr = 0
 
@@ -267,6 +269,23 @@ class LearnEngine:
     def hard_update(self):
         C.check(self.L.dqnx_hard_update(self.h, self.stream()), "hard_update")
 
+    # ---- prioritised replay ------------------------------------------------------------
+    def per_sample(self):
+        """ReplayMemoryPrioritized.sample_transitions: slots -> batch_idx, IS weights -> is_weights."""
+        C.check(self.L.dqnx_per_sample(self.h, self.stream()), "per_sample")
+
+    def per_update_priorities(self, slots: torch.Tensor, abs_td: torch.Tensor):
+        """update_batch_priorities(tree_indices, abs_td_errors) for device int32 ring slots
+        and float32 |delta|, in order."""
+        slots = slots.to(self.device, torch.int32).contiguous()
+        abs_td = abs_td.to(self.device, torch.float32).contiguous()
+        C.check(self.L.dqnx_per_update_priorities(self.h, ctypes.c_void_p(slots.data_ptr()),
+                                                  ctypes.c_void_p(abs_td.data_ptr()), int(slots.numel()),
+                                                  self.stream()), "per_update_priorities")
+
+    def set_agent_step(self, step_times_n_env: int):
+        C.check(self.L.dqnx_set_agent_step(self.h, int(step_times_n_env), self.stream()), "set_agent_step")
+
     def ctrl(self) -> C.Ctrl:
         """Snapshot of the device control block (synchronises)."""
         raw = self.ctrl_bytes.cpu().numpy().tobytes()
@@ -279,5 +298,7 @@ class LearnEngine:
         err = self.ctrl().error
         if err == C.DEVERR_SAMPLE_TOO_LARGE:
             raise ValueError("Sample larger than population or is negative")
+        if err == C.DEVERR_EMPTY_TREE:
+            raise RuntimeError("libdqnx: PER sample from a SumTree with total priority 0")
         if err:
             raise RuntimeError(f"libdqnx device error {err}")

@@ -353,7 +353,8 @@ class SumTree:
 class PerReplay:
     """ReplayMemoryPrioritized (R:dqn/replay_memory.py:43-98)."""
 
-    def __init__(self, buffer_size: int, batch_size: int, eps_dec: float):
+    def __init__(self, buffer_size: int, batch_size: int, eps_dec: float, pow_mode: str = "numpy"):
+        self.pow_mode = pow_mode
         self.batch_size = batch_size
         self.buffer_size = buffer_size
         self.replay_buffer = SumTree(buffer_size)
@@ -394,8 +395,17 @@ class PerReplay:
         return is_w, idxs, trans
 
     def priorities(self, abs_td_errors_np: np.ndarray) -> np.ndarray:
-        """float32 p = min(|d| + eps, 1)^alpha  (R:dqn/replay_memory.py:95)."""
-        return np.power(np.minimum(abs_td_errors_np + self.epsilon, self.max_priority_high), self.alpha)
+        """float32 p = min(|d| + eps, 1)^alpha  (R:dqn/replay_memory.py:95).
+
+        pow_mode "numpy": this host's numpy float32 power, which is what the reference computes
+        when run here (numpy >= 1.22 on AVX-512 dispatches to SVML, within 1 ulp of correctly
+        rounded).  pow_mode "cr": correctly rounded float32 power (float64 pow rounded once),
+        which is glibc powf's result (the reference's pinned numpy 1.21 calls libm powf) except
+        in rare hard cases; libdqnx computes this."""
+        x = np.minimum(abs_td_errors_np + self.epsilon, self.max_priority_high)
+        if self.pow_mode == "cr":
+            return np.power(x.astype(np.float64), np.float64(np.float32(self.alpha))).astype(np.float32)
+        return np.power(x, self.alpha)
 
     def update_batch_priorities(self, tree_indices, abs_td_errors_np):  # :94-98
         pr = self.priorities(abs_td_errors_np).reshape(-1)
@@ -469,7 +479,7 @@ class OracleLearner:
 
     def __init__(self, spec: NetSpec, algo: str, batch_size: int, buffer_size: int,
                  lr=1e-4, gamma=0.99, tau=1e-3, n_env=1, soft_update=True,
-                 update_target_frequency=30000, eps_dec=2e6, seed=0, params=None):
+                 update_target_frequency=30000, eps_dec=2e6, seed=0, params=None, per_pow="numpy"):
         assert algo in ALGOS
         self.spec, self.algo = spec, algo
         self.batch_size, self.buffer_size = batch_size, buffer_size
@@ -484,7 +494,8 @@ class OracleLearner:
         self.adam_step = 0
         self.step = 0
         self.per = algo == "PerDuelingDoubleDQNAgent"
-        self.replay = PerReplay(buffer_size, batch_size, eps_dec) if self.per else NaiveReplay(buffer_size, batch_size)
+        self.replay = PerReplay(buffer_size, batch_size, eps_dec, per_pow) if self.per \
+            else NaiveReplay(buffer_size, batch_size)
         self.py_state = py_state_to_array(random.getstate())
         self.np_state = np_state_to_array(np.random.get_state())
 

@@ -1,0 +1,205 @@
+"""GPU parity of prioritised replay (PerDuelingDoubleDQNAgent): device SumTree pushes,
+ordered priority updates (incl. max/min rescans), stratified sampling + IS weights, and the
+full PER learn step, through the C ABI, against the oracle (R:dqn/replay_memory.py:43-98,
+R:dqn/utils/sum_tree.py, R:dqn/agent.py:245-272).
+
+The oracle runs with pow_mode="cr" (correctly rounded float32 power, as libdqnx and glibc
+powf compute it); the golden fixture was made by the reference under this host's numpy
+(SVML power, within 1 ulp), so that comparison carries a tolerance on the tree."""
+import os
+import random
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import ref as O
+
+pytestmark = pytest.mark.gpu
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+ALGO = "PerDuelingDoubleDQNAgent"
+
+
+def _E():
+    from dqn import engine as E
+    return E
+
+
+def tree_state(eng):
+    c = eng.ctrl()
+    return eng.sumtree.cpu().numpy(), int(c.per_max_idx), int(c.per_min_idx)
+
+
+def assert_tree_equal(eng, st: O.SumTree, exact=True):
+    tree, mx, mn = tree_state(eng)
+    if exact:
+        bad = np.nonzero(tree != st.tree)[0]
+        assert bad.size == 0, f"{bad.size} tree nodes differ, first {bad[:5]}: {tree[bad[:5]]} vs {st.tree[bad[:5]]}"
+    else:   # priorities from |delta| that agree to ~1e-6: d(p)/d|delta| <= 0.6 * 1e-4^-0.4 = 24
+        np.testing.assert_allclose(tree, st.tree, rtol=1e-6, atol=1e-4)
+    assert mx == st.max_priority_index and mn == st.min_priority_index, (mx, mn, st.max_priority_index,
+                                                                         st.min_priority_index)
+
+
+def per_engine(obs_dim, batch, cap, graphs=True):
+    E = _E()
+    return E.LearnEngine(E.mlp_spec(obs_dim, 8, "dueling"), ALGO, batch, cap, graphs=graphs)
+
+
+def test_gpu_per_push_matches_sumtree_add():
+    cap = 500
+    eng = per_engine(14, 32, cap)
+    rep = O.PerReplay(cap, 32, 2e6, "cr")
+    obs, act, rew, done, new_obs = O.synth_transitions(1300, 14, 8, seed=5)
+    o = 0
+    for n in (1, 37, 300, 362, 1, 599):   # wraps the ring twice
+        sl = slice(o, o + n)
+        eng.push(obs[sl], act[sl], rew[sl], done[sl], new_obs[sl])
+        list(rep.store_transitions(obs[sl], act[sl], rew[sl], done[sl], new_obs[sl]))
+        o += n
+        torch.cuda.synchronize()
+        assert_tree_equal(eng, rep.replay_buffer)
+        assert eng.ctrl().ring_size == rep.replay_buffer.size
+
+
+@pytest.mark.parametrize("cap,fill,n,rounds", [(500, 300, 64, 40), (20000, 20000, 5000, 3)])
+def test_gpu_per_priority_updates_match_sequential_semantics(cap, fill, n, rounds):
+    """Batches with duplicate leaves, the max leaf lowered and the min leaf raised (the
+    argmax / argmin rescans), and more updates than one launch takes."""
+    eng = per_engine(14, 32, cap)
+    rep = O.PerReplay(cap, 32, 2e6, "cr")
+    data = O.synth_transitions(fill, 14, 8, seed=6)
+    eng.push(*data)
+    list(rep.store_transitions(*data))
+    rng = np.random.default_rng(7)
+    st = rep.replay_buffer
+    for r in range(rounds):
+        slots = rng.integers(0, fill, size=n).astype(np.int32)
+        slots[rng.integers(0, n, size=n // 8)] = slots[0]                   # duplicates
+        absd = (rng.random(n).astype(np.float32) * np.float32(3.0)) ** 3
+        absd[rng.random(n) < 0.1] = np.float32(0.0)
+        k = rng.integers(0, n, size=3)
+        slots[k[0]] = st.max_priority_index - (cap - 1)                     # lower the max leaf
+        absd[k[0]] = np.float32(1e-3)
+        slots[k[1]] = st.min_priority_index - (cap - 1)                     # raise the min leaf
+        absd[k[1]] = np.float32(5.0)
+        eng.per_update_priorities(torch.from_numpy(slots), torch.from_numpy(absd))
+        rep.update_batch_priorities((slots.astype(np.int64) + cap - 1).tolist(), absd.reshape(-1, 1))
+        torch.cuda.synchronize()
+        assert_tree_equal(eng, st)
+
+
+def test_gpu_per_sample_matches_oracle():
+    cap, fill, B = 3000, 2500, 256
+    eng = per_engine(14, B, cap)
+    rep = O.PerReplay(cap, B, 2e6, "cr")
+    data = O.synth_transitions(fill, 14, 8, seed=8)
+    eng.push(*data)
+    list(rep.store_transitions(*data))
+    rng = np.random.default_rng(9)
+    slots = rng.integers(0, fill, size=2000).astype(np.int32)
+    absd = rng.random(2000).astype(np.float32) * np.float32(2.0)
+    eng.per_update_priorities(torch.from_numpy(slots), torch.from_numpy(absd))
+    rep.update_batch_priorities((slots.astype(np.int64) + cap - 1).tolist(), absd.reshape(-1, 1))
+    np.random.seed(10)
+    nps = O.np_state_to_array()
+    eng.set_rng(1, nps)
+    for step in (0, 12345, 3_000_000):
+        eng.set_agent_step(step)
+        eng.per_sample()
+        isw, leaves, _ = rep.sample_transitions(step, nps)
+        torch.cuda.synchronize()
+        eng.check_device_error()
+        got = eng.batch_idx.cpu().numpy().astype(np.int64) + cap - 1
+        assert np.array_equal(got, np.asarray(leaves)), f"step {step}: leaves differ"
+        np.testing.assert_allclose(eng.is_weights.cpu().numpy(), np.asarray(isw, dtype=np.float32), rtol=2e-7, atol=0)
+        assert np.array_equal(eng.get_rng(1), nps)
+        assert abs(eng.ctrl().per_beta - rep.beta(step)) == 0.0
+        assert eng.ctrl().agent_step == step + 1
+
+
+def make_per_pair(obs_dim, batch, cap, n_fill, seed, graphs=True):
+    E = _E()
+    ospec = O.mlp_spec(obs_dim, 8, "dueling")
+    init = O.reference_init(ospec, seed)
+    oracle = O.OracleLearner(ospec, ALGO, batch, cap, seed=seed, params=init, per_pow="cr")
+    data = O.synth_transitions(n_fill, obs_dim, 8, seed=seed + 100)
+    O.fill_replay(oracle, *data)
+    eng = E.LearnEngine(E.mlp_spec(obs_dim, 8, "dueling"), ALGO, batch, cap, graphs=graphs)
+    eng.load_params(init)
+    eng.push(*data)
+    np.random.seed(seed + 11)
+    nps = O.np_state_to_array()
+    oracle.np_state = nps.copy()
+    eng.set_rng(1, nps)
+    return oracle, eng
+
+
+@pytest.mark.parametrize("obs_dim,batch,cap,n_fill,seed", [
+    (14, 32, 500, 300, 3),
+    (284, 256, 5000, 3000, 4),
+    (284, 1024, 20000, 20000, 5),
+])
+def test_gpu_per_learn_matches_oracle(obs_dim, batch, cap, n_fill, seed):
+    oracle, eng = make_per_pair(obs_dim, batch, cap, n_fill, seed)
+    for step in range(3):
+        rec = oracle.train_step()
+        eng.learn_step(soft_update=True)
+        torch.cuda.synchronize()
+        eng.check_device_error()
+        leaves = eng.batch_idx.cpu().numpy().astype(np.int64) + cap - 1
+        assert np.array_equal(leaves, rec.positions), f"step {step}: sampled leaves differ"
+        # IS weights depend on leaf priorities from earlier steps' |delta| (two devices, ~1e-6)
+        np.testing.assert_allclose(eng.is_weights.cpu().numpy(), rec.is_weights.astype(np.float32),
+                                   rtol=2e-7 if step == 0 else 1e-5)
+        np.testing.assert_allclose(eng.per_abs_td.cpu().numpy(), rec.abs_td.reshape(-1), atol=1e-5, rtol=0)
+        q = eng.q.cpu()
+        np.testing.assert_allclose(q[0].numpy(), rec.q_online.numpy(), atol=1e-5, rtol=0)
+        assert abs(eng.loss() - rec.loss) <= 1e-5 * max(1.0, abs(rec.loss))
+        g = eng.param_views(eng.grads[:-1])
+        for k, ref in rec.grads.items():
+            np.testing.assert_allclose(g[k].cpu().numpy(), ref.numpy(), atol=2e-6, rtol=1e-4, err_msg=k)
+        # the tree follows |delta| computed on two devices: equal when the fp32 |delta| agree
+        same = np.array_equal(eng.per_abs_td.cpu().numpy(), rec.abs_td.reshape(-1).astype(np.float32))
+        assert_tree_equal(eng, oracle.replay.replay_buffer, exact=same)
+        from test_gpu_engine import compare_state
+        compare_state(oracle, eng)
+    assert np.array_equal(eng.get_rng(1), oracle.np_state)
+
+
+def test_gpu_per_learn_golden():
+    """Against the reference's own PER steps (tests/golden, made by make_golden.py)."""
+    z = np.load(os.path.join(GOLDEN, "learn_mlp284_PerDuelingDoubleDQNAgent.npz"))
+    obs_dim, batch, cap = int(z["obs_dim"]), int(z["batch"]), int(z["buffer"])
+    init = O.reference_init(O.mlp_spec(obs_dim, 8, "dueling"), int(z["seed"]))
+    eng = per_engine(obs_dim, batch, cap)
+    eng.load_params(init)
+    eng.push(*O.synth_transitions(int(z["n_fill"]), obs_dim, 8, seed=int(z["seed"]) + 100))
+    eng.set_rng(1, z["np_state_in"])
+    for s in range(int(z["steps"])):
+        eng.learn_step(soft_update=True)
+        torch.cuda.synchronize()
+        eng.check_device_error()
+        assert np.array_equal(eng.batch_idx.cpu().numpy().astype(np.int64) + cap - 1, z["pos"][s])
+        np.testing.assert_allclose(eng.is_weights.cpu().numpy(), z["isw"][s].astype(np.float32), rtol=1e-6)
+        assert abs(eng.loss() - z["loss"][s]) <= 1e-5 * max(1.0, abs(z["loss"][s]))
+    assert np.array_equal(eng.get_rng(1), z["np_state_out"])
+    tree, mx, mn = tree_state(eng)
+    np.testing.assert_allclose(tree, z["tree"], rtol=1e-6, atol=1e-4)   # SVML powf (1 ulp) + |delta| 1e-6
+    assert mx == int(z["tree_max_idx"]) and mn == int(z["tree_min_idx"])
+    keys = [str(k) for k in z["keys"]]
+    on = eng.param_views(eng.params)
+    for i, k in enumerate(keys):
+        np.testing.assert_allclose(on[k].cpu().numpy().reshape(-1), z[f"online_{i}"], atol=1e-5, rtol=0)
+
+
+def test_gpu_per_graph_and_eager_identical():
+    o1, e1 = make_per_pair(284, 256, 3000, 3000, 31, graphs=True)
+    o2, e2 = make_per_pair(284, 256, 3000, 3000, 31, graphs=False)
+    for _ in range(4):
+        e1.learn_step(soft_update=True)
+        e2.learn_step(soft_update=True)
+    torch.cuda.synchronize()
+    assert torch.equal(e1.params, e2.params)
+    assert torch.equal(e1.sumtree, e2.sumtree)
