@@ -119,9 +119,14 @@ def cpu_baseline(args):
     sys.path.insert(0, REPO)
     from oracle import ref as O
     spec = O.mlp_spec(args.obs_dim, args.actions, "dueling")
-    L = O.OracleLearner(spec, args.algo, args.batch, args.capacity, seed=0)
-    obs, act, rew, done, nobs = O.synth_transitions(args.capacity, args.obs_dim, args.actions, seed=0)
-    L.replay.replay_buffer.extend(zip(obs, act, rew, done, nobs))
+    per = args.algo.startswith("Per")
+    cap = min(args.capacity, 100_000) if per else args.capacity   # Python SumTree fill is ~20 us/row
+    L = O.OracleLearner(spec, args.algo, args.batch, cap, seed=0)
+    obs, act, rew, done, nobs = O.synth_transitions(cap, args.obs_dim, args.actions, seed=0)
+    if per:
+        list(L.replay.store_transitions(obs, act, rew, done, nobs))
+    else:
+        L.replay.replay_buffer.extend(zip(obs, act, rew, done, nobs))
     random.seed(1234)
     L.py_state = O.py_state_to_array()
     for _ in range(2):
@@ -137,7 +142,7 @@ def cpu_baseline(args):
     return {"value": args.batch * steps / el, "unit": "transitions/s", "cores": torch.get_num_threads(),
             "kind": "port",
             "sample": f"oracle/ref.py OracleLearner {args.algo} MLP-{args.obs_dim} batch {args.batch}, "
-                      f"deque of {args.capacity} transitions, {steps} learn+soft-update steps in {el:.1f} s, "
+                      f"{'SumTree' if per else 'deque'} of {cap} transitions, {steps} learn+soft-update steps in {el:.1f} s, "
                       f"torch {torch.__version__} CPU, {torch.get_num_threads()} threads"}
 
 
@@ -163,6 +168,12 @@ def main():
     fill_ring(eng, args.capacity, args.obs_dim, args.actions, device, seed=0)
     random.seed(1234)   # the replay sampler continues CPython's global MT19937 stream
     eng.set_rng(C.DQNX_RNG_PY, np.array(random.getstate()[1], dtype=np.uint32))
+    per = args.algo.startswith("Per")
+    if per:             # PER draws numpy's legacy global stream (np.random.uniform)
+        np.random.seed(1234)
+        st = np.random.get_state()
+        eng.set_rng(C.DQNX_RNG_NP, np.append(st[1], st[2]).astype(np.uint32))
+    Bl = args.batch
 
     prefetch = args.prefetch
 
@@ -170,6 +181,8 @@ def main():
         if world > 1:
             eng.learn_step(grads_only=True, prefetch=prefetch)
             dist.all_reduce(eng.grads)
+            if per:   # every rank applies the same ordered priority update to its tree replica
+                dist.all_gather_into_tensor(eng.per_abs_td, eng.per_abs_td[rank * Bl:(rank + 1) * Bl])
             eng.apply_grads(soft_update=True)
         else:
             eng.learn_step(soft_update=True, prefetch=prefetch)

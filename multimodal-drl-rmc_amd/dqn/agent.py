@@ -1,0 +1,260 @@
+"""Drop-in `dqn.agent`: the reference's four agents (R:dqn/agent.py:18-320), with
+`learn()` running on the MI355X learn engine (libdqnx).
+
+The same class names, constructor keywords and public methods are kept, so `train.py`'s
+`getattr(Agents, args.algo)(...)` works unchanged.  The methods are `learn`,
+`store_transitions`, `choose_actions`, `epsilon`, `update_target_network`, `load_model`,
+`save_model`, `log`, `info_mean` and `transitions_to_tensor`.
+
+What changes underneath:
+
+* The replay memory is the engine's HBM ring (+ SumTree for PER).
+* Both networks' parameters are views into the engine's flat parameter buffers.
+* The Adam moments live in the engine.
+* `learn()` is one stream-ordered launch sequence: sample → gather → forwards → TD → loss →
+  backward → Adam.
+
+Host-visible RNG semantics are the reference's.
+* `random.sample` (uniform replay) continues Python's global MT19937 stream.
+* PER's `np.random.uniform` continues numpy's global legacy stream.
+Both are handed to the engine before the step and taken back after it, so
+`choose_actions`' ε-greedy draws interleave exactly as in the reference.
+"""
+from __future__ import annotations
+
+import random
+import time
+from collections import deque
+from datetime import timedelta
+
+import numpy as np
+import torch as T
+
+from . import _capi as C
+from .engine import LearnEngine, spec_from_body
+from .network import DeepQNetwork, DuelingDeepQNetwork
+from .replay_memory import ReplayMemoryNaive, ReplayMemoryPrioritized
+
+
+def _summary_writer(log_dir):
+    try:
+        from torch.utils.tensorboard import SummaryWriter
+        return SummaryWriter(log_dir)
+    except Exception:   # tensorboard is optional: logging is out of the hot path
+        class _Null:
+            def add_scalar(self, *a, **k):
+                pass
+
+            def close(self):
+                pass
+        return _Null()
+
+
+def _obs_dim(input_dim) -> int:
+    shape = getattr(input_dim, "shape", None)
+    if shape is not None:
+        return int(np.prod(shape))
+    return int(input_dim)
+
+
+class Agent:
+    """R:dqn/agent.py:18-147."""
+
+    _network_cls = None
+    _reduction = "mean"
+
+    def __init__(self, n_env, lr, gamma, epsilon_start, epsilon_min, epsilon_decay, epsilon_exp_decay, nn_conf_func,
+                 input_dim, output_dim, batch_size, min_buffer_size, buffer_size, update_target_frequency,
+                 target_soft_update, target_soft_update_tau, save_frequency, log_frequency, save_dir, log_dir, load,
+                 algo, gpu):
+        self.n_env = n_env
+        self.lr = lr
+        self.gamma = gamma
+        self.epsilon_start = epsilon_start
+        self.epsilon_min = epsilon_min
+        self.epsilon_decay = epsilon_decay
+        self.epsilon_exp_decay = epsilon_exp_decay
+        self.nn_conf_func = nn_conf_func
+        self.input_dim = input_dim
+        self.output_dim = output_dim
+        self.batch_size = batch_size
+        self.min_buffer_size = min_buffer_size
+        self.buffer_size = buffer_size
+        self.update_target_frequency = update_target_frequency
+        self.target_soft_update = target_soft_update
+        self.target_soft_update_tau = target_soft_update_tau
+        self.save_frequency = save_frequency
+        self.log_frequency = log_frequency
+        self.load = load
+
+        self.step = 0
+        self.resume_step = 0
+        self.episode_count = 0
+        self.ep_info_buffer = deque([], maxlen=50)
+
+        path = algo + '_lr' + str(lr)
+        self.save_path = save_dir + path + '_' + 'model.pack'
+        self.summary_writer = _summary_writer(log_dir + path + '/')
+
+        if not T.cuda.is_available():
+            raise RuntimeError("the dqn learn engine needs a ROCm GPU (MI355X); there is no CPU path")
+        self.device = T.device("cuda:" + str(gpu))
+        self.start_time = time.time()
+        self.algo = algo
+        self._build()
+
+    # -- composition (R:dqn/agent.py:275-320) ------------------------------------------
+    def _build(self):
+        cls = type(self)._network_cls
+        # same construction order as the reference: online, then target (torch RNG stream)
+        self.online_network = cls(self.device, self.lr, self.nn_conf_func, self.input_dim, self.output_dim,
+                                  reduction=self._reduction)
+        self.target_network = cls(self.device, self.lr, self.nn_conf_func, self.input_dim, self.output_dim,
+                                  reduction=self._reduction)
+        spec = spec_from_body(self.online_network.net, _obs_dim(self.input_dim), self.output_dim,
+                              dueling=cls is DuelingDeepQNetwork)
+        self.engine = LearnEngine(spec, type(self).__name__, self.batch_size, self.buffer_size, gamma=self.gamma,
+                                  lr=self.lr, tau=self.target_soft_update_tau, n_env=self.n_env, device=self.device,
+                                  eps_dec=self.epsilon_decay)
+        self.online_network.bind_flat(self.engine.param_views(self.engine.params))
+        self.target_network.bind_flat(self.engine.param_views(self.engine.target_params))
+        self.replay_memory_buffer = self._make_replay()
+        self._engine_step = 0          # agent.step * n_env the engine will use next (PER)
+        self.update_target_network(force=True)
+
+    def _make_replay(self):
+        return ReplayMemoryNaive(self.buffer_size, self.batch_size, engine=self.engine)
+
+    # -- replay ------------------------------------------------------------------------
+    def transitions_to_tensor(self, transitions):
+        """R:dqn/agent.py:71-78 (API compatibility; learn() gathers on the device)."""
+        obses_t = T.as_tensor(np.asarray([t[0] for t in transitions]), dtype=T.float32).to(self.device)
+        actions_t = T.as_tensor(np.asarray([t[1] for t in transitions]), dtype=T.int64).to(self.device).unsqueeze(-1)
+        rews_t = T.as_tensor(np.asarray([t[2] for t in transitions]), dtype=T.float32).to(self.device).unsqueeze(-1)
+        dones_t = T.as_tensor(np.asarray([t[3] for t in transitions]), dtype=T.float32).to(self.device).unsqueeze(-1)
+        new_obses_t = T.as_tensor(np.asarray([t[4] for t in transitions]), dtype=T.float32).to(self.device)
+        return obses_t, actions_t, rews_t, dones_t, new_obses_t
+
+    def store_transitions(self, obses, actions, rews, dones, new_obses, infos):
+        """R:dqn/agent.py:80-84."""
+        for i in self.replay_memory_buffer.store_transitions(obses, actions, rews, dones, new_obses):
+            if infos:
+                self.ep_info_buffer.append({'r': infos[i]['r'], 'l': infos[i]['l']})
+                self.episode_count += 1
+
+    # -- acting (R:dqn/agent.py:86-99) -------------------------------------------------
+    def epsilon(self):
+        if self.epsilon_exp_decay:
+            return np.exp(np.interp(self.step * self.n_env, [0, self.epsilon_decay],
+                                    [np.log(self.epsilon_start), np.log(self.epsilon_min)]))
+        return np.interp(self.step * self.n_env, [0, self.epsilon_decay], [self.epsilon_start, self.epsilon_min])
+
+    def choose_actions(self, obses):
+        actions = self.online_network.actions(obses)
+        for i in range(len(actions)):
+            if random.random() <= self.epsilon():
+                actions[i] = random.randint(0, self.output_dim - 1)
+        return actions
+
+    # -- learning ----------------------------------------------------------------------
+    def learn(self):
+        """One learn step on the engine (R:dqn/agent.py:166-185 / 204-226 / 245-272)."""
+        e = self.engine
+        e.set_py_state_from_global()
+        e.learn_step(soft_update=False)
+        e.get_py_state_to_global()       # synchronises the stream
+
+    def update_target_network(self, force=False):
+        """R:dqn/agent.py:101-110."""
+        if (not self.target_soft_update and self.step % (self.update_target_frequency // self.n_env) == 0) or force:
+            self.engine.hard_update()
+        elif self.target_soft_update:
+            self.engine.soft_update()
+
+    # -- checkpoints / logging (R:dqn/agent.py:112-147) ---------------------------------
+    def load_model(self):
+        import os
+        if self.load and os.path.exists(self.save_path):
+            print()
+            print("Resume training from " + self.save_path + "...")
+            self.resume_step, self.episode_count, rew_mean, len_mean = self.online_network.load(self.save_path)
+            [self.ep_info_buffer.append({'r': rew_mean, 'l': len_mean})
+             for _ in range(np.min([self.episode_count, self.ep_info_buffer.maxlen]))]
+            print("Step: ", self.resume_step * self.n_env, ", Episodes: ", self.episode_count, ", Avg Rew: ",
+                  rew_mean, ", Avg Ep Len: ", len_mean)
+            self.update_target_network(force=True)
+            self.step = self.resume_step
+
+    def save_model(self):
+        if self.step % self.save_frequency == 0 and self.step > self.resume_step:
+            print()
+            print("Saving model...")
+            T.cuda.synchronize(self.device)
+            self.online_network.save(self.save_path, self.step, self.episode_count, self.info_mean('r'),
+                                     self.info_mean('l'))
+            print("OK!")
+
+    def log(self):
+        if self.step % self.log_frequency == 0 and self.step > self.resume_step:
+            rew_mean, len_mean = self.info_mean('r'), self.info_mean('l')
+            print()
+            print('Step: ', self.step * self.n_env, ' (' + str(self.step) + 'x' + str(self.n_env) + ')')
+            print('Avg Rew: ', rew_mean)
+            print('Avg Ep Len: ', len_mean)
+            print('Episodes: ', self.episode_count)
+            print('---', str(timedelta(seconds=round((time.time() - self.start_time), 0))), '---')
+            self.summary_writer.add_scalar('AvgRew', rew_mean, global_step=self.step * self.n_env)
+            self.summary_writer.add_scalar('AvgEpLen', len_mean, global_step=self.step * self.n_env)
+            self.summary_writer.add_scalar('Episodes', self.episode_count, global_step=self.step * self.n_env)
+            self.summary_writer.add_scalar('Loss', self.engine.loss(), global_step=self.step * self.n_env)
+
+    def info_mean(self, i):
+        i_mean = np.mean([e[i] for e in self.ep_info_buffer])
+        return i_mean if not np.isnan(i_mean) else 0.0
+
+
+class SimpleAgent(Agent):
+    """R:dqn/agent.py:150-185 (vanilla DQN target: max over the target network)."""
+
+
+class DoubleAgent(Agent):
+    """R:dqn/agent.py:188-226 (Double DQN target)."""
+
+
+class PerDoubleAgent(Agent):
+    """R:dqn/agent.py:229-272 (prioritised replay, IS-weighted Huber)."""
+
+    _reduction = "none"
+
+    def _make_replay(self):
+        return ReplayMemoryPrioritized(self.buffer_size, self.batch_size, self.epsilon_decay, engine=self.engine)
+
+    def learn(self):
+        e = self.engine
+        step = self.step * self.n_env                      # R:dqn/agent.py:247
+        if step != self._engine_step:
+            e.set_agent_step(step)
+        e.set_np_state_from_global()
+        e.learn_step(soft_update=False)                   # advances the engine's step by n_env
+        e.get_np_state_to_global()
+        self._engine_step = step + self.n_env
+
+
+class DQNAgent(SimpleAgent):
+    """R:dqn/agent.py:275-284."""
+    _network_cls = DeepQNetwork
+
+
+class DoubleDQNAgent(DoubleAgent):
+    """R:dqn/agent.py:287-296."""
+    _network_cls = DeepQNetwork
+
+
+class DuelingDoubleDQNAgent(DoubleAgent):
+    """R:dqn/agent.py:299-308."""
+    _network_cls = DuelingDeepQNetwork
+
+
+class PerDuelingDoubleDQNAgent(PerDoubleAgent):
+    """R:dqn/agent.py:311-320."""
+    _network_cls = DuelingDeepQNetwork

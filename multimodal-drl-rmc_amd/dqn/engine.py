@@ -10,6 +10,7 @@ No CPU fallback: constructing an engine without a GPU or without libdqnx.so rais
 from __future__ import annotations
 
 import ctypes
+import random
 from dataclasses import dataclass
 from typing import Optional, Sequence, Tuple
 
@@ -282,6 +283,25 @@ class LearnEngine:
         C.check(self.L.dqnx_per_update_priorities(self.h, ctypes.c_void_p(slots.data_ptr()),
                                                   ctypes.c_void_p(abs_td.data_ptr()), int(slots.numel()),
                                                   self.stream()), "per_update_priorities")
+
+    # numpy's global legacy RandomState <-> the engine (PER draws np.random.uniform words)
+    def set_np_state_from_global(self):
+        st = np.random.get_state()
+        self.set_rng(C.DQNX_RNG_NP, np.append(np.asarray(st[1], dtype=np.uint32), np.uint32(st[2])))
+
+    def get_np_state_to_global(self):
+        a = self.get_rng(C.DQNX_RNG_NP)
+        st = np.random.get_state()
+        np.random.set_state((st[0], a[:624].copy(), int(a[624]), st[3], st[4]))
+
+    # CPython's global random state <-> the engine (the uniform sampler's random.sample)
+    def set_py_state_from_global(self):
+        self.set_rng(C.DQNX_RNG_PY, np.asarray(random.getstate()[1], dtype=np.uint32))
+
+    def get_py_state_to_global(self):
+        a = self.get_rng(C.DQNX_RNG_PY)
+        v, _, g = random.getstate()
+        random.setstate((v, tuple(int(x) for x in a), g))
 
     def set_agent_step(self, step_times_n_env: int):
         C.check(self.L.dqnx_set_agent_step(self.h, int(step_times_n_env), self.stream()), "set_agent_step")

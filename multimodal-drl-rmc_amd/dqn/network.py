@@ -1,0 +1,105 @@
+"""Drop-in `dqn.network`: the reference's Q-network classes (R:dqn/network.py:11-117).
+
+The classes keep the reference's constructor, attribute and method surface
+(`Net(device, lr, nn_conf_func, input_dim, output_dim, reduction)`, `.net`, `.fc_out` /
+`.fc_val` + `.fc_adv`, `.optimizer`, `.loss`, `forward`, `actions`, `value`, `advantages`,
+`save`, `load`, `state_dict()` keys), so `Agents` / Observe code constructs them unchanged.
+
+When an agent owns the network, `bind_flat()` re-points every parameter at its slice of
+the learn engine's flat fp32 buffer (online or target).  From then on `state_dict()`,
+`load_state_dict()`, `save()` and `forward()` read and write the same HBM the engine
+trains, with no copies.  The engine (not `.optimizer`) holds the Adam moments; see
+`dqn.agent`.
+"""
+from __future__ import annotations
+
+import torch as T
+import torch.nn as nn
+
+from .utils.pack import load_pack, save_pack
+
+
+class Network(nn.Module):
+    """R:dqn/network.py:11-47."""
+
+    def __init__(self, device, nn_conf_func, input_dim):
+        super().__init__()
+        self.net, self.fc_out_dim, optim_func, loss_func = nn_conf_func(input_dim)
+        self.optim_func = (lambda params, lr: optim_func(params, lr=lr))
+        self.loss_func = (lambda reduction: loss_func(reduction=reduction))
+        self.device = device
+
+    def forward(self, s):
+        raise NotImplementedError
+
+    def actions(self, obses):
+        raise NotImplementedError
+
+    # -- engine binding -------------------------------------------------------------
+    def bind_flat(self, views: dict):
+        """Move every parameter into `views[name]` (same shape, engine memory), keeping
+        the Parameter objects (so `.optimizer` and module references stay valid)."""
+        with T.no_grad():
+            for name, p in self.named_parameters():
+                v = views[name]
+                if tuple(v.shape) != tuple(p.shape):
+                    raise ValueError(f"{name}: engine shape {tuple(v.shape)} != {tuple(p.shape)}")
+                v.copy_(p.data.to(v.device, T.float32))
+                p.data = v
+
+    # -- checkpoints (R:dqn/network.py:27-47; format: dqn.utils.pack) -----------------
+    def save(self, save_path, step, episode_count, rew_mean, len_mean):
+        params = {k: v.detach().cpu().numpy() for k, v in self.state_dict().items()}
+        save_pack(save_path, params, step, episode_count, rew_mean, len_mean)
+
+    def load(self, load_path):
+        params, step, episode_count, rew_mean, len_mean = load_pack(load_path)
+        self.load_state_dict({k: T.as_tensor(v, device=self.device) for k, v in params.items()})
+        return step, episode_count, rew_mean, len_mean
+
+
+class DeepQNetwork(Network):
+    """R:dqn/network.py:50-74."""
+
+    def __init__(self, device, lr, nn_conf_func, input_dim, output_dim, reduction='mean'):
+        super().__init__(device, nn_conf_func, input_dim)
+        self.fc_out = nn.Linear(self.fc_out_dim, output_dim)
+        self.optimizer = self.optim_func(self.parameters(), lr=lr)
+        self.loss = self.loss_func(reduction=reduction)
+        self.to(self.device)
+
+    def forward(self, s):
+        return self.fc_out(self.net(s))
+
+    def actions(self, obses):
+        obses_t = T.as_tensor(obses, dtype=T.float32).to(self.device)
+        q_values = self(obses_t)
+        return T.argmax(q_values, dim=1).detach().tolist()
+
+
+class DuelingDeepQNetwork(Network):
+    """R:dqn/network.py:77-117.  Acting uses the advantage stream only (:110-117)."""
+
+    def __init__(self, device, lr, nn_conf_func, input_dim, output_dim, reduction='mean'):
+        super().__init__(device, nn_conf_func, input_dim)
+        self.fc_val = nn.Linear(self.fc_out_dim, 1)
+        self.fc_adv = nn.Linear(self.fc_out_dim, output_dim)
+        self.aggregate_layer = (lambda val, adv: T.add(val, (adv - adv.mean(dim=1, keepdim=True))))
+        self.optimizer = self.optim_func(self.parameters(), lr=lr)
+        self.loss = self.loss_func(reduction=reduction)
+        self.to(self.device)
+
+    def forward(self, s):
+        net = self.net(s)
+        return self.aggregate_layer(self.fc_val(net), self.fc_adv(net))
+
+    def value(self, s):
+        return self.fc_val(self.net(s))
+
+    def advantages(self, s):
+        return self.fc_adv(self.net(s))
+
+    def actions(self, obses):
+        obses_t = T.as_tensor(obses, dtype=T.float32).to(self.device)
+        adv_q_values = self.advantages(obses_t)
+        return T.argmax(adv_q_values, dim=1).detach().tolist()

@@ -1,0 +1,70 @@
+"""CPU checks of the drop-in Python surface (dqn.network / dqn.utils.pack / dqn.agent)."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from dqn import Agents, Networks
+from dqn.utils import pack
+from oracle import ref as O
+from refnets import Box, agent_kwargs, mlp_network_config
+
+REF_PACK = "/root/reference/env/custom_env/macro with lane/DuelingDoubleDQNAgent_lr0.0001_model_2e6_1e6.pack"
+
+
+@pytest.mark.parametrize("cls,head", [(Networks.DuelingDeepQNetwork, "dueling"), (Networks.DeepQNetwork, "linear")])
+def test_networks_match_reference_init_and_names(cls, head):
+    torch.manual_seed(3)
+    net = cls(torch.device("cpu"), 1e-4, mlp_network_config, Box(284), 8)
+    ref = O.reference_init(O.mlp_spec(284, 8, head), 3)
+    sd = net.state_dict()
+    assert list(sd.keys()) == list(ref.keys())
+    for k in ref:
+        assert torch.equal(sd[k], ref[k]), k
+    assert isinstance(net.loss, torch.nn.SmoothL1Loss) and isinstance(net.optimizer, torch.optim.Adam)
+
+
+def test_pack_roundtrip(tmp_path):
+    torch.manual_seed(0)
+    net = Networks.DuelingDeepQNetwork(torch.device("cpu"), 1e-4, mlp_network_config, Box(14), 8)
+    p = str(tmp_path / "m.pack")
+    net.save(p, 123, 7, np.float64(1.5), 90.0)
+    torch.manual_seed(1)
+    net2 = Networks.DuelingDeepQNetwork(torch.device("cpu"), 1e-4, mlp_network_config, Box(14), 8)
+    assert net2.load(p) == (123, 7, 1.5, 90.0)
+    for k, v in net.state_dict().items():
+        assert torch.equal(v, net2.state_dict()[k])
+
+
+@pytest.mark.skipif(not os.path.exists(REF_PACK), reason="reference checkpoint not present")
+def test_loads_reference_checkpoint():
+    """A .pack written by the reference's Network.save loads into the drop-in network."""
+    params, step, eps, rew, ln = pack.load_pack(REF_PACK)
+    net = Networks.DuelingDeepQNetwork(torch.device("cpu"), 1e-4, mlp_network_config, Box(14), 8)
+    assert net.load(REF_PACK) == (step, eps, rew, ln)
+    for k, v in net.state_dict().items():
+        assert np.array_equal(v.numpy(), params[k])
+    blob = pack.dumps({"parameters": params, "step": step, "episode_count": eps, "rew_mean": rew,
+                       "len_mean": ln})
+    assert pack.loads(blob)["step"] == step
+
+
+def test_agent_without_gpu_fails_loudly(tmp_path):
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    with pytest.raises(RuntimeError):
+        Agents.DuelingDoubleDQNAgent(**agent_kwargs("DuelingDoubleDQNAgent", 14, 32, 500, tmp_path))
+
+
+def test_agent_classes_and_constructor_surface():
+    import inspect
+    names = ["DQNAgent", "DoubleDQNAgent", "DuelingDoubleDQNAgent", "PerDuelingDoubleDQNAgent"]
+    for n in names:
+        assert hasattr(Agents, n)
+    sig = inspect.signature(Agents.Agent.__init__)
+    assert list(sig.parameters)[1:] == [
+        "n_env", "lr", "gamma", "epsilon_start", "epsilon_min", "epsilon_decay", "epsilon_exp_decay",
+        "nn_conf_func", "input_dim", "output_dim", "batch_size", "min_buffer_size", "buffer_size",
+        "update_target_frequency", "target_soft_update", "target_soft_update_tau", "save_frequency",
+        "log_frequency", "save_dir", "log_dir", "load", "algo", "gpu"]
