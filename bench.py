@@ -33,6 +33,7 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(REPO, "multimodal-drl-rmc_amd"))
 
 from dqn import _capi as C  # noqa: E402
+from dqn.data_parallel import dp_learn_step  # noqa: E402
 from dqn.engine import LearnEngine, mlp_spec  # noqa: E402
 
 PEAK_FP32_MFMA_TFLOPS = 157.3   # MI355X_MICROARCH.md: F32 matrix, dense
@@ -153,12 +154,18 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if args.gpus != world and world > 1:
         log(f"warning: --gpus {args.gpus} != WORLD_SIZE {world}; using WORLD_SIZE")
-    torch.cuda.set_device(local_rank)
-    device = torch.device("cuda", local_rank)
+    # rehearsal knobs for a 1-GPU box: every rank on cuda:0, gloo collectives
+    dev_index = 0 if os.environ.get("DQNX_SINGLE_DEVICE") == "1" else local_rank
+    torch.cuda.set_device(dev_index)
+    device = torch.device("cuda", dev_index)
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=device)
+        backend = os.environ.get("DQNX_DIST_BACKEND", "nccl")   # nccl = RCCL over xGMI
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=device)
+        else:
+            dist.init_process_group(backend)
 
     spec = mlp_spec(args.obs_dim, args.actions, "dueling" if "Dueling" in args.algo else "linear")
     Bg = args.batch * world
@@ -178,12 +185,8 @@ def main():
     prefetch = args.prefetch
 
     def step():
-        if world > 1:
-            eng.learn_step(grads_only=True, prefetch=prefetch)
-            dist.all_reduce(eng.grads)
-            if per:   # every rank applies the same ordered priority update to its tree replica
-                dist.all_gather_into_tensor(eng.per_abs_td, eng.per_abs_td[rank * Bl:(rank + 1) * Bl])
-            eng.apply_grads(soft_update=True)
+        if world > 1:   # shard compute, RCCL all-reduce (+ PER |delta| all-gather), replicated Adam
+            dp_learn_step(eng, soft_update=True)
         else:
             eng.learn_step(soft_update=True, prefetch=prefetch)
 
@@ -226,9 +229,7 @@ def main():
             infos.append((nm.value.decode(), fl.value, by.value))
         # consume a pending prefetched minibatch so the timing steps sample themselves
         if world > 1:
-            eng.learn_step(grads_only=True)
-            dist.all_reduce(eng.grads)
-            eng.apply_grads(soft_update=True)
+            dp_learn_step(eng, soft_update=True)
         else:
             eng.learn_step(soft_update=True)
         K = max(args.steps, 50)

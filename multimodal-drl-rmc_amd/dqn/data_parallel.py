@@ -1,0 +1,45 @@
+"""Data-parallel learn step: one process per GPU, minibatch sharded, one gradient all-reduce
+(SURVEY.md §8(e)).
+
+Every rank runs the same sampler on the same RNG state, so all ranks draw the identical
+global minibatch (bit-exact with one GPU). Rank r then computes samples
+[r*B/W, (r+1)*B/W) with `DQNX_STEP_GRADS_ONLY`. The loss is a mean over the GLOBAL batch
+(the engine scales by 1/B_global), so the SUM of the shard gradients is the full-batch
+gradient. Everything after that is identical on every rank:
+
+* one all-reduce (sum) of the flat gradient buffer (+ the loss slot) moves the gradient;
+* PER only: one all-gather of the shards' |δ| gives every rank the ordered priority update
+  for its tree replica (R:dqn/agent.py:263-265);
+* `dqnx_apply_grads` (Adam + soft update, and the PER tree update) runs on every rank.
+
+With backend "nccl" (RCCL on ROCm) the collectives run over xGMI. The same code runs under
+"gloo" for the CPU tests.
+"""
+from __future__ import annotations
+
+import torch
+import torch.distributed as dist
+
+
+def shard_bounds(batch: int, world: int, rank: int):
+    per = batch // world
+    return rank * per, (rank + 1) * per
+
+
+def dp_learn_step(engine, soft_update: bool = True, group=None):
+    """One data-parallel learn step (+ soft target update) on `engine` (a LearnEngine built
+    with world_size / rank).  Collectives are enqueued on the current stream."""
+    engine.learn_step(grads_only=True)
+    exchange(engine, group)
+    engine.apply_grads(soft_update=soft_update)
+
+
+def exchange(engine, group=None):
+    """The exchange step between the shard gradients and the optimizer."""
+    dist.all_reduce(engine.grads, op=dist.ReduceOp.SUM, group=group)
+    if engine.per_abs_td.numel():
+        world = engine.world_size
+        b0, b1 = shard_bounds(engine.batch, world, engine.rank)
+        parts = list(engine.per_abs_td.chunk(world))
+        mine = engine.per_abs_td[b0:b1].clone()
+        dist.all_gather(parts, mine, group=group)

@@ -506,8 +506,12 @@ class OracleLearner:
     def _q(self, P, x):
         return q_forward(self.spec, P, x)
 
-    def learn(self) -> StepRecord:
+    def learn(self, shard: Optional[Tuple[int, int]] = None) -> StepRecord:
+        """Agent.learn.  With shard=(b0, b1) (data-parallel restatement) the loss
+        is the shard's share of the global-batch mean, only the gradient is produced (no Adam,
+        no priority update) and apply_grads() finishes the step with the all-reduced sum."""
         rec = StepRecord()
+        B = self.batch_size
         if self.per:
             is_w, idxs, transitions = self.replay.sample_transitions(self.step * self.n_env, self.np_state)
             rec.positions = np.asarray(idxs, dtype=np.int64)
@@ -541,19 +545,30 @@ class OracleLearner:
             with torch.no_grad():
                 abs_td = torch.abs(targets - qa).detach().cpu().numpy()
                 rec.abs_td = abs_td
-                self.replay.update_batch_priorities(rec.positions.tolist(), abs_td)
-            loss = torch.mean(is_weights_t * F.smooth_l1_loss(qa, targets, reduction="none"))
-        else:
+                if shard is None:
+                    self.replay.update_batch_priorities(rec.positions.tolist(), abs_td)
+            per_sample = is_weights_t * F.smooth_l1_loss(qa, targets, reduction="none")
+            loss = torch.mean(per_sample) if shard is None else per_sample[shard[0]:shard[1]].sum() / B
+        elif shard is None:
             loss = F.smooth_l1_loss(qa, targets, reduction="mean")
+        else:
+            loss = F.smooth_l1_loss(qa[shard[0]:shard[1]], targets[shard[0]:shard[1]], reduction="sum") / B
         rec.loss = float(loss.item())
         grads = torch.autograd.grad(loss, list(params.values()))
         rec.grads = OrderedDict(zip(params.keys(), [g.detach() for g in grads]))
+        if shard is None:
+            self.apply_grads(rec.grads)
+        return rec
 
+    def apply_grads(self, grads, abs_td=None, positions=None):
+        """optimizer.step() with the given (all-reduced) gradient; under DP also the PER
+        priority update from the all-gathered |delta|."""
+        if self.per and abs_td is not None:
+            self.replay.update_batch_priorities(list(positions), np.asarray(abs_td, dtype=np.float32).reshape(-1, 1))
         self.adam_step += 1
         with torch.no_grad():
             for k in self.online:
-                adam_update(self.online[k], rec.grads[k], self.m[k], self.v[k], self.adam_step, self.lr)
-        return rec
+                adam_update(self.online[k], grads[k], self.m[k], self.v[k], self.adam_step, self.lr)
 
     def update_target_network(self, force=False):             # R:dqn/agent.py:101-110
         if (not self.target_soft_update and self.step % (self.update_target_frequency // self.n_env) == 0) or force:

@@ -1,0 +1,44 @@
+"""One rank of tests/test_gpu_dp.py: a LearnEngine shard driven by dqn.data_parallel."""
+import os
+import sys
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(HERE)
+sys.path[:0] = [REPO, os.path.join(REPO, "multimodal-drl-rmc_amd")]
+
+from dqn import engine as E  # noqa: E402
+from dqn.data_parallel import dp_learn_step  # noqa: E402
+from oracle import ref as O  # noqa: E402  (test data + initial weights only)
+
+
+def main():
+    rank, world, algo, out = int(sys.argv[1]), int(sys.argv[2]), sys.argv[3], sys.argv[4]
+    backend = os.environ.get("DQNX_TEST_BACKEND", "gloo")
+    torch.cuda.set_device(0)
+    dist.init_process_group(backend, rank=rank, world_size=world)
+    obs_dim, batch, cap, fill, seed = 284, 64, 1000, 700, 9
+    head = O.algo_spec_head(algo)
+    eng = E.LearnEngine(E.mlp_spec(obs_dim, 8, head), algo, batch, cap, world_size=world, rank=rank)
+    eng.load_params(O.reference_init(O.mlp_spec(obs_dim, 8, head), seed))
+    eng.push(*O.synth_transitions(fill, obs_dim, 8, seed=seed + 100))
+    eng.set_rng(0, O.py_state_to_array(__import__("random").Random(seed).getstate()))
+    eng.set_rng(1, O.np_state_to_array(np.random.RandomState(seed).get_state()))
+    losses, pos = [], []
+    for _ in range(3):
+        dp_learn_step(eng, soft_update=True)
+        torch.cuda.synchronize()
+        eng.check_device_error()
+        losses.append(float(eng.grads[-1].item()))
+        pos.append(eng.batch_idx.cpu().numpy().copy())
+    np.savez(os.path.join(out, f"rank{rank}.npz"), losses=np.array(losses), positions=np.stack(pos),
+             params=eng.params.cpu().numpy(), target=eng.target_params.cpu().numpy(),
+             tree=eng.sumtree.cpu().numpy())
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

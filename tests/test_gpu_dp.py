@@ -1,0 +1,49 @@
+"""GPU: the data-parallel learn step with 2 ranks (two processes sharing the box's one GPU,
+gloo collectives on device tensors) against the single-process oracle."""
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+from oracle import ref as O
+
+pytestmark = pytest.mark.gpu
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+@pytest.mark.parametrize("algo", ["DuelingDoubleDQNAgent", "PerDuelingDoubleDQNAgent"])
+def test_gpu_dp_world2_matches_oracle(tmp_path, algo):
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(free_port()))
+    procs = [subprocess.Popen([sys.executable, os.path.join(HERE, "dp_gpu_worker.py"), str(r), "2", algo,
+                               str(tmp_path)], env=env) for r in range(2)]
+    for p in procs:
+        assert p.wait(timeout=240) == 0
+    obs_dim, batch, cap, fill, seed = 284, 64, 1000, 700, 9
+    spec = O.mlp_spec(obs_dim, 8, O.algo_spec_head(algo))
+    ref = O.OracleLearner(spec, algo, batch, cap, seed=seed, params=O.reference_init(spec, seed), per_pow="cr")
+    O.fill_replay(ref, *O.synth_transitions(fill, obs_dim, 8, seed=seed + 100))
+    import random
+    ref.py_state = O.py_state_to_array(random.Random(seed).getstate())
+    ref.np_state = O.np_state_to_array(np.random.RandomState(seed).get_state())
+    recs = [ref.train_step() for _ in range(3)]
+    flat_on = np.concatenate([v.reshape(-1).numpy() for v in ref.online.values()])
+    flat_tg = np.concatenate([v.reshape(-1).numpy() for v in ref.target.values()])
+    z0, z1 = (np.load(tmp_path / f"rank{r}.npz") for r in (0, 1))
+    for z in (z0, z1):
+        got = z["positions"].astype(np.int64) + (cap - 1 if ref.per else 0)
+        assert np.array_equal(got, np.stack([np.asarray(r.positions) for r in recs]))
+        np.testing.assert_allclose(z["losses"], [r.loss for r in recs], rtol=1e-5, atol=1e-6)
+        np.testing.assert_allclose(z["params"], flat_on, atol=1e-5, rtol=0)
+        np.testing.assert_allclose(z["target"], flat_tg, atol=1e-5, rtol=0)
+        if ref.per:
+            np.testing.assert_allclose(z["tree"], ref.replay.replay_buffer.tree, rtol=1e-6, atol=1e-4)
+    assert np.array_equal(z0["params"], z1["params"]) and np.array_equal(z0["tree"], z1["tree"])
