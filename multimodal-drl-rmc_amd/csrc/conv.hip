@@ -1,0 +1,141 @@
+// Data movement of the two-stream hybrid Q-network (TwoStreamHybridNetwork,
+// R:env/dqn_config.py:66-143): im2col / col2im around the MFMA GEMMs that carry the
+// convolutions, and the flatten + concat in front of the dense stream.
+//
+// Layouts.  The obs row is [macro (macro_len) | micro grid (c,h,w) flattened CHW]
+// (R:env/dqn_config.py:126-133).  Conv activations are kept in GEMM layout
+// [rows = (b, ho, wo)][channels] (NHWC), so a conv is C[m][n] = A[m][k] W[n][k] with
+// k = (ci, i, j): torch's weight [Cout][Cin][kh][kw] is already row n = output channel,
+// K-contiguous, so the weight needs no permutation.  The dense stream's input is
+// cat(flatten_CHW(last conv), macro) (:135-138), materialised as F[b][strideF].
+#include "learn.hpp"
+
+namespace dqnx {
+
+__global__ __launch_bounds__(256) void k_im2col(Im2colArgs a) {
+    const int64_t per = (int64_t)a.M * a.Kstride;
+    const int64_t total = per * a.nstreams;
+    const int HoWo = a.Ho * a.Wo, KK = a.kh * a.kw;
+    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
+        const int z = (int)(t / per);
+        const int64_t rem = t - (int64_t)z * per;
+        const int m = (int)(rem / a.Kstride);
+        const int kk = (int)(rem - (int64_t)m * a.Kstride);
+        float v = 0.f;
+        if (kk < a.K) {
+            const int b = m / HoWo, p = m - b * HoWo;
+            const int ho = p / a.Wo, wo = p - ho * a.Wo;
+            const int ci = kk / KK, r = kk - ci * KK;
+            const int i = r / a.kw, j = r - i * a.kw;
+            const int h = ho * a.sh - a.ph + i, w = wo * a.sw - a.pw + j;
+            if (h >= 0 && h < a.Hi && w >= 0 && w < a.Wi) {
+                if (a.ring[z]) {   // first conv: CHW micro grid straight from the gathered ring row
+                    const int64_t row = a.phys[b];
+                    v = a.ring[z][row * a.ring_stride + a.ring_off + ((int64_t)ci * a.Hi + h) * a.Wi + w];
+                } else {
+                    v = a.src[z][((int64_t)(b * a.Hi + h) * a.Wi + w) * a.Ci + ci];
+                }
+            }
+        }
+        a.col[z][(int64_t)m * a.Kstride + kk] = v;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_flatten_concat(FlattenArgs a) {
+    const int64_t per = (int64_t)a.Bl * a.strideF;
+    const int64_t total = per * a.nstreams;
+    const int HoWo = a.Ho * a.Wo, CHW = a.C * HoWo;
+    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
+        const int z = (int)(t / per);
+        const int64_t rem = t - (int64_t)z * per;
+        const int b = (int)(rem / a.strideF);
+        const int col = (int)(rem - (int64_t)b * a.strideF);
+        float v = 0.f;
+        if (col < CHW) {                  // processed_micro_4d.flatten(start_dim=1): (c, h, w)
+            const int c = col / HoWo, hw = col - c * HoWo;
+            v = a.Hc[z][((int64_t)b * HoWo + hw) * a.C + c];
+        } else if (col < CHW + a.macro_len) {   // torch.cat([micro, macro], dim=1)
+            v = a.ring[z][(int64_t)a.phys[b] * a.ring_stride + (col - CHW)];
+        }
+        a.F[z][(int64_t)b * a.strideF + col] = v;
+    }
+}
+
+// dF (CHW-flatten order, already masked by the conv's activation) -> dZ rows (NHWC)
+__global__ __launch_bounds__(256) void k_unflatten(UnflattenArgs a) {
+    const int HoWo = a.Ho * a.Wo;
+    const int64_t total = (int64_t)a.Bl * HoWo * a.C;
+    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
+        const int c = (int)(t % a.C);
+        const int64_t mrow = t / a.C;
+        const int b = (int)(mrow / HoWo), hw = (int)(mrow - (int64_t)b * HoWo);
+        a.dZ[t] = a.dF[(int64_t)b * a.ldf + (int64_t)c * HoWo + hw];
+    }
+}
+
+// dX (NHWC) = col2im(dCol), gather form (fixed (i, j) order, deterministic), then the
+// previous conv's activation backward: dZprev = act'(Hprev) (.) dX.
+template <int ACT>
+__global__ __launch_bounds__(256) void k_col2im(Col2imArgs a) {
+    const int64_t total = (int64_t)a.Bl * a.Hi * a.Wi * a.Ci;
+    const int KK = a.kh * a.kw;
+    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
+        const int ci = (int)(t % a.Ci);
+        int64_t q = t / a.Ci;
+        const int w = (int)(q % a.Wi);
+        q /= a.Wi;
+        const int h = (int)(q % a.Hi);
+        const int b = (int)(q / a.Hi);
+        float s = 0.f;
+        for (int i = 0; i < a.kh; i++) {
+            const int hh = h + a.ph - i;
+            if (hh < 0 || hh % a.sh) continue;
+            const int ho = hh / a.sh;
+            if (ho >= a.Ho) continue;
+            for (int j = 0; j < a.kw; j++) {
+                const int ww = w + a.pw - j;
+                if (ww < 0 || ww % a.sw) continue;
+                const int wo = ww / a.sw;
+                if (wo >= a.Wo) continue;
+                const int64_t m = ((int64_t)b * a.Ho + ho) * a.Wo + wo;
+                s += a.dcol[m * a.ldcol + (ci * KK + i * a.kw + j)];
+            }
+        }
+        a.dZprev[t] = act_bwd<ACT>(s, a.Hprev[t]);
+    }
+}
+
+static dim3 grid_for(int64_t total) {
+    int64_t g = (total + 255) / 256;
+    if (g > 4096) g = 4096;
+    if (g < 1) g = 1;
+    return dim3((unsigned)g);
+}
+
+int launch_im2col(const Im2colArgs& a, hipStream_t s) {
+    hipLaunchKernelGGL(k_im2col, grid_for((int64_t)a.M * a.Kstride * a.nstreams), dim3(256), 0, s, a);
+    DQNX_HIP_CHECK(hipGetLastError());
+    return DQNX_OK;
+}
+
+int launch_flatten_concat(const FlattenArgs& a, hipStream_t s) {
+    hipLaunchKernelGGL(k_flatten_concat, grid_for((int64_t)a.Bl * a.strideF * a.nstreams), dim3(256), 0, s, a);
+    DQNX_HIP_CHECK(hipGetLastError());
+    return DQNX_OK;
+}
+
+int launch_unflatten(const UnflattenArgs& a, hipStream_t s) {
+    hipLaunchKernelGGL(k_unflatten, grid_for((int64_t)a.Bl * a.Ho * a.Wo * a.C), dim3(256), 0, s, a);
+    DQNX_HIP_CHECK(hipGetLastError());
+    return DQNX_OK;
+}
+
+int launch_col2im(const Col2imArgs& a, int act, hipStream_t s) {
+    const dim3 g = grid_for((int64_t)a.Bl * a.Hi * a.Wi * a.Ci);
+    if (act == DQNX_ACT_RELU) hipLaunchKernelGGL(k_col2im<DQNX_ACT_RELU>, g, dim3(256), 0, s, a);
+    else hipLaunchKernelGGL(k_col2im<DQNX_ACT_ELU>, g, dim3(256), 0, s, a);
+    DQNX_HIP_CHECK(hipGetLastError());
+    return DQNX_OK;
+}
+
+}  // namespace dqnx

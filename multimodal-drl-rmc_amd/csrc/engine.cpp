@@ -41,8 +41,16 @@ struct LayerPlan {
     int64_t off;        // flat offset of the weight ([out][in]); bias follows at off + out*in
 };
 
+struct ConvPlan {
+    int Ci, Hi, Wi, Co, Ho, Wo, kh, kw, sh, sw, ph, pw;
+    int K, Kstride;     // K = Ci*kh*kw (torch weight row), Kstride = K rounded up to 4
+    int64_t off;        // flat offset of the weight [Co][Ci][kh][kw]; bias follows
+};
+
 struct NetPlan {
     std::vector<dqnx_param_info> params;
+    std::vector<ConvPlan> conv;     // two-stream micro CNN (empty for MLP)
+    int macro_len = 0, strideF = 0; // two-stream: dense input = cat(flatten(conv), macro)
     std::vector<LayerPlan> dense;   // body Linear layers
     int F = 0;                      // body output features
     int NH = 0;                     // head rows (dueling: 1 + A)
@@ -90,13 +98,26 @@ static int plan_net(const dqnx_net_desc* d, NetPlan& np) {
         int c = d->micro_c, h = d->micro_h, w = d->micro_w;
         for (int l = 0; l < d->n_conv; l++) {
             const int f = d->conv_out[l], kh = d->conv_kh[l], kw = d->conv_kw[l];
+            if (f <= 0 || kh <= 0 || kw <= 0 || d->conv_sh[l] <= 0 || d->conv_sw[l] <= 0)
+                return set_error(DQNX_EINVAL, "bad conv layer %d", l);
+            ConvPlan cp;
+            cp.Ci = c; cp.Hi = h; cp.Wi = w; cp.Co = f; cp.kh = kh; cp.kw = kw;
+            cp.sh = d->conv_sh[l]; cp.sw = d->conv_sw[l]; cp.ph = kh / 2; cp.pw = kw / 2;   // padding k//2
+            cp.off = np.P;
             add_param(np, "net.cnn_stream." + std::to_string(2 * l) + ".weight", {f, c, kh, kw});
             add_param(np, "net.cnn_stream." + std::to_string(2 * l) + ".bias", {f});
             h = (h + 2 * (kh / 2) - kh) / d->conv_sh[l] + 1;
             w = (w + 2 * (kw / 2) - kw) / d->conv_sw[l] + 1;
+            if (h <= 0 || w <= 0) return set_error(DQNX_EINVAL, "conv layer %d output is empty", l);
+            cp.Ho = h; cp.Wo = w;
+            cp.K = c * kh * kw;
+            cp.Kstride = (cp.K + 3) & ~3;
+            np.conv.push_back(cp);
             c = f;
         }
         in = c * h * w + d->macro_len;
+        np.macro_len = d->macro_len;
+        np.strideF = (in + 3) & ~3;
         for (int l = 0; l < d->n_dense; l++) {
             const int out = d->dense[l];
             LayerPlan lp{in, out, np.P};
@@ -150,6 +171,11 @@ struct dqnx_engine {
     uint64_t ws_phys = 0, ws_pool = 0, ws_xobs = 0, ws_head_part = 0, ws_loss_part = 0, ws_stage = 0;
     uint64_t ws_adam_tab = 0, ws_stamps = 0, ws_dhead = 0;
     std::vector<uint64_t> ws_H, ws_dZ, ws_part;
+    // two-stream CNN: per conv layer im2col [3][M][Kstride], activations [3][M][Co],
+    // dZ [M][Co], split-K partial slabs; dense input F [3][Bl][strideF] and its gradient
+    std::vector<uint64_t> ws_col, ws_Hc, ws_dZc, ws_cpart;
+    std::vector<int> cslices, ckslice;
+    uint64_t ws_F = 0, ws_dF = 0, ws_dcol = 0;
     int stage_rows = 0;
     char* arena = nullptr;
     int64_t ring_size = 0, ring_wptr = 0;   // host mirror of the ring state (pushes are host-driven)
@@ -238,6 +264,26 @@ int layout(dqnx_engine* e) {
     e->ws_loss_part = sub((uint64_t)e->tiles * 4);
     e->stage_rows = 1024;
     e->ws_stage = sub((uint64_t)e->stage_rows * (2 * (uint64_t)c.net.obs_dim + 3) * 4 + 256);
+    const int NC = (int)np.conv.size();
+    e->ws_col.assign(NC, 0);
+    e->ws_Hc.assign(NC, 0);
+    e->ws_dZc.assign(NC, 0);
+    e->ws_cpart.assign(NC, 0);
+    uint64_t dcol_max = 0;
+    for (int l = 0; l < NC; l++) {
+        const ConvPlan& cp = np.conv[l];
+        const uint64_t M = (uint64_t)e->Bl * cp.Ho * cp.Wo;
+        e->ws_col[l] = sub(3 * M * cp.Kstride * 4);
+        e->ws_Hc[l] = sub(3 * M * cp.Co * 4);
+        e->ws_dZc[l] = sub(M * cp.Co * 4);
+        e->ws_cpart[l] = sub((uint64_t)e->cslices[l] * ((uint64_t)cp.Co * cp.K + cp.Co) * 4);
+        if (l > 0 && M * cp.K * 4 > dcol_max) dcol_max = M * cp.K * 4;
+    }
+    if (NC) {
+        e->ws_F = sub((uint64_t)3 * e->Bl * np.strideF * 4);
+        e->ws_dF = sub((uint64_t)e->Bl * np.dense[0].in * 4);
+        e->ws_dcol = sub(dcol_max);
+    }
     cur = align_up(cur, 256);
     e->bytes[DQNX_BUF_WORKSPACE] = cur - e->off[DQNX_BUF_WORKSPACE];
     e->total = cur;
@@ -366,6 +412,86 @@ std::vector<KStep> build_learn_steps(dqnx_engine* e, int key) {
     // 2. forward layers: streams 0 online(obs), 1 online(next) [double], 2 target(next)
     const bool dbl = c.algo != DQNX_ALGO_DQN;
     const int nstreams = dbl ? 3 : 2;
+    const int NC = (int)np.conv.size();
+    const float* ring_obs = at<float>(e, e->off[DQNX_BUF_RING_OBS]);
+    const float* ring_next = at<float>(e, e->off[DQNX_BUF_RING_NEXT_OBS]);
+    // 2a. two-stream micro CNN (R:env/dqn_config.py:92-101, forward :126-133): im2col + MFMA GEMM
+    for (int l = 0; l < NC; l++) {
+        const ConvPlan cp = np.conv[l];
+        const int M = e->Bl * cp.Ho * cp.Wo;
+        Im2colArgs ia;
+        memset(&ia, 0, sizeof(ia));
+        FwdArgs fa;
+        memset(&fa, 0, sizeof(fa));
+        fa.M = M;
+        fa.N = cp.Co;
+        fa.K = cp.K;
+        fa.ldc = cp.Co;
+        int np_ = 0;
+        for (int st = 0; st < 3; st++) {
+            if (st == 1 && !dbl) continue;
+            float* col = at<float>(e, e->ws_col[l]) + (int64_t)st * M * cp.Kstride;
+            if (l == 0) {
+                ia.ring[np_] = st == 0 ? ring_obs : ring_next;
+            } else {
+                ia.src[np_] = at<float>(e, e->ws_Hc[l - 1]) + (int64_t)st * e->Bl * cp.Hi * cp.Wi * cp.Ci;
+            }
+            ia.col[np_] = col;
+            FwdProblem& p = fa.p[np_++];
+            p.W = (st == 2 ? tparams : params) + cp.off;
+            p.bias = p.W + (int64_t)cp.Co * cp.K;
+            p.C = at<float>(e, e->ws_Hc[l]) + (int64_t)st * M * cp.Co;
+            p.A = col;
+            p.lda = cp.Kstride;
+        }
+        ia.nstreams = np_;
+        ia.phys = phys;
+        ia.ring_stride = e->stride;
+        ia.ring_off = np.macro_len;
+        ia.Ci = cp.Ci; ia.Hi = cp.Hi; ia.Wi = cp.Wi; ia.Ho = cp.Ho; ia.Wo = cp.Wo;
+        ia.kh = cp.kh; ia.kw = cp.kw; ia.sh = cp.sh; ia.sw = cp.sw; ia.ph = cp.ph; ia.pw = cp.pw;
+        ia.K = cp.K; ia.Kstride = cp.Kstride; ia.M = M;
+        {
+            KStep k;
+            k.name = "im2col_c" + std::to_string(l + 1);
+            k.bytes = 4.0 * nstreams * (double)M * cp.Kstride * 2.0;
+            k.run = [=](hipStream_t s) { return launch_im2col(ia, s); };
+            ks.push_back(k);
+        }
+        KStep k;
+        k.name = "conv_fwd_c" + std::to_string(l + 1);
+        k.flops = 2.0 * nstreams * (double)M * cp.Co * cp.K;
+        k.bytes = 4.0 * (nstreams * (double)M * (cp.Kstride + cp.Co) + 2.0 * cp.Co * (cp.K + 1.0));
+        const bool vecb = (cp.K % 4) == 0;
+        const int nps = np_;
+        k.run = [=](hipStream_t s) { return launch_linear_fwd(fa, nps, act, vecb, s); };
+        ks.push_back(k);
+    }
+    if (NC) {   // 2b. cat(flatten_CHW(conv), macro) (R:env/dqn_config.py:135-138)
+        const ConvPlan cl = np.conv[NC - 1];
+        FlattenArgs fl;
+        memset(&fl, 0, sizeof(fl));
+        int z = 0;
+        for (int st = 0; st < 3; st++) {
+            if (st == 1 && !dbl) continue;
+            fl.Hc[z] = at<float>(e, e->ws_Hc[NC - 1]) + (int64_t)st * e->Bl * cl.Ho * cl.Wo * cl.Co;
+            fl.ring[z] = st == 0 ? ring_obs : ring_next;
+            fl.F[z] = at<float>(e, e->ws_F) + (int64_t)st * e->Bl * np.strideF;
+            z++;
+        }
+        fl.nstreams = z;
+        fl.phys = phys;
+        fl.ring_stride = e->stride;
+        fl.macro_len = np.macro_len;
+        fl.C = cl.Co; fl.Ho = cl.Ho; fl.Wo = cl.Wo;
+        fl.Bl = e->Bl;
+        fl.strideF = np.strideF;
+        KStep k;
+        k.name = "flatten_concat";
+        k.bytes = 4.0 * nstreams * Bl * 2.0 * np.strideF;
+        k.run = [=](hipStream_t s) { return launch_flatten_concat(fl, s); };
+        ks.push_back(k);
+    }
     for (int l = 0; l < L; l++) {
         const LayerPlan lp = np.dense[l];
         FwdArgs fa;
@@ -383,7 +509,10 @@ std::vector<KStep> build_learn_steps(dqnx_engine* e, int key) {
             p.W = (tgt ? tparams : params) + lp.off;
             p.bias = p.W + (int64_t)lp.out * lp.in;
             p.C = H + (int64_t)st * e->Bl * lp.out;
-            if (l == 0) {
+            if (l == 0 && NC) {
+                p.A = at<float>(e, e->ws_F) + (int64_t)st * e->Bl * np.strideF;
+                p.lda = np.strideF;
+            } else if (l == 0) {
                 p.A = at<float>(e, e->off[st == 0 ? DQNX_BUF_RING_OBS : DQNX_BUF_RING_NEXT_OBS]);
                 p.lda = e->stride;
                 p.phys = phys;
@@ -399,7 +528,7 @@ std::vector<KStep> build_learn_steps(dqnx_engine* e, int key) {
         k.flops = 2.0 * nstreams * Bl * lp.out * lp.in;
         // unique bytes: input rows, weights (online + target), outputs (+ layer-1 row copy)
         k.bytes = 4.0 * (nstreams * Bl * lp.in + 2.0 * (lp.out * (double)lp.in + lp.out) + nstreams * Bl * lp.out
-                         + (l == 0 ? Bl * lp.in : 0.0));
+                         + (l == 0 && !NC ? Bl * lp.in : 0.0));
         const bool vecb = (lp.in % 4) == 0;
         k.run = [=](hipStream_t s) { return launch_linear_fwd(fa, np_, act, vecb, s); };
         ks.push_back(k);
@@ -490,15 +619,22 @@ std::vector<KStep> build_learn_steps(dqnx_engine* e, int key) {
             ba.dZprev = at<float>(e, e->ws_dZ[l - 1]);
             d.X = ba.Hprev;
             d.ldx = lp.in;
+        } else if (NC) {   // dense input F = cat(conv features, macro): dF, masked by the conv's ELU
+            ba.Hprev = at<float>(e, e->ws_F);
+            ba.ldh = np.strideF;
+            ba.dZprev = at<float>(e, e->ws_dF);
+            d.X = ba.Hprev;
+            d.ldx = np.strideF;
         } else {
             d.X = at<float>(e, e->ws_xobs);
             d.ldx = e->stride;
         }
         d.partial = at<float>(e, e->ws_part[l]);
         d.pstride = (int64_t)lp.out * lp.in + lp.out;
-        double flops = 2.0 * Bl * lp.out * (lp.in + 1.0) + (l > 0 ? 2.0 * Bl * lp.out * lp.in : 0.0);
+        const bool dx = l > 0 || NC;
+        double flops = 2.0 * Bl * lp.out * (lp.in + 1.0) + (dx ? 2.0 * Bl * lp.out * lp.in : 0.0);
         double bytes = 4.0 * (Bl * lp.out + Bl * lp.in + ba.dw_slices * (lp.out * (lp.in + 1.0))
-                              + (l > 0 ? lp.out * (double)lp.in + 2.0 * Bl * lp.in : 0.0));
+                              + (dx ? lp.out * (double)lp.in + 2.0 * Bl * lp.in : 0.0));
         if (l == L - 1) {   // head weight gradient: dHead^T [H_L | 1]
             DwProblem& h = ba.dw[ba.ndw++];
             h.dZ = at<float>(e, e->ws_dhead);
@@ -523,12 +659,90 @@ std::vector<KStep> build_learn_steps(dqnx_engine* e, int key) {
         ks.push_back(k);
     }
 
+    // 4b. micro CNN backward: unflatten dF, then per conv (last first) dW + dX columns, col2im
+    if (NC) {
+        {
+            const ConvPlan cl = np.conv[NC - 1];
+            UnflattenArgs ua;
+            ua.dF = at<float>(e, e->ws_dF);
+            ua.ldf = np.dense[0].in;
+            ua.dZ = at<float>(e, e->ws_dZc[NC - 1]);
+            ua.Bl = e->Bl;
+            ua.C = cl.Co; ua.Ho = cl.Ho; ua.Wo = cl.Wo;
+            KStep k;
+            k.name = "unflatten";
+            k.bytes = 8.0 * Bl * cl.Co * cl.Ho * cl.Wo;
+            k.run = [=](hipStream_t s) { return launch_unflatten(ua, s); };
+            ks.push_back(k);
+        }
+        for (int l = NC - 1; l >= 0; l--) {
+            const ConvPlan cp = np.conv[l];
+            const int M = e->Bl * cp.Ho * cp.Wo;
+            BwdArgs ba;
+            memset(&ba, 0, sizeof(ba));
+            ba.dZ = at<float>(e, e->ws_dZc[l]);
+            ba.Bl = M;
+            ba.in = cp.K;
+            ba.out = cp.Co;
+            ba.W = params + cp.off;
+            ba.kslice = e->ckslice[l];
+            ba.dw_slices = e->cslices[l];
+            if (l > 0) {   // dCol = dZ W (no mask here: col2im applies the previous conv's ELU')
+                ba.Hprev = nullptr;
+                ba.dZprev = at<float>(e, e->ws_dcol);
+            }
+            DwProblem& d = ba.dw[ba.ndw++];
+            d.dZ = ba.dZ;
+            d.ldz = cp.Co;
+            d.X = at<float>(e, e->ws_col[l]);   // stream 0 columns
+            d.ldx = cp.Kstride;
+            d.in = cp.K;
+            d.out = cp.Co;
+            d.partial = at<float>(e, e->ws_cpart[l]);
+            d.pstride = (int64_t)cp.Co * cp.K + cp.Co;
+            d.head_kind = -1;
+            bwd_level_grid(ba);
+            KStep k;
+            k.name = "conv_bwd_c" + std::to_string(l + 1);
+            k.flops = 2.0 * M * cp.Co * (cp.K + 1.0) + (l > 0 ? 2.0 * M * cp.Co * (double)cp.K : 0.0);
+            k.bytes = 4.0 * ((double)M * (cp.Co + cp.Kstride) + ba.dw_slices * (double)d.pstride
+                             + (l > 0 ? (double)M * cp.K + cp.Co * (double)cp.K : 0.0));
+            k.run = [=](hipStream_t s) { return launch_bwd_level(ba, act, s); };
+            ks.push_back(k);
+            if (l > 0) {
+                const ConvPlan pp = np.conv[l - 1];
+                Col2imArgs ca;
+                ca.dcol = at<float>(e, e->ws_dcol);
+                ca.ldcol = cp.K;
+                ca.Hprev = at<float>(e, e->ws_Hc[l - 1]);      // stream 0
+                ca.dZprev = at<float>(e, e->ws_dZc[l - 1]);
+                ca.Bl = e->Bl;
+                ca.Ci = cp.Ci; ca.Hi = cp.Hi; ca.Wi = cp.Wi; ca.Ho = cp.Ho; ca.Wo = cp.Wo;
+                ca.kh = cp.kh; ca.kw = cp.kw; ca.sh = cp.sh; ca.sw = cp.sw; ca.ph = cp.ph; ca.pw = cp.pw;
+                KStep k2;
+                k2.name = "col2im_c" + std::to_string(l + 1);
+                k2.bytes = 4.0 * ((double)M * cp.K + 2.0 * Bl * pp.Ho * pp.Wo * pp.Co);
+                k2.run = [=](hipStream_t s) { return launch_col2im(ca, act, s); };
+                ks.push_back(k2);
+            }
+        }
+    }
+
     // 5. gradient reduction + Adam (+ soft update)
     {
         AdamArgs aa;
         memset(&aa, 0, sizeof(aa));
         aa.nseg = 0;
         double part_elems = 0;
+        for (int l = 0; l < NC; l++) {   // segments in flat-offset order: convs, dense, head
+            const ConvPlan& cp = np.conv[l];
+            AdamSegment& sg = aa.seg[aa.nseg++];
+            sg.off = cp.off;
+            sg.partial = at<float>(e, e->ws_cpart[l]);
+            sg.pstride = (int64_t)cp.Co * cp.K + cp.Co;
+            sg.S = e->cslices[l];
+            part_elems += (double)sg.S * sg.pstride;
+        }
         for (int l = 0; l < L; l++) {
             AdamSegment& sg = aa.seg[aa.nseg++];
             sg.off = np.dense[l].off;
@@ -831,7 +1045,6 @@ int dqnx_engine_create(const dqnx_config* cfg, dqnx_engine** out) {
     int rc = plan_net(&cfg->net, e->np);
     if (rc) { delete e; return rc; }
     const dqnx_config& c = e->cfg;
-    if (c.net.kind != DQNX_NET_MLP) { delete e; return set_error(DQNX_EUNSUPPORTED, "two-stream network not built yet"); }
     if (c.algo < DQNX_ALGO_DQN || c.algo > DQNX_ALGO_PER_DOUBLE) { delete e; return set_error(DQNX_EINVAL, "bad algo"); }
     if (c.algo == DQNX_ALGO_PER_DOUBLE) {
         // exact float64 tree sums need cap <= 2^20 (see per.hip); one sampler workgroup <= PER_MAX_B
@@ -847,6 +1060,7 @@ int dqnx_engine_create(const dqnx_config* cfg, dqnx_engine** out) {
         if (e->np.dense[l].out % 4) { delete e; return set_error(DQNX_EUNSUPPORTED, "hidden widths must be multiples of 4"); }
     if (sample_hash_slots(c.batch) < 0) { delete e; return set_error(DQNX_EUNSUPPORTED, "batch too large for the sampler"); }
     if (const char* bp = getenv("DQNX_BWD_PLAN")) e->bwd_plan = atoi(bp) == 1 ? 1 : 0;
+    if (c.net.kind != DQNX_NET_MLP) e->bwd_plan = 0;   // the fused plan covers MLP bodies only
     e->Bg = c.batch;
     e->Bl = c.batch / c.world_size;
     e->shard_begin = c.rank * e->Bl;
@@ -864,6 +1078,20 @@ int dqnx_engine_create(const dqnx_config* cfg, dqnx_engine** out) {
         S = (e->Bl + ks - 1) / ks;
         e->slices[l] = S;
         e->kslice[l] = ks;
+    }
+    const int NC = (int)e->np.conv.size();
+    e->cslices.assign(NC, 1);
+    e->ckslice.assign(NC, 1);
+    for (int l = 0; l < NC; l++) {   // split-K over the conv's output pixels (b, ho, wo)
+        const int rows = e->Bl * e->np.conv[l].Ho * e->np.conv[l].Wo;
+        int S = rows / 512;
+        if (S < 1) S = 1;
+        if (S > 32) S = 32;
+        int ks = (int)align_up((uint64_t)((rows + S - 1) / S), 16);
+        S = (rows + ks - 1) / ks;
+        e->cslices[l] = S;
+        e->ckslice[l] = ks;
+        if (e->np.conv[l].Co % 4) { delete e; return set_error(DQNX_EUNSUPPORTED, "conv channels must be multiples of 4"); }
     }
     layout(e);
     *out = e;

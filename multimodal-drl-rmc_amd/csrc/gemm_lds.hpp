@@ -69,7 +69,7 @@ struct StageRowsK {
     }
 };
 
-template <int C, int KT>
+template <int C, int KT, bool VEC = true>
 struct StageKRows {
     static constexpr int S = C + 4;
     static constexpr int C4 = C / 4;
@@ -86,7 +86,17 @@ struct StageKRows {
             if (q < KT * C4) {
                 const int kr = q / C4, c = c0 + 4 * (q - kr * C4);
                 const int k = kb + kr;
-                if (k < o.K && c < o.nrows) x = ld4(o.base + (int64_t)k * o.ld + c);
+                if (k < o.K && c < o.nrows) {
+                    const float* p = o.base + (int64_t)k * o.ld + c;
+                    if (VEC) {   // row stride and column count multiples of 4
+                        x = ld4(p);
+                    } else {
+                        x.x = p[0];
+                        x.y = (c + 1 < o.nrows) ? p[1] : 0.f;
+                        x.z = (c + 2 < o.nrows) ? p[2] : 0.f;
+                        x.w = (c + 3 < o.nrows) ? p[3] : 0.f;
+                    }
+                }
             }
             v[j] = x;
         }
@@ -122,7 +132,7 @@ struct Stage<L_ROWS_K, R, KT, VEC> : StageRowsK<R, KT, VEC> {
     }
 };
 template <int R, int KT, bool VEC>
-struct Stage<L_K_ROWS, R, KT, VEC> : StageKRows<R, KT> {
+struct Stage<L_K_ROWS, R, KT, VEC> : StageKRows<R, KT, VEC> {
     __device__ __forceinline__ void fragx(const float* lds, int rw, int kk, float (&f)[4], int col_abs,
                                           int aug) const {
         this->frag(lds, rw, kk, f, col_abs, aug);

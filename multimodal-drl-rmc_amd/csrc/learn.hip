@@ -137,9 +137,11 @@ __global__ __launch_bounds__(256) void k_linear_fwd(FwdArgs args) {
 //   dx role:  dZprev = (dZ W) (.) act'(Hprev)      [Bl x in], K = out
 //   dw role:  partial[s] = dZ^T [Xprev | 1]        [out x (in+1)], K = samples of slice s
 // =====================================================================================
-template <int ACT>
+// VECW: the dx role's weight rows (length `in`) allow float4 loads (in % 4 == 0).
+// Hprev == null: no activation mask (conv dX columns before col2im).
+template <int ACT, bool VECW>
 __global__ __launch_bounds__(256) void k_bwd_level(BwdArgs a) {
-    using EX = Engine<BWD_BM, BWD_BN, DQNX_BWD_KT, DQNX_BWD_WM, L_ROWS_K, L_K_ROWS, true, true>;
+    using EX = Engine<BWD_BM, BWD_BN, DQNX_BWD_KT, DQNX_BWD_WM, L_ROWS_K, L_K_ROWS, true, VECW>;
     using EW = Engine<BWD_BM, BWD_BN, DQNX_BWD_KT, DQNX_BWD_WM, L_K_ROWS, L_K_ROWS, true, true>;
     constexpr int TM = EX::TM, TN = EX::TN;
     constexpr int LF = EX::LDS_FLOATS > EW::LDS_FLOATS ? EX::LDS_FLOATS : EW::LDS_FLOATS;
@@ -160,7 +162,8 @@ __global__ __launch_bounds__(256) void k_bwd_level(BwdArgs a) {
 #pragma unroll
                 for (int r = 0; r < 4; r++) {
                     const int col = n0 + EX::co() + tn * 16 + i, row = m0 + EX::ro() + tm * 16 + 4 * g + r;
-                    hm[tm][tn][r] = (col < a.in && row < a.Bl) ? a.Hprev[(int64_t)row * a.ldh + col] : 0.f;
+                    hm[tm][tn][r] = !a.Hprev ? 1.f   // act_bwd(g, h > 0) == g
+                                    : (col < a.in && row < a.Bl) ? a.Hprev[(int64_t)row * a.ldh + col] : 0.f;
                 }
         Operand A{a.dZ, a.out, nullptr, a.Bl, a.out, -1, nullptr, 0};
         Operand B{a.W, a.in, nullptr, a.in, a.out, -1, nullptr, 0};
@@ -617,8 +620,14 @@ void bwd_level_grid(BwdArgs& a) {
 int launch_bwd_level(const BwdArgs& a, int act, hipStream_t s) {
     int blocks = a.dx_blocks;
     for (int p = 0; p < a.ndw; p++) blocks += a.dw[p].blocks;
-    if (act == DQNX_ACT_RELU) hipLaunchKernelGGL(k_bwd_level<DQNX_ACT_RELU>, dim3(blocks), dim3(256), 0, s, a);
-    else hipLaunchKernelGGL(k_bwd_level<DQNX_ACT_ELU>, dim3(blocks), dim3(256), 0, s, a);
+    const bool vw = (a.in % 4) == 0;
+    if (act == DQNX_ACT_RELU) {
+        if (vw) hipLaunchKernelGGL((k_bwd_level<DQNX_ACT_RELU, true>), dim3(blocks), dim3(256), 0, s, a);
+        else hipLaunchKernelGGL((k_bwd_level<DQNX_ACT_RELU, false>), dim3(blocks), dim3(256), 0, s, a);
+    } else {
+        if (vw) hipLaunchKernelGGL((k_bwd_level<DQNX_ACT_ELU, true>), dim3(blocks), dim3(256), 0, s, a);
+        else hipLaunchKernelGGL((k_bwd_level<DQNX_ACT_ELU, false>), dim3(blocks), dim3(256), 0, s, a);
+    }
     DQNX_HIP_CHECK(hipGetLastError());
     return DQNX_OK;
 }

@@ -205,6 +205,45 @@ struct PerUpdateArgs {
     float eps, alpha, pmax;   // numpy float32 arithmetic on the python-float constants
 };
 
+// ---- two-stream hybrid network data movement (conv.hip) ----
+struct Im2colArgs {
+    int nstreams;
+    const float* ring[3];     // first conv: ring (obs / next_obs) per stream, else null
+    const int32_t* phys;      // [Bl] ring slots (first conv)
+    int64_t ring_stride;      // floats per ring row
+    int ring_off;             // micro grid offset inside the row (= macro_len)
+    const float* src[3];      // later convs: NHWC activations [Bl*Hi*Wi][Ci] per stream
+    float* col[3];            // [M][Kstride] per stream, k = (ci, i, j), zero padded
+    int Ci, Hi, Wi, Ho, Wo, kh, kw, sh, sw, ph, pw;
+    int K, Kstride, M;
+};
+struct FlattenArgs {
+    int nstreams;
+    const float* Hc[3];       // last conv NHWC [Bl*Ho*Wo][C]
+    const float* ring[3];     // macro source rows per stream
+    const int32_t* phys;
+    int64_t ring_stride;
+    int macro_len, C, Ho, Wo, Bl, strideF;
+    float* F[3];              // [Bl][strideF] = cat(flatten_CHW(conv), macro), zero padded
+};
+struct UnflattenArgs {
+    const float* dF;          // [Bl][ldf], CHW-flatten order
+    int ldf;
+    float* dZ;                // [Bl*Ho*Wo][C]
+    int Bl, C, Ho, Wo;
+};
+struct Col2imArgs {
+    const float* dcol;        // [Bl*Ho*Wo][ldcol], k = (ci, i, j)
+    int ldcol;
+    const float* Hprev;       // [Bl*Hi*Wi][Ci] activation output of the previous conv
+    float* dZprev;            // [Bl*Hi*Wi][Ci]
+    int Bl, Ci, Hi, Wi, Ho, Wo, kh, kw, sh, sw, ph, pw;
+};
+int launch_im2col(const Im2colArgs& a, hipStream_t s);
+int launch_flatten_concat(const FlattenArgs& a, hipStream_t s);
+int launch_unflatten(const UnflattenArgs& a, hipStream_t s);
+int launch_col2im(const Col2imArgs& a, int act, hipStream_t s);
+
 int launch_per_sample(const PerSampleArgs& a, hipStream_t s);
 int launch_per_update(const PerUpdateArgs& a, hipStream_t s);
 

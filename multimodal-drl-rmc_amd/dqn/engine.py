@@ -73,6 +73,18 @@ def mlp_spec(obs_dim=284, n_actions=8, head="dueling", hidden=(256, 128)) -> Net
                    activation=C.DQNX_ACT_RELU, obs_dim=obs_dim, n_actions=n_actions, dense=tuple(hidden))
 
 
+HYBRID_CONV = ((32, (3, 3), (1, 1)), (64, (3, 3), (2, 1)), (64, (3, 3), (2, 2)))   # R:env/dqn_config.py:163-167
+
+
+def hybrid_spec(n_actions=8, head="dueling", micro_chw=(2, 27, 5), macro_len=14, conv=HYBRID_CONV,
+                dense=(512, 256)) -> NetSpec:
+    """TwoStreamHybridNetwork as network_config builds it (R:env/dqn_config.py:148-193)."""
+    c, h, w = micro_chw
+    return NetSpec(kind=C.DQNX_NET_TWO_STREAM, head=C.DQNX_HEAD_DUELING if head == "dueling" else C.DQNX_HEAD_LINEAR,
+                   activation=C.DQNX_ACT_ELU, obs_dim=macro_len + c * h * w, n_actions=n_actions,
+                   dense=tuple(dense), macro_len=macro_len, micro_chw=tuple(micro_chw), conv=tuple(conv))
+
+
 def spec_from_body(net: nn.Module, obs_dim: int, n_actions: int, dueling: bool) -> NetSpec:
     """Recognise the two body families the reference ships (SURVEY §7 hard part 6) and
     refuse anything else:

@@ -1,0 +1,98 @@
+"""GPU parity of the two-stream hybrid Q-network learn step (TwoStreamHybridNetwork,
+R:env/dqn_config.py:66-193: 3 convs with ELU on the (2,27,5) micro grid, concat with the
+14 macro features, dense 1358->512->256, dueling / linear head) against the oracle and
+the reference's own golden steps."""
+import os
+import random
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import ref as O
+
+pytestmark = pytest.mark.gpu
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def _E():
+    from dqn import engine as E
+    return E
+
+
+def make_hybrid_pair(algo, batch, cap, n_fill, seed, graphs=True):
+    E = _E()
+    head = O.algo_spec_head(algo)
+    ospec = O.hybrid_spec(8, head)
+    init = O.reference_init(ospec, seed)
+    oracle = O.OracleLearner(ospec, algo, batch, cap, seed=seed, params=init, per_pow="cr")
+    data = O.synth_transitions(n_fill, ospec.obs_dim, 8, seed=seed + 100)
+    O.fill_replay(oracle, *data)
+    eng = E.LearnEngine(E.hybrid_spec(8, head), algo, batch, cap, graphs=graphs)
+    eng.load_params(init)
+    eng.push(*data)
+    random.seed(seed + 7)
+    st = O.py_state_to_array()
+    oracle.py_state = st.copy()
+    eng.set_rng(0, st)
+    np.random.seed(seed + 11)
+    nps = O.np_state_to_array()
+    oracle.np_state = nps.copy()
+    eng.set_rng(1, nps)
+    return oracle, eng
+
+
+@pytest.mark.parametrize("algo,batch,cap,n_fill,seed", [
+    ("DuelingDoubleDQNAgent", 32, 500, 300, 3),
+    ("DQNAgent", 64, 1000, 700, 4),
+    ("DuelingDoubleDQNAgent", 256, 5000, 3000, 5),
+    ("PerDuelingDoubleDQNAgent", 64, 1000, 700, 6),
+])
+def test_gpu_hybrid_learn_matches_oracle(algo, batch, cap, n_fill, seed):
+    oracle, eng = make_hybrid_pair(algo, batch, cap, n_fill, seed)
+    per = algo.startswith("Per")
+    for step in range(3):
+        rec = oracle.train_step()
+        eng.learn_step(soft_update=True)
+        torch.cuda.synchronize()
+        eng.check_device_error()
+        idx = eng.batch_idx.cpu().numpy().astype(np.int64) + (cap - 1 if per else 0)
+        assert np.array_equal(idx, rec.positions), f"step {step}: sampled indices differ"
+        q = eng.q.cpu()
+        np.testing.assert_allclose(q[0].numpy(), rec.q_online.numpy(), atol=1e-5, rtol=1e-5)
+        np.testing.assert_allclose(q[2].numpy(), rec.q_target_next.numpy(), atol=1e-5, rtol=1e-5)
+        assert abs(eng.loss() - rec.loss) <= 1e-5 * max(1.0, abs(rec.loss))
+        g = eng.param_views(eng.grads[:-1])
+        for k, ref in rec.grads.items():
+            np.testing.assert_allclose(g[k].cpu().numpy(), ref.numpy(), atol=5e-6, rtol=1e-3, err_msg=k)
+        on = eng.param_views(eng.params)
+        tg = eng.param_views(eng.target_params)
+        for k in oracle.online:
+            np.testing.assert_allclose(on[k].cpu().numpy(), oracle.online[k].numpy(), atol=1e-5, rtol=0, err_msg=k)
+            np.testing.assert_allclose(tg[k].cpu().numpy(), oracle.target[k].numpy(), atol=1e-5, rtol=0, err_msg=k)
+
+
+def test_gpu_hybrid_learn_golden():
+    """Against the reference's own hybrid DuelingDouble steps (tests/golden/make_golden.py)."""
+    E = _E()
+    z = np.load(os.path.join(GOLDEN, "learn_hybrid284_DuelingDoubleDQNAgent.npz"))
+    init = O.reference_init(O.hybrid_spec(8, "dueling"), int(z["seed"]))
+    eng = E.LearnEngine(E.hybrid_spec(8, "dueling"), str(z["algo"]), int(z["batch"]), int(z["buffer"]))
+    eng.load_params(init)
+    eng.push(*O.synth_transitions(int(z["n_fill"]), int(z["obs_dim"]), 8, seed=int(z["seed"]) + 100))
+    eng.set_rng(0, z["py_state_in"])
+    for s in range(int(z["steps"])):
+        eng.learn_step(soft_update=True)
+        torch.cuda.synchronize()
+        assert np.array_equal(eng.batch_idx.cpu().numpy().astype(np.int64), z["pos"][s])
+        assert abs(eng.loss() - z["loss"][s]) <= 1e-5 * max(1.0, abs(z["loss"][s]))
+    assert np.array_equal(eng.get_rng(0), z["py_state_out"])
+    stride = int(z["stride"])
+    keys = [str(k) for k in z["keys"]]
+    on, tg = eng.param_views(eng.params), eng.param_views(eng.target_params)
+    for i, k in enumerate(keys):
+        got = on[k].cpu().numpy().reshape(-1)
+        ref = z[f"online_{i}"]
+        if got.size != ref.size:
+            got = got[::stride]
+        np.testing.assert_allclose(got, ref, atol=1e-5, rtol=0, err_msg=k)
