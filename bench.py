@@ -34,7 +34,7 @@ sys.path.insert(0, os.path.join(REPO, "multimodal-drl-rmc_amd"))
 
 from dqn import _capi as C  # noqa: E402
 from dqn.data_parallel import dp_learn_step  # noqa: E402
-from dqn.engine import LearnEngine, mlp_spec  # noqa: E402
+from dqn.engine import LearnEngine, hybrid_spec, mlp_spec  # noqa: E402
 
 PEAK_FP32_MFMA_TFLOPS = 157.3   # MI355X_MICROARCH.md: F32 matrix, dense
 PEAK_HBM_GBS = 8000.0           # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
@@ -50,10 +50,14 @@ def parse():
     p.add_argument("--steps", type=int, default=200)
     p.add_argument("--warmup", type=int, default=20)
     p.add_argument("--batch", type=int, default=1024, help="transitions per GPU per step")
-    p.add_argument("--capacity", type=int, default=1_000_000)
+    p.add_argument("--capacity", type=int, default=None,
+                   help="replay capacity (default 1e6; 1e5 for hybrid84: 113 KB rows)")
     p.add_argument("--obs-dim", type=int, default=284)
     p.add_argument("--actions", type=int, default=8)
     p.add_argument("--algo", default="DuelingDoubleDQNAgent")
+    p.add_argument("--net", default="mlp", choices=["mlp", "hybrid", "hybrid84"],
+                   help="mlp: MLP-284 (configs[1]); hybrid: TwoStreamHybridNetwork on the (2,27,5) grid; "
+                        "hybrid84: the stacked (4,84,84) occupancy-grid CNN variant (configs[2])")
     p.add_argument("--no-graphs", action="store_true")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=15.0)
@@ -61,17 +65,32 @@ def parse():
     p.add_argument("--prefetch", action="store_true",
                    help="overlap the next step's replay sampling with this step's compute on a "
                         "side stream (measured slower at batch 1024: cross-stream event waits)")
-    return p.parse_args()
+    a = p.parse_args()
+    if a.capacity is None:
+        a.capacity = 100_000 if a.net == "hybrid84" else 1_000_000
+    return a
 
 
 def init_params(spec, seed=0):
-    """Random init of the Q-net architecture (torch default Linear init)."""
+    """Random init of the Q-net architecture (torch default Conv2d / Linear init), in the
+    reference's construction order (R:env/dqn_config.py:92-122, R:dqn/network.py:81-82)."""
     torch.manual_seed(seed)
-    d = spec.obs_dim
     mods = {}
-    for i, w in enumerate(spec.dense):
-        mods[f"net.{2 * i}"] = nn.Linear(d, w)
-        d = w
+    if spec.kind == C.DQNX_NET_TWO_STREAM:
+        c, h, w = spec.micro_chw
+        for i, (f, k, st) in enumerate(spec.conv):
+            mods[f"net.cnn_stream.{2 * i}"] = nn.Conv2d(c, f, kernel_size=k, stride=st, padding=(k[0] // 2, k[1] // 2))
+            h = (h + 2 * (k[0] // 2) - k[0]) // st[0] + 1
+            w = (w + 2 * (k[1] // 2) - k[1]) // st[1] + 1
+            c = f
+        d = c * h * w + spec.macro_len
+        prefix = "net.dense_stream"
+    else:
+        d = spec.obs_dim
+        prefix = "net"
+    for i, width in enumerate(spec.dense):
+        mods[f"{prefix}.{2 * i}"] = nn.Linear(d, width)
+        d = width
     if spec.head == C.DQNX_HEAD_DUELING:
         mods["fc_val"] = nn.Linear(d, 1)
         mods["fc_adv"] = nn.Linear(d, spec.n_actions)
@@ -84,13 +103,24 @@ def init_params(spec, seed=0):
     return sd
 
 
-def fill_ring(eng, n, D, A, device, seed=0, chunk=1 << 16):
+def make_spec(args):
+    head = "dueling" if "Dueling" in args.algo else "linear"
+    if args.net == "hybrid":
+        return hybrid_spec(args.actions, head, micro_chw=(2, 27, 5))
+    if args.net == "hybrid84":
+        return hybrid_spec(args.actions, head, micro_chw=(4, 84, 84))
+    return mlp_spec(args.obs_dim, args.actions, head)
+
+
+def fill_ring(eng, n, D, A, device, seed=0, chunk=None):
     """Synthetic 1ramp_1x3-shaped transitions generated on the GPU:
     macro U[0,1); micro grid occupancy ~ Bernoulli(0.2) with speed U[0,1); action U{0..A-1};
     reward U[-24,3]; done ~ Bernoulli(1/90)."""
     g = torch.Generator(device=device)
     g.manual_seed(seed)
     macro = min(14, D)
+    if chunk is None:   # ~256 MB of obs per chunk
+        chunk = max(256, min(1 << 16, (1 << 28) // (4 * D)))
 
     def obs_block(m):
         o = torch.empty(m, D, device=device)
@@ -113,17 +143,35 @@ def fill_ring(eng, n, D, A, device, seed=0, chunk=1 << 16):
     torch.cuda.synchronize()
 
 
+def net_name(args):
+    return {"mlp": f"MLP-{args.obs_dim}", "hybrid": "TwoStreamHybrid(2x27x5)",
+            "hybrid84": "TwoStreamHybrid(4x84x84)"}[args.net]
+
+
+WORKLOADS = {
+    "mlp": "configs[1]: synthetic 1ramp_1x3 state vectors, MLP Q-net fp32, GPU replay buffer",
+    "hybrid": "TwoStreamHybridNetwork (micro CNN on the 2x27x5 grid + 14 macro), fp32, GPU replay buffer",
+    "hybrid84": "configs[2]: stacked 4x84x84 occupancy-grid CNN encoder + dueling head, fp32, GPU replay buffer",
+}
+
+
 def cpu_baseline(args):
     """The oracle's torch-CPU restatement of the same learn step (reference algorithm:
     deque + random.sample + transitions_to_tensor + 3 forwards + Huber + autograd + Adam +
     soft update), timed on this host's cores on a bounded sample."""
     sys.path.insert(0, REPO)
     from oracle import ref as O
-    spec = O.mlp_spec(args.obs_dim, args.actions, "dueling")
+    head = "dueling" if "Dueling" in args.algo else "linear"
+    if args.net == "mlp":
+        spec = O.mlp_spec(args.obs_dim, args.actions, head)
+    else:
+        spec = O.hybrid_spec(args.actions, head, micro_chw=(2, 27, 5) if args.net == "hybrid" else (4, 84, 84))
     per = args.algo.startswith("Per")
     cap = min(args.capacity, 100_000) if per else args.capacity   # Python SumTree fill is ~20 us/row
+    if args.net == "hybrid84":
+        cap = min(cap, 2_000)   # 113 KB rows: a host deque of 1e5 would need 22.6 GB
     L = O.OracleLearner(spec, args.algo, args.batch, cap, seed=0)
-    obs, act, rew, done, nobs = O.synth_transitions(cap, args.obs_dim, args.actions, seed=0)
+    obs, act, rew, done, nobs = O.synth_transitions(cap, spec.obs_dim, args.actions, seed=0)
     if per:
         list(L.replay.store_transitions(obs, act, rew, done, nobs))
     else:
@@ -142,7 +190,7 @@ def cpu_baseline(args):
             break
     return {"value": args.batch * steps / el, "unit": "transitions/s", "cores": torch.get_num_threads(),
             "kind": "port",
-            "sample": f"oracle/ref.py OracleLearner {args.algo} MLP-{args.obs_dim} batch {args.batch}, "
+            "sample": f"oracle/ref.py OracleLearner {args.algo} {net_name(args)} batch {args.batch}, "
                       f"{'SumTree' if per else 'deque'} of {cap} transitions, {steps} learn+soft-update steps in {el:.1f} s, "
                       f"torch {torch.__version__} CPU, {torch.get_num_threads()} threads"}
 
@@ -167,12 +215,12 @@ def main():
         else:
             dist.init_process_group(backend)
 
-    spec = mlp_spec(args.obs_dim, args.actions, "dueling" if "Dueling" in args.algo else "linear")
+    spec = make_spec(args)
     Bg = args.batch * world
     eng = LearnEngine(spec, args.algo, Bg, args.capacity, world_size=world, rank=rank, device=device,
                       graphs=not args.no_graphs)
     eng.load_params(init_params(spec, 0))
-    fill_ring(eng, args.capacity, args.obs_dim, args.actions, device, seed=0)
+    fill_ring(eng, args.capacity, spec.obs_dim, args.actions, device, seed=0)
     random.seed(1234)   # the replay sampler continues CPython's global MT19937 stream
     eng.set_rng(C.DQNX_RNG_PY, np.array(random.getstate()[1], dtype=np.uint32))
     per = args.algo.startswith("Per")
@@ -305,8 +353,8 @@ def main():
             "dtype": "fp32",
             "data": "synthetic",
             "config": {
-                "workload": "configs[1]: synthetic 1ramp_1x3 state vectors, MLP Q-net fp32, GPU replay buffer",
-                "algo": args.algo, "net": f"MLP({args.obs_dim}->256->128, ReLU) + dueling head A={args.actions}",
+                "workload": WORKLOADS[args.net],
+                "algo": args.algo, "net": net_name(args),
                 "batch_per_gpu": args.batch, "global_batch": Bg, "replay_capacity": args.capacity,
                 "parallelism": f"dp{world}", "graphs": not args.no_graphs, "prefetch_sampling": prefetch,
             },

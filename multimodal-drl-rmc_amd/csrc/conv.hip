@@ -12,32 +12,35 @@
 
 namespace dqnx {
 
+// One wave per output row (z, b, ho, wo): the row's decomposition is computed once, the 64
+// lanes write 64 consecutive columns (coalesced), 32-bit index math throughout.
 __global__ __launch_bounds__(256) void k_im2col(Im2colArgs a) {
-    const int64_t per = (int64_t)a.M * a.Kstride;
-    const int64_t total = per * a.nstreams;
+    const int lane = threadIdx.x & 63;
+    const int rows = a.M * a.nstreams;
     const int HoWo = a.Ho * a.Wo, KK = a.kh * a.kw;
-    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
-        const int z = (int)(t / per);
-        const int64_t rem = t - (int64_t)z * per;
-        const int m = (int)(rem / a.Kstride);
-        const int kk = (int)(rem - (int64_t)m * a.Kstride);
-        float v = 0.f;
-        if (kk < a.K) {
-            const int b = m / HoWo, p = m - b * HoWo;
-            const int ho = p / a.Wo, wo = p - ho * a.Wo;
-            const int ci = kk / KK, r = kk - ci * KK;
-            const int i = r / a.kw, j = r - i * a.kw;
-            const int h = ho * a.sh - a.ph + i, w = wo * a.sw - a.pw + j;
-            if (h >= 0 && h < a.Hi && w >= 0 && w < a.Wi) {
-                if (a.ring[z]) {   // first conv: CHW micro grid straight from the gathered ring row
-                    const int64_t row = a.phys[b];
-                    v = a.ring[z][row * a.ring_stride + a.ring_off + ((int64_t)ci * a.Hi + h) * a.Wi + w];
-                } else {
-                    v = a.src[z][((int64_t)(b * a.Hi + h) * a.Wi + w) * a.Ci + ci];
+    const int wave0 = blockIdx.x * 4 + (threadIdx.x >> 6), nwaves = gridDim.x * 4;
+    for (int r = wave0; r < rows; r += nwaves) {
+        const int z = r / a.M, m = r - z * a.M;
+        const int b = m / HoWo, p = m - b * HoWo;
+        const int ho = p / a.Wo, wo = p - ho * a.Wo;
+        const int h0 = ho * a.sh - a.ph, w0 = wo * a.sw - a.pw;
+        const float* ring = a.ring[z];
+        const float* src = a.src[z];
+        const int64_t rbase = ring ? (int64_t)a.phys[b] * a.ring_stride + a.ring_off : 0;
+        float* out = a.col[z] + (int64_t)m * a.Kstride;
+        for (int kk = lane; kk < a.Kstride; kk += 64) {
+            float v = 0.f;
+            if (kk < a.K) {
+                const int ci = kk / KK, rr = kk - ci * KK;
+                const int i = rr / a.kw, j = rr - i * a.kw;
+                const int h = h0 + i, w = w0 + j;
+                if (h >= 0 && h < a.Hi && w >= 0 && w < a.Wi) {
+                    if (ring) v = ring[rbase + (ci * a.Hi + h) * a.Wi + w];   // CHW micro grid
+                    else v = src[((int64_t)(b * a.Hi + h) * a.Wi + w) * a.Ci + ci];   // NHWC
                 }
             }
+            out[kk] = v;
         }
-        a.col[z][(int64_t)m * a.Kstride + kk] = v;
     }
 }
 
@@ -77,15 +80,15 @@ __global__ __launch_bounds__(256) void k_unflatten(UnflattenArgs a) {
 // previous conv's activation backward: dZprev = act'(Hprev) (.) dX.
 template <int ACT>
 __global__ __launch_bounds__(256) void k_col2im(Col2imArgs a) {
-    const int64_t total = (int64_t)a.Bl * a.Hi * a.Wi * a.Ci;
+    const int total = a.Bl * a.Hi * a.Wi * a.Ci;
     const int KK = a.kh * a.kw;
-    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
-        const int ci = (int)(t % a.Ci);
-        int64_t q = t / a.Ci;
-        const int w = (int)(q % a.Wi);
+    for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < total; t += gridDim.x * blockDim.x) {
+        const int ci = t % a.Ci;
+        int q = t / a.Ci;
+        const int w = q % a.Wi;
         q /= a.Wi;
-        const int h = (int)(q % a.Hi);
-        const int b = (int)(q / a.Hi);
+        const int h = q % a.Hi;
+        const int b = q / a.Hi;
         float s = 0.f;
         for (int i = 0; i < a.kh; i++) {
             const int hh = h + a.ph - i;
@@ -113,7 +116,9 @@ static dim3 grid_for(int64_t total) {
 }
 
 int launch_im2col(const Im2colArgs& a, hipStream_t s) {
-    hipLaunchKernelGGL(k_im2col, grid_for((int64_t)a.M * a.Kstride * a.nstreams), dim3(256), 0, s, a);
+    int64_t g = ((int64_t)a.M * a.nstreams + 3) / 4;   // 4 rows (waves) per block
+    if (g > 8192) g = 8192;
+    hipLaunchKernelGGL(k_im2col, dim3((unsigned)g), dim3(256), 0, s, a);
     DQNX_HIP_CHECK(hipGetLastError());
     return DQNX_OK;
 }
