@@ -314,7 +314,8 @@ def main():
         intensity = fl / by if by else 0.0
         ridge = PEAK_FP32_MFMA_TFLOPS * 1e12 / (PEAK_HBM_GBS * 1e9)
         traffic = None
-        pmc_path = os.path.join(REPO, "profiles", "pmc_traffic.json")
+        # HBM bytes per launch from rocprofv3 PMC passes of this same workload (tools/pmc_traffic.py)
+        pmc_path = os.path.join(REPO, "profiles", f"pmc_traffic_{args.net}_b{args.batch}.json")
         if os.path.exists(pmc_path):
             try:
                 traffic = json.load(open(pmc_path)).get(nm, {}).get("hbm_bytes_per_launch")

@@ -1,0 +1,57 @@
+"""Per-kernel HBM traffic per dispatch from rocprofv3 --pmc passes (tools/pmc.sh with
+tools/pmc_traffic_groups.txt) -> profiles/pmc_traffic_<net>_b<batch>.json, read by bench.py's roofline.
+
+hbm_bytes_per_launch = (2 * FETCH_SIZE + WRITE_SIZE) * 1024, per MI355X_MICROARCH.md §HBM:
+FETCH_SIZE (KB) reads exactly half the bytes of a wide (16 B/lane) coalesced read on gfx950,
+WRITE_SIZE (KB) is exact for 16-B stores.  Kernel names map to bench.py's step names."""
+import csv
+import glob
+import json
+import os
+import sys
+from collections import defaultdict
+
+NAMES = [   # (substring of the HIP kernel name, bench step name)
+    ("k_linear_fwd<0, true, true>", "linear_fwd_l1"),
+    ("k_linear_fwd<0, true, false>", "linear_fwd_l2"),
+    ("k_sample_uniform", "sample_uniform"),
+    ("k_head<", "head_td_loss"),
+    ("k_bwd_level<", "linear_bwd (both levels)"),
+    ("k_adam", "adam_fused"),
+    ("k_per_sample", "per_sample"),
+    ("k_per_update", "per_update"),
+]
+
+
+def bench_name(kernel):
+    for sub, nm in NAMES:
+        if sub in kernel:
+            return nm
+    return None
+
+
+def main(root="gpurun_out/pmc", out="profiles/pmc_traffic_mlp_b1024.json"):
+    vals = defaultdict(lambda: defaultdict(list))   # bench name -> counter -> per-dispatch values
+    for f in glob.glob(os.path.join(root, "p*", "**", "*counter_collection.csv"), recursive=True):
+        for r in csv.DictReader(open(f)):
+            nm = bench_name(r.get("Kernel_Name", ""))
+            if nm is None:
+                continue
+            vals[nm][r["Counter_Name"]].append(float(r["Counter_Value"]))
+    res = {}
+    for nm, cs in vals.items():
+        d = {k: sum(v) / len(v) for k, v in cs.items()}
+        e = {"dispatches": max(len(v) for v in cs.values()), **{k + "_avg": v for k, v in d.items()}}
+        if "FETCH_SIZE" in d and "WRITE_SIZE" in d:
+            e["hbm_bytes_per_launch"] = (2.0 * d["FETCH_SIZE"] + d["WRITE_SIZE"]) * 1024.0
+        if "TCC_HIT_sum" in d and "TCC_MISS_sum" in d and d["TCC_HIT_sum"] + d["TCC_MISS_sum"] > 0:
+            e["l2_hit_rate"] = d["TCC_HIT_sum"] / (d["TCC_HIT_sum"] + d["TCC_MISS_sum"])
+        res[nm] = e
+    res["_note"] = ("per-dispatch averages over every dispatch of the bench run (timed + timing steps); "
+                    "hbm_bytes = (2*FETCH_SIZE + WRITE_SIZE)*1024 (gfx950 FETCH_SIZE half-count correction)")
+    json.dump(res, open(out, "w"), indent=1, sort_keys=True)
+    print(json.dumps(res, indent=1, sort_keys=True))
+
+
+if __name__ == "__main__":
+    main(*sys.argv[1:])
