@@ -38,6 +38,7 @@ __device__ __forceinline__ float act_fwd(float x) {
 
 __device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
 
+
 // XCD-aware block remap (CDNA guide T1): blocks are dealt round-robin over the 8 XCDs, so
 // hand XCD x a CONTIGUOUS range of tiles (bijective for any total).  Speed only: placement
 // never affects results.

@@ -169,7 +169,10 @@ struct dqnx_engine {
     uint64_t total = 0;
     // workspace sub-regions (byte offsets from the arena base)
     uint64_t ws_phys = 0, ws_pool = 0, ws_xobs = 0, ws_head_part = 0, ws_loss_part = 0, ws_stage = 0;
-    uint64_t ws_adam_tab = 0, ws_stamps = 0, ws_dhead = 0;
+    uint64_t ws_adam_tab = 0, ws_stamps = 0, ws_dhead = 0, ws_raw = 0, ws_trans = 0, ws_tickets = 0;
+    int64_t n_tickets = 0;
+    // fused plan: fragment-blocked weight copies [online fwd | target fwd | online chain] per layer
+    uint64_t ws_wblk[2][FUSED_MAX_L] = {{0}}, ws_wblkT[FUSED_MAX_L] = {0};
     std::vector<uint64_t> ws_H, ws_dZ, ws_part;
     // two-stream CNN: per conv layer im2col [3][M][Kstride], activations [3][M][Co],
     // dZ [M][Co], split-K partial slabs; dense input F [3][Bl][strideF] and its gradient
@@ -188,9 +191,12 @@ struct dqnx_engine {
     hipEvent_t fork_ev = nullptr, join_ev = nullptr;
     hipEvent_t ev_sampled[2] = {nullptr, nullptr}, ev_computed[2] = {nullptr, nullptr};
     bool pf_computed_valid[2] = {false, false};
-    // backward plan: 0 = split-K backward levels + Adam pass (default, fastest measured at
-    // batch 1024); 1 = head kernel also makes dZ_{L-1}, one full-K dW + Adam launch
+    // step plan: 2 = fused MLP plan (default where supported: one forward launch for every
+    // layer + head, one head/TD/dZ-chain launch, one split-K dW launch, Adam); 0 = per-layer
+    // forward + split-K backward levels + Adam pass (two-stream nets); 1 = head kernel also
+    // makes dZ_{L-1}, one full-K dW + Adam launch
     int bwd_plan = 0;
+    FusedFwdArgs fplan;     // LDS geometry of the fused plan (valid when bwd_plan == 2)
     bool pf_valid = false;   // a prefetched minibatch for the next step sits in slot pf_slot
     int pf_slot = 0;
 };
@@ -259,6 +265,22 @@ int layout(dqnx_engine* e) {
     }
     e->ws_head_part = sub((uint64_t)e->slices[L - 1] * np.head_params * 4);
     e->ws_dhead = sub((uint64_t)e->Bl * 16 * 4);
+    e->ws_raw = sub((uint64_t)3 * e->Bl * 16 * 4);
+    e->ws_trans = sub((uint64_t)e->Bl * 16);
+    {   // dW seam arrival counters: an upper bound on the parameter tiles (16 x 16 tiles)
+        uint64_t t = (uint64_t)((np.NH + 15) / 16) * ((np.F + 1 + 15) / 16);
+        for (int l = 0; l < L; l++) t += (uint64_t)((np.dense[l].out + 15) / 16) * ((np.dense[l].in + 1 + 15) / 16);
+        e->n_tickets = (int64_t)t;
+        e->ws_tickets = sub(t * 4);
+    }
+    if (e->bwd_plan == 2) {
+        for (int l = 0; l < L; l++) {
+            const uint64_t fwd = (uint64_t)np.dense[l].out * e->fplan.kpad[l] * 4;
+            e->ws_wblk[0][l] = sub(fwd);
+            e->ws_wblk[1][l] = sub(fwd);
+            if (l >= 1) e->ws_wblkT[l] = sub((uint64_t)np.dense[l].out * np.dense[l].in * 4);
+        }
+    }
     e->ws_adam_tab = sub((uint64_t)kAdamTable * 2 * 4);
     e->ws_stamps = sub(64 * 8);
     e->ws_loss_part = sub((uint64_t)e->tiles * 4);
@@ -354,6 +376,341 @@ int enqueue_per_update(dqnx_engine* e, const int32_t* idx, hipStream_t s) {
     return enqueue_per_update_pairs(e, idx, at<float>(e, e->off[DQNX_BUF_PER_ABS_TD]), e->Bg, s);
 }
 
+// Optimizer fields shared by AdamArgs and DwSeamArgs (torch Adam defaults of the config).
+template <class T>
+void fill_adam_fields(dqnx_engine* e, int flags, T& aa) {
+    const dqnx_config& c = e->cfg;
+    aa.mode = (flags & DQNX_STEP_GRADS_ONLY) ? 0 : 1;
+    aa.soft = (flags & DQNX_STEP_SOFT_UPDATE) ? 1 : 0;
+    aa.n_params = e->np.P;
+    aa.p = at<float>(e, e->off[DQNX_BUF_PARAMS]);
+    aa.m = at<float>(e, e->off[DQNX_BUF_ADAM_M]);
+    aa.v = at<float>(e, e->off[DQNX_BUF_ADAM_V]);
+    aa.grads = at<float>(e, e->off[DQNX_BUF_GRADS]);
+    aa.target = at<float>(e, e->off[DQNX_BUF_TARGET_PARAMS]);
+    aa.ctrl = ctrl_of(e);
+    aa.w1 = (float)(1.0 - c.beta1);          // Python: exp_avg.lerp_(grad, 1 - beta1)
+    aa.beta2 = (float)c.beta2;
+    aa.c2 = (float)(1.0 - c.beta2);
+    aa.eps = (float)c.adam_eps;
+    aa.tau = (float)(c.tau * c.n_env);      // (tau * n_env) * online + (1 - tau * n_env) * target
+    aa.one_minus_tau = (float)(1.0 - c.tau * c.n_env);
+    aa.adam_table = at<float>(e, e->ws_adam_tab);
+    aa.adam_table_len = kAdamTable;
+    aa.beta1d = c.beta1;
+    aa.beta2d = c.beta2;
+    aa.lrd = c.lr;
+    aa.loss_partial = at<float>(e, e->ws_loss_part);
+    aa.n_loss_partial = e->tiles;
+    aa.batch_global = e->Bg;
+}
+
+// Gradient reduction (fixed-order sum of the split-K slabs) + Adam (+ soft update).
+KStep adam_kstep(dqnx_engine* e, int flags) {
+    const dqnx_config& c = e->cfg;
+    const NetPlan& np = e->np;
+    const int L = (int)np.dense.size();
+    const int NC = (int)np.conv.size();
+    dqnx_ctrl* ctrl = ctrl_of(e);
+    float* params = at<float>(e, e->off[DQNX_BUF_PARAMS]);
+    float* tparams = at<float>(e, e->off[DQNX_BUF_TARGET_PARAMS]);
+    AdamArgs aa;
+    memset(&aa, 0, sizeof(aa));
+    aa.nseg = 0;
+    double part_elems = 0;
+    for (int l = 0; l < NC; l++) {   // segments in flat-offset order: convs, dense, head
+        const ConvPlan& cp = np.conv[l];
+        AdamSegment& sg = aa.seg[aa.nseg++];
+        sg.off = cp.off;
+        sg.partial = at<float>(e, e->ws_cpart[l]);
+        sg.pstride = (int64_t)cp.Co * cp.K + cp.Co;
+        sg.S = e->cslices[l];
+        part_elems += (double)sg.S * sg.pstride;
+    }
+    for (int l = 0; l < L; l++) {
+        AdamSegment& sg = aa.seg[aa.nseg++];
+        sg.off = np.dense[l].off;
+        sg.partial = at<float>(e, e->ws_part[l]);
+        sg.pstride = (int64_t)np.dense[l].out * np.dense[l].in + np.dense[l].out;
+        sg.S = e->slices[l];
+        part_elems += (double)sg.S * sg.pstride;
+    }
+    {
+        AdamSegment& sg = aa.seg[aa.nseg++];
+        sg.off = np.head_off;
+        sg.partial = at<float>(e, e->ws_head_part);
+        sg.pstride = np.head_params;
+        sg.S = e->slices[L - 1];
+        part_elems += (double)sg.S * sg.pstride;
+    }
+    aa.mode = (flags & DQNX_STEP_GRADS_ONLY) ? 0 : 1;
+    aa.soft = (flags & DQNX_STEP_SOFT_UPDATE) ? 1 : 0;
+    aa.n_params = np.P;
+    aa.p = params;
+    aa.m = at<float>(e, e->off[DQNX_BUF_ADAM_M]);
+    aa.v = at<float>(e, e->off[DQNX_BUF_ADAM_V]);
+    aa.grads = at<float>(e, e->off[DQNX_BUF_GRADS]);
+    aa.target = tparams;
+    aa.ctrl = ctrl;
+    aa.w1 = (float)(1.0 - c.beta1);          // Python: exp_avg.lerp_(grad, 1 - beta1)
+    aa.beta2 = (float)c.beta2;
+    aa.c2 = (float)(1.0 - c.beta2);
+    aa.eps = (float)c.adam_eps;
+    aa.tau = (float)(c.tau * c.n_env);      // (tau * n_env) * online + (1 - tau * n_env) * target
+    aa.one_minus_tau = (float)(1.0 - c.tau * c.n_env);
+    aa.adam_table = at<float>(e, e->ws_adam_tab);
+    aa.adam_table_len = kAdamTable;
+    aa.beta1d = c.beta1;
+    aa.beta2d = c.beta2;
+    aa.lrd = c.lr;
+    aa.loss_partial = at<float>(e, e->ws_loss_part);
+    aa.n_loss_partial = e->tiles;
+    aa.batch_global = e->Bg;
+    KStep k;
+    k.name = aa.mode ? "adam_fused" : "grad_reduce";
+    const double P = (double)np.P;
+    // read partials; write g; Adam: read p,m,v (+target), write p,m,v (+target)
+    k.bytes = 4.0 * (part_elems + P + (aa.mode ? 6.0 * P + (aa.soft ? 2.0 * P : 0.0) : 0.0));
+    k.flops = aa.mode ? 12.0 * P : 0.0;
+    k.run = [=](hipStream_t s) { return launch_adam(aa, s); };
+    return k;
+}
+
+// Blocked weight copies for the fused plan (relayout.hpp), rebuilt by spare workgroups of
+// the sampler launch at the start of every step.
+RelayoutArgs relayout_args(dqnx_engine* e, int* blocks) {
+    RelayoutArgs r;
+    memset(&r, 0, sizeof(r));
+    *blocks = 0;
+    if (e->bwd_plan != 2) return r;
+    const NetPlan& np = e->np;
+    float* params = at<float>(e, e->off[DQNX_BUF_PARAMS]);
+    float* tparams = at<float>(e, e->off[DQNX_BUF_TARGET_PARAMS]);
+    int64_t q = 0;
+    auto add = [&](const float* src, float* dst, int rows, int cols, int kind, int nch, int64_t nq) {
+        RelayoutJob& j = r.job[r.njobs++];
+        j.src = src; j.dst = dst; j.rows = rows; j.cols = cols; j.kind = kind; j.nch = nch; j.q0 = q;
+        q += nq;
+    };
+    for (int l = 0; l < (int)np.dense.size(); l++) {
+        const LayerPlan& lp = np.dense[l];
+        const int kp = e->fplan.kpad[l];
+        const int64_t nq = (int64_t)lp.out * kp / 4;
+        add(params + lp.off, at<float>(e, e->ws_wblk[0][l]), lp.out, lp.in, 0, kp / 16, nq);
+        add(tparams + lp.off, at<float>(e, e->ws_wblk[1][l]), lp.out, lp.in, 0, kp / 16, nq);
+        if (l >= 1) add(params + lp.off, at<float>(e, e->ws_wblkT[l]), lp.out, lp.in, 1, lp.out / 16,
+                        (int64_t)lp.out * lp.in / 4);
+    }
+    r.total_q = q;
+    int b = (int)((q + 1023) / 1024);
+    *blocks = b < 1 ? 1 : (b > 64 ? 64 : b);
+    return r;
+}
+
+// Fused MLP plan (bwd_plan 2): forward of every layer + head in one launch, head / TD /
+// dZ chain in one launch, every dW in one split-K launch, then the Adam pass.
+void build_fused_steps(dqnx_engine* e, int flags, int32_t* idx, int32_t* phys, std::vector<KStep>& ks) {
+    const dqnx_config& c = e->cfg;
+    const NetPlan& np = e->np;
+    const int L = (int)np.dense.size();
+    const int A = c.net.n_actions;
+    const int act = c.net.activation;
+    dqnx_ctrl* ctrl = ctrl_of(e);
+    float* params = at<float>(e, e->off[DQNX_BUF_PARAMS]);
+    float* tparams = at<float>(e, e->off[DQNX_BUF_TARGET_PARAMS]);
+    const double Bl = e->Bl;
+    const bool dbl = c.algo != DQNX_ALGO_DQN;
+    const int nstreams = dbl ? 3 : 2;
+    double body_flops = 0, wbytes = 0;   // per stream: 2 * in * out summed; weight bytes
+    for (int l = 0; l < L; l++) {
+        body_flops += 2.0 * np.dense[l].in * np.dense[l].out;
+        wbytes += 4.0 * (np.dense[l].in + 1.0) * np.dense[l].out;
+    }
+    // 2. forward (R:dqn/agent.py:209-214 / 172-173 streams, R:dqn/network.py:61-65, 90-96)
+    {
+        FusedFwdArgs fa = e->fplan;
+        fa.Bl = e->Bl;
+        fa.tiles = e->tiles;
+        fa.nstreams = nstreams;
+        for (int l = 0; l < L; l++) fa.woff[l] = np.dense[l].off;
+        fa.head_off = np.head_off;
+        fa.head_kind = c.net.head;
+        fa.stream_of[0] = 0;
+        fa.stream_of[1] = dbl ? 1 : 2;
+        fa.stream_of[2] = 2;
+        fa.params = params;
+        fa.tparams = tparams;
+        fa.ring_obs = at<float>(e, e->off[DQNX_BUF_RING_OBS]);
+        fa.ring_next = at<float>(e, e->off[DQNX_BUF_RING_NEXT_OBS]);
+        fa.ring_stride = e->stride;
+        fa.phys = phys;
+        fa.xcopy = at<float>(e, e->ws_xobs);
+        for (int l = 0; l < L; l++) fa.H[l] = at<float>(e, e->ws_H[l]);   // stream-0 third of [3][Bl][w]
+        fa.raw = at<float>(e, e->ws_raw);
+        fa.trans = at<float4>(e, e->ws_trans);
+        fa.act = at<int32_t>(e, e->off[DQNX_BUF_RING_ACT]);
+        fa.rew = at<float>(e, e->off[DQNX_BUF_RING_REW]);
+        fa.done = at<float>(e, e->off[DQNX_BUF_RING_DONE]);
+        for (int l = 0; l < L; l++) {
+            fa.wblk[0][l] = at<float>(e, e->ws_wblk[0][l]);
+            fa.wblk[1][l] = at<float>(e, e->ws_wblk[1][l]);
+        }
+        fa.stamps = at<int64_t>(e, e->ws_stamps);
+        KStep k;
+        k.name = "mlp_fwd";
+        k.flops = nstreams * Bl * (body_flops + 2.0 * np.NH * np.F);
+        // gathered rows in, stream-0 rows + activations + raw heads out, online + target weights
+        double hsum = 0;
+        for (int l = 0; l < L; l++) hsum += np.dense[l].out;
+        k.bytes = 4.0 * (nstreams * Bl * np.dense[0].in + Bl * np.dense[0].in + Bl * hsum + 3.0 * Bl * 16)
+                  + 2.0 * (wbytes + 4.0 * np.head_params);
+        k.run = [=](hipStream_t s) { return launch_fused_fwd(fa, act, s); };
+        ks.push_back(k);
+    }
+    // 3. head / TD / Huber / dZ chain (R:dqn/agent.py:209-221; PER :259-267)
+    {
+        HeadBwdArgs ha;
+        memset(&ha, 0, sizeof(ha));
+        ha.L = L;
+        ha.Bl = e->Bl;
+        ha.nsplit = 1;
+        if (L >= 2 && np.dense[0].out % (2 * 64) == 0) ha.nsplit = 2;   // dZ_1 columns over 2 workgroups
+        if (const char* ns = getenv("DQNX_HEAD_SPLIT")) { const int v = atoi(ns); if (v == 1 || (v == 2 && ha.nsplit == 2)) ha.nsplit = v; }
+        ha.A = A;
+        ha.NH = np.NH;
+        ha.F = np.F;
+        ha.head_kind = c.net.head;
+        ha.algo = c.algo;
+        for (int l = 0; l < L; l++) {
+            ha.in[l] = np.dense[l].in;
+            ha.out[l] = np.dense[l].out;
+            ha.woff[l] = np.dense[l].off;
+            ha.H[l] = at<float>(e, e->ws_H[l]);
+            ha.dZ[l] = at<float>(e, e->ws_dZ[l]);
+        }
+        ha.head_off = np.head_off;
+        ha.inv_bg = (float)(1.0 / (double)e->Bg);
+        ha.gamma = (float)c.gamma;
+        ha.params = params;
+        ha.raw = at<float>(e, e->ws_raw);
+        ha.trans = at<float4>(e, e->ws_trans);
+        ha.phys = phys;
+        ha.act = at<int32_t>(e, e->off[DQNX_BUF_RING_ACT]);
+        ha.rew = at<float>(e, e->off[DQNX_BUF_RING_REW]);
+        ha.done = at<float>(e, e->off[DQNX_BUF_RING_DONE]);
+        ha.isw = (c.algo == DQNX_ALGO_PER_DOUBLE) ? at<float>(e, e->off[DQNX_BUF_IS_WEIGHTS]) + e->shard_begin : nullptr;
+        ha.abs_td_out = (c.algo == DQNX_ALGO_PER_DOUBLE) ? at<float>(e, e->off[DQNX_BUF_PER_ABS_TD]) + e->shard_begin
+                                                         : nullptr;
+        ha.Q = at<float>(e, e->off[DQNX_BUF_Q]);
+        ha.td = at<float>(e, e->off[DQNX_BUF_TD]);
+        ha.dhead = at<float>(e, e->ws_dhead);
+        ha.loss_partial = at<float>(e, e->ws_loss_part);
+        ha.ctrl = ctrl;
+        for (int l = 1; l < L; l++) ha.wblkT[l] = at<float>(e, e->ws_wblkT[l]);
+        ha.stamps = at<int64_t>(e, e->ws_stamps);
+        KStep k;
+        k.name = "head_bwd";
+        double dzf = 2.0 * Bl * 16 * np.F, dzb = 0;
+        for (int l = L - 1; l >= 1; l--) {
+            dzf += 2.0 * Bl * np.dense[l].out * np.dense[l].in;
+            dzb += 4.0 * (np.dense[l].out * (double)np.dense[l].in + 2.0 * Bl * np.dense[l].in);
+        }
+        k.flops = dzf;
+        k.bytes = 4.0 * (3.0 * Bl * 16 + 2.0 * Bl * np.F + 16.0 * Bl + 3.0 * Bl * A + 6.0 * Bl) + dzb
+                  + 4.0 * np.head_params;
+        k.run = [=](hipStream_t s) { return launch_head_bwd(ha, act, s); };
+        ks.push_back(k);
+    }
+    // 3b. PER priorities (single GPU; under DP after the all-gather, in dqnx_apply_grads)
+    if (c.algo == DQNX_ALGO_PER_DOUBLE && !(flags & DQNX_STEP_GRADS_ONLY)) {
+        KStep k;
+        k.name = "per_update";
+        k.bytes = e->Bg * (4.0 + 4.0 + 8.0 * 2.0 * 21.0);
+        k.run = [=](hipStream_t s) { return enqueue_per_update(e, idx, s); };
+        ks.push_back(k);
+    }
+    // 4. every weight gradient: split-K slabs of dZ_l^T [X_l | 1] and dHead^T [H_L | 1]
+    {
+        BwdArgs ba;
+        memset(&ba, 0, sizeof(ba));
+        ba.Bl = e->Bl;
+        ba.kslice = e->kslice[0];
+        ba.dw_slices = e->slices[0];
+        double flops = 0, bytes = 0;
+        for (int l = L - 1; l >= 0; l--) {   // widest problems last: the grid tail is the head
+            const LayerPlan lp = np.dense[l];
+            DwProblem& d = ba.dw[ba.ndw++];
+            d.dZ = at<float>(e, e->ws_dZ[l]);
+            d.ldz = lp.out;
+            if (l > 0) {
+                d.X = at<float>(e, e->ws_H[l - 1]);
+                d.ldx = lp.in;
+            } else {
+                d.X = at<float>(e, e->ws_xobs);
+                d.ldx = e->stride;
+            }
+            d.in = lp.in;
+            d.out = lp.out;
+            d.partial = at<float>(e, e->ws_part[l]);
+            d.pstride = (int64_t)lp.out * lp.in + lp.out;
+            d.head_kind = -1;
+            flops += 2.0 * Bl * lp.out * (lp.in + 1.0);
+            bytes += 4.0 * (Bl * (lp.out + lp.in) + ba.dw_slices * (lp.out * (lp.in + 1.0)));
+        }
+        {
+            DwProblem& h = ba.dw[ba.ndw++];
+            h.dZ = at<float>(e, e->ws_dhead);
+            h.ldz = 16;
+            h.X = at<float>(e, e->ws_H[L - 1]);
+            h.ldx = np.F;
+            h.in = np.F;
+            h.out = np.NH;
+            h.partial = at<float>(e, e->ws_head_part);
+            h.pstride = np.head_params;
+            h.head_kind = c.net.head;
+            h.A = A;
+            flops += 2.0 * Bl * np.NH * (np.F + 1.0);
+            bytes += 4.0 * (16.0 * Bl + Bl * np.F + ba.dw_slices * (double)np.head_params);
+        }
+        const char* sv = getenv("DQNX_DW_SEAM");
+        if (sv && atoi(sv) == 0) {   // two launches: split-K slabs, then the Adam pass
+            bwd_level_grid(ba);
+            KStep k;
+            k.name = "dw_all";
+            k.flops = flops;
+            k.bytes = bytes;
+            k.run = [=](hipStream_t s) { return launch_bwd_level(ba, act, s); };
+            ks.push_back(k);
+            ks.push_back(adam_kstep(e, flags));
+            return;
+        }
+        // 5. one launch: slabs + last-arriver reduction + Adam (+ soft update)
+        DwSeamArgs da;
+        memset(&da, 0, sizeof(da));
+        da.b = ba;
+        const int ntiles = dw_seam_tiles(da.b);
+        if (ntiles > e->n_tickets) { e->n_tickets = -1; return; }   // cannot happen (16x16 bound)
+        int t0 = 0;
+        for (int p = 0; p < da.b.ndw; p++) {
+            da.tile0[p] = t0;
+            t0 += da.b.dw[p].grid_x * da.b.dw[p].grid_y;
+        }
+        for (int p = 0; p < da.b.ndw; p++) {   // problems were added layer L-1 .. 0, then the head
+            const int l = L - 1 - p;
+            da.poff[p] = (p < L) ? np.dense[l].off : np.head_off;
+        }
+        da.tickets = at<int>(e, e->ws_tickets);
+        fill_adam_fields(e, flags, da);
+        const double P = (double)np.P;
+        KStep k;
+        k.name = da.mode ? "dw_adam" : "dw_grads";
+        k.flops = flops + (da.mode ? 12.0 * P : 0.0);
+        k.bytes = bytes + 4.0 * (ba.dw_slices * P + P + (da.mode ? 6.0 * P + (da.soft ? 2.0 * P : 0.0) : 0.0));
+        k.run = [=](hipStream_t s) { return launch_dw_seam(da, s); };
+        ks.push_back(k);
+    }
+}
+
 // key = flags | (slot << 8): `slot` selects the (sampled indices, physical rows) buffer pair.
 std::vector<KStep> build_learn_steps(dqnx_engine* e, int key) {
     const int flags = key & 0xff;
@@ -373,8 +730,12 @@ std::vector<KStep> build_learn_steps(dqnx_engine* e, int key) {
     const double Bg_ = e->Bg;
 
     // 1. sample (R:dqn/replay_memory.py:38-39; PER :69-92)
+    int rl_blocks = 0;
+    const RelayoutArgs rl = relayout_args(e, &rl_blocks);
     if (c.algo == DQNX_ALGO_PER_DOUBLE) {
-        const PerSampleArgs pa = per_sample_args(e, idx, phys);
+        PerSampleArgs pa = per_sample_args(e, idx, phys);
+        pa.rl = rl;
+        pa.rl_blocks = rl_blocks;
         KStep k;
         k.name = "per_sample";
         k.bytes = 2.0 * 625 * 4 + 8.0 * Bg_ * 22 + 8.0 * e->Bg + 4.0 * Bl;
@@ -384,7 +745,9 @@ std::vector<KStep> build_learn_steps(dqnx_engine* e, int key) {
         KStep k;
         k.name = "idx_to_phys";
         k.bytes = 8.0 * Bl;
-        k.run = [=](hipStream_t s) { return launch_idx_to_phys(idx, phys, e->shard_begin, e->Bl, ctrl, c.capacity, s); };
+        k.run = [=](hipStream_t s) {
+            return launch_idx_to_phys(idx, phys, e->shard_begin, e->Bl, ctrl, c.capacity, &rl, rl_blocks, s);
+        };
         ks.push_back(k);
     } else {
         SampleArgs sa;
@@ -402,11 +765,18 @@ std::vector<KStep> build_learn_steps(dqnx_engine* e, int key) {
         sa.wptr_dev = &ctrl->ring_wptr;
         sa.capacity = c.capacity;
         sa.stamps = at<int64_t>(e, e->ws_stamps);
+        sa.rl = rl;
+        sa.rl_blocks = rl_blocks;
         KStep k;
         k.name = "sample_uniform";
         k.bytes = 2.0 * 625 * 4 + 4.0 * e->Bg + 4.0 * Bl;
         k.run = [=](hipStream_t s) { return launch_sample_uniform(sa, s); };
         ks.push_back(k);
+    }
+
+    if (e->bwd_plan == 2) {
+        build_fused_steps(e, flags, idx, phys, ks);
+        return ks;
     }
 
     // 2. forward layers: streams 0 online(obs), 1 online(next) [double], 2 target(next)
@@ -729,68 +1099,7 @@ std::vector<KStep> build_learn_steps(dqnx_engine* e, int key) {
     }
 
     // 5. gradient reduction + Adam (+ soft update)
-    {
-        AdamArgs aa;
-        memset(&aa, 0, sizeof(aa));
-        aa.nseg = 0;
-        double part_elems = 0;
-        for (int l = 0; l < NC; l++) {   // segments in flat-offset order: convs, dense, head
-            const ConvPlan& cp = np.conv[l];
-            AdamSegment& sg = aa.seg[aa.nseg++];
-            sg.off = cp.off;
-            sg.partial = at<float>(e, e->ws_cpart[l]);
-            sg.pstride = (int64_t)cp.Co * cp.K + cp.Co;
-            sg.S = e->cslices[l];
-            part_elems += (double)sg.S * sg.pstride;
-        }
-        for (int l = 0; l < L; l++) {
-            AdamSegment& sg = aa.seg[aa.nseg++];
-            sg.off = np.dense[l].off;
-            sg.partial = at<float>(e, e->ws_part[l]);
-            sg.pstride = (int64_t)np.dense[l].out * np.dense[l].in + np.dense[l].out;
-            sg.S = e->slices[l];
-            part_elems += (double)sg.S * sg.pstride;
-        }
-        {
-            AdamSegment& sg = aa.seg[aa.nseg++];
-            sg.off = np.head_off;
-            sg.partial = at<float>(e, e->ws_head_part);
-            sg.pstride = np.head_params;
-            sg.S = e->slices[L - 1];
-            part_elems += (double)sg.S * sg.pstride;
-        }
-        aa.mode = (flags & DQNX_STEP_GRADS_ONLY) ? 0 : 1;
-        aa.soft = (flags & DQNX_STEP_SOFT_UPDATE) ? 1 : 0;
-        aa.n_params = np.P;
-        aa.p = params;
-        aa.m = at<float>(e, e->off[DQNX_BUF_ADAM_M]);
-        aa.v = at<float>(e, e->off[DQNX_BUF_ADAM_V]);
-        aa.grads = at<float>(e, e->off[DQNX_BUF_GRADS]);
-        aa.target = tparams;
-        aa.ctrl = ctrl;
-        aa.w1 = (float)(1.0 - c.beta1);          // Python: exp_avg.lerp_(grad, 1 - beta1)
-        aa.beta2 = (float)c.beta2;
-        aa.c2 = (float)(1.0 - c.beta2);
-        aa.eps = (float)c.adam_eps;
-        aa.tau = (float)(c.tau * c.n_env);      // (tau * n_env) * online + (1 - tau * n_env) * target
-        aa.one_minus_tau = (float)(1.0 - c.tau * c.n_env);
-        aa.adam_table = at<float>(e, e->ws_adam_tab);
-        aa.adam_table_len = kAdamTable;
-        aa.beta1d = c.beta1;
-        aa.beta2d = c.beta2;
-        aa.lrd = c.lr;
-        aa.loss_partial = at<float>(e, e->ws_loss_part);
-        aa.n_loss_partial = e->tiles;
-        aa.batch_global = e->Bg;
-        KStep k;
-        k.name = aa.mode ? "adam_fused" : "grad_reduce";
-        const double P = (double)np.P;
-        // read partials; write g; Adam: read p,m,v (+target), write p,m,v (+target)
-        k.bytes = 4.0 * (part_elems + P + (aa.mode ? 6.0 * P + (aa.soft ? 2.0 * P : 0.0) : 0.0));
-        k.flops = aa.mode ? 12.0 * P : 0.0;
-        k.run = [=](hipStream_t s) { return launch_adam(aa, s); };
-        ks.push_back(k);
-    }
+    ks.push_back(adam_kstep(e, flags));
     } else {
     // 4. dZ of levels below L-1 (deeper MLPs only; the head kernel produced dZ_L and dZ_{L-1})
     for (int l = L - 2; l >= 1; l--) {
@@ -1059,8 +1368,23 @@ int dqnx_engine_create(const dqnx_config* cfg, dqnx_engine** out) {
     for (size_t l = 0; l < e->np.dense.size(); l++)
         if (e->np.dense[l].out % 4) { delete e; return set_error(DQNX_EUNSUPPORTED, "hidden widths must be multiples of 4"); }
     if (sample_hash_slots(c.batch) < 0) { delete e; return set_error(DQNX_EUNSUPPORTED, "batch too large for the sampler"); }
-    if (const char* bp = getenv("DQNX_BWD_PLAN")) e->bwd_plan = atoi(bp) == 1 ? 1 : 0;
-    if (c.net.kind != DQNX_NET_MLP) e->bwd_plan = 0;   // the fused plan covers MLP bodies only
+    {
+        FusedFwdArgs& fp = e->fplan;
+        memset(&fp, 0, sizeof(fp));
+        fp.L = (int)e->np.dense.size();
+        for (int l = 0; l < fp.L && l < FUSED_MAX_L; l++) {
+            fp.in[l] = e->np.dense[l].in;
+            fp.out[l] = e->np.dense[l].out;
+        }
+        fp.NH = e->np.NH;
+        fp.F = e->np.F;
+        const bool fused_ok = c.net.kind == DQNX_NET_MLP && fused_fwd_plan(fp, c.net.obs_dim);
+        e->bwd_plan = fused_ok ? 2 : 0;
+        if (const char* bp = getenv("DQNX_BWD_PLAN")) {
+            const int want = atoi(bp);
+            if (want == 0 || (want == 1 && c.net.kind == DQNX_NET_MLP) || (want == 2 && fused_ok)) e->bwd_plan = want;
+        }
+    }
     e->Bg = c.batch;
     e->Bl = c.batch / c.world_size;
     e->shard_begin = c.rank * e->Bl;
@@ -1332,8 +1656,10 @@ int dqnx_learn_step(dqnx_engine* e, int32_t flags, void* stream) {
     if (e->cfg.algo == DQNX_ALGO_PER_DOUBLE && (flags & DQNX_STEP_GIVEN_INDICES))
         return set_error(DQNX_EUNSUPPORTED, "PER learn step samples its own minibatch");
     // PER: step t+1's sample depends on step t's priority update, so nothing is drawn ahead
+    // Fused plan: the sampler launch also rebuilds the blocked weight copies, which must see
+    // this step's weights, so it cannot run a step ahead either.
     const bool prefetch = (flags & DQNX_STEP_PREFETCH) && !(flags & DQNX_STEP_GIVEN_INDICES) &&
-                          e->cfg.algo != DQNX_ALGO_PER_DOUBLE;
+                          e->cfg.algo != DQNX_ALGO_PER_DOUBLE && e->bwd_plan != 2;
     if (e->ring_size < e->Bg && !(flags & DQNX_STEP_GIVEN_INDICES) && !e->pf_valid)
         return set_error(DQNX_EINVAL, "Sample larger than population: %lld < %d", (long long)e->ring_size, e->Bg);
     const int base = flags & (DQNX_STEP_SOFT_UPDATE | DQNX_STEP_GIVEN_INDICES | DQNX_STEP_GRADS_ONLY);

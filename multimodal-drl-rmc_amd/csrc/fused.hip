@@ -1,0 +1,575 @@
+// Fused MLP learn-step kernels (gfx950): the whole forward of every stream in ONE launch and
+// the Q head / TD target / Huber / dZ chain in one more.
+//
+//   k_mlp_fwd   one workgroup = 16 rows of one stream (online(s), online(s'), target(s')):
+//               gather the rows from the replay ring into LDS, then every Linear layer and the
+//               Q head in turn, activations kept in LDS between layers.  Writes only what the
+//               backward needs: stream 0's activations and gathered rows, and the raw head
+//               outputs [3][B][16] of every stream.
+//   k_head_bwd  one workgroup = 16 samples (x nsplit column parts): dueling aggregate,
+//               Double-DQN argmax / DQN max, y = r + (1-d)*gamma*q', Huber (mean, or
+//               IS-weighted under PER), dHead, then dZ_L = (dHead W_head) (.) act'(H_L) and
+//               dZ_{l-1} = (dZ_l W_l) (.) act'(H_{l-1}) down to layer 1, all in LDS.
+// The weight gradients (split-K slabs, k_bwd_level) and Adam (k_adam) follow as two more
+// launches: 5 launches per learn step instead of 7.
+//
+// Reference path (R: = /root/reference/):
+//   DoubleAgent.learn R:dqn/agent.py:204-226, SimpleAgent.learn :166-185, PerDoubleAgent.learn
+//   :245-272; DuelingDeepQNetwork.forward R:dqn/network.py:90-96 (aggregate :83);
+//   DeepQNetwork.forward :61-65; MLP body R:env/custom_env/macro with lane/dqn_config.py:76-84.
+//
+// GEMM shape: M = 16 rows per workgroup, so every wave owns 16 output columns (one or two
+// 16x16 tiles) and streams ITS weights straight from L2 into registers; nothing about W is
+// shared between waves, so W never goes through LDS (cdna guide §5: "GEMV / M <= 16 ... load
+// straight to VGPRs").  The weights are read from fragment-blocked copies (relayout.hpp):
+// one coalesced 1 KiB buffer_load_dwordx4 per wave per 16x16x16 block.  The 16-row
+// activation tile is shared by all waves and lives in LDS (row stride = 8 mod 64 floats:
+// conflict-free ds_read_b128 fragments, MI355X_MICROARCH.md §LDS).
+#include "learn.hpp"
+
+namespace dqnx {
+
+constexpr int FW = FUSED_WAVES;
+constexpr int FT = 64 * FW;
+constexpr int FPF = 4;     // 16-deep chunks per group
+constexpr int FNB = 3;     // register sets: FNB-1 groups of W in flight ahead of the MFMAs
+constexpr int FGQ = 6;     // float4 gather slots per thread (input tile <= FGQ * FT float4)
+
+__host__ __device__ __forceinline__ int fused_stride(int K) { return ((K + 63) & ~63) + 8; }
+__host__ __device__ __forceinline__ int fused_groups(int K) { return (K + 16 * FPF - 1) / (16 * FPF); }
+
+// Workgroup barrier for LDS hand-offs only.  __syncthreads() also drains every outstanding
+// global access of the wave (vmcnt(0)) -- here that would wait for the activation stores
+// to HBM and for the weight prefetch in flight across the barrier.
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+// ---- weight streams -------------------------------------------------------------------
+// Buffer loads through a wave-uniform descriptor: they stay VMEM ops counted by vmcnt alone
+// (a generic pointer that lost its address space becomes a flat load, and the compiler then
+// drains vmcnt AND lgkmcnt at every use), and an out-of-range offset reads zeros without
+// touching memory (the prefetch overrun past the last chunk needs no branch).
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+constexpr uint32_t kOOB = 0x80000000u;
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t wave_rsrc(const float* base, uint32_t bytes) {
+    const uint64_t b = (uint64_t)base;
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)b);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(b >> 32));
+    return __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)hi << 32) | lo), 0,
+                                             __builtin_amdgcn_readfirstlane(bytes), 0x00020000);
+}
+__device__ __forceinline__ float4 bld4(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+    const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
+    return make_float4(__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z), __uint_as_float(v.w));
+}
+
+// The output tiles a wave owns: tiles wid and wid + FW of the N/16 column tiles.
+struct WaveCols {
+    int n0[2];
+    int tn;        // 0, 1 or 2 tiles
+};
+__device__ __forceinline__ WaveCols wave_cols(int N) {
+    const int wid = threadIdx.x >> 6, nt = N >> 4;
+    WaveCols c;
+    c.n0[0] = wid * 16;
+    c.n0[1] = (wid + FW) * 16;
+    c.tn = (wid + FW < nt) ? 2 : (wid < nt ? 1 : 0);
+    return c;
+}
+
+// One wave's stream over a fragment-blocked weight copy: chunk ch of column tile t is the
+// 1 KiB at byte (t * nch + ch) * 1024, lane-ordered, so off[t] = (t * nch * 64 + lane) * 16.
+struct WStream {
+    __amdgpu_buffer_rsrc_t rs;
+    uint32_t off[2];
+    int nch;
+};
+
+template <int TN>
+__device__ __forceinline__ void bfetch(const WStream& w, int ch, float4 (&d)[2]) {
+#pragma unroll
+    for (int t = 0; t < TN; t++) d[t] = bld4(w.rs, ch < w.nch ? w.off[t] + 1024u * ch : kOOB);
+}
+
+// Open the stream over the wave's tiles (column tile offset c0t) and issue groups 0..FNB-2.
+__device__ __forceinline__ void stream_open(const float* blk, int ntiles, int nch, int c0t, const WaveCols& c,
+                                            WStream& w, float4 (&wb)[FNB][FPF][2]) {
+    const uint32_t lane = threadIdx.x & 63;
+    w.rs = wave_rsrc(blk, (uint32_t)ntiles * nch * 1024u);
+    w.nch = nch;
+    w.off[0] = ((uint32_t)(c0t + (c.tn >= 1 ? c.n0[0] >> 4 : 0)) * nch * 64u + lane) * 16u;
+    w.off[1] = ((uint32_t)(c0t + (c.tn >= 2 ? c.n0[1] >> 4 : 0)) * nch * 64u + lane) * 16u;
+    if (c.tn == 2) {
+#pragma unroll
+        for (int u = 0; u + 1 < FNB; u++)
+#pragma unroll
+            for (int p = 0; p < FPF; p++) bfetch<2>(w, u * FPF + p, wb[u][p]);
+    } else if (c.tn == 1) {
+#pragma unroll
+        for (int u = 0; u + 1 < FNB; u++)
+#pragma unroll
+            for (int p = 0; p < FPF; p++) bfetch<1>(w, u * FPF + p, wb[u][p]);
+    }
+}
+
+// acc[t] += A[16][16 * ch0 ...] . B_t for one group of FPF chunks (A fragments from LDS).
+// MFMA jj of a chunk consumes k = 16 ch + 4 (lane >> 4) + jj for both operands.
+template <int TN>
+__device__ __forceinline__ void mma_group(const float* ap, int ch0, const float4 (&w)[FPF][2], floatx4 (&acc)[2]) {
+    float4 av[FPF];
+#pragma unroll
+    for (int p = 0; p < FPF; p++) av[p] = *reinterpret_cast<const float4*>(ap + (ch0 + p) * 16);
+#pragma unroll
+    for (int p = 0; p < FPF; p++) {
+#pragma unroll
+        for (int t = 0; t < TN; t++) acc[t] = mfma16x16x4(av[p].x, w[p][t].x, acc[t]);
+#pragma unroll
+        for (int t = 0; t < TN; t++) acc[t] = mfma16x16x4(av[p].y, w[p][t].y, acc[t]);
+#pragma unroll
+        for (int t = 0; t < TN; t++) acc[t] = mfma16x16x4(av[p].z, w[p][t].z, acc[t]);
+#pragma unroll
+        for (int t = 0; t < TN; t++) acc[t] = mfma16x16x4(av[p].w, w[p][t].w, acc[t]);
+    }
+}
+
+// acc = A[16][K] (LDS, stride sa) . B over ngroups groups (K zero padded to ngroups*64 on both
+// sides).  B fragments rotate through FNB register sets by group: group g+FNB-1 is issued
+// before group g is multiplied, so FNB-1 groups of MFMAs cover each L2 round trip.  Every
+// fetch is unconditional (past the last chunk it reads the out-of-range offset), which keeps
+// the compiler's vmcnt counts exact; only the MFMAs of missing groups are skipped.
+template <int TN>
+__device__ __forceinline__ void wave_mma_t(const float* As, int sa, int ngroups, const WStream& w,
+                                           float4 (&wb)[FNB][FPF][2], floatx4 (&acc)[2]) {
+    const int lane = threadIdx.x & 63, i = lane & 15, g = lane >> 4;
+    const float* ap = As + i * sa + 4 * g;
+#pragma unroll
+    for (int t = 0; t < TN; t++) acc[t] = floatx4{0.f, 0.f, 0.f, 0.f};
+    for (int grp = 0; grp < ngroups; grp += FNB) {
+#pragma unroll
+        for (int u = 0; u < FNB; u++) {
+            const int ch = (grp + u) * FPF;
+#pragma unroll
+            for (int p = 0; p < FPF; p++) bfetch<TN>(w, ch + (FNB - 1) * FPF + p, wb[(u + FNB - 1) % FNB][p]);
+            if (grp + u < ngroups) mma_group<TN>(ap, ch, wb[u], acc);
+        }
+    }
+}
+__device__ __forceinline__ void wave_mma(const float* As, int sa, int ngroups, const WaveCols& c, const WStream& w,
+                                         float4 (&wb)[FNB][FPF][2], floatx4 (&acc)[2]) {
+    if (c.tn == 2) wave_mma_t<2>(As, sa, ngroups, w, wb, acc);
+    else if (c.tn == 1) wave_mma_t<1>(As, sa, ngroups, w, wb, acc);
+}
+
+// =====================================================================================
+// Forward: every layer + head raw outputs for one 16-row tile of one stream.
+// LDS: buf0 = input tile [16][sx] (later hidden tiles / head partials), buf1 = hidden tiles.
+// =====================================================================================
+template <int ACT>
+__global__ __launch_bounds__(FT) void k_mlp_fwd(FusedFwdArgs a) {
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    // LDS tile b: pointer arithmetic on `lds` keeps the LDS address space visible to the
+    // compiler (ds_read, not flat loads that share the vmcnt counter with the W stream)
+#define FBUF(b) (lds + ((b) ? a.buf0 : 0))
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int i = lane & 15, g = lane >> 4;
+    const int T = xcd_remap(blockIdx.x, a.tiles * a.nstreams);
+    const int z = T / a.tiles, tile = T - z * a.tiles;
+    const int s = a.stream_of[z];
+    const int tgt = s == 2 ? 1 : 0;
+    const int b0 = tile * 16, nb = min(16, a.Bl - b0);
+    const float* P = tgt ? a.tparams : a.params;
+    const float* ring = (s == 0) ? a.ring_obs : a.ring_next;
+    const bool keep = (s == 0);
+
+    DQNX_STAMP(a.stamps, 24);
+    float4 wb[FNB][FPF][2];
+    WStream ws;
+    WaveCols c = wave_cols(a.out[0]);
+
+    // (0) gather the 16 ring rows -> LDS, zero beyond the batch / row; stream 0 keeps a copy.
+    //     Issue order matters (vmcnt retires in order): ring slots first, then layer 1's
+    //     weight stream (independent of the rows), then the dependent row loads.
+    {
+        const int kz = fused_groups(a.in[0]) * FPF * 16;   // columns the MMA loop reads
+        const int q4 = kz >> 2, rs4 = a.ring_stride >> 2;
+        // branch-free: every slot loads (clamped row / column) and selects zero afterwards,
+        // so the loads issue back to back (one phys round trip, then one ring round trip)
+        int32_t slot[FGQ];
+#pragma unroll
+        for (int j = 0; j < FGQ; j++) {
+            const int r = (tid + j * FT) / q4;
+            slot[j] = a.phys[b0 + (r < nb ? r : nb - 1)];
+        }
+        // stream 0 also gathers the transition scalars for the head kernel (one contiguous
+        // load there instead of a dependent phys -> ring chain)
+        int32_t tslot = 0;
+        if (keep && tid < nb) tslot = a.phys[b0 + tid];
+        stream_open(a.wblk[tgt][0], a.out[0] >> 4, fused_groups(a.in[0]) * FPF, 0, c, ws, wb);
+        if (keep && tid < nb)
+            a.trans[b0 + tid] = make_float4(__int_as_float(a.act[tslot]), a.rew[tslot], a.done[tslot], 0.f);
+        float4 xv[FGQ];
+#pragma unroll
+        for (int j = 0; j < FGQ; j++) {
+            const int q = tid + j * FT;
+            const int r = q / q4, c4 = q - r * q4;
+            const bool ok = r < nb && c4 < rs4;
+            float4 x = ld4(ring + (int64_t)slot[j] * a.ring_stride + 4 * (ok ? c4 : 0));
+            if (!ok) x = make_float4(0.f, 0.f, 0.f, 0.f);
+            xv[j] = x;
+        }
+#pragma unroll
+        for (int j = 0; j < FGQ; j++) {
+            const int q = tid + j * FT;
+            const int r = q / q4, c4 = q - r * q4;
+            if (r < 16) {
+                *reinterpret_cast<float4*>(FBUF(0) + r * a.sx + 4 * c4) = xv[j];
+                if (keep && r < nb && c4 < rs4)
+                    *reinterpret_cast<float4*>(a.xcopy + (int64_t)(b0 + r) * a.ring_stride + 4 * c4) = xv[j];
+            }
+        }
+    }
+    DQNX_STAMP(a.stamps, 25);
+    lds_barrier();
+    DQNX_STAMP(a.stamps, 26);
+
+    int cur = 0;
+    for (int l = 0; l < a.L; l++) {
+        const int K = a.in[l], N = a.out[l];
+        const float* bias_p = P + a.woff[l] + (int64_t)N * K;
+        float bias[2];
+#pragma unroll
+        for (int t = 0; t < 2; t++) bias[t] = (t < c.tn) ? bias_p[c.n0[t] + i] : 0.f;
+        floatx4 acc[2];
+        wave_mma(FBUF(cur), l == 0 ? a.sx : a.sh, fused_groups(K), c, ws, wb, acc);
+        DQNX_STAMP(a.stamps, 27 + 2 * l);
+        const WaveCols cl = c;
+        // next layer's weight stream in flight during the epilogue + barrier
+        if (l + 1 < a.L) {
+            c = wave_cols(a.out[l + 1]);
+            stream_open(a.wblk[tgt][l + 1], a.out[l + 1] >> 4, fused_groups(a.in[l + 1]) * FPF, 0, c, ws, wb);
+        }
+        float* Hs = FBUF(cur ^ 1);
+        float* Hg = keep ? a.H[l] : nullptr;
+#pragma unroll
+        for (int t = 0; t < 2; t++) {
+            if (t >= cl.tn) continue;
+            const int col = cl.n0[t] + i;
+#pragma unroll
+            for (int r = 0; r < 4; r++) {
+                const int rr = 4 * g + r;
+                const float v = act_fwd<ACT>(acc[t][r] + bias[t]);
+                Hs[rr * a.sh + col] = v;
+                if (Hg && rr < nb) Hg[(int64_t)(b0 + rr) * N + col] = v;
+            }
+        }
+        lds_barrier();
+        DQNX_STAMP(a.stamps, 28 + 2 * l);
+        cur ^= 1;
+    }
+
+    // head: raw[o] = H_L . W_head[o] + b_head[o], o < NH; K = F split over the waves
+    {
+        const int F = a.F, nck = F >> 4;
+        const int A = a.head_kind == DQNX_HEAD_DUELING ? a.NH - 1 : a.NH;
+        const float* hw = P + a.head_off + head_w_off(a.head_kind, i < a.NH ? i : 0, F);
+        const float* hs = FBUF(cur) + i * a.sh + 4 * g;
+        floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+        for (int ck = wid; ck < nck; ck += FW) {
+            float4 wv = ld4(hw + ck * 16 + 4 * g);
+            if (i >= a.NH) wv = make_float4(0.f, 0.f, 0.f, 0.f);
+            const float4 av = *reinterpret_cast<const float4*>(hs + ck * 16);
+            acc = mfma16x16x4(av.x, wv.x, acc);
+            acc = mfma16x16x4(av.y, wv.y, acc);
+            acc = mfma16x16x4(av.z, wv.z, acc);
+            acc = mfma16x16x4(av.w, wv.w, acc);
+        }
+        DQNX_STAMP(a.stamps, 36);
+        float* part = FBUF(cur ^ 1);   // [FW][16 rows][16 outputs]
+#pragma unroll
+        for (int r = 0; r < 4; r++) part[wid * 256 + (4 * g + r) * 16 + i] = acc[r];
+        float hb = 0.f;
+        if (tid < 256 && (tid & 15) < a.NH) hb = P[a.head_off + head_b_off(a.head_kind, tid & 15, F, A)];
+        lds_barrier();
+        if (tid < 256) {
+            const int b = tid >> 4, o = tid & 15;
+            float v = part[b * 16 + o];
+#pragma unroll
+            for (int w = 1; w < FW; w++) v += part[w * 256 + b * 16 + o];
+            v = (o < a.NH) ? v + hb : 0.f;
+            if (b < nb) a.raw[((int64_t)s * a.Bl + b0 + b) * 16 + o] = v;
+        }
+    }
+    DQNX_STAMP(a.stamps, 37);
+#undef FBUF
+}
+
+// =====================================================================================
+// Head / TD / Huber / dZ chain for 16 samples.
+// dZ_{l-1} = (dZ_l W_l) (.) act'(H_{l-1}): B[k][n] = W_l[k][n], read from the chain-blocked
+// copy of W_l (relayout.hpp, kind 1).
+// =====================================================================================
+constexpr int HB_SD = 264;   // LDS row stride of dZ tiles (width <= 256)
+
+template <int ACT>
+__global__ __launch_bounds__(FT) void k_head_bwd(HeadBwdArgs a) {
+    __shared__ __attribute__((aligned(16))) float dzs[2][16 * HB_SD];
+    __shared__ float raw[3][16][17];
+    __shared__ float qv[3][16][17];
+    __shared__ float dh[16][17];
+    __shared__ float gsh[16], lossv[16], rsh[16], dsh[16], wsh[16];
+    __shared__ int ash[16];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int i = lane & 15, g = lane >> 4;
+    // nsplit workgroups per 16-sample tile: each recomputes the (cheap) head part and takes
+    // 1/nsplit of the columns of the LAST dZ of the chain (dZ_1, the widest)
+    const int tile = blockIdx.x / a.nsplit, part = blockIdx.x - tile * a.nsplit;
+    const bool lead = part == 0;
+    const int b0 = tile * 16, nb = min(16, a.Bl - b0);
+    const int A = a.A, NH = a.NH, F = a.F, L = a.L;
+    const bool use1 = a.algo != DQNX_ALGO_DQN;
+    const float* Wh = a.params + a.head_off;
+    DQNX_STAMP(a.stamps, 40);
+
+    // chain level l: dZ_{l-1}[16][cols] = dZ_l[16][K] . W_l[K][cols], cols = this part's range
+    float4 wb[FNB][FPF][2];
+    float hm[2][4];
+    WStream ws;
+    WaveCols cw;
+    int coff = 0, ldn = 0;
+    auto setup = [&](int l) {
+        const int K = a.out[l], N = a.in[l];
+        const int nparts = (l == 1) ? a.nsplit : 1;
+        const int np_ = N / nparts;
+        coff = (l == 1) ? part * np_ : 0;
+        ldn = N;
+        cw = wave_cols(np_);
+        stream_open(a.wblkT[l], N >> 4, K >> 4, coff >> 4, cw, ws, wb);
+#pragma unroll
+        for (int t = 0; t < 2; t++)
+#pragma unroll
+            for (int r = 0; r < 4; r++)
+                hm[t][r] = (t < cw.tn && 4 * g + r < nb) ? a.H[l - 1][(int64_t)(b0 + 4 * g + r) * N + coff + cw.n0[t] + i] : 0.f;
+    };
+    // (0) every independent load first: raw head outputs, transition scalars, the head
+    //     weights this wave needs for dZ_L, H_L for the mask
+    for (int q = tid; q < 3 * 256; q += FT) {
+        const int s = q >> 8, b = (q >> 4) & 15, o = q & 15;
+        float v = 0.f;
+        if (b < nb && (s != 1 || use1)) v = a.raw[((int64_t)s * a.Bl + b0 + b) * 16 + o];
+        raw[s][b][o] = v;
+    }
+    if (tid < 16) {
+        const int b = tid;
+        int act = 0;
+        float rew = 0.f, done = 0.f, w = 1.f;
+        if (b < nb) {
+            const float4 tr = a.trans[b0 + b];
+            act = __float_as_int(tr.x);
+            rew = tr.y;
+            done = tr.z;
+            if (a.isw) w = a.isw[b0 + b];
+            if (act < 0 || act >= A) act = 0;
+        }
+        ash[b] = act;
+        rsh[b] = rew;
+        dsh[b] = done;
+        wsh[b] = w;
+    }
+    const WaveCols cF = wave_cols(F);
+    float whv[2][4], hmask[2][4];
+#pragma unroll
+    for (int t = 0; t < 2; t++)
+#pragma unroll
+        for (int jj = 0; jj < 4; jj++) {
+            const int o = 4 * g + jj;
+            whv[t][jj] = (t < cF.tn && o < NH) ? Wh[head_w_off(a.head_kind, o, F) + cF.n0[t] + i] : 0.f;
+            hmask[t][jj] = (t < cF.tn && 4 * g + jj < nb) ? a.H[L - 1][(int64_t)(b0 + 4 * g + jj) * F + cF.n0[t] + i] : 0.f;
+        }
+    // the first chain level's weight stream: issued after the loads phase 1 waits for
+    // (vmcnt retires in order), long before the chain needs it
+    if (L >= 2) setup(L - 1);
+    lds_barrier();
+    DQNX_STAMP(a.stamps, 41);
+
+    // (1) Q values (dueling aggregate, R:dqn/network.py:83,90-96)
+    if (tid < 256) {
+        const int b = tid >> 4, j = tid & 15;
+        for (int s = 0; s < 3; s++) {
+            if (s == 1 && !use1) continue;
+            float q = 0.f;
+            if (a.head_kind == DQNX_HEAD_DUELING) {
+                float sum = 0.f;
+                for (int jj = 0; jj < A; jj++) sum += raw[s][b][1 + jj];
+                const float mean = sum / (float)A;
+                if (j < A) q = raw[s][b][0] + (raw[s][b][1 + j] - mean);
+            } else if (j < A) {
+                q = raw[s][b][j];
+            }
+            qv[s][b][j] = q;
+            if (lead && j < A && b < nb) a.Q[((int64_t)s * a.Bl + b0 + b) * A + j] = q;
+        }
+    }
+    lds_barrier();
+    DQNX_STAMP(a.stamps, 42);
+
+    // (2) TD target, Huber value and gradient per sample (R:dqn/agent.py:172-181, 209-221, 259-267)
+    if (tid < 16) {
+        const int b = tid;
+        float gq = 0.f, lb = 0.f;
+        if (b < nb) {
+            float qn;
+            if (!use1) {
+                qn = qv[2][b][0];
+                for (int j = 1; j < A; j++) qn = qv[2][b][j] > qn ? qv[2][b][j] : qn;
+            } else {
+                int best = 0;
+                float bq = qv[1][b][0];
+                for (int j = 1; j < A; j++)
+                    if (qv[1][b][j] > bq) { bq = qv[1][b][j]; best = j; }
+                qn = qv[2][b][best];
+            }
+            const float t1 = 1.f - dsh[b];
+            const float t2 = t1 * a.gamma;
+            const float t3 = t2 * qn;
+            const float y = rsh[b] + t3;
+            const float qa = qv[0][b][ash[b]];
+            const float x = qa - y;
+            const float zabs = fabsf(x);
+            const float l = zabs < 1.f ? (0.5f * zabs) * zabs / 1.f : zabs - 0.5f;
+            if (a.isw) {
+                const float go = a.inv_bg * wsh[b];
+                gq = x <= -1.f ? -go : (x >= 1.f ? go : (x * go) / 1.f);
+                lb = wsh[b] * l;
+            } else {
+                gq = x <= -1.f ? -a.inv_bg : (x >= 1.f ? a.inv_bg : (a.inv_bg * x) / 1.f);
+                lb = l;
+            }
+            if (lead) {
+                const int gb = b0 + b;
+                a.td[gb] = y;
+                a.td[a.Bl + gb] = qa;
+                a.td[2 * a.Bl + gb] = zabs;
+                if (a.abs_td_out) a.abs_td_out[gb] = zabs;
+            }
+        }
+        gsh[b] = gq;
+        lossv[b] = lb;
+    }
+    lds_barrier();
+    DQNX_STAMP(a.stamps, 43);
+
+    // (3) d(head outputs)
+    if (tid < 256) {
+        const int b = tid >> 4, o = tid & 15;
+        const float gq = gsh[b];
+        const int act = ash[b];
+        float d = 0.f;
+        if (o < NH) {
+            if (a.head_kind == DQNX_HEAD_DUELING)
+                d = (o == 0) ? gq : ((o - 1 == act ? gq : 0.f) + (-gq) / (float)A);
+            else
+                d = (o == act) ? gq : 0.f;
+        }
+        dh[b][o] = d;
+        if (lead && b < nb) a.dhead[(int64_t)(b0 + b) * 16 + o] = d;
+    }
+    if (lead && tid == 256) {
+        float sacc = 0.f;
+        for (int b = 0; b < 16; b++) sacc += lossv[b];
+        a.loss_partial[tile] = sacc;
+    }
+    if (blockIdx.x == 0 && tid == 320 && a.ctrl) a.ctrl->adam_step = a.ctrl->adam_step + 1;
+    lds_barrier();
+    DQNX_STAMP(a.stamps, 44);
+
+    // (4) dZ_L = (dHead W_head) (.) act'(H_L): K = 16 head rows, one MFMA group per tile
+    int cur = 0;
+    {
+        float* dz = dzs[cur];
+        float* dzg = a.dZ[L - 1];
+#pragma unroll
+        for (int t = 0; t < 2; t++) {
+            if (t >= cF.tn) continue;
+            floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int jj = 0; jj < 4; jj++) acc = mfma16x16x4(dh[i][4 * g + jj], whv[t][jj], acc);
+            const int col = cF.n0[t] + i;
+#pragma unroll
+            for (int r = 0; r < 4; r++) {
+                const int rr = 4 * g + r;
+                const float v = act_bwd<ACT>(acc[r], hmask[t][r]);
+                dz[rr * HB_SD + col] = v;
+                if (lead && rr < nb) dzg[(int64_t)(b0 + rr) * F + col] = v;
+            }
+        }
+    }
+
+    DQNX_STAMP(a.stamps, 45);
+    // (5) dZ chain down to layer 1
+    for (int l = L - 1; l >= 1; l--) {
+        if (l < L - 1) setup(l);
+        floatx4 acc[2];
+        lds_barrier();   // dZ_l tile complete in LDS
+        DQNX_STAMP(a.stamps, 46 + 3 * (L - 1 - l));
+        wave_mma(dzs[cur], HB_SD, fused_groups(a.out[l]), cw, ws, wb, acc);
+        DQNX_STAMP(a.stamps, 47 + 3 * (L - 1 - l));
+        float* dz = dzs[cur ^ 1];
+        float* dzg = a.dZ[l - 1];
+        const bool store = lead || l == 1;
+#pragma unroll
+        for (int t = 0; t < 2; t++) {
+            if (t >= cw.tn) continue;
+            const int col = cw.n0[t] + i;
+#pragma unroll
+            for (int r = 0; r < 4; r++) {
+                const int rr = 4 * g + r;
+                const float v = act_bwd<ACT>(acc[t][r], hm[t][r]);
+                dz[rr * HB_SD + col] = v;
+                if (store && rr < nb) dzg[(int64_t)(b0 + rr) * ldn + coff + col] = v;
+            }
+        }
+        cur ^= 1;
+    }
+    DQNX_STAMP(a.stamps, 55);
+}
+
+// ---- host side ------------------------------------------------------------------------
+bool fused_fwd_plan(FusedFwdArgs& a, int obs_dim) {
+    if (a.L < 1 || a.L > FUSED_MAX_L || a.NH > 16) return false;
+    for (int l = 0; l < a.L; l++)
+        if (a.out[l] % 64 || a.out[l] > 256) return false;
+    if (a.F != a.out[a.L - 1]) return false;
+    const int kz = fused_groups(obs_dim) * FPF * 16;
+    if (16 * (kz / 4) > FGQ * FT) return false;   // gather slots
+    a.sx = fused_stride(kz);
+    int wmax = 0;
+    for (int l = 0; l < a.L; l++) wmax = a.out[l] > wmax ? a.out[l] : wmax;
+    a.sh = fused_stride(wmax);
+    int b0 = 16 * a.sx, b1 = 16 * a.sh;
+    if (b0 < 16 * a.sh) b0 = 16 * a.sh;
+    if (b0 < FW * 256) b0 = FW * 256;
+    if (b1 < FW * 256) b1 = FW * 256;
+    a.buf0 = (b0 + 3) & ~3;
+    a.buf1 = (b1 + 3) & ~3;
+    for (int l = 0; l < a.L; l++) a.kpad[l] = fused_groups(a.in[l]) * FPF * 16;
+    return (a.buf0 + a.buf1) * 4 <= 64 * 1024;
+}
+
+int launch_fused_fwd(const FusedFwdArgs& a, int act, hipStream_t s) {
+    const dim3 grid(a.tiles * a.nstreams), block(FT);
+    const size_t shm = (size_t)(a.buf0 + a.buf1) * 4;
+    if (act == DQNX_ACT_RELU) hipLaunchKernelGGL((k_mlp_fwd<DQNX_ACT_RELU>), grid, block, shm, s, a);
+    else hipLaunchKernelGGL((k_mlp_fwd<DQNX_ACT_ELU>), grid, block, shm, s, a);
+    DQNX_HIP_CHECK(hipGetLastError());
+    return DQNX_OK;
+}
+
+int launch_head_bwd(const HeadBwdArgs& a, int act, hipStream_t s) {
+    const dim3 grid(((a.Bl + 15) / 16) * a.nsplit), block(FT);
+    if (act == DQNX_ACT_RELU) hipLaunchKernelGGL((k_head_bwd<DQNX_ACT_RELU>), grid, block, 0, s, a);
+    else hipLaunchKernelGGL((k_head_bwd<DQNX_ACT_ELU>), grid, block, 0, s, a);
+    DQNX_HIP_CHECK(hipGetLastError());
+    return DQNX_OK;
+}
+
+}  // namespace dqnx

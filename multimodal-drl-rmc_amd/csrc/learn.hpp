@@ -1,8 +1,19 @@
 // Kernel argument structs and launchers shared by learn.hip / conv.hip / engine.cpp.
 #pragma once
 #include "common.hpp"
+#include "relayout.hpp"
 
 namespace dqnx {
+
+// Flat offsets inside the Q-head parameter block (torch named_parameters order):
+//   dueling: [fc_val.w (F) | fc_val.b | fc_adv.w (A*F) | fc_adv.b (A)], o = 0 val, 1..A adv
+//   linear:  [fc_out.w (A*F) | fc_out.b (A)]
+__host__ __device__ __forceinline__ int head_w_off(int kind, int o, int F) {
+    return kind == DQNX_HEAD_DUELING ? (o == 0 ? 0 : F + 1 + (o - 1) * F) : o * F;
+}
+__host__ __device__ __forceinline__ int head_b_off(int kind, int o, int F, int A) {
+    return kind == DQNX_HEAD_DUELING ? (o == 0 ? F : F + 1 + A * F + (o - 1)) : A * F + o;
+}
 
 struct FwdProblem {
     const float* A;        // dense rows, or the replay ring (layer 1, phys != null)
@@ -44,7 +55,7 @@ struct BwdArgs {
     float* dZprev;         // [Bl][in]
     int in, out;
     // dw roles
-    DwProblem dw[2];
+    DwProblem dw[4];       // dW of up to 3 dense layers + the head in one launch (fused plan)
     int ndw;
     int Bl, kslice, dw_slices;
     int dx_blocks, dx_grid_x;
@@ -172,6 +183,8 @@ struct SampleArgs {
     const int64_t* wptr_dev;
     int64_t capacity;
     int64_t* stamps;          // diagnostic builds (-DDQNX_STAMPS)
+    RelayoutArgs rl;          // fused plan: blocked weight copies, built by blocks 1.. of the launch
+    int rl_blocks;
 };
 
 // PER sampling: ReplayMemoryPrioritized.sample_transitions (R:dqn/replay_memory.py:69-92)
@@ -188,6 +201,8 @@ struct PerSampleArgs {
     float* isw;               // [Bg] importance weights (float32, like T.as_tensor(..., float32))
     double beta_start, beta_end, beta_steps;
     int32_t n_env;
+    RelayoutArgs rl;          // fused plan: blocked weight copies, built by blocks 1.. of the launch
+    int rl_blocks;
 };
 
 // PER priority writes with SumTree.update's sequential semantics (R:dqn/utils/sum_tree.py:15-32):
@@ -239,6 +254,92 @@ struct Col2imArgs {
     float* dZprev;            // [Bl*Hi*Wi][Ci]
     int Bl, Ci, Hi, Wi, Ho, Wo, kh, kw, sh, sw, ph, pw;
 };
+// ---- fused MLP plan (fused.hip): one forward launch for every layer + the Q head, one
+//      head / TD / dZ-chain launch per 16-sample tile ----
+constexpr int FUSED_MAX_L = 3;
+constexpr int FUSED_WAVES = 8;          // waves per workgroup of both fused kernels
+struct FusedFwdArgs {
+    int L, Bl, tiles, nstreams;
+    int in[FUSED_MAX_L], out[FUSED_MAX_L];
+    int64_t woff[FUSED_MAX_L];   // flat offset of W_l ([out][in]); the bias follows
+    int64_t head_off;
+    int head_kind, NH, F;
+    int stream_of[3];            // logical stream of grid slice z: 0 online(s), 1 online(s'), 2 target(s')
+    const float* params;
+    const float* tparams;
+    const float* ring_obs;
+    const float* ring_next;
+    int ring_stride;             // floats per ring row (obs_dim rounded up to 4)
+    const int32_t* phys;         // [Bl] physical ring slots
+    float* xcopy;                // [Bl][ring_stride] stream-0 gathered rows (layer-1 dW operand)
+    float* H[FUSED_MAX_L];       // stream-0 activations [Bl][out_l]
+    float* raw;                  // [3][Bl][16] head outputs per logical stream
+    float4* trans;               // [Bl] stream 0: {act (int bits), rew, done, 0} of each sampled slot
+    const int32_t* act;          // replay ring columns (gathered for `trans`)
+    const float* rew;
+    const float* done;
+    int sx, sh;                  // LDS row strides (floats) of the input tile / hidden tiles
+    int buf0, buf1;              // LDS buffer sizes (floats)
+    int kpad[FUSED_MAX_L];       // layer inputs zero padded to a multiple of 64 (blocked copies)
+    const float* wblk[2][FUSED_MAX_L];   // fragment-blocked W_l of the online / target net (relayout.hpp)
+    int64_t* stamps;             // diagnostic builds (-DDQNX_STAMPS): slots 24..39
+};
+struct HeadBwdArgs {
+    int L, Bl, A, NH, F, head_kind, algo;
+    int nsplit;                  // workgroups per 16-sample tile (split the last dZ's columns)
+    int in[FUSED_MAX_L], out[FUSED_MAX_L];
+    int64_t woff[FUSED_MAX_L], head_off;
+    float inv_bg, gamma;
+    const float* params;
+    const float* raw;            // [3][Bl][16]
+    const float4* trans;         // [Bl] {act, rew, done, 0} gathered by the forward (stream 0)
+    const int32_t* phys;
+    const int32_t* act;
+    const float* rew;
+    const float* done;
+    const float* isw;
+    float* abs_td_out;
+    float* Q;                    // [3][Bl][A]
+    float* td;                   // [3][Bl]
+    const float* H[FUSED_MAX_L]; // stream-0 activations
+    float* dZ[FUSED_MAX_L];      // [Bl][out_l]
+    float* dhead;                // [Bl][16]
+    float* loss_partial;         // [tiles]
+    dqnx_ctrl* ctrl;
+    const float* wblkT[FUSED_MAX_L];     // chain-blocked online W_l, l >= 1 (relayout.hpp)
+    int64_t* stamps;             // diagnostic builds (-DDQNX_STAMPS): slots 40..55
+};
+// Every weight gradient (split-K over the minibatch) + gradient reduction + Adam (+ soft
+// update) in ONE launch: the last-arriving K slice of each parameter tile sums the tile's
+// slabs in fixed slice order and applies the optimizer to it (k_dw_seam, learn.hip).
+struct DwSeamArgs {
+    BwdArgs b;                 // dW problems (dx role unused), Bl, kslice, dw_slices
+    int64_t poff[4];           // flat parameter offset of each problem's layer / head
+    int tile0[4];              // first ticket of each problem
+    int* tickets;              // one arrival counter per parameter tile, zero between launches
+    int mode;                  // 0: grads only (DP all-reduce follows), 1: grads + Adam
+    int soft;
+    int64_t n_params;
+    float* p;
+    float* m;
+    float* v;
+    float* grads;              // [n_params + 1] (last = loss)
+    float* target;
+    dqnx_ctrl* ctrl;
+    float w1, beta2, c2, eps, tau, one_minus_tau;
+    const float* loss_partial;
+    int n_loss_partial;
+    int batch_global;
+    const float* adam_table;
+    int adam_table_len;
+    double beta1d, beta2d, lrd;
+};
+int dw_seam_tiles(BwdArgs& b);   // fills the grids; returns the number of parameter tiles
+int launch_dw_seam(const DwSeamArgs& a, hipStream_t s);
+bool fused_fwd_plan(FusedFwdArgs& a, int obs_dim);   // fills sx/sh/buf sizes; false if unsupported
+int launch_fused_fwd(const FusedFwdArgs& a, int act, hipStream_t s);
+int launch_head_bwd(const HeadBwdArgs& a, int act, hipStream_t s);
+
 int launch_im2col(const Im2colArgs& a, hipStream_t s);
 int launch_flatten_concat(const FlattenArgs& a, hipStream_t s);
 int launch_unflatten(const UnflattenArgs& a, hipStream_t s);
@@ -259,7 +360,8 @@ int launch_soft_update(float* target, const float* p, int64_t n, float tau, floa
 int launch_replay_push(const PushArgs& a, hipStream_t s);
 
 int launch_sample_uniform(const SampleArgs& a, hipStream_t s);
-int launch_idx_to_phys(const int32_t* idx, int32_t* phys, int shard_begin, int n, dqnx_ctrl* ctrl, int64_t capacity, hipStream_t s);
+int launch_idx_to_phys(const int32_t* idx, int32_t* phys, int shard_begin, int n, dqnx_ctrl* ctrl, int64_t capacity,
+                       const RelayoutArgs* rl, int rl_blocks, hipStream_t s);
 int64_t sample_setsize(int64_t k);
 int sample_hash_slots(int32_t k);
 

@@ -33,6 +33,10 @@ __global__ __launch_bounds__(PER_NT) void k_per_sample(PerSampleArgs a) {
     __shared__ uint32_t words[2 * PER_MAX_B];
     __shared__ double top[PER_TOP];
     __shared__ uint32_t mt[624], tmp[624];
+    if (blockIdx.x > 0) {   // spare workgroups: blocked weight copies for the fused plan
+        relayout_run(a.rl, blockIdx.x - 1, gridDim.x - 1);
+        return;
+    }
     const int tid = threadIdx.x;
     const int64_t len = 2 * a.cap - 1;
     const double total = a.tree[0];                        // SumTree.total_priority
@@ -438,7 +442,7 @@ __global__ __launch_bounds__(PER_NT) void k_per_update(PerUpdateArgs a) {
 
 int launch_per_sample(const PerSampleArgs& a, hipStream_t s) {
     if (a.Bg < 1 || a.Bg > PER_MAX_B) return set_error(DQNX_EUNSUPPORTED, "PER batch %d outside [1, %d]", a.Bg, PER_MAX_B);
-    hipLaunchKernelGGL(k_per_sample, dim3(1), dim3(PER_NT), 0, s, a);
+    hipLaunchKernelGGL(k_per_sample, dim3(1 + a.rl_blocks), dim3(PER_NT), 0, s, a);
     DQNX_HIP_CHECK(hipGetLastError());
     return DQNX_OK;
 }

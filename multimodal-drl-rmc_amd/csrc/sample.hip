@@ -53,6 +53,10 @@ __global__ __launch_bounds__(SAMPLE_NT) void k_sample_uniform(SampleArgs a) {
     __shared__ int wave_cnt[NW];
     __shared__ int s_newpos;
 
+    if (blockIdx.x > 0) {   // spare workgroups: blocked weight copies for the fused plan
+        relayout_run(a.rl, blockIdx.x - 1, gridDim.x - 1);
+        return;
+    }
     const int tid = threadIdx.x;
     const int lane = tid & 63, wid = tid >> 6;
     DQNX_STAMP(a.stamps, 0);
@@ -178,7 +182,11 @@ __global__ __launch_bounds__(SAMPLE_NT) void k_sample_uniform(SampleArgs a) {
 
 // Logical positions (given by the caller) -> physical ring slots of the local shard.
 __global__ void k_idx_to_phys(const int32_t* idx, int32_t* phys, int shard_begin, int n, const dqnx_ctrl* ctrl,
-                              int64_t capacity) {
+                              int64_t capacity, RelayoutArgs rl, int pblocks) {
+    if ((int)blockIdx.x >= pblocks) {
+        relayout_run(rl, blockIdx.x - pblocks, gridDim.x - pblocks);
+        return;
+    }
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const int64_t size = ctrl->ring_size, wptr = ctrl->ring_wptr;
@@ -187,9 +195,13 @@ __global__ void k_idx_to_phys(const int32_t* idx, int32_t* phys, int shard_begin
 }
 
 int launch_idx_to_phys(const int32_t* idx, int32_t* phys, int shard_begin, int n, dqnx_ctrl* ctrl, int64_t capacity,
-                       hipStream_t s) {
-    hipLaunchKernelGGL(k_idx_to_phys, dim3((n + 255) / 256), dim3(256), 0, s, idx, phys, shard_begin, n, ctrl,
-                       capacity);
+                       const RelayoutArgs* rl, int rl_blocks, hipStream_t s) {
+    RelayoutArgs r = {};
+    if (rl && rl_blocks > 0) r = *rl;
+    else rl_blocks = 0;
+    const int pb = (n + 255) / 256;
+    hipLaunchKernelGGL(k_idx_to_phys, dim3(pb + 4 * rl_blocks), dim3(256), 0, s, idx, phys, shard_begin, n, ctrl,
+                       capacity, r, pb);
     DQNX_HIP_CHECK(hipGetLastError());
     return DQNX_OK;
 }
@@ -217,10 +229,10 @@ int launch_sample_uniform(const SampleArgs& a, hipStream_t s) {
     const int hs = sample_hash_slots(a.k);
     if (hs < 0) return set_error(DQNX_EUNSUPPORTED, "sample: k=%d too large for the LDS table", a.k);
     switch (hs) {
-        case 2048: hipLaunchKernelGGL(k_sample_uniform<2048>, dim3(1), dim3(SAMPLE_NT), 0, s, a); break;
-        case 4096: hipLaunchKernelGGL(k_sample_uniform<4096>, dim3(1), dim3(SAMPLE_NT), 0, s, a); break;
-        case 8192: hipLaunchKernelGGL(k_sample_uniform<8192>, dim3(1), dim3(SAMPLE_NT), 0, s, a); break;
-        default: hipLaunchKernelGGL(k_sample_uniform<16384>, dim3(1), dim3(SAMPLE_NT), 0, s, a); break;
+        case 2048: hipLaunchKernelGGL(k_sample_uniform<2048>, dim3(1 + a.rl_blocks), dim3(SAMPLE_NT), 0, s, a); break;
+        case 4096: hipLaunchKernelGGL(k_sample_uniform<4096>, dim3(1 + a.rl_blocks), dim3(SAMPLE_NT), 0, s, a); break;
+        case 8192: hipLaunchKernelGGL(k_sample_uniform<8192>, dim3(1 + a.rl_blocks), dim3(SAMPLE_NT), 0, s, a); break;
+        default: hipLaunchKernelGGL(k_sample_uniform<16384>, dim3(1 + a.rl_blocks), dim3(SAMPLE_NT), 0, s, a); break;
     }
     DQNX_HIP_CHECK(hipGetLastError());
     return DQNX_OK;

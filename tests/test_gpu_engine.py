@@ -134,6 +134,33 @@ def test_gpu_learn_fused_backward_plan_matches_oracle(monkeypatch, algo, obs_dim
     _check_learn(*make_pair(algo, obs_dim, batch, capacity, n_fill, seed))
 
 
+@pytest.mark.parametrize("algo,obs_dim,batch,capacity,n_fill,seed", [
+    ("DQNAgent", 14, 32, 500, 300, 23),
+    ("DoubleDQNAgent", 284, 256, 3000, 3000, 24),
+    ("DuelingDoubleDQNAgent", 284, 1000, 20000, 20000, 25),   # ragged last tile
+])
+def test_gpu_learn_per_layer_plan_matches_oracle(monkeypatch, algo, obs_dim, batch, capacity, n_fill, seed):
+    """Plan 0 (per-layer forward launches + split-K backward levels), the plan two-stream nets use."""
+    monkeypatch.setenv("DQNX_BWD_PLAN", "0")
+    _check_learn(*make_pair(algo, obs_dim, batch, capacity, n_fill, seed))
+
+
+@pytest.mark.parametrize("split", ["1", "2"])
+def test_gpu_fused_head_split_identical(monkeypatch, split):
+    """The fused plan's head/dZ-chain kernel with the last dZ split over 1 or 2 workgroups per
+    tile gives bitwise the same step (each column is computed the same way either way)."""
+    monkeypatch.setenv("DQNX_HEAD_SPLIT", split)
+    o, e = make_pair("DuelingDoubleDQNAgent", 284, 512, 4000, 4000, 31)
+    monkeypatch.setenv("DQNX_HEAD_SPLIT", "2" if split == "1" else "1")
+    o2, e2 = make_pair("DuelingDoubleDQNAgent", 284, 512, 4000, 4000, 31)
+    for _ in range(3):
+        e.learn_step(soft_update=True)
+        e2.learn_step(soft_update=True)
+    torch.cuda.synchronize()
+    assert torch.equal(e.params, e2.params)
+    assert torch.equal(e.target_params, e2.target_params)
+
+
 def _check_learn(oracle, eng):
     for step in range(3):
         rec = oracle.train_step()
@@ -194,8 +221,11 @@ def test_gpu_learn_golden(golden):
         np.testing.assert_allclose(tg[k].cpu().numpy().reshape(-1), z[f"target_{i}"], atol=1e-5, rtol=0)
 
 
-def test_gpu_prefetch_mode_bit_identical():
-    """DQNX_STEP_PREFETCH draws step t+1's minibatch during step t: same results, bitwise."""
+def test_gpu_prefetch_mode_bit_identical(monkeypatch):
+    """DQNX_STEP_PREFETCH draws step t+1's minibatch during step t: same results, bitwise.
+    (Per-layer plan: the fused plan rebuilds its blocked weights in the sampler launch and
+    never samples ahead.)"""
+    monkeypatch.setenv("DQNX_BWD_PLAN", "0")
     o1, e1 = make_pair("DuelingDoubleDQNAgent", 284, 256, 3000, 3000, 21)
     o2, e2 = make_pair("DuelingDoubleDQNAgent", 284, 256, 3000, 3000, 21)
     for _ in range(5):
@@ -211,8 +241,9 @@ def test_gpu_prefetch_mode_bit_identical():
     e2.push(*O.synth_transitions(4, 284, 8, seed=3))
 
 
-def test_gpu_push_refused_with_pending_prefetch():
+def test_gpu_push_refused_with_pending_prefetch(monkeypatch):
     from dqn import _capi as C
+    monkeypatch.setenv("DQNX_BWD_PLAN", "0")
     o, e = make_pair("DuelingDoubleDQNAgent", 14, 32, 500, 300, 22)
     e.learn_step(prefetch=True)
     with pytest.raises(C.DqnxError):
