@@ -376,6 +376,16 @@ int enqueue_per_update(dqnx_engine* e, const int32_t* idx, hipStream_t s) {
     return enqueue_per_update_pairs(e, idx, at<float>(e, e->off[DQNX_BUF_PER_ABS_TD]), e->Bg, s);
 }
 
+AdamBias adam_bias_args(dqnx_engine* e) {
+    AdamBias b;
+    b.table = at<float>(e, e->ws_adam_tab);
+    b.len = kAdamTable;
+    b.lrd = e->cfg.lr;
+    b.beta1d = e->cfg.beta1;
+    b.beta2d = e->cfg.beta2;
+    return b;
+}
+
 // Optimizer fields shared by AdamArgs and DwSeamArgs (torch Adam defaults of the config).
 template <class T>
 void fill_adam_fields(dqnx_engine* e, int flags, T& aa) {
@@ -607,6 +617,7 @@ void build_fused_steps(dqnx_engine* e, int flags, int32_t* idx, int32_t* phys, s
         ha.loss_partial = at<float>(e, e->ws_loss_part);
         ha.ctrl = ctrl;
         for (int l = 1; l < L; l++) ha.wblkT[l] = at<float>(e, e->ws_wblkT[l]);
+        ha.ab = adam_bias_args(e);
         ha.stamps = at<int64_t>(e, e->ws_stamps);
         KStep k;
         k.name = "head_bwd";
@@ -673,7 +684,7 @@ void build_fused_steps(dqnx_engine* e, int flags, int32_t* idx, int32_t* phys, s
             bytes += 4.0 * (16.0 * Bl + Bl * np.F + ba.dw_slices * (double)np.head_params);
         }
         const char* sv = getenv("DQNX_DW_SEAM");
-        if (sv && atoi(sv) == 0) {   // two launches: split-K slabs, then the Adam pass
+        if (!(sv && atoi(sv) == 1)) {   // default: split-K slabs, then the Adam pass
             bwd_level_grid(ba);
             KStep k;
             k.name = "dw_all";
@@ -684,7 +695,9 @@ void build_fused_steps(dqnx_engine* e, int flags, int32_t* idx, int32_t* phys, s
             ks.push_back(adam_kstep(e, flags));
             return;
         }
-        // 5. one launch: slabs + last-arriver reduction + Adam (+ soft update)
+        // 5. opt-in (DQNX_DW_SEAM=1): one launch, slabs + last-arriver reduction + Adam.  Measured
+        //    slower (25 us vs 9.6 + 7.4 at MLP-284 B=1024): the agent-scope release / acquire
+        //    write back and invalidate the XCD's L2 once per workgroup.
         DwSeamArgs da;
         memset(&da, 0, sizeof(da));
         da.b = ba;
@@ -942,6 +955,7 @@ std::vector<KStep> build_learn_steps(dqnx_engine* e, int key) {
         ha.beta1 = (float)c.beta1;
         ha.beta2 = (float)c.beta2;
         ha.lr = (float)c.lr;
+        ha.ab = adam_bias_args(e);
         ha.stamps = at<int64_t>(e, e->ws_stamps);
         KStep k;
         k.name = "head_td_loss";

@@ -478,7 +478,7 @@ __global__ __launch_bounds__(FT) void k_head_bwd(HeadBwdArgs a) {
         for (int b = 0; b < 16; b++) sacc += lossv[b];
         a.loss_partial[tile] = sacc;
     }
-    if (blockIdx.x == 0 && tid == 320 && a.ctrl) a.ctrl->adam_step = a.ctrl->adam_step + 1;
+    if (blockIdx.x == 0 && tid == 320 && a.ctrl) adam_advance(a.ctrl, a.ab);
     lds_barrier();
     DQNX_STAMP(a.stamps, 44);
 

@@ -460,7 +460,7 @@ __global__ __launch_bounds__(256) void k_head(HeadArgs a) {
         }
     }
     // Adam step counter of this learn step (read by the Adam pass, a later launch)
-    if (blockIdx.x == 0 && tid == 128 && a.ctrl) a.ctrl->adam_step = a.ctrl->adam_step + 1;
+    if (blockIdx.x == 0 && tid == 128 && a.ctrl) adam_advance(a.ctrl, a.ab);
     DQNX_STAMP(a.stamps, 20);
 }
 
@@ -477,15 +477,9 @@ __global__ __launch_bounds__(256) void k_adam(AdamArgs a) {
     const int64_t P = a.n_params;
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     float step_size = 0.f, bc2s = 1.f;
-    if (a.mode != 0) {
-        const int64_t t = a.ctrl->adam_step;
-        if (t >= 1 && t <= a.adam_table_len) {
-            step_size = a.adam_table[2 * (t - 1)];
-            bc2s = a.adam_table[2 * (t - 1) + 1];
-        } else {   // beyond the precomputed range: device libm (may differ in the last bit)
-            step_size = (float)(-(a.lrd / (1.0 - pow(a.beta1d, (double)t))));
-            bc2s = (float)pow(1.0 - pow(a.beta2d, (double)t), 0.5);
-        }
+    if (a.mode != 0) {   // this step's scalars, stored by the head kernel (adam_advance)
+        step_size = a.ctrl->adam_step_size;
+        bc2s = a.ctrl->adam_bc2_sqrt;
     }
     for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < P; e += stride) {
         // every load of this element is issued before the first use (one round trip)
@@ -527,12 +521,16 @@ __global__ __launch_bounds__(256) void k_adam(AdamArgs a) {
         a.p[e] = p;
         if (a.soft) a.target[e] = a.tau * p + a.one_minus_tau * tg;
     }
-    if (a.mode != 2 && blockIdx.x == 0 && threadIdx.x == 0 && a.loss_partial) {
+    if (a.mode != 2 && blockIdx.x == 0 && threadIdx.x < 64 && a.loss_partial) {   // one wave, fixed order
         float s = 0.f;
-        for (int j = 0; j < a.n_loss_partial; j++) s += a.loss_partial[j];
-        const float loss = s / (float)a.batch_global;
-        a.grads[P] = loss;     // all-reduced with the gradient under DP
-        a.ctrl->loss = loss;
+        for (int j = threadIdx.x; j < a.n_loss_partial; j += 64) s += a.loss_partial[j];
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) s += __shfl_xor(s, o);
+        if (threadIdx.x == 0) {
+            const float loss = s / (float)a.batch_global;
+            a.grads[P] = loss;     // all-reduced with the gradient under DP
+            a.ctrl->loss = loss;
+        }
     }
     if (a.mode == 2 && blockIdx.x == 0 && threadIdx.x == 0) a.ctrl->loss = a.grads[P];
 }
@@ -636,15 +634,11 @@ __global__ __launch_bounds__(256) void k_dw_seam(DwSeamArgs a) {
     Operand B{d.X, d.ldx, nullptr, d.in, ba.Bl, d.in, nullptr, 0};
     floatx4 acc[TM][TN];
     EW::G::run(lds, A, B, m0, n0, kb, ke, acc);
-    // Slabs are published write-through at agent scope (sc1 buffer stores) and read back the
-    // same way, so no L2 write-back / invalidate fence is needed around the ticket (a release
-    // fence would write back the XCD's whole dirty L2 once per workgroup).
-    const uint64_t pb = (uint64_t)d.partial;
-    const __amdgpu_buffer_rsrc_t prs = __builtin_amdgcn_make_buffer_rsrc(
-        (void*)(((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(pb >> 32)) << 32) |
-                __builtin_amdgcn_readfirstlane((uint32_t)pb)),
-        0, __builtin_amdgcn_readfirstlane((uint32_t)((int64_t)ba.dw_slices * d.pstride * 4)), 0x00020000);
-    const uint32_t sb = (uint32_t)((int64_t)bz * d.pstride * 4);
+    // publish the slab (agent-scope release), take a ticket; the last slice acquires and
+    // reduces.  (A write-through sc1 variant without the fences faulted under hipGraph
+    // replay and was removed; this form is correct but slower than dW + k_adam, so the plan
+    // uses it only with DQNX_DW_SEAM=1.)
+    float* part = d.partial + (int64_t)bz * d.pstride;
     if (EW::owner()) {
 #pragma unroll
         for (int tn = 0; tn < TN; tn++) {
@@ -655,19 +649,22 @@ __global__ __launch_bounds__(256) void k_dw_seam(DwSeamArgs a) {
 #pragma unroll
                 for (int r = 0; r < 4; r++) {
                     const int row = m0 + EW::ro() + tmi * 16 + 4 * g + r;
-                    if (row < d.out)
-                        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(acc[tmi][tn][r]), prs,
-                                                              sb + 4u * (uint32_t)dw_local_index(d, row, col), 0, 16);
+                    if (row < d.out) part[dw_local_index(d, row, col)] = acc[tmi][tn][r];
                 }
         }
     }
-    // take a ticket once every wave's slab stores have completed; the last slice reduces
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (tid == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         const int t = __hip_atomic_fetch_add(&a.tickets[tile], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         const int last = (t == ba.dw_slices - 1);
-        if (last) a.tickets[tile] = 0;   // ready for the next launch
+        if (last) {
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            a.tickets[tile] = 0;   // ready for the next launch
+        }
         s_last = last;
     }
     __syncthreads();
@@ -688,18 +685,15 @@ __global__ __launch_bounds__(256) void k_dw_seam(DwSeamArgs a) {
     float gs[TE];
 #pragma unroll
     for (int u = 0; u < TE; u++) {   // every slab load issued before the first add
-        const uint32_t eb = 4u * (uint32_t)(eo[u] >= 0 ? eo[u] : 0);
+        const int64_t eb = eo[u] >= 0 ? eo[u] : 0;
         float pv[8];
 #pragma unroll
-        for (int s2 = 0; s2 < 8; s2++)
-            pv[s2] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
-                prs, s2 < S ? (uint32_t)((int64_t)s2 * d.pstride * 4) + eb : 0x80000000u, 0, 16));
+        for (int s2 = 0; s2 < 8; s2++) pv[s2] = (s2 < S) ? d.partial[(int64_t)s2 * d.pstride + eb] : 0.f;
         float gsum = pv[0];
 #pragma unroll
         for (int s2 = 1; s2 < 8; s2++)
             if (s2 < S) gsum += pv[s2];
-        for (int s2 = 8; s2 < S; s2++)
-            gsum += __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(prs, (uint32_t)((int64_t)s2 * d.pstride * 4) + eb, 0, 16));
+        for (int s2 = 8; s2 < S; s2++) gsum += d.partial[(int64_t)s2 * d.pstride + eb];
         gs[u] = gsum;
     }
 #pragma unroll

@@ -15,6 +15,34 @@ __host__ __device__ __forceinline__ int head_b_off(int kind, int o, int F, int A
     return kind == DQNX_HEAD_DUELING ? (o == 0 ? F : F + 1 + A * F + (o - 1)) : A * F + o;
 }
 
+// torch single-tensor Adam's per-step scalars for step t (R:env/dqn_config.py:176):
+// step_size = -(lr / (1 - beta1**t)), bias_correction2**0.5, from the host-libm table for
+// t <= len (the same pow the CPU reference calls), device libm beyond.  The head kernel of a
+// step advances t and stores both in dqnx_ctrl, so the optimizer pass reads them in the
+// same round trip as its operands.
+struct AdamBias {
+    const float* table;
+    int len;
+    double lrd, beta1d, beta2d;
+};
+__device__ __forceinline__ void adam_bias(int64_t t, const AdamBias& b, float& step_size, float& bc2s) {
+    if (t >= 1 && t <= b.len) {
+        step_size = b.table[2 * (t - 1)];
+        bc2s = b.table[2 * (t - 1) + 1];
+    } else {
+        step_size = (float)(-(b.lrd / (1.0 - pow(b.beta1d, (double)t))));
+        bc2s = (float)pow(1.0 - pow(b.beta2d, (double)t), 0.5);
+    }
+}
+__device__ __forceinline__ void adam_advance(dqnx_ctrl* ctrl, const AdamBias& b) {
+    const int64_t t = ctrl->adam_step + 1;
+    float ss, bc;
+    adam_bias(t, b, ss, bc);
+    ctrl->adam_step = t;
+    ctrl->adam_step_size = ss;
+    ctrl->adam_bc2_sqrt = bc;
+}
+
 struct FwdProblem {
     const float* A;        // dense rows, or the replay ring (layer 1, phys != null)
     int lda;
@@ -86,6 +114,7 @@ struct HeadArgs {
     float* loss_partial;   // [tiles]
     dqnx_ctrl* ctrl;       // Adam step bookkeeping (block 0) or null
     float beta1, beta2, lr;
+    AdamBias ab;
     int64_t* stamps;       // diagnostic builds (-DDQNX_STAMPS)
 };
 
@@ -307,6 +336,7 @@ struct HeadBwdArgs {
     float* loss_partial;         // [tiles]
     dqnx_ctrl* ctrl;
     const float* wblkT[FUSED_MAX_L];     // chain-blocked online W_l, l >= 1 (relayout.hpp)
+    AdamBias ab;
     int64_t* stamps;             // diagnostic builds (-DDQNX_STAMPS): slots 40..55
 };
 // Every weight gradient (split-K over the minibatch) + gradient reduction + Adam (+ soft

@@ -45,5 +45,7 @@ for step in range(6):
         if h[j]:
             hw.append((40 + j, h[j] - prev))
             prev = h[j]
+    samp = [s[0], s[1]] + [x for x in s[2:15] if x] + [s[15]]
+    print(f"step {step}: sampler total {samp[-1] - samp[0]} cyc: {[samp[j + 1] - samp[j] for j in range(len(samp) - 1)]}")
     print(f"step {step}: fwd total {prev and (max(x for x in f if x) - f[0])} cyc: {fw}")
     print(f"         head_bwd total {max(x for x in h if x) - h[0]} cyc: {hw}")
