@@ -31,8 +31,17 @@ namespace dqnx {
 
 constexpr int FW = FUSED_WAVES;
 constexpr int FT = 64 * FW;
-constexpr int FPF = 4;     // 16-deep chunks per group
-constexpr int FNB = 3;     // register sets: FNB-1 groups of W in flight ahead of the MFMAs
+#ifndef DQNX_FPF
+#define DQNX_FPF 4
+#endif
+#ifndef DQNX_FNB
+#define DQNX_FNB 2   // measured: 3 and 4 sets are 0.9 / 2 us slower per forward at MLP-284 B=1024
+#endif
+#ifndef DQNX_FUSED_ORDER
+#define DQNX_FUSED_ORDER 0   // gather issue order: 0 slots, W, rows; 1 W, slots, rows; 2 slots, rows, W
+#endif
+constexpr int FPF = DQNX_FPF;   // 16-deep chunks per group
+constexpr int FNB = DQNX_FNB;   // register sets: FNB-1 groups of W in flight ahead of the MFMAs
 constexpr int FGQ = 6;     // float4 gather slots per thread (input tile <= FGQ * FT float4)
 
 __host__ __device__ __forceinline__ int fused_stride(int K) { return ((K + 63) & ~63) + 8; }
@@ -150,6 +159,9 @@ __device__ __forceinline__ void wave_mma_t(const float* As, int sa, int ngroups,
             const int ch = (grp + u) * FPF;
 #pragma unroll
             for (int p = 0; p < FPF; p++) bfetch<TN>(w, ch + (FNB - 1) * FPF + p, wb[(u + FNB - 1) % FNB][p]);
+            // pin the refill ahead of this group's MFMAs: left alone, the scheduler sinks the
+            // loads below them and the prefetch distance collapses to ~0
+            __builtin_amdgcn_sched_barrier(0);
             if (grp + u < ngroups) mma_group<TN>(ap, ch, wb[u], acc);
         }
     }
@@ -164,7 +176,10 @@ __device__ __forceinline__ void wave_mma(const float* As, int sa, int ngroups, c
 // Forward: every layer + head raw outputs for one 16-row tile of one stream.
 // LDS: buf0 = input tile [16][sx] (later hidden tiles / head partials), buf1 = hidden tiles.
 // =====================================================================================
-template <int ACT>
+// NL (dense layers) is a template parameter so every per-layer kernel-argument access has a
+// constant index: a runtime-indexed kernarg array element becomes a dependent global load
+// with its own wait (eight of them serialised the head kernel's prologue).
+template <int ACT, int NL>
 __global__ __launch_bounds__(FT) void k_mlp_fwd(FusedFwdArgs a) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     // LDS tile b: pointer arithmetic on `lds` keeps the LDS address space visible to the
@@ -194,6 +209,7 @@ __global__ __launch_bounds__(FT) void k_mlp_fwd(FusedFwdArgs a) {
         const int q4 = kz >> 2, rs4 = a.ring_stride >> 2;
         // branch-free: every slot loads (clamped row / column) and selects zero afterwards,
         // so the loads issue back to back (one phys round trip, then one ring round trip)
+        if (DQNX_FUSED_ORDER == 1) stream_open(a.wblk[tgt][0], a.out[0] >> 4, fused_groups(a.in[0]) * FPF, 0, c, ws, wb);
         int32_t slot[FGQ];
 #pragma unroll
         for (int j = 0; j < FGQ; j++) {
@@ -204,9 +220,7 @@ __global__ __launch_bounds__(FT) void k_mlp_fwd(FusedFwdArgs a) {
         // load there instead of a dependent phys -> ring chain)
         int32_t tslot = 0;
         if (keep && tid < nb) tslot = a.phys[b0 + tid];
-        stream_open(a.wblk[tgt][0], a.out[0] >> 4, fused_groups(a.in[0]) * FPF, 0, c, ws, wb);
-        if (keep && tid < nb)
-            a.trans[b0 + tid] = make_float4(__int_as_float(a.act[tslot]), a.rew[tslot], a.done[tslot], 0.f);
+        if (DQNX_FUSED_ORDER == 0) stream_open(a.wblk[tgt][0], a.out[0] >> 4, fused_groups(a.in[0]) * FPF, 0, c, ws, wb);
         float4 xv[FGQ];
 #pragma unroll
         for (int j = 0; j < FGQ; j++) {
@@ -217,6 +231,10 @@ __global__ __launch_bounds__(FT) void k_mlp_fwd(FusedFwdArgs a) {
             if (!ok) x = make_float4(0.f, 0.f, 0.f, 0.f);
             xv[j] = x;
         }
+        if (DQNX_FUSED_ORDER == 2) stream_open(a.wblk[tgt][0], a.out[0] >> 4, fused_groups(a.in[0]) * FPF, 0, c, ws, wb);
+        // after the row loads are in flight: the transition scalars' own round trip overlaps them
+        if (keep && tid < nb)
+            a.trans[b0 + tid] = make_float4(__int_as_float(a.act[tslot]), a.rew[tslot], a.done[tslot], 0.f);
 #pragma unroll
         for (int j = 0; j < FGQ; j++) {
             const int q = tid + j * FT;
@@ -233,18 +251,19 @@ __global__ __launch_bounds__(FT) void k_mlp_fwd(FusedFwdArgs a) {
     DQNX_STAMP(a.stamps, 26);
 
     int cur = 0;
-    for (int l = 0; l < a.L; l++) {
+#pragma unroll
+    for (int l = 0; l < NL; l++) {
         const int K = a.in[l], N = a.out[l];
         const float* bias_p = P + a.woff[l] + (int64_t)N * K;
         float bias[2];
 #pragma unroll
-        for (int t = 0; t < 2; t++) bias[t] = (t < c.tn) ? bias_p[c.n0[t] + i] : 0.f;
+        for (int t = 0; t < 2; t++) bias[t] = bias_p[(t < c.tn ? c.n0[t] : 0) + i];   // branch-free
         floatx4 acc[2];
         wave_mma(FBUF(cur), l == 0 ? a.sx : a.sh, fused_groups(K), c, ws, wb, acc);
         DQNX_STAMP(a.stamps, 27 + 2 * l);
         const WaveCols cl = c;
         // next layer's weight stream in flight during the epilogue + barrier
-        if (l + 1 < a.L) {
+        if (l + 1 < NL) {
             c = wave_cols(a.out[l + 1]);
             stream_open(a.wblk[tgt][l + 1], a.out[l + 1] >> 4, fused_groups(a.in[l + 1]) * FPF, 0, c, ws, wb);
         }
@@ -310,14 +329,11 @@ __global__ __launch_bounds__(FT) void k_mlp_fwd(FusedFwdArgs a) {
 // =====================================================================================
 constexpr int HB_SD = 264;   // LDS row stride of dZ tiles (width <= 256)
 
-template <int ACT>
+template <int ACT, int NL>
 __global__ __launch_bounds__(FT) void k_head_bwd(HeadBwdArgs a) {
     __shared__ __attribute__((aligned(16))) float dzs[2][16 * HB_SD];
-    __shared__ float raw[3][16][17];
-    __shared__ float qv[3][16][17];
     __shared__ float dh[16][17];
-    __shared__ float gsh[16], lossv[16], rsh[16], dsh[16], wsh[16];
-    __shared__ int ash[16];
+    __shared__ float lossv[16];
     const int tid = threadIdx.x, lane = tid & 63;
     const int i = lane & 15, g = lane >> 4;
     // nsplit workgroups per 16-sample tile: each recomputes the (cheap) head part and takes
@@ -325,7 +341,8 @@ __global__ __launch_bounds__(FT) void k_head_bwd(HeadBwdArgs a) {
     const int tile = blockIdx.x / a.nsplit, part = blockIdx.x - tile * a.nsplit;
     const bool lead = part == 0;
     const int b0 = tile * 16, nb = min(16, a.Bl - b0);
-    const int A = a.A, NH = a.NH, F = a.F, L = a.L;
+    const int A = a.A, NH = a.NH, F = a.F;
+    constexpr int L = NL;
     const bool use1 = a.algo != DQNX_ALGO_DQN;
     const float* Wh = a.params + a.head_off;
     DQNX_STAMP(a.stamps, 40);
@@ -348,32 +365,24 @@ __global__ __launch_bounds__(FT) void k_head_bwd(HeadBwdArgs a) {
         for (int t = 0; t < 2; t++)
 #pragma unroll
             for (int r = 0; r < 4; r++)
-                hm[t][r] = (t < cw.tn && 4 * g + r < nb) ? a.H[l - 1][(int64_t)(b0 + 4 * g + r) * N + coff + cw.n0[t] + i] : 0.f;
+                hm[t][r] = a.H[l - 1][(int64_t)(b0 + (4 * g + r < nb ? 4 * g + r : nb - 1)) * N + coff +
+                                      (t < cw.tn ? cw.n0[t] : 0) + i];
     };
-    // (0) every independent load first: raw head outputs, transition scalars, the head
-    //     weights this wave needs for dZ_L, H_L for the mask
-    for (int q = tid; q < 3 * 256; q += FT) {
-        const int s = q >> 8, b = (q >> 4) & 15, o = q & 15;
-        float v = 0.f;
-        if (b < nb && (s != 1 || use1)) v = a.raw[((int64_t)s * a.Bl + b0 + b) * 16 + o];
-        raw[s][b][o] = v;
-    }
-    if (tid < 16) {
-        const int b = tid;
-        int act = 0;
-        float rew = 0.f, done = 0.f, w = 1.f;
-        if (b < nb) {
-            const float4 tr = a.trans[b0 + b];
-            act = __float_as_int(tr.x);
-            rew = tr.y;
-            done = tr.z;
-            if (a.isw) w = a.isw[b0 + b];
-            if (act < 0 || act >= A) act = 0;
-        }
-        ash[b] = act;
-        rsh[b] = rew;
-        dsh[b] = done;
-        wsh[b] = w;
+    // (0) every independent load first.  Head part: lane (b, j) = (tid >> 4, tid & 15) of
+    //     waves 0-3 owns head slot j of sample b and reads its raw outputs straight into
+    //     registers (coalesced rows); all waves: the head weights for dZ_L and H_L for its mask;
+    //     then the first chain level's weight stream.  Branch-free clamped loads throughout.
+    const int hb = tid >> 4, hj = tid & 15;
+    const int hbc = hb < nb ? hb : nb - 1;
+    float r0 = 0.f, r1 = 0.f, r2 = 0.f, wis = 1.f;
+    float4 tr = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (tid < 256) {
+        const int64_t base = (int64_t)(b0 + hbc) * 16 + hj;
+        r0 = a.raw[base];
+        r1 = a.raw[(int64_t)a.Bl * 16 + base];   // online(s') (Double) / unused (DQN)
+        r2 = a.raw[(int64_t)2 * a.Bl * 16 + base];
+        tr = a.trans[b0 + hbc];
+        if (a.isw) wis = a.isw[b0 + hbc];
     }
     const WaveCols cF = wave_cols(F);
     float whv[2][4], hmask[2][4];
@@ -382,105 +391,103 @@ __global__ __launch_bounds__(FT) void k_head_bwd(HeadBwdArgs a) {
 #pragma unroll
         for (int jj = 0; jj < 4; jj++) {
             const int o = 4 * g + jj;
-            whv[t][jj] = (t < cF.tn && o < NH) ? Wh[head_w_off(a.head_kind, o, F) + cF.n0[t] + i] : 0.f;
-            hmask[t][jj] = (t < cF.tn && 4 * g + jj < nb) ? a.H[L - 1][(int64_t)(b0 + 4 * g + jj) * F + cF.n0[t] + i] : 0.f;
+            // rows o >= NH meet dh == 0, samples >= nb are never stored, tiles >= tn unused
+            const int col = (t < cF.tn ? cF.n0[t] : 0) + i;
+            whv[t][jj] = Wh[head_w_off(a.head_kind, o < NH ? o : 0, F) + col];
+            hmask[t][jj] = a.H[L - 1][(int64_t)(b0 + (4 * g + jj < nb ? 4 * g + jj : nb - 1)) * F + col];
         }
-    // the first chain level's weight stream: issued after the loads phase 1 waits for
-    // (vmcnt retires in order), long before the chain needs it
     if (L >= 2) setup(L - 1);
-    lds_barrier();
     DQNX_STAMP(a.stamps, 41);
 
-    // (1) Q values (dueling aggregate, R:dqn/network.py:83,90-96)
+    // (1) head part in registers, 16 lanes per sample, shuffles within the lane group:
+    //     Q = V + (A - mean A) (R:dqn/network.py:83,90-96), Double-DQN argmax of online(s') /
+    //     DQN max of target(s'), y = r + (1-d)*gamma*q' (R:dqn/agent.py:172-181, 209-216),
+    //     SmoothL1 value / gradient (mean, or IS-weighted 'none' under PER, :259-267), dHead.
     if (tid < 256) {
-        const int b = tid >> 4, j = tid & 15;
-        for (int s = 0; s < 3; s++) {
-            if (s == 1 && !use1) continue;
-            float q = 0.f;
-            if (a.head_kind == DQNX_HEAD_DUELING) {
-                float sum = 0.f;
-                for (int jj = 0; jj < A; jj++) sum += raw[s][b][1 + jj];
-                const float mean = sum / (float)A;
-                if (j < A) q = raw[s][b][0] + (raw[s][b][1 + j] - mean);
-            } else if (j < A) {
-                q = raw[s][b][j];
+        const bool duel = a.head_kind == DQNX_HEAD_DUELING;
+        auto qval = [&](float r) {   // Q of this lane's action slot j (valid for j < A)
+            if (!duel) return r;
+            const float v = __shfl(r, 0, 16);
+            const float adv = __shfl(r, hj + 1 < 16 ? hj + 1 : 15, 16);
+            float sum = (hj >= 1 && hj <= A) ? r : 0.f;
+#pragma unroll
+            for (int m = 8; m >= 1; m >>= 1) sum += __shfl_xor(sum, m, 16);
+            const float mean = sum / (float)A;
+            return v + (adv - mean);
+        };
+        const float q0 = qval(r0), q1 = qval(r1), q2 = qval(r2);
+        float qn;
+        if (!use1) {   // target(s').max(1)
+            float mx = hj < A ? q2 : -INFINITY;
+#pragma unroll
+            for (int m = 8; m >= 1; m >>= 1) mx = fmaxf(mx, __shfl_xor(mx, m, 16));
+            qn = mx;
+        } else {       // argmax online(s') (first maximum), gather target(s')
+            float bv = hj < A ? q1 : -INFINITY;
+            int bi = hj;
+#pragma unroll
+            for (int m = 8; m >= 1; m >>= 1) {
+                const float ov = __shfl_xor(bv, m, 16);
+                const int oi = __shfl_xor(bi, m, 16);
+                if (ov > bv || (ov == bv && oi < bi)) { bv = ov; bi = oi; }
             }
-            qv[s][b][j] = q;
-            if (lead && j < A && b < nb) a.Q[((int64_t)s * a.Bl + b0 + b) * A + j] = q;
+            qn = __shfl(q2, bi, 16);
         }
-    }
-    lds_barrier();
-    DQNX_STAMP(a.stamps, 42);
-
-    // (2) TD target, Huber value and gradient per sample (R:dqn/agent.py:172-181, 209-221, 259-267)
-    if (tid < 16) {
-        const int b = tid;
-        float gq = 0.f, lb = 0.f;
-        if (b < nb) {
-            float qn;
-            if (!use1) {
-                qn = qv[2][b][0];
-                for (int j = 1; j < A; j++) qn = qv[2][b][j] > qn ? qv[2][b][j] : qn;
-            } else {
-                int best = 0;
-                float bq = qv[1][b][0];
-                for (int j = 1; j < A; j++)
-                    if (qv[1][b][j] > bq) { bq = qv[1][b][j]; best = j; }
-                qn = qv[2][b][best];
+        int act = __float_as_int(tr.x);
+        if (act < 0 || act >= A) act = 0;
+        const float rew = tr.y, done = tr.z;
+        const float t1 = 1.f - done;
+        const float t2 = t1 * a.gamma;
+        const float t3 = t2 * qn;
+        const float y = rew + t3;
+        const float qa = __shfl(q0, act, 16);
+        const float x = qa - y;                        // smooth_l1: input - target
+        const float zabs = fabsf(x);
+        const float l = zabs < 1.f ? (0.5f * zabs) * zabs / 1.f : zabs - 0.5f;
+        float gq, lb;
+        if (a.isw) {
+            const float go = a.inv_bg * wis;
+            gq = x <= -1.f ? -go : (x >= 1.f ? go : (x * go) / 1.f);
+            lb = wis * l;
+        } else {
+            gq = x <= -1.f ? -a.inv_bg : (x >= 1.f ? a.inv_bg : (a.inv_bg * x) / 1.f);
+            lb = l;
+        }
+        const float gmean = (-gq) / (float)A;
+        float d = 0.f;
+        if (hj < NH) {
+            if (duel) d = (hj == 0) ? gq : ((hj - 1 == act ? gq : 0.f) + gmean);
+            else d = (hj == act) ? gq : 0.f;
+        }
+        const bool real = hb < nb;
+        if (!real) { d = 0.f; lb = 0.f; }
+        dh[hb][hj] = d;
+        if (hj == 0) lossv[hb] = lb;
+        if (lead && real) {
+            const int64_t qrow = (int64_t)(b0 + hb) * A + hj;
+            if (hj < A) {
+                a.Q[qrow] = q0;
+                if (use1) a.Q[(int64_t)a.Bl * A + qrow] = q1;
+                a.Q[(int64_t)2 * a.Bl * A + qrow] = q2;
             }
-            const float t1 = 1.f - dsh[b];
-            const float t2 = t1 * a.gamma;
-            const float t3 = t2 * qn;
-            const float y = rsh[b] + t3;
-            const float qa = qv[0][b][ash[b]];
-            const float x = qa - y;
-            const float zabs = fabsf(x);
-            const float l = zabs < 1.f ? (0.5f * zabs) * zabs / 1.f : zabs - 0.5f;
-            if (a.isw) {
-                const float go = a.inv_bg * wsh[b];
-                gq = x <= -1.f ? -go : (x >= 1.f ? go : (x * go) / 1.f);
-                lb = wsh[b] * l;
-            } else {
-                gq = x <= -1.f ? -a.inv_bg : (x >= 1.f ? a.inv_bg : (a.inv_bg * x) / 1.f);
-                lb = l;
-            }
-            if (lead) {
-                const int gb = b0 + b;
+            a.dhead[(int64_t)(b0 + hb) * 16 + hj] = d;
+            if (hj == 0) {
+                const int gb = b0 + hb;
                 a.td[gb] = y;
                 a.td[a.Bl + gb] = qa;
                 a.td[2 * a.Bl + gb] = zabs;
                 if (a.abs_td_out) a.abs_td_out[gb] = zabs;
             }
         }
-        gsh[b] = gq;
-        lossv[b] = lb;
-    }
-    lds_barrier();
-    DQNX_STAMP(a.stamps, 43);
-
-    // (3) d(head outputs)
-    if (tid < 256) {
-        const int b = tid >> 4, o = tid & 15;
-        const float gq = gsh[b];
-        const int act = ash[b];
-        float d = 0.f;
-        if (o < NH) {
-            if (a.head_kind == DQNX_HEAD_DUELING)
-                d = (o == 0) ? gq : ((o - 1 == act ? gq : 0.f) + (-gq) / (float)A);
-            else
-                d = (o == act) ? gq : 0.f;
-        }
-        dh[b][o] = d;
-        if (lead && b < nb) a.dhead[(int64_t)(b0 + b) * 16 + o] = d;
-    }
-    if (lead && tid == 256) {
-        float sacc = 0.f;
-        for (int b = 0; b < 16; b++) sacc += lossv[b];
-        a.loss_partial[tile] = sacc;
     }
     if (blockIdx.x == 0 && tid == 320 && a.ctrl) adam_advance(a.ctrl, a.ab);
     lds_barrier();
     DQNX_STAMP(a.stamps, 44);
+    if (lead && tid == 256) {   // loss partial of the tile, sample order
+        float sacc = 0.f;
+        for (int b = 0; b < 16; b++) sacc += lossv[b];
+        a.loss_partial[tile] = sacc;
+    }
 
     // (4) dZ_L = (dHead W_head) (.) act'(H_L): K = 16 head rows, one MFMA group per tile
     int cur = 0;
@@ -506,6 +513,7 @@ __global__ __launch_bounds__(FT) void k_head_bwd(HeadBwdArgs a) {
 
     DQNX_STAMP(a.stamps, 45);
     // (5) dZ chain down to layer 1
+#pragma unroll
     for (int l = L - 1; l >= 1; l--) {
         if (l < L - 1) setup(l);
         floatx4 acc[2];
@@ -555,19 +563,58 @@ bool fused_fwd_plan(FusedFwdArgs& a, int obs_dim) {
     return (a.buf0 + a.buf1) * 4 <= 64 * 1024;
 }
 
+// Occupancy: a workgroup streams every weight of its stream at the MFMA rate of ONE CU, so two
+// workgroups sharing a CU (the dispatcher packs up to 4 of these onto one CU while others sit
+// idle: 192 workgroups at B = 1024 on 256 CUs) double that CU's time and set the kernel's tail.
+// DQNX_FUSED_LDS_MIN pads the LDS request so only one fits per CU.
+#ifndef DQNX_FUSED_LDS_MIN
+#define DQNX_FUSED_LDS_MIN 0
+#endif
+#ifndef DQNX_HEAD_LDS_PAD
+#define DQNX_HEAD_LDS_PAD 0
+#endif
+template <class K>
+static void allow_lds(K kern, size_t bytes) {
+    if (bytes > 64 * 1024) (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+}
+
 int launch_fused_fwd(const FusedFwdArgs& a, int act, hipStream_t s) {
     const dim3 grid(a.tiles * a.nstreams), block(FT);
-    const size_t shm = (size_t)(a.buf0 + a.buf1) * 4;
-    if (act == DQNX_ACT_RELU) hipLaunchKernelGGL((k_mlp_fwd<DQNX_ACT_RELU>), grid, block, shm, s, a);
-    else hipLaunchKernelGGL((k_mlp_fwd<DQNX_ACT_ELU>), grid, block, shm, s, a);
+    size_t shm = (size_t)(a.buf0 + a.buf1) * 4;
+    if (shm < (size_t)DQNX_FUSED_LDS_MIN) shm = DQNX_FUSED_LDS_MIN;
+#define FUSED_FWD_CASE(ACTV, NLV)                                                                    \
+    do {                                                                                             \
+        if (shm > 64 * 1024) allow_lds(k_mlp_fwd<ACTV, NLV>, 160 * 1024);                            \
+        hipLaunchKernelGGL((k_mlp_fwd<ACTV, NLV>), grid, block, shm, s, a);                          \
+    } while (0)
+    const bool relu = act == DQNX_ACT_RELU;
+    switch (a.L) {
+        case 1: if (relu) FUSED_FWD_CASE(DQNX_ACT_RELU, 1); else FUSED_FWD_CASE(DQNX_ACT_ELU, 1); break;
+        case 2: if (relu) FUSED_FWD_CASE(DQNX_ACT_RELU, 2); else FUSED_FWD_CASE(DQNX_ACT_ELU, 2); break;
+        case 3: if (relu) FUSED_FWD_CASE(DQNX_ACT_RELU, 3); else FUSED_FWD_CASE(DQNX_ACT_ELU, 3); break;
+        default: return set_error(DQNX_EUNSUPPORTED, "fused forward: %d dense layers", a.L);
+    }
+#undef FUSED_FWD_CASE
     DQNX_HIP_CHECK(hipGetLastError());
     return DQNX_OK;
 }
 
 int launch_head_bwd(const HeadBwdArgs& a, int act, hipStream_t s) {
     const dim3 grid(((a.Bl + 15) / 16) * a.nsplit), block(FT);
-    if (act == DQNX_ACT_RELU) hipLaunchKernelGGL((k_head_bwd<DQNX_ACT_RELU>), grid, block, 0, s, a);
-    else hipLaunchKernelGGL((k_head_bwd<DQNX_ACT_ELU>), grid, block, 0, s, a);
+    const size_t pad = DQNX_HEAD_LDS_PAD;   // dynamic LDS on top of the static tiles (occupancy knob)
+#define HEAD_BWD_CASE(ACTV, NLV)                                                                     \
+    do {                                                                                             \
+        if (pad > 64 * 1024) allow_lds(k_head_bwd<ACTV, NLV>, 120 * 1024);                           \
+        hipLaunchKernelGGL((k_head_bwd<ACTV, NLV>), grid, block, pad, s, a);                         \
+    } while (0)
+    const bool relu = act == DQNX_ACT_RELU;
+    switch (a.L) {
+        case 1: if (relu) HEAD_BWD_CASE(DQNX_ACT_RELU, 1); else HEAD_BWD_CASE(DQNX_ACT_ELU, 1); break;
+        case 2: if (relu) HEAD_BWD_CASE(DQNX_ACT_RELU, 2); else HEAD_BWD_CASE(DQNX_ACT_ELU, 2); break;
+        case 3: if (relu) HEAD_BWD_CASE(DQNX_ACT_RELU, 3); else HEAD_BWD_CASE(DQNX_ACT_ELU, 3); break;
+        default: return set_error(DQNX_EUNSUPPORTED, "fused head: %d dense layers", a.L);
+    }
+#undef HEAD_BWD_CASE
     DQNX_HIP_CHECK(hipGetLastError());
     return DQNX_OK;
 }

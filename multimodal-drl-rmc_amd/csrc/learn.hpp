@@ -286,7 +286,10 @@ struct Col2imArgs {
 // ---- fused MLP plan (fused.hip): one forward launch for every layer + the Q head, one
 //      head / TD / dZ-chain launch per 16-sample tile ----
 constexpr int FUSED_MAX_L = 3;
-constexpr int FUSED_WAVES = 8;          // waves per workgroup of both fused kernels
+#ifndef DQNX_FUSED_WAVES
+#define DQNX_FUSED_WAVES 8
+#endif
+constexpr int FUSED_WAVES = DQNX_FUSED_WAVES;   // waves per workgroup of both fused kernels
 struct FusedFwdArgs {
     int L, Bl, tiles, nstreams;
     int in[FUSED_MAX_L], out[FUSED_MAX_L];
