@@ -1408,8 +1408,10 @@ int dqnx_engine_create(const dqnx_config* cfg, dqnx_engine** out) {
     const int L = (int)e->np.dense.size();
     e->slices.assign(L, 1);
     e->kslice.assign(L, e->Bl);
+    int dw_rows = 256;   // minibatch rows per split-K slice of the weight gradients
+    if (const char* v = getenv("DQNX_DW_ROWS")) dw_rows = std::max(16, atoi(v));
     for (int l = 0; l < L; l++) {
-        int S = e->Bl / 256;
+        int S = e->Bl / dw_rows;
         if (S < 1) S = 1;
         if (S > 32) S = 32;
         int ks = (int)align_up((uint64_t)((e->Bl + S - 1) / S), 16);

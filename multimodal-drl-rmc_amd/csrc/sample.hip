@@ -8,12 +8,14 @@
 // Set branch (n > setsize): draws are r = w >> (32 - bit_length(n)), rejected if r >= n,
 // redrawn while already selected.  The accepted sequence is therefore the sequence of
 // FIRST OCCURRENCES of valid candidates in the MT word stream.  One workgroup walks the
-// stream one MT block (<= 624 words) at a time: the 624-word twist runs in 3 parallel
-// phases in LDS, every lane tempers one word, inserts (value, stream position) into an
-// LDS open-addressing table with a 64-bit atomicMin (keeps the earliest position per
-// value), and a block-wide ballot scan compacts first occurrences in stream order.
-// The position after the k-th acceptance becomes the new MT index, so the state written
-// back equals Python's random.getstate() after the call.
+// stream in passes: a pass takes the rest of the current MT block plus as many freshly
+// twisted blocks (up to SAMPLE_AHEAD; each twist = 3 dependency phases in LDS) as the
+// expected number of draws needs, inserts every word's (value, stream position) into an
+// LDS open-addressing table with a 64-bit atomicMin (earliest position per value), and a
+// block-wide scan compacts first occurrences in stream order.  One pass normally covers the
+// whole minibatch, so the hashing and scan barriers are paid once, not once per block.  The
+// block holding the k-th acceptance and the index after it become the new MT state, so the
+// state written back equals Python's random.getstate() after the call.
 //
 // Pool branch (n <= setsize, only while the buffer is tiny): sequential on one lane.
 #include "learn.hpp"
@@ -44,14 +46,35 @@ __device__ __forceinline__ uint32_t hash_u32(uint32_t x) {
 
 constexpr int SAMPLE_NT = 1024;   // threads of the sampler workgroup (>= 624: one MT word per lane)
 
+constexpr int SAMPLE_AHEAD = 4;   // MT blocks twisted ahead per pass
+constexpr int SAMPLE_WPT = 4;     // words per thread per pass: (624 * (1 + AHEAD)) / NT rounded up
+
+// blk_new = twist(blk_old): CPython genrand_uint32's recurrence
+//   new[k] = X ^ mix(old[k], old[k+1]),  X = old[k+397] (k < 227), new[k-227] (k >= 227).
+// The dependency chain k -> k+227 -> k+454 stays inside thread k (< 227), in registers, so
+// one barrier completes the twist; new[623] = new[396] ^ mix(old[623], new[0]) is done by
+// thread 169, which owns new[396] and recomputes new[0] from `old`.
+// Every thread of the block must call it.
+__device__ __forceinline__ void mt_twist_into(const uint32_t* old, uint32_t* nw) {
+    const int t = threadIdx.x;
+    if (t < 227) {
+        const uint32_t a0 = old[t + 397] ^ mt_mix(old[t], old[t + 1]);
+        const uint32_t a1 = a0 ^ mt_mix(old[t + 227], old[t + 228]);
+        nw[t] = a0;
+        nw[t + 227] = a1;
+        if (t < 169) nw[t + 454] = a1 ^ mt_mix(old[t + 454], old[t + 455]);
+        if (t == 169) nw[623] = a1 ^ mt_mix(old[623], old[397] ^ mt_mix(old[0], old[1]));
+    }
+    __syncthreads();
+}
+
 template <int HS>  // hash slots (power of two)
 __global__ __launch_bounds__(SAMPLE_NT) void k_sample_uniform(SampleArgs a) {
     constexpr int NT = SAMPLE_NT, NW = NT / 64;
     __shared__ unsigned long long tab[HS];
-    __shared__ uint32_t mt[624];
-    __shared__ uint32_t tmp[624];
-    __shared__ int wave_cnt[NW];
-    __shared__ int s_newpos;
+    __shared__ uint32_t blk[SAMPLE_AHEAD + 1][624];   // [0] current block, [1..] twisted ahead
+    __shared__ int wave_tot[NW];
+    __shared__ int s_final;
 
     if (blockIdx.x > 0) {   // spare workgroups: blocked weight copies for the fused plan
         relayout_run(a.rl, blockIdx.x - 1, gridDim.x - 1);
@@ -73,13 +96,14 @@ __global__ __launch_bounds__(SAMPLE_NT) void k_sample_uniform(SampleArgs a) {
         phys_base = wptr - n;
         if (phys_base < 0) phys_base += a.capacity;
     }
-    if (tid < 624) mt[tid] = a.state[tid];
+    if (tid < 624) blk[0][tid] = a.state[tid];
     uint32_t pos = a.state[624];
 
     if (n <= a.setsize) {
         // ---- pool branch: one lane, CPython order (only while the buffer is tiny) ----
         __syncthreads();
         if (tid == 0) {
+            uint32_t* mt = blk[0];
             int32_t* pool = a.pool;
             for (int64_t i = 0; i < n; i++) pool[i] = (int32_t)i;
             for (int i = 0; i < k; i++) {
@@ -106,77 +130,130 @@ __global__ __launch_bounds__(SAMPLE_NT) void k_sample_uniform(SampleArgs a) {
     DQNX_STAMP(a.stamps, 1);
 #pragma unroll
     for (int i = 0; i < HS / NT; i++) tab[tid + i * NT] = ~0ull;
-    const uint32_t shift = 32u - (uint32_t)bit_length64((uint64_t)n);
+    const int bits = bit_length64((uint64_t)n);
+    const uint32_t shift = 32u - (uint32_t)bits;
+    const float inv_accept = (float)((double)(1ull << bits) / (double)n);   // words per valid draw
     int accepted = 0;
-    uint32_t consumed = 0;   // words consumed before the current MT block (stream position base)
-    bool twisted = false;
+    uint32_t spos0 = 0;      // stream position (since the call began) of blk[0][pos]
     int iter = 0;
     __syncthreads();
     while (true) {
-        if (pos >= 624) {   // parallel twist: 3 dependency phases (CPython genrand_uint32)
-            mt_twist_block(mt, tmp);
-            pos = 0;
-            twisted = true;
-        }
+        // ---- plan the pass: the rest of blk[0], then nb freshly twisted blocks ----
         const int avail = 624 - (int)pos;
-        bool valid = false, first = false;
-        uint32_t c = 0, sp = 0, h = 0;
-        if (tid < avail) {
-            c = mt_temper(mt[pos + tid]) >> shift;
-            sp = consumed + (uint32_t)tid;
-            valid = (int64_t)c < n;
-            if (valid) {   // insert (value, stream position); keep the earliest position per value
-                const unsigned long long key = ((unsigned long long)c << 32) | sp;
-                h = hash_u32(c) & (HS - 1);
-                while (true) {
-                    const unsigned long long prev = atomicCAS(&tab[h], ~0ull, key);
-                    if (prev == ~0ull) break;
-                    if ((uint32_t)(prev >> 32) == c) { atomicMin(&tab[h], key); break; }
-                    h = (h + 1) & (HS - 1);
+        const int need = k - accepted;
+        // expected words for `need` more acceptances (rejections + repeats), with margin
+        const float est = need * inv_accept * (1.f + (float)(accepted + need) / (2.f * (float)n)) + 32.f + need / 16.f;
+        int nb = (int)ceilf((est - (float)avail) / 624.f);
+        const int room = (3 * HS / 4 - accepted - avail) / 624;   // keep the table <= 3/4 full
+        nb = nb > room ? room : nb;
+        nb = nb > SAMPLE_AHEAD ? SAMPLE_AHEAD : nb;
+        nb = nb < (avail == 0 ? 1 : 0) ? 1 : nb;
+        for (int j = 1; j <= nb; j++) mt_twist_into(blk[j - 1], blk[j]);
+        if (iter == 0) DQNX_STAMP(a.stamps, 2);
+        const int nwords = avail + 624 * nb;
+        // ---- insert: thread t owns the contiguous words [t*m, t*m + m) of the pass ----
+        const int m = (nwords + NT - 1) / NT;
+        uint32_t cv[SAMPLE_WPT], hv[SAMPLE_WPT];
+        bool val[SAMPLE_WPT];
+        unsigned long long prev[SAMPLE_WPT];
+#pragma unroll
+        for (int u = 0; u < SAMPLE_WPT; u++) {   // first probe of every word, issued back to back
+            const int w = tid * m + u;
+            val[u] = false;
+            cv[u] = 0;
+            hv[u] = 0;
+            prev[u] = ~0ull;
+            if (u < m && w < nwords) {
+                const int bw = (w < avail) ? 0 : 1 + (w - avail) / 624;
+                const int ow = (w < avail) ? (int)pos + w : (w - avail) % 624;
+                const uint32_t c = mt_temper(blk[bw][ow]) >> shift;
+                if ((int64_t)c < n) {   // insert (value, stream position); earliest position wins
+                    val[u] = true;
+                    cv[u] = c;
+                    hv[u] = hash_u32(c) & (HS - 1);
+                    prev[u] = atomicCAS(&tab[hv[u]], ~0ull, ((unsigned long long)c << 32) | (spos0 + (uint32_t)w));
                 }
             }
         }
-        if (tid == 0) s_newpos = -1;
+#pragma unroll
+        for (int u = 0; u < SAMPLE_WPT; u++) {   // resolve: same value -> keep the minimum; else probe on
+            if (!val[u] || prev[u] == ~0ull) continue;
+            const unsigned long long key = ((unsigned long long)cv[u] << 32) | (spos0 + (uint32_t)(tid * m + u));
+            uint32_t h = hv[u];
+            unsigned long long pv = prev[u];
+            while (true) {
+                if ((uint32_t)(pv >> 32) == cv[u]) { atomicMin(&tab[h], key); break; }
+                h = (h + 1) & (HS - 1);
+                pv = atomicCAS(&tab[h], ~0ull, key);
+                if (pv == ~0ull) break;
+            }
+            hv[u] = h;
+        }
+        if (tid == 0) s_final = -1;
         __syncthreads();
-        if (valid) first = (uint32_t)(tab[h] & 0xffffffffull) == sp;   // h = the value's slot
-        // block-wide exclusive scan of `first` in thread (= stream) order
-        const unsigned long long bal = __ballot(first);
-        const int wprefix = __popcll(bal & ((1ull << lane) - 1ull));
-        if (lane == 0) wave_cnt[wid] = __popcll(bal);
+        if (iter == 0) DQNX_STAMP(a.stamps, 3);
+        // ---- first occurrences, exclusive scan in stream (= thread, then u) order ----
+        int cnt = 0;
+        bool first[SAMPLE_WPT];
+#pragma unroll
+        for (int u = 0; u < SAMPLE_WPT; u++) {
+            first[u] = val[u] && (uint32_t)(tab[hv[u]] & 0xffffffffull) == spos0 + (uint32_t)(tid * m + u);
+            cnt += first[u] ? 1 : 0;
+        }
+        int incl = cnt;   // wave inclusive scan
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int y = __shfl_up(incl, o);
+            if (lane >= o) incl += y;
+        }
+        if (lane == 63) wave_tot[wid] = incl;
         __syncthreads();
-        int before = 0, total = 0;
+        if (iter == 0) DQNX_STAMP(a.stamps, 4);
+        int before = incl - cnt, total = 0;
 #pragma unroll
         for (int w = 0; w < NW; w++) {
-            const int cw = wave_cnt[w];
-            before += (w < wid) ? cw : 0;
-            total += cw;
+            const int tw = wave_tot[w];
+            before += (w < wid) ? tw : 0;
+            total += tw;
         }
-        if (first) {
-            const int r = accepted + before + wprefix;
+        int r = accepted + before;
+#pragma unroll
+        for (int u = 0; u < SAMPLE_WPT; u++) {
+            if (!first[u]) continue;
             if (r < k) {
-                a.out[r] = (int32_t)c;
+                const int32_t c = (int32_t)cv[u];
+                a.out[r] = c;
                 if (a.phys_out && r >= a.shard_begin && r < a.shard_begin + a.shard_len) {
                     int64_t ps = phys_base + (int64_t)c;
                     if (ps >= a.capacity) ps -= a.capacity;
                     a.phys_out[r - a.shard_begin] = (int32_t)ps;
                 }
-                if (r == k - 1) s_newpos = (int)pos + tid + 1;
+                if (r == k - 1) s_final = tid * m + u;   // word index of the k-th acceptance
             }
+            r++;
         }
         __syncthreads();
-        DQNX_STAMP(a.stamps, 2 + (iter < 12 ? iter : 12));
+        DQNX_STAMP(a.stamps, 5 + (iter < 9 ? iter : 9));
         iter++;
         accepted += total;
         if (accepted >= k) {
-            pos = (uint32_t)s_newpos;
+            // state after the k-th draw: the block holding that word, index just past it
+            const int wf = s_final;
+            const int bf = (wf < avail) ? 0 : 1 + (wf - avail) / 624;
+            const uint32_t nx = (uint32_t)((wf < avail) ? (int)pos + wf + 1 : (wf - avail) % 624 + 1);
+            if (bf > 0 && tid < 624) a.state[tid] = blk[bf][tid];
+            if (tid == 0) a.state[624] = nx;
             break;
         }
-        consumed += (uint32_t)avail;
+        // the whole pass was consumed: continue from the last block's end
+        spos0 += (uint32_t)nwords;
+        if (nb > 0) {
+            if (tid < 624) blk[0][tid] = blk[nb][tid];
+            __syncthreads();
+        }
         pos = 624;
     }
     (void)iter;
-    if (twisted && tid < 624) a.state[tid] = mt[tid];
-    if (tid == 0) a.state[624] = pos;
     DQNX_STAMP(a.stamps, 15);
 }
 
@@ -218,10 +295,12 @@ int64_t sample_setsize(int64_t k) {
 }
 
 int sample_hash_slots(int32_t k) {
-    int64_t need = 2 * ((int64_t)k + 624);
+    // The table holds every value accepted so far plus one pass of words; the kernel caps a
+    // pass at 3/4 of the table minus the accepted values, and a pass needs room for >= 1 block.
+    int64_t need = 4 * ((int64_t)k + 624);   // load factor <= ~1/4 at the usual one-pass size
     int hs = 2048;
     while (hs < need && hs < 16384) hs <<= 1;
-    if ((int64_t)k + 624 > (int64_t)(0.9 * hs)) return -1;
+    if (4 * ((int64_t)k + 624) > 3 * (int64_t)hs) return -1;
     return hs;
 }
 

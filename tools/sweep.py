@@ -6,9 +6,17 @@ os.makedirs(OUT, exist_ok=True)
 libs = sorted(glob.glob(os.path.join(REPO, "multimodal-drl-rmc_amd/dqn/_lib/var/libdqnx_*.so")))
 extra = sys.argv[1:]
 summary = []
-for lib in libs:
-    name = os.path.basename(lib)[8:-3]
-    env = dict(os.environ, DQNX_LIB=lib)
+# optional runtime knobs: SWEEP_ENVS="tag:K=V,K2=V2;tag2:K=V" crosses every library with every set
+envsets = [("", {})]
+if os.environ.get("SWEEP_ENVS"):
+    envsets = []
+    for item in os.environ["SWEEP_ENVS"].split(";"):
+        tag, _, kv = item.partition(":")
+        envsets.append((tag, dict(p.split("=", 1) for p in kv.split(",") if p)))
+runs = [(lib, tag, ev) for lib in libs for tag, ev in envsets]
+for lib, tag, ev in runs:
+    name = os.path.basename(lib)[8:-3] + (("+" + tag) if tag else "")
+    env = dict(os.environ, DQNX_LIB=lib, **ev)
     r = subprocess.run(["timeout", "-k", "10", "240", sys.executable, os.path.join(REPO, "bench.py"), "--no-cpu-baseline",
                         "--no-kernel-timing", "--steps", "400"] + extra, env=env, capture_output=True, text=True)
     if r.returncode != 0:
