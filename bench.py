@@ -59,6 +59,8 @@ def parse():
                    help="mlp: MLP-284 (configs[1]); hybrid: TwoStreamHybridNetwork on the (2,27,5) grid; "
                         "hybrid84: the stacked (4,84,84) occupancy-grid CNN variant (configs[2])")
     p.add_argument("--no-graphs", action="store_true")
+    p.add_argument("--global-sampling", action="store_true",
+                   help="N > 1: every rank draws the same global minibatch (bit-exact with 1 GPU)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=15.0)
     p.add_argument("--no-kernel-timing", action="store_true")
@@ -217,13 +219,17 @@ def main():
 
     spec = make_spec(args)
     Bg = args.batch * world
+    per = args.algo.startswith("Per")
+    # N > 1: plain data parallelism -- every rank draws its own batch_per_gpu positions from its
+    # own MT19937 stream (O(batch_per_gpu) sampling per rank).  --global-sampling instead has
+    # every rank draw the same global minibatch (bit-exact with one GPU; PER always does this).
+    local = world > 1 and not per and not args.global_sampling
     eng = LearnEngine(spec, args.algo, Bg, args.capacity, world_size=world, rank=rank, device=device,
-                      graphs=not args.no_graphs)
+                      graphs=not args.no_graphs, local_sampling=local)
     eng.load_params(init_params(spec, 0))
     fill_ring(eng, args.capacity, spec.obs_dim, args.actions, device, seed=0)
-    random.seed(1234)   # the replay sampler continues CPython's global MT19937 stream
+    random.seed(1234 + (rank if local else 0))   # the replay sampler continues CPython's MT19937 stream
     eng.set_rng(C.DQNX_RNG_PY, np.array(random.getstate()[1], dtype=np.uint32))
-    per = args.algo.startswith("Per")
     if per:             # PER draws numpy's legacy global stream (np.random.uniform)
         np.random.seed(1234)
         st = np.random.get_state()
@@ -358,6 +364,7 @@ def main():
                 "algo": args.algo, "net": net_name(args),
                 "batch_per_gpu": args.batch, "global_batch": Bg, "replay_capacity": args.capacity,
                 "parallelism": f"dp{world}", "graphs": not args.no_graphs, "prefetch_sampling": prefetch,
+                "sampling": "rank-local" if local else "global",
             },
             "roofline": roofline,
             "cpu_baseline": cpu,

@@ -105,7 +105,10 @@ typedef struct dqnx_config {
     double beta1, beta2, adam_eps;  /* torch.optim.Adam defaults 0.9, 0.999, 1e-8 */
     double tau;                /* target_soft_update_tau */
     int32_t n_env;             /* soft update uses tau*n_env (R:dqn/agent.py:108-109) */
-    int32_t reserved0;
+    int32_t local_sampling;    /* world_size > 1, uniform replay only: 0 = every rank draws the same
+                                  global minibatch of `batch` (bit-exact with one GPU) and takes its
+                                  shard; 1 = each rank draws its own batch/world_size positions from
+                                  its own RNG stream (plain data parallelism; O(batch/world) sampling) */
     /* ReplayMemoryPrioritized constants (R:dqn/replay_memory.py:49-54) */
     double per_eps, per_alpha, per_max_priority;
     double per_beta_start, per_beta_end, per_beta_steps;   /* beta = interp(step,[0,steps],[start,end]) */

@@ -162,6 +162,8 @@ struct dqnx_engine {
     dqnx_config cfg;
     NetPlan np;
     int Bg = 0, Bl = 0, shard_begin = 0, stride = 0, tiles = 0;
+    int Bs = 0;              // positions the sampler draws: Bg, or Bl with rank-local sampling
+    bool local_sampling = false;
     int64_t setsize = 0;
     std::vector<int> slices;          // split-K slabs per dense layer
     std::vector<int> kslice;
@@ -767,7 +769,7 @@ std::vector<KStep> build_learn_steps(dqnx_engine* e, int key) {
         memset(&sa, 0, sizeof(sa));
         sa.state = ctrl->py_mt;
         sa.n_dev = &ctrl->ring_size;
-        sa.k = e->Bg;
+        sa.k = e->Bs;
         sa.setsize = e->setsize;
         sa.out = idx;
         sa.err = &ctrl->error;
@@ -782,7 +784,7 @@ std::vector<KStep> build_learn_steps(dqnx_engine* e, int key) {
         sa.rl_blocks = rl_blocks;
         KStep k;
         k.name = "sample_uniform";
-        k.bytes = 2.0 * 625 * 4 + 4.0 * e->Bg + 4.0 * Bl;
+        k.bytes = 2.0 * 625 * 4 + 4.0 * e->Bs + 4.0 * Bl;
         k.run = [=](hipStream_t s) { return launch_sample_uniform(sa, s); };
         ks.push_back(k);
     }
@@ -1401,10 +1403,16 @@ int dqnx_engine_create(const dqnx_config* cfg, dqnx_engine** out) {
     }
     e->Bg = c.batch;
     e->Bl = c.batch / c.world_size;
-    e->shard_begin = c.rank * e->Bl;
+    e->local_sampling = c.local_sampling && c.world_size > 1;
+    if (e->local_sampling && c.algo == DQNX_ALGO_PER_DOUBLE) {
+        delete e;   // the replicated SumTree needs every rank to apply the same ordered updates
+        return set_error(DQNX_EUNSUPPORTED, "rank-local sampling is for uniform replay (PER samples globally)");
+    }
+    e->shard_begin = e->local_sampling ? 0 : c.rank * e->Bl;
+    e->Bs = e->local_sampling ? e->Bl : e->Bg;
     e->stride = (int)align_up((uint64_t)c.net.obs_dim, 4);
     e->tiles = (e->Bl + 15) / 16;
-    e->setsize = sample_setsize(e->Bg);
+    e->setsize = sample_setsize(e->Bs);
     const int L = (int)e->np.dense.size();
     e->slices.assign(L, 1);
     e->kslice.assign(L, e->Bl);
@@ -1676,8 +1684,8 @@ int dqnx_learn_step(dqnx_engine* e, int32_t flags, void* stream) {
     // this step's weights, so it cannot run a step ahead either.
     const bool prefetch = (flags & DQNX_STEP_PREFETCH) && !(flags & DQNX_STEP_GIVEN_INDICES) &&
                           e->cfg.algo != DQNX_ALGO_PER_DOUBLE && e->bwd_plan != 2;
-    if (e->ring_size < e->Bg && !(flags & DQNX_STEP_GIVEN_INDICES) && !e->pf_valid)
-        return set_error(DQNX_EINVAL, "Sample larger than population: %lld < %d", (long long)e->ring_size, e->Bg);
+    if (e->ring_size < e->Bs && !(flags & DQNX_STEP_GIVEN_INDICES) && !e->pf_valid)
+        return set_error(DQNX_EINVAL, "Sample larger than population: %lld < %d", (long long)e->ring_size, e->Bs);
     const int base = flags & (DQNX_STEP_SOFT_UPDATE | DQNX_STEP_GIVEN_INDICES | DQNX_STEP_GRADS_ONLY);
     if (!prefetch && !e->pf_valid) {
         const std::vector<KStep>& ks = steps_for(e, base);
@@ -1743,8 +1751,8 @@ int dqnx_learn_step_timed(dqnx_engine* e, int32_t flags, int32_t kernel_index, v
     if (rc) return rc;
     if (!ev_start || !ev_stop) return set_error(DQNX_EINVAL, "null event");
     if (e->pf_valid) return set_error(DQNX_ESTATE, "timed step with a prefetched minibatch pending");
-    if (e->ring_size < e->Bg && !(flags & DQNX_STEP_GIVEN_INDICES))
-        return set_error(DQNX_EINVAL, "Sample larger than population: %lld < %d", (long long)e->ring_size, e->Bg);
+    if (e->ring_size < e->Bs && !(flags & DQNX_STEP_GIVEN_INDICES))
+        return set_error(DQNX_EINVAL, "Sample larger than population: %lld < %d", (long long)e->ring_size, e->Bs);
     const int key = flags & 7;
     const std::vector<KStep>& ks = steps_for(e, key);
     const int n = (int)ks.size();
@@ -1770,8 +1778,8 @@ int dqnx_learn_step_omit(dqnx_engine* e, int32_t flags, int32_t omit_index, void
     int rc = check_bound(e);
     if (rc) return rc;
     if (e->pf_valid) return set_error(DQNX_ESTATE, "timing step with a prefetched minibatch pending");
-    if (e->ring_size < e->Bg && !(flags & DQNX_STEP_GIVEN_INDICES))
-        return set_error(DQNX_EINVAL, "Sample larger than population: %lld < %d", (long long)e->ring_size, e->Bg);
+    if (e->ring_size < e->Bs && !(flags & DQNX_STEP_GIVEN_INDICES))
+        return set_error(DQNX_EINVAL, "Sample larger than population: %lld < %d", (long long)e->ring_size, e->Bs);
     const int base = flags & 7;
     const std::vector<KStep>& ks = steps_for(e, base);
     const int n = (int)ks.size();

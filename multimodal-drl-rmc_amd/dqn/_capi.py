@@ -56,7 +56,7 @@ class Config(ctypes.Structure):
         ("net", NetDesc), ("algo", I32), ("batch", I32), ("world_size", I32), ("rank", I32),
         ("capacity", I64), ("gamma", ctypes.c_double), ("lr", ctypes.c_double), ("beta1", ctypes.c_double),
         ("beta2", ctypes.c_double), ("adam_eps", ctypes.c_double), ("tau", ctypes.c_double), ("n_env", I32),
-        ("reserved0", I32), ("per_eps", ctypes.c_double), ("per_alpha", ctypes.c_double),
+        ("local_sampling", I32), ("per_eps", ctypes.c_double), ("per_alpha", ctypes.c_double),
         ("per_max_priority", ctypes.c_double), ("per_beta_start", ctypes.c_double),
         ("per_beta_end", ctypes.c_double), ("per_beta_steps", ctypes.c_double),
     ]

@@ -137,7 +137,8 @@ class LearnEngine:
     """One agent's learn-step engine on one GPU (one process per GPU under DP)."""
 
     def __init__(self, spec: NetSpec, algo: str, batch: int, capacity: int, gamma=0.99, lr=1e-4,
-                 tau=1e-3, n_env=1, world_size=1, rank=0, device=None, graphs=True, eps_dec=2e6):
+                 tau=1e-3, n_env=1, world_size=1, rank=0, device=None, graphs=True, eps_dec=2e6,
+                 local_sampling=False):
         if not torch.cuda.is_available():
             raise RuntimeError("libdqnx needs a ROCm GPU (MI355X / gfx950); there is no CPU fallback")
         self.L = C.lib()
@@ -151,6 +152,7 @@ class LearnEngine:
         cfg.batch, cfg.world_size, cfg.rank, cfg.capacity = batch, world_size, rank, capacity
         cfg.gamma, cfg.lr, cfg.tau, cfg.n_env = gamma, lr, tau, n_env
         cfg.per_beta_steps = eps_dec
+        cfg.local_sampling = 1 if local_sampling else 0
         self.cfg = cfg
         h = ctypes.c_void_p()
         C.check(self.L.dqnx_engine_create(ctypes.byref(cfg), ctypes.byref(h)), "dqnx_engine_create")

@@ -17,15 +17,17 @@ from oracle import ref as O  # noqa: E402  (test data + initial weights only)
 
 def main():
     rank, world, algo, out = int(sys.argv[1]), int(sys.argv[2]), sys.argv[3], sys.argv[4]
+    local = len(sys.argv) > 5 and sys.argv[5] == "local"
     backend = os.environ.get("DQNX_TEST_BACKEND", "gloo")
     torch.cuda.set_device(0)
     dist.init_process_group(backend, rank=rank, world_size=world)
     obs_dim, batch, cap, fill, seed = 284, 64, 1000, 700, 9
     head = O.algo_spec_head(algo)
-    eng = E.LearnEngine(E.mlp_spec(obs_dim, 8, head), algo, batch, cap, world_size=world, rank=rank)
+    eng = E.LearnEngine(E.mlp_spec(obs_dim, 8, head), algo, batch, cap, world_size=world, rank=rank,
+                        local_sampling=local)
     eng.load_params(O.reference_init(O.mlp_spec(obs_dim, 8, head), seed))
     eng.push(*O.synth_transitions(fill, obs_dim, 8, seed=seed + 100))
-    eng.set_rng(0, O.py_state_to_array(__import__("random").Random(seed).getstate()))
+    eng.set_rng(0, O.py_state_to_array(__import__("random").Random(seed + (rank if local else 0)).getstate()))
     eng.set_rng(1, O.np_state_to_array(np.random.RandomState(seed).get_state()))
     losses, pos = [], []
     for _ in range(3):

@@ -47,3 +47,39 @@ def test_gpu_dp_world2_matches_oracle(tmp_path, algo):
         if ref.per:
             np.testing.assert_allclose(z["tree"], ref.replay.replay_buffer.tree, rtol=1e-6, atol=1e-4)
     assert np.array_equal(z0["params"], z1["params"]) and np.array_equal(z0["tree"], z1["tree"])
+
+
+def test_gpu_dp_world2_rank_local_sampling(tmp_path):
+    """local_sampling: rank r draws its own batch/world positions from its own MT stream; the
+    all-reduced update equals one learner stepping on the concatenated minibatch."""
+    import random
+    algo = "DuelingDoubleDQNAgent"
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(free_port()))
+    procs = [subprocess.Popen([sys.executable, os.path.join(HERE, "dp_gpu_worker.py"), str(r), "2", algo,
+                               str(tmp_path), "local"], env=env) for r in range(2)]
+    for p in procs:
+        assert p.wait(timeout=240) == 0
+    obs_dim, batch, cap, fill, seed = 284, 64, 1000, 700, 9
+    spec = O.mlp_spec(obs_dim, 8, O.algo_spec_head(algo))
+    ref = O.OracleLearner(spec, algo, batch, cap, seed=seed, params=O.reference_init(spec, seed))
+    O.fill_replay(ref, *O.synth_transitions(fill, obs_dim, 8, seed=seed + 100))
+    states = [O.py_state_to_array(random.Random(seed + r).getstate()) for r in range(2)]
+    buf = ref.replay.replay_buffer
+    want = []
+
+    def sample_both(_state):   # the two ranks' draws, concatenated in rank order
+        pos = np.concatenate([O.sample_positions(states[r], len(buf), batch // 2) for r in range(2)])
+        want.append(pos)
+        return [buf[int(j)] for j in pos], pos
+    ref.replay.sample_transitions = sample_both
+    recs = [ref.train_step() for _ in range(3)]
+    flat_on = np.concatenate([v.reshape(-1).numpy() for v in ref.online.values()])
+    flat_tg = np.concatenate([v.reshape(-1).numpy() for v in ref.target.values()])
+    z = [np.load(tmp_path / f"rank{r}.npz") for r in (0, 1)]
+    for r in range(2):
+        got = z[r]["positions"][:, :batch // 2].astype(np.int64)
+        assert np.array_equal(got, np.stack([p[r * (batch // 2):(r + 1) * (batch // 2)] for p in want])), r
+        np.testing.assert_allclose(z[r]["losses"], [x.loss for x in recs], rtol=1e-5, atol=1e-6)
+        np.testing.assert_allclose(z[r]["params"], flat_on, atol=1e-5, rtol=0)
+        np.testing.assert_allclose(z[r]["target"], flat_tg, atol=1e-5, rtol=0)
+    assert np.array_equal(z[0]["params"], z[1]["params"])
