@@ -12,11 +12,13 @@ import sys
 from collections import defaultdict
 
 NAMES = [   # (substring of the HIP kernel name, bench step name)
+    ("k_mlp_fwd", "mlp_fwd"),
+    ("k_head_bwd", "head_bwd"),
     ("k_linear_fwd<0, true, true>", "linear_fwd_l1"),
     ("k_linear_fwd<0, true, false>", "linear_fwd_l2"),
     ("k_sample_uniform", "sample_uniform"),
     ("k_head<", "head_td_loss"),
-    ("k_bwd_level<", "linear_bwd (both levels)"),
+    ("k_bwd_level<", "dw_all"),
     ("k_adam", "adam_fused"),
     ("k_per_sample", "per_sample"),
     ("k_per_update", "per_update"),
