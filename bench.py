@@ -37,6 +37,7 @@ from dqn.data_parallel import dp_learn_step  # noqa: E402
 from dqn.engine import LearnEngine, hybrid_spec, mlp_spec  # noqa: E402
 
 PEAK_FP32_MFMA_TFLOPS = 157.3   # MI355X_MICROARCH.md: F32 matrix, dense
+PEAK_BF16_MFMA_TFLOPS = 2500.0  # MI355X_MICROARCH.md: BF16 MFMA ~2.5 PF dense (no sparsity)
 PEAK_HBM_GBS = 8000.0           # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 
 
@@ -59,6 +60,8 @@ def parse():
                    help="mlp: MLP-284 (configs[1]); hybrid: TwoStreamHybridNetwork on the (2,27,5) grid; "
                         "hybrid84: the stacked (4,84,84) occupancy-grid CNN variant (configs[2])")
     p.add_argument("--no-graphs", action="store_true")
+    p.add_argument("--compute", default="fp32", choices=["fp32", "bf16"],
+                   help="GEMM operand precision (bf16: BASELINE config 5; MLP only; fp32 accumulate, master weights, Adam)")
     p.add_argument("--global-sampling", action="store_true",
                    help="N > 1: every rank draws the same global minibatch (bit-exact with 1 GPU)")
     p.add_argument("--no-cpu-baseline", action="store_true")
@@ -225,7 +228,7 @@ def main():
     # every rank draw the same global minibatch (bit-exact with one GPU; PER always does this).
     local = world > 1 and not per and not args.global_sampling
     eng = LearnEngine(spec, args.algo, Bg, args.capacity, world_size=world, rank=rank, device=device,
-                      graphs=not args.no_graphs, local_sampling=local)
+                      graphs=not args.no_graphs, local_sampling=local, compute_dtype=args.compute)
     eng.load_params(init_params(spec, 0))
     fill_ring(eng, args.capacity, spec.obs_dim, args.actions, device, seed=0)
     random.seed(1234 + (rank if local else 0))   # the replay sampler continues CPython's MT19937 stream
@@ -318,10 +321,12 @@ def main():
         kernels[dom]["avg_us"] = avg_ms * 1e3
         nm, fl, by = infos[dom]
         intensity = fl / by if by else 0.0
-        ridge = PEAK_FP32_MFMA_TFLOPS * 1e12 / (PEAK_HBM_GBS * 1e9)
+        peak_mfma = PEAK_BF16_MFMA_TFLOPS if args.compute == "bf16" else PEAK_FP32_MFMA_TFLOPS
+        ridge = peak_mfma * 1e12 / (PEAK_HBM_GBS * 1e9)
         traffic = None
         # HBM bytes per launch from rocprofv3 PMC passes of this same workload (tools/pmc_traffic.py)
-        pmc_path = os.path.join(REPO, "profiles", f"pmc_traffic_{args.net}_b{args.batch}.json")
+        tag = "" if args.compute == "fp32" else f"_{args.compute}"
+        pmc_path = os.path.join(REPO, "profiles", f"pmc_traffic_{args.net}_b{args.batch}{tag}.json")
         if os.path.exists(pmc_path):
             try:
                 traffic = json.load(open(pmc_path)).get(nm, {}).get("hbm_bytes_per_launch")
@@ -329,8 +334,8 @@ def main():
                 traffic = None
         if intensity > ridge and fl > 0:
             ach = fl / (avg_ms * 1e-3) / 1e12
-            roofline = {"bound": "mfma", "achieved": ach, "peak": PEAK_FP32_MFMA_TFLOPS, "unit": "TFLOP/s",
-                        "frac": ach / PEAK_FP32_MFMA_TFLOPS, "traffic": traffic, "kernel": nm,
+            roofline = {"bound": "mfma", "achieved": ach, "peak": peak_mfma, "unit": "TFLOP/s",
+                        "frac": ach / peak_mfma, "traffic": traffic, "kernel": nm,
                         "avg_us": avg_ms * 1e3, "algorithmic_flops": fl, "algorithmic_bytes": by}
         else:
             ach = by / (avg_ms * 1e-3) / 1e9
@@ -357,7 +362,7 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "fp32",
+            "dtype": args.compute,
             "data": "synthetic",
             "config": {
                 "workload": WORKLOADS[args.net],

@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define DQNX_ABI_VERSION 1
+#define DQNX_ABI_VERSION 2
 
 /* ---- status codes ---------------------------------------------------------------- */
 #define DQNX_OK 0
@@ -43,6 +43,11 @@ extern "C" {
 enum dqnx_net_kind { DQNX_NET_MLP = 0, DQNX_NET_TWO_STREAM = 1 };
 enum dqnx_head_kind { DQNX_HEAD_LINEAR = 0, DQNX_HEAD_DUELING = 1 };
 enum dqnx_activation { DQNX_ACT_RELU = 0, DQNX_ACT_ELU = 1 };
+/* Arithmetic of the network GEMMs.  FP32 is the reference's (parity within 1e-5).  BF16
+ * (BASELINE config 5): forward and dZ-chain GEMM operands rounded to bf16 (RNE), fp32
+ * accumulate; bias, activations, TD target, Huber, weight gradients, Adam and the master
+ * weights stay fp32.  MLP networks only. */
+enum dqnx_compute_dtype { DQNX_COMPUTE_FP32 = 0, DQNX_COMPUTE_BF16 = 1 };
 /* Learner algorithm = which Agent.learn() runs:
  *   DQNX_ALGO_DQN        SimpleAgent.learn          R:dqn/agent.py:166-185  (DQNAgent)
  *   DQNX_ALGO_DOUBLE     DoubleAgent.learn          R:dqn/agent.py:204-226  (DoubleDQNAgent,
@@ -112,6 +117,8 @@ typedef struct dqnx_config {
     /* ReplayMemoryPrioritized constants (R:dqn/replay_memory.py:49-54) */
     double per_eps, per_alpha, per_max_priority;
     double per_beta_start, per_beta_end, per_beta_steps;   /* beta = interp(step,[0,steps],[start,end]) */
+    int32_t compute_dtype;     /* dqnx_compute_dtype (ABI 2) */
+    int32_t reserved1;
 } dqnx_config;
 
 /* Fill cfg with the reference's HYPER_PARAMS defaults for the given network. */

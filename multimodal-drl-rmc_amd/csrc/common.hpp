@@ -17,6 +17,20 @@ __device__ __forceinline__ floatx4 mfma16x16x4(float a, float b, floatx4 c) {
     return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
 
+// bf16 operands (DQNX_COMPUTE_BF16).  v_mfma_f32_16x16x32_bf16: lane l supplies
+// A[l&15][8(l>>4) + j] and B[8(l>>4) + j][l&15], j = 0..7 (16 bytes each); the accumulator
+// layout is the fp32 one above.  float -> bf16 is v_cvt_pk_bf16_f32 (round to nearest even,
+// torch's Tensor.to(torch.bfloat16) on finite values).
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ uint32_t bf16_pack2(float lo, float hi) {
+    return (uint32_t)__builtin_bit_cast(uint16_t, (__bf16)lo) | ((uint32_t)__builtin_bit_cast(uint16_t, (__bf16)hi) << 16);
+}
+__device__ __forceinline__ uint16_t bf16_bits(float x) { return __builtin_bit_cast(uint16_t, (__bf16)x); }
+__device__ __forceinline__ floatx4 mfma16x16x32bf16(u32x4 a, u32x4 b, floatx4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), c, 0, 0, 0);
+}
+
 __device__ __forceinline__ float relu_f(float x) { return x > 0.f ? x : 0.f; }
 
 // torch CPU ELU (alpha=scale=input_scale=1): x <= 0 ? expm1(x) : x

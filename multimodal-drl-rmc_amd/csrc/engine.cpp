@@ -277,10 +277,11 @@ int layout(dqnx_engine* e) {
     }
     if (e->bwd_plan == 2) {
         for (int l = 0; l < L; l++) {
-            const uint64_t fwd = (uint64_t)np.dense[l].out * e->fplan.kpad[l] * 4;
+            const bool bf = e->fplan.bf16 != 0;
+            const uint64_t fwd = (uint64_t)fused_wblk_bytes(bf, np.dense[l].out, e->fplan.kpad[l]);
             e->ws_wblk[0][l] = sub(fwd);
             e->ws_wblk[1][l] = sub(fwd);
-            if (l >= 1) e->ws_wblkT[l] = sub((uint64_t)np.dense[l].out * np.dense[l].in * 4);
+            if (l >= 1) e->ws_wblkT[l] = sub((uint64_t)fused_wblk_bytes(bf, np.dense[l].in, np.dense[l].out));
         }
     }
     e->ws_adam_tab = sub((uint64_t)kAdamTable * 2 * 4);
@@ -504,14 +505,16 @@ RelayoutArgs relayout_args(dqnx_engine* e, int* blocks) {
         j.src = src; j.dst = dst; j.rows = rows; j.cols = cols; j.kind = kind; j.nch = nch; j.q0 = q;
         q += nq;
     };
+    const bool bf = e->fplan.bf16 != 0;
+    const int kc = bf ? 32 : 16, per_q = bf ? 8 : 4;   // K per chunk, elements per 16-byte unit
     for (int l = 0; l < (int)np.dense.size(); l++) {
         const LayerPlan& lp = np.dense[l];
         const int kp = e->fplan.kpad[l];
-        const int64_t nq = (int64_t)lp.out * kp / 4;
-        add(params + lp.off, at<float>(e, e->ws_wblk[0][l]), lp.out, lp.in, 0, kp / 16, nq);
-        add(tparams + lp.off, at<float>(e, e->ws_wblk[1][l]), lp.out, lp.in, 0, kp / 16, nq);
-        if (l >= 1) add(params + lp.off, at<float>(e, e->ws_wblkT[l]), lp.out, lp.in, 1, lp.out / 16,
-                        (int64_t)lp.out * lp.in / 4);
+        const int64_t nq = (int64_t)lp.out * kp / per_q;
+        add(params + lp.off, at<float>(e, e->ws_wblk[0][l]), lp.out, lp.in, bf ? 2 : 0, kp / kc, nq);
+        add(tparams + lp.off, at<float>(e, e->ws_wblk[1][l]), lp.out, lp.in, bf ? 2 : 0, kp / kc, nq);
+        if (l >= 1) add(params + lp.off, at<float>(e, e->ws_wblkT[l]), lp.out, lp.in, bf ? 3 : 1, lp.out / kc,
+                        (int64_t)lp.out * lp.in / per_q);
     }
     r.total_q = q;
     int b = (int)((q + 1023) / 1024);
@@ -536,7 +539,7 @@ void build_fused_steps(dqnx_engine* e, int flags, int32_t* idx, int32_t* phys, s
     double body_flops = 0, wbytes = 0;   // per stream: 2 * in * out summed; weight bytes
     for (int l = 0; l < L; l++) {
         body_flops += 2.0 * np.dense[l].in * np.dense[l].out;
-        wbytes += 4.0 * (np.dense[l].in + 1.0) * np.dense[l].out;
+        wbytes += (e->fplan.bf16 ? 2.0 : 4.0) * np.dense[l].in * np.dense[l].out + 4.0 * np.dense[l].out;
     }
     // 2. forward (R:dqn/agent.py:209-214 / 172-173 streams, R:dqn/network.py:61-65, 90-96)
     {
@@ -586,6 +589,7 @@ void build_fused_steps(dqnx_engine* e, int flags, int32_t* idx, int32_t* phys, s
         ha.L = L;
         ha.Bl = e->Bl;
         ha.nsplit = 1;
+        ha.bf16 = e->fplan.bf16;
         if (L >= 2 && np.dense[0].out % (2 * 64) == 0) ha.nsplit = 2;   // dZ_1 columns over 2 workgroups
         if (const char* ns = getenv("DQNX_HEAD_SPLIT")) { const int v = atoi(ns); if (v == 1 || (v == 2 && ha.nsplit == 2)) ha.nsplit = v; }
         ha.A = A;
@@ -1394,11 +1398,18 @@ int dqnx_engine_create(const dqnx_config* cfg, dqnx_engine** out) {
         }
         fp.NH = e->np.NH;
         fp.F = e->np.F;
-        const bool fused_ok = c.net.kind == DQNX_NET_MLP && fused_fwd_plan(fp, c.net.obs_dim);
+        if (c.compute_dtype != DQNX_COMPUTE_FP32 && c.compute_dtype != DQNX_COMPUTE_BF16)
+            { delete e; return set_error(DQNX_EINVAL, "bad compute_dtype %d", c.compute_dtype); }
+        const bool bf = c.compute_dtype == DQNX_COMPUTE_BF16;
+        const bool fused_ok = c.net.kind == DQNX_NET_MLP && fused_fwd_plan(fp, c.net.obs_dim, bf);
         e->bwd_plan = fused_ok ? 2 : 0;
         if (const char* bp = getenv("DQNX_BWD_PLAN")) {
             const int want = atoi(bp);
             if (want == 0 || (want == 1 && c.net.kind == DQNX_NET_MLP) || (want == 2 && fused_ok)) e->bwd_plan = want;
+        }
+        if (bf && e->bwd_plan != 2) {   // bf16 lives in the fused MLP kernels only
+            delete e;
+            return set_error(DQNX_EUNSUPPORTED, "bf16 compute needs the fused MLP plan (MLP, widths multiple of 64 <= 256, <= 3 layers)");
         }
     }
     e->Bg = c.batch;

@@ -46,6 +46,14 @@ constexpr int FGQ = 6;     // float4 gather slots per thread (input tile <= FGQ 
 
 __host__ __device__ __forceinline__ int fused_stride(int K) { return ((K + 63) & ~63) + 8; }
 __host__ __device__ __forceinline__ int fused_groups(int K) { return (K + 16 * FPF - 1) / (16 * FPF); }
+// Chunks of one weight stream over K and MFMA groups of FPF chunks.  fp32: 16-deep chunks,
+// K padded to whole groups (the blocked copy holds the zero chunks).  bf16: 32-deep chunks,
+// K padded to 32 only; chunks past nch in the last group are skipped (their A columns in
+// LDS are not zeroed).
+template <bool BF>
+__host__ __device__ __forceinline__ int fwd_nch(int K) { return BF ? (K + 31) / 32 : fused_groups(K) * FPF; }
+template <bool BF>
+__host__ __device__ __forceinline__ int fwd_groups(int K) { return BF ? (fwd_nch<true>(K) + FPF - 1) / FPF : fused_groups(K); }
 
 // Workgroup barrier for LDS hand-offs only.  __syncthreads() also drains every outstanding
 // global access of the wave (vmcnt(0)) -- here that would wait for the activation stores
@@ -57,7 +65,6 @@ __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(
 // (a generic pointer that lost its address space becomes a flat load, and the compiler then
 // drains vmcnt AND lgkmcnt at every use), and an out-of-range offset reads zeros without
 // touching memory (the prefetch overrun past the last chunk needs no branch).
-typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 constexpr uint32_t kOOB = 0x80000000u;
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t wave_rsrc(const float* base, uint32_t bytes) {
@@ -121,23 +128,39 @@ __device__ __forceinline__ void stream_open(const float* blk, int ntiles, int nc
     }
 }
 
-// acc[t] += A[16][16 * ch0 ...] . B_t for one group of FPF chunks (A fragments from LDS).
-// MFMA jj of a chunk consumes k = 16 ch + 4 (lane >> 4) + jj for both operands.
-template <int TN>
-__device__ __forceinline__ void mma_group(const float* ap, int ch0, const float4 (&w)[FPF][2], floatx4 (&acc)[2]) {
-    float4 av[FPF];
+// acc[t] += A[16][K-chunks ch0 ...] . B_t for one group of FPF chunks (A fragments from LDS).
+// fp32: MFMA jj of a chunk consumes k = 16 ch + 4 (lane >> 4) + jj for both operands.
+// bf16: one 16x16x32 MFMA per chunk, k = 32 ch + 8 (lane >> 4) + j; chunks >= nch skipped.
+template <int TN, bool BF>
+__device__ __forceinline__ void mma_group(const void* ap_, int ch0, int nch, const float4 (&w)[FPF][2],
+                                          floatx4 (&acc)[2]) {
+    if constexpr (!BF) {
+        const float* ap = static_cast<const float*>(ap_);
+        float4 av[FPF];
 #pragma unroll
-    for (int p = 0; p < FPF; p++) av[p] = *reinterpret_cast<const float4*>(ap + (ch0 + p) * 16);
+        for (int p = 0; p < FPF; p++) av[p] = *reinterpret_cast<const float4*>(ap + (ch0 + p) * 16);
 #pragma unroll
-    for (int p = 0; p < FPF; p++) {
+        for (int p = 0; p < FPF; p++) {
 #pragma unroll
-        for (int t = 0; t < TN; t++) acc[t] = mfma16x16x4(av[p].x, w[p][t].x, acc[t]);
+            for (int t = 0; t < TN; t++) acc[t] = mfma16x16x4(av[p].x, w[p][t].x, acc[t]);
 #pragma unroll
-        for (int t = 0; t < TN; t++) acc[t] = mfma16x16x4(av[p].y, w[p][t].y, acc[t]);
+            for (int t = 0; t < TN; t++) acc[t] = mfma16x16x4(av[p].y, w[p][t].y, acc[t]);
 #pragma unroll
-        for (int t = 0; t < TN; t++) acc[t] = mfma16x16x4(av[p].z, w[p][t].z, acc[t]);
+            for (int t = 0; t < TN; t++) acc[t] = mfma16x16x4(av[p].z, w[p][t].z, acc[t]);
 #pragma unroll
-        for (int t = 0; t < TN; t++) acc[t] = mfma16x16x4(av[p].w, w[p][t].w, acc[t]);
+            for (int t = 0; t < TN; t++) acc[t] = mfma16x16x4(av[p].w, w[p][t].w, acc[t]);
+        }
+    } else {
+        const uint16_t* ap = static_cast<const uint16_t*>(ap_);
+        u32x4 av[FPF];
+#pragma unroll
+        for (int p = 0; p < FPF; p++) av[p] = *reinterpret_cast<const u32x4*>(ap + (ch0 + p) * 32);
+#pragma unroll
+        for (int p = 0; p < FPF; p++) {
+            if (ch0 + p >= nch) break;
+#pragma unroll
+            for (int t = 0; t < TN; t++) acc[t] = mfma16x16x32bf16(av[p], __builtin_bit_cast(u32x4, w[p][t]), acc[t]);
+        }
     }
 }
 
@@ -146,11 +169,12 @@ __device__ __forceinline__ void mma_group(const float* ap, int ch0, const float4
 // before group g is multiplied, so FNB-1 groups of MFMAs cover each L2 round trip.  Every
 // fetch is unconditional (past the last chunk it reads the out-of-range offset), which keeps
 // the compiler's vmcnt counts exact; only the MFMAs of missing groups are skipped.
-template <int TN>
-__device__ __forceinline__ void wave_mma_t(const float* As, int sa, int ngroups, const WStream& w,
+template <int TN, bool BF>
+__device__ __forceinline__ void wave_mma_t(const void* As, int sa, int ngroups, const WStream& w,
                                            float4 (&wb)[FNB][FPF][2], floatx4 (&acc)[2]) {
     const int lane = threadIdx.x & 63, i = lane & 15, g = lane >> 4;
-    const float* ap = As + i * sa + 4 * g;
+    const void* ap = BF ? (const void*)(static_cast<const uint16_t*>(As) + i * sa + 8 * g)
+                        : (const void*)(static_cast<const float*>(As) + i * sa + 4 * g);
 #pragma unroll
     for (int t = 0; t < TN; t++) acc[t] = floatx4{0.f, 0.f, 0.f, 0.f};
     for (int grp = 0; grp < ngroups; grp += FNB) {
@@ -162,14 +186,15 @@ __device__ __forceinline__ void wave_mma_t(const float* As, int sa, int ngroups,
             // pin the refill ahead of this group's MFMAs: left alone, the scheduler sinks the
             // loads below them and the prefetch distance collapses to ~0
             __builtin_amdgcn_sched_barrier(0);
-            if (grp + u < ngroups) mma_group<TN>(ap, ch, wb[u], acc);
+            if (grp + u < ngroups) mma_group<TN, BF>(ap, ch, w.nch, wb[u], acc);
         }
     }
 }
-__device__ __forceinline__ void wave_mma(const float* As, int sa, int ngroups, const WaveCols& c, const WStream& w,
+template <bool BF>
+__device__ __forceinline__ void wave_mma(const void* As, int sa, int ngroups, const WaveCols& c, const WStream& w,
                                          float4 (&wb)[FNB][FPF][2], floatx4 (&acc)[2]) {
-    if (c.tn == 2) wave_mma_t<2>(As, sa, ngroups, w, wb, acc);
-    else if (c.tn == 1) wave_mma_t<1>(As, sa, ngroups, w, wb, acc);
+    if (c.tn == 2) wave_mma_t<2, BF>(As, sa, ngroups, w, wb, acc);
+    else if (c.tn == 1) wave_mma_t<1, BF>(As, sa, ngroups, w, wb, acc);
 }
 
 // =====================================================================================
@@ -179,7 +204,9 @@ __device__ __forceinline__ void wave_mma(const float* As, int sa, int ngroups, c
 // NL (dense layers) is a template parameter so every per-layer kernel-argument access has a
 // constant index: a runtime-indexed kernarg array element becomes a dependent global load
 // with its own wait (eight of them serialised the head kernel's prologue).
-template <int ACT, int NL>
+// BF: bf16 activation tiles in LDS (row strides sx / sh in bf16 elements), bf16 blocked
+// weights, 16x16x32 bf16 MFMAs; accumulation, bias, activation and the H stores stay fp32.
+template <int ACT, int NL, bool BF>
 __global__ __launch_bounds__(FT) void k_mlp_fwd(FusedFwdArgs a) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     // LDS tile b: pointer arithmetic on `lds` keeps the LDS address space visible to the
@@ -205,11 +232,11 @@ __global__ __launch_bounds__(FT) void k_mlp_fwd(FusedFwdArgs a) {
     //     Issue order matters (vmcnt retires in order): ring slots first, then layer 1's
     //     weight stream (independent of the rows), then the dependent row loads.
     {
-        const int kz = fused_groups(a.in[0]) * FPF * 16;   // columns the MMA loop reads
+        const int kz = BF ? fwd_nch<true>(a.in[0]) * 32 : fused_groups(a.in[0]) * FPF * 16;   // columns multiplied
         const int q4 = kz >> 2, rs4 = a.ring_stride >> 2;
         // branch-free: every slot loads (clamped row / column) and selects zero afterwards,
         // so the loads issue back to back (one phys round trip, then one ring round trip)
-        if (DQNX_FUSED_ORDER == 1) stream_open(a.wblk[tgt][0], a.out[0] >> 4, fused_groups(a.in[0]) * FPF, 0, c, ws, wb);
+        if (DQNX_FUSED_ORDER == 1) stream_open(a.wblk[tgt][0], a.out[0] >> 4, fwd_nch<BF>(a.in[0]), 0, c, ws, wb);
         int32_t slot[FGQ];
 #pragma unroll
         for (int j = 0; j < FGQ; j++) {
@@ -220,7 +247,7 @@ __global__ __launch_bounds__(FT) void k_mlp_fwd(FusedFwdArgs a) {
         // load there instead of a dependent phys -> ring chain)
         int32_t tslot = 0;
         if (keep && tid < nb) tslot = a.phys[b0 + tid];
-        if (DQNX_FUSED_ORDER == 0) stream_open(a.wblk[tgt][0], a.out[0] >> 4, fused_groups(a.in[0]) * FPF, 0, c, ws, wb);
+        if (DQNX_FUSED_ORDER == 0) stream_open(a.wblk[tgt][0], a.out[0] >> 4, fwd_nch<BF>(a.in[0]), 0, c, ws, wb);
         float4 xv[FGQ];
 #pragma unroll
         for (int j = 0; j < FGQ; j++) {
@@ -231,7 +258,7 @@ __global__ __launch_bounds__(FT) void k_mlp_fwd(FusedFwdArgs a) {
             if (!ok) x = make_float4(0.f, 0.f, 0.f, 0.f);
             xv[j] = x;
         }
-        if (DQNX_FUSED_ORDER == 2) stream_open(a.wblk[tgt][0], a.out[0] >> 4, fused_groups(a.in[0]) * FPF, 0, c, ws, wb);
+        if (DQNX_FUSED_ORDER == 2) stream_open(a.wblk[tgt][0], a.out[0] >> 4, fwd_nch<BF>(a.in[0]), 0, c, ws, wb);
         // after the row loads are in flight: the transition scalars' own round trip overlaps them
         if (keep && tid < nb)
             a.trans[b0 + tid] = make_float4(__int_as_float(a.act[tslot]), a.rew[tslot], a.done[tslot], 0.f);
@@ -240,7 +267,11 @@ __global__ __launch_bounds__(FT) void k_mlp_fwd(FusedFwdArgs a) {
             const int q = tid + j * FT;
             const int r = q / q4, c4 = q - r * q4;
             if (r < 16) {
-                *reinterpret_cast<float4*>(FBUF(0) + r * a.sx + 4 * c4) = xv[j];
+                if constexpr (BF)
+                    *reinterpret_cast<uint2*>(reinterpret_cast<uint16_t*>(FBUF(0)) + r * a.sx + 4 * c4) =
+                        make_uint2(bf16_pack2(xv[j].x, xv[j].y), bf16_pack2(xv[j].z, xv[j].w));
+                else
+                    *reinterpret_cast<float4*>(FBUF(0) + r * a.sx + 4 * c4) = xv[j];
                 if (keep && r < nb && c4 < rs4)
                     *reinterpret_cast<float4*>(a.xcopy + (int64_t)(b0 + r) * a.ring_stride + 4 * c4) = xv[j];
             }
@@ -259,13 +290,13 @@ __global__ __launch_bounds__(FT) void k_mlp_fwd(FusedFwdArgs a) {
 #pragma unroll
         for (int t = 0; t < 2; t++) bias[t] = bias_p[(t < c.tn ? c.n0[t] : 0) + i];   // branch-free
         floatx4 acc[2];
-        wave_mma(FBUF(cur), l == 0 ? a.sx : a.sh, fused_groups(K), c, ws, wb, acc);
+        wave_mma<BF>(FBUF(cur), l == 0 ? a.sx : a.sh, fwd_groups<BF>(K), c, ws, wb, acc);
         DQNX_STAMP(a.stamps, 27 + 2 * l);
         const WaveCols cl = c;
         // next layer's weight stream in flight during the epilogue + barrier
         if (l + 1 < NL) {
             c = wave_cols(a.out[l + 1]);
-            stream_open(a.wblk[tgt][l + 1], a.out[l + 1] >> 4, fused_groups(a.in[l + 1]) * FPF, 0, c, ws, wb);
+            stream_open(a.wblk[tgt][l + 1], a.out[l + 1] >> 4, fwd_nch<BF>(a.in[l + 1]), 0, c, ws, wb);
         }
         float* Hs = FBUF(cur ^ 1);
         float* Hg = keep ? a.H[l] : nullptr;
@@ -277,7 +308,8 @@ __global__ __launch_bounds__(FT) void k_mlp_fwd(FusedFwdArgs a) {
             for (int r = 0; r < 4; r++) {
                 const int rr = 4 * g + r;
                 const float v = act_fwd<ACT>(acc[t][r] + bias[t]);
-                Hs[rr * a.sh + col] = v;
+                if constexpr (BF) reinterpret_cast<uint16_t*>(Hs)[rr * a.sh + col] = bf16_bits(v);
+                else Hs[rr * a.sh + col] = v;
                 if (Hg && rr < nb) Hg[(int64_t)(b0 + rr) * N + col] = v;
             }
         }
@@ -288,19 +320,29 @@ __global__ __launch_bounds__(FT) void k_mlp_fwd(FusedFwdArgs a) {
 
     // head: raw[o] = H_L . W_head[o] + b_head[o], o < NH; K = F split over the waves
     {
-        const int F = a.F, nck = F >> 4;
+        const int F = a.F;
         const int A = a.head_kind == DQNX_HEAD_DUELING ? a.NH - 1 : a.NH;
         const float* hw = P + a.head_off + head_w_off(a.head_kind, i < a.NH ? i : 0, F);
-        const float* hs = FBUF(cur) + i * a.sh + 4 * g;
         floatx4 acc = {0.f, 0.f, 0.f, 0.f};
-        for (int ck = wid; ck < nck; ck += FW) {
-            float4 wv = ld4(hw + ck * 16 + 4 * g);
-            if (i >= a.NH) wv = make_float4(0.f, 0.f, 0.f, 0.f);
-            const float4 av = *reinterpret_cast<const float4*>(hs + ck * 16);
-            acc = mfma16x16x4(av.x, wv.x, acc);
-            acc = mfma16x16x4(av.y, wv.y, acc);
-            acc = mfma16x16x4(av.z, wv.z, acc);
-            acc = mfma16x16x4(av.w, wv.w, acc);
+        if constexpr (BF) {   // head weights rounded to bf16 here (fp32 master copy)
+            const uint16_t* hs = reinterpret_cast<const uint16_t*>(FBUF(cur)) + i * a.sh + 8 * g;
+            for (int ck = wid; ck < (F >> 5); ck += FW) {
+                const float4 w0 = ld4(hw + ck * 32 + 8 * g), w1 = ld4(hw + ck * 32 + 8 * g + 4);
+                u32x4 wv = {bf16_pack2(w0.x, w0.y), bf16_pack2(w0.z, w0.w), bf16_pack2(w1.x, w1.y), bf16_pack2(w1.z, w1.w)};
+                if (i >= a.NH) wv = u32x4{0u, 0u, 0u, 0u};
+                acc = mfma16x16x32bf16(*reinterpret_cast<const u32x4*>(hs + ck * 32), wv, acc);
+            }
+        } else {
+            const float* hs = FBUF(cur) + i * a.sh + 4 * g;
+            for (int ck = wid; ck < (F >> 4); ck += FW) {
+                float4 wv = ld4(hw + ck * 16 + 4 * g);
+                if (i >= a.NH) wv = make_float4(0.f, 0.f, 0.f, 0.f);
+                const float4 av = *reinterpret_cast<const float4*>(hs + ck * 16);
+                acc = mfma16x16x4(av.x, wv.x, acc);
+                acc = mfma16x16x4(av.y, wv.y, acc);
+                acc = mfma16x16x4(av.z, wv.z, acc);
+                acc = mfma16x16x4(av.w, wv.w, acc);
+            }
         }
         DQNX_STAMP(a.stamps, 36);
         float* part = FBUF(cur ^ 1);   // [FW][16 rows][16 outputs]
@@ -327,9 +369,12 @@ __global__ __launch_bounds__(FT) void k_mlp_fwd(FusedFwdArgs a) {
 // dZ_{l-1} = (dZ_l W_l) (.) act'(H_{l-1}): B[k][n] = W_l[k][n], read from the chain-blocked
 // copy of W_l (relayout.hpp, kind 1).
 // =====================================================================================
-constexpr int HB_SD = 264;   // LDS row stride of dZ tiles (width <= 256)
+constexpr int HB_SD = 264;   // LDS row stride of fp32 dZ tiles (width <= 256)
+constexpr int HB_SDH = 272;  // LDS row stride of bf16 dZ tiles (bf16 elements, 32 bytes mod 256)
 
-template <int ACT, int NL>
+// BF: the chain's dZ tiles are rounded to bf16 in LDS and multiplied by bf16 blocked weights
+// (fp32 accumulate); dZ_L = dHead W_head (K = 16) and every global dZ stay fp32.
+template <int ACT, int NL, bool BF>
 __global__ __launch_bounds__(FT) void k_head_bwd(HeadBwdArgs a) {
     __shared__ __attribute__((aligned(16))) float dzs[2][16 * HB_SD];
     __shared__ float dh[16][17];
@@ -360,7 +405,7 @@ __global__ __launch_bounds__(FT) void k_head_bwd(HeadBwdArgs a) {
         coff = (l == 1) ? part * np_ : 0;
         ldn = N;
         cw = wave_cols(np_);
-        stream_open(a.wblkT[l], N >> 4, K >> 4, coff >> 4, cw, ws, wb);
+        stream_open(a.wblkT[l], N >> 4, fwd_nch<BF>(K), coff >> 4, cw, ws, wb);
 #pragma unroll
         for (int t = 0; t < 2; t++)
 #pragma unroll
@@ -505,7 +550,8 @@ __global__ __launch_bounds__(FT) void k_head_bwd(HeadBwdArgs a) {
             for (int r = 0; r < 4; r++) {
                 const int rr = 4 * g + r;
                 const float v = act_bwd<ACT>(acc[r], hmask[t][r]);
-                dz[rr * HB_SD + col] = v;
+                if constexpr (BF) reinterpret_cast<uint16_t*>(dz)[rr * HB_SDH + col] = bf16_bits(v);
+                else dz[rr * HB_SD + col] = v;
                 if (lead && rr < nb) dzg[(int64_t)(b0 + rr) * F + col] = v;
             }
         }
@@ -519,7 +565,7 @@ __global__ __launch_bounds__(FT) void k_head_bwd(HeadBwdArgs a) {
         floatx4 acc[2];
         lds_barrier();   // dZ_l tile complete in LDS
         DQNX_STAMP(a.stamps, 46 + 3 * (L - 1 - l));
-        wave_mma(dzs[cur], HB_SD, fused_groups(a.out[l]), cw, ws, wb, acc);
+        wave_mma<BF>(dzs[cur], BF ? HB_SDH : HB_SD, fwd_groups<BF>(a.out[l]), cw, ws, wb, acc);
         DQNX_STAMP(a.stamps, 47 + 3 * (L - 1 - l));
         float* dz = dzs[cur ^ 1];
         float* dzg = a.dZ[l - 1];
@@ -532,7 +578,10 @@ __global__ __launch_bounds__(FT) void k_head_bwd(HeadBwdArgs a) {
             for (int r = 0; r < 4; r++) {
                 const int rr = 4 * g + r;
                 const float v = act_bwd<ACT>(acc[t][r], hm[t][r]);
-                dz[rr * HB_SD + col] = v;
+                if (l > 1) {   // the last level's tile feeds nothing
+                    if constexpr (BF) reinterpret_cast<uint16_t*>(dz)[rr * HB_SDH + col] = bf16_bits(v);
+                    else dz[rr * HB_SD + col] = v;
+                }
                 if (store && rr < nb) dzg[(int64_t)(b0 + rr) * ldn + coff + col] = v;
             }
         }
@@ -542,26 +591,38 @@ __global__ __launch_bounds__(FT) void k_head_bwd(HeadBwdArgs a) {
 }
 
 // ---- host side ------------------------------------------------------------------------
-bool fused_fwd_plan(FusedFwdArgs& a, int obs_dim) {
+bool fused_fwd_plan(FusedFwdArgs& a, int obs_dim, bool bf16) {
     if (a.L < 1 || a.L > FUSED_MAX_L || a.NH > 16) return false;
     for (int l = 0; l < a.L; l++)
         if (a.out[l] % 64 || a.out[l] > 256) return false;
     if (a.F != a.out[a.L - 1]) return false;
-    const int kz = fused_groups(obs_dim) * FPF * 16;
+    a.bf16 = bf16 ? 1 : 0;
+    const int kz = bf16 ? fwd_nch<true>(obs_dim) * 32 : fused_groups(obs_dim) * FPF * 16;
     if (16 * (kz / 4) > FGQ * FT) return false;   // gather slots
-    a.sx = fused_stride(kz);
     int wmax = 0;
     for (int l = 0; l < a.L; l++) wmax = a.out[l] > wmax ? a.out[l] : wmax;
-    a.sh = fused_stride(wmax);
-    int b0 = 16 * a.sx, b1 = 16 * a.sh;
-    if (b0 < 16 * a.sh) b0 = 16 * a.sh;
+    int t0, t1;   // tile sizes in floats
+    if (bf16) {   // rows cover every chunk of the last group; stride = 32 bytes mod 256
+        a.sx = fwd_groups<true>(obs_dim) * FPF * 32 + 16;
+        a.sh = ((wmax + 127) & ~127) + 16;
+        t0 = 8 * a.sx;
+        t1 = 8 * a.sh;
+    } else {
+        a.sx = fused_stride(kz);
+        a.sh = fused_stride(wmax);
+        t0 = 16 * a.sx;
+        t1 = 16 * a.sh;
+    }
+    int b0 = t0 > t1 ? t0 : t1, b1 = t1;
     if (b0 < FW * 256) b0 = FW * 256;
     if (b1 < FW * 256) b1 = FW * 256;
     a.buf0 = (b0 + 3) & ~3;
     a.buf1 = (b1 + 3) & ~3;
-    for (int l = 0; l < a.L; l++) a.kpad[l] = fused_groups(a.in[l]) * FPF * 16;
+    for (int l = 0; l < a.L; l++) a.kpad[l] = bf16 ? fwd_nch<true>(a.in[l]) * 32 : fused_groups(a.in[l]) * FPF * 16;
     return (a.buf0 + a.buf1) * 4 <= 64 * 1024;
 }
+
+int fused_wblk_bytes(bool bf16, int rows, int kpad) { return rows * kpad * (bf16 ? 2 : 4); }
 
 // Occupancy: a workgroup streams every weight of its stream at the MFMA rate of ONE CU, so two
 // workgroups sharing a CU (the dispatcher packs up to 4 of these onto one CU while others sit
@@ -584,8 +645,13 @@ int launch_fused_fwd(const FusedFwdArgs& a, int act, hipStream_t s) {
     if (shm < (size_t)DQNX_FUSED_LDS_MIN) shm = DQNX_FUSED_LDS_MIN;
 #define FUSED_FWD_CASE(ACTV, NLV)                                                                    \
     do {                                                                                             \
-        if (shm > 64 * 1024) allow_lds(k_mlp_fwd<ACTV, NLV>, 160 * 1024);                            \
-        hipLaunchKernelGGL((k_mlp_fwd<ACTV, NLV>), grid, block, shm, s, a);                          \
+        if (a.bf16) {                                                                                \
+            if (shm > 64 * 1024) allow_lds(k_mlp_fwd<ACTV, NLV, true>, 160 * 1024);                  \
+            hipLaunchKernelGGL((k_mlp_fwd<ACTV, NLV, true>), grid, block, shm, s, a);                \
+        } else {                                                                                     \
+            if (shm > 64 * 1024) allow_lds(k_mlp_fwd<ACTV, NLV, false>, 160 * 1024);                 \
+            hipLaunchKernelGGL((k_mlp_fwd<ACTV, NLV, false>), grid, block, shm, s, a);               \
+        }                                                                                            \
     } while (0)
     const bool relu = act == DQNX_ACT_RELU;
     switch (a.L) {
@@ -604,8 +670,13 @@ int launch_head_bwd(const HeadBwdArgs& a, int act, hipStream_t s) {
     const size_t pad = DQNX_HEAD_LDS_PAD;   // dynamic LDS on top of the static tiles (occupancy knob)
 #define HEAD_BWD_CASE(ACTV, NLV)                                                                     \
     do {                                                                                             \
-        if (pad > 64 * 1024) allow_lds(k_head_bwd<ACTV, NLV>, 120 * 1024);                           \
-        hipLaunchKernelGGL((k_head_bwd<ACTV, NLV>), grid, block, pad, s, a);                         \
+        if (a.bf16) {                                                                                \
+            if (pad > 64 * 1024) allow_lds(k_head_bwd<ACTV, NLV, true>, 120 * 1024);                 \
+            hipLaunchKernelGGL((k_head_bwd<ACTV, NLV, true>), grid, block, pad, s, a);               \
+        } else {                                                                                     \
+            if (pad > 64 * 1024) allow_lds(k_head_bwd<ACTV, NLV, false>, 120 * 1024);                \
+            hipLaunchKernelGGL((k_head_bwd<ACTV, NLV, false>), grid, block, pad, s, a);              \
+        }                                                                                            \
     } while (0)
     const bool relu = act == DQNX_ACT_RELU;
     switch (a.L) {

@@ -310,15 +310,17 @@ struct FusedFwdArgs {
     const int32_t* act;          // replay ring columns (gathered for `trans`)
     const float* rew;
     const float* done;
-    int sx, sh;                  // LDS row strides (floats) of the input tile / hidden tiles
+    int bf16;                    // DQNX_COMPUTE_BF16: bf16 LDS tiles, bf16 blocked weights, bf16 MFMA
+    int sx, sh;                  // LDS row strides (elements: floats, or bf16 under bf16) of the input / hidden tiles
     int buf0, buf1;              // LDS buffer sizes (floats)
-    int kpad[FUSED_MAX_L];       // layer inputs zero padded to a multiple of 64 (blocked copies)
+    int kpad[FUSED_MAX_L];       // layer inputs zero padded to kpad (blocked copies): fp32 a multiple of 64, bf16 of 32
     const float* wblk[2][FUSED_MAX_L];   // fragment-blocked W_l of the online / target net (relayout.hpp)
     int64_t* stamps;             // diagnostic builds (-DDQNX_STAMPS): slots 24..39
 };
 struct HeadBwdArgs {
     int L, Bl, A, NH, F, head_kind, algo;
     int nsplit;                  // workgroups per 16-sample tile (split the last dZ's columns)
+    int bf16;                    // DQNX_COMPUTE_BF16: dZ chain on bf16 operands (LDS tiles + wblkT)
     int in[FUSED_MAX_L], out[FUSED_MAX_L];
     int64_t woff[FUSED_MAX_L], head_off;
     float inv_bg, gamma;
@@ -369,7 +371,8 @@ struct DwSeamArgs {
 };
 int dw_seam_tiles(BwdArgs& b);   // fills the grids; returns the number of parameter tiles
 int launch_dw_seam(const DwSeamArgs& a, hipStream_t s);
-bool fused_fwd_plan(FusedFwdArgs& a, int obs_dim);   // fills sx/sh/buf sizes; false if unsupported
+bool fused_fwd_plan(FusedFwdArgs& a, int obs_dim, bool bf16);   // fills sx/sh/buf/kpad; false if unsupported
+int fused_wblk_bytes(bool bf16, int rows, int kpad);          // one blocked weight copy
 int launch_fused_fwd(const FusedFwdArgs& a, int act, hipStream_t s);
 int launch_head_bwd(const HeadBwdArgs& a, int act, hipStream_t s);
 

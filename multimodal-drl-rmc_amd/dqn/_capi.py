@@ -16,9 +16,11 @@ LIB_PATH = os.environ.get("DQNX_LIB") or os.path.join(_HERE, "_lib", "libdqnx.so
 
 # ---- constants (mirror dqnx.h) --------------------------------------------------------
 DQNX_OK = 0
+DQNX_EINVAL, DQNX_ESTATE, DQNX_EUNSUPPORTED, DQNX_EDEVICE = -1, -2, -3, -4
 DQNX_NET_MLP, DQNX_NET_TWO_STREAM = 0, 1
 DQNX_HEAD_LINEAR, DQNX_HEAD_DUELING = 0, 1
 DQNX_ACT_RELU, DQNX_ACT_ELU = 0, 1
+DQNX_COMPUTE_FP32, DQNX_COMPUTE_BF16 = 0, 1
 DQNX_ALGO_DQN, DQNX_ALGO_DOUBLE, DQNX_ALGO_PER_DOUBLE = 0, 1, 2
 DQNX_MAX_DENSE, DQNX_MAX_CONV = 6, 4
 (BUF_PARAMS, BUF_TARGET_PARAMS, BUF_GRADS, BUF_ADAM_M, BUF_ADAM_V, BUF_CTRL, BUF_RING_OBS,
@@ -59,6 +61,7 @@ class Config(ctypes.Structure):
         ("local_sampling", I32), ("per_eps", ctypes.c_double), ("per_alpha", ctypes.c_double),
         ("per_max_priority", ctypes.c_double), ("per_beta_start", ctypes.c_double),
         ("per_beta_end", ctypes.c_double), ("per_beta_steps", ctypes.c_double),
+        ("compute_dtype", I32), ("reserved1", I32),
     ]
 
 

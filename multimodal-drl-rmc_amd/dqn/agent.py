@@ -22,6 +22,7 @@ Both are handed to the engine before the step and taken back after it, so
 """
 from __future__ import annotations
 
+import os
 import random
 import time
 from collections import deque
@@ -115,7 +116,8 @@ class Agent:
                               dueling=cls is DuelingDeepQNetwork)
         self.engine = LearnEngine(spec, type(self).__name__, self.batch_size, self.buffer_size, gamma=self.gamma,
                                   lr=self.lr, tau=self.target_soft_update_tau, n_env=self.n_env, device=self.device,
-                                  eps_dec=self.epsilon_decay)
+                                  eps_dec=self.epsilon_decay,
+                                  compute_dtype=os.environ.get("DQNX_COMPUTE_DTYPE", "fp32"))
         self.online_network.bind_flat(self.engine.param_views(self.engine.params))
         self.target_network.bind_flat(self.engine.param_views(self.engine.target_params))
         self.replay_memory_buffer = self._make_replay()

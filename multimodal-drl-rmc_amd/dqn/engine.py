@@ -138,7 +138,7 @@ class LearnEngine:
 
     def __init__(self, spec: NetSpec, algo: str, batch: int, capacity: int, gamma=0.99, lr=1e-4,
                  tau=1e-3, n_env=1, world_size=1, rank=0, device=None, graphs=True, eps_dec=2e6,
-                 local_sampling=False):
+                 local_sampling=False, compute_dtype="fp32"):
         if not torch.cuda.is_available():
             raise RuntimeError("libdqnx needs a ROCm GPU (MI355X / gfx950); there is no CPU fallback")
         self.L = C.lib()
@@ -153,6 +153,10 @@ class LearnEngine:
         cfg.gamma, cfg.lr, cfg.tau, cfg.n_env = gamma, lr, tau, n_env
         cfg.per_beta_steps = eps_dec
         cfg.local_sampling = 1 if local_sampling else 0
+        if compute_dtype not in ("fp32", "bf16"):
+            raise ValueError(f"compute_dtype must be 'fp32' or 'bf16', got {compute_dtype!r}")
+        cfg.compute_dtype = C.DQNX_COMPUTE_BF16 if compute_dtype == "bf16" else C.DQNX_COMPUTE_FP32
+        self.compute_dtype = compute_dtype
         self.cfg = cfg
         h = ctypes.c_void_p()
         C.check(self.L.dqnx_engine_create(ctypes.byref(cfg), ctypes.byref(h)), "dqnx_engine_create")

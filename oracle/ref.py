@@ -214,12 +214,43 @@ def param_count(spec: NetSpec) -> int:
 # Forward (functional restatement of the module forwards)
 # ----------------------------------------------------------------------------------------
 
-def body_forward(spec: NetSpec, P, x: torch.Tensor) -> torch.Tensor:
+def bf16r(t: torch.Tensor) -> torch.Tensor:
+    """Round to bf16 (round to nearest even) and back to fp32."""
+    return t.to(torch.bfloat16).to(torch.float32)
+
+
+class _Bf16Linear(torch.autograd.Function):
+    """The engine's bf16 compute mode (include/dqnx.h DQNX_COMPUTE_BF16), restated: GEMM
+    operands rounded to bf16, products summed in fp32.  Not in the reference (fp32 only);
+    this is the checker for BASELINE config 5's bf16 variant.
+      y  = bf16(x) bf16(W)^T + b
+      dx = bf16(dy) bf16(W)   (dense layers >= 2: the engine's dZ chain)  /  dy W  (head)
+      dW = dy^T x, db = sum dy (fp32: the engine's weight-gradient kernel is fp32)"""
+
+    @staticmethod
+    def forward(ctx, x, W, b, round_dx):
+        ctx.save_for_backward(x, W)
+        ctx.round_dx = round_dx
+        return bf16r(x) @ bf16r(W).t() + b
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, W = ctx.saved_tensors
+        dx = bf16r(dy) @ bf16r(W) if ctx.round_dx else dy @ W
+        return dx, dy.t() @ x, dy.sum(0), None
+
+
+def _linear(x, W, b, bf16: bool, round_dx: bool = True):
+    return _Bf16Linear.apply(x, W, b, round_dx) if bf16 else F.linear(x, W, b)
+
+
+def body_forward(spec: NetSpec, P, x: torch.Tensor, bf16: bool = False) -> torch.Tensor:
     if spec.kind == "mlp":   # R:env/custom_env/macro with lane/dqn_config.py:76-84
         h = x
         for i in range(len(spec.hidden)):
-            h = torch.relu(F.linear(h, P[f"net.{2 * i}.weight"], P[f"net.{2 * i}.bias"]))
+            h = torch.relu(_linear(h, P[f"net.{2 * i}.weight"], P[f"net.{2 * i}.bias"], bf16))
         return h
+    assert not bf16, "bf16 compute is implemented for MLP networks only"
     # TwoStreamHybridNetwork.forward (R:env/dqn_config.py:118-143)
     L = spec.macro_len
     macro = x[:, :L]
@@ -234,13 +265,13 @@ def body_forward(spec: NetSpec, P, x: torch.Tensor) -> torch.Tensor:
     return h
 
 
-def q_forward(spec: NetSpec, P, x: torch.Tensor) -> torch.Tensor:
-    h = body_forward(spec, P, x)
+def q_forward(spec: NetSpec, P, x: torch.Tensor, bf16: bool = False) -> torch.Tensor:
+    h = body_forward(spec, P, x, bf16)
     if spec.head == "dueling":   # R:dqn/network.py:90-96 (aggregate :83)
-        val = F.linear(h, P["fc_val.weight"], P["fc_val.bias"])
-        adv = F.linear(h, P["fc_adv.weight"], P["fc_adv.bias"])
+        val = _linear(h, P["fc_val.weight"], P["fc_val.bias"], bf16, round_dx=False)
+        adv = _linear(h, P["fc_adv.weight"], P["fc_adv.bias"], bf16, round_dx=False)
         return torch.add(val, (adv - adv.mean(dim=1, keepdim=True)))
-    return F.linear(h, P["fc_out.weight"], P["fc_out.bias"])   # R:dqn/network.py:61-65
+    return _linear(h, P["fc_out.weight"], P["fc_out.bias"], bf16, round_dx=False)   # R:dqn/network.py:61-65
 
 
 def advantages(spec: NetSpec, P, x: torch.Tensor) -> torch.Tensor:
@@ -479,8 +510,10 @@ class OracleLearner:
 
     def __init__(self, spec: NetSpec, algo: str, batch_size: int, buffer_size: int,
                  lr=1e-4, gamma=0.99, tau=1e-3, n_env=1, soft_update=True,
-                 update_target_frequency=30000, eps_dec=2e6, seed=0, params=None, per_pow="numpy"):
-        assert algo in ALGOS
+                 update_target_frequency=30000, eps_dec=2e6, seed=0, params=None, per_pow="numpy",
+                 compute="fp32"):
+        assert algo in ALGOS and compute in ("fp32", "bf16")
+        self.bf16 = compute == "bf16"
         self.spec, self.algo = spec, algo
         self.batch_size, self.buffer_size = batch_size, buffer_size
         self.lr, self.gamma, self.tau, self.n_env = lr, gamma, tau, n_env
@@ -504,7 +537,7 @@ class OracleLearner:
         return list(self.replay.store_transitions(obses, actions, rews, dones, new_obses))
 
     def _q(self, P, x):
-        return q_forward(self.spec, P, x)
+        return q_forward(self.spec, P, x, self.bf16)
 
     def learn(self, shard: Optional[Tuple[int, int]] = None) -> StepRecord:
         """Agent.learn.  With shard=(b0, b1) (data-parallel restatement) the loss

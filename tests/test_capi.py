@@ -112,3 +112,25 @@ def test_engine_create_without_gpu_fails_loudly():
     from dqn import engine as E
     with pytest.raises(RuntimeError):
         E.LearnEngine(E.mlp_spec(14, 8, "dueling"), "DuelingDoubleDQNAgent", 32, 500)
+
+
+def _create(spec, dtype):
+    cfg = C.Config()
+    cfg.net = spec.to_c()
+    C.lib().dqnx_config_defaults(ctypes.byref(cfg))
+    cfg.batch, cfg.capacity = 64, 1000
+    cfg.compute_dtype = dtype
+    h = ctypes.c_void_p()
+    rc = C.lib().dqnx_engine_create(ctypes.byref(cfg), ctypes.byref(h))
+    if rc == 0:
+        C.lib().dqnx_engine_destroy(h)
+    return rc
+
+
+def test_bf16_compute_is_mlp_only():
+    """bf16 lives in the fused MLP kernels; other nets and unknown dtypes are refused at create."""
+    from dqn import engine as E
+    assert _create(E.mlp_spec(284, 8, "dueling"), C.DQNX_COMPUTE_BF16) == 0
+    assert _create(E.mlp_spec(14, 8, "linear"), C.DQNX_COMPUTE_BF16) == 0
+    assert _create(_engine_spec(O.hybrid_spec(8, "dueling")), C.DQNX_COMPUTE_BF16) == C.DQNX_EUNSUPPORTED
+    assert _create(E.mlp_spec(284, 8, "dueling"), 7) == C.DQNX_EINVAL

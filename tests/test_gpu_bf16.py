@@ -1,0 +1,176 @@
+"""GPU parity of the bf16 compute mode (BASELINE config 5: PER + Double/Dueling, bf16 compute).
+
+Two checkers, two tolerances:
+  * the oracle in bf16 emulation (oracle/ref.py _Bf16Linear: GEMM operands rounded to bf16,
+    fp32 sums) -- the same arithmetic up to summation order, so the engine must agree to
+    fp32-accumulation noise plus the occasional one-ulp bf16 rounding flip that noise causes;
+  * the reference's own fp32 arithmetic (the plain oracle) -- the error the bf16 mode costs,
+    bounded by a stated relative tolerance ("bf16 numerics get a looser
+    stated tolerance against the fp32 oracle").
+Sampling (CPython MT19937 / numpy legacy uniform + SumTree descent) is not affected by the
+compute dtype and stays bit-exact.
+"""
+import random
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import ref as O
+
+pytestmark = pytest.mark.gpu
+
+# engine vs bf16-emulating oracle.  Summation order differs (fp32 noise, ~1e-7 here); where
+# that noise moves a value across a bf16 rounding boundary, the operand downstream differs by
+# one bf16 ulp (2^-8 relative).  So: nearly every element within Q_TIGHT, the rest (flip
+# descendants, at most Q_FLIP_FRAC of them) within Q_ATOL.
+Q_TIGHT = 2e-6
+Q_FLIP_FRAC = 2e-3
+Q_ATOL = 1e-3          # Q values, targets
+LOSS_RTOL = 1e-4
+GRAD_TOL = 2e-3        # max |dg| / max |g| per tensor
+W_ATOL = 2e-5          # weights after Adam (one lr = 1e-4 is the size of a sign flip)
+# engine vs the reference's fp32 arithmetic: stated bf16 error bound
+Q_REL_FP32 = 2e-2      # max |dQ| / max |Q|
+GRAD_REL_FP32 = 5e-2   # max |dg| / max |g| per tensor
+
+
+def _E():
+    from dqn import engine as E
+    return E
+
+
+def make_bf16_pair(algo, obs_dim, batch, capacity, n_fill, seed, per=False, graphs=True):
+    E = _E()
+    head = O.algo_spec_head(algo)
+    ospec = O.mlp_spec(obs_dim, 8, head)
+    init = O.reference_init(ospec, seed)
+    kw = dict(seed=seed, params=init)
+    if per:
+        kw["per_pow"] = "cr"
+    emu = O.OracleLearner(ospec, algo, batch, capacity, compute="bf16", **kw)
+    ref = O.OracleLearner(ospec, algo, batch, capacity, **kw)
+    data = O.synth_transitions(n_fill, obs_dim, 8, seed=seed + 100)
+    O.fill_replay(emu, *data)
+    O.fill_replay(ref, *data)
+    eng = E.LearnEngine(E.mlp_spec(obs_dim, 8, head), algo, batch, capacity, compute_dtype="bf16", graphs=graphs)
+    eng.load_params(init)
+    eng.push(*data)
+    if per:
+        np.random.seed(seed + 11)
+        st = O.np_state_to_array()
+        emu.np_state, ref.np_state = st.copy(), st.copy()
+        eng.set_rng(1, st)
+    else:
+        random.seed(seed + 7)
+        st = O.py_state_to_array()
+        emu.py_state, ref.py_state = st.copy(), st.copy()
+        eng.set_rng(0, st)
+    return emu, ref, eng
+
+
+def _rel(a, b):
+    return float(np.abs(a - b).max() / max(np.abs(b).max(), 1e-30))
+
+
+def _close(got, want, what):
+    d = np.abs(np.asarray(got, np.float64) - np.asarray(want, np.float64))
+    frac = float((d > Q_TIGHT).mean())
+    assert d.max() <= Q_ATOL and frac <= Q_FLIP_FRAC, (what, float(d.max()), frac)
+    return float(d.max()), frac
+
+
+def _check_step(eng, rec, rec32, step, cap=None):
+    if cap is None:
+        idx = eng.batch_idx.cpu().numpy().astype(np.int64)
+    else:
+        idx = eng.batch_idx.cpu().numpy().astype(np.int64) + cap - 1
+    assert np.array_equal(idx, rec.positions), f"step {step}: sampled indices differ"
+    q = eng.q.cpu().numpy()
+    dq = _close(q[0], rec.q_online.numpy(), "Q(s)")
+    _close(q[2], rec.q_target_next.numpy(), "Qtarget(s')")
+    if rec.q_online_next is not None:
+        _close(q[1], rec.q_online_next.numpy(), "Q(s')")
+    _close(eng.td[0].cpu().numpy(), rec.targets.view(-1).numpy(), "y")
+    assert abs(eng.loss() - rec.loss) <= LOSS_RTOL * max(1.0, abs(rec.loss))
+    g = eng.param_views(eng.grads[:-1])
+    worst = {}
+    for k, r in rec.grads.items():
+        worst[k] = _rel(g[k].cpu().numpy(), r.numpy())
+        assert worst[k] <= GRAD_TOL, (k, worst[k])
+    print(f"step {step}: vs emu: max|dQ| {dq[0]:.2e} ({dq[1]:.1e} beyond fp32 noise), grad rel {max(worst.values()):.2e}")
+    if rec32 is not None:   # bf16 error against the reference's fp32 arithmetic
+        assert np.array_equal(rec32.positions, rec.positions)
+        qr = _rel(q[0], rec32.q_online.numpy())
+        assert qr <= Q_REL_FP32, qr
+        gr = max(_rel(g[k].cpu().numpy(), r.numpy()) for k, r in rec32.grads.items())
+        assert gr <= GRAD_REL_FP32, gr
+        print(f"step {step}: vs fp32 reference: Q rel {qr:.2e}, grad rel {gr:.2e}")
+
+
+def _compare_weights(emu, eng):
+    views = {"online": eng.param_views(eng.params), "target": eng.param_views(eng.target_params)}
+    for nm, src in (("online", emu.online), ("target", emu.target)):
+        for k, r in src.items():
+            d = float((views[nm][k].detach().cpu() - r).abs().max())
+            assert d <= W_ATOL, (nm, k, d)
+
+
+@pytest.mark.parametrize("algo,obs_dim,batch,capacity,n_fill,seed", [
+    ("DQNAgent", 14, 32, 500, 300, 3),
+    ("DoubleDQNAgent", 284, 100, 700, 650, 8),              # ragged last tile
+    ("DuelingDoubleDQNAgent", 284, 1024, 20000, 20000, 7),
+    ("DuelingDoubleDQNAgent", 284, 8192, 40000, 40000, 9),  # config 5's batch
+])
+def test_gpu_bf16_learn_matches_bf16_oracle(algo, obs_dim, batch, capacity, n_fill, seed):
+    emu, ref, eng = make_bf16_pair(algo, obs_dim, batch, capacity, n_fill, seed)
+    for step in range(3):
+        rec = emu.train_step()
+        eng.learn_step(soft_update=True)
+        torch.cuda.synchronize()
+        eng.check_device_error()
+        _check_step(eng, rec, None, step)
+        _compare_weights(emu, eng)
+    assert np.array_equal(eng.get_rng(0), emu.py_state)
+
+
+@pytest.mark.parametrize("algo,obs_dim,batch,capacity,n_fill,seed", [
+    ("DuelingDoubleDQNAgent", 284, 1024, 20000, 20000, 17),
+    ("DQNAgent", 284, 256, 3000, 3000, 18),
+])
+def test_gpu_bf16_error_vs_fp32_reference(algo, obs_dim, batch, capacity, n_fill, seed):
+    """One step from identical state: the bf16 engine against the reference's fp32 learn step."""
+    emu, ref, eng = make_bf16_pair(algo, obs_dim, batch, capacity, n_fill, seed)
+    rec = emu.train_step()
+    rec32 = ref.train_step()
+    eng.learn_step(soft_update=True)
+    torch.cuda.synchronize()
+    _check_step(eng, rec, rec32, 0)
+
+
+@pytest.mark.parametrize("obs_dim,batch,cap,n_fill,seed", [
+    (14, 32, 500, 300, 3),
+    (284, 1024, 20000, 20000, 5),
+])
+def test_gpu_bf16_per_learn_matches_bf16_oracle(obs_dim, batch, cap, n_fill, seed):
+    """Config 5's algorithm: PER + Dueling Double DQN in bf16 (tree sampling bit-exact)."""
+    emu, ref, eng = make_bf16_pair("PerDuelingDoubleDQNAgent", obs_dim, batch, cap, n_fill, seed, per=True)
+    rec = emu.train_step()
+    eng.learn_step(soft_update=True)
+    torch.cuda.synchronize()
+    eng.check_device_error()
+    _check_step(eng, rec, None, 0, cap=cap)
+    np.testing.assert_allclose(eng.is_weights.cpu().numpy(), rec.is_weights.astype(np.float32), rtol=2e-7)
+    _close(eng.per_abs_td.cpu().numpy(), rec.abs_td.reshape(-1), "|delta|")
+    _compare_weights(emu, eng)
+
+
+def test_gpu_bf16_graph_and_eager_identical():
+    outs = []
+    for graphs in (True, False):
+        _, _, eng = make_bf16_pair("DuelingDoubleDQNAgent", 284, 512, 4000, 4000, 11, graphs=graphs)
+        for _ in range(3):
+            eng.learn_step(soft_update=True)
+        torch.cuda.synchronize()
+        outs.append(eng.params.clone())
+    assert torch.equal(outs[0], outs[1])

@@ -136,3 +136,40 @@ def test_oracle_learn_golden(path):
                 got = got[::stride]
             tol = 1e-5 if nm in ("online", "target") else 1e-6
             np.testing.assert_allclose(got, ref, atol=tol, rtol=0, err_msg=f"{nm} {k}")
+
+
+def test_bf16_emulation_linear_matches_explicit_formula():
+    """oracle bf16 mode: y = bf16(x) bf16(W)^T + b; dx = bf16(dy) bf16(W) (or dy W); dW = dy^T x."""
+    g = torch.Generator().manual_seed(0)
+    x = torch.randn(7, 37, generator=g, requires_grad=True)
+    W = torch.randn(11, 37, generator=g, requires_grad=True)
+    b = torch.randn(11, generator=g, requires_grad=True)
+    dy = torch.randn(7, 11, generator=g)
+    for round_dx in (True, False):
+        y = O._Bf16Linear.apply(x, W, b, round_dx)
+        bx, bW = O.bf16r(x.detach()), O.bf16r(W.detach())
+        assert torch.allclose(y, bx @ bW.t() + b, atol=0, rtol=0)
+        gx, gW, gb = torch.autograd.grad(y, (x, W, b), dy)
+        want_dx = O.bf16r(dy) @ bW if round_dx else dy @ W.detach()
+        assert torch.equal(gx, want_dx)
+        assert torch.equal(gW, dy.t() @ x.detach())
+        assert torch.equal(gb, dy.sum(0))
+    # bf16 rounding is round-to-nearest-even on the 16 dropped bits
+    v = torch.tensor([1.0 + 2 ** -8, 1.0 + 3 * 2 ** -8, 1.0 + 2 ** -8 + 2 ** -20])
+    assert O.bf16r(v).tolist() == [1.0, 1.0 + 2 ** -6, 1.0 + 2 ** -7]
+
+
+def test_bf16_oracle_learn_close_to_fp32():
+    spec = O.mlp_spec(284, 8, "dueling")
+    init = O.reference_init(spec, 3)
+    data = O.synth_transitions(600, 284, 8, seed=5)
+    recs = []
+    for compute in ("fp32", "bf16"):
+        lr = O.OracleLearner(spec, "DuelingDoubleDQNAgent", 64, 1000, seed=3, params=init, compute=compute)
+        O.fill_replay(lr, *data)
+        lr.py_state = O.py_state_to_array(random.Random(9).getstate())
+        recs.append(lr.train_step())
+    a, b = recs
+    assert np.array_equal(a.positions, b.positions)
+    qa, qb = a.q_online.numpy(), b.q_online.numpy()
+    assert 0 < np.abs(qa - qb).max() <= 2e-2 * np.abs(qa).max()
