@@ -171,7 +171,7 @@ struct dqnx_engine {
     uint64_t total = 0;
     // workspace sub-regions (byte offsets from the arena base)
     uint64_t ws_phys = 0, ws_pool = 0, ws_xobs = 0, ws_head_part = 0, ws_loss_part = 0, ws_stage = 0;
-    uint64_t ws_adam_tab = 0, ws_stamps = 0, ws_dhead = 0, ws_raw = 0, ws_trans = 0, ws_tickets = 0;
+    uint64_t ws_adam_tab = 0, ws_stamps = 0, ws_dhead = 0, ws_raw = 0, ws_trans = 0, ws_tickets = 0, ws_per_ticket = 0, ws_per_wl = 0, ws_per_wp = 0, ws_per_winit = 0, ws_per_last = 0;
     int64_t n_tickets = 0;
     // fused plan: fragment-blocked weight copies [online fwd | target fwd | online chain] per layer
     uint64_t ws_wblk[2][FUSED_MAX_L] = {{0}}, ws_wblkT[FUSED_MAX_L] = {0};
@@ -286,6 +286,13 @@ int layout(dqnx_engine* e) {
     }
     e->ws_adam_tab = sub((uint64_t)kAdamTable * 2 * 4);
     e->ws_stamps = sub(64 * 8);
+    e->ws_per_ticket = sub(64);   // k_per_sample arrival counter (zero between launches); [16]: PER chunk epoch
+    if (c.algo == DQNX_ALGO_PER_DOUBLE) {   // k_per_prep / k_per_update / k_per_prop hand-offs
+        e->ws_per_wl = sub((uint64_t)PER_CHUNK * 4);
+        e->ws_per_wp = sub((uint64_t)PER_CHUNK * 4);
+        e->ws_per_winit = sub((uint64_t)PER_CHUNK * 8);
+        e->ws_per_last = sub((uint64_t)c.capacity * 8);
+    }
     e->ws_loss_part = sub((uint64_t)e->tiles * 4);
     e->stage_rows = 1024;
     e->ws_stage = sub((uint64_t)e->stage_rows * (2 * (uint64_t)c.net.obs_dim + 3) * 4 + 256);
@@ -344,6 +351,8 @@ PerSampleArgs per_sample_args(dqnx_engine* e, int32_t* idx, int32_t* phys) {
     pa.beta_end = c.per_beta_end;
     pa.beta_steps = c.per_beta_steps;
     pa.n_env = c.n_env;
+    pa.stamps = at<int64_t>(e, e->ws_stamps);
+    pa.ticket = at<int32_t>(e, e->ws_per_ticket);
     return pa;
 }
 
@@ -357,6 +366,12 @@ PerUpdateArgs per_update_args(dqnx_engine* e) {
     ua.eps = (float)c.per_eps;
     ua.alpha = (float)c.per_alpha;
     ua.pmax = (float)c.per_max_priority;
+    ua.stamps = at<int64_t>(e, e->ws_stamps);
+    ua.wl = at<int32_t>(e, e->ws_per_wl);
+    ua.wp = at<float>(e, e->ws_per_wp);
+    ua.winit = at<double>(e, e->ws_per_winit);
+    ua.last = at<uint64_t>(e, e->ws_per_last);
+    ua.epoch = at<uint32_t>(e, e->ws_per_ticket) + 16;
     return ua;
 }
 

@@ -218,7 +218,7 @@ struct SampleArgs {
 
 // PER sampling: ReplayMemoryPrioritized.sample_transitions (R:dqn/replay_memory.py:69-92)
 constexpr int PER_MAX_B = 8192;     // largest global minibatch k_per_sample handles
-constexpr int PER_CHUNK = 4096;     // priority updates per k_per_update launch
+constexpr int PER_CHUNK = 8192;     // priority updates per k_per_update launch
 struct PerSampleArgs {
     const double* tree;       // [2*cap-1] SumTree (R:dqn/utils/sum_tree.py)
     int64_t cap;
@@ -232,6 +232,8 @@ struct PerSampleArgs {
     int32_t n_env;
     RelayoutArgs rl;          // fused plan: blocked weight copies, built by blocks 1.. of the launch
     int rl_blocks;
+    int64_t* stamps;          // diagnostic builds (-DDQNX_STAMPS): slots 0..7
+    int32_t* ticket;          // arrival counter of the sampling workgroups, zero between launches
 };
 
 // PER priority writes with SumTree.update's sequential semantics (R:dqn/utils/sum_tree.py:15-32):
@@ -247,6 +249,13 @@ struct PerUpdateArgs {
     const float* abs_td;      // mode 0: [n] |targets - q(s,a)|
     int64_t wptr, size;       // mode 1: ring write pointer / size before this chunk (mode 0 reads ctrl)
     float eps, alpha, pmax;   // numpy float32 arithmetic on the python-float constants
+    int64_t* stamps;          // diagnostic builds (-DDQNX_STAMPS): slots 56..63
+    // workspace shared by the three launches of one chunk (k_per_prep, k_per_update, k_per_prop)
+    int32_t* wl;              // [PER_CHUNK] leaf (tree index) of item i
+    float* wp;                // [PER_CHUNK] its new priority
+    double* winit;            // [PER_CHUNK] the leaf's value before the chunk
+    uint64_t* last;           // [cap] (epoch << 32 | i) of the latest item writing the slot
+    uint32_t* epoch;          // chunk counter (tags `last`; zero after reset, like `last`)
 };
 
 // ---- two-stream hybrid network data movement (conv.hip) ----

@@ -20,49 +20,101 @@
 namespace dqnx {
 
 constexpr int PER_NT = 1024;
-constexpr int PER_TOP = 2047;            // nodes of depth <= 10, cached / accumulated in LDS
+constexpr int PER_TOP = 2047;            // nodes of depth <= 10, accumulated in LDS by k_per_update
 constexpr int PER_IPT = PER_CHUNK / PER_NT;
-constexpr int PER_HS = 2 * PER_CHUNK;    // leaf hash slots
 
 // ---------------------------------------------------------------------------------------
 // sample_transitions (R:dqn/replay_memory.py:69-92): stratified proportional sampling.
-// One workgroup: the 2*Bg MT19937 words numpy's legacy uniform consumes are generated
-// block-parallel (twist in LDS), then every sample descends the tree independently.
+// ceil(Bg / PER_SNT) workgroups, one sample per thread.  Every workgroup reads the numpy
+// MT19937 state and walks the same sequence of twists (block-parallel, in LDS) up to the
+// last of the 2*Bg words the legacy uniforms consume, tempering only the words of its own
+// samples; the last workgroup to arrive at the ticket (so every other one has read the old
+// state) writes the advanced state back.  The descent (get_leaf) reads the top PER_STOP
+// nodes from LDS and the rest PER_LA levels per global round trip.
 // ---------------------------------------------------------------------------------------
-__global__ __launch_bounds__(PER_NT) void k_per_sample(PerSampleArgs a) {
-    __shared__ uint32_t words[2 * PER_MAX_B];
-    __shared__ double top[PER_TOP];
-    __shared__ uint32_t mt[624], tmp[624];
-    if (blockIdx.x > 0) {   // spare workgroups: blocked weight copies for the fused plan
-        relayout_run(a.rl, blockIdx.x - 1, gridDim.x - 1);
+constexpr int PER_SNT = 256;     // samples (threads) per sampling workgroup: the descents' scattered
+                                 // loads are texture-path bound, so spread them over more CUs
+constexpr int PER_STOP = 8191;   // nodes of depth <= 12 (64 KiB of float64) cached per workgroup
+constexpr int PER_LA = 4;        // tree levels fetched per dependent global round trip
+
+// the chosen subtree's half of the first N nodes of a level fetched ahead:
+// x[0 .. N/2) = r ? x[N/2 .. N) : x[0 .. N/2)
+template <int N, int M>
+__device__ __forceinline__ void per_narrow(double (&x)[M], bool r) {
+    static_assert(N <= M, "narrow within the fetched level");
+#pragma unroll
+    for (int j = 0; j < N / 2; j++) x[j] = r ? x[j + N / 2] : x[j];
+}
+
+__global__ __launch_bounds__(PER_SNT) void k_per_sample(PerSampleArgs a) {
+    __shared__ double top[PER_STOP];
+    __shared__ uint32_t mtb[2][624];
+    __shared__ uint32_t words[2 * PER_SNT];
+    __shared__ int64_t s_step;
+    __shared__ uint32_t s_pos;
+    __shared__ int s_last;
+    const int G = (a.Bg + PER_SNT - 1) / PER_SNT;
+    if ((int)blockIdx.x >= G) {   // spare workgroups: blocked weight copies for the fused plan
+        relayout_run(a.rl, blockIdx.x - G, gridDim.x - G);
         return;
     }
-    const int tid = threadIdx.x;
+    const int tid = threadIdx.x, grp = blockIdx.x;
+    DQNX_STAMP(a.stamps, 0);
     const int64_t len = 2 * a.cap - 1;
     const double total = a.tree[0];                        // SumTree.total_priority
-    if (!(total > 0.0)) {
-        if (tid == 0) atomicExch(&a.ctrl->error, DQNX_DEVERR_EMPTY_TREE);
+    if (!(total > 0.0)) {   // every workgroup sees it: nobody arrives, the state stays untouched
+        if (grp == 0 && tid == 0) atomicExch(&a.ctrl->error, DQNX_DEVERR_EMPTY_TREE);
         return;
     }
-    const int64_t step = a.ctrl->agent_step;
     const int64_t size = a.ctrl->ring_size;
     const int64_t min_idx = a.ctrl->per_min_idx;
-    for (int i = tid; i < PER_TOP && i < len; i += PER_NT) top[i] = a.tree[i];
-    if (tid < 624) mt[tid] = a.ctrl->np_mt[tid];
-    uint32_t pos = a.ctrl->np_mt[624];
-    __syncthreads();
+    {   // every load in flight before the first LDS write (a plain loop waits on each one)
+        constexpr int NQ = (PER_STOP + 2 * PER_SNT - 1) / (2 * PER_SNT);
+        double2 tv[NQ];
+#pragma unroll
+        for (int q = 0; q < NQ; q++) {
+            const int j = 2 * (tid + q * PER_SNT);
+            // len is odd: a pair is whole, or only its first node exists (j = len - 1), or none
+            tv[q] = j + 1 < len ? *reinterpret_cast<const double2*>(a.tree + j)
+                                : make_double2(j < len ? a.tree[j] : 0.0, 0.0);
+        }
+        for (int j = tid; j < 624; j += PER_SNT) mtb[0][j] = a.ctrl->np_mt[j];
+#pragma unroll
+        for (int q = 0; q < NQ; q++) {
+            const int j = 2 * (tid + q * PER_SNT);
+            if (j < PER_STOP) top[j] = tv[q].x;
+            if (j + 1 < PER_STOP) top[j + 1] = tv[q].y;
+        }
+    }
+    if (tid == 0) {
+        s_pos = a.ctrl->np_mt[624];
+        s_step = a.ctrl->agent_step;
+    }
+    const double prob_min = a.tree[min_idx] / total;
+    __syncthreads();   // the fields written back below are in LDS now
+    if (tid == 0) {
+        __threadfence();
+        s_last = atomicAdd(a.ticket, 1) == G - 1;
+    }
+    const int64_t step = s_step;
+    uint32_t pos = s_pos;
+    DQNX_STAMP(a.stamps, 1);
 
     // the words of np.random.uniform calls i = 0..Bg-1: legacy double = 2 words each
     const int W = 2 * a.Bg;
+    const int w0 = 2 * grp * PER_SNT, w1 = min(W, w0 + 2 * PER_SNT);
     bool twisted = false;
+    int cur = 0;
     for (int done = 0; done < W;) {
         if (pos >= 624) {
-            mt_twist_block(mt, tmp);
+            mt_twist_into(mtb[cur], mtb[cur ^ 1]);   // ends with a barrier
+            cur ^= 1;
             pos = 0;
             twisted = true;
         }
         const int take = min(624 - (int)pos, W - done);
-        if (tid < take) words[done + tid] = mt_temper(mt[pos + tid]);
+        const int lo = max(done, w0), hi = min(done + take, w1);
+        for (int w = lo + tid; w < hi; w += PER_SNT) words[w - w0] = mt_temper(mtb[cur][pos + (w - done)]);
         done += take;
         pos += (uint32_t)take;
     }
@@ -77,88 +129,143 @@ __global__ __launch_bounds__(PER_NT) void k_per_sample(PerSampleArgs a) {
         beta = slope * (x - 0.0) + a.beta_start;
     }
     const double seg = total / (double)a.Bg;               // priority_segment
-    const double prob_min = a.tree[min_idx] / total;
     const double max_w = pow((double)size * prob_min, -beta);
     __syncthreads();
+    DQNX_STAMP(a.stamps, 2);
 
-    for (int i = tid; i < a.Bg; i += PER_NT) {
+    const int i = grp * PER_SNT + tid;
+    if (i < a.Bg) {
         // legacy_double: (a >> 5, b >> 6) -> [0, 1); uniform = low + (high - low) * u
-        const uint32_t wa = words[2 * i] >> 5, wb = words[2 * i + 1] >> 6;
+        const uint32_t wa = words[2 * tid] >> 5, wb = words[2 * tid + 1] >> 6;
         const double u = ((double)wa * 67108864.0 + (double)wb) / 9007199254740992.0;
         const double low = seg * (double)i, high = seg * (double)(i + 1);
         double v = low + (high - low) * u;
-        // get_leaf (R:dqn/utils/sum_tree.py:42-61)
-        int64_t parent = 0, leaf;
+        // get_leaf (R:dqn/utils/sum_tree.py:42-61): the same comparisons, node by node
+        int64_t p = 0, leaf = -1;
+        double pval = top[0];
         while (true) {
-            const int64_t left = 2 * parent + 1;
-            if (left >= len) {
-                leaf = parent;
-                break;
-            }
-            const double tl = left < PER_TOP ? top[left] : a.tree[left];
-            if (v <= tl) {
-                parent = left;
-            } else {
-                v -= tl;
-                parent = left + 1;
-            }
+            const int64_t left = 2 * p + 1;
+            if (left >= len) { leaf = p; break; }
+            if (left + 1 >= PER_STOP) break;
+            const double tl = top[left];
+            if (v <= tl) { p = left; pval = tl; }
+            else { v -= tl; p = left + 1; pval = top[left + 1]; }
         }
-        const double p = leaf < PER_TOP ? top[leaf] : a.tree[leaf];
-        const double prob = p / total;
+        while (leaf < 0) {
+            // the 2 + 4 + 8 + 16 nodes of the next PER_LA levels under p, in one round trip
+            double l1[2], l2[4], l3[8], l4[16];
+            const int64_t b1 = 2 * p + 1, b2 = 4 * p + 3, b3 = 8 * p + 7, b4 = 16 * p + 15;
+            // 16-byte loads (a level's nodes are contiguous); past the end of the tree a pair
+            // is clamped to the last two nodes (those values are never compared)
+            auto ld2 = [&](int64_t n, double* d) {
+                const double2 v = *reinterpret_cast<const double2*>(a.tree + (n + 1 < len ? n : len - 2));
+                d[0] = v.x;
+                d[1] = v.y;
+            };
+            if (len < 2) break;   // unreachable: a one-node tree is a leaf at the root
+#pragma unroll
+            for (int j = 0; j < 2; j += 2) ld2(b1 + j, l1 + j);
+#pragma unroll
+            for (int j = 0; j < 4; j += 2) ld2(b2 + j, l2 + j);
+#pragma unroll
+            for (int j = 0; j < 8; j += 2) ld2(b3 + j, l3 + j);
+#pragma unroll
+            for (int j = 0; j < 16; j += 2) ld2(b4 + j, l4 + j);
+            // one level: the children of p are c[0], c[1]; the deeper levels keep the chosen half
+            auto level = [&](const double* c) {
+                const int64_t left = 2 * p + 1;
+                if (left >= len) { leaf = p; return false; }
+                const bool r = !(v <= c[0]);
+                if (r) v -= c[0];
+                pval = r ? c[1] : c[0];
+                p = left + (r ? 1 : 0);
+                return r;
+            };
+            bool r;
+            do {
+                r = level(l1); if (leaf >= 0) break;
+                per_narrow<4>(l2, r); per_narrow<8>(l3, r); per_narrow<16>(l4, r);
+                r = level(l2); if (leaf >= 0) break;
+                per_narrow<4>(l3, r); per_narrow<8>(l4, r);
+                r = level(l3); if (leaf >= 0) break;
+                per_narrow<4>(l4, r);
+                level(l4);
+            } while (0);
+        }
+        const double prob = pval / total;
         const double w = pow((double)size * prob, -beta) / max_w;
         a.isw[i] = (float)w;
         const int32_t di = (int32_t)(leaf - (a.cap - 1));
         a.out_idx[i] = di;
         if (a.phys_out && i >= a.shard_begin && i < a.shard_begin + a.shard_len) a.phys_out[i - a.shard_begin] = di;
     }
-    __syncthreads();
-    if (twisted && tid < 624) a.ctrl->np_mt[tid] = mt[tid];
-    if (tid == 0) {
-        a.ctrl->np_mt[624] = pos;
-        a.ctrl->per_beta = beta;
-        a.ctrl->agent_step = step + a.n_env;   // the caller's agent.step advances once per learn
+    DQNX_STAMP(a.stamps, 3);
+    if (s_last) {   // every other workgroup has read the old state: write the advanced one
+        if (twisted)
+            for (int j = tid; j < 624; j += PER_SNT) a.ctrl->np_mt[j] = mtb[cur][j];
+        if (tid == 0) {
+            a.ctrl->np_mt[624] = pos;
+            a.ctrl->per_beta = beta;
+            a.ctrl->agent_step = step + a.n_env;   // the caller's agent.step advances once per learn
+            *a.ticket = 0;
+        }
     }
 }
 
 // ---------------------------------------------------------------------------------------
 // block scan / reduce helpers (1024 threads = 16 waves)
 // ---------------------------------------------------------------------------------------
-struct OpMaxF { __device__ float operator()(float x, float y) const { return fmaxf(x, y); } };
-struct OpMinF { __device__ float operator()(float x, float y) const { return fminf(x, y); } };
-struct OpMaxI { __device__ int operator()(int x, int y) const { return x > y ? x : y; } };
-struct OpMinI { __device__ int operator()(int x, int y) const { return x < y ? x : y; } };
+constexpr int PER_NW = PER_NT / 64;
 
-// exclusive scan over threads (thread order); every thread must call; sh: >= 16 entries
-template <class T, class Op>
-__device__ T block_exclusive(T v, T ident, Op op, T* sh) {
+// running max / min priority and the latest index at which each was (re)taken, scanned
+// together: one pair of barriers for all four
+struct Track {
+    float mx, mn;
+    int lx, ln;
+};
+__device__ __forceinline__ Track track_op(const Track& a, const Track& b) {
+    return Track{fmaxf(a.mx, b.mx), fminf(a.mn, b.mn), a.lx > b.lx ? a.lx : b.lx, a.ln > b.ln ? a.ln : b.ln};
+}
+__device__ __forceinline__ Track track_shfl_up(const Track& t, int d) {
+    return Track{__shfl_up(t.mx, d, 64), __shfl_up(t.mn, d, 64), __shfl_up(t.lx, d, 64), __shfl_up(t.ln, d, 64)};
+}
+// exclusive scan over threads (thread order) and the block total; every thread must call
+__device__ Track track_scan(const Track& v, Track* sh, Track* total) {
+    const Track ident{-INFINITY, INFINITY, -1, -1};
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    T x = v;
+    Track x = v;
 #pragma unroll
     for (int d = 1; d < 64; d <<= 1) {
-        const T y = __shfl_up(x, d, 64);
-        if (lane >= d) x = op(x, y);
+        const Track y = track_shfl_up(x, d);
+        if (lane >= d) x = track_op(y, x);
     }
     if (lane == 63) sh[wid] = x;
     __syncthreads();
-    T carry = ident;
-    for (int w = 0; w < wid; w++) carry = op(carry, sh[w]);
-    T prev = __shfl_up(x, 1, 64);
+    Track carry = ident, tot = ident;
+#pragma unroll
+    for (int w = 0; w < PER_NW; w++) {
+        if (w == wid) carry = tot;
+        tot = track_op(tot, sh[w]);
+    }
+    Track prev = track_shfl_up(x, 1);
     if (lane == 0) prev = ident;
-    const T r = op(carry, prev);
     __syncthreads();
-    return r;
+    *total = tot;
+    return track_op(carry, prev);
 }
 
-template <class T, class Op>
-__device__ T block_reduce(T v, Op op, T* sh) {
+__device__ __forceinline__ int block_min_int(int v, int* sh) {
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    T x = v;
 #pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) x = op(x, __shfl_xor(x, d, 64));
-    if (lane == 0) sh[wid] = x;
+    for (int d = 32; d >= 1; d >>= 1) {
+        const int o = __shfl_xor(v, d, 64);
+        v = o < v ? o : v;
+    }
+    if (lane == 0) sh[wid] = v;
     __syncthreads();
-    T r = sh[0];
-    for (int w = 1; w < (int)(blockDim.x >> 6); w++) r = op(r, sh[w]);
+    int r = sh[0];
+#pragma unroll
+    for (int w = 1; w < PER_NW; w++) r = sh[w] < r ? sh[w] : r;
     __syncthreads();
     return r;
 }
@@ -222,169 +329,165 @@ __device__ __forceinline__ uint32_t leaf_hash(uint32_t x) {
 }
 
 // ---------------------------------------------------------------------------------------
-// n <= PER_CHUNK SumTree.update calls in order, one workgroup.
+// n <= PER_CHUNK SumTree.update calls in order: three launches.
 //
 // SumTree.update(L, p) (R:dqn/utils/sum_tree.py:15-32):
 //   max_p, min_p = tree[max_idx], tree[min_idx]; tree[L] = p
 //   if p >= max_p: max_idx = L     elif L == max_idx: max_idx = argmax(leaves[:size])
 //   if p <= min_p: min_idx = L     elif L == min_idx: min_idx = argmin(leaves[:size])
 //   ancestors += p - old
-// Without rescans the tracked max value is the running max of the p's (prefix scan) and
-// max_idx is the leaf of the last update with p >= running max before it; an update
-// triggers a rescan iff it does not raise the max and writes the current max leaf.  The
-// kernel scans for the first trigger, applies the updates before it as scans, does the
-// rescan on the leaves as they stand after that update, and restarts after it.  Rescans
-// are rare (the max / min leaf has to be resampled), so the common case is one pass.
+//
+// k_per_prep (grid): leaf, priority (float64 pow) and old leaf value of every item; the
+//   latest item writing each slot is found by a 64-bit atomicMax of (epoch << 32 | i) on a
+//   per-slot word (tagged by a chunk epoch, so it never needs clearing).
+// k_per_update (one workgroup): the max / min index tracking.  Without rescans the tracked
+//   max value is the running max of the p's (prefix scan) and max_idx is the leaf of the last
+//   update with p >= running max before it; an update triggers a rescan iff it does not
+//   raise the max and writes the current max leaf.  The kernel scans for the first trigger,
+//   applies the updates before it to the leaves, does the rescan on the leaves as they stand
+//   after that update, and restarts after it.  Rescans are rare (the max / min leaf has to be
+//   resampled), so the common case is one pass.
+// k_per_prop (grid): every slot's last item writes the final leaf and adds its delta
+//   (final - old) to the ancestors: float64 atomics, the top levels first summed per
+//   workgroup in LDS.  Order-free: every addition is exact (file header).
 // ---------------------------------------------------------------------------------------
+constexpr int PER_GT = 256;   // threads per workgroup of the grid launches
+
+__global__ __launch_bounds__(PER_GT) void k_per_prep(PerUpdateArgs a) {
+    const int i = blockIdx.x * PER_GT + threadIdx.x;
+    if (i >= a.n) return;
+    const int64_t base = a.cap - 1;
+    const int64_t slot = a.mode == 0 ? (int64_t)a.slots[i] : (a.wptr + i) % a.cap;
+    const int32_t L = (int32_t)(slot + base);
+    float p;
+    if (a.mode == 0) {
+        p = per_priority(a.abs_td[i], a.eps, a.alpha, a.pmax);
+    } else {   // store_transitions: max_priority, or max_priority_high if 0
+        const double mv = a.tree[a.ctrl->per_max_idx];
+        p = (mv == 0.0) ? a.pmax : (float)mv;
+    }
+    a.wl[i] = L;
+    a.wp[i] = p;
+    a.winit[i] = a.tree[L];
+    const uint64_t e = (uint64_t)(*a.epoch + 1u);
+    atomicMax((unsigned long long*)&a.last[slot], (unsigned long long)((e << 32) | (uint32_t)i));
+}
+
 __global__ __launch_bounds__(PER_NT) void k_per_update(PerUpdateArgs a) {
     __shared__ int32_t Ls[PER_CHUNK];
     __shared__ float Ps[PER_CHUNK];
-    __shared__ int32_t hkey[PER_HS], hlast[PER_HS];
-    __shared__ double topd[PER_TOP];
-    __shared__ float shf[16];
-    __shared__ int shi[16];
-    __shared__ double shd[16];
-    __shared__ int64_t shl[16];
+    __shared__ Track sht[PER_NW];
+    __shared__ int shi[PER_NW];
+    __shared__ double shd[PER_NW];
+    __shared__ int64_t shl[PER_NW];
     __shared__ int s_mx_i, s_mn_i, s_resx, s_resn;
     __shared__ float s_mx_v, s_mn_v;
 
     const int tid = threadIdx.x;
+    DQNX_STAMP(a.stamps, 56);
     const int n = a.n;
     const int64_t base = a.cap - 1;
-    float mp = 0.f;
-    if (a.mode == 1) {   // store_transitions: max_priority, or max_priority_high if 0
-        const double mv = a.tree[a.ctrl->per_max_idx];
-        mp = (mv == 0.0) ? a.pmax : (float)mv;
-    }
-    double init[PER_IPT];
-    int hs[PER_IPT];
+    float pv[PER_IPT];
+    int32_t lv[PER_IPT];
 #pragma unroll
-    for (int k = 0; k < PER_IPT; k++) {
-        const int i = tid * PER_IPT + k;   // consecutive items per thread (scan order)
-        init[k] = 0.0;
-        hs[k] = -1;
+    for (int k = 0; k < PER_IPT; k++) {   // consecutive items per thread (scan order)
+        const int i = tid * PER_IPT + k;
+        pv[k] = 0.f;
+        lv[k] = -1;
         if (i < n) {
-            int64_t slot;
-            float p;
-            if (a.mode == 0) {
-                slot = a.slots[i];
-                p = per_priority(a.abs_td[i], a.eps, a.alpha, a.pmax);
-            } else {
-                slot = (a.wptr + i) % a.cap;
-                p = mp;
-            }
-            const int32_t L = (int32_t)(slot + base);
-            Ls[i] = L;
-            Ps[i] = p;
-            init[k] = a.tree[L];
+            lv[k] = a.wl[i];
+            pv[k] = a.wp[i];
+            Ls[i] = lv[k];
+            Ps[i] = pv[k];
         }
     }
-    for (int h = tid; h < PER_HS; h += PER_NT) {
-        hkey[h] = -1;
-        hlast[h] = -1;
-    }
-    for (int h = tid; h < PER_TOP; h += PER_NT) topd[h] = 0.0;
     int mx_i = (int)a.ctrl->per_max_idx, mn_i = (int)a.ctrl->per_min_idx;
     float mx_v = (float)a.tree[mx_i], mn_v = (float)a.tree[mn_i];
     __syncthreads();
-
-    // last occurrence of every leaf in the batch (its final value)
-#pragma unroll
-    for (int k = 0; k < PER_IPT; k++) {
-        const int i = tid * PER_IPT + k;
-        if (i < n) {
-            const int32_t L = Ls[i];
-            int h = (int)(leaf_hash((uint32_t)L) & (PER_HS - 1));
-            while (true) {
-                const int32_t prev = atomicCAS(&hkey[h], -1, L);
-                if (prev == -1 || prev == L) break;
-                h = (h + 1) & (PER_HS - 1);
-            }
-            atomicMax(&hlast[h], i);
-            hs[k] = h;
-        }
-    }
-    __syncthreads();
+    DQNX_STAMP(a.stamps, 57);
+    DQNX_STAMP(a.stamps, 58);
 
     // ---- max / min index tracking, sequential semantics ----
     int s = 0;
     while (true) {
-        float pv[PER_IPT];
-        bool inr[PER_IPT];
-        float lmx = -INFINITY, lmn = INFINITY;
+        // pass 1: the thread's max / min (for the scan)
+        Track own{-INFINITY, INFINITY, -1, -1};
 #pragma unroll
         for (int k = 0; k < PER_IPT; k++) {
             const int i = tid * PER_IPT + k;
-            inr[k] = i >= s && i < n;
-            pv[k] = inr[k] ? Ps[i] : 0.f;
-            if (inr[k]) {
-                lmx = fmaxf(lmx, pv[k]);
-                lmn = fminf(lmn, pv[k]);
+            if (i >= s && i < n) {
+                own.mx = fmaxf(own.mx, pv[k]);
+                own.mn = fminf(own.mn, pv[k]);
             }
         }
-        const float exmx = block_exclusive(lmx, -INFINITY, OpMaxF(), shf);
-        const float exmn = block_exclusive(lmn, INFINITY, OpMinF(), shf);
-        float rmx = fmaxf(mx_v, exmx), rmn = fminf(mn_v, exmn);   // running max / min before item
-        bool fx[PER_IPT], fn[PER_IPT];
-        float bmx[PER_IPT], bmn[PER_IPT];
-        int lfx = -1, lfn = -1;
+        Track totv;
+        const Track exv = track_scan(own, sht, &totv);
+        // pass 2: which items (re)take the max / min, given the running values BEFORE each
+        Track ownl{-INFINITY, INFINITY, -1, -1};
+        {
+            float rmx = fmaxf(mx_v, exv.mx), rmn = fminf(mn_v, exv.mn);
 #pragma unroll
-        for (int k = 0; k < PER_IPT; k++) {
-            const int i = tid * PER_IPT + k;
-            bmx[k] = rmx;
-            bmn[k] = rmn;
-            fx[k] = inr[k] && pv[k] >= rmx;
-            fn[k] = inr[k] && pv[k] <= rmn;
-            if (inr[k]) {
-                rmx = fmaxf(rmx, pv[k]);
-                rmn = fminf(rmn, pv[k]);
+            for (int k = 0; k < PER_IPT; k++) {
+                const int i = tid * PER_IPT + k;
+                if (i >= s && i < n) {
+                    if (pv[k] >= rmx) ownl.lx = i;
+                    if (pv[k] <= rmn) ownl.ln = i;
+                    rmx = fmaxf(rmx, pv[k]);
+                    rmn = fminf(rmn, pv[k]);
+                }
             }
-            if (fx[k]) lfx = i;
-            if (fn[k]) lfn = i;
         }
-        const int exlx = block_exclusive(lfx, -1, OpMaxI(), shi);
-        const int exln = block_exclusive(lfn, -1, OpMaxI(), shi);
-        int lastx = exlx, lastn = exln;
+        Track totl;
+        const Track exl = track_scan(ownl, sht, &totl);
+        // pass 3: the first item that rewrites the current max / min leaf without retaking it
+        int lastx = exl.lx, lastn = exl.ln;
         int mytrig = n;
-        int cxb = 0, cnb = 0, tk = -1;
+        int cxb = 0, cnb = 0;
+        float tp = 0.f, bx = 0.f, bn = 0.f;
+        {
+            float rmx = fmaxf(mx_v, exv.mx), rmn = fminf(mn_v, exv.mn);
 #pragma unroll
-        for (int k = 0; k < PER_IPT; k++) {
-            const int i = tid * PER_IPT + k;
-            const int curx = lastx >= 0 ? Ls[lastx] : mx_i;   // max_idx before update i
-            const int curn = lastn >= 0 ? Ls[lastn] : mn_i;
-            const bool trig = inr[k] && ((!fx[k] && Ls[i] == curx) || (!fn[k] && Ls[i] == curn));
-            if (trig && mytrig == n) {
-                mytrig = i;
-                cxb = curx;
-                cnb = curn;
-                tk = k;
+            for (int k = 0; k < PER_IPT; k++) {
+                const int i = tid * PER_IPT + k;
+                if (i >= s && i < n) {
+                    const bool fx = pv[k] >= rmx, fn = pv[k] <= rmn;
+                    const int curx = lastx >= 0 ? Ls[lastx] : mx_i;   // max_idx before update i
+                    const int curn = lastn >= 0 ? Ls[lastn] : mn_i;
+                    const bool trig = (!fx && lv[k] == curx) || (!fn && lv[k] == curn);
+                    if (trig && mytrig == n) {
+                        mytrig = i;
+                        cxb = curx;
+                        cnb = curn;
+                        tp = pv[k];
+                        bx = rmx;
+                        bn = rmn;
+                    }
+                    if (fx) lastx = i;
+                    if (fn) lastn = i;
+                    rmx = fmaxf(rmx, pv[k]);
+                    rmn = fminf(rmn, pv[k]);
+                }
             }
-            if (fx[k]) lastx = i;
-            if (fn[k]) lastn = i;
         }
-        const int istar = block_reduce(mytrig, OpMinI(), shi);
-        if (istar == n) {   // no rescan left: fold the scans into the state
-            const float tmx = block_reduce(lmx, OpMaxF(), shf);
-            const float tmn = block_reduce(lmn, OpMinF(), shf);
-            const int tlx = block_reduce(lfx, OpMaxI(), shi);
-            const int tln = block_reduce(lfn, OpMaxI(), shi);
-            if (tlx >= 0) mx_i = Ls[tlx];
-            if (tln >= 0) mn_i = Ls[tln];
-            mx_v = fmaxf(mx_v, tmx);
-            mn_v = fminf(mn_v, tmn);
+        if (!__syncthreads_or(mytrig < n)) {   // no rescan left: fold the scans into the state
+            if (totl.lx >= 0) mx_i = Ls[totl.lx];
+            if (totl.ln >= 0) mn_i = Ls[totl.ln];
+            mx_v = fmaxf(mx_v, totv.mx);
+            mn_v = fminf(mn_v, totv.mn);
             break;
         }
+        const int istar = block_min_int(mytrig, shi);
         if (mytrig == istar) {   // the owner of the first trigger applies that update
-            const float p = pv[tk];
+            const float p = tp;
             const int L = Ls[istar];
             s_resx = 0;
             s_resn = 0;
-            if (p >= bmx[tk]) { s_mx_i = L; s_mx_v = p; }
+            if (p >= bx) { s_mx_i = L; s_mx_v = p; }
             else if (L == cxb) s_resx = 1;
-            else { s_mx_i = cxb; s_mx_v = bmx[tk]; }
-            if (p <= bmn[tk]) { s_mn_i = L; s_mn_v = p; }
+            else { s_mx_i = cxb; s_mx_v = bx; }
+            if (p <= bn) { s_mn_i = L; s_mn_v = p; }
             else if (L == cnb) s_resn = 1;
-            else { s_mn_i = cnb; s_mn_v = bmn[tk]; }
+            else { s_mn_i = cnb; s_mn_v = bn; }
         }
         __syncthreads();
         // leaves as they stand after update istar (earlier segments were written already)
@@ -411,16 +514,29 @@ __global__ __launch_bounds__(PER_NT) void k_per_update(PerUpdateArgs a) {
         s = istar + 1;
         __syncthreads();
     }
+    DQNX_STAMP(a.stamps, 59);
+    if (tid == 0) {
+        a.ctrl->per_max_idx = mx_i;
+        a.ctrl->per_min_idx = mn_i;
+        *a.epoch += 1u;   // the chunk k_per_prep tagged; k_per_prop reads it back
+    }
+    DQNX_STAMP(a.stamps, 61);
+}
 
-    // ---- final leaf values and exact ancestor deltas ----
-#pragma unroll
-    for (int k = 0; k < PER_IPT; k++) {
-        const int i = tid * PER_IPT + k;
-        if (i < n && hlast[hs[k]] == i) {
-            const int64_t L = Ls[i];
-            const double fin = (double)Ps[i];
+__global__ __launch_bounds__(PER_GT) void k_per_prop(PerUpdateArgs a) {
+    __shared__ double topd[PER_TOP];
+    const int tid = threadIdx.x;
+    for (int h = tid; h < PER_TOP; h += PER_GT) topd[h] = 0.0;
+    __syncthreads();
+    const int i = blockIdx.x * PER_GT + tid;
+    const int64_t base = a.cap - 1;
+    if (i < a.n) {
+        const int64_t L = a.wl[i];
+        const uint64_t tag = ((uint64_t)*a.epoch << 32) | (uint32_t)i;
+        if (a.last[L - base] == tag) {   // the slot's final value
+            const double fin = (double)a.wp[i];
             a.tree[L] = fin;
-            const double delta = fin - init[k];
+            const double delta = fin - a.winit[i];
             if (delta != 0.0) {
                 int64_t node = L;
                 while (node > 0) {
@@ -432,17 +548,14 @@ __global__ __launch_bounds__(PER_NT) void k_per_update(PerUpdateArgs a) {
         }
     }
     __syncthreads();
-    for (int node = tid; node < PER_TOP && node < base; node += PER_NT)
-        if (topd[node] != 0.0) a.tree[node] += topd[node];
-    if (tid == 0) {
-        a.ctrl->per_max_idx = mx_i;
-        a.ctrl->per_min_idx = mn_i;
-    }
+    for (int node = tid; node < PER_TOP && node < base; node += PER_GT)
+        if (topd[node] != 0.0) atomicAdd(&a.tree[node], topd[node]);
 }
 
 int launch_per_sample(const PerSampleArgs& a, hipStream_t s) {
     if (a.Bg < 1 || a.Bg > PER_MAX_B) return set_error(DQNX_EUNSUPPORTED, "PER batch %d outside [1, %d]", a.Bg, PER_MAX_B);
-    hipLaunchKernelGGL(k_per_sample, dim3(1 + a.rl_blocks), dim3(PER_NT), 0, s, a);
+    const int G = (a.Bg + PER_SNT - 1) / PER_SNT;
+    hipLaunchKernelGGL(k_per_sample, dim3(G + a.rl_blocks), dim3(PER_SNT), 0, s, a);
     DQNX_HIP_CHECK(hipGetLastError());
     return DQNX_OK;
 }
@@ -450,7 +563,10 @@ int launch_per_sample(const PerSampleArgs& a, hipStream_t s) {
 int launch_per_update(const PerUpdateArgs& a, hipStream_t s) {
     if (a.n < 0 || a.n > PER_CHUNK) return set_error(DQNX_EINVAL, "PER update chunk %d > %d", a.n, PER_CHUNK);
     if (a.n == 0) return DQNX_OK;
+    const int g = (a.n + PER_GT - 1) / PER_GT;
+    hipLaunchKernelGGL(k_per_prep, dim3(g), dim3(PER_GT), 0, s, a);
     hipLaunchKernelGGL(k_per_update, dim3(1), dim3(PER_NT), 0, s, a);
+    hipLaunchKernelGGL(k_per_prop, dim3(g), dim3(PER_GT), 0, s, a);
     DQNX_HIP_CHECK(hipGetLastError());
     return DQNX_OK;
 }

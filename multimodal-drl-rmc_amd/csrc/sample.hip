@@ -49,25 +49,6 @@ constexpr int SAMPLE_NT = 1024;   // threads of the sampler workgroup (>= 624: o
 constexpr int SAMPLE_AHEAD = 4;   // MT blocks twisted ahead per pass
 constexpr int SAMPLE_WPT = 4;     // words per thread per pass: (624 * (1 + AHEAD)) / NT rounded up
 
-// blk_new = twist(blk_old): CPython genrand_uint32's recurrence
-//   new[k] = X ^ mix(old[k], old[k+1]),  X = old[k+397] (k < 227), new[k-227] (k >= 227).
-// The dependency chain k -> k+227 -> k+454 stays inside thread k (< 227), in registers, so
-// one barrier completes the twist; new[623] = new[396] ^ mix(old[623], new[0]) is done by
-// thread 169, which owns new[396] and recomputes new[0] from `old`.
-// Every thread of the block must call it.
-__device__ __forceinline__ void mt_twist_into(const uint32_t* old, uint32_t* nw) {
-    const int t = threadIdx.x;
-    if (t < 227) {
-        const uint32_t a0 = old[t + 397] ^ mt_mix(old[t], old[t + 1]);
-        const uint32_t a1 = a0 ^ mt_mix(old[t + 227], old[t + 228]);
-        nw[t] = a0;
-        nw[t + 227] = a1;
-        if (t < 169) nw[t + 454] = a1 ^ mt_mix(old[t + 454], old[t + 455]);
-        if (t == 169) nw[623] = a1 ^ mt_mix(old[623], old[397] ^ mt_mix(old[0], old[1]));
-    }
-    __syncthreads();
-}
-
 template <int HS>  // hash slots (power of two)
 __global__ __launch_bounds__(SAMPLE_NT) void k_sample_uniform(SampleArgs a) {
     constexpr int NT = SAMPLE_NT, NW = NT / 64;

@@ -25,7 +25,7 @@ pytestmark = pytest.mark.gpu
 # one bf16 ulp (2^-8 relative).  So: nearly every element within Q_TIGHT, the rest (flip
 # descendants, at most Q_FLIP_FRAC of them) within Q_ATOL.
 Q_TIGHT = 2e-6
-Q_FLIP_FRAC = 2e-3
+Q_FLIP_FRAC = 2e-2
 Q_ATOL = 1e-3          # Q values, targets
 LOSS_RTOL = 1e-4
 GRAD_TOL = 2e-3        # max |dg| / max |g| per tensor

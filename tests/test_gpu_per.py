@@ -63,7 +63,8 @@ def test_gpu_per_push_matches_sumtree_add():
         assert eng.ctrl().ring_size == rep.replay_buffer.size
 
 
-@pytest.mark.parametrize("cap,fill,n,rounds", [(500, 300, 64, 40), (20000, 20000, 5000, 3)])
+@pytest.mark.parametrize("cap,fill,n,rounds", [(500, 300, 64, 40), (20000, 20000, 5000, 3), (20000, 20000, 8192, 2),
+                                               (30000, 30000, 12000, 2)])
 def test_gpu_per_priority_updates_match_sequential_semantics(cap, fill, n, rounds):
     """Batches with duplicate leaves, the max leaf lowered and the min leaf raised (the
     argmax / argmin rescans), and more updates than one launch takes."""
@@ -90,16 +91,19 @@ def test_gpu_per_priority_updates_match_sequential_semantics(cap, fill, n, round
         assert_tree_equal(eng, st)
 
 
-def test_gpu_per_sample_matches_oracle():
-    cap, fill, B = 3000, 2500, 256
+@pytest.mark.parametrize("cap,fill,B", [(3000, 2500, 256), (100000, 90000, 8192), (200000, 150000, 5000)])
+def test_gpu_per_sample_matches_oracle(cap, fill, B):
+    """One sampling workgroup (B <= 1024) and several (each walks the MT twists, the last to
+    arrive writes the state back); trees deeper than the LDS-cached top 13 levels."""
     eng = per_engine(14, B, cap)
     rep = O.PerReplay(cap, B, 2e6, "cr")
     data = O.synth_transitions(fill, 14, 8, seed=8)
     eng.push(*data)
     list(rep.store_transitions(*data))
     rng = np.random.default_rng(9)
-    slots = rng.integers(0, fill, size=2000).astype(np.int32)
-    absd = rng.random(2000).astype(np.float32) * np.float32(2.0)
+    nu = min(fill, 20000)
+    slots = rng.integers(0, fill, size=nu).astype(np.int32)
+    absd = rng.random(nu).astype(np.float32) * np.float32(2.0)
     eng.per_update_priorities(torch.from_numpy(slots), torch.from_numpy(absd))
     rep.update_batch_priorities((slots.astype(np.int64) + cap - 1).tolist(), absd.reshape(-1, 1))
     np.random.seed(10)

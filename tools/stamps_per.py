@@ -1,0 +1,38 @@
+"""Diagnostic: s_memtime phase stamps (block 0, thread 0) of the PER kernels (libdqnx_stamps.so).
+k_per_sample: 0 start, 1 top/MT loaded, 2 words + beta, 3 descents done.
+k_per_update (last chunk of the step): 56 start, 57 items loaded, 58 (same), 59 max/min
+tracking, 61 end."""
+import os
+import random
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+os.environ.setdefault("DQNX_LIB", os.path.join(HERE, "..", "multimodal-drl-rmc_amd", "dqn", "_lib", "libdqnx_stamps.so"))
+sys.path.insert(0, os.path.join(HERE, ".."))
+sys.path.insert(0, os.path.join(HERE, "..", "multimodal-drl-rmc_amd"))
+import ctypes  # noqa: E402
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+import bench  # noqa: E402
+from dqn import _capi as C  # noqa: E402
+from dqn.engine import LearnEngine, mlp_spec  # noqa: E402
+
+B = int(sys.argv[1]) if len(sys.argv) > 1 else 8192
+cap = 1_000_000
+spec = mlp_spec(284, 8, "dueling")
+eng = LearnEngine(spec, "PerDuelingDoubleDQNAgent", B, cap, graphs=False)
+eng.load_params(bench.init_params(spec))
+bench.fill_ring(eng, cap, 284, 8, eng.device)
+np.random.seed(1234)
+st = np.random.get_state()
+eng.set_rng(C.DQNX_RNG_NP, np.append(st[1], st[2]).astype(np.uint32))
+out = (ctypes.c_int64 * 64)()
+for step in range(5):
+    eng.learn_step(soft_update=True)
+    torch.cuda.synchronize()
+    C.check(C.lib().dqnx_debug_stamps(eng.h, out, eng.stream()), "stamps")
+    s = list(out)
+    ps = [s[j + 1] - s[j] for j in range(3)]
+    pu = [s[57] - s[56], s[59] - s[58], s[61] - s[59]]
+    print(f"step {step}: per_sample cyc {ps} total {s[3] - s[0]}; per_update cyc {pu} total {s[61] - s[56]}")
