@@ -33,7 +33,7 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(REPO, "multimodal-drl-rmc_amd"))
 
 from dqn import _capi as C  # noqa: E402
-from dqn.data_parallel import dp_learn_step  # noqa: E402
+from dqn.data_parallel import GraphedDPStep, dp_learn_step  # noqa: E402
 from dqn.engine import LearnEngine, hybrid_spec, mlp_spec  # noqa: E402
 
 PEAK_FP32_MFMA_TFLOPS = 157.3   # MI355X_MICROARCH.md: F32 matrix, dense
@@ -60,6 +60,9 @@ def parse():
                    help="mlp: MLP-284 (configs[1]); hybrid: TwoStreamHybridNetwork on the (2,27,5) grid; "
                         "hybrid84: the stacked (4,84,84) occupancy-grid CNN variant (configs[2])")
     p.add_argument("--no-graphs", action="store_true")
+    p.add_argument("--no-dp-graph", action="store_true",
+                   help="N > 1: launch the learn graph, the all-reduce and Adam separately each step "
+                        "instead of replaying them as one captured HIP graph")
     p.add_argument("--compute", default="fp32", choices=["fp32", "bf16"],
                    help="GEMM operand precision (bf16: BASELINE config 5; MLP only; fp32 accumulate, master weights, Adam)")
     p.add_argument("--global-sampling", action="store_true",
@@ -212,6 +215,7 @@ def main():
     torch.cuda.set_device(dev_index)
     device = torch.device("cuda", dev_index)
     dist = None
+    backend = None
     if world > 1:
         import torch.distributed as dist
         backend = os.environ.get("DQNX_DIST_BACKEND", "nccl")   # nccl = RCCL over xGMI
@@ -251,6 +255,18 @@ def main():
         step()
     torch.cuda.synchronize()
     eng.check_device_error()
+    dp_graph = False
+    if world > 1 and backend == "nccl" and not args.no_dp_graph and not args.no_graphs:
+        # the whole DP step (shard kernels + RCCL all-reduce + Adam) as one replayed graph: the
+        # eager loop is host-bound (3 launches + a collective call per ~50 us step).  RCCL
+        # collectives are capturable; gloo's are host calls and never are.
+        g = GraphedDPStep(eng, soft_update=True)
+        g()   # one untimed replay
+        torch.cuda.synchronize()
+        dp_graph = True
+
+        def step():
+            g()
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
@@ -261,6 +277,8 @@ def main():
     if dist:
         dist.barrier()
     el = time.perf_counter() - t0
+    if dp_graph:
+        eng.set_graphs(True)   # the kernel timing below replays the engine's own graphs
     if dist:
         t = torch.tensor([el], device=device, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -370,6 +388,8 @@ def main():
                 "batch_per_gpu": args.batch, "global_batch": Bg, "replay_capacity": args.capacity,
                 "parallelism": f"dp{world}", "graphs": not args.no_graphs, "prefetch_sampling": prefetch,
                 "sampling": "rank-local" if local else "global",
+                "dp_step": ("one HIP graph" if dp_graph else "eager") if world > 1 else None,
+                "compute": args.compute,
             },
             "roofline": roofline,
             "cpu_baseline": cpu,

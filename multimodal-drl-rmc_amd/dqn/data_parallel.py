@@ -43,3 +43,29 @@ def exchange(engine, group=None):
         parts = list(engine.per_abs_td.chunk(world))
         mine = engine.per_abs_td[b0:b1].clone()
         dist.all_gather(parts, mine, group=group)
+
+
+class GraphedDPStep:
+    """The whole data-parallel step -- the shard's learn kernels, the RCCL all-reduce (+ the
+    PER |delta| all-gather), Adam + soft update -- captured once into one HIP graph
+    (torch.cuda.CUDAGraph) and replayed: one host launch per step instead of a learn-graph
+    launch, a collective call and an optimizer launch, so the GPU never waits on the host.
+
+    The step state (RNG, ring size, Adam step, SumTree) lives on the device, so replays
+    continue the same sequence of steps as eager dp_learn_step calls (transitions pushed in
+    between are seen: the samplers read the ring size on the device).  Run at least one eager
+    dp_learn_step first (communicator warm-up).  The engine's own per-step graphs are switched
+    off: its kernels become nodes of this graph.
+    """
+
+    def __init__(self, engine, soft_update: bool = True, group=None):
+        self.engine = engine
+        engine.set_graphs(False)
+        self.graph = torch.cuda.CUDAGraph()
+        torch.cuda.synchronize()
+        with torch.cuda.graph(self.graph):
+            dp_learn_step(engine, soft_update=soft_update, group=group)
+        torch.cuda.synchronize()
+
+    def __call__(self):
+        self.graph.replay()

@@ -271,6 +271,11 @@ class LearnEngine:
         return a
 
     # ---- steps -----------------------------------------------------------------------
+    def set_graphs(self, on: bool):
+        """Replay each learn step as a captured HIP graph (default) or launch its kernels one by
+        one (e.g. into a caller's own stream capture)."""
+        C.check(self.L.dqnx_engine_set_graphs(self.h, 1 if on else 0), "set_graphs")
+
     def learn_step(self, soft_update=False, given_indices=False, grads_only=False, prefetch=False):
         """One learn step (+ fused soft update).  prefetch=True also draws the next step's
         minibatch on a forked graph branch (pure learning loops; see DQNX_STEP_PREFETCH)."""

@@ -83,3 +83,15 @@ def test_gpu_dp_world2_rank_local_sampling(tmp_path):
         np.testing.assert_allclose(z[r]["params"], flat_on, atol=1e-5, rtol=0)
         np.testing.assert_allclose(z[r]["target"], flat_tg, atol=1e-5, rtol=0)
     assert np.array_equal(z[0]["params"], z[1]["params"])
+
+
+@pytest.mark.parametrize("algo", ["DuelingDoubleDQNAgent", "PerDuelingDoubleDQNAgent"])
+def test_gpu_graphed_dp_step_matches_eager(algo):
+    """dqn.data_parallel.GraphedDPStep (learn kernels + RCCL all-reduce + Adam captured as one
+    HIP graph) continues exactly like eager dp_learn_step calls (world 1 over RCCL, one GPU),
+    and both equal the single-GPU learn step; the script asserts it."""
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(free_port()))
+    r = subprocess.run([sys.executable, os.path.join(os.path.dirname(HERE), "tools", "dp_graph_check.py"), algo, "256"],
+                       env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    assert "graphed == eager: True; dp == single: True" in r.stdout, r.stdout[-2000:]

@@ -22,6 +22,8 @@ NAMES = [   # (substring of the HIP kernel name, bench step name)
     ("k_adam", "adam_fused"),
     ("k_per_sample", "per_sample"),
     ("k_per_update", "per_update"),
+    ("k_per_prep", "per_update_prep"),
+    ("k_per_prop", "per_update_prop"),
 ]
 
 
