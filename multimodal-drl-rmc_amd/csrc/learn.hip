@@ -507,7 +507,13 @@ __global__ __launch_bounds__(256) void k_adam(AdamArgs a) {
 #pragma unroll
             for (int u = 1; u < 8; u++)
                 if (u < sg.S) gsum += pv[u];
-            for (int u = 8; u < sg.S; u++) gsum += pp[(int64_t)u * sg.pstride];
+            for (int u0 = 8; u0 < sg.S; u0 += 8) {   // 8 loads in flight per round trip
+#pragma unroll
+                for (int u = 0; u < 8; u++) pv[u] = (u0 + u < sg.S) ? pp[(int64_t)(u0 + u) * sg.pstride] : 0.f;
+#pragma unroll
+                for (int u = 0; u < 8; u++)
+                    if (u0 + u < sg.S) gsum += pv[u];
+            }
             a.grads[e] = gsum;
         }
         if (a.mode == 0) continue;
