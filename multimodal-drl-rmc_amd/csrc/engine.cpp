@@ -560,7 +560,7 @@ void build_fused_steps(dqnx_engine* e, int flags, int32_t* idx, int32_t* phys, s
     {
         FusedFwdArgs fa = e->fplan;
         fa.Bl = e->Bl;
-        fa.tiles = e->tiles;
+        fa.tiles = (e->Bl + 16 * fa.mr - 1) / (16 * fa.mr);
         fa.nstreams = nstreams;
         for (int l = 0; l < L; l++) fa.woff[l] = np.dense[l].off;
         fa.head_off = np.head_off;
@@ -1416,7 +1416,7 @@ int dqnx_engine_create(const dqnx_config* cfg, dqnx_engine** out) {
         if (c.compute_dtype != DQNX_COMPUTE_FP32 && c.compute_dtype != DQNX_COMPUTE_BF16)
             { delete e; return set_error(DQNX_EINVAL, "bad compute_dtype %d", c.compute_dtype); }
         const bool bf = c.compute_dtype == DQNX_COMPUTE_BF16;
-        const bool fused_ok = c.net.kind == DQNX_NET_MLP && fused_fwd_plan(fp, c.net.obs_dim, bf);
+        const bool fused_ok = c.net.kind == DQNX_NET_MLP && fused_fwd_plan(fp, c.net.obs_dim, bf, 1);
         e->bwd_plan = fused_ok ? 2 : 0;
         if (const char* bp = getenv("DQNX_BWD_PLAN")) {
             const int want = atoi(bp);
@@ -1438,6 +1438,20 @@ int dqnx_engine_create(const dqnx_config* cfg, dqnx_engine** out) {
     e->Bs = e->local_sampling ? e->Bl : e->Bg;
     e->stride = (int)align_up((uint64_t)c.net.obs_dim, 4);
     e->tiles = (e->Bl + 15) / 16;
+    if (e->bwd_plan == 2) {
+        // forward rows per workgroup.  bf16: the largest of 4, 2 (x16) that still gives every
+        // CU a workgroup (each weight fragment streamed from L2 then feeds mr MFMAs): 30.5 ->
+        // 26.2 us at B=8192.  fp32 is MFMA-bound per CU and gains nothing (B=4096: 37.8 us at
+        // mr 1, 43.8 at 2, 41.0 at 4), so it keeps 16-row workgroups.
+        const int nst = c.algo == DQNX_ALGO_DQN ? 2 : 3;
+        int mr = 1;
+        if (e->fplan.bf16)
+            for (int cand : {4, 2})
+                if (mr == 1 && ((e->Bl + 16 * cand - 1) / (16 * cand)) * nst >= 256) mr = cand;
+        if (const char* v = getenv("DQNX_FWD_MR")) mr = atoi(v);
+        FusedFwdArgs trial = e->fplan;
+        if (mr != 1 && fused_fwd_plan(trial, c.net.obs_dim, e->fplan.bf16 != 0, mr)) e->fplan = trial;
+    }
     e->setsize = sample_setsize(e->Bs);
     const int L = (int)e->np.dense.size();
     e->slices.assign(L, 1);

@@ -197,8 +197,83 @@ __device__ __forceinline__ void wave_mma(const void* As, int sa, int ngroups, co
     else if (c.tn == 1) wave_mma_t<1, BF>(As, sa, ngroups, w, wb, acc);
 }
 
+// MR row tiles (16 * MR rows per workgroup, large batches): every weight fragment fetched
+// from L2 feeds MR MFMAs, so the weight stream per row shrinks MR-fold.  A fragments are read
+// per chunk (MR of them) to keep the register budget of MR accumulator sets.
+template <int TN, bool BF, int MR>
+__device__ __forceinline__ void mma_group_mr(const void* ap_, int rowoff, int ch0, int nch, const float4 (&w)[FPF][2],
+                                             floatx4 (&acc)[MR][2]) {
+#pragma unroll
+    for (int p = 0; p < FPF; p++) {
+        if constexpr (!BF) {
+            const float* ap = static_cast<const float*>(ap_);
+            float4 av[MR];
+#pragma unroll
+            for (int m = 0; m < MR; m++) av[m] = *reinterpret_cast<const float4*>(ap + m * rowoff + (ch0 + p) * 16);
+#pragma unroll
+            for (int m = 0; m < MR; m++)
+#pragma unroll
+                for (int t = 0; t < TN; t++) acc[m][t] = mfma16x16x4(av[m].x, w[p][t].x, acc[m][t]);
+#pragma unroll
+            for (int m = 0; m < MR; m++)
+#pragma unroll
+                for (int t = 0; t < TN; t++) acc[m][t] = mfma16x16x4(av[m].y, w[p][t].y, acc[m][t]);
+#pragma unroll
+            for (int m = 0; m < MR; m++)
+#pragma unroll
+                for (int t = 0; t < TN; t++) acc[m][t] = mfma16x16x4(av[m].z, w[p][t].z, acc[m][t]);
+#pragma unroll
+            for (int m = 0; m < MR; m++)
+#pragma unroll
+                for (int t = 0; t < TN; t++) acc[m][t] = mfma16x16x4(av[m].w, w[p][t].w, acc[m][t]);
+        } else {
+            if (ch0 + p >= nch) break;
+            const uint16_t* ap = static_cast<const uint16_t*>(ap_);
+            u32x4 av[MR];
+#pragma unroll
+            for (int m = 0; m < MR; m++) av[m] = *reinterpret_cast<const u32x4*>(ap + m * rowoff + (ch0 + p) * 32);
+#pragma unroll
+            for (int m = 0; m < MR; m++)
+#pragma unroll
+                for (int t = 0; t < TN; t++)
+                    acc[m][t] = mfma16x16x32bf16(av[m], __builtin_bit_cast(u32x4, w[p][t]), acc[m][t]);
+        }
+    }
+}
+template <int TN, bool BF, int MR>
+__device__ __forceinline__ void wave_mma_mr_t(const void* As, int sa, int ngroups, const WStream& w,
+                                              float4 (&wb)[FNB][FPF][2], floatx4 (&acc)[MR][2]) {
+    const int lane = threadIdx.x & 63, i = lane & 15, g = lane >> 4;
+    const void* ap = BF ? (const void*)(static_cast<const uint16_t*>(As) + i * sa + 8 * g)
+                        : (const void*)(static_cast<const float*>(As) + i * sa + 4 * g);
+#pragma unroll
+    for (int m = 0; m < MR; m++)
+#pragma unroll
+        for (int t = 0; t < TN; t++) acc[m][t] = floatx4{0.f, 0.f, 0.f, 0.f};
+    for (int grp = 0; grp < ngroups; grp += FNB) {
+#pragma unroll
+        for (int u = 0; u < FNB; u++) {
+            const int ch = (grp + u) * FPF;
+#pragma unroll
+            for (int p = 0; p < FPF; p++) bfetch<TN>(w, ch + (FNB - 1) * FPF + p, wb[(u + FNB - 1) % FNB][p]);
+            __builtin_amdgcn_sched_barrier(0);
+            if (grp + u < ngroups) mma_group_mr<TN, BF, MR>(ap, 16 * sa, ch, w.nch, wb[u], acc);
+        }
+    }
+}
+template <bool BF, int MR>
+__device__ __forceinline__ void wave_mma_rows(const void* As, int sa, int ngroups, const WaveCols& c, const WStream& w,
+                                              float4 (&wb)[FNB][FPF][2], floatx4 (&acc)[MR][2]) {
+    if constexpr (MR == 1) {
+        wave_mma<BF>(As, sa, ngroups, c, w, wb, acc[0]);
+    } else {
+        if (c.tn == 2) wave_mma_mr_t<2, BF, MR>(As, sa, ngroups, w, wb, acc);
+        else if (c.tn == 1) wave_mma_mr_t<1, BF, MR>(As, sa, ngroups, w, wb, acc);
+    }
+}
+
 // =====================================================================================
-// Forward: every layer + head raw outputs for one 16-row tile of one stream.
+// Forward: every layer + head raw outputs for one 16 * MR-row tile of one stream.
 // LDS: buf0 = input tile [16][sx] (later hidden tiles / head partials), buf1 = hidden tiles.
 // =====================================================================================
 // NL (dense layers) is a template parameter so every per-layer kernel-argument access has a
@@ -206,8 +281,10 @@ __device__ __forceinline__ void wave_mma(const void* As, int sa, int ngroups, co
 // with its own wait (eight of them serialised the head kernel's prologue).
 // BF: bf16 activation tiles in LDS (row strides sx / sh in bf16 elements), bf16 blocked
 // weights, 16x16x32 bf16 MFMAs; accumulation, bias, activation and the H stores stay fp32.
-template <int ACT, int NL, bool BF>
+template <int ACT, int NL, bool BF, int MR>
 __global__ __launch_bounds__(FT) void k_mlp_fwd(FusedFwdArgs a) {
+    constexpr int RW = 16 * MR;          // rows per workgroup
+    constexpr int GQ = FGQ * MR;         // float4 gather slots per thread
     extern __shared__ __attribute__((aligned(16))) float lds[];
     // LDS tile b: pointer arithmetic on `lds` keeps the LDS address space visible to the
     // compiler (ds_read, not flat loads that share the vmcnt counter with the W stream)
@@ -218,7 +295,7 @@ __global__ __launch_bounds__(FT) void k_mlp_fwd(FusedFwdArgs a) {
     const int z = T / a.tiles, tile = T - z * a.tiles;
     const int s = a.stream_of[z];
     const int tgt = s == 2 ? 1 : 0;
-    const int b0 = tile * 16, nb = min(16, a.Bl - b0);
+    const int b0 = tile * RW, nb = min(RW, a.Bl - b0);
     const float* P = tgt ? a.tparams : a.params;
     const float* ring = (s == 0) ? a.ring_obs : a.ring_next;
     const bool keep = (s == 0);
@@ -237,9 +314,9 @@ __global__ __launch_bounds__(FT) void k_mlp_fwd(FusedFwdArgs a) {
         // branch-free: every slot loads (clamped row / column) and selects zero afterwards,
         // so the loads issue back to back (one phys round trip, then one ring round trip)
         if (DQNX_FUSED_ORDER == 1) stream_open(a.wblk[tgt][0], a.out[0] >> 4, fwd_nch<BF>(a.in[0]), 0, c, ws, wb);
-        int32_t slot[FGQ];
+        int32_t slot[GQ];
 #pragma unroll
-        for (int j = 0; j < FGQ; j++) {
+        for (int j = 0; j < GQ; j++) {
             const int r = (tid + j * FT) / q4;
             slot[j] = a.phys[b0 + (r < nb ? r : nb - 1)];
         }
@@ -248,9 +325,9 @@ __global__ __launch_bounds__(FT) void k_mlp_fwd(FusedFwdArgs a) {
         int32_t tslot = 0;
         if (keep && tid < nb) tslot = a.phys[b0 + tid];
         if (DQNX_FUSED_ORDER == 0) stream_open(a.wblk[tgt][0], a.out[0] >> 4, fwd_nch<BF>(a.in[0]), 0, c, ws, wb);
-        float4 xv[FGQ];
+        float4 xv[GQ];
 #pragma unroll
-        for (int j = 0; j < FGQ; j++) {
+        for (int j = 0; j < GQ; j++) {
             const int q = tid + j * FT;
             const int r = q / q4, c4 = q - r * q4;
             const bool ok = r < nb && c4 < rs4;
@@ -263,10 +340,10 @@ __global__ __launch_bounds__(FT) void k_mlp_fwd(FusedFwdArgs a) {
         if (keep && tid < nb)
             a.trans[b0 + tid] = make_float4(__int_as_float(a.act[tslot]), a.rew[tslot], a.done[tslot], 0.f);
 #pragma unroll
-        for (int j = 0; j < FGQ; j++) {
+        for (int j = 0; j < GQ; j++) {
             const int q = tid + j * FT;
             const int r = q / q4, c4 = q - r * q4;
-            if (r < 16) {
+            if (r < RW) {
                 if constexpr (BF)
                     *reinterpret_cast<uint2*>(reinterpret_cast<uint16_t*>(FBUF(0)) + r * a.sx + 4 * c4) =
                         make_uint2(bf16_pack2(xv[j].x, xv[j].y), bf16_pack2(xv[j].z, xv[j].w));
@@ -289,8 +366,8 @@ __global__ __launch_bounds__(FT) void k_mlp_fwd(FusedFwdArgs a) {
         float bias[2];
 #pragma unroll
         for (int t = 0; t < 2; t++) bias[t] = bias_p[(t < c.tn ? c.n0[t] : 0) + i];   // branch-free
-        floatx4 acc[2];
-        wave_mma<BF>(FBUF(cur), l == 0 ? a.sx : a.sh, fwd_groups<BF>(K), c, ws, wb, acc);
+        floatx4 acc[MR][2];
+        wave_mma_rows<BF, MR>(FBUF(cur), l == 0 ? a.sx : a.sh, fwd_groups<BF>(K), c, ws, wb, acc);
         DQNX_STAMP(a.stamps, 27 + 2 * l);
         const WaveCols cl = c;
         // next layer's weight stream in flight during the epilogue + barrier
@@ -305,13 +382,15 @@ __global__ __launch_bounds__(FT) void k_mlp_fwd(FusedFwdArgs a) {
             if (t >= cl.tn) continue;
             const int col = cl.n0[t] + i;
 #pragma unroll
-            for (int r = 0; r < 4; r++) {
-                const int rr = 4 * g + r;
-                const float v = act_fwd<ACT>(acc[t][r] + bias[t]);
-                if constexpr (BF) reinterpret_cast<uint16_t*>(Hs)[rr * a.sh + col] = bf16_bits(v);
-                else Hs[rr * a.sh + col] = v;
-                if (Hg && rr < nb) Hg[(int64_t)(b0 + rr) * N + col] = v;
-            }
+            for (int m = 0; m < MR; m++)
+#pragma unroll
+                for (int r = 0; r < 4; r++) {
+                    const int rr = 16 * m + 4 * g + r;
+                    const float v = act_fwd<ACT>(acc[m][t][r] + bias[t]);
+                    if constexpr (BF) reinterpret_cast<uint16_t*>(Hs)[rr * a.sh + col] = bf16_bits(v);
+                    else Hs[rr * a.sh + col] = v;
+                    if (Hg && rr < nb) Hg[(int64_t)(b0 + rr) * N + col] = v;
+                }
         }
         lds_barrier();
         DQNX_STAMP(a.stamps, 28 + 2 * l);
@@ -323,39 +402,48 @@ __global__ __launch_bounds__(FT) void k_mlp_fwd(FusedFwdArgs a) {
         const int F = a.F;
         const int A = a.head_kind == DQNX_HEAD_DUELING ? a.NH - 1 : a.NH;
         const float* hw = P + a.head_off + head_w_off(a.head_kind, i < a.NH ? i : 0, F);
-        floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+        floatx4 acc[MR];
+#pragma unroll
+        for (int m = 0; m < MR; m++) acc[m] = floatx4{0.f, 0.f, 0.f, 0.f};
         if constexpr (BF) {   // head weights rounded to bf16 here (fp32 master copy)
             const uint16_t* hs = reinterpret_cast<const uint16_t*>(FBUF(cur)) + i * a.sh + 8 * g;
             for (int ck = wid; ck < (F >> 5); ck += FW) {
                 const float4 w0 = ld4(hw + ck * 32 + 8 * g), w1 = ld4(hw + ck * 32 + 8 * g + 4);
                 u32x4 wv = {bf16_pack2(w0.x, w0.y), bf16_pack2(w0.z, w0.w), bf16_pack2(w1.x, w1.y), bf16_pack2(w1.z, w1.w)};
                 if (i >= a.NH) wv = u32x4{0u, 0u, 0u, 0u};
-                acc = mfma16x16x32bf16(*reinterpret_cast<const u32x4*>(hs + ck * 32), wv, acc);
+#pragma unroll
+                for (int m = 0; m < MR; m++)
+                    acc[m] = mfma16x16x32bf16(*reinterpret_cast<const u32x4*>(hs + 16 * m * a.sh + ck * 32), wv, acc[m]);
             }
         } else {
             const float* hs = FBUF(cur) + i * a.sh + 4 * g;
             for (int ck = wid; ck < (F >> 4); ck += FW) {
                 float4 wv = ld4(hw + ck * 16 + 4 * g);
                 if (i >= a.NH) wv = make_float4(0.f, 0.f, 0.f, 0.f);
-                const float4 av = *reinterpret_cast<const float4*>(hs + ck * 16);
-                acc = mfma16x16x4(av.x, wv.x, acc);
-                acc = mfma16x16x4(av.y, wv.y, acc);
-                acc = mfma16x16x4(av.z, wv.z, acc);
-                acc = mfma16x16x4(av.w, wv.w, acc);
+#pragma unroll
+                for (int m = 0; m < MR; m++) {
+                    const float4 av = *reinterpret_cast<const float4*>(hs + 16 * m * a.sh + ck * 16);
+                    acc[m] = mfma16x16x4(av.x, wv.x, acc[m]);
+                    acc[m] = mfma16x16x4(av.y, wv.y, acc[m]);
+                    acc[m] = mfma16x16x4(av.z, wv.z, acc[m]);
+                    acc[m] = mfma16x16x4(av.w, wv.w, acc[m]);
+                }
             }
         }
         DQNX_STAMP(a.stamps, 36);
-        float* part = FBUF(cur ^ 1);   // [FW][16 rows][16 outputs]
+        float* part = FBUF(cur ^ 1);   // [FW][RW rows][16 outputs]
 #pragma unroll
-        for (int r = 0; r < 4; r++) part[wid * 256 + (4 * g + r) * 16 + i] = acc[r];
+        for (int m = 0; m < MR; m++)
+#pragma unroll
+            for (int r = 0; r < 4; r++) part[(wid * RW + 16 * m + 4 * g + r) * 16 + i] = acc[m][r];
         float hb = 0.f;
-        if (tid < 256 && (tid & 15) < a.NH) hb = P[a.head_off + head_b_off(a.head_kind, tid & 15, F, A)];
+        if ((tid & 15) < a.NH) hb = P[a.head_off + head_b_off(a.head_kind, tid & 15, F, A)];
         lds_barrier();
-        if (tid < 256) {
-            const int b = tid >> 4, o = tid & 15;
+        for (int e = tid; e < RW * 16; e += FT) {   // FT is a multiple of 16: o == tid & 15
+            const int b = e >> 4, o = e & 15;
             float v = part[b * 16 + o];
 #pragma unroll
-            for (int w = 1; w < FW; w++) v += part[w * 256 + b * 16 + o];
+            for (int w = 1; w < FW; w++) v += part[(w * RW + b) * 16 + o];
             v = (o < a.NH) ? v + hb : 0.f;
             if (b < nb) a.raw[((int64_t)s * a.Bl + b0 + b) * 16 + o] = v;
         }
@@ -591,35 +679,38 @@ __global__ __launch_bounds__(FT) void k_head_bwd(HeadBwdArgs a) {
 }
 
 // ---- host side ------------------------------------------------------------------------
-bool fused_fwd_plan(FusedFwdArgs& a, int obs_dim, bool bf16) {
+bool fused_fwd_plan(FusedFwdArgs& a, int obs_dim, bool bf16, int mr) {
+    if (mr != 1 && mr != 2 && mr != 4) return false;
     if (a.L < 1 || a.L > FUSED_MAX_L || a.NH > 16) return false;
     for (int l = 0; l < a.L; l++)
         if (a.out[l] % 64 || a.out[l] > 256) return false;
     if (a.F != a.out[a.L - 1]) return false;
     a.bf16 = bf16 ? 1 : 0;
     const int kz = bf16 ? fwd_nch<true>(obs_dim) * 32 : fused_groups(obs_dim) * FPF * 16;
-    if (16 * (kz / 4) > FGQ * FT) return false;   // gather slots
+    if (16 * (kz / 4) > FGQ * FT) return false;   // gather slots (per 16 rows)
+    const int rw = 16 * mr;
+    a.mr = mr;
     int wmax = 0;
     for (int l = 0; l < a.L; l++) wmax = a.out[l] > wmax ? a.out[l] : wmax;
     int t0, t1;   // tile sizes in floats
     if (bf16) {   // rows cover every chunk of the last group; stride = 32 bytes mod 256
         a.sx = fwd_groups<true>(obs_dim) * FPF * 32 + 16;
         a.sh = ((wmax + 127) & ~127) + 16;
-        t0 = 8 * a.sx;
-        t1 = 8 * a.sh;
+        t0 = rw * a.sx / 2;
+        t1 = rw * a.sh / 2;
     } else {
         a.sx = fused_stride(kz);
         a.sh = fused_stride(wmax);
-        t0 = 16 * a.sx;
-        t1 = 16 * a.sh;
+        t0 = rw * a.sx;
+        t1 = rw * a.sh;
     }
     int b0 = t0 > t1 ? t0 : t1, b1 = t1;
-    if (b0 < FW * 256) b0 = FW * 256;
-    if (b1 < FW * 256) b1 = FW * 256;
+    if (b0 < FW * rw * 16) b0 = FW * rw * 16;   // head partials [FW][rw][16]
+    if (b1 < FW * rw * 16) b1 = FW * rw * 16;
     a.buf0 = (b0 + 3) & ~3;
     a.buf1 = (b1 + 3) & ~3;
     for (int l = 0; l < a.L; l++) a.kpad[l] = bf16 ? fwd_nch<true>(a.in[l]) * 32 : fused_groups(a.in[l]) * FPF * 16;
-    return (a.buf0 + a.buf1) * 4 <= 64 * 1024;
+    return (a.buf0 + a.buf1) * 4 <= (mr == 1 ? 64 : 160) * 1024;
 }
 
 int fused_wblk_bytes(bool bf16, int rows, int kpad) { return rows * kpad * (bf16 ? 2 : 4); }
@@ -643,15 +734,21 @@ int launch_fused_fwd(const FusedFwdArgs& a, int act, hipStream_t s) {
     const dim3 grid(a.tiles * a.nstreams), block(FT);
     size_t shm = (size_t)(a.buf0 + a.buf1) * 4;
     if (shm < (size_t)DQNX_FUSED_LDS_MIN) shm = DQNX_FUSED_LDS_MIN;
+#define FUSED_FWD_MR(ACTV, NLV, BFV, MRV)                                                            \
+    do {                                                                                             \
+        if (shm > 64 * 1024) allow_lds(k_mlp_fwd<ACTV, NLV, BFV, MRV>, 160 * 1024);                  \
+        hipLaunchKernelGGL((k_mlp_fwd<ACTV, NLV, BFV, MRV>), grid, block, shm, s, a);                \
+    } while (0)
+#define FUSED_FWD_BF(ACTV, NLV, BFV)                                                                 \
+    do {                                                                                             \
+        if (a.mr == 4) FUSED_FWD_MR(ACTV, NLV, BFV, 4);                                              \
+        else if (a.mr == 2) FUSED_FWD_MR(ACTV, NLV, BFV, 2);                                         \
+        else FUSED_FWD_MR(ACTV, NLV, BFV, 1);                                                        \
+    } while (0)
 #define FUSED_FWD_CASE(ACTV, NLV)                                                                    \
     do {                                                                                             \
-        if (a.bf16) {                                                                                \
-            if (shm > 64 * 1024) allow_lds(k_mlp_fwd<ACTV, NLV, true>, 160 * 1024);                  \
-            hipLaunchKernelGGL((k_mlp_fwd<ACTV, NLV, true>), grid, block, shm, s, a);                \
-        } else {                                                                                     \
-            if (shm > 64 * 1024) allow_lds(k_mlp_fwd<ACTV, NLV, false>, 160 * 1024);                 \
-            hipLaunchKernelGGL((k_mlp_fwd<ACTV, NLV, false>), grid, block, shm, s, a);               \
-        }                                                                                            \
+        if (a.bf16) FUSED_FWD_BF(ACTV, NLV, true);                                                   \
+        else FUSED_FWD_BF(ACTV, NLV, false);                                                         \
     } while (0)
     const bool relu = act == DQNX_ACT_RELU;
     switch (a.L) {
@@ -661,6 +758,8 @@ int launch_fused_fwd(const FusedFwdArgs& a, int act, hipStream_t s) {
         default: return set_error(DQNX_EUNSUPPORTED, "fused forward: %d dense layers", a.L);
     }
 #undef FUSED_FWD_CASE
+#undef FUSED_FWD_BF
+#undef FUSED_FWD_MR
     DQNX_HIP_CHECK(hipGetLastError());
     return DQNX_OK;
 }

@@ -320,6 +320,7 @@ struct FusedFwdArgs {
     const float* rew;
     const float* done;
     int bf16;                    // DQNX_COMPUTE_BF16: bf16 LDS tiles, bf16 blocked weights, bf16 MFMA
+    int mr;                      // 16-row tiles per workgroup (1, 2 or 4; `tiles` counts 16*mr-row tiles)
     int sx, sh;                  // LDS row strides (elements: floats, or bf16 under bf16) of the input / hidden tiles
     int buf0, buf1;              // LDS buffer sizes (floats)
     int kpad[FUSED_MAX_L];       // layer inputs zero padded to kpad (blocked copies): fp32 a multiple of 64, bf16 of 32
@@ -380,7 +381,7 @@ struct DwSeamArgs {
 };
 int dw_seam_tiles(BwdArgs& b);   // fills the grids; returns the number of parameter tiles
 int launch_dw_seam(const DwSeamArgs& a, hipStream_t s);
-bool fused_fwd_plan(FusedFwdArgs& a, int obs_dim, bool bf16);   // fills sx/sh/buf/kpad; false if unsupported
+bool fused_fwd_plan(FusedFwdArgs& a, int obs_dim, bool bf16, int mr);   // fills sx/sh/buf/kpad; false if unsupported
 int fused_wblk_bytes(bool bf16, int rows, int kpad);          // one blocked weight copy
 int launch_fused_fwd(const FusedFwdArgs& a, int act, hipStream_t s);
 int launch_head_bwd(const HeadBwdArgs& a, int act, hipStream_t s);

@@ -165,6 +165,19 @@ def test_gpu_bf16_per_learn_matches_bf16_oracle(obs_dim, batch, cap, n_fill, see
     _compare_weights(emu, eng)
 
 
+@pytest.mark.parametrize("mr", ["1", "2", "4"])
+def test_gpu_bf16_forward_row_tiles(monkeypatch, mr):
+    """bf16 fused forward with 16-, 32- and 64-row workgroups (ragged batch)."""
+    monkeypatch.setenv("DQNX_FWD_MR", mr)
+    emu, ref, eng = make_bf16_pair("DuelingDoubleDQNAgent", 284, 1000, 20000, 20000, 43)
+    for step in range(2):
+        rec = emu.train_step()
+        eng.learn_step(soft_update=True)
+        torch.cuda.synchronize()
+        _check_step(eng, rec, None, step)
+        _compare_weights(emu, eng)
+
+
 def test_gpu_bf16_graph_and_eager_identical():
     outs = []
     for graphs in (True, False):

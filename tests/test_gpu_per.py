@@ -14,6 +14,7 @@ import pytest
 import torch
 
 from oracle import ref as O
+from parity import assert_grad_close
 
 pytestmark = pytest.mark.gpu
 
@@ -163,7 +164,7 @@ def test_gpu_per_learn_matches_oracle(obs_dim, batch, cap, n_fill, seed):
         assert abs(eng.loss() - rec.loss) <= 1e-5 * max(1.0, abs(rec.loss))
         g = eng.param_views(eng.grads[:-1])
         for k, ref in rec.grads.items():
-            np.testing.assert_allclose(g[k].cpu().numpy(), ref.numpy(), atol=2e-6, rtol=1e-4, err_msg=k)
+            assert_grad_close(g[k].cpu().numpy(), ref.numpy(), k)
         # the tree follows |delta| computed on two devices: equal when the fp32 |delta| agree
         same = np.array_equal(eng.per_abs_td.cpu().numpy(), rec.abs_td.reshape(-1).astype(np.float32))
         assert_tree_equal(eng, oracle.replay.replay_buffer, exact=same)
