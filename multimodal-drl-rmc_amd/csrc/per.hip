@@ -19,7 +19,8 @@
 
 namespace dqnx {
 
-constexpr int PER_NT = 1024;
+constexpr int PER_NT = 1024;   // threads of the one-workgroup tracking kernel (256 x 32 items measured
+                               // slower: serial per-item LDS lookups, strided LDS stores)
 constexpr int PER_TOP = 2047;            // nodes of depth <= 10, accumulated in LDS by k_per_update
 constexpr int PER_IPT = PER_CHUNK / PER_NT;
 
@@ -213,7 +214,7 @@ __global__ __launch_bounds__(PER_SNT) void k_per_sample(PerSampleArgs a) {
 }
 
 // ---------------------------------------------------------------------------------------
-// block scan / reduce helpers (1024 threads = 16 waves)
+// block scan / reduce helpers (PER_NT threads)
 // ---------------------------------------------------------------------------------------
 constexpr int PER_NW = PER_NT / 64;
 
@@ -389,20 +390,42 @@ __global__ __launch_bounds__(PER_NT) void k_per_update(PerUpdateArgs a) {
     const int64_t base = a.cap - 1;
     float pv[PER_IPT];
     int32_t lv[PER_IPT];
-#pragma unroll
-    for (int k = 0; k < PER_IPT; k++) {   // consecutive items per thread (scan order)
-        const int i = tid * PER_IPT + k;
-        pv[k] = 0.f;
-        lv[k] = -1;
-        if (i < n) {
-            lv[k] = a.wl[i];
-            pv[k] = a.wp[i];
-            Ls[i] = lv[k];
-            Ps[i] = pv[k];
-        }
-    }
+    // the tracked max / min leaves first (a dependent pair of round trips)
     int mx_i = (int)a.ctrl->per_max_idx, mn_i = (int)a.ctrl->per_min_idx;
     float mx_v = (float)a.tree[mx_i], mn_v = (float)a.tree[mn_i];
+    // PER_IPT consecutive items per thread (scan order): 16-byte loads (the workspace holds
+    // PER_CHUNK items, so the tail past n stays in bounds and is masked below)
+    static_assert(PER_IPT % 4 == 0, "16-byte loads");
+    {
+        const int4* wl4 = reinterpret_cast<const int4*>(a.wl) + (PER_IPT / 4) * tid;
+        const float4* wp4 = reinterpret_cast<const float4*>(a.wp) + (PER_IPT / 4) * tid;
+        int4 l4[PER_IPT / 4];
+        float4 p4[PER_IPT / 4];
+#pragma unroll
+        for (int q = 0; q < PER_IPT / 4; q++) {
+            l4[q] = wl4[q];
+            p4[q] = wp4[q];
+        }
+#pragma unroll
+        for (int q = 0; q < PER_IPT / 4; q++) {
+            lv[4 * q] = l4[q].x; lv[4 * q + 1] = l4[q].y; lv[4 * q + 2] = l4[q].z; lv[4 * q + 3] = l4[q].w;
+            pv[4 * q] = p4[q].x; pv[4 * q + 1] = p4[q].y; pv[4 * q + 2] = p4[q].z; pv[4 * q + 3] = p4[q].w;
+        }
+    }
+    DQNX_STAMP(a.stamps, 8);
+#pragma unroll
+    for (int k = 0; k < PER_IPT; k++) {
+        const int i = tid * PER_IPT + k;
+        if (i < n) {
+            Ls[i] = lv[k];
+            Ps[i] = pv[k];
+        } else {
+            lv[k] = -1;
+            pv[k] = 0.f;
+        }
+    }
+    DQNX_STAMP(a.stamps, 9);
+    DQNX_STAMP(a.stamps, 10);
     __syncthreads();
     DQNX_STAMP(a.stamps, 57);
     DQNX_STAMP(a.stamps, 58);
@@ -421,7 +444,9 @@ __global__ __launch_bounds__(PER_NT) void k_per_update(PerUpdateArgs a) {
             }
         }
         Track totv;
+        DQNX_STAMP(a.stamps, 11);
         const Track exv = track_scan(own, sht, &totv);
+        DQNX_STAMP(a.stamps, 12);
         // pass 2: which items (re)take the max / min, given the running values BEFORE each
         Track ownl{-INFINITY, INFINITY, -1, -1};
         {
@@ -438,7 +463,9 @@ __global__ __launch_bounds__(PER_NT) void k_per_update(PerUpdateArgs a) {
             }
         }
         Track totl;
+        DQNX_STAMP(a.stamps, 13);
         const Track exl = track_scan(ownl, sht, &totl);
+        DQNX_STAMP(a.stamps, 14);
         // pass 3: the first item that rewrites the current max / min leaf without retaking it
         int lastx = exl.lx, lastn = exl.ln;
         int mytrig = n;
@@ -469,6 +496,7 @@ __global__ __launch_bounds__(PER_NT) void k_per_update(PerUpdateArgs a) {
                 }
             }
         }
+        DQNX_STAMP(a.stamps, 15);
         if (!__syncthreads_or(mytrig < n)) {   // no rescan left: fold the scans into the state
             if (totl.lx >= 0) mx_i = Ls[totl.lx];
             if (totl.ln >= 0) mn_i = Ls[totl.ln];

@@ -35,4 +35,6 @@ for step in range(5):
     s = list(out)
     ps = [s[j + 1] - s[j] for j in range(3)]
     pu = [s[57] - s[56], s[59] - s[58], s[61] - s[59]]
-    print(f"step {step}: per_sample cyc {ps} total {s[3] - s[0]}; per_update cyc {pu} total {s[61] - s[56]}")
+    det = [s[8] - s[56], s[9] - s[8], s[10] - s[9], s[57] - s[10], s[11] - s[58], s[12] - s[11], s[13] - s[12],
+           s[14] - s[13], s[15] - s[14], s[59] - s[15]]
+    print(f"step {step}: per_sample cyc {ps} total {s[3] - s[0]}; per_update cyc {pu} total {s[61] - s[56]}; detail {det}")
