@@ -705,6 +705,17 @@ void build_fused_steps(dqnx_engine* e, int flags, int32_t* idx, int32_t* phys, s
             bytes += 4.0 * (16.0 * Bl + Bl * np.F + ba.dw_slices * (double)np.head_params);
         }
         const char* sv = getenv("DQNX_DW_SEAM");
+        if (e->fplan.bf16) {   // bf16 operands, fp32 slabs: the same Adam pass follows
+            dw_bf16_grid(ba);
+            KStep k;
+            k.name = "dw_all";
+            k.flops = flops;
+            k.bytes = bytes;
+            k.run = [=](hipStream_t s) { return launch_dw_bf16(ba, s); };
+            ks.push_back(k);
+            ks.push_back(adam_kstep(e, flags));
+            return;
+        }
         if (!(sv && atoi(sv) == 1)) {   // default: split-K slabs, then the Adam pass
             bwd_level_grid(ba);
             KStep k;

@@ -678,6 +678,185 @@ __global__ __launch_bounds__(FT) void k_head_bwd(HeadBwdArgs a) {
     DQNX_STAMP(a.stamps, 55);
 }
 
+// =====================================================================================
+// Weight gradients in bf16 (DQNX_COMPUTE_BF16): partial[slice] = bf16(dZ)^T [bf16(X) | 1],
+// fp32 accumulate, the same split-K slabs and flat layouts as k_bwd_level (the Adam pass is
+// shared).  32 x 32 or 64 x 64 output tiles, 4 waves, K (samples) in passes of KT.  Operands are read as fp32 rows [k][cols], rounded, and stored TRANSPOSED in LDS
+// ([col][k], k contiguous) so an MFMA fragment (8 consecutive k of one column) is one
+// ds_read_b128; a column stride of KT/2 + 4 dwords makes those reads and the paired-k stores
+// conflict-free.
+// =====================================================================================
+#ifndef DQNX_DWB_KT64
+#define DQNX_DWB_KT64 32
+#endif
+#ifndef DQNX_DWB_KT32
+#define DQNX_DWB_KT32 128
+#endif
+// LDS column stride in dwords (2 bf16 each) for KT samples per pass: KT/2 + 4, i.e. 4 mod 16
+// dwords (b128 fragment reads of 16 consecutive columns hit distinct banks).
+template <int KT>
+struct DwbShape {
+    static constexpr int SD = KT / 2 + 4;
+    static constexpr int KP = KT / 2;   // k pairs per pass
+};
+
+// rows [k0, k0 + KT) x cols [c0, c0 + BT) of a [K][ld] operand; pair index q = (column group of
+// 4) * KP + k pair, q = tid + 256 u.  Column j reads 0 past `ncols`, or 1.0 at j == aug.
+template <int BT, int KT>
+__device__ __forceinline__ void dwb_stage(const float* base, int ld, int ncols, int aug, int c0, int k0, int kend,
+                                          float4 (&v)[(KT / 2) * (BT / 4) / 256 > 0 ? (KT / 2) * (BT / 4) / 256 : 1][2]) {
+    constexpr int KP = DwbShape<KT>::KP, NQ = KP * (BT / 4), NU = NQ / 256 > 0 ? NQ / 256 : 1;
+#pragma unroll
+    for (int u = 0; u < NU; u++) {
+        const int q = threadIdx.x + 256 * u;
+        const int kp = q % KP, cg = q / KP;
+        const int c = c0 + 4 * cg;
+#pragma unroll
+        for (int h = 0; h < 2; h++) {
+            const int k = k0 + 2 * kp + h;
+            float4 x = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (q < NQ && k < kend) {
+                const float* row = base + (int64_t)k * ld;
+                if (c + 3 < ncols) {
+                    x = ld4(row + c);
+                } else if ((c <= aug && aug < c + 4) || c < ncols) {   // the group holding the edge
+                    float e[4];
+#pragma unroll
+                    for (int j = 0; j < 4; j++) e[j] = (c + j < ncols) ? row[c + j] : (c + j == aug ? 1.f : 0.f);
+                    x = make_float4(e[0], e[1], e[2], e[3]);
+                }
+            }
+            v[u][h] = x;
+        }
+    }
+}
+template <int BT, int KT>
+__device__ __forceinline__ void dwb_store(uint32_t* dst,
+                                          const float4 (&v)[(KT / 2) * (BT / 4) / 256 > 0 ? (KT / 2) * (BT / 4) / 256 : 1][2]) {
+    constexpr int KP = DwbShape<KT>::KP, SD = DwbShape<KT>::SD, NQ = KP * (BT / 4), NU = NQ / 256 > 0 ? NQ / 256 : 1;
+#pragma unroll
+    for (int u = 0; u < NU; u++) {
+        const int q = threadIdx.x + 256 * u;
+        if (q >= NQ) continue;
+        const int kp = q % KP, cg = q / KP;
+        uint32_t* p = dst + (4 * cg) * SD + kp;
+        p[0 * SD] = bf16_pack2(v[u][0].x, v[u][1].x);
+        p[1 * SD] = bf16_pack2(v[u][0].y, v[u][1].y);
+        p[2 * SD] = bf16_pack2(v[u][0].z, v[u][1].z);
+        p[3 * SD] = bf16_pack2(v[u][0].w, v[u][1].w);
+    }
+}
+
+// BT x BT output tile (32 or 64), 4 waves of (BT/32) x (BT/32) 16x16 tiles, KT samples per pass.
+template <int BT, int KT>
+__global__ __launch_bounds__(256) void k_dw_bf16(BwdArgs a) {
+    static_assert(BT == 32 || BT == 64, "tile");
+    static_assert(KT % 32 == 0, "whole MFMA chunks");
+    constexpr int T = BT / 32, SD = DwbShape<KT>::SD;
+    constexpr int NU = (KT / 2) * (BT / 4) / 256 > 0 ? (KT / 2) * (BT / 4) / 256 : 1;
+    static_assert((KT / 2) * (BT / 4) <= 256 * NU, "pairs per thread");
+    __shared__ __attribute__((aligned(16))) uint32_t lds[2 * BT * SD];
+    uint32_t* la = lds;            // dZ columns (rows m of the gradient tile)
+    uint32_t* lb = lds + BT * SD;  // X columns (+ ones)
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int i = lane & 15, g = lane >> 4;
+    const int wm = wid >> 1, wn = wid & 1;
+    int b = blockIdx.x;
+    int p = 0;
+    while (p + 1 < a.ndw && b >= a.dw[p].blocks) { b -= a.dw[p].blocks; p++; }
+    const DwProblem& d = a.dw[p];
+    b = xcd_remap(b, d.blocks);
+    const int bx = b % d.grid_x;
+    const int t2 = b / d.grid_x;
+    const int by = t2 % d.grid_y, bz = t2 / d.grid_y;
+    const int m0 = by * BT, n0 = bx * BT;
+    const int kb = bz * a.kslice;
+    const int ke = min(a.Bl, kb + a.kslice);
+    floatx4 acc[T][T];
+#pragma unroll
+    for (int tm = 0; tm < T; tm++)
+#pragma unroll
+        for (int tn = 0; tn < T; tn++) acc[tm][tn] = floatx4{0.f, 0.f, 0.f, 0.f};
+    const int ncz = d.out < d.ldz ? d.out : d.ldz;   // dZ columns that exist (head: ldz 16 >= NH)
+    float4 va[NU][2], vb[NU][2];
+    dwb_stage<BT, KT>(d.dZ, d.ldz, ncz, -1, m0, kb, ke, va);
+    dwb_stage<BT, KT>(d.X, d.ldx, d.in, d.in, n0, kb, ke, vb);
+    for (int k0 = kb; k0 < ke; k0 += KT) {
+        __syncthreads();   // previous pass's fragments read
+        dwb_store<BT, KT>(la, va);
+        dwb_store<BT, KT>(lb, vb);
+        __syncthreads();
+        if (k0 + KT < ke) {   // next pass in flight during this one's MFMAs
+            dwb_stage<BT, KT>(d.dZ, d.ldz, ncz, -1, m0, k0 + KT, ke, va);
+            dwb_stage<BT, KT>(d.X, d.ldx, d.in, d.in, n0, k0 + KT, ke, vb);
+        }
+#pragma unroll
+        for (int ch = 0; ch < KT / 32; ch++) {
+            u32x4 fa[T], fb[T];
+#pragma unroll
+            for (int t = 0; t < T; t++) {
+                fa[t] = *reinterpret_cast<const u32x4*>(la + (wm * 16 * T + t * 16 + i) * SD + 16 * ch + 4 * g);
+                fb[t] = *reinterpret_cast<const u32x4*>(lb + (wn * 16 * T + t * 16 + i) * SD + 16 * ch + 4 * g);
+            }
+#pragma unroll
+            for (int tm = 0; tm < T; tm++)
+#pragma unroll
+                for (int tn = 0; tn < T; tn++) acc[tm][tn] = mfma16x16x32bf16(fa[tm], fb[tn], acc[tm][tn]);
+        }
+    }
+    // rows beyond `out` / columns beyond `in` (+1) of the tile are not stored
+    float* part = d.partial + (int64_t)bz * d.pstride;
+#pragma unroll
+    for (int tn = 0; tn < T; tn++) {
+        const int col = n0 + wn * 16 * T + tn * 16 + i;
+        if (col > d.in) continue;
+#pragma unroll
+        for (int tm = 0; tm < T; tm++)
+#pragma unroll
+            for (int r = 0; r < 4; r++) {
+                const int row = m0 + wm * 16 * T + tm * 16 + 4 * g + r;
+                if (row >= d.out) continue;
+                int64_t o;
+                if (d.head_kind < 0) o = (col < d.in) ? (int64_t)row * d.in + col : (int64_t)d.out * d.in + row;
+                else o = (col < d.in) ? head_w_off(d.head_kind, row, d.in) + col : head_b_off(d.head_kind, row, d.in, d.A);
+                part[o] = acc[tm][tn][r];
+            }
+    }
+}
+
+// Tile size: 64 x 64 when that still gives >= 512 workgroups (large batches: fewer operand
+// re-reads), else 32 x 32 (B=1024: 132 workgroups of 64 x 64 left the chip idle).
+static int dw_bf16_tile(const BwdArgs& a) {
+    int n64 = 0;
+    for (int p = 0; p < a.ndw; p++)
+        n64 += ((a.dw[p].in + 1 + 63) / 64) * ((a.dw[p].out + 63) / 64) * a.dw_slices;
+    return n64 >= 512 ? 64 : 32;
+}
+
+void dw_bf16_grid(BwdArgs& a) {
+    const int bt = dw_bf16_tile(a);
+    for (int p = 0; p < a.ndw; p++) {
+        DwProblem& d = a.dw[p];
+        d.grid_x = (d.in + 1 + bt - 1) / bt;
+        d.grid_y = (d.out + bt - 1) / bt;
+        d.blocks = d.grid_x * d.grid_y * a.dw_slices;
+    }
+}
+
+int launch_dw_bf16(const BwdArgs& a, hipStream_t s) {
+    int blocks = 0;
+    for (int p = 0; p < a.ndw; p++) blocks += a.dw[p].blocks;
+    for (int p = 0; p < a.ndw; p++)   // 16-byte row loads
+        if (a.dw[p].ldx % 4 || a.dw[p].ldz % 4)
+            return set_error(DQNX_EUNSUPPORTED, "bf16 weight gradients need row strides that are multiples of 4");
+    // measured: 64 x 64 tiles best with 32-sample passes (64: +1.7 us, 128: +6 us at B=8192);
+    // 32 x 32 tiles with 128-sample passes (the fp32 kernel's depth)
+    if (dw_bf16_tile(a) == 64) hipLaunchKernelGGL((k_dw_bf16<64, DQNX_DWB_KT64>), dim3(blocks), dim3(256), 0, s, a);
+    else hipLaunchKernelGGL((k_dw_bf16<32, DQNX_DWB_KT32>), dim3(blocks), dim3(256), 0, s, a);
+    DQNX_HIP_CHECK(hipGetLastError());
+    return DQNX_OK;
+}
+
 // ---- host side ------------------------------------------------------------------------
 bool fused_fwd_plan(FusedFwdArgs& a, int obs_dim, bool bf16, int mr) {
     if (mr != 1 && mr != 2 && mr != 4) return false;

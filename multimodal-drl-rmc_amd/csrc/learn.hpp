@@ -385,6 +385,8 @@ bool fused_fwd_plan(FusedFwdArgs& a, int obs_dim, bool bf16, int mr);   // fills
 int fused_wblk_bytes(bool bf16, int rows, int kpad);          // one blocked weight copy
 int launch_fused_fwd(const FusedFwdArgs& a, int act, hipStream_t s);
 int launch_head_bwd(const HeadBwdArgs& a, int act, hipStream_t s);
+void dw_bf16_grid(BwdArgs& a);                               // 64x64 tiles of k_dw_bf16
+int launch_dw_bf16(const BwdArgs& a, hipStream_t s);          // bf16 split-K weight gradients
 
 int launch_im2col(const Im2colArgs& a, hipStream_t s);
 int launch_flatten_concat(const FlattenArgs& a, hipStream_t s);

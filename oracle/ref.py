@@ -225,7 +225,7 @@ class _Bf16Linear(torch.autograd.Function):
     this is the checker for BASELINE config 5's bf16 variant.
       y  = bf16(x) bf16(W)^T + b
       dx = bf16(dy) bf16(W)   (dense layers >= 2: the engine's dZ chain)  /  dy W  (head)
-      dW = dy^T x, db = sum dy (fp32: the engine's weight-gradient kernel is fp32)"""
+      dW = bf16(dy)^T bf16(x), db = sum bf16(dy)   (k_dw_bf16: the bias is the ones column)"""
 
     @staticmethod
     def forward(ctx, x, W, b, round_dx):
@@ -237,7 +237,8 @@ class _Bf16Linear(torch.autograd.Function):
     def backward(ctx, dy):
         x, W = ctx.saved_tensors
         dx = bf16r(dy) @ bf16r(W) if ctx.round_dx else dy @ W
-        return dx, dy.t() @ x, dy.sum(0), None
+        dyr = bf16r(dy)
+        return dx, dyr.t() @ bf16r(x), dyr.sum(0), None
 
 
 def _linear(x, W, b, bf16: bool, round_dx: bool = True):

@@ -139,7 +139,7 @@ def test_oracle_learn_golden(path):
 
 
 def test_bf16_emulation_linear_matches_explicit_formula():
-    """oracle bf16 mode: y = bf16(x) bf16(W)^T + b; dx = bf16(dy) bf16(W) (or dy W); dW = dy^T x."""
+    """oracle bf16 mode: y = bf16(x) bf16(W)^T + b; dx = bf16(dy) bf16(W) (or dy W); dW = bf16(dy)^T bf16(x)."""
     g = torch.Generator().manual_seed(0)
     x = torch.randn(7, 37, generator=g, requires_grad=True)
     W = torch.randn(11, 37, generator=g, requires_grad=True)
@@ -152,8 +152,8 @@ def test_bf16_emulation_linear_matches_explicit_formula():
         gx, gW, gb = torch.autograd.grad(y, (x, W, b), dy)
         want_dx = O.bf16r(dy) @ bW if round_dx else dy @ W.detach()
         assert torch.equal(gx, want_dx)
-        assert torch.equal(gW, dy.t() @ x.detach())
-        assert torch.equal(gb, dy.sum(0))
+        assert torch.equal(gW, O.bf16r(dy).t() @ bx)
+        assert torch.equal(gb, O.bf16r(dy).sum(0))
     # bf16 rounding is round-to-nearest-even on the 16 dropped bits
     v = torch.tensor([1.0 + 2 ** -8, 1.0 + 3 * 2 ** -8, 1.0 + 2 ** -8 + 2 ** -20])
     assert O.bf16r(v).tolist() == [1.0, 1.0 + 2 ** -6, 1.0 + 2 ** -7]
