@@ -605,8 +605,15 @@ void build_fused_steps(dqnx_engine* e, int flags, int32_t* idx, int32_t* phys, s
         ha.Bl = e->Bl;
         ha.nsplit = 1;
         ha.bf16 = e->fplan.bf16;
-        if (L >= 2 && np.dense[0].out % (2 * 64) == 0) ha.nsplit = 2;   // dZ_1 columns over 2 workgroups
-        if (const char* ns = getenv("DQNX_HEAD_SPLIT")) { const int v = atoi(ns); if (v == 1 || (v == 2 && ha.nsplit == 2)) ha.nsplit = v; }
+        // dZ_1's columns over nsplit workgroups per 16-sample tile: the largest of 4, 2 that keeps
+        // tiles * nsplit <= 256 (one workgroup per CU).  Measured at MLP-284: B=1024 head 6.5 ->
+        // 6.0 us with 4 parts; B=4096 best unsplit (9.2 vs 9.5 with 2, 13.8 with 4)
+        for (int v : {4, 2})
+            if (ha.nsplit == 1 && L >= 2 && np.dense[0].out % (v * 16) == 0 && e->tiles * v <= 256) ha.nsplit = v;
+        if (const char* ns = getenv("DQNX_HEAD_SPLIT")) {
+            const int v = atoi(ns);
+            if (v == 1 || ((v == 2 || v == 4) && L >= 2 && np.dense[0].out % (v * 16) == 0)) ha.nsplit = v;
+        }
         ha.A = A;
         ha.NH = np.NH;
         ha.F = np.F;
