@@ -166,13 +166,13 @@ def test_gpu_learn_forward_row_tiles_match_oracle(monkeypatch, mr, algo, obs_dim
     _check_learn(*make_pair(algo, obs_dim, batch, capacity, n_fill, seed))
 
 
-@pytest.mark.parametrize("split", ["1", "2"])
+@pytest.mark.parametrize("split", ["2", "4"])
 def test_gpu_fused_head_split_identical(monkeypatch, split):
-    """The fused plan's head/dZ-chain kernel with the last dZ split over 1 or 2 workgroups per
-    tile gives bitwise the same step (each column is computed the same way either way)."""
+    """The fused plan's head/dZ-chain kernel with the last dZ split over 2 or 4 workgroups per
+    tile gives bitwise the same step as unsplit (each column is computed the same way)."""
     monkeypatch.setenv("DQNX_HEAD_SPLIT", split)
     o, e = make_pair("DuelingDoubleDQNAgent", 284, 512, 4000, 4000, 31)
-    monkeypatch.setenv("DQNX_HEAD_SPLIT", "2" if split == "1" else "1")
+    monkeypatch.setenv("DQNX_HEAD_SPLIT", "1")
     o2, e2 = make_pair("DuelingDoubleDQNAgent", 284, 512, 4000, 4000, 31)
     for _ in range(3):
         e.learn_step(soft_update=True)
