@@ -46,14 +46,14 @@ constexpr int FGQ = 6;     // float4 gather slots per thread (input tile <= FGQ 
 
 __host__ __device__ __forceinline__ int fused_stride(int K) { return ((K + 63) & ~63) + 8; }
 __host__ __device__ __forceinline__ int fused_groups(int K) { return (K + 16 * FPF - 1) / (16 * FPF); }
-// Chunks of one weight stream over K and MFMA groups of FPF chunks.  fp32: 16-deep chunks,
-// K padded to whole groups (the blocked copy holds the zero chunks).  bf16: 32-deep chunks,
-// K padded to 32 only; chunks past nch in the last group are skipped (their A columns in
-// LDS are not zeroed).
+// Chunks of one weight stream over K and MFMA groups of FPF chunks: 16-deep chunks (fp32) or
+// 32-deep (bf16), K padded to a whole chunk only; chunks past nch in the last group are
+// skipped (their A columns in LDS are not zeroed).  fp32 layer 1 of MLP-284: 18 chunks
+// instead of the 20 of whole groups.
 template <bool BF>
-__host__ __device__ __forceinline__ int fwd_nch(int K) { return BF ? (K + 31) / 32 : fused_groups(K) * FPF; }
+__host__ __device__ __forceinline__ int fwd_nch(int K) { return BF ? (K + 31) / 32 : (K + 15) / 16; }
 template <bool BF>
-__host__ __device__ __forceinline__ int fwd_groups(int K) { return BF ? (fwd_nch<true>(K) + FPF - 1) / FPF : fused_groups(K); }
+__host__ __device__ __forceinline__ int fwd_groups(int K) { return (fwd_nch<BF>(K) + FPF - 1) / FPF; }
 
 // Workgroup barrier for LDS hand-offs only.  __syncthreads() also drains every outstanding
 // global access of the wave (vmcnt(0)) -- here that would wait for the activation stores
@@ -141,6 +141,7 @@ __device__ __forceinline__ void mma_group(const void* ap_, int ch0, int nch, con
         for (int p = 0; p < FPF; p++) av[p] = *reinterpret_cast<const float4*>(ap + (ch0 + p) * 16);
 #pragma unroll
         for (int p = 0; p < FPF; p++) {
+            if (ch0 + p >= nch) break;
 #pragma unroll
             for (int t = 0; t < TN; t++) acc[t] = mfma16x16x4(av[p].x, w[p][t].x, acc[t]);
 #pragma unroll
@@ -205,6 +206,7 @@ __device__ __forceinline__ void mma_group_mr(const void* ap_, int rowoff, int ch
                                              floatx4 (&acc)[MR][2]) {
 #pragma unroll
     for (int p = 0; p < FPF; p++) {
+        if (ch0 + p >= nch) break;
         if constexpr (!BF) {
             const float* ap = static_cast<const float*>(ap_);
             float4 av[MR];
@@ -227,7 +229,6 @@ __device__ __forceinline__ void mma_group_mr(const void* ap_, int rowoff, int ch
 #pragma unroll
                 for (int t = 0; t < TN; t++) acc[m][t] = mfma16x16x4(av[m].w, w[p][t].w, acc[m][t]);
         } else {
-            if (ch0 + p >= nch) break;
             const uint16_t* ap = static_cast<const uint16_t*>(ap_);
             u32x4 av[MR];
 #pragma unroll
@@ -309,7 +310,7 @@ __global__ __launch_bounds__(FT) void k_mlp_fwd(FusedFwdArgs a) {
     //     Issue order matters (vmcnt retires in order): ring slots first, then layer 1's
     //     weight stream (independent of the rows), then the dependent row loads.
     {
-        const int kz = BF ? fwd_nch<true>(a.in[0]) * 32 : fused_groups(a.in[0]) * FPF * 16;   // columns multiplied
+        const int kz = fwd_nch<BF>(a.in[0]) * (BF ? 32 : 16);   // columns multiplied
         const int q4 = kz >> 2, rs4 = a.ring_stride >> 2;
         // branch-free: every slot loads (clamped row / column) and selects zero afterwards,
         // so the loads issue back to back (one phys round trip, then one ring round trip)
@@ -865,7 +866,7 @@ bool fused_fwd_plan(FusedFwdArgs& a, int obs_dim, bool bf16, int mr) {
         if (a.out[l] % 64 || a.out[l] > 256) return false;
     if (a.F != a.out[a.L - 1]) return false;
     a.bf16 = bf16 ? 1 : 0;
-    const int kz = bf16 ? fwd_nch<true>(obs_dim) * 32 : fused_groups(obs_dim) * FPF * 16;
+    const int kz = bf16 ? fwd_nch<true>(obs_dim) * 32 : fwd_nch<false>(obs_dim) * 16;
     if (16 * (kz / 4) > FGQ * FT) return false;   // gather slots (per 16 rows)
     const int rw = 16 * mr;
     a.mr = mr;
@@ -888,7 +889,7 @@ bool fused_fwd_plan(FusedFwdArgs& a, int obs_dim, bool bf16, int mr) {
     if (b1 < FW * rw * 16) b1 = FW * rw * 16;
     a.buf0 = (b0 + 3) & ~3;
     a.buf1 = (b1 + 3) & ~3;
-    for (int l = 0; l < a.L; l++) a.kpad[l] = bf16 ? fwd_nch<true>(a.in[l]) * 32 : fused_groups(a.in[l]) * FPF * 16;
+    for (int l = 0; l < a.L; l++) a.kpad[l] = bf16 ? fwd_nch<true>(a.in[l]) * 32 : fwd_nch<false>(a.in[l]) * 16;
     return (a.buf0 + a.buf1) * 4 <= (mr == 1 ? 64 : 160) * 1024;
 }
 
