@@ -199,6 +199,7 @@ struct dqnx_engine {
     // makes dZ_{L-1}, one full-K dW + Adam launch
     int bwd_plan = 0;
     FusedFwdArgs fplan;     // LDS geometry of the fused plan (valid when bwd_plan == 2)
+    int fsplit = 1;         // layer-1 column parts of the split forward (1: one forward launch)
     bool pf_valid = false;   // a prefetched minibatch for the next step sits in slot pf_slot
     int pf_slot = 0;
 };
@@ -594,8 +595,30 @@ void build_fused_steps(dqnx_engine* e, int flags, int32_t* idx, int32_t* phys, s
         for (int l = 0; l < L; l++) hsum += np.dense[l].out;
         k.bytes = 4.0 * (nstreams * Bl * np.dense[0].in + Bl * np.dense[0].in + Bl * hsum + 3.0 * Bl * 16)
                   + 2.0 * (wbytes + 4.0 * np.head_params);
-        k.run = [=](hipStream_t s) { return launch_fused_fwd(fa, act, s); };
-        ks.push_back(k);
+        if (e->fsplit > 1 && L >= 2 && fa.mr == 1) {
+            // layer 1 on csplit workgroups per row tile, then layers 2.. + head (H_1 via HBM)
+            const double w0 = (double)np.dense[0].in * np.dense[0].out;
+            FusedFwdArgs f1 = fa, f2 = fa;
+            f1.phase = 1;
+            f1.csplit = e->fsplit;
+            f2.phase = 2;
+            KStep k1, k2;
+            k1.name = "mlp_fwd_l1";
+            k1.flops = nstreams * Bl * 2.0 * w0;
+            k1.bytes = 4.0 * (nstreams * Bl * (np.dense[0].in + np.dense[0].out) + Bl * np.dense[0].in)
+                       + 2.0 * (e->fplan.bf16 ? 2.0 : 4.0) * w0;
+            k1.run = [=](hipStream_t s) { return launch_fused_fwd(f1, act, s); };
+            k2.name = "mlp_fwd_rest";
+            k2.flops = k.flops - k1.flops;
+            k2.bytes = 4.0 * (nstreams * Bl * np.dense[0].out + Bl * (hsum - np.dense[0].out) + 3.0 * Bl * 16)
+                       + 2.0 * (wbytes - (e->fplan.bf16 ? 2.0 : 4.0) * w0 + 4.0 * np.head_params);
+            k2.run = [=](hipStream_t s) { return launch_fused_fwd(f2, act, s); };
+            ks.push_back(k1);
+            ks.push_back(k2);
+        } else {
+            k.run = [=](hipStream_t s) { return launch_fused_fwd(fa, act, s); };
+            ks.push_back(k);
+        }
     }
     // 3. head / TD / Huber / dZ chain (R:dqn/agent.py:209-221; PER :259-267)
     {
@@ -1469,6 +1492,17 @@ int dqnx_engine_create(const dqnx_config* cfg, dqnx_engine** out) {
         if (const char* v = getenv("DQNX_FWD_MR")) mr = atoi(v);
         FusedFwdArgs trial = e->fplan;
         if (mr != 1 && fused_fwd_plan(trial, c.net.obs_dim, e->fplan.bf16 != 0, mr)) e->fplan = trial;
+        // opt-in (DQNX_FWD_SPLIT=2|4): layer 1 in a launch of its own over 2 or 4 column parts
+        // per row tile.  Measured slower (B=1024: layer 1 alone 12.1 us on 384 workgroups vs
+        // 15.7 us for the whole one-launch forward; step 47.7 vs 45.2 us): the weight bytes
+        // streamed from L2 stay the same in total, so more workgroups do not help
+        if (e->fplan.mr == 1 && e->np.dense.size() >= 2) {
+            if (const char* v = getenv("DQNX_FWD_SPLIT")) {
+                const int w = atoi(v);
+                if (w <= 1) e->fsplit = 1;
+                else if (e->np.dense[0].out % (16 * w) == 0) e->fsplit = w;
+            }
+        }
     }
     e->setsize = sample_setsize(e->Bs);
     const int L = (int)e->np.dense.size();

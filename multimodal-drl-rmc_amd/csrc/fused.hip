@@ -282,17 +282,23 @@ __device__ __forceinline__ void wave_mma_rows(const void* As, int sa, int ngroup
 // with its own wait (eight of them serialised the head kernel's prologue).
 // BF: bf16 activation tiles in LDS (row strides sx / sh in bf16 elements), bf16 blocked
 // weights, 16x16x32 bf16 MFMAs; accumulation, bias, activation and the H stores stay fp32.
-template <int ACT, int NL, bool BF, int MR>
+// PH (phase): 0 the whole forward; 1 only layer 1, its columns split over a.csplit
+// workgroups per row tile, writing H_1 of every stream to HBM; 2 layers 2.. + head, reading
+// H_1 back (the split-layer pair: twice or four times the workgroups on the widest GEMM).
+template <int ACT, int NL, bool BF, int MR, int PH>
 __global__ __launch_bounds__(FT) void k_mlp_fwd(FusedFwdArgs a) {
     constexpr int RW = 16 * MR;          // rows per workgroup
     constexpr int GQ = FGQ * MR;         // float4 gather slots per thread
+    constexpr int LB = PH == 2 ? 1 : 0, LE = PH == 1 ? 1 : NL;   // layers of this launch
     extern __shared__ __attribute__((aligned(16))) float lds[];
     // LDS tile b: pointer arithmetic on `lds` keeps the LDS address space visible to the
     // compiler (ds_read, not flat loads that share the vmcnt counter with the W stream)
 #define FBUF(b) (lds + ((b) ? a.buf0 : 0))
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int i = lane & 15, g = lane >> 4;
-    const int T = xcd_remap(blockIdx.x, a.tiles * a.nstreams);
+    const int nsp = PH == 1 ? a.csplit : 1;
+    const int T0 = xcd_remap(blockIdx.x, a.tiles * a.nstreams * nsp);
+    const int part = T0 % nsp, T = T0 / nsp;   // the parts of one row tile are neighbours (one XCD)
     const int z = T / a.tiles, tile = T - z * a.tiles;
     const int s = a.stream_of[z];
     const int tgt = s == 2 ? 1 : 0;
@@ -300,11 +306,39 @@ __global__ __launch_bounds__(FT) void k_mlp_fwd(FusedFwdArgs a) {
     const float* P = tgt ? a.tparams : a.params;
     const float* ring = (s == 0) ? a.ring_obs : a.ring_next;
     const bool keep = (s == 0);
+    const int coff = PH == 1 ? part * (a.out[0] / nsp) : 0;   // layer-1 columns of this part
 
     DQNX_STAMP(a.stamps, 24);
     float4 wb[FNB][FPF][2];
     WStream ws;
-    WaveCols c = wave_cols(a.out[0]);
+    WaveCols c = wave_cols(PH == 1 ? a.out[0] / nsp : a.out[LB]);
+    if constexpr (PH == 2) {
+        // H_1 rows of this stream, written by the split layer-1 launch -> LDS (zero past the batch)
+        stream_open(a.wblk[tgt][1], a.out[1] >> 4, fwd_nch<BF>(a.in[1]), 0, c, ws, wb);
+        const int N0 = a.out[0], q4 = N0 >> 2;
+        const float* h1 = a.H[0] + (int64_t)s * a.Bl * N0;
+        float4 hv[2 * MR];
+#pragma unroll
+        for (int j = 0; j < 2 * MR; j++) {
+            const int q = tid + j * FT;
+            const int r = q / q4, c4 = q - r * q4;
+            const bool ok = r < nb && r < RW;
+            float4 x = ld4(h1 + (int64_t)(b0 + (ok ? r : 0)) * N0 + 4 * c4);
+            hv[j] = ok ? x : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+#pragma unroll
+        for (int j = 0; j < 2 * MR; j++) {
+            const int q = tid + j * FT;
+            const int r = q / q4, c4 = q - r * q4;
+            if (r < RW) {
+                if constexpr (BF)
+                    *reinterpret_cast<uint2*>(reinterpret_cast<uint16_t*>(FBUF(0)) + r * a.sh + 4 * c4) =
+                        make_uint2(bf16_pack2(hv[j].x, hv[j].y), bf16_pack2(hv[j].z, hv[j].w));
+                else
+                    *reinterpret_cast<float4*>(FBUF(0) + r * a.sh + 4 * c4) = hv[j];
+            }
+        }
+    } else {
 
     // (0) gather the 16 ring rows -> LDS, zero beyond the batch / row; stream 0 keeps a copy.
     //     Issue order matters (vmcnt retires in order): ring slots first, then layer 1's
@@ -314,7 +348,7 @@ __global__ __launch_bounds__(FT) void k_mlp_fwd(FusedFwdArgs a) {
         const int q4 = kz >> 2, rs4 = a.ring_stride >> 2;
         // branch-free: every slot loads (clamped row / column) and selects zero afterwards,
         // so the loads issue back to back (one phys round trip, then one ring round trip)
-        if (DQNX_FUSED_ORDER == 1) stream_open(a.wblk[tgt][0], a.out[0] >> 4, fwd_nch<BF>(a.in[0]), 0, c, ws, wb);
+        if (DQNX_FUSED_ORDER == 1) stream_open(a.wblk[tgt][0], a.out[0] >> 4, fwd_nch<BF>(a.in[0]), coff >> 4, c, ws, wb);
         int32_t slot[GQ];
 #pragma unroll
         for (int j = 0; j < GQ; j++) {
@@ -324,8 +358,9 @@ __global__ __launch_bounds__(FT) void k_mlp_fwd(FusedFwdArgs a) {
         // stream 0 also gathers the transition scalars for the head kernel (one contiguous
         // load there instead of a dependent phys -> ring chain)
         int32_t tslot = 0;
-        if (keep && tid < nb) tslot = a.phys[b0 + tid];
-        if (DQNX_FUSED_ORDER == 0) stream_open(a.wblk[tgt][0], a.out[0] >> 4, fwd_nch<BF>(a.in[0]), 0, c, ws, wb);
+        const bool keep0 = keep && part == 0;   // one part writes the stream-0 copies
+        if (keep0 && tid < nb) tslot = a.phys[b0 + tid];
+        if (DQNX_FUSED_ORDER == 0) stream_open(a.wblk[tgt][0], a.out[0] >> 4, fwd_nch<BF>(a.in[0]), coff >> 4, c, ws, wb);
         float4 xv[GQ];
 #pragma unroll
         for (int j = 0; j < GQ; j++) {
@@ -336,9 +371,9 @@ __global__ __launch_bounds__(FT) void k_mlp_fwd(FusedFwdArgs a) {
             if (!ok) x = make_float4(0.f, 0.f, 0.f, 0.f);
             xv[j] = x;
         }
-        if (DQNX_FUSED_ORDER == 2) stream_open(a.wblk[tgt][0], a.out[0] >> 4, fwd_nch<BF>(a.in[0]), 0, c, ws, wb);
+        if (DQNX_FUSED_ORDER == 2) stream_open(a.wblk[tgt][0], a.out[0] >> 4, fwd_nch<BF>(a.in[0]), coff >> 4, c, ws, wb);
         // after the row loads are in flight: the transition scalars' own round trip overlaps them
-        if (keep && tid < nb)
+        if (keep0 && tid < nb)
             a.trans[b0 + tid] = make_float4(__int_as_float(a.act[tslot]), a.rew[tslot], a.done[tslot], 0.f);
 #pragma unroll
         for (int j = 0; j < GQ; j++) {
@@ -350,20 +385,21 @@ __global__ __launch_bounds__(FT) void k_mlp_fwd(FusedFwdArgs a) {
                         make_uint2(bf16_pack2(xv[j].x, xv[j].y), bf16_pack2(xv[j].z, xv[j].w));
                 else
                     *reinterpret_cast<float4*>(FBUF(0) + r * a.sx + 4 * c4) = xv[j];
-                if (keep && r < nb && c4 < rs4)
+                if (keep0 && r < nb && c4 < rs4)
                     *reinterpret_cast<float4*>(a.xcopy + (int64_t)(b0 + r) * a.ring_stride + 4 * c4) = xv[j];
             }
         }
     }
+    }   // PH != 2
     DQNX_STAMP(a.stamps, 25);
     lds_barrier();
     DQNX_STAMP(a.stamps, 26);
 
     int cur = 0;
 #pragma unroll
-    for (int l = 0; l < NL; l++) {
+    for (int l = LB; l < LE; l++) {
         const int K = a.in[l], N = a.out[l];
-        const float* bias_p = P + a.woff[l] + (int64_t)N * K;
+        const float* bias_p = P + a.woff[l] + (int64_t)N * K + (l == 0 ? coff : 0);
         float bias[2];
 #pragma unroll
         for (int t = 0; t < 2; t++) bias[t] = bias_p[(t < c.tn ? c.n0[t] : 0) + i];   // branch-free
@@ -372,12 +408,13 @@ __global__ __launch_bounds__(FT) void k_mlp_fwd(FusedFwdArgs a) {
         DQNX_STAMP(a.stamps, 27 + 2 * l);
         const WaveCols cl = c;
         // next layer's weight stream in flight during the epilogue + barrier
-        if (l + 1 < NL) {
+        if (l + 1 < LE) {
             c = wave_cols(a.out[l + 1]);
             stream_open(a.wblk[tgt][l + 1], a.out[l + 1] >> 4, fwd_nch<BF>(a.in[l + 1]), 0, c, ws, wb);
         }
         float* Hs = FBUF(cur ^ 1);
-        float* Hg = keep ? a.H[l] : nullptr;
+        // H to HBM: stream 0 (the backward's operands); the split layer 1 writes every stream's
+        float* Hg = (PH == 1) ? a.H[0] + (int64_t)s * a.Bl * N : (keep ? a.H[l] : nullptr);
 #pragma unroll
         for (int t = 0; t < 2; t++) {
             if (t >= cl.tn) continue;
@@ -388,18 +425,21 @@ __global__ __launch_bounds__(FT) void k_mlp_fwd(FusedFwdArgs a) {
                 for (int r = 0; r < 4; r++) {
                     const int rr = 16 * m + 4 * g + r;
                     const float v = act_fwd<ACT>(acc[m][t][r] + bias[t]);
-                    if constexpr (BF) reinterpret_cast<uint16_t*>(Hs)[rr * a.sh + col] = bf16_bits(v);
-                    else Hs[rr * a.sh + col] = v;
-                    if (Hg && rr < nb) Hg[(int64_t)(b0 + rr) * N + col] = v;
+                    if constexpr (PH != 1) {
+                        if constexpr (BF) reinterpret_cast<uint16_t*>(Hs)[rr * a.sh + col] = bf16_bits(v);
+                        else Hs[rr * a.sh + col] = v;
+                    }
+                    if (Hg && rr < nb) Hg[(int64_t)(b0 + rr) * N + coff + col] = v;
                 }
         }
+        if constexpr (PH == 1) return;
         lds_barrier();
         DQNX_STAMP(a.stamps, 28 + 2 * l);
         cur ^= 1;
     }
 
     // head: raw[o] = H_L . W_head[o] + b_head[o], o < NH; K = F split over the waves
-    {
+    if constexpr (PH != 1) {
         const int F = a.F;
         const int A = a.head_kind == DQNX_HEAD_DUELING ? a.NH - 1 : a.NH;
         const float* hw = P + a.head_off + head_w_off(a.head_kind, i < a.NH ? i : 0, F);
@@ -911,19 +951,23 @@ static void allow_lds(K kern, size_t bytes) {
 }
 
 int launch_fused_fwd(const FusedFwdArgs& a, int act, hipStream_t s) {
-    const dim3 grid(a.tiles * a.nstreams), block(FT);
+    if (a.phase != 0 && (a.L < 2 || a.mr != 1 || (a.phase == 1 && (a.csplit < 1 || a.out[0] % (16 * a.csplit)))))
+        return set_error(DQNX_EUNSUPPORTED, "split forward: L >= 2, 16-row tiles, layer 1 width / parts a multiple of 16");
+    const dim3 grid(a.tiles * a.nstreams * (a.phase == 1 ? a.csplit : 1)), block(FT);
     size_t shm = (size_t)(a.buf0 + a.buf1) * 4;
     if (shm < (size_t)DQNX_FUSED_LDS_MIN) shm = DQNX_FUSED_LDS_MIN;
-#define FUSED_FWD_MR(ACTV, NLV, BFV, MRV)                                                            \
+#define FUSED_FWD_MR(ACTV, NLV, BFV, MRV, PHV)                                                       \
     do {                                                                                             \
-        if (shm > 64 * 1024) allow_lds(k_mlp_fwd<ACTV, NLV, BFV, MRV>, 160 * 1024);                  \
-        hipLaunchKernelGGL((k_mlp_fwd<ACTV, NLV, BFV, MRV>), grid, block, shm, s, a);                \
+        if (shm > 64 * 1024) allow_lds(k_mlp_fwd<ACTV, NLV, BFV, MRV, PHV>, 160 * 1024);             \
+        hipLaunchKernelGGL((k_mlp_fwd<ACTV, NLV, BFV, MRV, PHV>), grid, block, shm, s, a);           \
     } while (0)
 #define FUSED_FWD_BF(ACTV, NLV, BFV)                                                                 \
     do {                                                                                             \
-        if (a.mr == 4) FUSED_FWD_MR(ACTV, NLV, BFV, 4);                                              \
-        else if (a.mr == 2) FUSED_FWD_MR(ACTV, NLV, BFV, 2);                                         \
-        else FUSED_FWD_MR(ACTV, NLV, BFV, 1);                                                        \
+        if (a.phase == 1) { if constexpr (NLV >= 2) FUSED_FWD_MR(ACTV, NLV, BFV, 1, 1); }             \
+        else if (a.phase == 2) { if constexpr (NLV >= 2) FUSED_FWD_MR(ACTV, NLV, BFV, 1, 2); }        \
+        else if (a.mr == 4) FUSED_FWD_MR(ACTV, NLV, BFV, 4, 0);                                      \
+        else if (a.mr == 2) FUSED_FWD_MR(ACTV, NLV, BFV, 2, 0);                                      \
+        else FUSED_FWD_MR(ACTV, NLV, BFV, 1, 0);                                                     \
     } while (0)
 #define FUSED_FWD_CASE(ACTV, NLV)                                                                    \
     do {                                                                                             \

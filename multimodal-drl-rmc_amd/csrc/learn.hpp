@@ -321,6 +321,8 @@ struct FusedFwdArgs {
     const float* done;
     int bf16;                    // DQNX_COMPUTE_BF16: bf16 LDS tiles, bf16 blocked weights, bf16 MFMA
     int mr;                      // 16-row tiles per workgroup (1, 2 or 4; `tiles` counts 16*mr-row tiles)
+    int phase;                   // 0 whole forward; 1 layer 1 split over csplit parts; 2 layers 2.. + head
+    int csplit;
     int sx, sh;                  // LDS row strides (elements: floats, or bf16 under bf16) of the input / hidden tiles
     int buf0, buf1;              // LDS buffer sizes (floats)
     int kpad[FUSED_MAX_L];       // layer inputs zero padded to kpad (blocked copies): fp32 a multiple of 64, bf16 of 32

@@ -161,9 +161,35 @@ def test_gpu_learn_per_layer_plan_matches_oracle(monkeypatch, algo, obs_dim, bat
     ("DQNAgent", 14, 100, 500, 300, 42),
 ])
 def test_gpu_learn_forward_row_tiles_match_oracle(monkeypatch, mr, algo, obs_dim, batch, capacity, n_fill, seed):
-    """Fused forward with 32- / 64-row workgroups (chosen automatically at B >= 4096 / 8192)."""
+    """Fused forward with 16- / 32- / 64-row workgroups (one launch: no layer-1 split)."""
     monkeypatch.setenv("DQNX_FWD_MR", mr)
+    monkeypatch.setenv("DQNX_FWD_SPLIT", "1")
     _check_learn(*make_pair(algo, obs_dim, batch, capacity, n_fill, seed))
+
+
+@pytest.mark.parametrize("compute", ["fp32", "bf16"])
+@pytest.mark.parametrize("split", ["2", "4"])
+def test_gpu_split_forward_identical(monkeypatch, split, compute):
+    """Layer 1 in a launch of its own over 2 / 4 column parts (H_1 through HBM) gives bitwise
+    the same steps as the one-launch forward; ragged batch."""
+    E = _engine_mod()
+    outs = []
+    for sp in (split, "1"):
+        monkeypatch.setenv("DQNX_FWD_SPLIT", sp)
+        o, e = make_pair("DuelingDoubleDQNAgent", 284, 1000, 20000, 20000, 44)
+        if compute == "bf16":
+            e = E.LearnEngine(E.mlp_spec(284, 8, "dueling"), "DuelingDoubleDQNAgent", 1000, 20000,
+                              compute_dtype="bf16")
+            e.load_params(O.reference_init(O.mlp_spec(284, 8, "dueling"), 44))
+            e.push(*O.synth_transitions(20000, 284, 8, seed=144))
+            random.seed(51)
+            e.set_rng(0, O.py_state_to_array())
+        for _ in range(3):
+            e.learn_step(soft_update=True)
+        torch.cuda.synchronize()
+        outs.append((e.params.clone(), e.q.clone()))
+    assert torch.equal(outs[0][0], outs[1][0])
+    assert torch.equal(outs[0][1], outs[1][1])
 
 
 @pytest.mark.parametrize("split", ["2", "4"])
