@@ -247,6 +247,21 @@ int dqnx_apply_grads(dqnx_engine* e, int32_t flags, void* stream);
 int dqnx_soft_update(dqnx_engine* e, void* stream);
 int dqnx_hard_update(dqnx_engine* e, void* stream);
 
+/* ---- acting path: replaces Network.actions (DeepQNetwork R:dqn/network.py:67-74: argmax of Q;
+ *      DuelingDeepQNetwork R:dqn/network.py:110-117: argmax of the advantage stream only), as
+ *      called by Agent.choose_actions (R:dqn/agent.py:92-99) before the epsilon-greedy override.
+ * Stateless: `params` is a device fp32 vector in the layout of dqnx_net_param_info (the engine's
+ * DQNX_BUF_PARAMS / DQNX_BUF_TARGET_PARAMS, or any flat copy).  obs: device [n][obs_dim];
+ * actions: device int32[n] (first maximal index, like torch.argmax); values: device [n][n_actions]
+ * or NULL (receives the argmaxed values: Q, or the advantages for a dueling head).  scratch:
+ * 16-byte aligned device buffer of scratch_bytes >= dqnx_act_scratch_bytes(net, n) bytes (a
+ * multiple of 4), zero-filled before its first use; every call leaves it ready for the next, so
+ * calls with any n up to its size may share it on one stream.  MLP nets only (DQNX_EUNSUPPORTED for two-stream nets); one launch, stream-ordered, no
+ * sync. */
+uint64_t dqnx_act_scratch_bytes(const dqnx_net_desc* net, int32_t n);
+int dqnx_act(const dqnx_net_desc* net, const float* params, const float* obs, int32_t n, int32_t* actions,
+             float* values, void* scratch, uint64_t scratch_bytes, void* stream);
+
 /* ---- kernel-level timing (bench.py roofline) ---------------------------------------
  * A learn step is an ordered list of kernel launches (sample, linear_fwd_l1.., head_td_loss,
  * linear_bwd_lL..l1, adam_fused).  dqnx_learn_step_timed runs one whole step exactly like

@@ -1,0 +1,280 @@
+// Acting path: Network.actions(obses) as one launch.
+//
+//   DeepQNetwork.actions          R:dqn/network.py:67-74   argmax_a Q(s, a)
+//   DuelingDeepQNetwork.actions   R:dqn/network.py:110-117 argmax_a A(s, a)  (advantage stream only)
+//   called by Agent.choose_actions R:dqn/agent.py:92-99 once per env step with n_env rows.
+//
+// At n_env rows the forward is latency-bound: MLP-284 reads 428 KB of weights once and does
+// 0.4 MFLOP per row.  What costs time is the number of dependent HBM round trips, so the
+// kernel is shaped to keep that count at about one per layer:
+//   * layer 1 (68 % of the weights) is spread over G = ceil(h0/16) workgroups of 16 waves, one
+//     output neuron per wave: each lane issues its ceil(in/256) float4 loads of that weight row
+//     at once, a wave butterfly reduces the row, lane r writes row r's activation to scratch;
+//   * the last workgroup to finish layer 1 (agent-scope ticket, no spinning: every workgroup
+//     exits) stages h0 into LDS and runs the remaining layers and the head, 8 neurons per wave
+//     per pass with all of a pass's loads in flight before the first FMA;
+//   * the argmax (first maximal index, like torch.argmax) is one thread per row.
+// Rows are processed R = 1, 2 or 4 at a time per workgroup column (grid.y = row groups).
+#include "common.hpp"
+#include "learn.hpp"
+
+namespace dqnx {
+
+namespace {
+
+constexpr int kActThreads = 1024;
+constexpr int kActWaves = kActThreads / kWave;
+constexpr int kActU = 8;   // output neurons per wave per pass after layer 1
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, kWave);
+    return v;
+}
+
+// y[r][j] = act?(sum_k W[j][k] * x[r][k] + b[j]) for j < out, r < R; x, y in LDS (row stride ld).
+// VEC: in % 4 == 0 and W 16-byte aligned -> float4 weight loads and LDS reads.
+template <int R, int ACT, bool APPLY, bool VEC>
+__device__ __forceinline__ void act_dense(const float* __restrict__ W, const float* __restrict__ b, int in, int out,
+                                          const float* x, float* y, int ld) {
+    const int lane = threadIdx.x & (kWave - 1);
+    const int wave = threadIdx.x / kWave;
+    constexpr int V = VEC ? 4 : 1;
+    const int nk = in / V;
+    constexpr int U = R >= 4 ? kActU / 2 : kActU;   // 4 rows x 8 neurons would spill at 128 VGPRs
+    for (int j0 = wave * U; j0 < out; j0 += kActWaves * U) {
+        float acc[U][R];
+#pragma unroll
+        for (int u = 0; u < U; u++)
+#pragma unroll
+            for (int r = 0; r < R; r++) acc[u][r] = 0.f;
+        const float* wr[U];
+#pragma unroll
+        for (int u = 0; u < U; u++) wr[u] = W + (int64_t)min(j0 + u, out - 1) * in;   // clamped: valid reads, result dropped
+        float bias[U];   // issued with the first weight loads, not after the reduction
+#pragma unroll
+        for (int u = 0; u < U; u++) bias[u] = b[min(j0 + u, out - 1)];
+        for (int kv = lane; kv < nk; kv += kWave) {
+            if (VEC) {
+                float4 wv[U];
+#pragma unroll
+                for (int u = 0; u < U; u++) wv[u] = ld4(wr[u] + 4 * kv);
+#pragma unroll
+                for (int r = 0; r < R; r++) {
+                    const float4 xv = *reinterpret_cast<const float4*>(x + r * ld + 4 * kv);
+#pragma unroll
+                    for (int u = 0; u < U; u++) {
+                        acc[u][r] = fmaf(wv[u].x, xv.x, acc[u][r]);
+                        acc[u][r] = fmaf(wv[u].y, xv.y, acc[u][r]);
+                        acc[u][r] = fmaf(wv[u].z, xv.z, acc[u][r]);
+                        acc[u][r] = fmaf(wv[u].w, xv.w, acc[u][r]);
+                    }
+                }
+            } else {
+                float wv[U];
+#pragma unroll
+                for (int u = 0; u < U; u++) wv[u] = wr[u][kv];
+#pragma unroll
+                for (int r = 0; r < R; r++) {
+                    const float xv = x[r * ld + kv];
+#pragma unroll
+                    for (int u = 0; u < U; u++) acc[u][r] = fmaf(wv[u], xv, acc[u][r]);
+                }
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+#pragma unroll
+            for (int r = 0; r < R; r++) {
+                const float s = wave_sum(acc[u][r]);
+                if (lane == r && j0 + u < out) {
+                    const float v = s + bias[u];
+                    y[r * ld + j0 + u] = APPLY ? act_fwd<ACT>(v) : v;
+                }
+            }
+        }
+    }
+}
+
+template <int R, int ACT, bool APPLY>
+__device__ __forceinline__ void act_dense_any(const float* W, const float* b, int in, int out, const float* x,
+                                              float* y, int ld) {
+    if ((in & 3) == 0 && ((uintptr_t)W & 15) == 0)
+        act_dense<R, ACT, APPLY, true>(W, b, in, out, x, y, ld);
+    else
+        act_dense<R, ACT, APPLY, false>(W, b, in, out, x, y, ld);
+}
+
+// Layer 1, one neuron per wave: h[r][j] = act(W[j] . x[r] + b[j]).  VEC as above (also needs D % 4 == 0).
+template <int R, int ACT, bool VEC>
+__device__ __forceinline__ void act_layer1_neuron(const float* __restrict__ W, const float* __restrict__ b, int in,
+                                                  int j, const float* x, int ld, float* h, int ldh) {
+    const int lane = threadIdx.x & (kWave - 1);
+    constexpr int V = VEC ? 4 : 1;
+    const int nk = in / V;
+    const float* w = W + (int64_t)j * in;
+    const float bias = b[j];
+    float acc[R];
+#pragma unroll
+    for (int r = 0; r < R; r++) acc[r] = 0.f;
+    constexpr int P = VEC ? 4 : 8;   // loads of the row issued together per lane
+    for (int k0 = lane; k0 < nk; k0 += P * kWave) {
+        if (VEC) {
+            float4 wv[P];
+#pragma unroll
+            for (int p = 0; p < P; p++) {
+                const int kv = k0 + p * kWave;
+                wv[p] = kv < nk ? ld4(w + 4 * kv) : make_float4(0.f, 0.f, 0.f, 0.f);
+            }
+#pragma unroll
+            for (int p = 0; p < P; p++) {
+                const int kv = min(k0 + p * kWave, nk - 1);
+#pragma unroll
+                for (int r = 0; r < R; r++) {
+                    const float4 xv = *reinterpret_cast<const float4*>(x + r * ld + 4 * kv);
+                    acc[r] = fmaf(wv[p].x, xv.x, acc[r]);
+                    acc[r] = fmaf(wv[p].y, xv.y, acc[r]);
+                    acc[r] = fmaf(wv[p].z, xv.z, acc[r]);
+                    acc[r] = fmaf(wv[p].w, xv.w, acc[r]);
+                }
+            }
+        } else {
+            float wv[P];
+#pragma unroll
+            for (int p = 0; p < P; p++) {
+                const int kv = k0 + p * kWave;
+                wv[p] = kv < nk ? w[kv] : 0.f;
+            }
+#pragma unroll
+            for (int p = 0; p < P; p++) {
+                const int kv = min(k0 + p * kWave, nk - 1);
+#pragma unroll
+                for (int r = 0; r < R; r++) acc[r] = fmaf(wv[p], x[r * ld + kv], acc[r]);
+            }
+        }
+    }
+#pragma unroll
+    for (int r = 0; r < R; r++) {
+        const float s = wave_sum(acc[r]);
+        if (lane == r) h[r * ldh + j] = act_fwd<ACT>(s + bias);
+    }
+}
+
+template <int R, int ACT>
+__global__ __launch_bounds__(kActThreads) void k_act_mlp(ActArgs a) {
+    extern __shared__ float lds[];
+    __shared__ int s_last;
+    float* x = lds;
+    float* y = lds + R * a.ld;
+    const int grp = blockIdx.y;
+    const int row0 = grp * R;
+    const int nr = min(R, a.n - row0);
+    const int tid = threadIdx.x;
+    for (int i = tid; i < R * a.D; i += kActThreads) {
+        const int r = i / a.D, k = i - r * a.D;
+        x[r * a.ld + k] = r < nr ? a.obs[(int64_t)(row0 + r) * a.D + k] : 0.f;
+    }
+    __syncthreads();
+
+    // ---- layer 1 slice: neurons [16 * blockIdx.x, +16), one per wave, into scratch
+    const int h0 = a.out[0];
+    float* hs = a.scratch + (int64_t)row0 * h0;   // [R][h0] of this row group
+    {
+        const int j = blockIdx.x * kActWaves + tid / kWave;
+        const float* W = a.params + a.off[0];
+        if (j < h0) {
+            if ((a.D & 3) == 0 && (a.off[0] & 3) == 0 && (a.ld & 3) == 0)
+                act_layer1_neuron<R, ACT, true>(W, W + (int64_t)h0 * a.D, a.D, j, x, a.ld, hs, h0);
+            else
+                act_layer1_neuron<R, ACT, false>(W, W + (int64_t)h0 * a.D, a.D, j, x, a.ld, hs, h0);
+        }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (gridDim.x > 1) {
+        if (tid == 0) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            const uint32_t t = __hip_atomic_fetch_add(a.tickets - grp, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const int last = t == gridDim.x - 1;
+            if (last) {
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                *(a.tickets - grp) = 0;   // ready for the next launch
+            }
+            s_last = last;
+        }
+        __syncthreads();
+        if (!s_last) return;
+    }
+
+    // ---- last arriver: h0 -> LDS, remaining layers, head, argmax
+    for (int i = tid; i < R * h0; i += kActThreads) {
+        const int r = i / h0, k = i - r * h0;
+        x[r * a.ld + k] = hs[(int64_t)r * h0 + k];
+    }
+    __syncthreads();
+    for (int l = 1; l < a.L; l++) {
+        const float* W = a.params + a.off[l];
+        act_dense_any<R, ACT, true>(W, W + (int64_t)a.out[l] * a.in[l], a.in[l], a.out[l], x, y, a.ld);
+        __syncthreads();
+        float* t = x; x = y; y = t;
+    }
+    const float* H = a.params + a.head_off;
+    const int F = a.F, A = a.A;
+    // dueling: only the advantage stream decides (R:dqn/network.py:110-117); fc_val is not evaluated
+    const float* Wh = a.dueling ? H + F + 1 : H;
+    act_dense_any<R, ACT, false>(Wh, Wh + (int64_t)A * F, F, A, x, y, a.ld);
+    __syncthreads();
+    if (tid < nr) {
+        const int r = tid;
+        const float* q = y + r * a.ld;
+        int best = 0;
+        float bv = q[0];
+        for (int j = 0; j < A; j++) {
+            const float v = q[j];
+            if (a.values) a.values[(int64_t)(row0 + r) * A + j] = v;
+            if (v > bv || (v != v && bv == bv)) { bv = v; best = j; }   // first max; NaN wins like torch
+        }
+        a.actions[row0 + r] = best;
+    }
+}
+
+template <int R>
+int launch_act_r(const ActArgs& a, hipStream_t s) {
+    const dim3 grid((a.out[0] + kActWaves - 1) / kActWaves, (a.n + R - 1) / R);
+    const size_t lds = (size_t)2 * R * a.ld * sizeof(float);
+    if (a.act == DQNX_ACT_RELU)
+        hipLaunchKernelGGL((k_act_mlp<R, DQNX_ACT_RELU>), grid, dim3(kActThreads), lds, s, a);
+    else
+        hipLaunchKernelGGL((k_act_mlp<R, DQNX_ACT_ELU>), grid, dim3(kActThreads), lds, s, a);
+    DQNX_HIP_CHECK(hipGetLastError());
+    return DQNX_OK;
+}
+
+}  // namespace
+
+int act_rows_per_block(int n, int ld) {
+    int R = n <= 1 ? 1 : (n == 2 ? 2 : 4);
+    while (R > 1 && (size_t)2 * R * ld * sizeof(float) > kActMaxLds) R /= 2;
+    return (size_t)2 * R * ld * sizeof(float) > kActMaxLds ? 0 : R;
+}
+
+uint64_t act_scratch_bytes(int n, int h0, int ld) {
+    const int R = act_rows_per_block(n, ld);
+    if (R == 0 || n <= 0) return 0;
+    const int64_t groups = (n + R - 1) / R;
+    return (uint64_t)groups * R * h0 * sizeof(float) + (uint64_t)groups * 4;
+}
+
+int launch_act(const ActArgs& a, hipStream_t s) {
+    if (a.n <= 0) return DQNX_OK;
+    switch (act_rows_per_block(a.n, a.ld)) {
+        case 4: return launch_act_r<4>(a, s);
+        case 2: return launch_act_r<2>(a, s);
+        case 1: return launch_act_r<1>(a, s);
+        default: return set_error(DQNX_EUNSUPPORTED, "dqnx_act: layer width %d does not fit LDS", a.ld);
+    }
+}
+
+}  // namespace dqnx

@@ -1958,6 +1958,57 @@ int dqnx_hard_update(dqnx_engine* e, void* stream) {
     return DQNX_OK;
 }
 
+// acting kernel geometry of a network (host only)
+static int act_plan(const dqnx_net_desc* net, NetPlan& np, ActArgs& a) {
+    int rc = plan_net(net, np);
+    if (rc) return rc;
+    if (net->kind != DQNX_NET_MLP) return set_error(DQNX_EUNSUPPORTED, "dqnx_act: MLP networks only");
+    memset(&a, 0, sizeof(a));
+    a.D = net->obs_dim; a.L = (int)np.dense.size(); a.A = net->n_actions; a.F = np.F;
+    a.dueling = net->head == DQNX_HEAD_DUELING; a.act = net->activation;
+    a.ld = std::max(a.D, a.A);
+    for (int l = 0; l < a.L; l++) {
+        a.in[l] = np.dense[l].in; a.out[l] = np.dense[l].out; a.off[l] = np.dense[l].off;
+        a.ld = std::max(a.ld, a.out[l]);
+    }
+    a.ld = (a.ld + 3) & ~3;   // float4 LDS rows
+    a.head_off = np.head_off;
+    return DQNX_OK;
+}
+
+uint64_t dqnx_act_scratch_bytes(const dqnx_net_desc* net, int32_t n) {
+    NetPlan np;
+    ActArgs a;
+    if (act_plan(net, np, a)) return 0;
+    return act_scratch_bytes(n, a.out[0], a.ld);
+}
+
+int dqnx_act(const dqnx_net_desc* net, const float* params, const float* obs, int32_t n, int32_t* actions,
+             float* values, void* scratch, uint64_t scratch_bytes, void* stream) {
+    NetPlan np;
+    ActArgs a;
+    int rc = act_plan(net, np, a);
+    if (rc) return rc;
+    if (n < 0 || (n > 0 && (!params || !obs || !actions || !scratch)))
+        return set_error(DQNX_EINVAL, "dqnx_act: bad argument");
+    if (n > 0 && act_rows_per_block(n, a.ld) == 0)
+        return set_error(DQNX_EUNSUPPORTED, "dqnx_act: layer width %d does not fit LDS", a.ld);
+    a.params = params; a.obs = obs; a.actions = actions; a.values = values; a.n = n;
+    if (n > 0) {
+        // activations from the start, tickets from the END (ticket g at bytes - 4(g+1)): a larger
+        // call's activations never reach a smaller call's tickets, so every ticket word only ever
+        // holds counts that the last arriver returns to zero, whatever n the buffer last served.
+        const int R = act_rows_per_block(n, a.ld);
+        const int64_t groups = (n + R - 1) / R;
+        if (scratch_bytes < act_scratch_bytes(n, a.out[0], a.ld) || (scratch_bytes & 3) || ((uintptr_t)scratch & 15))
+            return set_error(DQNX_EINVAL, "dqnx_act: scratch of %llu bytes too small or misaligned for n=%d",
+                             (unsigned long long)scratch_bytes, n);
+        a.scratch = (float*)scratch;
+        a.tickets = (uint32_t*)((char*)scratch + scratch_bytes) - 1;   // ticket g = tickets[-g]
+    }
+    return launch_act(a, (hipStream_t)stream);
+}
+
 int dqnx_debug_stamps(dqnx_engine* e, int64_t* out64, void* stream) {
 #ifdef DQNX_STAMPS
     int rc = check_bound(e);

@@ -406,6 +406,24 @@ bool head_supported(int F);
 int launch_adam(const AdamArgs& a, hipStream_t s);
 void dw_adam_grid(DwAdamArgs& a);
 int launch_dw_adam(const DwAdamArgs& a, hipStream_t s);
+// acting path (act.hip): Network.actions for MLP nets, one launch
+constexpr int kActMaxDense = DQNX_MAX_DENSE;
+constexpr size_t kActMaxLds = 64 * 1024;
+struct ActArgs {
+    const float* params;    // flat fp32 vector, named_parameters order
+    const float* obs;       // [n][D]
+    int32_t* actions;       // [n]
+    float* values;          // [n][A] or null: Q (linear head) / advantages (dueling), the argmaxed values
+    uint32_t* tickets;      // layer-1 arrival counter of row group g at tickets[-g] (zero between launches)
+    float* scratch;         // [row groups * R][h0] layer-1 activations
+    int n, D, L, A, F, dueling, act, ld;   // ld: LDS row stride (max layer width)
+    int in[kActMaxDense], out[kActMaxDense];
+    int64_t off[kActMaxDense];
+    int64_t head_off;
+};
+int act_rows_per_block(int n, int ld);
+uint64_t act_scratch_bytes(int n, int h0, int ld);
+int launch_act(const ActArgs& a, hipStream_t s);
 int launch_soft_update(float* target, const float* p, int64_t n, float tau, float omt, hipStream_t s);
 int launch_replay_push(const PushArgs& a, hipStream_t s);
 

@@ -83,7 +83,7 @@ EXPORTS = [
     "dqnx_sample_scratch_bytes", "dqnx_sample_uniform", "dqnx_last_error", "dqnx_abi_version",
     "dqnx_learn_kernel_count", "dqnx_learn_kernel_info", "dqnx_learn_step_timed", "dqnx_learn_step_omit", "dqnx_events_create",
     "dqnx_events_destroy", "dqnx_event_elapsed", "dqnx_debug_stamps",
-    "dqnx_per_sample", "dqnx_per_update_priorities", "dqnx_set_agent_step",
+    "dqnx_per_sample", "dqnx_per_update_priorities", "dqnx_set_agent_step", "dqnx_act", "dqnx_act_scratch_bytes",
 ]
 
 _lib = None
@@ -139,6 +139,8 @@ def lib():
         "dqnx_per_sample": ([vp, vp], ctypes.c_int),
         "dqnx_per_update_priorities": ([vp, vp, vp, I32, vp], ctypes.c_int),
         "dqnx_set_agent_step": ([vp, I64, vp], ctypes.c_int),
+        "dqnx_act": ([P(NetDesc), vp, vp, I32, vp, vp, vp, ctypes.c_uint64, vp], ctypes.c_int),
+        "dqnx_act_scratch_bytes": ([P(NetDesc), I32], ctypes.c_uint64),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)

@@ -118,8 +118,9 @@ class Agent:
                                   lr=self.lr, tau=self.target_soft_update_tau, n_env=self.n_env, device=self.device,
                                   eps_dec=self.epsilon_decay,
                                   compute_dtype=os.environ.get("DQNX_COMPUTE_DTYPE", "fp32"))
-        self.online_network.bind_flat(self.engine.param_views(self.engine.params))
-        self.target_network.bind_flat(self.engine.param_views(self.engine.target_params))
+        self.online_network.bind_flat(self.engine.param_views(self.engine.params), self.engine.params, spec)
+        self.target_network.bind_flat(self.engine.param_views(self.engine.target_params), self.engine.target_params,
+                                      spec)
         self.replay_memory_buffer = self._make_replay()
         self._engine_step = 0          # agent.step * n_env the engine will use next (PER)
         self.update_target_network(force=True)

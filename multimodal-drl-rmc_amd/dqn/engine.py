@@ -131,6 +131,43 @@ def spec_from_body(net: nn.Module, obs_dim: int, n_actions: int, dueling: bool) 
 
 
 # ----------------------------------------------------------------------------------------
+# acting path (dqnx_act)
+# ----------------------------------------------------------------------------------------
+def act_scratch(spec: NetSpec, n: int, device) -> torch.Tensor:
+    """Zeroed scratch for dqnx_act calls of up to n rows (reusable across calls on one stream)."""
+    nbytes = int(C.lib().dqnx_act_scratch_bytes(ctypes.byref(spec.to_c()), int(n)))
+    return torch.zeros((nbytes + 15) // 16 * 4, dtype=torch.float32, device=device)
+
+
+def act(spec: NetSpec, flat: torch.Tensor, obs: torch.Tensor, values: Optional[torch.Tensor] = None,
+        scratch: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Greedy actions of an MLP Q-network, one HIP launch (`dqnx_act`).
+
+    `flat`: the network's flat fp32 parameters on the GPU (dqnx_net_param_info layout);
+    `obs`: [n, obs_dim] on the same GPU.  Returns int32 actions [n] (first maximal index, like
+    torch.argmax) of Q, or of the advantage stream for a dueling head (R:dqn/network.py:67-74,
+    110-117).  `values`, if given ([n, n_actions] fp32), receives the argmaxed values."""
+    if spec.kind != C.DQNX_NET_MLP:
+        raise NotImplementedError("dqnx_act: MLP networks only")
+    obs = obs.to(flat.device, torch.float32).contiguous()
+    if obs.dim() != 2 or obs.shape[1] != spec.obs_dim:
+        raise ValueError(f"obs must be [n, {spec.obs_dim}], got {tuple(obs.shape)}")
+    n = obs.shape[0]
+    out = torch.empty(n, dtype=torch.int32, device=flat.device)
+    if values is not None and (values.shape != (n, spec.n_actions) or not values.is_contiguous()
+                               or values.dtype != torch.float32 or values.device != flat.device):
+        raise ValueError("values must be a contiguous fp32 [n, n_actions] tensor on the parameters' device")
+    if scratch is None:
+        scratch = act_scratch(spec, n, flat.device)
+    d = spec.to_c()
+    stream = ctypes.c_void_p(torch.cuda.current_stream(flat.device).cuda_stream)
+    C.check(C.lib().dqnx_act(ctypes.byref(d), flat.data_ptr(), obs.data_ptr(), n, out.data_ptr(),
+                             values.data_ptr() if values is not None else None, scratch.data_ptr(),
+                             scratch.numel() * 4, stream), "act")
+    return out
+
+
+# ----------------------------------------------------------------------------------------
 # engine
 # ----------------------------------------------------------------------------------------
 class LearnEngine:

@@ -16,6 +16,9 @@ from __future__ import annotations
 import torch as T
 import torch.nn as nn
 
+from .engine import act as _act_native
+from .engine import act_scratch
+from .engine import spec_from_body
 from .utils.pack import load_pack, save_pack
 
 
@@ -28,6 +31,12 @@ class Network(nn.Module):
         self.optim_func = (lambda params, lr: optim_func(params, lr=lr))
         self.loss_func = (lambda reduction: loss_func(reduction=reduction))
         self.device = device
+        self._act_spec = None       # NetSpec of the acting kernel (None: not yet planned)
+        self._act_flat = None       # flat fp32 parameter buffer the acting kernel reads
+        self._act_ptrs = None       # data_ptr of every parameter when _act_flat was bound
+        self._act_engine = False    # _act_flat belongs to a learn engine
+        self._act_scratch = None    # dqnx_act scratch, sized for _act_scratch_rows rows
+        self._act_scratch_rows = 0
 
     def forward(self, s):
         raise NotImplementedError
@@ -36,9 +45,11 @@ class Network(nn.Module):
         raise NotImplementedError
 
     # -- engine binding -------------------------------------------------------------
-    def bind_flat(self, views: dict):
+    def bind_flat(self, views: dict, flat=None, spec=None):
         """Move every parameter into `views[name]` (same shape, engine memory), keeping
-        the Parameter objects (so `.optimizer` and module references stay valid)."""
+        the Parameter objects (so `.optimizer` and module references stay valid).  With
+        `flat`/`spec` (the learn engine's buffer and network description) `actions()` runs
+        the acting kernel straight on that buffer."""
         with T.no_grad():
             for name, p in self.named_parameters():
                 v = views[name]
@@ -46,6 +57,45 @@ class Network(nn.Module):
                     raise ValueError(f"{name}: engine shape {tuple(v.shape)} != {tuple(p.shape)}")
                 v.copy_(p.data.to(v.device, T.float32))
                 p.data = v
+        if flat is not None:
+            self._act_flat, self._act_spec, self._act_engine = flat, spec, True
+            self._act_ptrs = [p.data_ptr() for p in self.parameters()]
+
+    # -- acting path: one dqnx_act launch for MLP bodies on a GPU -----------------------
+    def _act_head_dim(self):
+        head = self.fc_adv if hasattr(self, "fc_adv") else self.fc_out
+        return head.out_features
+
+    def _act_gpu(self, obses_t):
+        spec, flat = self._native_act()
+        x = obses_t.reshape(obses_t.shape[0], -1)
+        if x.shape[0] > self._act_scratch_rows:
+            self._act_scratch = act_scratch(spec, x.shape[0], flat.device)
+            self._act_scratch_rows = x.shape[0]
+        return _act_native(spec, flat, x, scratch=self._act_scratch).tolist()
+
+    def _native_act(self):
+        """(spec, flat) for the acting kernel, or None when the reference's torch forward is
+        the path: a CPU device (the caller asked for CPU) or a two-stream body (dqnx_act
+        covers MLP bodies)."""
+        if T.device(self.device).type != "cuda" or not isinstance(self.net, nn.Sequential):
+            return None
+        if self._act_flat is not None:
+            if [p.data_ptr() for p in self.parameters()] == self._act_ptrs:
+                return self._act_spec, self._act_flat
+            if self._act_engine:
+                raise RuntimeError("network parameters were moved out of the learn engine's buffer")
+        # standalone network (e.g. Observe): pack its parameters into one flat buffer once
+        spec = spec_from_body(self.net, self.net[0].in_features, self._act_head_dim(),
+                              dueling=hasattr(self, "fc_adv"))
+        n, layout = spec.param_infos()
+        dev = next(self.parameters()).device
+        flat = T.empty(n, dtype=T.float32, device=dev)
+        views = {name: flat[off:off + int(T.Size(shape).numel())].view(*shape) for name, off, shape in layout}
+        self.bind_flat(views)
+        self._act_spec, self._act_flat, self._act_engine = spec, flat, False
+        self._act_ptrs = [p.data_ptr() for p in self.parameters()]
+        return spec, flat
 
     # -- checkpoints (R:dqn/network.py:27-47; format: dqn.utils.pack) -----------------
     def save(self, save_path, step, episode_count, rew_mean, len_mean):
@@ -73,6 +123,8 @@ class DeepQNetwork(Network):
 
     def actions(self, obses):
         obses_t = T.as_tensor(obses, dtype=T.float32).to(self.device)
+        if self._native_act() is not None:
+            return self._act_gpu(obses_t)
         q_values = self(obses_t)
         return T.argmax(q_values, dim=1).detach().tolist()
 
@@ -101,5 +153,7 @@ class DuelingDeepQNetwork(Network):
 
     def actions(self, obses):
         obses_t = T.as_tensor(obses, dtype=T.float32).to(self.device)
+        if self._native_act() is not None:
+            return self._act_gpu(obses_t)
         adv_q_values = self.advantages(obses_t)
         return T.argmax(adv_q_values, dim=1).detach().tolist()

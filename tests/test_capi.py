@@ -134,3 +134,19 @@ def test_bf16_compute_is_mlp_only():
     assert _create(E.mlp_spec(14, 8, "linear"), C.DQNX_COMPUTE_BF16) == 0
     assert _create(_engine_spec(O.hybrid_spec(8, "dueling")), C.DQNX_COMPUTE_BF16) == C.DQNX_EUNSUPPORTED
     assert _create(E.mlp_spec(284, 8, "dueling"), 7) == C.DQNX_EINVAL
+
+
+def test_act_argument_checks_without_gpu():
+    """dqnx_act validates on the host before any launch: two-stream nets are refused,
+    null buffers rejected, n = 0 is a no-op."""
+    from dqn import engine as E
+    L = C.lib()
+    hyb = _engine_spec(O.hybrid_spec(8, "dueling")).to_c()
+    mlp = E.mlp_spec(284, 8, "dueling").to_c()
+    assert L.dqnx_act(ctypes.byref(hyb), 16, 16, 1, 16, None, 16, 1 << 20, None) == C.DQNX_EUNSUPPORTED
+    assert L.dqnx_act(ctypes.byref(mlp), None, None, 4, None, None, None, 0, None) == C.DQNX_EINVAL
+    assert L.dqnx_act(ctypes.byref(mlp), None, None, 0, None, None, None, 0, None) == C.DQNX_OK
+    need = L.dqnx_act_scratch_bytes(ctypes.byref(mlp), 3)
+    assert need == 4 * 256 * 4 + 4    # one group of R = 4 rows of layer-1 activations + its ticket
+    # too small a scratch is refused before any launch
+    assert L.dqnx_act(ctypes.byref(mlp), 16, 16, 3, 16, None, 16, need - 4, None) == C.DQNX_EINVAL

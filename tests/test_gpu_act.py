@@ -1,0 +1,111 @@
+"""GPU: the acting path (`dqnx_act`, one launch per Network.actions call) against the oracle's
+torch-CPU forward (R:dqn/network.py:67-74 DeepQNetwork, :110-117 Dueling: advantage argmax).
+
+Values within 1e-5 (scaled by max(1, |v|)); actions equal the oracle's argmax wherever the
+top-two gap exceeds that tolerance (closer ties are decided by summation order, which no
+fp32 implementation shares with torch's CPU GEMM)."""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from dqn import engine as E
+from dqn.network import DeepQNetwork, DuelingDeepQNetwork
+from oracle import ref as O
+from refnets import Box, mlp_network_config
+
+pytestmark = pytest.mark.gpu
+TOL = 1e-5
+
+
+def _flat(espec, params):
+    n, layout = espec.param_infos()
+    flat = torch.empty(n, dtype=torch.float32)
+    for name, off, shape in layout:
+        flat[off:off + int(np.prod(shape))] = params[name].reshape(-1)
+    return flat.cuda()
+
+
+def _check(vals, ref, acts):
+    np.testing.assert_allclose(vals, ref, atol=TOL * max(1.0, float(np.abs(ref).max())), rtol=0)
+    srt = np.sort(ref, axis=1)
+    clear = (srt[:, -1] - srt[:, -2]) > 4 * TOL * max(1.0, float(np.abs(ref).max()))
+    assert np.array_equal(acts[clear], ref.argmax(axis=1)[clear])
+    assert clear.mean() > 0.9
+
+
+@pytest.mark.parametrize("obs_dim", [14, 284])
+@pytest.mark.parametrize("head", ["dueling", "linear"])
+@pytest.mark.parametrize("n", [1, 2, 3, 8, 37, 1000])
+def test_gpu_act_matches_oracle(obs_dim, head, n):
+    ospec = O.mlp_spec(obs_dim, 8, head)
+    params = O.reference_init(ospec, 5)
+    espec = E.mlp_spec(obs_dim, 8, head)
+    flat = _flat(espec, params)
+    x = torch.from_numpy(np.random.default_rng(n).random((n, obs_dim), dtype=np.float32))
+    vals = torch.empty(n, 8, dtype=torch.float32, device="cuda")
+    acts = E.act(espec, flat, x.cuda(), vals)
+    torch.cuda.synchronize()
+    with torch.no_grad():
+        ref = (O.advantages(ospec, params, x) if head == "dueling" else O.q_forward(ospec, params, x)).numpy()
+    _check(vals.cpu().numpy(), ref, acts.cpu().numpy())
+
+
+def test_gpu_act_elu_deep_wide_body():
+    """ELU body, 3 layers up to 600 wide, odd action count: the generic layer loop."""
+    spec = E.NetSpec(kind=E.C.DQNX_NET_MLP, head=E.C.DQNX_HEAD_LINEAR, activation=E.C.DQNX_ACT_ELU,
+                     obs_dim=37, n_actions=5, dense=(600, 130, 64))
+    n_params, layout = spec.param_infos()
+    g = torch.Generator().manual_seed(0)
+    flat = torch.randn(n_params, generator=g) * 0.2
+    P = {name: flat[off:off + int(np.prod(s))].view(*s) for name, off, s in layout}
+    x = torch.randn(9, 37, generator=g)
+    h = x
+    for l in range(3):
+        h = F.elu(F.linear(h, P[f"net.{2 * l}.weight"], P[f"net.{2 * l}.bias"]))
+    ref = F.linear(h, P["fc_out.weight"], P["fc_out.bias"]).numpy()
+    vals = torch.empty(9, 5, device="cuda")
+    acts = E.act(spec, flat.cuda(), x.cuda(), vals)
+    _check(vals.cpu().numpy(), ref, acts.cpu().numpy())
+
+
+def test_gpu_act_shared_scratch_across_row_counts():
+    """One scratch serves calls with different n in any order (tickets never clobbered)."""
+    ospec = O.mlp_spec(284, 8, "dueling")
+    params = O.reference_init(ospec, 6)
+    espec = E.mlp_spec(284, 8, "dueling")
+    flat = _flat(espec, params)
+    scratch = E.act_scratch(espec, 64, "cuda")
+    rng = np.random.default_rng(0)
+    for n in (64, 1, 3, 2, 64, 5, 1, 33):
+        x = torch.from_numpy(rng.random((n, 284), dtype=np.float32))
+        vals = torch.empty(n, 8, device="cuda")
+        acts = E.act(espec, flat, x.cuda(), vals, scratch=scratch)
+        with torch.no_grad():
+            ref = O.advantages(ospec, params, x).numpy()
+        _check(vals.cpu().numpy(), ref, acts.cpu().numpy())
+
+
+def test_gpu_act_rejects_two_stream():
+    spec = E.hybrid_spec()
+    with pytest.raises(NotImplementedError):
+        E.act(spec, torch.zeros(10, device="cuda"), torch.zeros(1, spec.obs_dim, device="cuda"))
+
+
+@pytest.mark.parametrize("cls", [DeepQNetwork, DuelingDeepQNetwork])
+def test_gpu_standalone_network_actions(cls):
+    """Observe-style use (R:observe.py:24-37): a network built on its own, then reloaded."""
+    torch.manual_seed(3)
+    net = cls("cuda:0", 1e-4, mlp_network_config, Box(284), 8)
+    x = np.random.default_rng(1).random((4, 284), dtype=np.float32)
+    xt = torch.from_numpy(x).cuda()
+    with torch.no_grad():
+        ref = (net.advantages(xt) if cls is DuelingDeepQNetwork else net(xt)).argmax(1).tolist()
+    assert net.actions(x) == ref
+    # new weights through load_state_dict land in the kernel's buffer
+    torch.manual_seed(4)
+    other = cls("cuda:0", 1e-4, mlp_network_config, Box(284), 8)
+    net.load_state_dict(other.state_dict())
+    with torch.no_grad():
+        ref2 = (other.advantages(xt) if cls is DuelingDeepQNetwork else other(xt)).argmax(1).tolist()
+    assert net.actions(x) == ref2
