@@ -72,6 +72,76 @@ __global__ __launch_bounds__(256) void k_im2col_flat(Im2colArgs a) {
     }
 }
 
+// One workgroup per output image row (z, b, ho): the kh input rows it reads (all Ci channels,
+// all Wi columns, zeros outside the image) are staged once into LDS as [i][ci][w] with
+// coalesced global reads, then the Wo output rows -- one contiguous [Wo][Kstride] block of the
+// column matrix -- are written with consecutive threads on consecutive addresses.  The
+// row-per-wave kernel above reads the NHWC source at a 4*Ci-byte stride across lanes (k runs
+// over (ci, i, j)), i.e. about one cache line per element; here every input byte of the row
+// band is read once per band.  Bit-identical output (a copy).
+__global__ __launch_bounds__(256) void k_im2col_lds(Im2colArgs a) {
+    extern __shared__ float band[];   // [kh][Ci][Wi], then the per-column table [Kstride]
+    const int HoWo = a.Ho * a.Wo, KK = a.kh * a.kw;
+    const int Bl = a.M / HoWo;
+    const int blk = blockIdx.x;
+    const int z = blk / (Bl * a.Ho);
+    const int rem = blk - z * Bl * a.Ho;
+    const int b = rem / a.Ho, ho = rem - b * a.Ho;
+    const int hbase = ho * a.sh - a.ph;
+    const int CW = a.Ci * a.Wi;
+    const int nband = a.kh * CW;
+    int* tab = reinterpret_cast<int*>(band + nband);   // column kk -> (band offset of (i, ci, w=j) << 8) | j, or -1
+    const int tid = threadIdx.x;
+    // index math is incremental (one division per thread up front): at these sizes the
+    // per-element divisions, not the bytes, were the cost
+    for (int kk = tid; kk < a.Kstride; kk += 256) {
+        int v = -1;
+        if (kk < a.K) {
+            const int ci = kk / KK, rr = kk - ci * KK;
+            const int i = rr / a.kw, j = rr - i * a.kw;
+            v = (((i * a.Ci + ci) * a.Wi + j) << 8) | j;
+        }
+        tab[kk] = v;
+    }
+    const float* ring = a.ring[z];
+    for (int i = 0; i < a.kh; i++) {
+        const int h = hbase + i;
+        const bool inside = h >= 0 && h < a.Hi;
+        float* dst = band + i * CW;
+        if (ring) {   // conv 1: CHW micro grid inside the ring row, w fastest
+            const float* src = ring + (int64_t)a.phys[b] * a.ring_stride + a.ring_off + h * a.Wi;
+            const int sw_ = 256 / a.Wi, sr = 256 - sw_ * a.Wi;
+            int ci = tid / a.Wi, w = tid - ci * a.Wi;
+            for (int t = tid; t < CW; t += 256) {
+                dst[t] = inside ? src[ci * a.Hi * a.Wi + w] : 0.f;
+                ci += sw_; w += sr;
+                if (w >= a.Wi) { w -= a.Wi; ci++; }
+            }
+        } else {      // NHWC activations, ci fastest (coalesced), transposed into [ci][w]
+            const float* src = a.src[z] + ((int64_t)(b * a.Hi + h) * a.Wi) * a.Ci;
+            const int sw_ = 256 / a.Ci, sc = 256 - sw_ * a.Ci;
+            int w = tid / a.Ci, ci = tid - w * a.Ci;
+            for (int t = tid; t < CW; t += 256) {
+                dst[ci * a.Wi + w] = inside ? src[t] : 0.f;
+                w += sw_; ci += sc;
+                if (ci >= a.Ci) { ci -= a.Ci; w++; }
+            }
+        }
+    }
+    __syncthreads();
+    float* out = a.col[z] + ((int64_t)b * HoWo + (int64_t)ho * a.Wo) * a.Kstride;
+    const int total = a.Wo * a.Kstride;
+    const int so = 256 / a.Kstride, sk = 256 - so * a.Kstride;
+    int wo = tid / a.Kstride, kk = tid - wo * a.Kstride;
+    for (int t = tid; t < total; t += 256) {
+        const int e = tab[kk];
+        const int w = wo * a.sw - a.pw + (e & 255);
+        out[t] = (e >= 0 && w >= 0 && w < a.Wi) ? band[(e >> 8) + wo * a.sw - a.pw] : 0.f;
+        wo += so; kk += sk;
+        if (kk >= a.Kstride) { kk -= a.Kstride; wo++; }
+    }
+}
+
 __global__ __launch_bounds__(256) void k_flatten_concat(FlattenArgs a) {
     const int64_t per = (int64_t)a.Bl * a.strideF;
     const int64_t total = per * a.nstreams;
@@ -143,7 +213,28 @@ static dim3 grid_for(int64_t total) {
     return dim3((unsigned)g);
 }
 
+int im2col_mode() {
+    static int mode = -1;   // DQNX_IM2COL: 0 = flat/row kernels only, 1 = LDS band kernel where it fits (default)
+    if (mode < 0) {
+        const char* e = getenv("DQNX_IM2COL");
+        mode = e ? atoi(e) : 1;
+    }
+    return mode;
+}
+
 int launch_im2col(const Im2colArgs& a, hipStream_t s) {
+    const size_t band = (size_t)a.kh * a.Ci * a.Wi * sizeof(float) + (size_t)a.Kstride * sizeof(int);
+    // the band kernel pays off when one output image row is a large block (the (4,84,84)
+    // variant); the (2,27,5) grid's rows are a few KB and stay on the kernels below
+    // measured on the (4,84,84) variant, B=256: conv 1 819 -> 263 us, conv 2 2102 -> 1156 us; conv 3
+    // (stride 2x2, a 67 KB band: 2 workgroups per CU) was slower, 955 -> 1310 us, hence the 64 KB cap
+    if (im2col_mode() == 1 && band <= 64 * 1024 && a.M % (a.Ho * a.Wo) == 0 && a.Wo * a.Kstride >= 2048 &&
+        a.kw < 256 && (size_t)a.kh * a.Ci * a.Wi < (1u << 23)) {
+        const int64_t g = (int64_t)a.nstreams * (a.M / (a.Ho * a.Wo)) * a.Ho;
+        hipLaunchKernelGGL(k_im2col_lds, dim3((unsigned)g), dim3(256), band, s, a);
+        DQNX_HIP_CHECK(hipGetLastError());
+        return DQNX_OK;
+    }
     if (a.Kstride < 64) {   // measured: conv 1 (K 18 / 36) 30 -> 15 us / 1.40 -> 0.82 ms; K >= 288 slower
         int64_t g = ((int64_t)a.M * a.nstreams * a.Kstride + 255) / 256;
         if (g > 16384) g = 16384;

@@ -140,7 +140,7 @@ def act_scratch(spec: NetSpec, n: int, device) -> torch.Tensor:
 
 
 def act(spec: NetSpec, flat: torch.Tensor, obs: torch.Tensor, values: Optional[torch.Tensor] = None,
-        scratch: Optional[torch.Tensor] = None) -> torch.Tensor:
+        scratch: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None, desc=None) -> torch.Tensor:
     """Greedy actions of an MLP Q-network, one HIP launch (`dqnx_act`).
 
     `flat`: the network's flat fp32 parameters on the GPU (dqnx_net_param_info layout);
@@ -153,18 +153,21 @@ def act(spec: NetSpec, flat: torch.Tensor, obs: torch.Tensor, values: Optional[t
     if obs.dim() != 2 or obs.shape[1] != spec.obs_dim:
         raise ValueError(f"obs must be [n, {spec.obs_dim}], got {tuple(obs.shape)}")
     n = obs.shape[0]
-    out = torch.empty(n, dtype=torch.int32, device=flat.device)
+    if out is None:
+        out = torch.empty(n, dtype=torch.int32, device=flat.device)
+    elif out.dtype != torch.int32 or out.device != flat.device or out.numel() < n or not out.is_contiguous():
+        raise ValueError("out must be a contiguous int32 tensor of >= n elements on the parameters' device")
     if values is not None and (values.shape != (n, spec.n_actions) or not values.is_contiguous()
                                or values.dtype != torch.float32 or values.device != flat.device):
         raise ValueError("values must be a contiguous fp32 [n, n_actions] tensor on the parameters' device")
     if scratch is None:
         scratch = act_scratch(spec, n, flat.device)
-    d = spec.to_c()
+    d = spec.to_c() if desc is None else desc
     stream = ctypes.c_void_p(torch.cuda.current_stream(flat.device).cuda_stream)
     C.check(C.lib().dqnx_act(ctypes.byref(d), flat.data_ptr(), obs.data_ptr(), n, out.data_ptr(),
                              values.data_ptr() if values is not None else None, scratch.data_ptr(),
                              scratch.numel() * 4, stream), "act")
-    return out
+    return out[:n]
 
 
 # ----------------------------------------------------------------------------------------

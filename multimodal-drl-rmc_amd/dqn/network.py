@@ -35,8 +35,7 @@ class Network(nn.Module):
         self._act_flat = None       # flat fp32 parameter buffer the acting kernel reads
         self._act_ptrs = None       # data_ptr of every parameter when _act_flat was bound
         self._act_engine = False    # _act_flat belongs to a learn engine
-        self._act_scratch = None    # dqnx_act scratch, sized for _act_scratch_rows rows
-        self._act_scratch_rows = 0
+        self._act_bufs = None       # (rows, desc, scratch, device obs/actions, pinned obs/actions)
 
     def forward(self, s):
         raise NotImplementedError
@@ -66,13 +65,31 @@ class Network(nn.Module):
         head = self.fc_adv if hasattr(self, "fc_adv") else self.fc_out
         return head.out_features
 
-    def _act_gpu(self, obses_t):
+    def _act_gpu(self, obses):
+        """Greedy actions through dqnx_act: obs staged through pinned memory, one launch, the
+        actions copied back and the stream synchronised once (the caller needs a list)."""
         spec, flat = self._native_act()
-        x = obses_t.reshape(obses_t.shape[0], -1)
-        if x.shape[0] > self._act_scratch_rows:
-            self._act_scratch = act_scratch(spec, x.shape[0], flat.device)
-            self._act_scratch_rows = x.shape[0]
-        return _act_native(spec, flat, x, scratch=self._act_scratch).tolist()
+        x = T.as_tensor(obses, dtype=T.float32)
+        n = x.shape[0]
+        x = x.reshape(n, -1)
+        if self._act_bufs is None or self._act_bufs[0] < n or self._act_bufs[1] is not spec:
+            dev = flat.device
+            self._act_bufs = (n, spec, spec.to_c(), act_scratch(spec, n, dev),
+                              T.empty(n, spec.obs_dim, dtype=T.float32, device=dev),
+                              T.empty(n, dtype=T.int32, device=dev),
+                              T.empty(n, spec.obs_dim, dtype=T.float32).pin_memory(),
+                              T.empty(n, dtype=T.int32).pin_memory())
+        _, _, desc, scratch, d_obs, d_act, h_obs, h_act = self._act_bufs
+        if x.is_cuda:
+            d_in = x
+        else:
+            h_obs[:n].copy_(x)
+            d_obs[:n].copy_(h_obs[:n], non_blocking=True)
+            d_in = d_obs[:n]
+        _act_native(spec, flat, d_in, scratch=scratch, out=d_act, desc=desc)
+        h_act[:n].copy_(d_act[:n], non_blocking=True)
+        T.cuda.current_stream(flat.device).synchronize()
+        return h_act[:n].tolist()
 
     def _native_act(self):
         """(spec, flat) for the acting kernel, or None when the reference's torch forward is
@@ -122,9 +139,9 @@ class DeepQNetwork(Network):
         return self.fc_out(self.net(s))
 
     def actions(self, obses):
-        obses_t = T.as_tensor(obses, dtype=T.float32).to(self.device)
         if self._native_act() is not None:
-            return self._act_gpu(obses_t)
+            return self._act_gpu(obses)
+        obses_t = T.as_tensor(obses, dtype=T.float32).to(self.device)
         q_values = self(obses_t)
         return T.argmax(q_values, dim=1).detach().tolist()
 
@@ -152,8 +169,8 @@ class DuelingDeepQNetwork(Network):
         return self.fc_adv(self.net(s))
 
     def actions(self, obses):
-        obses_t = T.as_tensor(obses, dtype=T.float32).to(self.device)
         if self._native_act() is not None:
-            return self._act_gpu(obses_t)
+            return self._act_gpu(obses)
+        obses_t = T.as_tensor(obses, dtype=T.float32).to(self.device)
         adv_q_values = self.advantages(obses_t)
         return T.argmax(adv_q_values, dim=1).detach().tolist()

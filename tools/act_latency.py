@@ -45,9 +45,10 @@ def main():
         assert net.actions(x) == torch_path()
         spec, flat = net._native_act()
         res = torch.empty(n, dtype=torch.int32, device="cuda")
+        scratch, desc = E.act_scratch(spec, n, "cuda"), spec.to_c()
 
         def launch():
-            E.act(spec, flat, xt)
+            E.act(spec, flat, xt, scratch=scratch, out=res, desc=desc)
         ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         for _ in range(20):
             launch()
