@@ -146,6 +146,16 @@ static int plan_net(const dqnx_net_desc* d, NetPlan& np) {
     return DQNX_OK;
 }
 
+// DQNX_FWD_BIG=0 keeps every dense forward on the 16x64-tile kernel (A/B measurements)
+static bool fwd_big_mode() {
+    static int mode = -1;
+    if (mode < 0) {
+        const char* v = getenv("DQNX_FWD_BIG");
+        mode = v ? atoi(v) : 1;
+    }
+    return mode != 0;
+}
+
 static inline uint64_t align_up(uint64_t x, uint64_t a) { return (x + a - 1) / a * a; }
 
 struct KStep {
@@ -975,6 +985,25 @@ std::vector<KStep> build_learn_steps(dqnx_engine* e, int key) {
         k.bytes = 4.0 * (nstreams * Bl * lp.in + 2.0 * (lp.out * (double)lp.in + lp.out) + nstreams * Bl * lp.out
                          + (l == 0 && !NC ? Bl * lp.in : 0.0));
         const bool vecb = (lp.in % 4) == 0;
+        // large-K layers that read dense rows (not the ring gather): 128x128 tiles + split-K into
+        // the layer's dW partial slabs (free until the backward), then an ordered reduce
+        const uint64_t part_floats = (uint64_t)e->slices[l] * ((uint64_t)lp.out * lp.in + lp.out);
+        int kchunk = 0;
+        const int ksplit = fwd_big_ksplit(e->Bl, lp.out, lp.in, np_, (int64_t)part_floats, &kchunk);
+        if ((l > 0 || NC) && lp.in >= 8192 && e->Bl >= 64 && fwd_big_mode() &&
+            (uint64_t)ksplit * np_ * e->Bl * lp.out <= part_floats) {
+            fa.ksplit = ksplit;
+            fa.kchunk = kchunk;
+            fa.partial = at<float>(e, e->ws_part[l]);
+            k.run = [=](hipStream_t s) { return launch_linear_fwd_big(fa, np_, act, vecb, s); };
+            ks.push_back(k);
+            KStep kr;
+            kr.name = k.name + "_reduce";
+            kr.bytes = 4.0 * ((double)ksplit + 1) * np_ * Bl * lp.out;
+            kr.run = [=](hipStream_t s) { return launch_linear_fwd_reduce(fa, np_, act, s); };
+            ks.push_back(kr);
+            continue;
+        }
         k.run = [=](hipStream_t s) { return launch_linear_fwd(fa, np_, act, vecb, s); };
         ks.push_back(k);
     }

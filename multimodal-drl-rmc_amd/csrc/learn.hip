@@ -124,6 +124,61 @@ __global__ __launch_bounds__(256) void k_linear_fwd(FwdArgs args) {
     }
 }
 
+// Large-K forward (a 128x128 tile re-reads each weight row ntm = M/128 times instead of M/16):
+// split-K over ksplit chunks, raw sums to `partial`, then k_linear_fwd_reduce.
+template <int ACT, bool VECB>
+__global__ __launch_bounds__(256) void k_linear_fwd_big(FwdArgs args) {
+    using G = TileGemm<FWD_BIG_BM, FWD_BIG_BN, FWD_BIG_KT, 2, 2, L_ROWS_K, L_ROWS_K, true, VECB>;
+    constexpr int TM = G::TM, TN = G::TN;
+    __shared__ __attribute__((aligned(16))) float lds[G::LDS_FLOATS];
+    const int M = args.M, N = args.N, K = args.K;
+    const int ntn = (N + FWD_BIG_BN - 1) / FWD_BIG_BN, ntm = (M + FWD_BIG_BM - 1) / FWD_BIG_BM;
+    const int tiles = ntn * ntm * args.nprob;
+    // chunk-major order: an XCD's contiguous range shares one K chunk of A and W in its L2
+    const int T = xcd_remap(blockIdx.x, tiles * args.ksplit);
+    const int sl = T / tiles, T2 = T - sl * tiles;
+    const int z = T2 / (ntn * ntm), rem = T2 - z * ntn * ntm;
+    const int tm_ = rem / ntn, tn_ = rem - tm_ * ntn;
+    const FwdProblem& P = args.p[z];
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int i = lane & 15, g = lane >> 4;
+    const int m0 = tm_ * FWD_BIG_BM, n0 = tn_ * FWD_BIG_BN;
+    const int Kpad = (K + 3) & ~3;
+    const int kb = sl * args.kchunk, ke = min(Kpad, kb + args.kchunk);
+    Operand A{P.A, P.lda, nullptr, M, Kpad, -1, nullptr, P.lda};
+    Operand B{P.W, K, nullptr, N, K, -1, nullptr, 0};
+    floatx4 acc[TM][TN];
+    G::run(lds, A, B, m0, n0, kb, ke, acc);
+    const int ro = (wid / 2) * TM * 16, co = (wid % 2) * TN * 16;
+    float* part = args.partial + ((int64_t)sl * args.nprob + z) * M * N;
+#pragma unroll
+    for (int tn = 0; tn < TN; tn++) {
+        const int col = n0 + co + tn * 16 + i;
+        if (col >= N) continue;
+#pragma unroll
+        for (int tm = 0; tm < TM; tm++)
+#pragma unroll
+            for (int r = 0; r < 4; r++) {
+                const int row = m0 + ro + tm * 16 + 4 * g + r;
+                if (row < M) part[(int64_t)row * N + col] = acc[tm][tn][r];
+            }
+    }
+}
+
+template <int ACT>
+__global__ __launch_bounds__(256) void k_linear_fwd_reduce(FwdArgs args) {
+    const int M = args.M, N = args.N;
+    const int64_t per = (int64_t)M * N, total = per * args.nprob;
+    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
+        const int z = (int)(t / per);
+        const int64_t e = t - (int64_t)z * per;
+        const int row = (int)(e / N), col = (int)(e - (int64_t)row * N);
+        float s = args.partial[((int64_t)0 * args.nprob + z) * per + e];
+        for (int sl = 1; sl < args.ksplit; sl++) s += args.partial[((int64_t)sl * args.nprob + z) * per + e];
+        args.p[z].C[(int64_t)row * args.ldc + col] = act_fwd<ACT>(s + args.p[z].bias[col]);
+    }
+}
+
 // =====================================================================================
 // Backward level: independent GEMMs in one launch.
 //   dx role:  dZprev = (dZ W) (.) act'(Hprev)      [Bl x in], K = out
@@ -758,6 +813,45 @@ int launch_linear_fwd(const FwdArgs& args, int nprob, int act, bool vecb, hipStr
         if (vecb) launch_fwd_gather<DQNX_ACT_ELU, true>(a2, grid, s);
         else launch_fwd_gather<DQNX_ACT_ELU, false>(a2, grid, s);
     }
+    DQNX_HIP_CHECK(hipGetLastError());
+    return DQNX_OK;
+}
+
+int fwd_big_ksplit(int M, int N, int K, int nprob, int64_t partial_floats, int* kchunk) {
+    const int tiles = ((N + FWD_BIG_BN - 1) / FWD_BIG_BN) * ((M + FWD_BIG_BM - 1) / FWD_BIG_BM) * nprob;
+    const int Kpad = (K + 3) & ~3;
+    int S = std::max(1, std::min((512 + tiles - 1) / tiles, Kpad / (8 * FWD_BIG_KT)));
+    while (S > 1 && (int64_t)S * nprob * M * N > partial_floats) S--;
+    int kc = (Kpad + S - 1) / S;
+    kc = (kc + FWD_BIG_KT - 1) / FWD_BIG_KT * FWD_BIG_KT;
+    S = (Kpad + kc - 1) / kc;
+    *kchunk = kc;
+    return S;
+}
+
+int launch_linear_fwd_big(const FwdArgs& args, int nprob, int act, bool vecb, hipStream_t s) {
+    FwdArgs a2 = args;
+    a2.nprob = nprob;
+    const int tiles = ((args.N + FWD_BIG_BN - 1) / FWD_BIG_BN) * ((args.M + FWD_BIG_BM - 1) / FWD_BIG_BM) * nprob;
+    const dim3 grid(tiles * args.ksplit);
+    if (act == DQNX_ACT_RELU) {
+        if (vecb) hipLaunchKernelGGL((k_linear_fwd_big<DQNX_ACT_RELU, true>), grid, dim3(256), 0, s, a2);
+        else hipLaunchKernelGGL((k_linear_fwd_big<DQNX_ACT_RELU, false>), grid, dim3(256), 0, s, a2);
+    } else {
+        if (vecb) hipLaunchKernelGGL((k_linear_fwd_big<DQNX_ACT_ELU, true>), grid, dim3(256), 0, s, a2);
+        else hipLaunchKernelGGL((k_linear_fwd_big<DQNX_ACT_ELU, false>), grid, dim3(256), 0, s, a2);
+    }
+    DQNX_HIP_CHECK(hipGetLastError());
+    return DQNX_OK;
+}
+
+int launch_linear_fwd_reduce(const FwdArgs& args, int nprob, int act, hipStream_t s) {
+    FwdArgs a2 = args;
+    a2.nprob = nprob;
+    int64_t g = ((int64_t)args.M * args.N * nprob + 255) / 256;
+    if (g > 4096) g = 4096;
+    if (act == DQNX_ACT_RELU) hipLaunchKernelGGL((k_linear_fwd_reduce<DQNX_ACT_RELU>), dim3((unsigned)g), dim3(256), 0, s, a2);
+    else hipLaunchKernelGGL((k_linear_fwd_reduce<DQNX_ACT_ELU>), dim3((unsigned)g), dim3(256), 0, s, a2);
     DQNX_HIP_CHECK(hipGetLastError());
     return DQNX_OK;
 }

@@ -56,6 +56,11 @@ struct FwdArgs {
     FwdProblem p[3];
     int M, N, K, ldc;
     int nprob;
+    // large-K layers (k_linear_fwd_big): K split into ksplit chunks of kchunk columns; chunk s of
+    // problem z writes its raw sums to partial[(s * nprob + z) * M * N ...], a second launch adds
+    // them in chunk order (deterministic), then bias and activation
+    int ksplit, kchunk;
+    float* partial;
 };
 
 // One split-K weight-gradient GEMM: partial[s] = dZ^T [X | 1] over the samples of slice s.
@@ -399,6 +404,11 @@ int launch_per_sample(const PerSampleArgs& a, hipStream_t s);
 int launch_per_update(const PerUpdateArgs& a, hipStream_t s);
 
 int launch_linear_fwd(const FwdArgs& args, int nprob, int act, bool vecb, hipStream_t s);
+// large-K dense layers (the (4,84,84) variant's 56,462 -> 512): 128x128 tiles, split-K
+constexpr int FWD_BIG_BM = 128, FWD_BIG_BN = 128, FWD_BIG_KT = 32;
+int fwd_big_ksplit(int M, int N, int K, int nprob, int64_t partial_floats, int* kchunk);
+int launch_linear_fwd_big(const FwdArgs& args, int nprob, int act, bool vecb, hipStream_t s);
+int launch_linear_fwd_reduce(const FwdArgs& args, int nprob, int act, hipStream_t s);
 void bwd_level_grid(BwdArgs& a);
 int launch_bwd_level(const BwdArgs& a, int act, hipStream_t s);
 int launch_head(const HeadArgs& a, int act, hipStream_t s);

@@ -96,3 +96,41 @@ def test_gpu_hybrid_learn_golden():
         if got.size != ref.size:
             got = got[::stride]
         np.testing.assert_allclose(got, ref, atol=1e-5, rtol=0, err_msg=k)
+
+
+def test_gpu_hybrid84_learn_matches_oracle():
+    """The stacked (4,84,84) variant (BASELINE configs[2]) at B=64: exercises the LDS band im2col
+    (convs 1-2), the 128x128 split-K forward of the 56,462-wide dense layer and its ordered reduce.
+    Tolerances are those of the (2,27,5) cases, with the gradient check scale-relative (the
+    56,462-term sums differ from torch's CPU order by a few ulps of the largest terms)."""
+    E = _E()
+    from parity import assert_grad_close
+    algo, batch, cap, n_fill, seed = "DuelingDoubleDQNAgent", 64, 200, 150, 8
+    ospec = O.hybrid_spec(8, "dueling", micro_chw=(4, 84, 84))
+    init = O.reference_init(ospec, seed)
+    oracle = O.OracleLearner(ospec, algo, batch, cap, seed=seed, params=init)
+    data = O.synth_transitions(n_fill, ospec.obs_dim, 8, seed=seed + 100)
+    O.fill_replay(oracle, *data)
+    eng = E.LearnEngine(E.hybrid_spec(8, "dueling", micro_chw=(4, 84, 84)), algo, batch, cap)
+    eng.load_params(init)
+    eng.push(*data)
+    random.seed(seed + 7)
+    st = O.py_state_to_array()
+    oracle.py_state = st.copy()
+    eng.set_rng(0, st)
+    for step in range(2):
+        rec = oracle.train_step()
+        eng.learn_step(soft_update=True)
+        torch.cuda.synchronize()
+        eng.check_device_error()
+        assert np.array_equal(eng.batch_idx.cpu().numpy().astype(np.int64), rec.positions)
+        q = eng.q.cpu()
+        np.testing.assert_allclose(q[0].numpy(), rec.q_online.numpy(), atol=1e-5, rtol=1e-5)
+        np.testing.assert_allclose(q[2].numpy(), rec.q_target_next.numpy(), atol=1e-5, rtol=1e-5)
+        assert abs(eng.loss() - rec.loss) <= 1e-5 * max(1.0, abs(rec.loss))
+        g = eng.param_views(eng.grads[:-1])
+        for k, ref in rec.grads.items():
+            assert_grad_close(g[k].cpu(), ref, k)
+        on = eng.param_views(eng.params)
+        for k in oracle.online:
+            np.testing.assert_allclose(on[k].cpu().numpy(), oracle.online[k].numpy(), atol=1e-5, rtol=0, err_msg=k)
