@@ -919,7 +919,15 @@ std::vector<KStep> build_learn_steps(dqnx_engine* e, int key) {
         k.bytes = 4.0 * (nstreams * (double)M * (cp.Kstride + cp.Co) + 2.0 * cp.Co * (cp.K + 1.0));
         const bool vecb = (cp.K % 4) == 0;
         const int nps = np_;
-        k.run = [=](hipStream_t s) { return launch_linear_fwd(fa, nps, act, vecb, s); };
+        // conv GEMMs with enough rows to fill the chip with 128-row tiles (weight slab loaded once per
+        // 128 rows): (4,84,84) B=256 convs 1-3 1538/1849/717 -> 408/1228/546 us; (2,27,5) conv 1
+        // 31.6 -> 12.8 us, conv 3 (126 tiles) was slower on 128-row tiles and stays on 16 x 64
+        if (fwd_big_mode() && (int64_t)((fa.M + 127) / 128) * np_ >= 256) {
+            fa.ksplit = 1;
+            k.run = [=](hipStream_t s) { return launch_linear_fwd_big(fa, nps, act, vecb, s); };
+        } else {
+            k.run = [=](hipStream_t s) { return launch_linear_fwd(fa, nps, act, vecb, s); };
+        }
         ks.push_back(k);
     }
     if (NC) {   // 2b. cat(flatten_CHW(conv), macro) (R:env/dqn_config.py:135-138)

@@ -126,13 +126,18 @@ __global__ __launch_bounds__(256) void k_linear_fwd(FwdArgs args) {
 
 // Large-K forward (a 128x128 tile re-reads each weight row ntm = M/128 times instead of M/16):
 // split-K over ksplit chunks, raw sums to `partial`, then k_linear_fwd_reduce.
-template <int ACT, bool VECB>
+// ksplit == 1 (the conv GEMMs: M = B*Ho*Wo rows, N = Cout): bias + activation epilogue straight
+// into C.  A 128-row tile loads each weight K-slab once per 128 rows instead of once per 16.
+// The per-element accumulation order (K ascending, 16-deep MFMA chunks) is the one of the
+// 16x64 kernel, so both give bit-identical outputs.
+template <int ACT, bool VECB, int BM, int BN, int WM>
 __global__ __launch_bounds__(256) void k_linear_fwd_big(FwdArgs args) {
-    using G = TileGemm<FWD_BIG_BM, FWD_BIG_BN, FWD_BIG_KT, 2, 2, L_ROWS_K, L_ROWS_K, true, VECB>;
+    constexpr int WN = 4 / WM;
+    using G = TileGemm<BM, BN, FWD_BIG_KT, WM, WN, L_ROWS_K, L_ROWS_K, true, VECB>;
     constexpr int TM = G::TM, TN = G::TN;
     __shared__ __attribute__((aligned(16))) float lds[G::LDS_FLOATS];
     const int M = args.M, N = args.N, K = args.K;
-    const int ntn = (N + FWD_BIG_BN - 1) / FWD_BIG_BN, ntm = (M + FWD_BIG_BM - 1) / FWD_BIG_BM;
+    const int ntn = (N + BN - 1) / BN, ntm = (M + BM - 1) / BM;
     const int tiles = ntn * ntm * args.nprob;
     // chunk-major order: an XCD's contiguous range shares one K chunk of A and W in its L2
     const int T = xcd_remap(blockIdx.x, tiles * args.ksplit);
@@ -142,14 +147,30 @@ __global__ __launch_bounds__(256) void k_linear_fwd_big(FwdArgs args) {
     const FwdProblem& P = args.p[z];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const int i = lane & 15, g = lane >> 4;
-    const int m0 = tm_ * FWD_BIG_BM, n0 = tn_ * FWD_BIG_BN;
+    const int m0 = tm_ * BM, n0 = tn_ * BN;
     const int Kpad = (K + 3) & ~3;
     const int kb = sl * args.kchunk, ke = min(Kpad, kb + args.kchunk);
     Operand A{P.A, P.lda, nullptr, M, Kpad, -1, nullptr, P.lda};
     Operand B{P.W, K, nullptr, N, K, -1, nullptr, 0};
     floatx4 acc[TM][TN];
     G::run(lds, A, B, m0, n0, kb, ke, acc);
-    const int ro = (wid / 2) * TM * 16, co = (wid % 2) * TN * 16;
+    const int ro = (wid / WN) * TM * 16, co = (wid % WN) * TN * 16;
+    if (args.ksplit == 1) {
+#pragma unroll
+        for (int tn = 0; tn < TN; tn++) {
+            const int col = n0 + co + tn * 16 + i;
+            if (col >= N) continue;
+            const float bv = P.bias[col];
+#pragma unroll
+            for (int tm = 0; tm < TM; tm++)
+#pragma unroll
+                for (int r = 0; r < 4; r++) {
+                    const int row = m0 + ro + tm * 16 + 4 * g + r;
+                    if (row < M) P.C[(int64_t)row * args.ldc + col] = act_fwd<ACT>(acc[tm][tn][r] + bv);
+                }
+        }
+        return;
+    }
     float* part = args.partial + ((int64_t)sl * args.nprob + z) * M * N;
 #pragma unroll
     for (int tn = 0; tn < TN; tn++) {
@@ -829,18 +850,28 @@ int fwd_big_ksplit(int M, int N, int K, int nprob, int64_t partial_floats, int* 
     return S;
 }
 
+template <int BM, int BN, int WM>
+static void launch_fwd_big_t(const FwdArgs& a, int act, bool vecb, hipStream_t s) {
+    const int tiles = ((a.N + BN - 1) / BN) * ((a.M + BM - 1) / BM) * a.nprob;
+    const dim3 grid(tiles * a.ksplit);
+    if (act == DQNX_ACT_RELU) {
+        if (vecb) hipLaunchKernelGGL((k_linear_fwd_big<DQNX_ACT_RELU, true, BM, BN, WM>), grid, dim3(256), 0, s, a);
+        else hipLaunchKernelGGL((k_linear_fwd_big<DQNX_ACT_RELU, false, BM, BN, WM>), grid, dim3(256), 0, s, a);
+    } else {
+        if (vecb) hipLaunchKernelGGL((k_linear_fwd_big<DQNX_ACT_ELU, true, BM, BN, WM>), grid, dim3(256), 0, s, a);
+        else hipLaunchKernelGGL((k_linear_fwd_big<DQNX_ACT_ELU, false, BM, BN, WM>), grid, dim3(256), 0, s, a);
+    }
+}
+
 int launch_linear_fwd_big(const FwdArgs& args, int nprob, int act, bool vecb, hipStream_t s) {
     FwdArgs a2 = args;
     a2.nprob = nprob;
-    const int tiles = ((args.N + FWD_BIG_BN - 1) / FWD_BIG_BN) * ((args.M + FWD_BIG_BM - 1) / FWD_BIG_BM) * nprob;
-    const dim3 grid(tiles * args.ksplit);
-    if (act == DQNX_ACT_RELU) {
-        if (vecb) hipLaunchKernelGGL((k_linear_fwd_big<DQNX_ACT_RELU, true>), grid, dim3(256), 0, s, a2);
-        else hipLaunchKernelGGL((k_linear_fwd_big<DQNX_ACT_RELU, false>), grid, dim3(256), 0, s, a2);
-    } else {
-        if (vecb) hipLaunchKernelGGL((k_linear_fwd_big<DQNX_ACT_ELU, true>), grid, dim3(256), 0, s, a2);
-        else hipLaunchKernelGGL((k_linear_fwd_big<DQNX_ACT_ELU, false>), grid, dim3(256), 0, s, a2);
-    }
+    if (a2.ksplit < 1) a2.ksplit = 1;
+    if (a2.ksplit == 1) a2.kchunk = (args.K + 3) & ~3;
+    // tile width follows N (conv Cout 32 / 64): no MFMA work on padding columns
+    if (a2.ksplit == 1 && args.N <= 32) launch_fwd_big_t<128, 32, 4>(a2, act, vecb, s);
+    else if (a2.ksplit == 1 && args.N <= 64) launch_fwd_big_t<128, 64, 2>(a2, act, vecb, s);
+    else launch_fwd_big_t<FWD_BIG_BM, FWD_BIG_BN, 2>(a2, act, vecb, s);
     DQNX_HIP_CHECK(hipGetLastError());
     return DQNX_OK;
 }
