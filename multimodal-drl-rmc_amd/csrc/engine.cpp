@@ -1170,9 +1170,15 @@ std::vector<KStep> build_learn_steps(dqnx_engine* e, int key) {
             ba.W = params + cp.off;
             ba.kslice = e->ckslice[l];
             ba.dw_slices = e->cslices[l];
-            if (l > 0) {   // dCol = dZ W (no mask here: col2im applies the previous conv's ELU')
+            // dCol = dZ W (no mask here: col2im applies the previous conv's ELU'); on 128x64 tiles in
+            // its own launch when that fills the chip, else as the dx role of the level
+            const bool dx_big = l > 0 && fwd_big_mode() && conv_dx_big_tiles(M, cp.K) >= 256;
+            BwdArgs bdx;
+            if (l > 0) {
                 ba.Hprev = nullptr;
                 ba.dZprev = at<float>(e, e->ws_dcol);
+                bdx = ba;
+                if (dx_big) ba.dZprev = nullptr;
             }
             DwProblem& d = ba.dw[ba.ndw++];
             d.dZ = ba.dZ;
@@ -1191,7 +1197,19 @@ std::vector<KStep> build_learn_steps(dqnx_engine* e, int key) {
             k.bytes = 4.0 * ((double)M * (cp.Co + cp.Kstride) + ba.dw_slices * (double)d.pstride
                              + (l > 0 ? (double)M * cp.K + cp.Co * (double)cp.K : 0.0));
             k.run = [=](hipStream_t s) { return launch_bwd_level(ba, act, s); };
+            if (dx_big) {
+                k.flops = 2.0 * M * cp.Co * (cp.K + 1.0);
+                k.bytes = 4.0 * ((double)M * (cp.Co + cp.Kstride) + ba.dw_slices * (double)d.pstride);
+            }
             ks.push_back(k);
+            if (dx_big) {
+                KStep kx;
+                kx.name = "conv_dx_c" + std::to_string(l + 1);
+                kx.flops = 2.0 * M * cp.Co * (double)cp.K;
+                kx.bytes = 4.0 * ((double)M * cp.K + (double)M * cp.Co + cp.Co * (double)cp.K);
+                kx.run = [=](hipStream_t s) { return launch_conv_dx_big(bdx, s); };
+                ks.push_back(kx);
+            }
             if (l > 0) {
                 const ConvPlan pp = np.conv[l - 1];
                 Col2imArgs ca;

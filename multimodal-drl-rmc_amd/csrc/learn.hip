@@ -200,6 +200,50 @@ __global__ __launch_bounds__(256) void k_linear_fwd_reduce(FwdArgs args) {
     }
 }
 
+// Conv dX role on 128x64 tiles (dCol = dZ W, no mask: col2im applies the previous conv's ELU'),
+// for convs whose M = B*Ho*Wo rows fill the chip: the 32x32 dx role re-reads the weight per 32
+// rows and dZ per 32 columns.  Same K order as the 32x32 role: bit-identical dCol.
+template <bool VECW>
+__global__ __launch_bounds__(256) void k_conv_dx_big(BwdArgs a) {
+    constexpr int BM = 128, BN = 64, WM = 2, WN = 2;
+    using G = TileGemm<BM, BN, FWD_BIG_KT, WM, WN, L_ROWS_K, L_K_ROWS, true, VECW>;
+    constexpr int TM = G::TM, TN = G::TN;
+    __shared__ __attribute__((aligned(16))) float lds[G::LDS_FLOATS];
+    const int ntn = (a.in + BN - 1) / BN, ntm = (a.Bl + BM - 1) / BM;
+    const int T = xcd_remap(blockIdx.x, ntn * ntm);
+    const int tm_ = T / ntn, tn_ = T - tm_ * ntn;
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int i = lane & 15, g = lane >> 4;
+    const int m0 = tm_ * BM, n0 = tn_ * BN;
+    Operand A{a.dZ, a.out, nullptr, a.Bl, a.out, -1, nullptr, 0};
+    Operand B{a.W, a.in, nullptr, a.in, a.out, -1, nullptr, 0};
+    floatx4 acc[TM][TN];
+    G::run(lds, A, B, m0, n0, 0, a.out, acc);
+    const int ro = (wid / WN) * TM * 16, co = (wid % WN) * TN * 16;
+#pragma unroll
+    for (int tn = 0; tn < TN; tn++) {
+        const int col = n0 + co + tn * 16 + i;
+        if (col >= a.in) continue;
+#pragma unroll
+        for (int tm = 0; tm < TM; tm++)
+#pragma unroll
+            for (int r = 0; r < 4; r++) {
+                const int row = m0 + ro + tm * 16 + 4 * g + r;
+                if (row < a.Bl) a.dZprev[(int64_t)row * a.in + col] = acc[tm][tn][r];
+            }
+    }
+}
+
+int conv_dx_big_tiles(int Bl, int in) { return ((in + 63) / 64) * ((Bl + 127) / 128); }
+
+int launch_conv_dx_big(const BwdArgs& a, hipStream_t s) {
+    const dim3 grid(conv_dx_big_tiles(a.Bl, a.in));
+    if (a.in % 4 == 0) hipLaunchKernelGGL((k_conv_dx_big<true>), grid, dim3(256), 0, s, a);
+    else hipLaunchKernelGGL((k_conv_dx_big<false>), grid, dim3(256), 0, s, a);
+    DQNX_HIP_CHECK(hipGetLastError());
+    return DQNX_OK;
+}
+
 // =====================================================================================
 // Backward level: independent GEMMs in one launch.
 //   dx role:  dZprev = (dZ W) (.) act'(Hprev)      [Bl x in], K = out
