@@ -146,6 +146,8 @@ static int plan_net(const dqnx_net_desc* d, NetPlan& np) {
     return DQNX_OK;
 }
 
+constexpr int BWD_TILE = 32;   // k_bwd_level dW tile edge (DQNX_BWD_BM = DQNX_BWD_BN = 32)
+
 // DQNX_FWD_BIG=0 keeps every dense forward on the 16x64-tile kernel (A/B measurements)
 static bool fwd_big_mode() {
     static int mode = -1;
@@ -1577,11 +1579,18 @@ int dqnx_engine_create(const dqnx_config* cfg, dqnx_engine** out) {
     const int NC = (int)e->np.conv.size();
     e->cslices.assign(NC, 1);
     e->ckslice.assign(NC, 1);
+    // conv dW workgroups to aim for: the (4,84,84) conv 1 ([32 x 37] tile grid 2 x 1) had only
+    // 64 workgroups at the old 32-slice cap; DQNX_CONV_DW_WGS=0 restores that rule
+    int dw_wgs = 1024;
+    if (const char* v = getenv("DQNX_CONV_DW_WGS")) dw_wgs = std::max(0, atoi(v));
     for (int l = 0; l < NC; l++) {   // split-K over the conv's output pixels (b, ho, wo)
-        const int rows = e->Bl * e->np.conv[l].Ho * e->np.conv[l].Wo;
+        const ConvPlan& cq = e->np.conv[l];
+        const int rows = e->Bl * cq.Ho * cq.Wo;
         int S = rows / 512;
         if (S < 1) S = 1;
         if (S > 32) S = 32;
+        const int tiles = ((cq.K + 1 + BWD_TILE - 1) / BWD_TILE) * ((cq.Co + BWD_TILE - 1) / BWD_TILE);
+        if (dw_wgs > 0) S = std::max(S, std::min({rows / 512, (dw_wgs + tiles - 1) / tiles, 256}));
         int ks = (int)align_up((uint64_t)((rows + S - 1) / S), 16);
         S = (rows + ks - 1) / ks;
         e->cslices[l] = S;
