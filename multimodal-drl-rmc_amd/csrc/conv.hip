@@ -79,29 +79,35 @@ __global__ __launch_bounds__(256) void k_im2col_flat(Im2colArgs a) {
 // row-per-wave kernel above reads the NHWC source at a 4*Ci-byte stride across lanes (k runs
 // over (ci, i, j)), i.e. about one cache line per element; here every input byte of the row
 // band is read once per band.  Bit-identical output (a copy).
-__global__ __launch_bounds__(256) void k_im2col_lds(Im2colArgs a) {
-    extern __shared__ float band[];   // [kh][Ci][Wi], then the per-column table [Kstride]
+// Channel groups (grid.x = rows * G): workgroup g of a row stages channels [g*Cg, (g+1)*Cg) only
+// and writes their column range [g*Cg*KK, ...) of each of the Wo rows (the last group also
+// the zero padding up to Kstride), keeping the band at <= 32 KB.
+__global__ __launch_bounds__(256) void k_im2col_lds(Im2colArgs a, int G) {
+    extern __shared__ float band[];   // [kh][Cg][Wi], then the per-column table
     const int HoWo = a.Ho * a.Wo, KK = a.kh * a.kw;
     const int Bl = a.M / HoWo;
-    const int blk = blockIdx.x;
+    const int blk = blockIdx.x / G, grp = blockIdx.x - (blockIdx.x / G) * G;
     const int z = blk / (Bl * a.Ho);
     const int rem = blk - z * Bl * a.Ho;
     const int b = rem / a.Ho, ho = rem - b * a.Ho;
     const int hbase = ho * a.sh - a.ph;
-    const int CW = a.Ci * a.Wi;
+    const int Cg = a.Ci / G, c0 = grp * Cg;
+    const int kk0 = c0 * KK, kk1 = grp == G - 1 ? a.Kstride : (c0 + Cg) * KK, Wk = kk1 - kk0;
+    const int CW = Cg * a.Wi;
     const int nband = a.kh * CW;
-    int* tab = reinterpret_cast<int*>(band + nband);   // column kk -> (band offset of (i, ci, w=j) << 8) | j, or -1
+    int* tab = reinterpret_cast<int*>(band + nband);   // local column -> (band offset of (i, ci, w=j) << 8) | j, or -1
     const int tid = threadIdx.x;
     // index math is incremental (one division per thread up front): at these sizes the
     // per-element divisions, not the bytes, were the cost
-    for (int kk = tid; kk < a.Kstride; kk += 256) {
+    for (int kl = tid; kl < Wk; kl += 256) {
+        const int kk = kk0 + kl;
         int v = -1;
         if (kk < a.K) {
-            const int ci = kk / KK, rr = kk - ci * KK;
+            const int ci = kk / KK - c0, rr = kk - (ci + c0) * KK;
             const int i = rr / a.kw, j = rr - i * a.kw;
-            v = (((i * a.Ci + ci) * a.Wi + j) << 8) | j;
+            v = (((i * Cg + ci) * a.Wi + j) << 8) | j;
         }
-        tab[kk] = v;
+        tab[kl] = v;
     }
     const float* ring = a.ring[z];
     for (int i = 0; i < a.kh; i++) {
@@ -109,7 +115,7 @@ __global__ __launch_bounds__(256) void k_im2col_lds(Im2colArgs a) {
         const bool inside = h >= 0 && h < a.Hi;
         float* dst = band + i * CW;
         if (ring) {   // conv 1: CHW micro grid inside the ring row, w fastest
-            const float* src = ring + (int64_t)a.phys[b] * a.ring_stride + a.ring_off + h * a.Wi;
+            const float* src = ring + (int64_t)a.phys[b] * a.ring_stride + a.ring_off + h * a.Wi + (int64_t)c0 * a.Hi * a.Wi;
             const int sw_ = 256 / a.Wi, sr = 256 - sw_ * a.Wi;
             int ci = tid / a.Wi, w = tid - ci * a.Wi;
             for (int t = tid; t < CW; t += 256) {
@@ -118,27 +124,45 @@ __global__ __launch_bounds__(256) void k_im2col_lds(Im2colArgs a) {
                 if (w >= a.Wi) { w -= a.Wi; ci++; }
             }
         } else {      // NHWC activations, ci fastest (coalesced), transposed into [ci][w]
-            const float* src = a.src[z] + ((int64_t)(b * a.Hi + h) * a.Wi) * a.Ci;
-            const int sw_ = 256 / a.Ci, sc = 256 - sw_ * a.Ci;
-            int w = tid / a.Ci, ci = tid - w * a.Ci;
+            const float* src = a.src[z] + ((int64_t)(b * a.Hi + h) * a.Wi) * a.Ci + c0;
+            const int sw_ = 256 / Cg, sc = 256 - sw_ * Cg;
+            int w = tid / Cg, ci = tid - w * Cg;
             for (int t = tid; t < CW; t += 256) {
-                dst[ci * a.Wi + w] = inside ? src[t] : 0.f;
+                dst[ci * a.Wi + w] = inside ? src[(int64_t)w * a.Ci + ci] : 0.f;
                 w += sw_; ci += sc;
-                if (ci >= a.Ci) { ci -= a.Ci; w++; }
+                if (ci >= Cg) { ci -= Cg; w++; }
             }
         }
     }
     __syncthreads();
-    float* out = a.col[z] + ((int64_t)b * HoWo + (int64_t)ho * a.Wo) * a.Kstride;
-    const int total = a.Wo * a.Kstride;
-    const int so = 256 / a.Kstride, sk = 256 - so * a.Kstride;
-    int wo = tid / a.Kstride, kk = tid - wo * a.Kstride;
+    float* out = a.col[z] + ((int64_t)b * HoWo + (int64_t)ho * a.Wo) * a.Kstride + kk0;
+    if ((Wk & 3) == 0 && (kk0 & 3) == 0 && (a.Kstride & 3) == 0) {   // 16-byte stores
+        const int W4 = Wk >> 2, total = a.Wo * W4;
+        const int so = 256 / W4, sk = 256 - so * W4;
+        int wo = tid / W4, q = tid - wo * W4;
+        for (int t = tid; t < total; t += 256) {
+            float v[4];
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const int e = tab[4 * q + u];
+                const int w = wo * a.sw - a.pw + (e & 255);
+                v[u] = (e >= 0 && w >= 0 && w < a.Wi) ? band[(e >> 8) + wo * a.sw - a.pw] : 0.f;
+            }
+            *reinterpret_cast<float4*>(out + (int64_t)wo * a.Kstride + 4 * q) = make_float4(v[0], v[1], v[2], v[3]);
+            wo += so; q += sk;
+            if (q >= W4) { q -= W4; wo++; }
+        }
+        return;
+    }
+    const int total = a.Wo * Wk;
+    const int so = 256 / Wk, sk = 256 - so * Wk;
+    int wo = tid / Wk, kl = tid - wo * Wk;
     for (int t = tid; t < total; t += 256) {
-        const int e = tab[kk];
+        const int e = tab[kl];
         const int w = wo * a.sw - a.pw + (e & 255);
-        out[t] = (e >= 0 && w >= 0 && w < a.Wi) ? band[(e >> 8) + wo * a.sw - a.pw] : 0.f;
-        wo += so; kk += sk;
-        if (kk >= a.Kstride) { kk -= a.Kstride; wo++; }
+        out[(int64_t)wo * a.Kstride + kl] = (e >= 0 && w >= 0 && w < a.Wi) ? band[(e >> 8) + wo * a.sw - a.pw] : 0.f;
+        wo += so; kl += sk;
+        if (kl >= Wk) { kl -= Wk; wo++; }
     }
 }
 
@@ -223,15 +247,17 @@ int im2col_mode() {
 }
 
 int launch_im2col(const Im2colArgs& a, hipStream_t s) {
-    const size_t band = (size_t)a.kh * a.Ci * a.Wi * sizeof(float) + (size_t)a.Kstride * sizeof(int);
+    // channel groups: the smallest G dividing Ci whose band fits 32 KB
+    int G = 1;
+    while (G < a.Ci && ((size_t)a.kh * (a.Ci / G) * a.Wi * sizeof(float) > 32 * 1024 || a.Ci % G)) G++;
+    const size_t band = (size_t)a.kh * (a.Ci / G) * a.Wi * sizeof(float) + (size_t)a.Kstride * sizeof(int);
     // the band kernel pays off when one output image row is a large block (the (4,84,84)
-    // variant); the (2,27,5) grid's rows are a few KB and stay on the kernels below
-    // measured on the (4,84,84) variant, B=256: conv 1 819 -> 263 us, conv 2 2102 -> 1156 us; conv 3
-    // (stride 2x2, a 67 KB band: 2 workgroups per CU) was slower, 955 -> 1310 us, hence the 64 KB cap
+    // variant); the (2,27,5) grid's rows are a few KB and stay on the kernels below.
+    // measured on the (4,84,84) variant, B=256: conv 1 819 -> 263 us, conv 2 2102 -> 1156 us
     if (im2col_mode() == 1 && band <= 64 * 1024 && a.M % (a.Ho * a.Wo) == 0 && a.Wo * a.Kstride >= 2048 &&
         a.kw < 256 && (size_t)a.kh * a.Ci * a.Wi < (1u << 23)) {
-        const int64_t g = (int64_t)a.nstreams * (a.M / (a.Ho * a.Wo)) * a.Ho;
-        hipLaunchKernelGGL(k_im2col_lds, dim3((unsigned)g), dim3(256), band, s, a);
+        const int64_t g = (int64_t)a.nstreams * (a.M / (a.Ho * a.Wo)) * a.Ho * G;
+        hipLaunchKernelGGL(k_im2col_lds, dim3((unsigned)g), dim3(256), band, s, a, G);
         DQNX_HIP_CHECK(hipGetLastError());
         return DQNX_OK;
     }
