@@ -1000,7 +1000,8 @@ std::vector<KStep> build_learn_steps(dqnx_engine* e, int key) {
         const uint64_t part_floats = (uint64_t)e->slices[l] * ((uint64_t)lp.out * lp.in + lp.out);
         int kchunk = 0;
         const int ksplit = fwd_big_ksplit(e->Bl, lp.out, lp.in, np_, (int64_t)part_floats, &kchunk);
-        if ((l > 0 || NC) && lp.in >= 8192 && e->Bl >= 64 && fwd_big_mode() &&
+        static const int big_min_k = getenv("DQNX_FWD_BIG_MINK") ? atoi(getenv("DQNX_FWD_BIG_MINK")) : 8192;
+        if ((l > 0 || NC) && lp.in >= big_min_k && e->Bl >= 64 && fwd_big_mode() &&
             (uint64_t)ksplit * np_ * e->Bl * lp.out <= part_floats) {
             fa.ksplit = ksplit;
             fa.kchunk = kchunk;
