@@ -102,9 +102,13 @@ class Network(nn.Module):
                 return self._act_spec, self._act_flat
             if self._act_engine:
                 raise RuntimeError("network parameters were moved out of the learn engine's buffer")
-        # standalone network (e.g. Observe): pack its parameters into one flat buffer once
-        spec = spec_from_body(self.net, self.net[0].in_features, self._act_head_dim(),
-                              dueling=hasattr(self, "fc_adv"))
+        # standalone network (e.g. Observe): pack its parameters into one flat buffer once.  A
+        # body outside the two reference families keeps the reference's torch forward.
+        try:
+            spec = spec_from_body(self.net, self.net[0].in_features, self._act_head_dim(),
+                                  dueling=hasattr(self, "fc_adv"))
+        except (NotImplementedError, AttributeError):
+            return None
         n, layout = spec.param_infos()
         dev = next(self.parameters()).device
         flat = T.empty(n, dtype=T.float32, device=dev)

@@ -68,3 +68,33 @@ def test_agent_classes_and_constructor_surface():
         "nn_conf_func", "input_dim", "output_dim", "batch_size", "min_buffer_size", "buffer_size",
         "update_target_frequency", "target_soft_update", "target_soft_update_tau", "save_frequency",
         "log_frequency", "save_dir", "log_dir", "load", "algo", "gpu"]
+
+
+def test_network_acting_path_selection_cpu():
+    """Network.actions picks dqnx_act only for MLP bodies on a GPU device: on a CPU device the
+    caller asked for the reference's torch forward, which must still give torch.argmax."""
+    import numpy as np
+    import torch
+    from dqn.network import DeepQNetwork, DuelingDeepQNetwork
+    from refnets import Box, mlp_network_config
+    for cls in (DeepQNetwork, DuelingDeepQNetwork):
+        torch.manual_seed(0)
+        net = cls("cpu", 1e-4, mlp_network_config, Box(14), 8)
+        assert net._native_act() is None
+        x = np.random.default_rng(0).random((5, 14), dtype=np.float32)
+        with torch.no_grad():
+            xt = torch.from_numpy(x)
+            ref = (net.advantages(xt) if cls is DuelingDeepQNetwork else net(xt)).argmax(1).tolist()
+        assert net.actions(x) == ref
+
+
+def test_act_scratch_layout_is_monotone():
+    """dqnx_act keeps activations at the front and tickets at the back of its scratch; sharing one
+    buffer across row counts is safe because the activation bytes never decrease with n."""
+    import ctypes
+    from dqn import _capi as C
+    from dqn import engine as E
+    d = E.mlp_spec(284, 8, "dueling").to_c()
+    sizes = [C.lib().dqnx_act_scratch_bytes(ctypes.byref(d), n) for n in range(1, 70)]
+    assert all(b >= a for a, b in zip(sizes, sizes[1:]))
+    assert sizes[0] == 256 * 4 + 4
