@@ -10,6 +10,6 @@ python - <<'PY'
 import json
 for n in ("h_0","h_1","h84_0","h84_1"):
     d=json.load(open(f"gpurun_out/hyb/{n}.json"))
-    ks={k["kernel"]:round(k["avg_us"],1) for k in d.get("kernels",[]) if "im2col" in k["kernel"] or "conv" in k["kernel"] or "linear_fwd" in k["kernel"] or "dx" in k["kernel"] or "col2im" in k["kernel"] or "adam" in k["kernel"]}
+    ks={k["kernel"]:round(k["avg_us"],1) for k in d.get("kernels",[]) if "im2col" in k["kernel"] or "conv" in k["kernel"] or "linear_fwd" in k["kernel"] or "dx" in k["kernel"] or "col2im" in k["kernel"] or "adam" in k["kernel"] or "flatten" in k["kernel"]}
     print(n, round(d["value"]), round(d["ms_per_step"]*1e3,1), ks)
 PY
