@@ -262,6 +262,47 @@ __global__ __launch_bounds__(256) void k_col2im(Col2imArgs a) {
     }
 }
 
+// k_col2im for the reference's 3x3 / padding-1 convs with strides SH x SW fixed at compile time
+// and a power-of-two channel count: the per-element index math of the generic kernel (runtime
+// divisions and remainders by Ci, Wi, Hi, the strides) was its cost, not its bytes.  Same (i, j)
+// order, same sums.
+template <int ACT, int SH, int SW>
+__global__ __launch_bounds__(256) void k_col2im_3x3(Col2imArgs a, int ci_shift) {
+    const int total = a.Bl * a.Hi * a.Wi * a.Ci;
+    const int cmask = a.Ci - 1;
+    for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < total; t += gridDim.x * blockDim.x) {
+        const int ci = t & cmask;
+        const int q = t >> ci_shift;
+        const int bh = q / a.Wi, w = q - bh * a.Wi;
+        const int b = bh / a.Hi, h = bh - b * a.Hi;
+        const float* dc = a.dcol + ci * 9;
+        float s = 0.f;
+#pragma unroll
+        for (int i = 0; i < 3; i++) {
+            const int hh = h + 1 - i;
+            if (hh < 0 || hh % SH) continue;
+            const int ho = hh / SH;
+            if (ho >= a.Ho) continue;
+#pragma unroll
+            for (int j = 0; j < 3; j++) {
+                const int ww = w + 1 - j;
+                if (ww < 0 || ww % SW) continue;
+                const int wo = ww / SW;
+                if (wo >= a.Wo) continue;
+                const int64_t m = ((int64_t)b * a.Ho + ho) * a.Wo + wo;
+                s += dc[m * a.ldcol + i * 3 + j];
+            }
+        }
+        a.dZprev[t] = act_bwd<ACT>(s, a.Hprev[t]);
+    }
+}
+
+template <int SH, int SW>
+static void launch_col2im_3x3(const Col2imArgs& a, int act, int shift, dim3 g, hipStream_t s) {
+    if (act == DQNX_ACT_RELU) hipLaunchKernelGGL((k_col2im_3x3<DQNX_ACT_RELU, SH, SW>), g, dim3(256), 0, s, a, shift);
+    else hipLaunchKernelGGL((k_col2im_3x3<DQNX_ACT_ELU, SH, SW>), g, dim3(256), 0, s, a, shift);
+}
+
 static dim3 grid_for(int64_t total) {
     int64_t g = (total + 255) / 256;
     if (g > 4096) g = 4096;
@@ -328,6 +369,17 @@ int launch_unflatten(const UnflattenArgs& a, hipStream_t s) {
 
 int launch_col2im(const Col2imArgs& a, int act, hipStream_t s) {
     const dim3 g = grid_for((int64_t)a.Bl * a.Hi * a.Wi * a.Ci);
+    const bool pow2 = a.Ci > 0 && (a.Ci & (a.Ci - 1)) == 0;
+    if (im2col_mode() == 1 && pow2 && a.kh == 3 && a.kw == 3 && a.ph == 1 && a.pw == 1 && a.sh <= 2 && a.sw <= 2) {
+        int shift = 0;
+        while ((1 << shift) < a.Ci) shift++;
+        if (a.sh == 1 && a.sw == 1) launch_col2im_3x3<1, 1>(a, act, shift, g, s);
+        else if (a.sh == 2 && a.sw == 1) launch_col2im_3x3<2, 1>(a, act, shift, g, s);
+        else if (a.sh == 1 && a.sw == 2) launch_col2im_3x3<1, 2>(a, act, shift, g, s);
+        else launch_col2im_3x3<2, 2>(a, act, shift, g, s);
+        DQNX_HIP_CHECK(hipGetLastError());
+        return DQNX_OK;
+    }
     if (act == DQNX_ACT_RELU) hipLaunchKernelGGL(k_col2im<DQNX_ACT_RELU>, g, dim3(256), 0, s, a);
     else hipLaunchKernelGGL(k_col2im<DQNX_ACT_ELU>, g, dim3(256), 0, s, a);
     DQNX_HIP_CHECK(hipGetLastError());
