@@ -14,6 +14,6 @@ timeout -k 10 300 python bench.py --net hybrid84 --batch 256 --steps 20 --warmup
 timeout -k 10 300 python bench.py --net hybrid --batch 256 --steps 100 --warmup 10 > $OUT/bench_hybrid.json 2> $OUT/bench_hybrid.err || exit $?
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_hybrid84 -o run -- \
     python bench.py --net hybrid84 --batch 256 --steps 10 --warmup 3 --no-cpu-baseline --no-kernel-timing > /dev/null 2> $OUT/prof_h84.err || exit $?
-timeout -k 10 120 python tools/act_latency.py > $OUT/act_latency.json || exit $?
-cat $OUT/bench_mlp.json; echo; cat $OUT/act_latency.json
+timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 || exit $?
+cat $OUT/bench_mlp.json; echo; cat $OUT/smoke.log
 echo done
