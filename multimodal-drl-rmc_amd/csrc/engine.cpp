@@ -911,7 +911,8 @@ std::vector<KStep> build_learn_steps(dqnx_engine* e, int key) {
         {
             KStep k;
             k.name = "im2col_c" + std::to_string(l + 1);
-            k.bytes = 4.0 * nstreams * (double)M * cp.Kstride * 2.0;
+            // algorithmic: write the column matrix once, read the source image once
+            k.bytes = 4.0 * nstreams * ((double)M * cp.Kstride + (double)Bl * cp.Ci * cp.Hi * cp.Wi);
             k.run = [=](hipStream_t s) { return launch_im2col(ia, s); };
             ks.push_back(k);
         }

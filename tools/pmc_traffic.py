@@ -27,6 +27,13 @@ NAMES = [   # (substring of the HIP kernel name, bench step name)
 ]
 
 
+# kernels launched more than once per step under one name: bench step names in dispatch order
+CYCLES = [
+    ("k_im2col_lds", ["im2col_c1", "im2col_c2", "im2col_c3"]),   # (4,84,84) variant
+    ("k_linear_fwd_big<1, true, 128, 64", ["conv_fwd_c2", "conv_fwd_c3"]),
+]
+
+
 def bench_name(kernel):
     for sub, nm in NAMES:
         if sub in kernel:
@@ -37,11 +44,22 @@ def bench_name(kernel):
 def main(root="gpurun_out/pmc", out="profiles/pmc_traffic_mlp_b1024.json"):
     vals = defaultdict(lambda: defaultdict(list))   # bench name -> counter -> per-dispatch values
     for f in glob.glob(os.path.join(root, "p*", "**", "*counter_collection.csv"), recursive=True):
+        cyc = defaultdict(list)   # (cycle index, counter) -> rows
         for r in csv.DictReader(open(f)):
-            nm = bench_name(r.get("Kernel_Name", ""))
+            kn = r.get("Kernel_Name", "")
+            ci = next((i for i, (sub, _) in enumerate(CYCLES) if sub in kn), None)
+            if ci is not None:
+                cyc[(ci, r["Counter_Name"])].append(r)
+                continue
+            nm = bench_name(kn)
             if nm is None:
                 continue
             vals[nm][r["Counter_Name"]].append(float(r["Counter_Value"]))
+        for (ci, cn), rows in cyc.items():
+            names = CYCLES[ci][1]
+            rows.sort(key=lambda r: int(r.get("Dispatch_Id", 0)))
+            for i, r in enumerate(rows):
+                vals[names[i % len(names)]][cn].append(float(r["Counter_Value"]))
     res = {}
     for nm, cs in vals.items():
         d = {k: sum(v) / len(v) for k, v in cs.items()}
