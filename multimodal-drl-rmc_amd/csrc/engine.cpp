@@ -148,6 +148,19 @@ static int plan_net(const dqnx_net_desc* d, NetPlan& np) {
 
 constexpr int BWD_TILE = 32;   // k_bwd_level dW tile edge (DQNX_BWD_BM = DQNX_BWD_BN = 32)
 
+// conv dW on 64x128 tiles (k_conv_dw_big) for convs of at least 64K output pixels per step and
+// a K of at least 127 (the (4,84,84) variant, B=256: conv 2 605 -> 421 us, conv 3 278 -> 226 us;
+// conv 1, K = 36, was slower on 128-wide tiles, 108 -> 382 us); DQNX_CONV_DW_BIG=0 keeps
+// k_bwd_level's 32x32 role
+static bool conv_dw_big(int64_t rows, int K) {
+    static int mode = -1;
+    if (mode < 0) {
+        const char* v = getenv("DQNX_CONV_DW_BIG");
+        mode = v ? atoi(v) : 1;
+    }
+    return mode != 0 && rows >= 65536 && K >= 127;
+}
+
 // DQNX_FWD_BIG=0 keeps every dense forward on the 16x64-tile kernel (A/B measurements)
 static bool fwd_big_mode() {
     static int mode = -1;
@@ -1200,7 +1213,21 @@ std::vector<KStep> build_learn_steps(dqnx_engine* e, int key) {
             k.flops = 2.0 * M * cp.Co * (cp.K + 1.0) + (l > 0 ? 2.0 * M * cp.Co * (double)cp.K : 0.0);
             k.bytes = 4.0 * ((double)M * (cp.Co + cp.Kstride) + ba.dw_slices * (double)d.pstride
                              + (l > 0 ? (double)M * cp.K + cp.Co * (double)cp.K : 0.0));
-            k.run = [=](hipStream_t s) { return launch_bwd_level(ba, act, s); };
+            if (conv_dw_big(M, cp.K)) {   // dx role (if any) runs as conv_dx_c* or stays in a level launch
+                BwdArgs bw = ba;
+                if (ba.dZprev) {    // small dx: keep it in its own level launch without the dW role
+                    BwdArgs bl = ba;
+                    bl.ndw = 0;
+                    bwd_level_grid(bl);
+                    KStep kl;
+                    kl.name = "conv_dxs_c" + std::to_string(l + 1);
+                    kl.run = [=](hipStream_t s) { return launch_bwd_level(bl, act, s); };
+                    ks.push_back(kl);
+                }
+                k.run = [=](hipStream_t s) { return launch_conv_dw_big(bw, s); };
+            } else {
+                k.run = [=](hipStream_t s) { return launch_bwd_level(ba, act, s); };
+            }
             if (dx_big) {
                 k.flops = 2.0 * M * cp.Co * (cp.K + 1.0);
                 k.bytes = 4.0 * ((double)M * (cp.Co + cp.Kstride) + ba.dw_slices * (double)d.pstride);
@@ -1591,7 +1618,9 @@ int dqnx_engine_create(const dqnx_config* cfg, dqnx_engine** out) {
         int S = rows / 512;
         if (S < 1) S = 1;
         if (S > 32) S = 32;
-        const int tiles = ((cq.K + 1 + BWD_TILE - 1) / BWD_TILE) * ((cq.Co + BWD_TILE - 1) / BWD_TILE);
+        const bool big = conv_dw_big(rows, cq.K);
+        const int tiles = big ? conv_dw_big_tiles(cq.K, cq.Co)
+                              : ((cq.K + 1 + BWD_TILE - 1) / BWD_TILE) * ((cq.Co + BWD_TILE - 1) / BWD_TILE);
         if (dw_wgs > 0) S = std::max(S, std::min({rows / 512, (dw_wgs + tiles - 1) / tiles, 256}));
         int ks = (int)align_up((uint64_t)((rows + S - 1) / S), 16);
         S = (rows + ks - 1) / ks;

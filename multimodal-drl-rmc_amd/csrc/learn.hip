@@ -234,6 +234,53 @@ __global__ __launch_bounds__(256) void k_conv_dx_big(BwdArgs a) {
     }
 }
 
+// Conv dW (partial[s] = dZ^T [X | 1] over the pixels of slice s) on 64x128 tiles for large
+// convs: the 32x32 role re-reads the column matrix X per 32 output channels and dZ per 32
+// columns.  Its own launch; the slab layout and the Adam-side slab sum are unchanged.
+__global__ __launch_bounds__(256) void k_conv_dw_big(BwdArgs a) {
+    constexpr int BM = 64, BN = 128, WM = 2, WN = 2;
+    using G = TileGemm<BM, BN, FWD_BIG_KT, WM, WN, L_K_ROWS, L_K_ROWS, true, true>;
+    constexpr int TM = G::TM, TN = G::TN;
+    __shared__ __attribute__((aligned(16))) float lds[G::LDS_FLOATS];
+    const DwProblem& d = a.dw[0];
+    const int ntn = (d.in + 1 + BN - 1) / BN, ntm = (d.out + BM - 1) / BM;
+    const int T = xcd_remap(blockIdx.x, ntn * ntm * a.dw_slices);
+    const int bz = T / (ntn * ntm), rem = T - bz * ntn * ntm;
+    const int by = rem / ntn, bx = rem - by * ntn;
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int i = lane & 15, g = lane >> 4;
+    const int m0 = by * BM, n0 = bx * BN;
+    const int kb = bz * a.kslice, ke = min(a.Bl, kb + a.kslice);
+    Operand A{d.dZ, d.ldz, nullptr, d.out, a.Bl, -1, nullptr, 0};
+    Operand B{d.X, d.ldx, nullptr, d.in, a.Bl, d.in, nullptr, 0};
+    floatx4 acc[TM][TN];
+    G::run(lds, A, B, m0, n0, kb, ke, acc);
+    const int ro = (wid / WN) * TM * 16, co = (wid % WN) * TN * 16;
+    float* part = d.partial + (int64_t)bz * d.pstride;
+#pragma unroll
+    for (int tn = 0; tn < TN; tn++) {
+        const int col = n0 + co + tn * 16 + i;
+        if (col > d.in) continue;
+#pragma unroll
+        for (int tm = 0; tm < TM; tm++)
+#pragma unroll
+            for (int r = 0; r < 4; r++) {
+                const int row = m0 + ro + tm * 16 + 4 * g + r;
+                if (row >= d.out) continue;
+                part[col < d.in ? (int64_t)row * d.in + col : (int64_t)d.out * d.in + row] = acc[tm][tn][r];
+            }
+    }
+}
+
+int conv_dw_big_tiles(int in, int out) { return ((in + 1 + 127) / 128) * ((out + 63) / 64); }
+
+int launch_conv_dw_big(const BwdArgs& a, hipStream_t s) {
+    const dim3 grid(conv_dw_big_tiles(a.dw[0].in, a.dw[0].out) * a.dw_slices);
+    hipLaunchKernelGGL(k_conv_dw_big, grid, dim3(256), 0, s, a);
+    DQNX_HIP_CHECK(hipGetLastError());
+    return DQNX_OK;
+}
+
 int conv_dx_big_tiles(int Bl, int in) { return ((in + 63) / 64) * ((Bl + 127) / 128); }
 
 int launch_conv_dx_big(const BwdArgs& a, hipStream_t s) {

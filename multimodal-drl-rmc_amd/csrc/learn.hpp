@@ -410,6 +410,8 @@ int fwd_big_ksplit(int M, int N, int K, int nprob, int64_t partial_floats, int* 
 int launch_linear_fwd_big(const FwdArgs& args, int nprob, int act, bool vecb, hipStream_t s);
 int launch_linear_fwd_reduce(const FwdArgs& args, int nprob, int act, hipStream_t s);
 int conv_dx_big_tiles(int Bl, int in);
+int conv_dw_big_tiles(int in, int out);
+int launch_conv_dw_big(const BwdArgs& a, hipStream_t s);
 int launch_conv_dx_big(const BwdArgs& a, hipStream_t s);
 void bwd_level_grid(BwdArgs& a);
 int launch_bwd_level(const BwdArgs& a, int act, hipStream_t s);
