@@ -1,21 +1,27 @@
 #!/usr/bin/env python3
 """bench.py -- DQN learn-step throughput (transitions/s) on MI355X through libdqnx.
 
-Workload (BASELINE.json configs[1]): synthetic 1ramp_1x3 state vectors (D=284, A=8),
-MLP(256,128) dueling Q-net, fp32, DuelingDoubleDQNAgent learn step, minibatch 1024 per
-GPU sampled from a GPU-resident replay ring of 1e6 transitions.  One "step" = one
-Agent.learn() + update_target_network() (R:train.py:99-101): sample (bit-exact CPython
-random.sample) -> gather -> online(s'), target(s'), online(s) -> Double-DQN TD target ->
-Huber -> backward -> Adam -> soft target update.
+One "step" = one Agent.learn() + update_target_network() (R:train.py:99-101): sample
+(bit-exact CPython random.sample) -> gather -> online(s'), target(s'), online(s) ->
+Double-DQN TD target -> Huber -> backward -> Adam -> soft target update, on synthetic
+1ramp_1x3-shaped transitions (D=284, A=8) in a GPU-resident replay ring of 1e6.
+
+Workloads (BASELINE.json configs):
+  * N = 1 (default): configs[1] -- MLP(256,128) dueling Q-net fp32, DuelingDoubleDQNAgent,
+    minibatch 1024.  The line also carries `configs3_n1` (the same learn step at configs[3]'s
+    global minibatch 4096 on this one GPU: the N = 1 point of the strong-scaling series) and
+    `projection_w8` (the rank-0 shard step of a world_size = 8 engine -- 512 rows + the global
+    4096-draw sampling + Adam -- timed here; the all-reduce is the only missing term).
+  * N > 1 (torchrun, one process per GPU, RCCL over xGMI): configs[3] strong scaling --
+    global minibatch 4096 (--global-batch), 4096/N rows per rank, every rank drawing the SAME
+    global index set from the same MT19937 state (reference-exact random.sample semantics),
+    one gradient all-reduce per step, the whole DP step replayed as one HIP graph.  The line
+    also carries `weak` (4096 rows per rank, same semantics).
 
     python bench.py [--gpus N --steps K --warmup W]
-    torchrun --nproc-per-node N bench.py --gpus N ...    (one process per GPU, RCCL)
+    torchrun --nproc-per-node N bench.py --gpus N ...
 
-Data parallel = weak scaling: every rank processes `--batch` transitions per step; all
-ranks draw the same global index set (batch * N) from the same MT19937 state and take
-their shard; gradients are summed with one RCCL all-reduce per step.
-
-Prints ONE JSON line on rank 0 (fields: see the driver contract in DESIGN.md).
+Prints ONE JSON line on rank 0 (fields: see the driver contract in DESIGN.md section 5).
 """
 import argparse
 import ctypes
@@ -50,14 +56,20 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=200)
     p.add_argument("--warmup", type=int, default=20)
-    p.add_argument("--batch", type=int, default=1024, help="transitions per GPU per step")
+    p.add_argument("--batch", type=int, default=None,
+                   help="minibatch of a one-GPU run (default 1024, configs[1]); rows per rank with --scaling weak "
+                        "(default 4096)")
+    p.add_argument("--global-batch", type=int, default=4096,
+                   help="N > 1, --scaling strong: global minibatch sharded over the ranks (configs[3]: 4096)")
+    p.add_argument("--scaling", default="strong", choices=["strong", "weak"],
+                   help="N > 1: strong = fixed global minibatch (configs[3]); weak = --batch rows per rank")
     p.add_argument("--capacity", type=int, default=None,
                    help="replay capacity (default 1e6; 1e5 for hybrid84: 113 KB rows)")
     p.add_argument("--obs-dim", type=int, default=284)
     p.add_argument("--actions", type=int, default=8)
     p.add_argument("--algo", default="DuelingDoubleDQNAgent")
     p.add_argument("--net", default="mlp", choices=["mlp", "hybrid", "hybrid84"],
-                   help="mlp: MLP-284 (configs[1]); hybrid: TwoStreamHybridNetwork on the (2,27,5) grid; "
+                   help="mlp: MLP-284 (configs[1]/[3]/[4]); hybrid: TwoStreamHybridNetwork on the (2,27,5) grid; "
                         "hybrid84: the stacked (4,84,84) occupancy-grid CNN variant (configs[2])")
     p.add_argument("--no-graphs", action="store_true")
     p.add_argument("--no-dp-graph", action="store_true",
@@ -65,11 +77,14 @@ def parse():
                         "instead of replaying them as one captured HIP graph")
     p.add_argument("--compute", default="fp32", choices=["fp32", "bf16"],
                    help="GEMM operand precision (bf16: BASELINE config 5; MLP only; fp32 accumulate, master weights, Adam)")
-    p.add_argument("--global-sampling", action="store_true",
-                   help="N > 1: every rank draws the same global minibatch (bit-exact with 1 GPU)")
+    p.add_argument("--local-sampling", action="store_true",
+                   help="N > 1, uniform replay: each rank draws its own rows from its own MT stream (plain data "
+                        "parallelism; NOT the reference's random.sample semantics)")
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--cpu-seconds", type=float, default=15.0)
+    p.add_argument("--cpu-seconds", type=float, default=6.0, help="seconds per CPU-baseline leg")
     p.add_argument("--no-kernel-timing", action="store_true")
+    p.add_argument("--no-extras", action="store_true",
+                   help="skip the secondary measurements (configs3_n1 / projection_w8 / weak)")
     p.add_argument("--prefetch", action="store_true",
                    help="overlap the next step's replay sampling with this step's compute on a "
                         "side stream (measured slower at batch 1024: cross-stream event waits)")
@@ -156,51 +171,294 @@ def net_name(args):
             "hybrid84": "TwoStreamHybrid(4x84x84)"}[args.net]
 
 
-WORKLOADS = {
-    "mlp": "configs[1]: synthetic 1ramp_1x3 state vectors, MLP Q-net fp32, GPU replay buffer",
-    "hybrid": "TwoStreamHybridNetwork (micro CNN on the 2x27x5 grid + 14 macro), fp32, GPU replay buffer",
-    "hybrid84": "configs[2]: stacked 4x84x84 occupancy-grid CNN encoder + dueling head, fp32, GPU replay buffer",
-}
+def workload_name(args, world):
+    """Which BASELINE.json config a line measures."""
+    per = args.algo.startswith("Per")
+    if args.net == "hybrid84":
+        return "configs[2]: stacked 4x84x84 occupancy-grid CNN encoder + dueling head, fp32, GPU replay buffer"
+    if args.net == "hybrid":
+        return ("TwoStreamHybridNetwork (micro CNN on the 2x27x5 grid + 14 macro; the reference HEAD net), "
+                "fp32, GPU replay buffer")
+    if per or args.compute == "bf16":
+        return (f"configs[4]: prioritised replay (GPU sum-tree) + double/dueling DQN, {args.compute} compute, "
+                f"MLP Q-net, synthetic 1ramp_1x3 state vectors")
+    if world > 1 and args.scaling == "strong":
+        return "configs[3]: MLP Q-net fp32, global minibatch sharded DP over the GPUs, RCCL grad all-reduce over xGMI"
+    if world > 1:
+        return "configs[3] weak-scaling variant: MLP Q-net fp32, fixed minibatch per GPU, RCCL grad all-reduce"
+    return "configs[1]: synthetic 1ramp_1x3 state vectors, MLP Q-net fp32, GPU replay buffer, 1 GPU"
 
 
-def cpu_baseline(args):
-    """The oracle's torch-CPU restatement of the same learn step (reference algorithm:
-    deque + random.sample + transitions_to_tensor + 3 forwards + Huber + autograd + Adam +
-    soft update), timed on this host's cores on a bounded sample."""
+# ----------------------------------------------------------------------------------------
+# CPU baseline: the oracle (torch-CPU restatement of the reference learn step)
+# ----------------------------------------------------------------------------------------
+def cpu_info():
+    """CPU model and core counts of this host (lscpu), and the CPUs this process may use."""
+    model, phys = None, None
+    try:
+        import subprocess
+        out = subprocess.run(["lscpu", "-p=CORE,SOCKET"], capture_output=True, text=True, timeout=10).stdout
+        cores = {tuple(l.split(",")) for l in out.splitlines() if l and not l.startswith("#")}
+        phys = len(cores) or None
+        for line in subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout.splitlines():
+            if line.startswith("Model name:"):
+                model = line.split(":", 1)[1].strip()
+    except Exception:
+        pass
+    try:
+        usable = len(os.sched_getaffinity(0))
+    except Exception:
+        usable = os.cpu_count()
+    return {"model": model, "physical_cores": phys, "usable_cpus": usable,
+            "omp_num_threads": os.environ.get("OMP_NUM_THREADS")}
+
+
+def cpu_baseline(args, batch):
+    """The oracle learner (deque + random.sample + transitions_to_tensor + 3 forwards + Huber +
+    autograd + Adam + soft update) timed on this host's cores on bounded samples: every
+    combination of {all usable physical cores, 8 threads} x {capacity 1e5, 1e6} (BASELINE.md
+    section 3; deque sampling is O(n)).  `value` is the all-cores run at the GPU run's capacity."""
     sys.path.insert(0, REPO)
     from oracle import ref as O
+    info = cpu_info()
     head = "dueling" if "Dueling" in args.algo else "linear"
     if args.net == "mlp":
         spec = O.mlp_spec(args.obs_dim, args.actions, head)
     else:
         spec = O.hybrid_spec(args.actions, head, micro_chw=(2, 27, 5) if args.net == "hybrid" else (4, 84, 84))
     per = args.algo.startswith("Per")
-    cap = min(args.capacity, 100_000) if per else args.capacity   # Python SumTree fill is ~20 us/row
-    if args.net == "hybrid84":
-        cap = min(cap, 2_000)   # 113 KB rows: a host deque of 1e5 would need 22.6 GB
-    L = O.OracleLearner(spec, args.algo, args.batch, cap, seed=0)
-    obs, act, rew, done, nobs = O.synth_transitions(cap, spec.obs_dim, args.actions, seed=0)
+    caps = sorted({min(args.capacity, 100_000), args.capacity})
     if per:
-        list(L.replay.store_transitions(obs, act, rew, done, nobs))
-    else:
-        L.replay.replay_buffer.extend(zip(obs, act, rew, done, nobs))
-    random.seed(1234)
-    L.py_state = O.py_state_to_array()
-    for _ in range(2):
-        L.train_step()
+        caps = [min(args.capacity, 100_000)]   # the Python SumTree fill is ~20 us per row
+    if args.net == "hybrid84":
+        caps = [2_000]                          # 113 KB rows: a host deque of 1e5 would need 22.6 GB
+    ncap = max(caps)
+    obs, act, rew, done, nobs = O.synth_transitions(ncap, spec.obs_dim, args.actions, seed=0)
+    # "all cores" = the physical cores this process may actually use: the box's CPU share is set
+    # by OMP_NUM_THREADS (its cgroup quota), not by the affinity mask, which spans the machine
+    share = [info["physical_cores"], info["usable_cpus"]]
+    if (info["omp_num_threads"] or "").isdigit():
+        share.append(int(info["omp_num_threads"]))
+    allc = min(x for x in share if x) if any(share) else torch.get_num_threads()
+    threads = sorted({allc, 8}, reverse=True)
+    runs = []
+    saved = torch.get_num_threads()
+    for cap in caps:
+        L = O.OracleLearner(spec, args.algo, batch, cap, seed=0)
+        if per:
+            list(L.replay.store_transitions(obs[:cap], act[:cap], rew[:cap], done[:cap], nobs[:cap]))
+        else:
+            L.replay.replay_buffer.extend(zip(obs[:cap], act[:cap], rew[:cap], done[:cap], nobs[:cap]))
+        for th in threads:
+            torch.set_num_threads(th)
+            random.seed(1234)
+            L.py_state = O.py_state_to_array()
+            for _ in range(2):
+                L.train_step()
+            t0 = time.perf_counter()
+            steps = 0
+            while True:
+                L.train_step()
+                steps += 1
+                el = time.perf_counter() - t0
+                if el >= args.cpu_seconds and steps >= 3:
+                    break
+            runs.append({"threads": th, "capacity": cap, "value": batch * steps / el, "steps": steps,
+                         "seconds": round(el, 2)})
+        del L
+    torch.set_num_threads(saved)
+    main_run = next((r for r in runs if r["threads"] == threads[0] and r["capacity"] == min(args.capacity, ncap)),
+                    runs[0])
+    return {"value": main_run["value"], "unit": "transitions/s", "cores": main_run["threads"], "kind": "port",
+            "sample": f"oracle/ref.py OracleLearner {args.algo} {net_name(args)} batch {batch}, "
+                      f"{'SumTree' if per else 'deque'} of {main_run['capacity']} transitions, {main_run['steps']} "
+                      f"learn+soft-update steps in {main_run['seconds']} s, torch {torch.__version__} CPU, "
+                      f"{main_run['threads']} threads on {info['model']} ({info['physical_cores']} physical cores "
+                      f"on the host, {info['usable_cpus']} usable by this process)",
+            "cpu": info, "runs": runs}
+
+
+# ----------------------------------------------------------------------------------------
+# GPU measurements
+# ----------------------------------------------------------------------------------------
+def set_rngs(eng, per, rank_seed=0):
+    random.seed(1234 + rank_seed)   # the replay sampler continues CPython's MT19937 stream
+    eng.set_rng(C.DQNX_RNG_PY, np.array(random.getstate()[1], dtype=np.uint32))
+    if per:                         # PER draws numpy's legacy global stream (np.random.uniform)
+        np.random.seed(1234)
+        st = np.random.get_state()
+        eng.set_rng(C.DQNX_RNG_NP, np.append(st[1], st[2]).astype(np.uint32))
+
+
+def make_engine(args, spec, batch_global, world, rank, device, local=False):
+    eng = LearnEngine(spec, args.algo, batch_global, args.capacity, world_size=world, rank=rank, device=device,
+                      graphs=not args.no_graphs, local_sampling=local, compute_dtype=args.compute)
+    eng.load_params(init_params(spec, 0))
+    fill_ring(eng, args.capacity, spec.obs_dim, args.actions, device, seed=0)
+    set_rngs(eng, args.algo.startswith("Per"), rank if local else 0)
+    return eng
+
+
+def timed_steps(step, steps, dist, device):
+    """`steps` steps bracketed by barrier + synchronize on both sides; max over ranks (s)."""
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
     t0 = time.perf_counter()
-    steps = 0
-    while True:
-        L.train_step()
-        steps += 1
-        el = time.perf_counter() - t0
-        if el >= args.cpu_seconds and steps >= 3:
-            break
-    return {"value": args.batch * steps / el, "unit": "transitions/s", "cores": torch.get_num_threads(),
-            "kind": "port",
-            "sample": f"oracle/ref.py OracleLearner {args.algo} {net_name(args)} batch {args.batch}, "
-                      f"{'SumTree' if per else 'deque'} of {cap} transitions, {steps} learn+soft-update steps in {el:.1f} s, "
-                      f"torch {torch.__version__} CPU, {torch.get_num_threads()} threads"}
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    if dist:
+        t = torch.tensor([el], device=device, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    return el
+
+
+def run_learner(args, eng, world, backend, steps, warmup, dist, device):
+    """Warm up, then time `steps` learn steps (single GPU: the engine's graph; DP: the whole DP
+    step as one HIP graph over RCCL).  Returns (seconds, dp_graph)."""
+    def step():
+        if world > 1:   # shard compute, RCCL all-reduce (+ PER |delta| all-gather), replicated Adam
+            dp_learn_step(eng, soft_update=True)
+        else:
+            eng.learn_step(soft_update=True, prefetch=args.prefetch)
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize()
+    eng.check_device_error()
+    dp_graph = False
+    if world > 1 and backend == "nccl" and not args.no_dp_graph and not args.no_graphs:
+        # the whole DP step (shard kernels + RCCL all-reduce + Adam) as one replayed graph: the
+        # eager loop is host-bound (3 launches + a collective call per ~50 us step).  RCCL
+        # collectives are capturable; gloo's are host calls and never are.
+        g = GraphedDPStep(eng, soft_update=True)
+        g()   # one untimed replay
+        torch.cuda.synchronize()
+        dp_graph = True
+        step = g
+    el = timed_steps(step, steps, dist, device)
+    if dp_graph:
+        eng.set_graphs(True)   # later kernel timing replays the engine's own graphs
+    eng.check_device_error()
+    return el, dp_graph
+
+
+def kernel_infos(eng, flags):
+    L = C.lib()
+    n = C.I32()
+    C.check(L.dqnx_learn_kernel_count(eng.h, flags, ctypes.byref(n)), "kernel_count")
+    infos = []
+    for i in range(n.value):
+        nm = ctypes.create_string_buffer(64)
+        fl, by = ctypes.c_double(), ctypes.c_double()
+        C.check(L.dqnx_learn_kernel_info(eng.h, flags, i, nm, 64, ctypes.byref(fl), ctypes.byref(by)), "info")
+        infos.append((nm.value.decode(), fl.value, by.value))
+    return infos
+
+
+def kernel_times(eng, flags, count=50, reps=5, only=None):
+    """In-context time per launch of every kernel of a learn step: K graph-launched steps with
+    and without the kernel (dqnx_learn_step_omit), bracketed by HIP events recorded on the
+    engine's own stream; the median of `reps` interleaved pairs.  Returns [(name, us, flops, bytes)]."""
+    L = C.lib()
+    infos = kernel_infos(eng, flags)
+    stream = eng.stream()
+    hs = torch.cuda.current_stream(eng.device)   # the engine launches on this stream: events go there too
+
+    def graph_steps_ms(omit):
+        C.check(L.dqnx_learn_step_omit(eng.h, flags, omit, stream), "omit step")   # capture
+        t0, t1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda.synchronize()
+        t0.record(hs)
+        for _ in range(count):
+            C.check(L.dqnx_learn_step_omit(eng.h, flags, omit, stream), "omit step")
+        t1.record(hs)
+        t1.synchronize()
+        return t0.elapsed_time(t1) / count
+
+    out = []
+    for i, (nm, fl, by) in enumerate(infos):
+        if only is not None and nm not in only:
+            continue
+        d = sorted(graph_steps_ms(-1) - graph_steps_ms(i) for _ in range(reps))
+        out.append((nm, d[len(d) // 2] * 1e3, fl, by))
+    return out
+
+
+def roofline_of(args, kern, batch_tag):
+    """roofline object for the dominant kernel: achieved algorithmic FLOP/s (or B/s) against the
+    MI355X peak of the compute dtype, plus both fractions; `traffic` = HBM bytes per launch
+    from the committed rocprofv3 PMC passes of the same workload (profiles/pmc_traffic_*.json)."""
+    nm, us, fl, by = kern
+    peak_mfma = PEAK_BF16_MFMA_TFLOPS if args.compute == "bf16" else PEAK_FP32_MFMA_TFLOPS
+    traffic = None
+    tag = "" if args.compute == "fp32" else f"_{args.compute}"
+    pmc_path = os.path.join(REPO, "profiles", f"pmc_traffic_{args.net}_b{batch_tag}{tag}.json")
+    if os.path.exists(pmc_path):
+        try:
+            traffic = json.load(open(pmc_path)).get(nm, {}).get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+    sec = us * 1e-6
+    mfma_ach = fl / sec / 1e12 if fl else 0.0
+    hbm_ach = by / sec / 1e9
+    mfma_frac = mfma_ach / peak_mfma
+    hbm_frac = hbm_ach / PEAK_HBM_GBS
+    # the bounding roof by the kernel's intensity, taken over the MEASURED HBM traffic when the
+    # PMC passes exist (algorithmic bytes otherwise), against the dtype's ridge point
+    ridge = peak_mfma * 1e12 / (PEAK_HBM_GBS * 1e9)
+    intensity = fl / (traffic or by) if (traffic or by) else 0.0
+    common = {"traffic": traffic, "kernel": nm, "avg_us": us, "algorithmic_flops": fl, "algorithmic_bytes": by,
+              "mfma_frac": mfma_frac, "hbm_frac": hbm_frac, "intensity_flop_per_byte": intensity,
+              "ridge_flop_per_byte": ridge}
+    if fl > 0 and intensity > ridge:
+        return dict({"bound": "mfma", "achieved": mfma_ach, "peak": peak_mfma, "unit": "TFLOP/s",
+                     "frac": mfma_frac}, **common)
+    return dict({"bound": "hbm", "achieved": hbm_ach, "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": hbm_frac},
+                **common)
+
+
+def single_gpu_extras(args, spec, device):
+    """configs[3] points measured on this one GPU:
+    * configs3_n1: the learn step at the global minibatch 4096 (strong-scaling N = 1 point);
+    * projection_w8: the rank-0 shard step of a world_size = 8 engine (512 rows, the global
+      4096-draw sampler, Adam + soft update) -- every term of the 8-GPU step but the all-reduce."""
+    out = {}
+    Bg = args.global_batch
+    eng = make_engine(args, spec, Bg, 1, 0, device)
+    el, _ = run_learner(args, eng, 1, None, max(args.steps, 50), args.warmup, None, device)
+    ks = kernel_times(eng, C.STEP_SOFT_UPDATE, count=50, reps=3, only={"sample_uniform", "mlp_fwd"})
+    steps = max(args.steps, 50)
+    out["configs3_n1"] = {"value": Bg * steps / el, "ms_per_step": el / steps * 1e3, "batch": Bg,
+                          "kernels": [{"kernel": k[0], "avg_us": k[1]} for k in ks]}
+    del eng
+    torch.cuda.empty_cache()
+    W = 8
+    eng = make_engine(args, spec, Bg, W, 0, device)
+
+    def shard_step():   # what each rank runs around the all-reduce
+        eng.learn_step(grads_only=True)
+        eng.apply_grads(soft_update=True)
+    for _ in range(args.warmup):
+        shard_step()
+    el = timed_steps(shard_step, steps, None, device)
+    ks = kernel_times(eng, C.STEP_GRADS_ONLY, count=50, reps=3)
+    samp = next((k[1] for k in ks if k[0] == "sample_uniform"), None)
+    out["projection_w8"] = {
+        "rows_per_rank": Bg // W, "global_batch": Bg, "shard_step_us": el / steps * 1e6,
+        "global_sampling_us": samp,
+        "tr_per_s_without_allreduce": Bg / (el / steps),
+        "kernels": [{"kernel": k[0], "avg_us": k[1]} for k in ks],
+        "note": "rank 0 of world_size 8 on one GPU: sampler (all 4096 draws) + 512-row shard + grad reduce + "
+                "Adam/soft update (two graph launches); add the RCCL all-reduce of the 428 KB gradient for the "
+                "8-GPU step"}
+    del eng
+    torch.cuda.empty_cache()
+    return out
 
 
 def main():
@@ -225,65 +483,22 @@ def main():
             dist.init_process_group(backend)
 
     spec = make_spec(args)
-    Bg = args.batch * world
     per = args.algo.startswith("Per")
-    # N > 1: plain data parallelism -- every rank draws its own batch_per_gpu positions from its
-    # own MT19937 stream (O(batch_per_gpu) sampling per rank).  --global-sampling instead has
-    # every rank draw the same global minibatch (bit-exact with one GPU; PER always does this).
-    local = world > 1 and not per and not args.global_sampling
-    eng = LearnEngine(spec, args.algo, Bg, args.capacity, world_size=world, rank=rank, device=device,
-                      graphs=not args.no_graphs, local_sampling=local, compute_dtype=args.compute)
-    eng.load_params(init_params(spec, 0))
-    fill_ring(eng, args.capacity, spec.obs_dim, args.actions, device, seed=0)
-    random.seed(1234 + (rank if local else 0))   # the replay sampler continues CPython's MT19937 stream
-    eng.set_rng(C.DQNX_RNG_PY, np.array(random.getstate()[1], dtype=np.uint32))
-    if per:             # PER draws numpy's legacy global stream (np.random.uniform)
-        np.random.seed(1234)
-        st = np.random.get_state()
-        eng.set_rng(C.DQNX_RNG_NP, np.append(st[1], st[2]).astype(np.uint32))
-    Bl = args.batch
-
-    prefetch = args.prefetch
-
-    def step():
-        if world > 1:   # shard compute, RCCL all-reduce (+ PER |delta| all-gather), replicated Adam
-            dp_learn_step(eng, soft_update=True)
-        else:
-            eng.learn_step(soft_update=True, prefetch=prefetch)
-
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
-    eng.check_device_error()
-    dp_graph = False
-    if world > 1 and backend == "nccl" and not args.no_dp_graph and not args.no_graphs:
-        # the whole DP step (shard kernels + RCCL all-reduce + Adam) as one replayed graph: the
-        # eager loop is host-bound (3 launches + a collective call per ~50 us step).  RCCL
-        # collectives are capturable; gloo's are host calls and never are.
-        g = GraphedDPStep(eng, soft_update=True)
-        g()   # one untimed replay
-        torch.cuda.synchronize()
-        dp_graph = True
-
-        def step():
-            g()
-    if dist:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    torch.cuda.synchronize()
-    if dist:
-        dist.barrier()
-    el = time.perf_counter() - t0
-    if dp_graph:
-        eng.set_graphs(True)   # the kernel timing below replays the engine's own graphs
-    if dist:
-        t = torch.tensor([el], device=device, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        el = float(t.item())
-    eng.check_device_error()
+    if world == 1:
+        Bg = args.batch or 1024
+        scaling = "strong"
+    elif args.scaling == "strong":
+        Bg = args.global_batch
+        scaling = "strong"
+    else:
+        Bg = (args.batch or 4096) * world
+        scaling = "weak"
+    if Bg % world:
+        raise SystemExit(f"global batch {Bg} is not a multiple of {world} ranks")
+    Bl = Bg // world
+    local = world > 1 and args.local_sampling and not per
+    eng = make_engine(args, spec, Bg, world, rank, device, local=local)
+    el, dp_graph = run_learner(args, eng, world, backend, args.steps, args.warmup, dist, device)
     loss = eng.loss()
     ms_per_step = el / args.steps * 1e3
     value = Bg * args.steps / el
@@ -293,78 +508,31 @@ def main():
     kernels = []
     if not args.no_kernel_timing:
         flags = C.STEP_GRADS_ONLY if world > 1 else C.STEP_SOFT_UPDATE
-        L = C.lib()
-        n = C.I32()
-        C.check(L.dqnx_learn_kernel_count(eng.h, flags, ctypes.byref(n)), "kernel_count")
-        infos = []
-        for i in range(n.value):
-            nm = ctypes.create_string_buffer(64)
-            fl, by = ctypes.c_double(), ctypes.c_double()
-            C.check(L.dqnx_learn_kernel_info(eng.h, flags, i, nm, 64, ctypes.byref(fl), ctypes.byref(by)), "info")
-            infos.append((nm.value.decode(), fl.value, by.value))
-        # consume a pending prefetched minibatch so the timing steps sample themselves
-        if world > 1:
-            dp_learn_step(eng, soft_update=True)
-        else:
-            eng.learn_step(soft_update=True)
-        K = max(args.steps, 50)
-        stream = eng.stream()
+        ks = kernel_times(eng, flags, count=50, reps=5)
+        dom = max(ks, key=lambda k: k[1])
+        # re-time the dominant kernel with more steps per sample
+        dom = kernel_times(eng, flags, count=max(args.steps, 100), reps=7, only={dom[0]})[0]
+        kernels = [{"kernel": k[0], "avg_us": (dom[1] if k[0] == dom[0] else k[1]), "flops": k[2], "bytes": k[3]}
+                   for k in ks]
+        roofline = roofline_of(args, dom, Bl)
 
-        def graph_steps_ms(omit, count):
-            """`count` graph-launched learn steps with kernel `omit` left out (-1: none),
-            bracketed by HIP events on the engine's stream; ms per step."""
-            C.check(L.dqnx_learn_step_omit(eng.h, flags, omit, stream), "omit step")   # capture
-            t0, t1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            torch.cuda.synchronize()
-            t0.record()
-            for _ in range(count):
-                C.check(L.dqnx_learn_step_omit(eng.h, flags, omit, stream), "omit step")
-            t1.record()
-            t1.synchronize()
-            return t0.elapsed_time(t1) / count
-
-        # a kernel's in-context time per launch = step time with it - step time without it;
-        # full and omitted runs are interleaved and the median of `reps` pairs is kept
-        def kernel_ms(i, count, reps):
-            d = []
-            for _ in range(reps):
-                d.append(graph_steps_ms(-1, count) - graph_steps_ms(i, count))
-            d.sort()
-            return d[len(d) // 2]
-
-        for i, (nm, fl, by) in enumerate(infos):
-            kernels.append({"kernel": nm, "avg_us": kernel_ms(i, 50, 3) * 1e3, "flops": fl, "bytes": by})
-        dom = max(range(len(kernels)), key=lambda i: kernels[i]["avg_us"])
-        avg_ms = kernel_ms(dom, K, 5)
-        kernels[dom]["avg_us"] = avg_ms * 1e3
-        nm, fl, by = infos[dom]
-        intensity = fl / by if by else 0.0
-        peak_mfma = PEAK_BF16_MFMA_TFLOPS if args.compute == "bf16" else PEAK_FP32_MFMA_TFLOPS
-        ridge = peak_mfma * 1e12 / (PEAK_HBM_GBS * 1e9)
-        traffic = None
-        # HBM bytes per launch from rocprofv3 PMC passes of this same workload (tools/pmc_traffic.py)
-        tag = "" if args.compute == "fp32" else f"_{args.compute}"
-        pmc_path = os.path.join(REPO, "profiles", f"pmc_traffic_{args.net}_b{args.batch}{tag}.json")
-        if os.path.exists(pmc_path):
-            try:
-                traffic = json.load(open(pmc_path)).get(nm, {}).get("hbm_bytes_per_launch")
-            except Exception:
-                traffic = None
-        if intensity > ridge and fl > 0:
-            ach = fl / (avg_ms * 1e-3) / 1e12
-            roofline = {"bound": "mfma", "achieved": ach, "peak": peak_mfma, "unit": "TFLOP/s",
-                        "frac": ach / peak_mfma, "traffic": traffic, "kernel": nm,
-                        "avg_us": avg_ms * 1e3, "algorithmic_flops": fl, "algorithmic_bytes": by}
-        else:
-            ach = by / (avg_ms * 1e-3) / 1e9
-            roofline = {"bound": "hbm", "achieved": ach, "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                        "frac": ach / PEAK_HBM_GBS, "traffic": traffic, "kernel": nm,
-                        "avg_us": avg_ms * 1e3, "algorithmic_flops": fl, "algorithmic_bytes": by}
+    extras = {}
+    if not args.no_extras and args.net == "mlp" and not per and args.compute == "fp32":
+        del eng
+        torch.cuda.empty_cache()
+        if world == 1:
+            extras = single_gpu_extras(args, spec, device)
+        elif scaling == "strong":   # the weak-scaling companion line: 4096 rows per rank
+            weng = make_engine(args, spec, 4096 * world, world, rank, device, local=local)
+            wel, _ = run_learner(args, weng, world, backend, args.steps, args.warmup, dist, device)
+            extras["weak"] = {"value": 4096 * world * args.steps / wel, "ms_per_step": wel / args.steps * 1e3,
+                              "batch_per_gpu": 4096, "global_batch": 4096 * world}
+            del weng
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
-            cpu = cpu_baseline(args)
+            cpu = cpu_baseline(args, Bg)
         except Exception as ex:  # the baseline must never hide the GPU number
             log(f"cpu baseline failed: {ex!r}")
 
@@ -378,16 +546,16 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": ms_per_step,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": scaling,
             "vs_baseline": None,
             "dtype": args.compute,
             "data": "synthetic",
             "config": {
-                "workload": WORKLOADS[args.net],
+                "workload": workload_name(args, world),
                 "algo": args.algo, "net": net_name(args),
-                "batch_per_gpu": args.batch, "global_batch": Bg, "replay_capacity": args.capacity,
-                "parallelism": f"dp{world}", "graphs": not args.no_graphs, "prefetch_sampling": prefetch,
-                "sampling": "rank-local" if local else "global",
+                "batch_per_gpu": Bl, "global_batch": Bg, "replay_capacity": args.capacity,
+                "parallelism": f"dp{world}", "graphs": not args.no_graphs, "prefetch_sampling": args.prefetch,
+                "sampling": "rank-local" if local else "global (reference-exact random.sample on every rank)",
                 "dp_step": ("one HIP graph" if dp_graph else "eager") if world > 1 else None,
                 "compute": args.compute,
             },
@@ -396,6 +564,7 @@ def main():
             "loss": loss,
             "kernels": kernels,
         }
+        out.update(extras)
         print(json.dumps(out), flush=True)
     if dist:
         dist.destroy_process_group()

@@ -152,23 +152,17 @@ constexpr int BWD_TILE = 32;   // k_bwd_level dW tile edge (DQNX_BWD_BM = DQNX_B
 // a K of at least 127 (the (4,84,84) variant, B=256: conv 2 605 -> 421 us, conv 3 278 -> 226 us;
 // conv 1, K = 36, was slower on 128-wide tiles, 108 -> 382 us); DQNX_CONV_DW_BIG=0 keeps
 // k_bwd_level's 32x32 role
+// (environment knobs are read when a plan is built, so tests can switch them per engine)
 static bool conv_dw_big(int64_t rows, int K) {
-    static int mode = -1;
-    if (mode < 0) {
-        const char* v = getenv("DQNX_CONV_DW_BIG");
-        mode = v ? atoi(v) : 1;
-    }
+    const char* v = getenv("DQNX_CONV_DW_BIG");
+    const int mode = v ? atoi(v) : 1;
     return mode != 0 && rows >= 65536 && K >= 127;
 }
 
 // DQNX_FWD_BIG=0 keeps every dense forward on the 16x64-tile kernel (A/B measurements)
 static bool fwd_big_mode() {
-    static int mode = -1;
-    if (mode < 0) {
-        const char* v = getenv("DQNX_FWD_BIG");
-        mode = v ? atoi(v) : 1;
-    }
-    return mode != 0;
+    const char* v = getenv("DQNX_FWD_BIG");
+    return v ? atoi(v) != 0 : true;
 }
 
 static inline uint64_t align_up(uint64_t x, uint64_t a) { return (x + a - 1) / a * a; }
@@ -196,8 +190,7 @@ struct dqnx_engine {
     uint64_t total = 0;
     // workspace sub-regions (byte offsets from the arena base)
     uint64_t ws_phys = 0, ws_pool = 0, ws_xobs = 0, ws_head_part = 0, ws_loss_part = 0, ws_stage = 0;
-    uint64_t ws_adam_tab = 0, ws_stamps = 0, ws_dhead = 0, ws_raw = 0, ws_trans = 0, ws_tickets = 0, ws_per_ticket = 0, ws_per_wl = 0, ws_per_wp = 0, ws_per_winit = 0, ws_per_last = 0;
-    int64_t n_tickets = 0;
+    uint64_t ws_adam_tab = 0, ws_stamps = 0, ws_dhead = 0, ws_raw = 0, ws_trans = 0, ws_per_ticket = 0, ws_per_wl = 0, ws_per_wp = 0, ws_per_winit = 0, ws_per_last = 0;
     // fused plan: fragment-blocked weight copies [online fwd | target fwd | online chain] per layer
     uint64_t ws_wblk[2][FUSED_MAX_L] = {{0}}, ws_wblkT[FUSED_MAX_L] = {0};
     std::vector<uint64_t> ws_H, ws_dZ, ws_part;
@@ -295,12 +288,6 @@ int layout(dqnx_engine* e) {
     e->ws_dhead = sub((uint64_t)e->Bl * 16 * 4);
     e->ws_raw = sub((uint64_t)3 * e->Bl * 16 * 4);
     e->ws_trans = sub((uint64_t)e->Bl * 16);
-    {   // dW seam arrival counters: an upper bound on the parameter tiles (16 x 16 tiles)
-        uint64_t t = (uint64_t)((np.NH + 15) / 16) * ((np.F + 1 + 15) / 16);
-        for (int l = 0; l < L; l++) t += (uint64_t)((np.dense[l].out + 15) / 16) * ((np.dense[l].in + 1 + 15) / 16);
-        e->n_tickets = (int64_t)t;
-        e->ws_tickets = sub(t * 4);
-    }
     if (e->bwd_plan == 2) {
         for (int l = 0; l < L; l++) {
             const bool bf = e->fplan.bf16 != 0;
@@ -428,35 +415,6 @@ AdamBias adam_bias_args(dqnx_engine* e) {
     b.beta1d = e->cfg.beta1;
     b.beta2d = e->cfg.beta2;
     return b;
-}
-
-// Optimizer fields shared by AdamArgs and DwSeamArgs (torch Adam defaults of the config).
-template <class T>
-void fill_adam_fields(dqnx_engine* e, int flags, T& aa) {
-    const dqnx_config& c = e->cfg;
-    aa.mode = (flags & DQNX_STEP_GRADS_ONLY) ? 0 : 1;
-    aa.soft = (flags & DQNX_STEP_SOFT_UPDATE) ? 1 : 0;
-    aa.n_params = e->np.P;
-    aa.p = at<float>(e, e->off[DQNX_BUF_PARAMS]);
-    aa.m = at<float>(e, e->off[DQNX_BUF_ADAM_M]);
-    aa.v = at<float>(e, e->off[DQNX_BUF_ADAM_V]);
-    aa.grads = at<float>(e, e->off[DQNX_BUF_GRADS]);
-    aa.target = at<float>(e, e->off[DQNX_BUF_TARGET_PARAMS]);
-    aa.ctrl = ctrl_of(e);
-    aa.w1 = (float)(1.0 - c.beta1);          // Python: exp_avg.lerp_(grad, 1 - beta1)
-    aa.beta2 = (float)c.beta2;
-    aa.c2 = (float)(1.0 - c.beta2);
-    aa.eps = (float)c.adam_eps;
-    aa.tau = (float)(c.tau * c.n_env);      // (tau * n_env) * online + (1 - tau * n_env) * target
-    aa.one_minus_tau = (float)(1.0 - c.tau * c.n_env);
-    aa.adam_table = at<float>(e, e->ws_adam_tab);
-    aa.adam_table_len = kAdamTable;
-    aa.beta1d = c.beta1;
-    aa.beta2d = c.beta2;
-    aa.lrd = c.lr;
-    aa.loss_partial = at<float>(e, e->ws_loss_part);
-    aa.n_loss_partial = e->tiles;
-    aa.batch_global = e->Bg;
 }
 
 // Gradient reduction (fixed-order sum of the split-K slabs) + Adam (+ soft update).
@@ -759,7 +717,6 @@ void build_fused_steps(dqnx_engine* e, int flags, int32_t* idx, int32_t* phys, s
             flops += 2.0 * Bl * np.NH * (np.F + 1.0);
             bytes += 4.0 * (16.0 * Bl + Bl * np.F + ba.dw_slices * (double)np.head_params);
         }
-        const char* sv = getenv("DQNX_DW_SEAM");
         if (e->fplan.bf16) {   // bf16 operands, fp32 slabs: the same Adam pass follows
             dw_bf16_grid(ba);
             KStep k;
@@ -768,10 +725,7 @@ void build_fused_steps(dqnx_engine* e, int flags, int32_t* idx, int32_t* phys, s
             k.bytes = bytes;
             k.run = [=](hipStream_t s) { return launch_dw_bf16(ba, s); };
             ks.push_back(k);
-            ks.push_back(adam_kstep(e, flags));
-            return;
-        }
-        if (!(sv && atoi(sv) == 1)) {   // default: split-K slabs, then the Adam pass
+        } else {                // split-K slabs of every dW, then the Adam pass sums them
             bwd_level_grid(ba);
             KStep k;
             k.name = "dw_all";
@@ -779,35 +733,8 @@ void build_fused_steps(dqnx_engine* e, int flags, int32_t* idx, int32_t* phys, s
             k.bytes = bytes;
             k.run = [=](hipStream_t s) { return launch_bwd_level(ba, act, s); };
             ks.push_back(k);
-            ks.push_back(adam_kstep(e, flags));
-            return;
         }
-        // 5. opt-in (DQNX_DW_SEAM=1): one launch, slabs + last-arriver reduction + Adam.  Measured
-        //    slower (25 us vs 9.6 + 7.4 at MLP-284 B=1024): the agent-scope release / acquire
-        //    write back and invalidate the XCD's L2 once per workgroup.
-        DwSeamArgs da;
-        memset(&da, 0, sizeof(da));
-        da.b = ba;
-        const int ntiles = dw_seam_tiles(da.b);
-        if (ntiles > e->n_tickets) { e->n_tickets = -1; return; }   // cannot happen (16x16 bound)
-        int t0 = 0;
-        for (int p = 0; p < da.b.ndw; p++) {
-            da.tile0[p] = t0;
-            t0 += da.b.dw[p].grid_x * da.b.dw[p].grid_y;
-        }
-        for (int p = 0; p < da.b.ndw; p++) {   // problems were added layer L-1 .. 0, then the head
-            const int l = L - 1 - p;
-            da.poff[p] = (p < L) ? np.dense[l].off : np.head_off;
-        }
-        da.tickets = at<int>(e, e->ws_tickets);
-        fill_adam_fields(e, flags, da);
-        const double P = (double)np.P;
-        KStep k;
-        k.name = da.mode ? "dw_adam" : "dw_grads";
-        k.flops = flops + (da.mode ? 12.0 * P : 0.0);
-        k.bytes = bytes + 4.0 * (ba.dw_slices * P + P + (da.mode ? 6.0 * P + (da.soft ? 2.0 * P : 0.0) : 0.0));
-        k.run = [=](hipStream_t s) { return launch_dw_seam(da, s); };
-        ks.push_back(k);
+        ks.push_back(adam_kstep(e, flags));
     }
 }
 
@@ -1014,7 +941,7 @@ std::vector<KStep> build_learn_steps(dqnx_engine* e, int key) {
         const uint64_t part_floats = (uint64_t)e->slices[l] * ((uint64_t)lp.out * lp.in + lp.out);
         int kchunk = 0;
         const int ksplit = fwd_big_ksplit(e->Bl, lp.out, lp.in, np_, (int64_t)part_floats, &kchunk);
-        static const int big_min_k = getenv("DQNX_FWD_BIG_MINK") ? atoi(getenv("DQNX_FWD_BIG_MINK")) : 8192;
+        const int big_min_k = getenv("DQNX_FWD_BIG_MINK") ? atoi(getenv("DQNX_FWD_BIG_MINK")) : 8192;
         if ((l > 0 || NC) && lp.in >= big_min_k && e->Bl >= 64 && fwd_big_mode() &&
             (uint64_t)ksplit * np_ * e->Bl * lp.out <= part_floats) {
             fa.ksplit = ksplit;
@@ -1213,7 +1140,8 @@ std::vector<KStep> build_learn_steps(dqnx_engine* e, int key) {
             k.flops = 2.0 * M * cp.Co * (cp.K + 1.0) + (l > 0 ? 2.0 * M * cp.Co * (double)cp.K : 0.0);
             k.bytes = 4.0 * ((double)M * (cp.Co + cp.Kstride) + ba.dw_slices * (double)d.pstride
                              + (l > 0 ? (double)M * cp.K + cp.Co * (double)cp.K : 0.0));
-            if (conv_dw_big(M, cp.K)) {   // dx role (if any) runs as conv_dx_c* or stays in a level launch
+            const bool dw_big = conv_dw_big(M, cp.K);
+            if (dw_big) {   // dx role (if any) runs as conv_dx_c* or stays in a level launch
                 BwdArgs bw = ba;
                 if (ba.dZprev) {    // small dx: keep it in its own level launch without the dW role
                     BwdArgs bl = ba;
@@ -1221,6 +1149,8 @@ std::vector<KStep> build_learn_steps(dqnx_engine* e, int key) {
                     bwd_level_grid(bl);
                     KStep kl;
                     kl.name = "conv_dxs_c" + std::to_string(l + 1);
+                    kl.flops = 2.0 * M * cp.Co * (double)cp.K;
+                    kl.bytes = 4.0 * ((double)M * cp.K + (double)M * cp.Co + cp.Co * (double)cp.K);
                     kl.run = [=](hipStream_t s) { return launch_bwd_level(bl, act, s); };
                     ks.push_back(kl);
                 }
@@ -1228,7 +1158,7 @@ std::vector<KStep> build_learn_steps(dqnx_engine* e, int key) {
             } else {
                 k.run = [=](hipStream_t s) { return launch_bwd_level(ba, act, s); };
             }
-            if (dx_big) {
+            if (dx_big || dw_big) {   // the conv_bwd launch is the dW GEMM alone
                 k.flops = 2.0 * M * cp.Co * (cp.K + 1.0);
                 k.bytes = 4.0 * ((double)M * (cp.Co + cp.Kstride) + ba.dw_slices * (double)d.pstride);
             }

@@ -741,171 +741,6 @@ __global__ void k_replay_push(PushArgs a) {
 
 
 // =====================================================================================
-// dW of every layer + Adam in one launch (fused plan).  Each (parameter tile, K slice)
-// workgroup writes its split-K slab as in k_bwd_level; the LAST slice to arrive at the tile
-// (agent-scope release / ticket / acquire, cdna guide "Projection GEMM at M = 256" item 2)
-// sums the tile's slabs in fixed slice order -- the same order as k_adam, so results are
-// deterministic and identical to the two-launch form -- and applies torch's single-tensor
-// Adam and the soft update to the tile.  The tile's optimizer state is fetched into
-// registers before the GEMM by every slice (only the reducer uses it).
-// =====================================================================================
-__device__ __forceinline__ int64_t dw_local_index(const DwProblem& d, int row, int col) {
-    if (d.head_kind < 0) return (col < d.in) ? (int64_t)row * d.in + col : (int64_t)d.out * d.in + row;
-    return (col < d.in) ? head_w_off(d.head_kind, row, d.in) + col : head_b_off(d.head_kind, row, d.in, d.A);
-}
-
-__global__ __launch_bounds__(256) void k_dw_seam(DwSeamArgs a) {
-    using EW = Engine<BWD_BM, BWD_BN, DQNX_BWD_KT, DQNX_BWD_WM, L_K_ROWS, L_K_ROWS, true, true>;
-    constexpr int TM = EW::TM, TN = EW::TN;
-    constexpr int TE = BWD_BM * BWD_BN / 256;   // tile elements per thread in the reducer
-    __shared__ __attribute__((aligned(16))) float lds[EW::LDS_FLOATS];
-    __shared__ int s_last;
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int i = lane & 15, g = lane >> 4;
-    const BwdArgs& ba = a.b;
-
-    if (blockIdx.x == 0 && tid < 64 && a.loss_partial) {   // loss = sum of the head tiles' partials / B
-        float sacc = 0.f;
-        for (int j = tid; j < a.n_loss_partial; j += 64) sacc += a.loss_partial[j];
-#pragma unroll
-        for (int o = 32; o >= 1; o >>= 1) sacc += __shfl_xor(sacc, o);
-        if (tid == 0) {
-            const float loss = sacc / (float)a.batch_global;
-            a.grads[a.n_params] = loss;   // all-reduced with the gradient under DP
-            a.ctrl->loss = loss;
-        }
-    }
-
-    int b = blockIdx.x, p = 0;
-    while (p + 1 < ba.ndw && b >= ba.dw[p].blocks) { b -= ba.dw[p].blocks; p++; }
-    const DwProblem& d = ba.dw[p];
-    b = xcd_remap(b, d.blocks);
-    const int bx = b % d.grid_x;
-    const int t2 = b / d.grid_x;
-    const int by = t2 % d.grid_y, bz = t2 / d.grid_y;
-    const int m0 = by * BWD_BM, n0 = bx * BWD_BN;
-    const int tile = a.tile0[p] + by * d.grid_x + bx;
-
-    // the reducer's operands, fetched before the GEMM (every slice; one of them reduces)
-    int64_t eo[TE];
-    float pm[TE], mm[TE], vm[TE], tm_[TE];
-#pragma unroll
-    for (int u = 0; u < TE; u++) {
-        const int q = tid + 256 * u, row = m0 + q / BWD_BN, col = n0 + q % BWD_BN;
-        const bool ok = row < d.out && col <= d.in;
-        eo[u] = ok ? dw_local_index(d, row, col) : -1;
-        const int64_t e = a.poff[p] + (ok ? eo[u] : 0);
-        pm[u] = a.mode ? a.p[e] : 0.f;
-        mm[u] = a.mode ? a.m[e] : 0.f;
-        vm[u] = a.mode ? a.v[e] : 0.f;
-        tm_[u] = (a.mode && a.soft) ? a.target[e] : 0.f;
-    }
-
-    const int kb = bz * ba.kslice;
-    const int ke = min(ba.Bl, kb + ba.kslice);
-    Operand A{d.dZ, d.ldz, nullptr, d.out, ba.Bl, -1, nullptr, 0};
-    Operand B{d.X, d.ldx, nullptr, d.in, ba.Bl, d.in, nullptr, 0};
-    floatx4 acc[TM][TN];
-    EW::G::run(lds, A, B, m0, n0, kb, ke, acc);
-    // publish the slab (agent-scope release), take a ticket; the last slice acquires and
-    // reduces.  (A write-through sc1 variant without the fences faulted under hipGraph
-    // replay and was removed; this form is correct but slower than dW + k_adam, so the plan
-    // uses it only with DQNX_DW_SEAM=1.)
-    float* part = d.partial + (int64_t)bz * d.pstride;
-    if (EW::owner()) {
-#pragma unroll
-        for (int tn = 0; tn < TN; tn++) {
-            const int col = n0 + EW::co() + tn * 16 + i;
-            if (col > d.in) continue;
-#pragma unroll
-            for (int tmi = 0; tmi < TM; tmi++)
-#pragma unroll
-                for (int r = 0; r < 4; r++) {
-                    const int row = m0 + EW::ro() + tmi * 16 + 4 * g + r;
-                    if (row < d.out) part[dw_local_index(d, row, col)] = acc[tmi][tn][r];
-                }
-        }
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (tid == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        const int t = __hip_atomic_fetch_add(&a.tickets[tile], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const int last = (t == ba.dw_slices - 1);
-        if (last) {
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            a.tickets[tile] = 0;   // ready for the next launch
-        }
-        s_last = last;
-    }
-    __syncthreads();
-    if (!s_last) return;
-
-    float step_size = 0.f, bc2s = 1.f;
-    if (a.mode) {
-        const int64_t t = a.ctrl->adam_step;
-        if (t >= 1 && t <= a.adam_table_len) {
-            step_size = a.adam_table[2 * (t - 1)];
-            bc2s = a.adam_table[2 * (t - 1) + 1];
-        } else {
-            step_size = (float)(-(a.lrd / (1.0 - pow(a.beta1d, (double)t))));
-            bc2s = (float)pow(1.0 - pow(a.beta2d, (double)t), 0.5);
-        }
-    }
-    const int S = ba.dw_slices;
-    float gs[TE];
-#pragma unroll
-    for (int u = 0; u < TE; u++) {   // every slab load issued before the first add
-        const int64_t eb = eo[u] >= 0 ? eo[u] : 0;
-        float pv[8];
-#pragma unroll
-        for (int s2 = 0; s2 < 8; s2++) pv[s2] = (s2 < S) ? d.partial[(int64_t)s2 * d.pstride + eb] : 0.f;
-        float gsum = pv[0];
-#pragma unroll
-        for (int s2 = 1; s2 < 8; s2++)
-            if (s2 < S) gsum += pv[s2];
-        for (int s2 = 8; s2 < S; s2++) gsum += d.partial[(int64_t)s2 * d.pstride + eb];
-        gs[u] = gsum;
-    }
-#pragma unroll
-    for (int u = 0; u < TE; u++) {
-        if (eo[u] < 0) continue;
-        const int64_t e = a.poff[p] + eo[u];
-        const float gsum = gs[u];
-        a.grads[e] = gsum;
-        if (!a.mode) continue;
-        // torch _single_tensor_adam (op-by-op mapping: k_adam)
-        float m = fmaf(a.w1, gsum - mm[u], mm[u]);
-        float v = vm[u] * a.beta2;
-        v = v + (a.c2 * gsum) * gsum;
-        const float denom = sqrtf(v) / bc2s + a.eps;
-        const float pv = pm[u] + (step_size * m) / denom;
-        a.m[e] = m;
-        a.v[e] = v;
-        a.p[e] = pv;
-        if (a.soft) a.target[e] = a.tau * pv + a.one_minus_tau * tm_[u];
-    }
-}
-
-int dw_seam_tiles(BwdArgs& b) {
-    bwd_level_grid(b);
-    int t = 0;
-    for (int p = 0; p < b.ndw; p++) t += b.dw[p].grid_x * b.dw[p].grid_y;
-    return t;
-}
-
-int launch_dw_seam(const DwSeamArgs& a, hipStream_t s) {
-    if (a.b.dw_slices > 64) return set_error(DQNX_EUNSUPPORTED, "dw seam: %d slices", a.b.dw_slices);
-    int blocks = 0;
-    for (int p = 0; p < a.b.ndw; p++) blocks += a.b.dw[p].blocks;
-    hipLaunchKernelGGL(k_dw_seam, dim3(blocks), dim3(256), 0, s, a);
-    DQNX_HIP_CHECK(hipGetLastError());
-    return DQNX_OK;
-}
-
-// =====================================================================================
 // host-side launchers
 // =====================================================================================
 template <int ACT, bool VECB>

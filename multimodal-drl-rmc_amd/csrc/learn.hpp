@@ -361,33 +361,6 @@ struct HeadBwdArgs {
     AdamBias ab;
     int64_t* stamps;             // diagnostic builds (-DDQNX_STAMPS): slots 40..55
 };
-// Every weight gradient (split-K over the minibatch) + gradient reduction + Adam (+ soft
-// update) in ONE launch: the last-arriving K slice of each parameter tile sums the tile's
-// slabs in fixed slice order and applies the optimizer to it (k_dw_seam, learn.hip).
-struct DwSeamArgs {
-    BwdArgs b;                 // dW problems (dx role unused), Bl, kslice, dw_slices
-    int64_t poff[4];           // flat parameter offset of each problem's layer / head
-    int tile0[4];              // first ticket of each problem
-    int* tickets;              // one arrival counter per parameter tile, zero between launches
-    int mode;                  // 0: grads only (DP all-reduce follows), 1: grads + Adam
-    int soft;
-    int64_t n_params;
-    float* p;
-    float* m;
-    float* v;
-    float* grads;              // [n_params + 1] (last = loss)
-    float* target;
-    dqnx_ctrl* ctrl;
-    float w1, beta2, c2, eps, tau, one_minus_tau;
-    const float* loss_partial;
-    int n_loss_partial;
-    int batch_global;
-    const float* adam_table;
-    int adam_table_len;
-    double beta1d, beta2d, lrd;
-};
-int dw_seam_tiles(BwdArgs& b);   // fills the grids; returns the number of parameter tiles
-int launch_dw_seam(const DwSeamArgs& a, hipStream_t s);
 bool fused_fwd_plan(FusedFwdArgs& a, int obs_dim, bool bf16, int mr);   // fills sx/sh/buf/kpad; false if unsupported
 int fused_wblk_bytes(bool bf16, int rows, int kpad);          // one blocked weight copy
 int launch_fused_fwd(const FusedFwdArgs& a, int act, hipStream_t s);

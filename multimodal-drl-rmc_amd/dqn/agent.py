@@ -58,6 +58,23 @@ def _obs_dim(input_dim) -> int:
     return int(input_dim)
 
 
+def _check_optim_loss(network):
+    """The engine implements torch.optim.Adam (default betas / eps, no weight decay, no amsgrad)
+    and nn.SmoothL1Loss (beta 1).  network_config may name others (R:env/custom_env/macro with
+    lane/dqn_config.py:96, 101 lists RMSprop and MSELoss): refuse them instead of silently
+    training with a different update rule."""
+    opt, loss = network.optimizer, network.loss
+    if type(opt) is not T.optim.Adam:
+        raise NotImplementedError(f"libdqnx trains with torch.optim.Adam only, got {type(opt).__name__}")
+    g = opt.param_groups[0]
+    if (tuple(g["betas"]) != (0.9, 0.999) or g["eps"] != 1e-8 or g["weight_decay"] != 0 or g["amsgrad"]
+            or g.get("maximize", False)):
+        raise NotImplementedError("libdqnx implements Adam with its defaults (betas (0.9, 0.999), eps 1e-8, "
+                                  "weight_decay 0, amsgrad off)")
+    if type(loss) is not T.nn.SmoothL1Loss or getattr(loss, "beta", 1.0) != 1.0:
+        raise NotImplementedError(f"libdqnx trains with nn.SmoothL1Loss(beta=1) only, got {loss!r}")
+
+
 class Agent:
     """R:dqn/agent.py:18-147."""
 
@@ -112,6 +129,7 @@ class Agent:
                                   reduction=self._reduction)
         self.target_network = cls(self.device, self.lr, self.nn_conf_func, self.input_dim, self.output_dim,
                                   reduction=self._reduction)
+        _check_optim_loss(self.online_network)
         spec = spec_from_body(self.online_network.net, _obs_dim(self.input_dim), self.output_dim,
                               dueling=cls is DuelingDeepQNetwork)
         self.engine = LearnEngine(spec, type(self).__name__, self.batch_size, self.buffer_size, gamma=self.gamma,
@@ -122,7 +140,8 @@ class Agent:
         self.target_network.bind_flat(self.engine.param_views(self.engine.target_params), self.engine.target_params,
                                       spec)
         self.replay_memory_buffer = self._make_replay()
-        self._engine_step = 0          # agent.step * n_env the engine will use next (PER)
+        self._learn_steps = 0          # learn() calls since the last log (throughput metric)
+        self._learn_t0 = time.time()
         self.update_target_network(force=True)
 
     def _make_replay(self):
@@ -166,6 +185,19 @@ class Agent:
         e.set_py_state_from_global()
         e.learn_step(soft_update=False)
         e.get_py_state_to_global()       # synchronises the stream
+        self._count_learn()
+
+    def _count_learn(self):
+        self._learn_steps += 1
+
+    def learn_throughput(self):
+        """Sampled transitions per second through learn() since the last call (the metric
+        SURVEY.md §5 adds at log cadence; host clock, no extra device sync)."""
+        now = time.time()
+        dt = now - self._learn_t0
+        rate = self._learn_steps * self.batch_size / dt if dt > 0 else 0.0
+        self._learn_steps, self._learn_t0 = 0, now
+        return rate
 
     def update_target_network(self, force=False):
         """R:dqn/agent.py:101-110."""
@@ -210,6 +242,8 @@ class Agent:
             self.summary_writer.add_scalar('AvgEpLen', len_mean, global_step=self.step * self.n_env)
             self.summary_writer.add_scalar('Episodes', self.episode_count, global_step=self.step * self.n_env)
             self.summary_writer.add_scalar('Loss', self.engine.loss(), global_step=self.step * self.n_env)
+            self.summary_writer.add_scalar('LearnTransitionsPerSec', self.learn_throughput(),
+                                           global_step=self.step * self.n_env)
 
     def info_mean(self, i):
         i_mean = np.mean([e[i] for e in self.ep_info_buffer])
@@ -235,12 +269,12 @@ class PerDoubleAgent(Agent):
     def learn(self):
         e = self.engine
         step = self.step * self.n_env                      # R:dqn/agent.py:247
-        if step != self._engine_step:
+        if step != e.agent_step:                          # any other sampler call moved it too
             e.set_agent_step(step)
         e.set_np_state_from_global()
         e.learn_step(soft_update=False)                   # advances the engine's step by n_env
         e.get_np_state_to_global()
-        self._engine_step = step + self.n_env
+        self._count_learn()
 
 
 class DQNAgent(SimpleAgent):

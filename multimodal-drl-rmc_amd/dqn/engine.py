@@ -113,20 +113,46 @@ def spec_from_body(net: nn.Module, obs_dim: int, n_actions: int, dueling: bool) 
         return NetSpec(kind=C.DQNX_NET_MLP, head=head, activation=act, obs_dim=obs_dim, n_actions=n_actions,
                        dense=tuple(dense))
     if hasattr(net, "cnn_stream") and hasattr(net, "dense_stream") and hasattr(net, "micro_shape"):
+        # TwoStreamHybridNetwork (R:env/dqn_config.py:66-143): [Conv2d, act]* then [Linear, act]*;
+        # the engine plans exactly that layer sequence, so refuse anything it would plan differently
         conv = []
         mods = list(net.cnn_stream)
+        c, h, w = (int(x) for x in net.micro_shape)
+        macro_len = int(net.macro_len)
+        if len(mods) % 2 or not mods:
+            raise NotImplementedError("libdqnx: cnn_stream must alternate Conv2d and activation")
         for i in range(0, len(mods), 2):
             cv = mods[i]
-            if not isinstance(cv, nn.Conv2d) or cv.padding != (cv.kernel_size[0] // 2, cv.kernel_size[1] // 2):
+            ok = (isinstance(cv, nn.Conv2d) and cv.in_channels == c and cv.bias is not None
+                  and cv.padding == (cv.kernel_size[0] // 2, cv.kernel_size[1] // 2)
+                  and tuple(cv.dilation) == (1, 1) and cv.groups == 1 and cv.padding_mode == "zeros")
+            if not ok:
                 raise NotImplementedError(f"libdqnx: unsupported conv {cv!r}")
-            conv.append((cv.out_channels, tuple(cv.kernel_size), tuple(cv.stride)))
-        dense = [m.out_features for m in net.dense_stream if isinstance(m, nn.Linear)]
-        acts = [m for m in list(net.cnn_stream) + list(net.dense_stream) if not isinstance(m, (nn.Linear, nn.Conv2d))]
+            (kh, kw), (sh, sw) = tuple(cv.kernel_size), tuple(cv.stride)
+            h = (h + 2 * (kh // 2) - kh) // sh + 1
+            w = (w + 2 * (kw // 2) - kw) // sw + 1
+            c = cv.out_channels
+            conv.append((cv.out_channels, (kh, kw), (sh, sw)))
+        dmods = list(net.dense_stream)
+        if len(dmods) % 2 or not dmods:
+            raise NotImplementedError("libdqnx: dense_stream must alternate Linear and activation")
+        dense = []
+        d = c * h * w + macro_len      # flatten(conv) ++ macro (R:env/dqn_config.py:135-138)
+        for i in range(0, len(dmods), 2):
+            lin = dmods[i]
+            if not isinstance(lin, nn.Linear) or lin.in_features != d or lin.bias is None:
+                raise NotImplementedError(f"libdqnx: unsupported dense layer {lin!r} (expects in_features {d})")
+            dense.append(lin.out_features)
+            d = lin.out_features
+        acts = mods[1::2] + dmods[1::2]
         if not all(isinstance(a, nn.ELU) and a.alpha == 1.0 for a in acts):
             raise NotImplementedError("libdqnx: two-stream net must use ELU(alpha=1)")
+        cm, hm, wm = (int(x) for x in net.micro_shape)
+        if obs_dim != macro_len + cm * hm * wm:
+            raise NotImplementedError(f"libdqnx: obs_dim {obs_dim} != macro_len + prod(micro_shape)")
         return NetSpec(kind=C.DQNX_NET_TWO_STREAM, head=head, activation=C.DQNX_ACT_ELU, obs_dim=obs_dim,
-                       n_actions=n_actions, dense=tuple(dense), macro_len=int(net.macro_len),
-                       micro_chw=tuple(int(x) for x in net.micro_shape), conv=tuple(conv))
+                       n_actions=n_actions, dense=tuple(dense), macro_len=macro_len,
+                       micro_chw=(cm, hm, wm), conv=tuple(conv))
     raise NotImplementedError(f"libdqnx: unsupported Q-network body {type(net).__name__}")
 
 
@@ -233,6 +259,7 @@ class LearnEngine:
         self.per_abs_td = self.view(C.BUF_PER_ABS_TD, torch.float32)  # [batch] (PER), else empty
         self.ring_size = 0
         self.ring_wptr = 0
+        self.agent_step = 0      # host mirror of dqnx_ctrl.agent_step (PER beta schedule)
 
     # ---- plumbing ------------------------------------------------------------------
     def buffer(self, which) -> Tuple[int, int]:
@@ -260,6 +287,7 @@ class LearnEngine:
         C.check(self.L.dqnx_engine_reset(self.h, self.stream()), "reset")
         self.ring_size = 0
         self.ring_wptr = 0
+        self.agent_step = 0
 
     def param_views(self, flat: torch.Tensor):
         """name -> view into a flat parameter vector, in state_dict order."""
@@ -322,6 +350,8 @@ class LearnEngine:
         flags = (C.STEP_SOFT_UPDATE if soft_update else 0) | (C.STEP_GIVEN_INDICES if given_indices else 0) \
             | (C.STEP_GRADS_ONLY if grads_only else 0) | (C.STEP_PREFETCH if prefetch else 0)
         C.check(self.L.dqnx_learn_step(self.h, flags, self.stream()), "learn_step")
+        if self.cfg.algo == C.DQNX_ALGO_PER_DOUBLE:   # every PER learn step samples: step += n_env
+            self.agent_step += self.cfg.n_env
 
     def apply_grads(self, soft_update=False):
         C.check(self.L.dqnx_apply_grads(self.h, C.STEP_SOFT_UPDATE if soft_update else 0, self.stream()),
@@ -337,6 +367,7 @@ class LearnEngine:
     def per_sample(self):
         """ReplayMemoryPrioritized.sample_transitions: slots -> batch_idx, IS weights -> is_weights."""
         C.check(self.L.dqnx_per_sample(self.h, self.stream()), "per_sample")
+        self.agent_step += self.cfg.n_env
 
     def per_update_priorities(self, slots: torch.Tensor, abs_td: torch.Tensor):
         """update_batch_priorities(tree_indices, abs_td_errors) for device int32 ring slots
@@ -368,6 +399,7 @@ class LearnEngine:
 
     def set_agent_step(self, step_times_n_env: int):
         C.check(self.L.dqnx_set_agent_step(self.h, int(step_times_n_env), self.stream()), "set_agent_step")
+        self.agent_step = int(step_times_n_env)
 
     def ctrl(self) -> C.Ctrl:
         """Snapshot of the device control block (synchronises)."""

@@ -28,3 +28,18 @@ def gpu_available():
         return torch.cuda.is_available()
     except Exception:
         return False
+
+
+def pytest_sessionfinish(session, exitstatus):
+    """Put the parity exemption counts (tests/parity.py) on record."""
+    try:
+        import json
+        from parity import EXEMPTIONS
+    except Exception:
+        return
+    if not EXEMPTIONS:
+        return
+    out = os.path.join(REPO, "gpurun_out")
+    os.makedirs(out, exist_ok=True)
+    with open(os.path.join(out, "parity_exemptions.json"), "w") as f:
+        json.dump(EXEMPTIONS, f, indent=1)

@@ -15,16 +15,26 @@ from dqn.data_parallel import dp_learn_step  # noqa: E402
 from oracle import ref as O  # noqa: E402  (test data + initial weights only)
 
 
+# workload of the DP tests: (obs_dim, global batch, capacity, fill, seed) per name
+CASES = {
+    "small": (284, 64, 1000, 700, 9),
+    "c3": (284, 4096, 60000, 60000, 29),      # configs[3]: global minibatch 4096
+}
+
+
 def main():
+    """argv: rank world algo out_dir [sampling=global|local] [case=small|c3] [compute=fp32|bf16]"""
     rank, world, algo, out = int(sys.argv[1]), int(sys.argv[2]), sys.argv[3], sys.argv[4]
     local = len(sys.argv) > 5 and sys.argv[5] == "local"
+    case = sys.argv[6] if len(sys.argv) > 6 else "small"
+    compute = sys.argv[7] if len(sys.argv) > 7 else "fp32"
     backend = os.environ.get("DQNX_TEST_BACKEND", "gloo")
     torch.cuda.set_device(0)
     dist.init_process_group(backend, rank=rank, world_size=world)
-    obs_dim, batch, cap, fill, seed = 284, 64, 1000, 700, 9
+    obs_dim, batch, cap, fill, seed = CASES[case]
     head = O.algo_spec_head(algo)
     eng = E.LearnEngine(E.mlp_spec(obs_dim, 8, head), algo, batch, cap, world_size=world, rank=rank,
-                        local_sampling=local)
+                        local_sampling=local, compute_dtype=compute)
     eng.load_params(O.reference_init(O.mlp_spec(obs_dim, 8, head), seed))
     eng.push(*O.synth_transitions(fill, obs_dim, 8, seed=seed + 100))
     eng.set_rng(0, O.py_state_to_array(__import__("random").Random(seed + (rank if local else 0)).getstate()))

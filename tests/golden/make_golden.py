@@ -292,20 +292,47 @@ def gen_sumtree(sumtree_mod):
 
 
 def main():
+    """python make_golden.py [name ...]: regenerate every fixture, or only the named groups
+    (sampler, np_uniform, sumtree, mlp14, mlp284, hybrid284, mlp284b1024, mlp284b4096, mlp284b8192)."""
+    only = set(sys.argv[1:])
+
+    def want(name):
+        return not only or name in only
     agent_mod, replay_mod, sumtree_mod, cfg, mlp_cfg = load_reference()
     torch.set_num_threads(1)
-    gen_sampler(replay_mod)
-    gen_np_uniform()
-    gen_sumtree(sumtree_mod)
+    if want("sampler"):
+        gen_sampler(replay_mod)
+    if want("np_uniform"):
+        gen_np_uniform()
+    if want("sumtree"):
+        gen_sumtree(sumtree_mod)
     all_algos = ["DQNAgent", "DoubleDQNAgent", "DuelingDoubleDQNAgent", "PerDuelingDoubleDQNAgent"]
-    gen_learn(agent_mod, mlp_cfg.network_config, "mlp14", lambda h: O.mlp_spec(14, 8, h), 14,
-              batch=32, buffer=500, n_fill=300, steps=3, seed=3, algos=all_algos)
-    gen_learn(agent_mod, mlp_cfg.network_config, "mlp284", lambda h: O.mlp_spec(284, 8, h), 284,
-              batch=256, buffer=5000, n_fill=3000, steps=2, seed=5,
-              algos=["DuelingDoubleDQNAgent", "PerDuelingDoubleDQNAgent"])
-    gen_learn(agent_mod, cfg.network_config, "hybrid284", lambda h: O.hybrid_spec(8, h), 284,
-              batch=64, buffer=1000, n_fill=600, steps=2, seed=9,
-              algos=["DuelingDoubleDQNAgent"], full_weights=False, stride=37)
+    mlp284 = lambda h: O.mlp_spec(284, 8, h)   # noqa: E731
+    if want("mlp14"):
+        gen_learn(agent_mod, mlp_cfg.network_config, "mlp14", lambda h: O.mlp_spec(14, 8, h), 14,
+                  batch=32, buffer=500, n_fill=300, steps=3, seed=3, algos=all_algos)
+    if want("mlp284"):
+        gen_learn(agent_mod, mlp_cfg.network_config, "mlp284", mlp284, 284,
+                  batch=256, buffer=5000, n_fill=3000, steps=2, seed=5,
+                  algos=["DuelingDoubleDQNAgent", "PerDuelingDoubleDQNAgent"])
+    if want("hybrid284"):
+        gen_learn(agent_mod, cfg.network_config, "hybrid284", lambda h: O.hybrid_spec(8, h), 284,
+                  batch=64, buffer=1000, n_fill=600, steps=2, seed=9,
+                  algos=["DuelingDoubleDQNAgent"], full_weights=False, stride=37)
+    # the bench batch (configs[1]) and the north-star batch (configs[3]'s global minibatch),
+    # and configs[4]'s PER batch (fp32 reference arithmetic); weights strided to keep them small
+    if want("mlp284b1024"):
+        gen_learn(agent_mod, mlp_cfg.network_config, "mlp284b1024", mlp284, 284,
+                  batch=1024, buffer=20000, n_fill=20000, steps=2, seed=21,
+                  algos=["DuelingDoubleDQNAgent"], full_weights=False, stride=5)
+    if want("mlp284b4096"):
+        gen_learn(agent_mod, mlp_cfg.network_config, "mlp284b4096", mlp284, 284,
+                  batch=4096, buffer=60000, n_fill=60000, steps=2, seed=22,
+                  algos=["DuelingDoubleDQNAgent"], full_weights=False, stride=5)
+    if want("mlp284b8192"):
+        gen_learn(agent_mod, mlp_cfg.network_config, "mlp284b8192", mlp284, 284,
+                  batch=8192, buffer=40000, n_fill=40000, steps=2, seed=23,
+                  algos=["PerDuelingDoubleDQNAgent"], full_weights=False, stride=5)
 
 
 if __name__ == "__main__":

@@ -17,3 +17,16 @@ def assert_grad_close(got, ref, what=""):
     d = np.abs(got - ref)
     bad = d > tol
     assert not bad.any(), (what, int(bad.sum()), float(d.max()), scale)
+
+
+# Weight entries that used compare_state's 2 lr exemption (tests/test_gpu_engine.py), per test
+# and tensor; conftest.py writes them to gpurun_out/parity_exemptions.json at session end so the
+# count is on record for every run.
+EXEMPTIONS = []
+
+
+def record_exemptions(counts, numels):
+    import os
+    test = os.environ.get("PYTEST_CURRENT_TEST", "?").split(" ")[0]
+    for k, n in counts.items():
+        EXEMPTIONS.append({"test": test, "tensor": k, "entries": int(n), "numel": int(numels[k])})

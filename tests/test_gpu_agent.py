@@ -10,22 +10,27 @@ import torch
 
 from dqn import Agents
 from oracle import ref as O
-from refnets import agent_kwargs
+from refnets import agent_kwargs, hybrid_network_config, mse_network_config, rmsprop_network_config
 
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("algo,obs_dim,batch,buffer,n_fill", [
-    ("DQNAgent", 14, 32, 500, 300),
-    ("DuelingDoubleDQNAgent", 284, 64, 1000, 700),
-    ("PerDuelingDoubleDQNAgent", 284, 64, 1000, 700),
+@pytest.mark.parametrize("algo,obs_dim,batch,buffer,n_fill,net", [
+    ("DQNAgent", 14, 32, 500, 300, "mlp"),
+    ("DuelingDoubleDQNAgent", 284, 64, 1000, 700, "mlp"),
+    ("PerDuelingDoubleDQNAgent", 284, 64, 1000, 700, "mlp"),
+    # the reference's HEAD configuration: DuelingDoubleDQNAgent on env/dqn_config.network_config
+    # (TwoStreamHybridNetwork), as bin/train.sh launches it (R:train.py:24, R:bin/train.sh:5)
+    ("DuelingDoubleDQNAgent", 284, 64, 1000, 700, "hybrid"),
+    ("PerDuelingDoubleDQNAgent", 284, 32, 500, 300, "hybrid"),
 ])
-def test_gpu_agent_train_loop_matches_oracle(tmp_path, algo, obs_dim, batch, buffer, n_fill):
+def test_gpu_agent_train_loop_matches_oracle(tmp_path, algo, obs_dim, batch, buffer, n_fill, net):
     seed = 17
     torch.manual_seed(seed)
-    agent = getattr(Agents, algo)(**agent_kwargs(algo, obs_dim, batch, buffer, tmp_path))
+    over = {"nn_conf_func": hybrid_network_config} if net == "hybrid" else {}
+    agent = getattr(Agents, algo)(**agent_kwargs(algo, obs_dim, batch, buffer, tmp_path, **over))
     head = O.algo_spec_head(algo)
-    spec = O.mlp_spec(obs_dim, 8, head)
+    spec = O.hybrid_spec(8, head) if net == "hybrid" else O.mlp_spec(obs_dim, 8, head)
     init = O.reference_init(spec, seed)
     for k, v in agent.online_network.state_dict().items():
         assert torch.equal(v.cpu(), init[k]), k
@@ -77,3 +82,48 @@ def test_gpu_agent_train_loop_matches_oracle(tmp_path, algo, obs_dim, batch, buf
     for k in init:
         np.testing.assert_allclose(agent.online_network.state_dict()[k].cpu().numpy(),
                                    oracle.online[k].numpy(), atol=1e-5, rtol=0)
+
+
+@pytest.mark.parametrize("conf", [rmsprop_network_config, mse_network_config])
+def test_gpu_agent_refuses_other_optimizer_or_loss(tmp_path, conf):
+    """network_config may name RMSprop / MSELoss; the engine implements Adam + SmoothL1 only and
+    must refuse instead of training with a different update rule."""
+    with pytest.raises(NotImplementedError):
+        Agents.DuelingDoubleDQNAgent(**agent_kwargs("DuelingDoubleDQNAgent", 14, 32, 500, tmp_path,
+                                                    nn_conf_func=conf))
+
+
+def test_gpu_agent_log_reports_learn_throughput(tmp_path):
+    """Agent.log adds the learn-throughput scalar (transitions/s) next to the reference's
+    AvgRew / AvgEpLen / Episodes (R:dqn/agent.py:130-147)."""
+    agent = Agents.DuelingDoubleDQNAgent(**agent_kwargs("DuelingDoubleDQNAgent", 14, 32, 500, tmp_path,
+                                                        log_frequency=2))
+    obs, act, rew, done, nobs = O.synth_transitions(100, 14, 8, seed=1)
+    for i in range(100):
+        agent.store_transitions(obs[i:i + 1], [int(act[i])], [float(rew[i])], [bool(done[i])], nobs[i:i + 1], None)
+    seen = {}
+    agent.summary_writer.add_scalar = lambda tag, v, global_step=None: seen.__setitem__(tag, v)
+    for t in range(3):
+        agent.step = t
+        agent.learn()
+        agent.update_target_network()
+        agent.log()
+    assert {"AvgRew", "AvgEpLen", "Episodes", "Loss", "LearnTransitionsPerSec"} <= set(seen)
+    assert seen["LearnTransitionsPerSec"] > 0
+
+
+def test_gpu_per_agent_step_survives_host_sampling(tmp_path):
+    """A host-side ReplayMemoryPrioritized.sample_transitions(step) moves the engine's PER step;
+    the next learn() must still interpolate beta from agent.step (ADVICE: stale cached step)."""
+    agent = Agents.PerDuelingDoubleDQNAgent(**agent_kwargs("PerDuelingDoubleDQNAgent", 14, 32, 500, tmp_path))
+    obs, act, rew, done, nobs = O.synth_transitions(100, 14, 8, seed=2)
+    for i in range(100):
+        agent.store_transitions(obs[i:i + 1], [int(act[i])], [float(rew[i])], [bool(done[i])], nobs[i:i + 1], None)
+    agent.step = 7
+    agent.learn()
+    agent.replay_memory_buffer.sample_transitions(123456)
+    agent.step = 8
+    agent.learn()
+    torch.cuda.synchronize()
+    beta = float(agent.engine.ctrl().per_beta)
+    assert abs(beta - float(np.interp(8, [0, 2e6], [0.4, 1.0]))) < 1e-12, beta

@@ -148,21 +148,37 @@ def test_gpu_bf16_error_vs_fp32_reference(algo, obs_dim, batch, capacity, n_fill
     _check_step(eng, rec, rec32, 0)
 
 
-@pytest.mark.parametrize("obs_dim,batch,cap,n_fill,seed", [
-    (14, 32, 500, 300, 3),
-    (284, 1024, 20000, 20000, 5),
+@pytest.mark.parametrize("obs_dim,batch,cap,n_fill,seed,steps", [
+    (14, 32, 500, 300, 3, 1),
+    (284, 1024, 20000, 20000, 5, 1),
+    (284, 8192, 40000, 40000, 6, 2),   # configs[4] on one GPU: PER + Dueling Double, bf16, B=8192
 ])
-def test_gpu_bf16_per_learn_matches_bf16_oracle(obs_dim, batch, cap, n_fill, seed):
-    """Config 5's algorithm: PER + Dueling Double DQN in bf16 (tree sampling bit-exact)."""
+def test_gpu_bf16_per_learn_matches_bf16_oracle(obs_dim, batch, cap, n_fill, seed, steps):
+    """Config 5's algorithm: PER + Dueling Double DQN in bf16 (tree sampling bit-exact).  At
+    B=8192 the second step samples from the tree the first step's priorities updated."""
+    import copy
+    from test_gpu_per import assert_tree_equal
     emu, ref, eng = make_bf16_pair("PerDuelingDoubleDQNAgent", obs_dim, batch, cap, n_fill, seed, per=True)
-    rec = emu.train_step()
-    eng.learn_step(soft_update=True)
-    torch.cuda.synchronize()
-    eng.check_device_error()
-    _check_step(eng, rec, None, 0, cap=cap)
-    np.testing.assert_allclose(eng.is_weights.cpu().numpy(), rec.is_weights.astype(np.float32), rtol=2e-7)
-    _close(eng.per_abs_td.cpu().numpy(), rec.abs_td.reshape(-1), "|delta|")
-    _compare_weights(emu, eng)
+    for step in range(steps):
+        t = emu.replay.replay_buffer
+        snap = copy.copy(t)
+        snap.tree, snap.data = t.tree.copy(), list(t.data)
+        rec = emu.train_step()
+        eng.learn_step(soft_update=True)
+        torch.cuda.synchronize()
+        eng.check_device_error()
+        _check_step(eng, rec, None, step, cap=cap)
+        np.testing.assert_allclose(eng.is_weights.cpu().numpy(), rec.is_weights.astype(np.float32), rtol=2e-7)
+        absd = eng.per_abs_td.cpu().numpy()
+        _close(absd, rec.abs_td.reshape(-1), "|delta|")
+        _compare_weights(emu, eng)
+        # the tree update itself is exact: the oracle's SumTree, updated in order with the
+        # ENGINE's |delta| (bf16 moves |delta| within the tolerance above), equals the engine's
+        # tree bit for bit; the oracle continues from it so the next step samples the same tree
+        emu.replay.replay_buffer = snap
+        emu.replay.update_batch_priorities(rec.positions.tolist(), absd.reshape(-1, 1))
+        assert_tree_equal(eng, snap, exact=True)
+    assert np.array_equal(eng.get_rng(1), emu.np_state)
 
 
 @pytest.mark.parametrize("mr", ["1", "2", "4"])

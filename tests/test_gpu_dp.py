@@ -14,6 +14,15 @@ pytestmark = pytest.mark.gpu
 HERE = os.path.dirname(os.path.abspath(__file__))
 
 
+def run_ranks(tmp_path, world, algo, sampling="global", case="small", compute="fp32", timeout=300):
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(free_port()))
+    procs = [subprocess.Popen([sys.executable, os.path.join(HERE, "dp_gpu_worker.py"), str(r), str(world), algo,
+                               str(tmp_path), sampling, case, compute], env=env) for r in range(world)]
+    for p in procs:
+        assert p.wait(timeout=timeout) == 0
+    return [np.load(tmp_path / f"rank{r}.npz") for r in range(world)]
+
+
 def free_port():
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
@@ -95,3 +104,56 @@ def test_gpu_graphed_dp_step_matches_eager(algo):
                        env=env, capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
     assert "graphed == eager: True; dp == single: True" in r.stdout, r.stdout[-2000:]
+
+
+@pytest.mark.parametrize("world", [2, 8])
+def test_gpu_dp_global_batch_4096_matches_oracle(tmp_path, world):
+    """configs[3]: global minibatch 4096 sharded over `world` ranks (2048 / 512 rows per rank),
+    every rank drawing the same global index set (reference-exact random.sample), one gradient
+    all-reduce; against the single-process oracle learning on the whole minibatch.  The ranks
+    share the box's one GPU and all-reduce over gloo (8 GPUs and RCCL are the driver's node)."""
+    import random
+    sys.path.insert(0, HERE)
+    from dp_gpu_worker import CASES
+    algo = "DuelingDoubleDQNAgent"
+    z = run_ranks(tmp_path, world, algo, case="c3", timeout=600)
+    obs_dim, batch, cap, fill, seed = CASES["c3"]
+    spec = O.mlp_spec(obs_dim, 8, O.algo_spec_head(algo))
+    ref = O.OracleLearner(spec, algo, batch, cap, seed=seed, params=O.reference_init(spec, seed))
+    O.fill_replay(ref, *O.synth_transitions(fill, obs_dim, 8, seed=seed + 100))
+    ref.py_state = O.py_state_to_array(random.Random(seed).getstate())
+    recs = [ref.train_step() for _ in range(3)]
+    flat_on = np.concatenate([v.reshape(-1).numpy() for v in ref.online.values()])
+    flat_tg = np.concatenate([v.reshape(-1).numpy() for v in ref.target.values()])
+    for r in range(world):
+        assert np.array_equal(z[r]["positions"].astype(np.int64), np.stack([x.positions for x in recs])), r
+        np.testing.assert_allclose(z[r]["losses"], [x.loss for x in recs], rtol=1e-5, atol=1e-6)
+        np.testing.assert_allclose(z[r]["params"], flat_on, atol=1e-5, rtol=0)
+        np.testing.assert_allclose(z[r]["target"], flat_tg, atol=1e-5, rtol=0)
+        assert np.array_equal(z[r]["params"], z[0]["params"])   # replicas stay bitwise identical
+
+
+def test_gpu_dp_world2_bf16_matches_bf16_oracle(tmp_path):
+    """bf16 compute under DP (GRADS_ONLY shard steps + all-reduce + apply_grads), PER Dueling
+    Double (configs[4]'s algorithm), against the oracle's bf16 emulation on the whole
+    minibatch with the bf16 tolerances of tests/test_gpu_bf16.py."""
+    import random
+    sys.path.insert(0, HERE)
+    from dp_gpu_worker import CASES
+    from test_gpu_bf16 import LOSS_RTOL, W_ATOL
+    algo = "PerDuelingDoubleDQNAgent"
+    z = run_ranks(tmp_path, 2, algo, compute="bf16")
+    obs_dim, batch, cap, fill, seed = CASES["small"]
+    spec = O.mlp_spec(obs_dim, 8, O.algo_spec_head(algo))
+    emu = O.OracleLearner(spec, algo, batch, cap, seed=seed, params=O.reference_init(spec, seed), per_pow="cr",
+                          compute="bf16")
+    O.fill_replay(emu, *O.synth_transitions(fill, obs_dim, 8, seed=seed + 100))
+    emu.py_state = O.py_state_to_array(random.Random(seed).getstate())
+    emu.np_state = O.np_state_to_array(np.random.RandomState(seed).get_state())
+    recs = [emu.train_step() for _ in range(3)]
+    flat_on = np.concatenate([v.reshape(-1).numpy() for v in emu.online.values()])
+    for r in range(2):
+        assert np.array_equal(z[r]["positions"].astype(np.int64) + cap - 1, np.stack([x.positions for x in recs]))
+        np.testing.assert_allclose(z[r]["losses"], [x.loss for x in recs], rtol=LOSS_RTOL, atol=1e-6)
+        np.testing.assert_allclose(z[r]["params"], flat_on, atol=W_ATOL, rtol=0)
+    assert np.array_equal(z[0]["params"], z[1]["params"]) and np.array_equal(z[0]["tree"], z[1]["tree"])

@@ -8,7 +8,7 @@ import pytest
 import torch
 
 from oracle import ref as O
-from parity import assert_grad_close
+from parity import assert_grad_close, record_exemptions
 
 pytestmark = pytest.mark.gpu
 
@@ -99,24 +99,41 @@ def make_pair(algo, obs_dim, batch, capacity, n_fill, seed, graphs=True):
     return oracle, eng
 
 
-def compare_state(oracle, eng, atol=1e-5, loose=None):
+LOOSE_MAX_FRAC = 1e-3   # at most 0.1 % of a tensor's entries may use the 2 lr bound
+
+
+def compare_state(oracle, eng, atol=1e-5, loose=None, report=None):
     """Weights within atol, Adam m / v within 1e-6 / 1e-7.  `loose` (from _check_learn): per
     tensor, the entries whose gradient differed by more than 0.1 % in some step.  Adam moves a
     weight by about lr * g / |g| whatever the size of g, so there the step is not determined to
     1e-5 by a gradient that agrees to the gradient tolerance (a ReLU mask flipped by an fp32
     pre-activation within rounding of zero does this); those entries are bounded by 2 lr per
-    step instead, everything else by atol."""
+    step instead, everything else by atol.  Only the exempted entries that actually exceed atol
+    are counted; more than LOOSE_MAX_FRAC of a tensor fails the test, and the counts are
+    returned (and printed) so the exemption is never silent."""
     views = {"online": eng.param_views(eng.params), "target": eng.param_views(eng.target_params),
              "m": eng.param_views(eng.adam_m), "v": eng.param_views(eng.adam_v)}
     worst = {}
+    exempt = {}
     for nm, src in (("online", oracle.online), ("target", oracle.target), ("m", oracle.m), ("v", oracle.v)):
         for k, ref in src.items():
             got = views[nm][k].detach().cpu()
             d = (got - ref).abs()
             if nm in ("online", "target") and loose is not None and bool(loose[k].any()):
-                assert float(d[loose[k]].max()) <= 2.0 * oracle.lr + atol, (nm, k)   # one step from synced state
+                over = loose[k] & (d > atol)
+                n_over = int(over.sum())
+                if n_over:
+                    assert float(d[over].max()) <= 2.0 * oracle.lr + atol, (nm, k)   # one step from synced state
+                    exempt[f"{nm}:{k}"] = n_over
+                    assert n_over <= LOOSE_MAX_FRAC * d.numel(), (nm, k, n_over, d.numel())
                 d = d * (~loose[k])
             worst[nm] = max(worst.get(nm, 0.0), float(d.max()))
+    if exempt:
+        print("exempted entries (2 lr bound):", exempt)
+        numels = {f"{nm}:{k}": views[nm][k].numel() for nm in ("online", "target") for k in oracle.online}
+        record_exemptions(exempt, numels)
+    if report is not None:
+        report.update(exempt)
     assert worst["online"] <= atol and worst["target"] <= atol, worst
     assert worst["m"] <= 1e-6 and worst["v"] <= 1e-7, worst
     return worst
@@ -129,6 +146,7 @@ def compare_state(oracle, eng, atol=1e-5, loose=None):
     ("DuelingDoubleDQNAgent", 284, 256, 5000, 3000, 6),
     ("DuelingDoubleDQNAgent", 284, 1024, 20000, 20000, 7),
     ("DoubleDQNAgent", 284, 100, 700, 650, 8),
+    ("DuelingDoubleDQNAgent", 284, 4096, 60000, 60000, 19),   # configs[3]'s global minibatch
 ])
 def test_gpu_learn_matches_oracle(algo, obs_dim, batch, capacity, n_fill, seed):
     _check_learn(*make_pair(algo, obs_dim, batch, capacity, n_fill, seed))
@@ -256,31 +274,57 @@ def test_gpu_learn_graph_and_eager_identical():
     assert torch.equal(e1.target_params, e2.target_params)
 
 
-@pytest.mark.parametrize("golden", ["learn_mlp14_DQNAgent", "learn_mlp14_DoubleDQNAgent",
-                                    "learn_mlp14_DuelingDoubleDQNAgent", "learn_mlp284_DuelingDoubleDQNAgent"])
+GOLDEN_MLP = ["learn_mlp14_DQNAgent", "learn_mlp14_DoubleDQNAgent", "learn_mlp14_DuelingDoubleDQNAgent",
+              "learn_mlp284_DuelingDoubleDQNAgent", "learn_mlp284b1024_DuelingDoubleDQNAgent",
+              "learn_mlp284b4096_DuelingDoubleDQNAgent", "learn_mlp284b8192_PerDuelingDoubleDQNAgent"]
+
+
+@pytest.mark.parametrize("golden", GOLDEN_MLP)
 def test_gpu_learn_golden(golden):
-    """Engine against the reference's own outputs (tests/golden, made by make_golden.py)."""
+    """Engine against the reference's own outputs (tests/golden, made by make_golden.py by
+    running the reference): sampled positions / tree leaves and RNG state bit-exact, loss and
+    the online and target weights after every step within a strict 1e-5 (no exemptions).
+    Covers configs[1]'s batch (1024), configs[3]'s global batch (4096) and configs[4]'s PER
+    batch (8192, fp32 arithmetic)."""
     E = _engine_mod()
     z = np.load(os.path.join(GOLDEN, golden + ".npz"))
     algo = str(z["algo"])
-    obs_dim = int(z["obs_dim"])
+    per = algo.startswith("Per")
+    obs_dim, batch, cap = int(z["obs_dim"]), int(z["batch"]), int(z["buffer"])
     head = O.algo_spec_head(algo)
     init = O.reference_init(O.mlp_spec(obs_dim, 8, head), int(z["seed"]))
-    eng = E.LearnEngine(E.mlp_spec(obs_dim, 8, head), algo, int(z["batch"]), int(z["buffer"]))
+    eng = E.LearnEngine(E.mlp_spec(obs_dim, 8, head), algo, batch, cap)
     eng.load_params(init)
     eng.push(*O.synth_transitions(int(z["n_fill"]), obs_dim, 8, seed=int(z["seed"]) + 100))
     eng.set_rng(0, z["py_state_in"])
+    eng.set_rng(1, z["np_state_in"])
     for s in range(int(z["steps"])):
         eng.learn_step(soft_update=True)
         torch.cuda.synchronize()
-        assert np.array_equal(eng.batch_idx.cpu().numpy().astype(np.int64), z["pos"][s])
-        assert abs(eng.loss() - z["loss"][s]) <= 1e-5 * max(1.0, abs(z["loss"][s]))
-    assert np.array_equal(eng.get_rng(0), z["py_state_out"])
+        eng.check_device_error()
+        got = eng.batch_idx.cpu().numpy().astype(np.int64) + (cap - 1 if per else 0)
+        assert np.array_equal(got, z["pos"][s]), f"step {s}: positions differ"
+        if per:
+            # step 1 samples a tree of pushed max priorities: exact to fp32 rounding.  Later steps
+            # weight by (p / p_min)^-beta, and p_min = (|delta_min| + 1e-4)^0.6 comes from a small
+            # |delta| that carries the forward's fp32 noise amplified by dp/d|delta| (<= 24)
+            rtol = 1e-6 if s == 0 else 1e-5
+            np.testing.assert_allclose(eng.is_weights.cpu().numpy(), z["isw"][s].astype(np.float32), rtol=rtol)
+        assert abs(eng.loss() - z["loss"][s]) <= 1e-5 * max(1.0, abs(z["loss"][s])), (s, eng.loss(), z["loss"][s])
+    if per:
+        assert np.array_equal(eng.get_rng(1), z["np_state_out"])
+    else:
+        assert np.array_equal(eng.get_rng(0), z["py_state_out"])
+    stride = int(z["stride"])
     keys = [str(k) for k in z["keys"]]
     on, tg = eng.param_views(eng.params), eng.param_views(eng.target_params)
     for i, k in enumerate(keys):
-        np.testing.assert_allclose(on[k].cpu().numpy().reshape(-1), z[f"online_{i}"], atol=1e-5, rtol=0)
-        np.testing.assert_allclose(tg[k].cpu().numpy().reshape(-1), z[f"target_{i}"], atol=1e-5, rtol=0)
+        for nm, views in (("online", on), ("target", tg)):
+            got = views[k].cpu().numpy().reshape(-1)
+            ref = z[f"{nm}_{i}"]
+            if got.size != ref.size:
+                got = got[::stride]
+            np.testing.assert_allclose(got, ref, atol=1e-5, rtol=0, err_msg=f"{nm} {k}")
 
 
 def test_gpu_prefetch_mode_bit_identical(monkeypatch):
