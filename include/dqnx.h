@@ -145,6 +145,7 @@ typedef struct dqnx_ctrl {
 /* device error codes written to dqnx_ctrl.error */
 #define DQNX_DEVERR_SAMPLE_TOO_LARGE 1   /* random.sample: k > n (ValueError) */
 #define DQNX_DEVERR_EMPTY_TREE 2         /* PER sample with total priority 0 */
+#define DQNX_DEVERR_SAMPLER_STUCK 3      /* internal: a sampler wait exceeded its bound (never expected) */
 
 /* ---- engine lifetime --------------------------------------------------------------- */
 typedef struct dqnx_engine dqnx_engine;
@@ -184,6 +185,11 @@ int dqnx_engine_buffer(const dqnx_engine* e, int32_t which, uint64_t* offset, ui
 int dqnx_engine_obs_stride(const dqnx_engine* e, int32_t* stride);
 /* Bind the caller-allocated arena (device pointer, 256-byte aligned). */
 int dqnx_engine_bind(dqnx_engine* e, void* arena, uint64_t bytes);
+/* The caller wrote the parameters (DQNX_BUF_PARAMS / DQNX_BUF_TARGET_PARAMS) directly, e.g. a
+ * checkpoint load through state_dict() views (R:dqn/network.py:37-47, R:dqn/agent.py:112-121):
+ * the next learn step rebuilds the engine's derived weight layouts.  Host only, no device work.
+ * (dqnx_soft_update / dqnx_hard_update / dqnx_engine_reset imply it.) */
+int dqnx_params_modified(dqnx_engine* e);
 /* Zero Adam moments, ring state, tree, control block (params untouched); stream-ordered. */
 int dqnx_engine_reset(dqnx_engine* e, void* stream);
 /* Use hipGraph capture/replay for learn steps (default on). */

@@ -52,6 +52,14 @@ __device__ __forceinline__ float act_fwd(float x) {
 
 __device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
 
+// Loads through the global address space.  A generic pointer the compiler cannot prove global
+// (e.g. one fetched from a struct member) compiles to flat_load, which counts in lgkmcnt as
+// well: the next s_waitcnt for a kernel-argument s_load then drains it, serialising round trips.
+template <class T>
+__device__ __forceinline__ T gld(const T* p) {
+    return *(const __attribute__((address_space(1))) T*)p;
+}
+
 
 // XCD-aware block remap (CDNA guide T1): blocks are dealt round-robin over the 8 XCDs, so
 // hand XCD x a CONTIGUOUS range of tiles (bijective for any total).  Speed only: placement

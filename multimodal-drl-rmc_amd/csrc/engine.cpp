@@ -190,7 +190,7 @@ struct dqnx_engine {
     uint64_t total = 0;
     // workspace sub-regions (byte offsets from the arena base)
     uint64_t ws_phys = 0, ws_pool = 0, ws_xobs = 0, ws_head_part = 0, ws_loss_part = 0, ws_stage = 0;
-    uint64_t ws_adam_tab = 0, ws_stamps = 0, ws_dhead = 0, ws_raw = 0, ws_trans = 0, ws_per_ticket = 0, ws_per_wl = 0, ws_per_wp = 0, ws_per_winit = 0, ws_per_last = 0;
+    uint64_t ws_adam_tab = 0, ws_stamps = 0, ws_dhead = 0, ws_raw = 0, ws_trans = 0, ws_gtab = 0, ws_mtc = 0, ws_per_ticket = 0, ws_per_wl = 0, ws_per_wp = 0, ws_per_winit = 0, ws_per_last = 0;
     // fused plan: fragment-blocked weight copies [online fwd | target fwd | online chain] per layer
     uint64_t ws_wblk[2][FUSED_MAX_L] = {{0}}, ws_wblkT[FUSED_MAX_L] = {0};
     std::vector<uint64_t> ws_H, ws_dZ, ws_part;
@@ -216,6 +216,8 @@ struct dqnx_engine {
     // forward + split-K backward levels + Adam pass (two-stream nets); 1 = head kernel also
     // makes dZ_{L-1}, one full-K dW + Adam launch
     int bwd_plan = 0;
+    int mtc_blocks = 0;     // uniform sampler's MT block cache (fused plan only; 0 = off)
+    bool wblk_dirty = true; // the fused plan's blocked weight copies must be rebuilt before the next step
     FusedFwdArgs fplan;     // LDS geometry of the fused plan (valid when bwd_plan == 2)
     int fsplit = 1;         // layer-1 column parts of the split forward (1: one forward launch)
     bool pf_valid = false;   // a prefetched minibatch for the next step sits in slot pf_slot
@@ -273,6 +275,10 @@ int layout(dqnx_engine* e) {
     };
     e->ws_phys = sub((uint64_t)2 * e->Bl * 4);
     e->ws_pool = sub((uint64_t)(e->setsize + 64) * 4);
+    e->ws_gtab = sub(sample_table_bytes(e->Bs));   // 0 unless the minibatch exceeds the LDS tables
+    e->mtc_blocks = (e->bwd_plan == 2 && c.algo != DQNX_ALGO_PER_DOUBLE && !getenv("DQNX_NO_MT_CACHE"))
+                        ? mt_cache_target_blocks(e->Bs, c.capacity) : 0;
+    e->ws_mtc = sub((uint64_t)mt_cache_words() * 4);   // always valid for the sampler's loads
     e->ws_xobs = sub((uint64_t)e->Bl * e->stride * 4);
     e->ws_H.assign(L, 0);
     e->ws_dZ.assign(L, 0);
@@ -417,6 +423,40 @@ AdamBias adam_bias_args(dqnx_engine* e) {
     return b;
 }
 
+// The fused plan's blocked weight copies, written by the Adam pass next to every weight.
+// Opt-in (DQNX_ADAM_BLK=1): the Adam pass writes the blocked copies next to every weight, so
+// the sampler launch rebuilds them only after host-side writes (dqnx_params_modified).  Measured
+// on MI355X (MLP-284, B = 1024): Adam 4.1 -> 6.6 us (three scattered stores per weight) while the
+// rebuild by spare workgroups of the sampler launch costs the sampler ~0.4 us, so the default
+// keeps the per-step rebuild.  (Adam's row/column split needs out * in < 2^24.)
+bool adam_keeps_blk(const dqnx_engine* e) {
+    if (e->bwd_plan != 2) return false;
+    const char* v = getenv("DQNX_ADAM_BLK");
+    if (!v || atoi(v) == 0) return false;
+    for (const LayerPlan& lp : e->np.dense)
+        if ((int64_t)lp.out * lp.in >= ((int64_t)1 << 24)) return false;
+    return true;
+}
+
+void fill_blk_layers(dqnx_engine* e, AdamArgs& aa) {
+    aa.nblk = 0;
+    if (!adam_keeps_blk(e)) return;
+    const NetPlan& np = e->np;
+    aa.blk_bf16 = e->fplan.bf16 ? 1 : 0;
+    for (int l = 0; l < (int)np.dense.size() && l < 3; l++) {
+        AdamArgs::BlkLayer& B = aa.blk[aa.nblk++];
+        B.woff = np.dense[l].off;
+        B.in = np.dense[l].in;
+        B.out = np.dense[l].out;
+        B.inv_in = 1.0f / (float)B.in;
+        B.kpad = e->fplan.kpad[l];
+
+        B.fwd_online = at<float>(e, e->ws_wblk[0][l]);
+        B.fwd_target = at<float>(e, e->ws_wblk[1][l]);
+        B.chain = l >= 1 ? at<float>(e, e->ws_wblkT[l]) : nullptr;
+    }
+}
+
 // Gradient reduction (fixed-order sum of the split-K slabs) + Adam (+ soft update).
 KStep adam_kstep(dqnx_engine* e, int flags) {
     const dqnx_config& c = e->cfg;
@@ -478,6 +518,11 @@ KStep adam_kstep(dqnx_engine* e, int flags) {
     aa.loss_partial = at<float>(e, e->ws_loss_part);
     aa.n_loss_partial = e->tiles;
     aa.batch_global = e->Bg;
+    fill_blk_layers(e, aa);
+    if (e->mtc_blocks && !(flags & DQNX_STEP_GIVEN_INDICES)) {   // keep the sampler's MT blocks ahead
+        aa.mtc = at<uint32_t>(e, e->ws_mtc);
+        aa.mtc_blocks = e->mtc_blocks;
+    }
     KStep k;
     k.name = aa.mode ? "adam_fused" : "grad_reduce";
     const double P = (double)np.P;
@@ -738,9 +783,12 @@ void build_fused_steps(dqnx_engine* e, int flags, int32_t* idx, int32_t* phys, s
     }
 }
 
-// key = flags | (slot << 8): `slot` selects the (sampled indices, physical rows) buffer pair.
+// key = flags | (slot << 8) | KEY_RELAYOUT: `slot` selects the (sampled indices, physical rows)
+// buffer pair; KEY_RELAYOUT = the sampler launch also rebuilds the fused plan's blocked weight
+// copies (only after the weights changed outside the Adam pass, which keeps them current).
+constexpr int KEY_RELAYOUT = 0x40;
 std::vector<KStep> build_learn_steps(dqnx_engine* e, int key) {
-    const int flags = key & 0xff;
+    const int flags = key & 0x3f;
     const int slot = (key >> 8) & 1;
     std::vector<KStep> ks;
     const dqnx_config& c = e->cfg;
@@ -758,7 +806,12 @@ std::vector<KStep> build_learn_steps(dqnx_engine* e, int key) {
 
     // 1. sample (R:dqn/replay_memory.py:38-39; PER :69-92)
     int rl_blocks = 0;
-    const RelayoutArgs rl = relayout_args(e, &rl_blocks);
+    RelayoutArgs rl = relayout_args(e, &rl_blocks);
+    if (!(key & KEY_RELAYOUT)) {
+        rl.njobs = 0;
+        rl.total_q = 0;
+        rl_blocks = 0;
+    }
     if (c.algo == DQNX_ALGO_PER_DOUBLE) {
         PerSampleArgs pa = per_sample_args(e, idx, phys);
         pa.rl = rl;
@@ -794,6 +847,9 @@ std::vector<KStep> build_learn_steps(dqnx_engine* e, int key) {
         sa.stamps = at<int64_t>(e, e->ws_stamps);
         sa.rl = rl;
         sa.rl_blocks = rl_blocks;
+        sa.gtab = sample_table_bytes(e->Bs) ? at<unsigned long long>(e, e->ws_gtab) : nullptr;
+        sa.mtc = at<uint32_t>(e, e->ws_mtc);
+        sa.mtc_blocks = e->mtc_blocks;
         KStep k;
         k.name = "sample_uniform";
         k.bytes = 2.0 * 625 * 4 + 4.0 * e->Bs + 4.0 * Bl;
@@ -1333,6 +1389,7 @@ int enqueue_apply(dqnx_engine* e, int flags, hipStream_t s) {
     aa.beta2d = c.beta2;
     aa.lrd = c.lr;
     aa.batch_global = e->Bg;
+    fill_blk_layers(e, aa);
     return launch_adam(aa, s);
 }
 
@@ -1600,6 +1657,12 @@ int dqnx_engine_obs_stride(const dqnx_engine* e, int32_t* stride) {
     return DQNX_OK;
 }
 
+int dqnx_params_modified(dqnx_engine* e) {
+    if (!e) return set_error(DQNX_EINVAL, "null engine");
+    e->wblk_dirty = true;
+    return DQNX_OK;
+}
+
 int dqnx_engine_bind(dqnx_engine* e, void* arena, uint64_t bytes) {
     if (!e || !arena) return set_error(DQNX_EINVAL, "null argument");
     if (bytes < e->total) return set_error(DQNX_EINVAL, "arena too small: %llu < %llu", (unsigned long long)bytes,
@@ -1607,6 +1670,7 @@ int dqnx_engine_bind(dqnx_engine* e, void* arena, uint64_t bytes) {
     if (((uintptr_t)arena) % 256) return set_error(DQNX_EINVAL, "arena must be 256-byte aligned");
     drop_graphs(e);
     e->arena = (char*)arena;
+    e->wblk_dirty = true;
     return DQNX_OK;
 }
 
@@ -1651,6 +1715,7 @@ int dqnx_engine_reset(dqnx_engine* e, void* stream) {
     e->ring_size = 0;
     e->ring_wptr = 0;
     e->pf_valid = false;
+    e->wblk_dirty = true;
     return DQNX_OK;
 }
 
@@ -1805,8 +1870,12 @@ int dqnx_learn_step(dqnx_engine* e, int32_t flags, void* stream) {
         return set_error(DQNX_EINVAL, "Sample larger than population: %lld < %d", (long long)e->ring_size, e->Bs);
     const int base = flags & (DQNX_STEP_SOFT_UPDATE | DQNX_STEP_GIVEN_INDICES | DQNX_STEP_GRADS_ONLY);
     if (!prefetch && !e->pf_valid) {
-        const std::vector<KStep>& ks = steps_for(e, base);
-        return run_graphed(e, base, s, [&](hipStream_t cs) { return enqueue_range(ks, 0, (int)ks.size(), cs); });
+        // the weights changed outside the Adam pass: this step's sampler launch rebuilds the copies
+        const int key = base | ((e->bwd_plan == 2 && (e->wblk_dirty || !adam_keeps_blk(e))) ? KEY_RELAYOUT : 0);
+        const std::vector<KStep>& ks = steps_for(e, key);
+        rc = run_graphed(e, key, s, [&](hipStream_t cs) { return enqueue_range(ks, 0, (int)ks.size(), cs); });
+        if (!rc) e->wblk_dirty = false;
+        return rc;
     }
     rc = pf_events(e);
     if (rc) return rc;
@@ -1969,6 +2038,7 @@ int dqnx_apply_grads(dqnx_engine* e, int32_t flags, void* stream) {
 int dqnx_soft_update(dqnx_engine* e, void* stream) {
     int rc = check_bound(e);
     if (rc) return rc;
+    e->wblk_dirty = true;   // the target copies change outside the Adam pass
     const float tau = (float)((double)e->cfg.tau * e->cfg.n_env);
     const float omt = (float)(1.0 - (double)e->cfg.tau * e->cfg.n_env);
     return launch_soft_update(at<float>(e, e->off[DQNX_BUF_TARGET_PARAMS]), at<float>(e, e->off[DQNX_BUF_PARAMS]),
@@ -1978,6 +2048,7 @@ int dqnx_soft_update(dqnx_engine* e, void* stream) {
 int dqnx_hard_update(dqnx_engine* e, void* stream) {
     int rc = check_bound(e);
     if (rc) return rc;
+    e->wblk_dirty = true;
     DQNX_HIP_CHECK(hipMemcpyAsync(e->arena + e->off[DQNX_BUF_TARGET_PARAMS], e->arena + e->off[DQNX_BUF_PARAMS],
                                   (size_t)e->np.P * 4, hipMemcpyDeviceToDevice, (hipStream_t)stream));
     return DQNX_OK;

@@ -15,6 +15,7 @@
 #include "gemm_lds.hpp"
 #include "gemm_sk.hpp"
 #include "learn.hpp"
+#include "mt.hpp"
 
 namespace dqnx {
 
@@ -640,9 +641,49 @@ __global__ __launch_bounds__(256) void k_head(HeadArgs a) {
 //   target = (tau*n_env)*p + (1 - tau*n_env)*target
 // mode 0: partials -> grads only; 1: partials -> grads + Adam; 2: grads -> Adam.
 // =====================================================================================
+// The uniform sampler's MT block cache (learn.hpp): twist the last cached block forward until
+// the cache holds `target` blocks.  One 256-thread workgroup; blocks ping-pong through LDS.
+__device__ __forceinline__ void mt_cache_extend(uint32_t* mtc, int target) {
+    __shared__ uint32_t mb[2][624];
+    __shared__ int s_cnt;
+    const int tid = threadIdx.x;
+    if (tid == 0) s_cnt = (int)mtc[0];
+    __syncthreads();
+    const int cnt = s_cnt;
+    if (cnt <= 0 || cnt >= target) return;
+    uint32_t* blocks = mtc + 64;
+    for (int j = tid; j < 624; j += blockDim.x) mb[0][j] = blocks[(int64_t)(cnt - 1) * 624 + j];
+    __syncthreads();
+    int cur = 0;
+    for (int b = cnt; b < target; b++) {
+        mt_twist_into(mb[cur], mb[cur ^ 1]);   // ends with a barrier
+        cur ^= 1;
+        for (int j = tid; j < 624; j += blockDim.x) blocks[(int64_t)b * 624 + j] = mb[cur][j];
+    }
+    if (tid == 0) mtc[0] = (uint32_t)target;   // read by a later kernel only: no fence needed
+}
+
+// Position of W_l[r][q] in its fragment-blocked copies (relayout.hpp): fp32 fwd blocks are
+// [t = r/16][c = q/16][g = q%16/4][i = r%16][j = q%4] with c < kpad/16; chain blocks the same with
+// the roles of r and q exchanged (c < out/16).  bf16 blocks are 16 x 32: c = q/32, g = q%32/8,
+// j = q%8, 8 elements per 16-byte unit.
+__device__ __forceinline__ int64_t blk_pos(int r, int q, int nch, bool bf16) {
+    if (!bf16) return 4 * ((((int64_t)(r >> 4) * nch + (q >> 4)) * 64) + ((q & 15) >> 2) * 16 + (r & 15)) + (q & 3);
+    return 8 * ((((int64_t)(r >> 4) * nch + (q >> 5)) * 64) + ((q & 31) >> 3) * 16 + (r & 15)) + (q & 7);
+}
+
+__device__ __forceinline__ void blk_store(float* base, int64_t pos, float v, bool bf16) {
+    if (bf16) reinterpret_cast<uint16_t*>(base)[pos] = bf16_bits(v);
+    else base[pos] = v;
+}
+
 __global__ __launch_bounds__(256) void k_adam(AdamArgs a) {
+    if (a.mtc && blockIdx.x == gridDim.x - 1) {   // the extra workgroup: sampler cache for the next step
+        mt_cache_extend(a.mtc, a.mtc_blocks);
+        return;
+    }
     const int64_t P = a.n_params;
-    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    const int64_t stride = (int64_t)(gridDim.x - (a.mtc ? 1 : 0)) * blockDim.x;
     float step_size = 0.f, bc2s = 1.f;
     if (a.mode != 0) {   // this step's scalars, stored by the head kernel (adam_advance)
         step_size = a.ctrl->adam_step_size;
@@ -692,7 +733,26 @@ __global__ __launch_bounds__(256) void k_adam(AdamArgs a) {
         a.m[e] = m;
         a.v[e] = v;
         a.p[e] = p;
-        if (a.soft) a.target[e] = a.tau * p + a.one_minus_tau * tg;
+        if (a.soft) tg = a.tau * p + a.one_minus_tau * tg;
+        if (a.soft) a.target[e] = tg;
+#pragma unroll
+        for (int l = 0; l < 3; l++) {   // the blocked copies of a dense-layer weight
+            if (l >= a.nblk) break;
+            const AdamArgs::BlkLayer& L = a.blk[l];
+            const int64_t le64 = e - L.woff;
+            if (le64 < 0 || le64 >= (int64_t)L.out * L.in) continue;
+            // row / column by a float reciprocal, corrected by one step (le < 2^24: exact enough)
+            const int le = (int)le64;
+            int r = (int)((float)le * L.inv_in);
+            r -= (r * L.in > le) ? 1 : 0;
+            r += ((r + 1) * L.in <= le) ? 1 : 0;
+            const int q = le - r * L.in;
+            const bool bf = a.blk_bf16 != 0;
+            const int64_t pf = blk_pos(r, q, L.kpad / (bf ? 32 : 16), bf);
+            blk_store(L.fwd_online, pf, p, bf);
+            if (a.soft) blk_store(L.fwd_target, pf, tg, bf);
+            if (L.chain) blk_store(L.chain, blk_pos(q, r, L.out / (bf ? 32 : 16), bf), p, bf);
+        }
     }
     if (a.mode != 2 && blockIdx.x == 0 && threadIdx.x < 64 && a.loss_partial) {   // one wave, fixed order
         float s = 0.f;
@@ -869,6 +929,7 @@ int launch_adam(const AdamArgs& a, hipStream_t s) {
     int blocks = (int)((a.n_params + 255) / 256);
     if (blocks > 2048) blocks = 2048;
     if (blocks < 1) blocks = 1;
+    if (a.mtc) blocks++;   // + the sampler-cache workgroup
     hipLaunchKernelGGL(k_adam, dim3(blocks), dim3(256), 0, s, a);
     DQNX_HIP_CHECK(hipGetLastError());
     return DQNX_OK;

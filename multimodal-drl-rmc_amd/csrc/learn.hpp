@@ -150,6 +150,20 @@ struct AdamArgs {
     const float* adam_table;   // [t-1] = {-lr/bc1, bc2**0.5} for t <= adam_table_len (host libm)
     int adam_table_len;
     double beta1d, beta2d, lrd;
+    uint32_t* mtc;         // uniform sampler's MT block cache, extended by an extra workgroup (or null)
+    int mtc_blocks;
+    // fused plan: the fragment-blocked weight copies (relayout.hpp) written next to every updated
+    // weight, so they never need a rebuild launch (nblk = 0: none)
+    int nblk;
+    struct BlkLayer {
+        int64_t woff;      // flat offset of W_l [out][in]
+        int in, out, kpad;
+        float inv_in;      // 1 / in
+        float* fwd_online; // fwd-blocked online W_l
+        float* fwd_target; // fwd-blocked target W_l (soft update)
+        float* chain;      // chain-blocked online W_l (l >= 1) or null
+    } blk[3];
+    int blk_bf16;
 };
 
 // Full-K weight gradients of every layer + Adam (+ soft update) in one launch.
@@ -219,7 +233,19 @@ struct SampleArgs {
     int64_t* stamps;          // diagnostic builds (-DDQNX_STAMPS)
     RelayoutArgs rl;          // fused plan: blocked weight copies, built by blocks 1.. of the launch
     int rl_blocks;
+    unsigned long long* gtab; // k too large for an LDS table: sample_table_bytes(k) of global scratch
+    int test_flags;           // tests only (DQNX_SAMPLER_FORCE_FALLBACK): 1 = take the fast path's fallback
+    uint32_t* mtc;            // MT block cache (mt_cache_words), or null: [0] = blocks held, [64 + 624 b + o]
+    int mtc_blocks;           // blocks the cache is kept at (the state's block + its successors)
 };
+// MT block cache: the state block of the uniform sampler and its twisted successors, kept ahead
+// by the Adam launch of the previous step (k_adam's extra workgroup), so the next sample reads the
+// blocks it consumes instead of twisting them on its critical path.  Valid by construction: cache
+// block b+1 is always twist(cache block b), and it is used only when cache block 0 equals the
+// state block the caller hands in.
+constexpr int MTC_MAX_BLOCKS = 22;
+constexpr int64_t mt_cache_words() { return 64 + (int64_t)MTC_MAX_BLOCKS * 624; }
+int mt_cache_target_blocks(int32_t k, int64_t n);   // blocks a sample of k from n consumes (+ margin)
 
 // PER sampling: ReplayMemoryPrioritized.sample_transitions (R:dqn/replay_memory.py:69-92)
 constexpr int PER_MAX_B = 8192;     // largest global minibatch k_per_sample handles
@@ -418,6 +444,7 @@ int launch_sample_uniform(const SampleArgs& a, hipStream_t s);
 int launch_idx_to_phys(const int32_t* idx, int32_t* phys, int shard_begin, int n, dqnx_ctrl* ctrl, int64_t capacity,
                        const RelayoutArgs* rl, int rl_blocks, hipStream_t s);
 int64_t sample_setsize(int64_t k);
-int sample_hash_slots(int32_t k);
+int sample_hash_slots(int32_t k);            // hash slots of the sampler for k (LDS or global table)
+uint64_t sample_table_bytes(int32_t k);      // global scratch the sampler needs for k (0: none)
 
 }  // namespace dqnx

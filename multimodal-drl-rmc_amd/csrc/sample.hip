@@ -18,20 +18,41 @@
 // state written back equals Python's random.getstate() after the call.
 //
 // Pool branch (n <= setsize, only while the buffer is tiny): sequential on one lane.
-#include "sample_body.hpp"
+#include "sample_pipe.hpp"
 
 namespace dqnx {
 
 constexpr int SAMPLE_NT = 1024;   // threads of the sampler workgroup
+constexpr int SAMPLE_LDS_MAX_HS = 16384;      // largest LDS table of k_sample_uniform (128 KiB)
 
-template <int HS>  // hash slots (power of two)
+// k <= SAMPLE_FAST_MAX_K: the bitmap-dedup sampler (sample_pipe.hpp)
+__global__ __launch_bounds__(SAMPLE_FAST_NT) void k_sample_fast(SampleArgs a) {
+    __shared__ SampleFastUnion S;
+    if (blockIdx.x > 0) {   // spare workgroups: blocked weight copies for the fused plan
+        relayout_run(a.rl, blockIdx.x - 1, gridDim.x - 1);
+        return;
+    }
+    sample_fast_body(a, S);
+}
+
+template <int HS>  // hash slots (power of two) in LDS
 __global__ __launch_bounds__(SAMPLE_NT) void k_sample_uniform(SampleArgs a) {
     __shared__ SampleLds<SAMPLE_NT, HS> S;
     if (blockIdx.x > 0) {   // spare workgroups: blocked weight copies for the fused plan
         relayout_run(a.rl, blockIdx.x - 1, gridDim.x - 1);
         return;
     }
-    sample_uniform_body<SAMPLE_NT, HS>(a, S);
+    sample_uniform_body<SAMPLE_NT, HS>(a, S, S.tab);
+}
+
+template <int HS>  // hash slots (power of two) in global scratch (a.gtab): k beyond the LDS tables
+__global__ __launch_bounds__(SAMPLE_NT) void k_sample_uniform_g(SampleArgs a) {
+    __shared__ SampleLdsBase<SAMPLE_NT> S;
+    if (blockIdx.x > 0) {
+        relayout_run(a.rl, blockIdx.x - 1, gridDim.x - 1);
+        return;
+    }
+    sample_uniform_body<SAMPLE_NT, HS>(a, S, a.gtab);
 }
 
 
@@ -72,24 +93,77 @@ int64_t sample_setsize(int64_t k) {
     return setsize;
 }
 
-int sample_hash_slots(int32_t k) {
+// LDS table of k_sample_uniform for k (the original rule), or -1 if k needs more than 16384 slots
+static int lds_hash_slots(int32_t k) {
     // The table holds every value accepted so far plus one pass of words; the kernel caps a
     // pass at 3/4 of the table minus the accepted values, and a pass needs room for >= 1 block.
     int64_t need = 4 * ((int64_t)k + 624);   // load factor <= ~1/4 at the usual one-pass size
     int hs = 2048;
-    while (hs < need && hs < 16384) hs <<= 1;
-    if (4 * ((int64_t)k + 624) > 3 * (int64_t)hs) return -1;
+    while (hs < need && hs < SAMPLE_LDS_MAX_HS) hs <<= 1;
+    if (need > 3 * (int64_t)hs) return -1;
     return hs;
 }
 
-int launch_sample_uniform(const SampleArgs& a, hipStream_t s) {
-    const int hs = sample_hash_slots(a.k);
-    if (hs < 0) return set_error(DQNX_EUNSUPPORTED, "sample: k=%d too large for the LDS table", a.k);
-    switch (hs) {
-        case 2048: hipLaunchKernelGGL(k_sample_uniform<2048>, dim3(1 + a.rl_blocks), dim3(SAMPLE_NT), 0, s, a); break;
-        case 4096: hipLaunchKernelGGL(k_sample_uniform<4096>, dim3(1 + a.rl_blocks), dim3(SAMPLE_NT), 0, s, a); break;
-        case 8192: hipLaunchKernelGGL(k_sample_uniform<8192>, dim3(1 + a.rl_blocks), dim3(SAMPLE_NT), 0, s, a); break;
-        default: hipLaunchKernelGGL(k_sample_uniform<16384>, dim3(1 + a.rl_blocks), dim3(SAMPLE_NT), 0, s, a); break;
+// global table of k_sample_uniform_g (k beyond every LDS table)
+static int global_hash_slots(int32_t k) {
+    const int64_t need = 4 * ((int64_t)k + 624);
+    int64_t hs = 2 * SAMPLE_LDS_MAX_HS;
+    while (hs < need) hs <<= 1;
+    return hs > ((int64_t)1 << 20) ? -1 : (int)hs;   // k > ~260 K: beyond any configured minibatch
+}
+
+int sample_hash_slots(int32_t k) {
+    if (k <= SAMPLE_FAST_MAX_K) return SAMPLE_LDS_MAX_HS;
+    const int hs = lds_hash_slots(k);
+    return hs > 0 ? hs : global_hash_slots(k);
+}
+
+int mt_cache_target_blocks(int32_t k, int64_t n) {
+    if (k < SAMPLE_FAST_MIN_K || k > SAMPLE_FAST_MAX_K || n <= k) return 0;   // the fast path only
+    // the fast sampler's word estimate (sample_pipe.hpp) at population n, from a fully consumed
+    // state block; + the state block itself
+    int bits = 0;
+    while (bits < 63 && ((int64_t)1 << bits) <= n) bits++;
+    const double nf = (double)n, pf = nf / (double)((int64_t)1 << bits);
+    const double D = nf * log1p((double)k / (nf - (double)k));
+    const double words = D / pf + 8.0 * sqrt(D * (1.0 - pf)) / pf + 64.0;
+    const int b = (int)ceil(words / 624.0) + 1;
+    return b > MTC_MAX_BLOCKS ? MTC_MAX_BLOCKS : b;
+}
+
+uint64_t sample_table_bytes(int32_t k) {
+    if (k <= SAMPLE_FAST_MAX_K || lds_hash_slots(k) > 0) return 0;
+    const int hs = global_hash_slots(k);
+    return hs > 0 ? (uint64_t)hs * 8 : 0;
+}
+
+int launch_sample_uniform(const SampleArgs& a_in, hipStream_t s) {
+    SampleArgs a = a_in;
+    a.test_flags = getenv("DQNX_SAMPLER_FORCE_FALLBACK") ? 1 : 0;
+    const dim3 grid(1 + a.rl_blocks);
+    const int lhs = lds_hash_slots(a.k);
+    if (a.k <= SAMPLE_FAST_MAX_K && (a.k >= SAMPLE_FAST_MIN_K || getenv("DQNX_SAMPLER_FAST") || a.test_flags) &&
+        !getenv("DQNX_SAMPLER_OLD")) {
+        hipLaunchKernelGGL(k_sample_fast, grid, dim3(SAMPLE_FAST_NT), 0, s, a);
+    } else if (lhs > 0) {
+        switch (lhs) {
+            case 2048: hipLaunchKernelGGL(k_sample_uniform<2048>, grid, dim3(SAMPLE_NT), 0, s, a); break;
+            case 4096: hipLaunchKernelGGL(k_sample_uniform<4096>, grid, dim3(SAMPLE_NT), 0, s, a); break;
+            case 8192: hipLaunchKernelGGL(k_sample_uniform<8192>, grid, dim3(SAMPLE_NT), 0, s, a); break;
+            default: hipLaunchKernelGGL(k_sample_uniform<16384>, grid, dim3(SAMPLE_NT), 0, s, a); break;
+        }
+    } else {
+        const int ghs = global_hash_slots(a.k);
+        if (ghs < 0) return set_error(DQNX_EUNSUPPORTED, "sample: k=%d too large", a.k);
+        if (!a.gtab) return set_error(DQNX_EINVAL, "sample: k=%d needs a global table", a.k);
+        switch (ghs) {
+            case 32768: hipLaunchKernelGGL(k_sample_uniform_g<32768>, grid, dim3(SAMPLE_NT), 0, s, a); break;
+            case 65536: hipLaunchKernelGGL(k_sample_uniform_g<65536>, grid, dim3(SAMPLE_NT), 0, s, a); break;
+            case 131072: hipLaunchKernelGGL(k_sample_uniform_g<131072>, grid, dim3(SAMPLE_NT), 0, s, a); break;
+            case 262144: hipLaunchKernelGGL(k_sample_uniform_g<262144>, grid, dim3(SAMPLE_NT), 0, s, a); break;
+            case 524288: hipLaunchKernelGGL(k_sample_uniform_g<524288>, grid, dim3(SAMPLE_NT), 0, s, a); break;
+            default: hipLaunchKernelGGL(k_sample_uniform_g<1048576>, grid, dim3(SAMPLE_NT), 0, s, a); break;
+        }
     }
     DQNX_HIP_CHECK(hipGetLastError());
     return DQNX_OK;
@@ -97,10 +171,14 @@ int launch_sample_uniform(const SampleArgs& a, hipStream_t s) {
 
 }  // namespace dqnx
 
+// test-hook scratch: [n, n as the ring write pointer | MT block cache (empty) | pool | global table]
+static uint64_t hook_pool_off() { return 256 + ((uint64_t)dqnx::mt_cache_words() * 4 + 255) / 256 * 256; }
+
 extern "C" uint64_t dqnx_sample_scratch_bytes(int64_t n, int32_t k) {
     const int64_t ss = dqnx::sample_setsize(k);
     const int64_t m = n < ss ? n : ss;
-    return (uint64_t)((m + 64) * sizeof(int32_t));
+    const uint64_t pool = ((uint64_t)((m + 64) * sizeof(int32_t)) + 255) / 256 * 256;
+    return hook_pool_off() + pool + dqnx::sample_table_bytes(k);
 }
 
 extern "C" int dqnx_sample_uniform(uint32_t* mt625, int64_t n, int32_t k, int32_t* out, void* scratch,
@@ -110,13 +188,29 @@ extern "C" int dqnx_sample_uniform(uint32_t* mt625, int64_t n, int32_t k, int32_
     if (n >= (int64_t)1 << 31) return dqnx::set_error(DQNX_EUNSUPPORTED, "dqnx_sample_uniform: n >= 2^31");
     dqnx::SampleArgs a = {};
     a.state = mt625;
-    a.n_dev = nullptr;
-    a.n_val = n;
     a.k = k;
     a.setsize = dqnx::sample_setsize(k);
     a.out = out;
     a.err = err;
-    a.pool = (int32_t*)scratch;
+    char* sc = (char*)scratch;
+    {   // the population size as the device-side ring size (the samplers read it from memory)
+        const int64_t hv[2] = {n, n};
+        hipError_t e = hipMemcpyAsync(sc, hv, sizeof(hv), hipMemcpyHostToDevice, (hipStream_t)stream);
+        if (e == hipSuccess) e = hipMemsetAsync(sc + 256, 0, (size_t)dqnx::mt_cache_words() * 4, (hipStream_t)stream);
+        if (e == hipSuccess) e = hipStreamSynchronize((hipStream_t)stream);   // hv is on this stack frame
+        if (e != hipSuccess) return dqnx::set_hip_error(e, "dqnx_sample_uniform staging", __FILE__, __LINE__);
+    }
+    a.n_dev = (const int64_t*)sc;
+    a.n_val = n;
+    a.wptr_dev = (const int64_t*)sc + 1;
+    a.mtc = (uint32_t*)(sc + 256);
+    a.mtc_blocks = 0;
+    a.pool = (int32_t*)(sc + hook_pool_off());
     a.phys_out = nullptr;
+    {
+        const int64_t ss = a.setsize, m = n < ss ? n : ss;
+        const uint64_t pool = ((uint64_t)((m + 64) * sizeof(int32_t)) + 255) / 256 * 256;
+        a.gtab = dqnx::sample_table_bytes(k) ? (unsigned long long*)(sc + hook_pool_off() + pool) : nullptr;
+    }
     return dqnx::launch_sample_uniform(a, (hipStream_t)stream);
 }

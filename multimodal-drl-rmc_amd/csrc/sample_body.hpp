@@ -34,18 +34,22 @@ struct SampleShape {
     static constexpr int WPT = (624 * (1 + AHEAD) + NT - 1) / NT;
 };
 
-template <int NT, int HS>   // HS: hash slots (power of two)
-struct SampleLds {
-    unsigned long long tab[HS];
+template <int NT>
+struct SampleLdsBase {
     uint32_t blk[SampleShape<NT>::AHEAD + 1][624];   // [0] current block, [1..] twisted ahead
     int wave_tot[NT / 64];
     int s_final;
 };
+template <int NT, int HS>   // HS: hash slots (power of two) of a table in LDS
+struct SampleLds : SampleLdsBase<NT> {
+    unsigned long long tab[HS];
+};
 
+// `tab`: HS slots in LDS, or (k too large for LDS) in global memory, used by this one workgroup
 template <int NT, int HS>
-__device__ __forceinline__ void sample_uniform_body(const SampleArgs& a, SampleLds<NT, HS>& S) {
+__device__ __forceinline__ void sample_uniform_body(const SampleArgs& a, SampleLdsBase<NT>& S,
+                                                    unsigned long long* tab) {
     constexpr int NW = NT / 64, AHEAD = SampleShape<NT>::AHEAD, WPT = SampleShape<NT>::WPT;
-    unsigned long long* tab = S.tab;
     auto& blk = S.blk;
     int* wave_tot = S.wave_tot;
     int& s_final = S.s_final;
@@ -97,8 +101,13 @@ __device__ __forceinline__ void sample_uniform_body(const SampleArgs& a, SampleL
 
     // ---- set branch ----
     DQNX_STAMP(a.stamps, 1);
+    if (HS / NT <= 16) {
 #pragma unroll
-    for (int i = 0; i < HS / NT; i++) tab[tid + i * NT] = ~0ull;
+        for (int i = 0; i < HS / NT; i++) tab[tid + i * NT] = ~0ull;
+    } else {
+        for (int i = 0; i < HS / NT; i++) tab[tid + i * NT] = ~0ull;
+        __threadfence_block();
+    }
     const int bits = bit_length64((uint64_t)n);
     const uint32_t shift = 32u - (uint32_t)bits;
     const float inv_accept = (float)((double)(1ull << bits) / (double)n);   // words per valid draw
@@ -166,7 +175,10 @@ __device__ __forceinline__ void sample_uniform_body(const SampleArgs& a, SampleL
         bool first[WPT];
 #pragma unroll
         for (int u = 0; u < WPT; u++) {
-            first[u] = val[u] && (uint32_t)(tab[hv[u]] & 0xffffffffull) == spos0 + (uint32_t)(tid * m + u);
+            // (an agent-scope load: a global table's lines must come from L2, where the atomics ran)
+            const unsigned long long tv =
+                val[u] ? __hip_atomic_load(&tab[hv[u]], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
+            first[u] = val[u] && (uint32_t)(tv & 0xffffffffull) == spos0 + (uint32_t)(tid * m + u);
             cnt += first[u] ? 1 : 0;
         }
         int incl = cnt;   // wave inclusive scan

@@ -84,6 +84,7 @@ EXPORTS = [
     "dqnx_learn_kernel_count", "dqnx_learn_kernel_info", "dqnx_learn_step_timed", "dqnx_learn_step_omit", "dqnx_events_create",
     "dqnx_events_destroy", "dqnx_event_elapsed", "dqnx_debug_stamps",
     "dqnx_per_sample", "dqnx_per_update_priorities", "dqnx_set_agent_step", "dqnx_act", "dqnx_act_scratch_bytes",
+    "dqnx_params_modified",
 ]
 
 _lib = None
@@ -115,6 +116,7 @@ def lib():
         "dqnx_engine_obs_stride": ([vp, P(I32)], ctypes.c_int),
         "dqnx_engine_bind": ([vp, vp, ctypes.c_uint64], ctypes.c_int),
         "dqnx_engine_reset": ([vp, vp], ctypes.c_int),
+        "dqnx_params_modified": ([vp], ctypes.c_int),
         "dqnx_engine_set_graphs": ([vp, I32], ctypes.c_int),
         "dqnx_replay_push": ([vp, vp, vp, vp, vp, vp, I32, I32, vp], ctypes.c_int),
         "dqnx_rng_set": ([vp, I32, P(ctypes.c_uint32), vp], ctypes.c_int),

@@ -136,9 +136,10 @@ class Agent:
                                   lr=self.lr, tau=self.target_soft_update_tau, n_env=self.n_env, device=self.device,
                                   eps_dec=self.epsilon_decay,
                                   compute_dtype=os.environ.get("DQNX_COMPUTE_DTYPE", "fp32"))
-        self.online_network.bind_flat(self.engine.param_views(self.engine.params), self.engine.params, spec)
+        self.online_network.bind_flat(self.engine.param_views(self.engine.params), self.engine.params, spec,
+                                      engine=self.engine)
         self.target_network.bind_flat(self.engine.param_views(self.engine.target_params), self.engine.target_params,
-                                      spec)
+                                      spec, engine=self.engine)
         self.replay_memory_buffer = self._make_replay()
         self._learn_steps = 0          # learn() calls since the last log (throughput metric)
         self._learn_t0 = time.time()

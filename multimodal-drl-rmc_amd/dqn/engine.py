@@ -299,6 +299,13 @@ class LearnEngine:
         tsrc = state if target is None else target
         for name, v in self.param_views(self.target_params).items():
             v.copy_(tsrc[name].to(self.device, torch.float32))
+        self.params_modified()
+
+    def params_modified(self):
+        """Call after writing `params` / `target_params` (or their state_dict views) directly:
+        the next learn step rebuilds the engine's derived weight layouts (dqnx_params_modified).
+        Adam, soft / hard updates and load_params keep them current by themselves."""
+        C.check(self.L.dqnx_params_modified(self.h), "params_modified")
 
     # ---- replay ----------------------------------------------------------------------
     def push(self, obs, act, rew, done, next_obs):

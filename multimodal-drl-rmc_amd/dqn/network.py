@@ -36,6 +36,7 @@ class Network(nn.Module):
         self._act_ptrs = None       # data_ptr of every parameter when _act_flat was bound
         self._act_engine = False    # _act_flat belongs to a learn engine
         self._act_bufs = None       # (rows, desc, scratch, device obs/actions, pinned obs/actions)
+        self._engine = None         # the learn engine whose buffer holds these parameters
 
     def forward(self, s):
         raise NotImplementedError
@@ -44,7 +45,7 @@ class Network(nn.Module):
         raise NotImplementedError
 
     # -- engine binding -------------------------------------------------------------
-    def bind_flat(self, views: dict, flat=None, spec=None):
+    def bind_flat(self, views: dict, flat=None, spec=None, engine=None):
         """Move every parameter into `views[name]` (same shape, engine memory), keeping
         the Parameter objects (so `.optimizer` and module references stay valid).  With
         `flat`/`spec` (the learn engine's buffer and network description) `actions()` runs
@@ -56,6 +57,9 @@ class Network(nn.Module):
                     raise ValueError(f"{name}: engine shape {tuple(v.shape)} != {tuple(p.shape)}")
                 v.copy_(p.data.to(v.device, T.float32))
                 p.data = v
+        self._engine = engine
+        if engine is not None:
+            engine.params_modified()
         if flat is not None:
             self._act_flat, self._act_spec, self._act_engine = flat, spec, True
             self._act_ptrs = [p.data_ptr() for p in self.parameters()]
@@ -127,6 +131,12 @@ class Network(nn.Module):
         params, step, episode_count, rew_mean, len_mean = load_pack(load_path)
         self.load_state_dict({k: T.as_tensor(v, device=self.device) for k, v in params.items()})
         return step, episode_count, rew_mean, len_mean
+
+    def load_state_dict(self, state_dict, *args, **kwargs):
+        out = super().load_state_dict(state_dict, *args, **kwargs)
+        if self._engine is not None:   # written into the engine's buffer: refresh its derived layouts
+            self._engine.params_modified()
+        return out
 
 
 class DeepQNetwork(Network):

@@ -26,7 +26,11 @@ def test_gpu_sampler_matches_oracle():
     dev = torch.device("cuda")
     cases = [(50, 32), (200, 32), (4117, 1024), (4118, 1024), (10000, 1024), (100000, 4096),
              (1000000, 1024), (1000000, 8192), (16405, 4096), (16406, 4096), (7, 5), (6, 6), (1, 1),
-             (3000, 0), (999, 999)]
+             (3000, 0), (999, 999),
+             # pipelined sampler (k <= 5984): acceptance ~1/2 (two rounds), its largest k, small k
+             (524289, 4096), (524289, 5984), (1000000, 5984), (5000, 100), (2049, 600),
+             # k beyond the LDS tables: the global-memory hash table
+             (100000, 12000), (1000000, 16384)]
     for j, (n, k) in enumerate(cases):
         random.seed(1000 + j)
         st = O.py_state_to_array()
@@ -46,6 +50,15 @@ def test_gpu_sampler_matches_oracle():
             new_state = d_state.cpu().numpy().view(np.uint32)
             assert np.array_equal(new_state, want_state), (n, k, rep)
             st = want_state
+
+
+@pytest.mark.parametrize("mode", ["DQNX_SAMPLER_FORCE_FALLBACK", "DQNX_SAMPLER_OLD", "DQNX_SAMPLER_FAST"])
+def test_gpu_sampler_other_paths_match_oracle(monkeypatch, mode):
+    """The fast sampler's exact fallback (taken when a draw needs more words than the 8-sigma
+    margin provides), the multi-pass kernel alone, and the fast path below its default k range,
+    on the same cases."""
+    monkeypatch.setenv(mode, "1")
+    test_gpu_sampler_matches_oracle()
 
 
 def test_gpu_sampler_golden():
@@ -261,6 +274,58 @@ def _check_learn(oracle, eng):
         compare_state(oracle, eng, loose=loose)
         sync_oracle(oracle, eng)
     assert np.array_equal(eng.get_rng(0), oracle.py_state)
+
+
+@pytest.mark.parametrize("adam_blk", ["0", "1"])
+@pytest.mark.parametrize("compute", ["fp32", "bf16"])
+def test_gpu_weights_written_from_host_are_used(monkeypatch, compute, adam_blk):
+    """The fused plan keeps fragment-blocked weight copies current from the Adam pass; weights
+    written from the host (a checkpoint load through load_params / state_dict views, hard or
+    soft updates) must reach the next step's forward (DQNX_STEP relayout after
+    dqnx_params_modified).  Checked by loading fresh weights mid-run into engine and oracle,
+    with the copies rebuilt every step (default) and maintained by Adam (DQNX_ADAM_BLK=1)."""
+    monkeypatch.setenv("DQNX_ADAM_BLK", adam_blk)
+    o, e = make_pair("DuelingDoubleDQNAgent", 284, 256, 3000, 3000, 27)
+    if compute == "bf16":   # bf16: only that the host-written weights are the ones used
+        E = _engine_mod()
+        e = E.LearnEngine(E.mlp_spec(284, 8, "dueling"), "DuelingDoubleDQNAgent", 256, 3000, compute_dtype="bf16")
+        e.push(*O.synth_transitions(3000, 284, 8, seed=127))
+        random.seed(3)
+        e.set_rng(0, O.py_state_to_array())
+    e.load_params(O.reference_init(O.mlp_spec(284, 8, "dueling"), 27))
+    e.learn_step(soft_update=True)
+    if compute == "fp32":
+        o.train_step()
+    fresh = O.reference_init(O.mlp_spec(284, 8, "dueling"), 99)
+    e.load_params(fresh)
+    if compute == "bf16":
+        # the first forward after the load equals a forward of a fresh engine holding `fresh`
+        e2 = _engine_mod().LearnEngine(e.spec, "DuelingDoubleDQNAgent", 256, 3000, compute_dtype="bf16")
+        e2.push(*O.synth_transitions(3000, 284, 8, seed=127))
+        e2.load_params(fresh)
+        e2.set_rng(0, e.get_rng(0))
+        e.learn_step(soft_update=True)
+        e2.learn_step(soft_update=True)
+        torch.cuda.synchronize()
+        assert torch.equal(e.q, e2.q)
+        return
+    for k in o.online:
+        o.online[k].copy_(fresh[k])
+        o.target[k].copy_(fresh[k])
+    rec = o.train_step()
+    e.learn_step(soft_update=True)
+    torch.cuda.synchronize()
+    np.testing.assert_allclose(e.q[0].cpu().numpy(), rec.q_online.numpy(), atol=1e-5, rtol=0)
+    np.testing.assert_allclose(e.q[2].cpu().numpy(), rec.q_target_next.numpy(), atol=1e-5, rtol=0)
+    # a hard update (target <- online) is seen by the next step's target forward too
+    e.hard_update()
+    for k in o.online:
+        o.target[k].copy_(o.online[k])
+    sync_oracle(o, e)
+    rec = o.train_step()
+    e.learn_step(soft_update=True)
+    torch.cuda.synchronize()
+    np.testing.assert_allclose(e.q[2].cpu().numpy(), rec.q_target_next.numpy(), atol=1e-5, rtol=0)
 
 
 def test_gpu_learn_graph_and_eager_identical():

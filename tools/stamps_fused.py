@@ -45,7 +45,8 @@ for step in range(6):
         if h[j]:
             hw.append((40 + j, h[j] - prev))
             prev = h[j]
-    samp = [s[0], s[1]] + [x for x in s[2:15] if x] + [s[15]]
-    print(f"step {step}: sampler total {samp[-1] - samp[0]} cyc: {[samp[j + 1] - samp[j] for j in range(len(samp) - 1)]}")
+    ph = ["loads+clear", "cache/twist", "seen bits", "contended", "ballots", "scan", "out+cache"]
+    print(f"step {step}: sampler total {s[7] - s[0]} cyc (nb {s[8]}, cached {s[9]}): "
+          + ", ".join(f"{ph[j]} {s[j + 1] - s[j]}" for j in range(7)))
     print(f"step {step}: fwd total {prev and (max(x for x in f if x) - f[0])} cyc: {fw}")
     print(f"         head_bwd total {max(x for x in h if x) - h[0]} cyc: {hw}")
