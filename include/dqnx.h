@@ -262,8 +262,9 @@ int dqnx_hard_update(dqnx_engine* e, void* stream);
  * or NULL (receives the argmaxed values: Q, or the advantages for a dueling head).  scratch:
  * 16-byte aligned device buffer of scratch_bytes >= dqnx_act_scratch_bytes(net, n) bytes (a
  * multiple of 4), zero-filled before its first use; every call leaves it ready for the next, so
- * calls with any n up to its size may share it on one stream.  MLP nets only (DQNX_EUNSUPPORTED for two-stream nets); one launch, stream-ordered, no
- * sync. */
+ * calls with any n up to its size may share it on one stream.  MLP nets: one launch.  Two-stream
+ * nets (TwoStreamHybridNetwork, R:env/dqn_config.py:66-143): one launch per conv layer, then the
+ * dense stream + head as for an MLP on cat(flatten(conv), macro).  Stream-ordered, no sync. */
 uint64_t dqnx_act_scratch_bytes(const dqnx_net_desc* net, int32_t n);
 int dqnx_act(const dqnx_net_desc* net, const float* params, const float* obs, int32_t n, int32_t* actions,
              float* values, void* scratch, uint64_t scratch_bytes, void* stream);

@@ -2054,13 +2054,15 @@ int dqnx_hard_update(dqnx_engine* e, void* stream) {
     return DQNX_OK;
 }
 
-// acting kernel geometry of a network (host only)
+// acting kernel geometry of a network (host only).  A two-stream net acts as its convs (one
+// launch each, act_hybrid.hip) followed by the MLP acting kernel on F = cat(flatten(conv), macro).
 static int act_plan(const dqnx_net_desc* net, NetPlan& np, ActArgs& a) {
     int rc = plan_net(net, np);
     if (rc) return rc;
-    if (net->kind != DQNX_NET_MLP) return set_error(DQNX_EUNSUPPORTED, "dqnx_act: MLP networks only");
     memset(&a, 0, sizeof(a));
-    a.D = net->obs_dim; a.L = (int)np.dense.size(); a.A = net->n_actions; a.F = np.F;
+    a.D = net->kind == DQNX_NET_MLP ? net->obs_dim : np.dense[0].in;
+    a.L = (int)np.dense.size(); a.A = net->n_actions; a.F = np.F;
+    if (a.L > kActMaxDense) return set_error(DQNX_EUNSUPPORTED, "dqnx_act: more than %d dense layers", kActMaxDense);
     a.dueling = net->head == DQNX_HEAD_DUELING; a.act = net->activation;
     a.ld = std::max(a.D, a.A);
     for (int l = 0; l < a.L; l++) {
@@ -2069,14 +2071,33 @@ static int act_plan(const dqnx_net_desc* net, NetPlan& np, ActArgs& a) {
     }
     a.ld = (a.ld + 3) & ~3;   // float4 LDS rows
     a.head_off = np.head_off;
+    for (const ConvPlan& cp : np.conv) {   // each conv's row image + one channel's weights in LDS
+        ActConvArgs ca;
+        memset(&ca, 0, sizeof(ca));
+        ca.Ci = cp.Ci; ca.Hi = cp.Hi; ca.Wi = cp.Wi; ca.Ho = cp.Ho; ca.Wo = cp.Wo; ca.kh = cp.kh; ca.kw = cp.kw;
+        if (act_conv_lds_bytes(ca) > 64 * 1024)
+            return set_error(DQNX_EUNSUPPORTED, "dqnx_act: conv input %dx%dx%d too large for the acting kernel",
+                             cp.Ci, cp.Hi, cp.Wi);
+    }
     return DQNX_OK;
+}
+
+// two-stream scratch: conv outputs of every conv but the last, F [n][D]; the MLP part follows
+static uint64_t act_conv_scratch_bytes(const NetPlan& np, int n, int D) {
+    uint64_t b = 0;
+    for (size_t l = 0; l + 1 < np.conv.size(); l++)
+        b += (uint64_t)n * np.conv[l].Co * np.conv[l].Ho * np.conv[l].Wo * 4;
+    b += (uint64_t)n * D * 4;
+    return (b + 255) / 256 * 256;
 }
 
 uint64_t dqnx_act_scratch_bytes(const dqnx_net_desc* net, int32_t n) {
     NetPlan np;
     ActArgs a;
     if (act_plan(net, np, a)) return 0;
-    return act_scratch_bytes(n, a.out[0], a.ld);
+    const uint64_t mlp = act_scratch_bytes(n, a.out[0], a.ld);
+    if (!mlp) return 0;
+    return (net->kind == DQNX_NET_MLP ? 0 : act_conv_scratch_bytes(np, n, a.D)) + mlp;
 }
 
 int dqnx_act(const dqnx_net_desc* net, const float* params, const float* obs, int32_t n, int32_t* actions,
@@ -2090,19 +2111,59 @@ int dqnx_act(const dqnx_net_desc* net, const float* params, const float* obs, in
     if (n > 0 && act_rows_per_block(n, a.ld) == 0)
         return set_error(DQNX_EUNSUPPORTED, "dqnx_act: layer width %d does not fit LDS", a.ld);
     a.params = params; a.obs = obs; a.actions = actions; a.values = values; a.n = n;
-    if (n > 0) {
-        // activations from the start, tickets from the END (ticket g at bytes - 4(g+1)): a larger
-        // call's activations never reach a smaller call's tickets, so every ticket word only ever
-        // holds counts that the last arriver returns to zero, whatever n the buffer last served.
-        const int R = act_rows_per_block(n, a.ld);
-        const int64_t groups = (n + R - 1) / R;
-        if (scratch_bytes < act_scratch_bytes(n, a.out[0], a.ld) || (scratch_bytes & 3) || ((uintptr_t)scratch & 15))
-            return set_error(DQNX_EINVAL, "dqnx_act: scratch of %llu bytes too small or misaligned for n=%d",
-                             (unsigned long long)scratch_bytes, n);
-        a.scratch = (float*)scratch;
-        a.tickets = (uint32_t*)((char*)scratch + scratch_bytes) - 1;   // ticket g = tickets[-g]
+    if (n == 0) return DQNX_OK;
+    const uint64_t need = dqnx_act_scratch_bytes(net, n);
+    if (scratch_bytes < need || (scratch_bytes & 3) || ((uintptr_t)scratch & 15))
+        return set_error(DQNX_EINVAL, "dqnx_act: scratch of %llu bytes too small or misaligned for n=%d",
+                         (unsigned long long)scratch_bytes, n);
+    char* sc = (char*)scratch;
+    hipStream_t s = (hipStream_t)stream;
+    if (net->kind == DQNX_NET_TWO_STREAM) {   // the conv stack, rows' CHW images through scratch
+        const int NC = (int)np.conv.size();
+        const float* in = obs;
+        int64_t in_stride = net->obs_dim;
+        int in_off = np.macro_len;   // the micro grid viewed as (c, h, w) (R:env/dqn_config.py:126-128)
+        char* cur = sc;
+        float* F = nullptr;
+        {
+            uint64_t b = 0;
+            for (int l = 0; l + 1 < NC; l++) b += (uint64_t)n * np.conv[l].Co * np.conv[l].Ho * np.conv[l].Wo * 4;
+            F = (float*)(sc + b);
+        }
+        for (int l = 0; l < NC; l++) {
+            const ConvPlan& cp = np.conv[l];
+            ActConvArgs ca;
+            memset(&ca, 0, sizeof(ca));
+            ca.in = in; ca.in_stride = in_stride; ca.in_off = in_off;
+            ca.W = params + cp.off; ca.b = ca.W + (int64_t)cp.Co * cp.K;
+            ca.n = n; ca.Ci = cp.Ci; ca.Hi = cp.Hi; ca.Wi = cp.Wi; ca.Co = cp.Co; ca.Ho = cp.Ho; ca.Wo = cp.Wo;
+            ca.kh = cp.kh; ca.kw = cp.kw; ca.sh = cp.sh; ca.sw = cp.sw; ca.ph = cp.ph; ca.pw = cp.pw;
+            if (l + 1 < NC) {
+                ca.out = (float*)cur;
+                ca.out_stride = (int64_t)cp.Co * cp.Ho * cp.Wo;
+                cur += (uint64_t)n * ca.out_stride * 4;
+            } else {   // flatten(conv) ++ macro = the dense input F (R:env/dqn_config.py:135-138)
+                ca.out = F;
+                ca.out_stride = a.D;
+                ca.macro = obs;
+                ca.macro_stride = net->obs_dim;
+                ca.macro_len = np.macro_len;
+            }
+            rc = launch_act_conv(ca, s);
+            if (rc) return rc;
+            in = ca.out; in_stride = ca.out_stride; in_off = 0;
+        }
+        a.obs = F;
+        const uint64_t cb = act_conv_scratch_bytes(np, n, a.D);
+        sc += cb;
+        scratch_bytes -= cb;
     }
-    return launch_act(a, (hipStream_t)stream);
+    // activations from the start, tickets from the END (ticket g at bytes - 4(g+1)): a larger
+    // call's activations never reach a smaller call's tickets, so every ticket word only ever
+    // holds counts that the last arriver returns to zero, whatever n the buffer last served.
+    a.scratch = (float*)sc;
+    a.tickets = (uint32_t*)(sc + scratch_bytes) - 1;   // ticket g = tickets[-g]
+    return launch_act(a, s);
 }
 
 int dqnx_debug_stamps(dqnx_engine* e, int64_t* out64, void* stream) {

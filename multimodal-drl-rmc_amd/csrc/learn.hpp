@@ -434,6 +434,16 @@ struct ActArgs {
     int64_t off[kActMaxDense];
     int64_t head_off;
 };
+// two-stream acting: one conv layer over n rows (act_hybrid.hip); images CHW, rows strided
+struct ActConvArgs {
+    const float* in;  int64_t in_stride;  int in_off;    // input image of row r: in + r*in_stride + in_off
+    const float* W;   const float* b;                    // [Co][Ci][kh][kw], [Co]
+    float* out;       int64_t out_stride; int out_off;   // output [Co][Ho][Wo] of row r
+    const float* macro; int64_t macro_stride; int macro_len;   // last conv: copy macro features after its output
+    int n, Ci, Hi, Wi, Co, Ho, Wo, kh, kw, sh, sw, ph, pw;
+};
+size_t act_conv_lds_bytes(const ActConvArgs& a);
+int launch_act_conv(const ActConvArgs& a, hipStream_t s);
 int act_rows_per_block(int n, int ld);
 uint64_t act_scratch_bytes(int n, int h0, int ld);
 int launch_act(const ActArgs& a, hipStream_t s);

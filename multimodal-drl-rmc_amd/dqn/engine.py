@@ -165,16 +165,21 @@ def act_scratch(spec: NetSpec, n: int, device) -> torch.Tensor:
     return torch.zeros((nbytes + 15) // 16 * 4, dtype=torch.float32, device=device)
 
 
+def act_supported(spec: NetSpec) -> bool:
+    """dqnx_act implements this network (MLP bodies; two-stream bodies whose conv inputs fit the
+    acting kernel's LDS, e.g. the reference's 2x27x5 grid but not the 4x84x84 variant)."""
+    return int(C.lib().dqnx_act_scratch_bytes(ctypes.byref(spec.to_c()), 1)) > 0
+
+
 def act(spec: NetSpec, flat: torch.Tensor, obs: torch.Tensor, values: Optional[torch.Tensor] = None,
         scratch: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None, desc=None) -> torch.Tensor:
-    """Greedy actions of an MLP Q-network, one HIP launch (`dqnx_act`).
+    """Greedy actions of a Q-network on the GPU (`dqnx_act`: one launch for an MLP, the conv
+    launches + the MLP kernel for a two-stream net).
 
     `flat`: the network's flat fp32 parameters on the GPU (dqnx_net_param_info layout);
     `obs`: [n, obs_dim] on the same GPU.  Returns int32 actions [n] (first maximal index, like
     torch.argmax) of Q, or of the advantage stream for a dueling head (R:dqn/network.py:67-74,
     110-117).  `values`, if given ([n, n_actions] fp32), receives the argmaxed values."""
-    if spec.kind != C.DQNX_NET_MLP:
-        raise NotImplementedError("dqnx_act: MLP networks only")
     obs = obs.to(flat.device, torch.float32).contiguous()
     if obs.dim() != 2 or obs.shape[1] != spec.obs_dim:
         raise ValueError(f"obs must be [n, {spec.obs_dim}], got {tuple(obs.shape)}")

@@ -17,7 +17,7 @@ import torch as T
 import torch.nn as nn
 
 from .engine import act as _act_native
-from .engine import act_scratch
+from .engine import act_scratch, act_supported
 from .engine import spec_from_body
 from .utils.pack import load_pack, save_pack
 
@@ -95,13 +95,21 @@ class Network(nn.Module):
         T.cuda.current_stream(flat.device).synchronize()
         return h_act[:n].tolist()
 
+    def _body_obs_dim(self):
+        if isinstance(self.net, nn.Sequential):
+            return self.net[0].in_features
+        c, h, w = (int(x) for x in self.net.micro_shape)   # TwoStreamHybridNetwork
+        return int(self.net.macro_len) + c * h * w
+
     def _native_act(self):
-        """(spec, flat) for the acting kernel, or None when the reference's torch forward is
-        the path: a CPU device (the caller asked for CPU) or a two-stream body (dqnx_act
-        covers MLP bodies)."""
-        if T.device(self.device).type != "cuda" or not isinstance(self.net, nn.Sequential):
+        """(spec, flat) for the acting kernels, or None when the reference's torch forward is
+        the path: a CPU device (the caller asked for CPU) or a body outside the two families
+        the engine implements."""
+        if T.device(self.device).type != "cuda":
             return None
         if self._act_flat is not None:
+            if not act_supported(self._act_spec):
+                return None
             if [p.data_ptr() for p in self.parameters()] == self._act_ptrs:
                 return self._act_spec, self._act_flat
             if self._act_engine:
@@ -109,9 +117,11 @@ class Network(nn.Module):
         # standalone network (e.g. Observe): pack its parameters into one flat buffer once.  A
         # body outside the two reference families keeps the reference's torch forward.
         try:
-            spec = spec_from_body(self.net, self.net[0].in_features, self._act_head_dim(),
+            spec = spec_from_body(self.net, self._body_obs_dim(), self._act_head_dim(),
                                   dueling=hasattr(self, "fc_adv"))
-        except (NotImplementedError, AttributeError):
+        except (NotImplementedError, AttributeError, TypeError, IndexError):
+            return None
+        if not act_supported(spec):
             return None
         n, layout = spec.param_infos()
         dev = next(self.parameters()).device

@@ -143,7 +143,9 @@ def test_act_argument_checks_without_gpu():
     L = C.lib()
     hyb = _engine_spec(O.hybrid_spec(8, "dueling")).to_c()
     mlp = E.mlp_spec(284, 8, "dueling").to_c()
-    assert L.dqnx_act(ctypes.byref(hyb), 16, 16, 1, 16, None, 16, 1 << 20, None) == C.DQNX_EUNSUPPORTED
+    need_h = L.dqnx_act_scratch_bytes(ctypes.byref(hyb), 1)
+    assert need_h > 0   # two-stream nets act too (conv launches + the MLP acting kernel)
+    assert L.dqnx_act(ctypes.byref(hyb), 16, 16, 1, 16, None, 16, need_h - 4, None) == C.DQNX_EINVAL
     assert L.dqnx_act(ctypes.byref(mlp), None, None, 4, None, None, None, 0, None) == C.DQNX_EINVAL
     assert L.dqnx_act(ctypes.byref(mlp), None, None, 0, None, None, None, 0, None) == C.DQNX_OK
     need = L.dqnx_act_scratch_bytes(ctypes.byref(mlp), 3)

@@ -86,10 +86,47 @@ def test_gpu_act_shared_scratch_across_row_counts():
         _check(vals.cpu().numpy(), ref, acts.cpu().numpy())
 
 
-def test_gpu_act_rejects_two_stream():
-    spec = E.hybrid_spec()
-    with pytest.raises(NotImplementedError):
-        E.act(spec, torch.zeros(10, device="cuda"), torch.zeros(1, spec.obs_dim, device="cuda"))
+@pytest.mark.parametrize("head", ["dueling", "linear"])
+@pytest.mark.parametrize("n", [1, 2, 3, 8, 37])
+def test_gpu_act_two_stream_matches_oracle(head, n):
+    """The reference's HEAD network (TwoStreamHybridNetwork on the 2x27x5 grid, R:env/dqn_config.py
+    :66-193): conv launches + the MLP acting kernel on cat(flatten(conv3), macro)."""
+    ospec = O.hybrid_spec(8, head)
+    params = O.reference_init(ospec, 7)
+    espec = E.hybrid_spec(8, head)
+    flat = _flat(espec, params)
+    x = torch.from_numpy(O.synth_transitions(n, ospec.obs_dim, 8, seed=n)[0])
+    vals = torch.empty(n, 8, dtype=torch.float32, device="cuda")
+    acts = E.act(espec, flat, x.cuda(), vals)
+    torch.cuda.synchronize()
+    with torch.no_grad():
+        ref = (O.advantages(ospec, params, x) if head == "dueling" else O.q_forward(ospec, params, x)).numpy()
+    _check(vals.cpu().numpy(), ref, acts.cpu().numpy())
+
+
+def test_gpu_act_two_stream_84_falls_back():
+    """The (4,84,84) variant's conv input does not fit the acting kernel: dqnx_act refuses it and
+    Network.actions keeps the torch forward."""
+    spec = E.hybrid_spec(micro_chw=(4, 84, 84))
+    assert not E.act_supported(spec)
+    assert E.act_supported(E.hybrid_spec())
+
+
+@pytest.mark.parametrize("cls", [DeepQNetwork, DuelingDeepQNetwork])
+def test_gpu_standalone_two_stream_network_actions(cls):
+    """Observe-style use of the HEAD net: a standalone two-stream network acts through dqnx_act."""
+    from refnets import hybrid_network_config
+    torch.manual_seed(5)
+    net = cls("cuda:0", 1e-4, hybrid_network_config, Box(284), 8)
+    x = O.synth_transitions(6, 284, 8, seed=2)[0]
+    xt = torch.from_numpy(x).cuda()
+    assert net._native_act() is not None
+    with torch.no_grad():
+        q = (net.advantages(xt) if cls is DuelingDeepQNetwork else net(xt)).cpu().numpy()
+    got = net.actions(x)
+    srt = np.sort(q, axis=1)
+    clear = (srt[:, -1] - srt[:, -2]) > 1e-4
+    assert np.array_equal(np.asarray(got)[clear], q.argmax(1)[clear])
 
 
 @pytest.mark.parametrize("cls", [DeepQNetwork, DuelingDeepQNetwork])

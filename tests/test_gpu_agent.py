@@ -127,3 +127,42 @@ def test_gpu_per_agent_step_survives_host_sampling(tmp_path):
     torch.cuda.synchronize()
     beta = float(agent.engine.ctrl().per_beta)
     assert abs(beta - float(np.interp(8, [0, 2e6], [0.4, 1.0]))) < 1e-12, beta
+
+
+def test_gpu_agent_drives_gymnasium_env_through_adapter(tmp_path):
+    """R:train.py's init_replay_memory_buffer + train_loop over dqn.env_adapter.GymnasiumVecEnv
+    (gymnasium 5-tuple envs): the replay ring holds exactly the transitions the
+    env produced (reset observations in new_obs at episode ends, as DummyVecEnv stores them), and
+    finished episodes reach the agent's episode buffer."""
+    from dqn.env_adapter import GymnasiumVecEnv
+    from test_env_adapter import ToyEnv
+
+    class Env284(ToyEnv):
+        def __init__(self):
+            super().__init__(length=5, dim=14)
+
+    env = GymnasiumVecEnv([Env284])
+    agent = Agents.DuelingDoubleDQNAgent(**agent_kwargs("DuelingDoubleDQNAgent", 14, 8, 100, tmp_path))
+    seen = []
+    obses = env.reset()
+    for t in range(12):                                # init_replay_memory_buffer (R:train.py:63-81)
+        actions = [t % 8]
+        new_obses, rews, dones, infos = env.step(actions)
+        agent.store_transitions(obses, actions, rews, dones, new_obses, infos)
+        seen.append((obses[0].copy(), actions[0], float(rews[0]), bool(dones[0]), new_obses[0].copy()))
+        obses = new_obses
+    for step in range(3):                              # train_loop (R:train.py:83-108)
+        agent.step = step
+        actions = agent.choose_actions(obses)
+        new_obses, rews, dones, infos = env.step(actions)
+        agent.store_transitions(obses, actions, rews, dones, new_obses, infos)
+        seen.append((obses[0].copy(), int(actions[0]), float(rews[0]), bool(dones[0]), new_obses[0].copy()))
+        obses = new_obses
+        agent.learn()
+        agent.update_target_network()
+    ring = agent.replay_memory_buffer.replay_buffer
+    assert len(ring) == len(seen)
+    for i, (o, a, r, d, no) in enumerate(seen):
+        ro, ra, rr, rd, rno = ring[i]
+        assert np.array_equal(ro, o) and ra == a and rr == np.float32(r) and rd == d and np.array_equal(rno, no), i
+    assert agent.episode_count == sum(1 for s in seen if s[3])
