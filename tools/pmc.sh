@@ -10,7 +10,7 @@ while read -r grp; do
   [ -z "$grp" ] && continue
   i=$((i+1))
   timeout -s KILL ${PMC_TIMEOUT:-90} rocprofv3 --pmc $grp --output-format csv -d $OUT/p$i -o run -- \
-     python bench.py --steps 50 --warmup 5 --no-cpu-baseline --no-kernel-timing ${BENCH_ARGS:-} > $OUT/p$i.json 2> $OUT/p$i.err
+     python bench.py --steps 50 --warmup 5 --no-cpu-baseline --no-kernel-timing --no-extras ${BENCH_ARGS:-} > $OUT/p$i.json 2> $OUT/p$i.err
   rc=$?; echo "pass $i ($grp) rc=$rc"
   if [ $rc -ge 124 ]; then exit $rc; fi
 done < ${PMC_GROUPS:-tools/pmc_groups.txt}

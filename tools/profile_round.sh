@@ -13,6 +13,6 @@ cp $OUT/pmc_traffic_${NET}_b${B}${TAG}.json profiles/pmc_traffic_${NET}_b${B}${T
 rm -rf gpurun_out/pmc
 timeout -k 10 300 python bench.py ${BENCH_ARGS:-} > $OUT/bench.json 2> $OUT/bench.err || exit $?
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- \
-    python bench.py --steps 200 --warmup 20 --no-cpu-baseline ${BENCH_ARGS:-} > $OUT/prof_bench.json 2> $OUT/prof_bench.err || exit $?
+    python bench.py --steps 200 --warmup 20 --no-cpu-baseline --no-extras ${BENCH_ARGS:-} > $OUT/prof_bench.json 2> $OUT/prof_bench.err || exit $?
 cat $OUT/bench.json
 echo done
