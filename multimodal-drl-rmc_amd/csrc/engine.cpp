@@ -167,6 +167,186 @@ static bool fwd_big_mode() {
 
 static inline uint64_t align_up(uint64_t x, uint64_t a) { return (x + a - 1) / a * a; }
 
+// ---- implicit-GEMM conv geometry (conv_ig.hip) ----
+// Row tile of TR class rows (full width) on a BM-row workgroup tile: the BM of 256 / 128 / 64
+// wasting the fewest padded rows, the larger on ties ((4,84,84) convs 1/2: 3 x 84 rows on 256;
+// conv 3: 3 x 42 on 128; conv 3's data-gradient phases: 3 x 21 on 64 -- all 98.4 % full).
+static bool cig_tile(int Hq, int Wq, int& BM, int& TR) {
+    double best = 0;
+    BM = 0;
+    for (int bm : {256, 128, 64}) {
+        int tr = bm / Wq;
+        if (tr < 1) continue;
+        tr = std::min(tr, Hq);
+        const int tiles = (Hq + tr - 1) / tr;
+        const double eff = (double)Hq * Wq / ((double)tiles * bm);
+        if (eff > best + 0.01) { best = eff; BM = bm; TR = tr; }
+    }
+    return BM > 0;
+}
+
+// channels staged per pass: all of them when the band stays <= 50 KB (fewer restages), else
+// 32 or 16; LDS floats per pixel CB + 4 (16-byte aligned rows for the float4 stage / b128 reads)
+// a band must fit the kernels' staging registers: 256 threads x NQ float4 (NHWC sources) or
+// x 4*NQ floats (CHW sources)
+// (lines of one band row / one channel row, dealt round-robin to the 4 waves: conv_ig.hip)
+static bool cig_stage_fits(int NR, int WP, int CB, bool vec) {
+    constexpr int NQ = 12, NQS = 12;   // conv_ig.hip: float4 / floats per thread
+    if (vec) return (int64_t)NR * ((WP * (CB / 4) + 63) / 64) <= 4 * NQ;
+    return (int64_t)CB * NR * ((WP + 63) / 64) <= 4 * NQS;
+}
+static int cig_cb(int C, int NR, int WP, bool vec) {
+    if (C == 4) return 4;
+    for (int cb : {64, 32})
+        if (C % cb == 0 && (size_t)NR * WP * (cb + 4) * 4 <= 50 * 1024 && cig_stage_fits(NR, WP, cb, vec)) return cb;
+    return 16;
+}
+static int cig_cs(int CB) { return CB == 4 ? 4 : CB + 4; }
+
+// forward of conv cp: one class, band = the input rows of TR output rows
+static bool cig_fwd_geom(const ConvPlan& cp, int Bl, bool first, ConvIgArgs& a) {
+    memset(&a, 0, sizeof(a));
+    if (!cig_tile(cp.Ho, cp.Wo, a.BM, a.TR)) return false;
+    if (!conv_ig_supported(cp.Co, a.BM, cp.Ci)) return false;
+    a.Bl = Bl;
+    a.nclass = 1;
+    a.RM = cp.sh;
+    a.CM = cp.sw;
+    a.WP = (cp.Wo - 1) * cp.sw + cp.kw;
+    a.NR = (a.TR - 1) * cp.sh + cp.kh;
+    a.N = cp.Co;
+    const bool vec = cp.Ci != 4 && !first;   // the first conv stages CHW ring rows
+    a.CB = cig_cb(cp.Ci, a.NR, a.WP, vec);
+    a.CS = cig_cs(a.CB);
+    if (!cig_stage_fits(a.NR, a.WP, a.CB, vec)) return false;
+    CigClass& k = a.cls[0];
+    k.Hq = cp.Ho;
+    k.Wq = cp.Wo;
+    k.tiles = (cp.Ho + a.TR - 1) / a.TR;
+    k.ntaps = cp.kh * cp.kw;
+    k.rmin = -cp.ph;
+    k.cmin = -cp.pw;
+    k.ni = cp.kh; k.nj = cp.kw; k.i0 = k.j0 = 0; k.di = k.dj = 1; k.kw = cp.kw;
+    k.o0 = 0; k.oi = a.WP; k.oj = 1;
+    a.maxtiles = k.tiles;
+    a.Kw = cp.kh * cp.kw * cp.Ci;
+    a.ymul = a.xmul = 1;
+    if (const char* v = getenv("DQNX_CIG_EXP")) a.exp = atoi(v);
+    a.src.H = cp.Hi;
+    a.src.W = cp.Wi;
+    a.src.C = cp.Ci;
+    return conv_ig_lds_bytes(a) <= 64 * 1024;
+}
+
+// data gradient of conv cp (into the previous conv's NHWC dZ): one class per output phase
+// (a, c): taps i = i0 + ii*sh with (a + ph - i) % sh == 0 read dZ row yq + (a + ph - i)/sh, i.e.
+// band row ni-1-ii above the class origin; columns alike
+static bool cig_dx_geom(const ConvPlan& cp, int Bl, bool last, ConvIgArgs& a) {
+    memset(&a, 0, sizeof(a));
+    if (cp.sh * cp.sw > 4 || cp.Co % 16) return false;
+    const int Hq0 = (cp.Hi + cp.sh - 1) / cp.sh, Wq0 = (cp.Wi + cp.sw - 1) / cp.sw;
+    if (!cig_tile(Hq0, Wq0, a.BM, a.TR)) return false;
+    if (!conv_ig_supported(cp.Ci, a.BM, cp.Co)) return false;
+    a.Bl = Bl;
+    a.RM = a.CM = 1;
+    int nr = 0, wp = 0;
+    for (int pa = 0; pa < cp.sh; pa++)
+        for (int pc = 0; pc < cp.sw; pc++) {
+            const int Hq = (cp.Hi - pa + cp.sh - 1) / cp.sh, Wq = (cp.Wi - pc + cp.sw - 1) / cp.sw;
+            if (Hq <= 0 || Wq <= 0) continue;
+            CigClass& k = a.cls[a.nclass++];
+            k.a = pa;
+            k.c = pc;
+            k.Hq = Hq;
+            k.Wq = Wq;
+            k.tiles = (Hq + a.TR - 1) / a.TR;
+            k.i0 = ((pa + cp.ph) % cp.sh);
+            k.j0 = ((pc + cp.pw) % cp.sw);
+            k.ni = k.i0 < cp.kh ? (cp.kh - 1 - k.i0) / cp.sh + 1 : 0;
+            k.nj = k.j0 < cp.kw ? (cp.kw - 1 - k.j0) / cp.sw + 1 : 0;
+            k.di = cp.sh; k.dj = cp.sw; k.kw = cp.kw;
+            k.ntaps = k.ni * k.nj;
+            // source row of tap ii: yq + (pa + ph - i0)/sh - ii; the band starts at its minimum
+            const int rtop = (pa + cp.ph - k.i0) / cp.sh, ctop = (pc + cp.pw - k.j0) / cp.sw;
+            k.rmin = k.ni ? rtop - (k.ni - 1) : 0;
+            k.cmin = k.nj ? ctop - (k.nj - 1) : 0;
+            nr = std::max(nr, a.TR + std::max(k.ni, 1) - 1);
+            wp = std::max(wp, Wq + std::max(k.nj, 1) - 1);
+            a.maxtiles = std::max(a.maxtiles, k.tiles);
+        }
+    a.NR = nr;
+    a.WP = wp;
+    for (int q = 0; q < a.nclass; q++) {
+        CigClass& k = a.cls[q];
+        k.o0 = (std::max(k.ni, 1) - 1) * a.WP + std::max(k.nj, 1) - 1;
+        k.oi = -a.WP;
+        k.oj = -1;
+    }
+    a.N = cp.Ci;
+    (void)last;                                 // every dZ source is NHWC (the last conv's via k_unflatten_tiled)
+    a.CB = cig_cb(cp.Co, a.NR, a.WP, true);
+    a.CS = cig_cs(a.CB);
+    if (!cig_stage_fits(a.NR, a.WP, a.CB, true)) return false;
+    a.Kw = cp.kh * cp.kw * cp.Co;
+    a.ymul = cp.sh;
+    a.xmul = cp.sw;
+    if (const char* v = getenv("DQNX_CIG_EXP")) a.exp = atoi(v);
+    a.src.H = cp.Ho;
+    a.src.W = cp.Wo;
+    a.src.C = cp.Co;
+    a.nstreams = 1;
+    return conv_ig_lds_bytes(a) <= 64 * 1024;
+}
+
+// weight gradient of conv cp: row groups of RB output rows (X band <= 64 KB, pixel chunks as
+// full as possible), slices of gps groups sized for ~512 workgroups over the channel blocks
+static bool cig_dw_geom(const ConvPlan& cp, int Bl, bool first, ConvDwIgArgs& d) {
+    memset(&d, 0, sizeof(d));
+    d.Bl = Bl; d.Ho = cp.Ho; d.Wo = cp.Wo;
+    d.Co = cp.Co; d.C = cp.Ci; d.CB = cp.Ci == 4 ? 4 : 16;
+    d.CS = cp.Ci == 4 ? 5 : 20;
+    d.ntaps = cp.kh * cp.kw; d.kw = cp.kw;
+    d.sh = cp.sh; d.sw = cp.sw; d.ph = cp.ph; d.pw = cp.pw;
+    d.K = cp.K;
+    d.TN = (d.ntaps * d.CB + 15) / 16;
+    if ((d.Co != 32 && d.Co != 64) || (d.TN != 3 && d.TN != 9) || d.C % d.CB) return false;
+    d.WP = (cp.Wo - 1) * cp.sw + cp.kw;
+    double best = 0;
+    for (int rb = 8; rb >= 1; rb--) {
+        const int nr = (rb - 1) * cp.sh + cp.kh;
+        if ((size_t)nr * d.WP * d.CS * 4 > 64 * 1024 || rb > cp.Ho || !cig_stage_fits(nr, d.WP, d.CB, !first)) continue;
+        const int G = (cp.Ho + rb - 1) / rb;
+        // useful pixels over MFMA pixel slots (16-pixel chunks per group)
+        const double slots = (double)(G - 1) * ((rb * cp.Wo + 15) / 16 * 16) + ((cp.Ho - (G - 1) * rb) * cp.Wo + 15) / 16 * 16;
+        const double eff = (double)cp.Ho * cp.Wo / slots;
+        if (eff > best + 0.005) { best = eff; d.RB = rb; d.NR = nr; }
+    }
+    if (!d.RB) return false;
+    d.G = (cp.Ho + d.RB - 1) / d.RB;
+    const int groups = Bl * d.G, ncb = d.C / d.CB;
+    const int target = std::max(1, std::min(groups, 512 / ncb));
+    d.gps = (groups + target - 1) / target;
+    d.slices = (groups + d.gps - 1) / d.gps;
+    d.pstride = (int64_t)cp.Co * cp.K + cp.Co;
+    return conv_dw_ig_lds_bytes(d) <= 64 * 1024;
+}
+
+// implicit-GEMM convs for every conv of a large micro grid (DQNX_CONV_IG=0: explicit path)
+static bool conv_ig_plan(const NetPlan& np, int Bl) {
+    if (np.conv.empty()) return false;
+    const char* v = getenv("DQNX_CONV_IG");
+    if (v && atoi(v) == 0) return false;
+    if ((int64_t)np.conv[0].Hi * np.conv[0].Wi < 1024) return false;   // the (2,27,5) grid keeps the explicit kernels
+    for (size_t l = 0; l < np.conv.size(); l++) {
+        ConvIgArgs f;
+        ConvDwIgArgs d;
+        const bool first = l == 0, last = l + 1 == np.conv.size();
+        if (!cig_fwd_geom(np.conv[l], Bl, first, f) || !cig_dw_geom(np.conv[l], Bl, first, d)) return false;
+        if (l > 0 && !cig_dx_geom(np.conv[l], Bl, last, f)) return false;
+    }
+    return true;
+}
+
 struct KStep {
     std::string name;
     double flops = 0, bytes = 0;
@@ -199,6 +379,10 @@ struct dqnx_engine {
     std::vector<uint64_t> ws_col, ws_Hc, ws_dZc, ws_cpart;
     std::vector<int> cslices, ckslice;
     uint64_t ws_F = 0, ws_dF = 0, ws_dcol = 0;
+    // implicit-GEMM convs (conv_ig.hip): no column matrices; permuted weight copies per conv
+    // ([co][tap][ci] online / target, [ci][tap][co] online), the last conv writes F directly
+    bool conv_ig = false;
+    std::vector<uint64_t> ws_wperm0, ws_wperm1, ws_wpermT;
     int stage_rows = 0;
     char* arena = nullptr;
     int64_t ring_size = 0, ring_wptr = 0;   // host mirror of the ring state (pushes are host-driven)
@@ -321,19 +505,28 @@ int layout(dqnx_engine* e) {
     e->ws_dZc.assign(NC, 0);
     e->ws_cpart.assign(NC, 0);
     uint64_t dcol_max = 0;
+    e->ws_wperm0.assign(NC, 0);
+    e->ws_wperm1.assign(NC, 0);
+    e->ws_wpermT.assign(NC, 0);
     for (int l = 0; l < NC; l++) {
         const ConvPlan& cp = np.conv[l];
         const uint64_t M = (uint64_t)e->Bl * cp.Ho * cp.Wo;
-        e->ws_col[l] = sub(3 * M * cp.Kstride * 4);
-        e->ws_Hc[l] = sub(3 * M * cp.Co * 4);
+        const bool last = l == NC - 1;
+        if (!e->conv_ig) e->ws_col[l] = sub(3 * M * cp.Kstride * 4);
+        if (!(e->conv_ig && last)) e->ws_Hc[l] = sub(3 * M * cp.Co * 4);   // the implicit path's last conv writes F
         e->ws_dZc[l] = sub(M * cp.Co * 4);
         e->ws_cpart[l] = sub((uint64_t)e->cslices[l] * ((uint64_t)cp.Co * cp.K + cp.Co) * 4);
-        if (l > 0 && M * cp.K * 4 > dcol_max) dcol_max = M * cp.K * 4;
+        if (!e->conv_ig && l > 0 && M * cp.K * 4 > dcol_max) dcol_max = M * cp.K * 4;
+        if (e->conv_ig) {
+            e->ws_wperm0[l] = sub((uint64_t)cp.Co * cp.K * 4);
+            e->ws_wperm1[l] = sub((uint64_t)cp.Co * cp.K * 4);
+            if (l > 0) e->ws_wpermT[l] = sub((uint64_t)cp.Co * cp.K * 4);
+        }
     }
     if (NC) {
         e->ws_F = sub((uint64_t)3 * e->Bl * np.strideF * 4);
         e->ws_dF = sub((uint64_t)e->Bl * np.dense[0].in * 4);
-        e->ws_dcol = sub(dcol_max);
+        if (dcol_max) e->ws_dcol = sub(dcol_max);
     }
     cur = align_up(cur, 256);
     e->bytes[DQNX_BUF_WORKSPACE] = cur - e->off[DQNX_BUF_WORKSPACE];
@@ -868,6 +1061,86 @@ std::vector<KStep> build_learn_steps(dqnx_engine* e, int key) {
     const int NC = (int)np.conv.size();
     const float* ring_obs = at<float>(e, e->off[DQNX_BUF_RING_OBS]);
     const float* ring_next = at<float>(e, e->off[DQNX_BUF_RING_NEXT_OBS]);
+    if (NC && e->conv_ig) {   // 2a'. implicit-GEMM convs, the last one writing F (conv_ig.hip)
+        ConvPermArgs pa;
+        memset(&pa, 0, sizeof(pa));
+        double pbytes = 0;
+        for (int l = 0; l < NC; l++) {
+            const ConvPlan& cp = np.conv[l];
+            const int taps = cp.kh * cp.kw;
+            pa.job[pa.njobs++] = ConvPermJob{params + cp.off, at<float>(e, e->ws_wperm0[l]), cp.Co, cp.Ci, taps, 0};
+            pa.job[pa.njobs++] = ConvPermJob{tparams + cp.off, at<float>(e, e->ws_wperm1[l]), cp.Co, cp.Ci, taps, 0};
+            if (l > 0) pa.job[pa.njobs++] = ConvPermJob{params + cp.off, at<float>(e, e->ws_wpermT[l]), cp.Co, cp.Ci, taps, 1};
+            pbytes += 8.0 * cp.Co * cp.K * (l > 0 ? 3 : 2);
+        }
+        {
+            KStep k;
+            k.name = "conv_perm";
+            k.bytes = pbytes;
+            k.run = [=](hipStream_t s) { return launch_conv_perm(pa, s); };
+            ks.push_back(k);
+        }
+        for (int l = 0; l < NC; l++) {
+            const ConvPlan cp = np.conv[l];
+            const bool last = l == NC - 1;
+            ConvIgArgs ca;
+            cig_fwd_geom(cp, e->Bl, l == 0, ca);
+            ca.act = act;
+            CigSource& S = ca.src;
+            if (l == 0) {   // the micro grid straight from the ring rows (CHW after the macro features)
+                S.phys = phys;
+                S.bstride = e->stride;
+                S.off = np.macro_len;
+                S.pstride = 1;
+                S.cstride = cp.Hi * cp.Wi;
+            } else {
+                S.bstride = (int64_t)cp.Hi * cp.Wi * cp.Ci;
+                S.pstride = cp.Ci;
+                S.cstride = 1;
+            }
+            int z = 0;
+            for (int st = 0; st < 3; st++) {
+                if (st == 1 && !dbl) continue;
+                S.base[z] = l == 0 ? (st == 0 ? ring_obs : ring_next)
+                                   : at<float>(e, e->ws_Hc[l - 1]) + (int64_t)st * e->Bl * cp.Hi * cp.Wi * cp.Ci;
+                ca.W[z] = at<float>(e, st == 2 ? e->ws_wperm1[l] : e->ws_wperm0[l]);
+                ca.bias[z] = (st == 2 ? tparams : params) + cp.off + (int64_t)cp.Co * cp.K;
+                if (last) {
+                    ca.out[z] = at<float>(e, e->ws_F) + (int64_t)st * e->Bl * np.strideF;
+                    ca.ring[z] = st == 0 ? ring_obs : ring_next;
+                } else {
+                    ca.out[z] = at<float>(e, e->ws_Hc[l]) + (int64_t)st * e->Bl * cp.Ho * cp.Wo * cp.Co;
+                }
+                z++;
+            }
+            ca.nstreams = z;
+            if (last) {   // F[b] = cat(flatten_CHW(conv), macro) (R:env/dqn_config.py:135-138)
+                ca.ob = np.strideF;
+                ca.orow = cp.Wo;
+                ca.opix = 1;
+                ca.och = cp.Ho * cp.Wo;
+                ca.phys = phys;
+                ca.ring_stride = e->stride;
+                ca.macro_len = np.macro_len;
+                ca.flat_cols = cp.Co * cp.Ho * cp.Wo;
+                ca.strideF = np.strideF;
+            } else {
+                ca.ob = (int64_t)cp.Ho * cp.Wo * cp.Co;
+                ca.orow = cp.Wo * cp.Co;
+                ca.opix = cp.Co;
+                ca.och = 1;
+            }
+            const double M = (double)e->Bl * cp.Ho * cp.Wo;
+            KStep k;
+            k.name = "conv_fwd_c" + std::to_string(l + 1);
+            k.flops = 2.0 * nstreams * M * cp.Co * cp.K;
+            k.bytes = 4.0 * (nstreams * (Bl * (double)cp.Ci * cp.Hi * cp.Wi + M * cp.Co) + 2.0 * cp.Co * (cp.K + 1.0));
+            const int epi = last ? CIG_EPI_FLAT : CIG_EPI_NHWC;
+            k.run = [=](hipStream_t s) { return launch_conv_ig(ca, epi, s); };
+            ks.push_back(k);
+        }
+    }
+    if (!e->conv_ig) {
     // 2a. two-stream micro CNN (R:env/dqn_config.py:92-101, forward :126-133): im2col + MFMA GEMM
     for (int l = 0; l < NC; l++) {
         const ConvPlan cp = np.conv[l];
@@ -953,6 +1226,7 @@ std::vector<KStep> build_learn_steps(dqnx_engine* e, int key) {
         k.bytes = 4.0 * nstreams * Bl * 2.0 * np.strideF;
         k.run = [=](hipStream_t s) { return launch_flatten_concat(fl, s); };
         ks.push_back(k);
+    }
     }
     for (int l = 0; l < L; l++) {
         const LayerPlan lp = np.dense[l];
@@ -1142,8 +1416,87 @@ std::vector<KStep> build_learn_steps(dqnx_engine* e, int key) {
         ks.push_back(k);
     }
 
+    // 4b'. implicit-GEMM conv backward, last conv first: dW (+ db) slabs, then the data gradient
+    //      with the previous conv's activation derivative in its epilogue
+    if (NC && e->conv_ig) {
+        for (int l = NC - 1; l >= 0; l--) {
+            const ConvPlan cp = np.conv[l];
+            const bool last = l == NC - 1;
+            const double M = (double)e->Bl * cp.Ho * cp.Wo;
+            // this conv's dZ (NHWC): for the last conv dF (CHW-flatten rows, masked by the dense
+            // layer's dx role) transposed, else what the next conv's data gradient wrote
+            if (last) {
+                UnflattenArgs ua;
+                ua.dF = at<float>(e, e->ws_dF);
+                ua.ldf = np.dense[0].in;
+                ua.dZ = at<float>(e, e->ws_dZc[l]);
+                ua.Bl = e->Bl;
+                ua.C = cp.Co; ua.Ho = cp.Ho; ua.Wo = cp.Wo;
+                KStep k;
+                k.name = "unflatten";
+                k.bytes = 8.0 * M * cp.Co;
+                k.run = [=](hipStream_t s) { return launch_unflatten_tiled(ua, s); };
+                ks.push_back(k);
+            }
+            const float* dZ = at<float>(e, e->ws_dZc[l]);
+            const int64_t dzb = (int64_t)cp.Ho * cp.Wo * cp.Co;
+            const int dzp = cp.Co, dzc = 1;
+            ConvDwIgArgs d;
+            cig_dw_geom(cp, e->Bl, l == 0, d);
+            CigSource& X = d.X;
+            X.H = cp.Hi; X.W = cp.Wi; X.C = cp.Ci;
+            if (l == 0) {
+                X.base[0] = ring_obs;
+                X.phys = phys;
+                X.bstride = e->stride;
+                X.off = np.macro_len;
+                X.pstride = 1;
+                X.cstride = cp.Hi * cp.Wi;
+            } else {
+                X.base[0] = at<float>(e, e->ws_Hc[l - 1]);   // stream 0
+                X.bstride = (int64_t)cp.Hi * cp.Wi * cp.Ci;
+                X.pstride = cp.Ci;
+                X.cstride = 1;
+            }
+            d.dZ = dZ;
+            d.dzb = dzb;
+            d.dzp = dzp;
+            d.dzc = dzc;
+            d.partial = at<float>(e, e->ws_cpart[l]);
+            {
+                KStep k;
+                k.name = "conv_dw_c" + std::to_string(l + 1);
+                k.flops = 2.0 * M * cp.Co * (cp.K + 1.0);
+                k.bytes = 4.0 * (M * cp.Co + Bl * (double)cp.Ci * cp.Hi * cp.Wi + (double)d.slices * d.pstride);
+                k.run = [=](hipStream_t s) { return launch_conv_dw_ig(d, s); };
+                ks.push_back(k);
+            }
+            if (l == 0) continue;
+            const ConvPlan pp = np.conv[l - 1];
+            ConvIgArgs ca;
+            cig_dx_geom(cp, e->Bl, last, ca);
+            ca.act = act;
+            ca.src.base[0] = dZ;
+            ca.src.bstride = dzb;
+            ca.src.pstride = dzp;
+            ca.src.cstride = dzc;
+            ca.W[0] = at<float>(e, e->ws_wpermT[l]);
+            ca.out[0] = at<float>(e, e->ws_dZc[l - 1]);
+            ca.Hprev = at<float>(e, e->ws_Hc[l - 1]);   // stream 0
+            ca.ob = (int64_t)pp.Ho * pp.Wo * pp.Co;
+            ca.orow = pp.Wo * pp.Co;
+            ca.opix = pp.Co;
+            ca.och = 1;
+            KStep k;
+            k.name = "conv_dx_c" + std::to_string(l + 1);
+            k.flops = 2.0 * M * cp.Co * cp.K;
+            k.bytes = 4.0 * (M * cp.Co + 2.0 * Bl * pp.Ho * pp.Wo * pp.Co + (double)cp.Co * cp.K);
+            k.run = [=](hipStream_t s) { return launch_conv_ig(ca, CIG_EPI_DX, s); };
+            ks.push_back(k);
+        }
+    }
     // 4b. micro CNN backward: unflatten dF, then per conv (last first) dW + dX columns, col2im
-    if (NC) {
+    if (NC && !e->conv_ig) {
         {
             const ConvPlan cl = np.conv[NC - 1];
             UnflattenArgs ua;
@@ -1595,6 +1948,7 @@ int dqnx_engine_create(const dqnx_config* cfg, dqnx_engine** out) {
     const int NC = (int)e->np.conv.size();
     e->cslices.assign(NC, 1);
     e->ckslice.assign(NC, 1);
+    e->conv_ig = conv_ig_plan(e->np, e->Bl);
     // conv dW workgroups to aim for: the (4,84,84) conv 1 ([32 x 37] tile grid 2 x 1) had only
     // 64 workgroups at the old 32-slice cap; DQNX_CONV_DW_WGS=0 restores that rule
     int dw_wgs = 1024;
@@ -1613,6 +1967,11 @@ int dqnx_engine_create(const dqnx_config* cfg, dqnx_engine** out) {
         S = (rows + ks - 1) / ks;
         e->cslices[l] = S;
         e->ckslice[l] = ks;
+        if (e->conv_ig) {   // slices of output row groups (k_conv_dw_ig)
+            ConvDwIgArgs d;
+            cig_dw_geom(cq, e->Bl, l == 0, d);
+            e->cslices[l] = d.slices;
+        }
         if (e->np.conv[l].Co % 4) { delete e; return set_error(DQNX_EUNSUPPORTED, "conv channels must be multiples of 4"); }
     }
     layout(e);

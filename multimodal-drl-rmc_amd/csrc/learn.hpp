@@ -394,6 +394,84 @@ int launch_head_bwd(const HeadBwdArgs& a, int act, hipStream_t s);
 void dw_bf16_grid(BwdArgs& a);                               // 64x64 tiles of k_dw_bf16
 int launch_dw_bf16(const BwdArgs& a, hipStream_t s);          // bf16 split-K weight gradients
 
+// ---- implicit-GEMM convolutions (conv_ig.hip): the (4,84,84) variant's convs without
+//      materialised column matrices ----
+// One output class of a conv GEMM: the forward has one; the data gradient of a strided conv has
+// one per (row, column) phase (sub-pixel decomposition), each with its own tap subset.
+struct CigClass {
+    int a, c;                 // output image offsets: y = ymul * yq + a, x = xmul * xq + c
+    int Hq, Wq, tiles;        // class grid, row tiles of TR class rows
+    int ntaps;                // = ni * nj
+    int rmin, cmin;           // band origin relative to (yq * RM, xq * CM) in source pixels
+    // tap (ii, jj) of the ni x nj tap grid: weight tap (i0 + ii*di) * kw + (j0 + jj*dj), at LDS
+    // pixel offset o0 + ii*oi + jj*oj inside the band (uniform integer math, no table loads)
+    int ni, nj, i0, j0, di, dj, kw;
+    int o0, oi, oj;
+};
+// A staged image: element (b, r, w, ch) at base[z] + (phys ? phys[b] : b) * bstride + off
+// + (r * W + w) * pstride + ch * cstride (NHWC: pstride = C, cstride = 1; CHW: pstride = 1).
+struct CigSource {
+    const float* base[3];
+    const int32_t* phys;
+    int64_t bstride, off;
+    int pstride, cstride;
+    int H, W, C;
+};
+enum { CIG_EPI_NHWC = 0, CIG_EPI_FLAT = 1, CIG_EPI_DX = 2 };
+struct ConvIgArgs {
+    int nstreams, Bl, nclass, maxtiles;
+    int TR, RM, CM, NR, WP;   // tile = TR class rows; band NR x WP source pixels
+    int BM, act;              // tile rows (64 / 128 / 256; TR * Wq <= BM), activation
+    int exp;                  // DQNX_CIG_EXP timing experiments (wrong results): 1 no band staging,
+                              // 2 no weight loads, 4 no epilogue stores, 8 no MFMA
+    int N, CB, CS;            // GEMM columns, channels staged per pass, LDS floats per pixel
+    CigSource src;
+    CigClass cls[4];
+    const float* W[3];        // permuted weights [N][kh*kw][C] per stream
+    int Kw;                   // = kh*kw*C
+    const float* bias[3];     // forward only
+    float* out[3];            // element (b, y, x, n) at out + b*ob + y*orow + x*opix + n*och
+    int64_t ob;
+    int ymul, xmul, orow, opix, och;
+    const float* Hprev;       // DX: the previous conv's activation output, same layout as out
+    // FLAT: F row tail cat(..., macro) + zero padding, written by each image's tile-0 workgroup
+    const float* ring[3];
+    const int32_t* phys;
+    int64_t ring_stride;
+    int macro_len, flat_cols, strideF;
+};
+size_t conv_ig_lds_bytes(const ConvIgArgs& a);
+bool conv_ig_supported(int N, int BM, int C);
+int launch_conv_ig(const ConvIgArgs& a, int epi, hipStream_t s);
+// conv dW + db over slices of output row groups: partial[s] = [dZ^T X | dZ^T 1] in torch order
+struct ConvDwIgArgs {
+    int Bl, Ho, Wo, RB, G, gps, slices;   // RB output rows per group, G groups per image, gps groups per slice
+    int Co, C, CB, CS, ntaps, kw, sh, sw, ph, pw, NR, WP;
+    int TN;                   // column tiles: 16 * TN >= ntaps * CB
+    CigSource X;              // stream-0 conv input
+    const float* dZ;          // element (b, p, co) at dZ + b*dzb + p*dzp + co*dzc
+    int64_t dzb;
+    int dzp, dzc;
+    float* partial;
+    int64_t pstride;
+    int K;                    // C * kh * kw
+};
+size_t conv_dw_ig_lds_bytes(const ConvDwIgArgs& a);
+int launch_conv_dw_ig(const ConvDwIgArgs& a, hipStream_t s);
+// weight relayouts for the implicit convs: mode 0 [co][ci][t] -> [co][t][ci] (forward),
+// mode 1 -> [ci][t][co] (data gradient)
+struct ConvPermJob {
+    const float* src;
+    float* dst;
+    int Co, Ci, taps, mode;
+};
+struct ConvPermArgs {
+    int njobs;
+    ConvPermJob job[12];
+};
+int launch_conv_perm(const ConvPermArgs& a, hipStream_t s);
+int launch_unflatten_tiled(const UnflattenArgs& a, hipStream_t s);
+
 int launch_im2col(const Im2colArgs& a, hipStream_t s);
 int launch_flatten_concat(const FlattenArgs& a, hipStream_t s);
 int launch_unflatten(const UnflattenArgs& a, hipStream_t s);

@@ -98,18 +98,21 @@ def test_gpu_hybrid_learn_golden():
         np.testing.assert_allclose(got, ref, atol=1e-5, rtol=0, err_msg=k)
 
 
-@pytest.mark.parametrize("batch,fwd_big", [(64, "1"), (128, "1"), (128, "0")])
-def test_gpu_hybrid84_learn_matches_oracle(monkeypatch, batch, fwd_big):
-    """The stacked (4,84,84) variant (BASELINE configs[2]): exercises the LDS band im2col
-    (convs 1-2), the 128x128 split-K forward of the 56,462-wide dense layer and its ordered reduce.
-    B=128 takes the kernel routes of the B=256 bench: conv 2 and conv 3 (882*B >= 65,536 rows)
-    on the 64x128 k_conv_dw_big tiles; with DQNX_FWD_BIG=0 the conv dX runs as the split
-    conv_dxs level beside the big dW.  Tolerances are those of the (2,27,5) cases, with the
+@pytest.mark.parametrize("batch,fwd_big,conv_ig", [(64, "1", "1"), (128, "1", "1"), (128, "1", "0"), (128, "0", "0")])
+def test_gpu_hybrid84_learn_matches_oracle(monkeypatch, batch, fwd_big, conv_ig):
+    """The stacked (4,84,84) variant (BASELINE configs[2]).  conv_ig=1 (the default): the
+    implicit-GEMM convs of conv_ig.hip (forward with F written by the last conv, phase-split data
+    gradients, row-group dW slabs) and the 128x128 split-K forward of the 56,462-wide dense layer.
+    conv_ig=0: the explicit path -- LDS band im2col (convs 1-2), conv GEMMs, col2im; B=128 takes
+    the kernel routes of the B=256 bench: conv 2 and conv 3 (882*B >= 65,536 rows) on the 64x128
+    k_conv_dw_big tiles; with DQNX_FWD_BIG=0 the conv dX runs as the split conv_dxs level beside
+    the big dW.  Tolerances are those of the (2,27,5) cases, with the
     gradient check scale-relative (the 56,462-term sums differ from torch's CPU order by a few
     ulps of the largest terms)."""
     E = _E()
     from parity import assert_grad_close
     monkeypatch.setenv("DQNX_FWD_BIG", fwd_big)
+    monkeypatch.setenv("DQNX_CONV_IG", conv_ig)
     algo, cap, n_fill, seed = "DuelingDoubleDQNAgent", 200, 150, 8
     ospec = O.hybrid_spec(8, "dueling", micro_chw=(4, 84, 84))
     init = O.reference_init(ospec, seed)

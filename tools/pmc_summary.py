@@ -1,27 +1,36 @@
-"""Summarise rocprofv3 --pmc passes (tools/pmc.sh): mean counter value per dispatch for each
-libdqnx kernel, plus its VGPR / AGPR / LDS / scratch allocation."""
+"""Per-kernel averages of rocprofv3 --pmc counters (any groups), keyed by kernel name and grid
+size (launches of one template at different shapes stay apart).
+usage: python tools/pmc_summary.py gpurun_out/pmcX [filter-substring]"""
 import csv
 import glob
 import os
+import re
 import sys
 from collections import defaultdict
 
-root = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/pmc"
-vals = defaultdict(list)
-info = {}
-for f in sorted(glob.glob(os.path.join(root, "**", "*counter_collection.csv"), recursive=True)):
-    for row in csv.DictReader(open(f)):
-        k = row["Kernel_Name"]
-        if "dqnx" not in k or "push" in k:
-            continue
-        name = k.split("(")[0].replace("void ", "").replace("dqnx::", "")
-        vals[(name, row["Counter_Name"])].append(float(row["Counter_Value"]))
-        info[name] = (row["VGPR_Count"], row["Accum_VGPR_Count"], row["SGPR_Count"], row["LDS_Block_Size"],
-                      row["Scratch_Size"], row["Grid_Size"], row["Workgroup_Size"])
-names = sorted({n for n, _ in vals})
-for n in names:
-    v, a, sg, lds, scr, grid, wg = info[n]
-    print(f"{n}: vgpr {v} agpr {a} sgpr {sg} lds {lds} scratch {scr} grid {grid} wg {wg}")
-    for (nn, c), xs in sorted(vals.items()):
-        if nn == n:
-            print(f"    {c:32s} {sum(xs) / len(xs):14.1f}  (n={len(xs)})")
+
+def short(name):
+    name = re.sub(r"\(.*$", "", name)
+    return name.replace("dqnx::", "").replace("(anonymous namespace)::", "")
+
+
+def main(root, filt=""):
+    vals = defaultdict(lambda: defaultdict(list))
+    for f in glob.glob(os.path.join(root, "**", "*counter_collection.csv"), recursive=True):
+        for r in csv.DictReader(open(f)):
+            kn = r.get("Kernel_Name", "")
+            if filt and filt not in kn:
+                continue
+            key = (short(kn), r.get("Grid_Size", r.get("Grid_Size_X", "")))
+            vals[key][r["Counter_Name"]].append(float(r["Counter_Value"]))
+    for key in sorted(vals):
+        cs = vals[key]
+        n = max(len(v) for v in cs.values())
+        print(f"{key[0]}  grid={key[1]}  dispatches~{n}")
+        for c in sorted(cs):
+            v = cs[c]
+            print(f"    {c:32s} {sum(v) / len(v):16.1f}")
+
+
+if __name__ == "__main__":
+    main(sys.argv[1], sys.argv[2] if len(sys.argv) > 2 else "")
