@@ -149,7 +149,7 @@ __global__ __launch_bounds__(256, 2) void k_conv_ig(ConvIgArgs a) {
     const int total = a.nstreams * a.nclass * per_cls;
     const int C = a.src.C, CB = C4 ? 4 : a.CB;
     const int ncb = C / CB;
-    const float4* band4 = reinterpret_cast<const float4*>(band);
+    const floatx4* band4 = reinterpret_cast<const floatx4*>(band);   // native vectors: one ds_read_b128
     const int CS4 = a.CS >> 2;
     const bool relu = a.act == DQNX_ACT_RELU;
 
@@ -219,15 +219,15 @@ __global__ __launch_bounds__(256, 2) void k_conv_ig(ConvIgArgs a) {
         // pixels its B operand, so a lane's accumulator holds 4 consecutive channels of one pixel
         // (acc[tm][tn][r] = channel (wn*TN + tn)*16 + 4g + r of pixel (wm*TM + tm)*16 + i16):
         // NHWC outputs leave as float4 stores
-        auto mma = [&](const float4 (&av)[TM], const float4 (&bq)[TN]) {
+        auto mma = [&](const floatx4 (&av)[TM], const float4 (&bq)[TN]) {
 #pragma unroll
             for (int tm = 0; tm < TM; tm++)
 #pragma unroll
                 for (int tn = 0; tn < TN; tn++) {
-                    acc[tm][tn] = mfma16x16x4(bq[tn].x, av[tm].x, acc[tm][tn]);
-                    acc[tm][tn] = mfma16x16x4(bq[tn].y, av[tm].y, acc[tm][tn]);
-                    acc[tm][tn] = mfma16x16x4(bq[tn].z, av[tm].z, acc[tm][tn]);
-                    acc[tm][tn] = mfma16x16x4(bq[tn].w, av[tm].w, acc[tm][tn]);
+                    acc[tm][tn] = mfma16x16x4(bq[tn].x, av[tm][0], acc[tm][tn]);
+                    acc[tm][tn] = mfma16x16x4(bq[tn].y, av[tm][1], acc[tm][tn]);
+                    acc[tm][tn] = mfma16x16x4(bq[tn].z, av[tm][2], acc[tm][tn]);
+                    acc[tm][tn] = mfma16x16x4(bq[tn].w, av[tm][3], acc[tm][tn]);
                 }
         };
         const int ntaps = K.ntaps;
@@ -272,12 +272,12 @@ __global__ __launch_bounds__(256, 2) void k_conv_ig(ConvIgArgs a) {
             // keep the prefetch at the top of the chunk: under register pressure the scheduler
             // otherwise sinks it below the MFMAs, exposing the L2 latency at every chunk
             __builtin_amdgcn_sched_barrier(0);
-            float4 av[TM];
+            floatx4 av[TM];
 #pragma unroll
             for (int tm = 0; tm < TM; tm++) av[tm] = band4[ppos4[tm] + aoff4];
             if (a.exp & 8) {
 #pragma unroll
-                for (int tm = 0; tm < TM; tm++) acc[tm][0][0] += av[tm].x + cur[0].y;
+                for (int tm = 0; tm < TM; tm++) acc[tm][0][0] += av[tm][0] + cur[0].y;
             } else {
                 mma(av, cur);
             }

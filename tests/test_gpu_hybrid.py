@@ -20,15 +20,15 @@ def _E():
     return E
 
 
-def make_hybrid_pair(algo, batch, cap, n_fill, seed, graphs=True):
+def make_hybrid_pair(algo, batch, cap, n_fill, seed, graphs=True, micro_chw=(2, 27, 5)):
     E = _E()
     head = O.algo_spec_head(algo)
-    ospec = O.hybrid_spec(8, head)
+    ospec = O.hybrid_spec(8, head, micro_chw=micro_chw)
     init = O.reference_init(ospec, seed)
     oracle = O.OracleLearner(ospec, algo, batch, cap, seed=seed, params=init, per_pow="cr")
     data = O.synth_transitions(n_fill, ospec.obs_dim, 8, seed=seed + 100)
     O.fill_replay(oracle, *data)
-    eng = E.LearnEngine(E.hybrid_spec(8, head), algo, batch, cap, graphs=graphs)
+    eng = E.LearnEngine(E.hybrid_spec(8, head, micro_chw=micro_chw), algo, batch, cap, graphs=graphs)
     eng.load_params(init)
     eng.push(*data)
     random.seed(seed + 7)
@@ -142,3 +142,36 @@ def test_gpu_hybrid84_learn_matches_oracle(monkeypatch, batch, fwd_big, conv_ig)
         on = eng.param_views(eng.params)
         for k in oracle.online:
             np.testing.assert_allclose(on[k].cpu().numpy(), oracle.online[k].numpy(), atol=1e-5, rtol=0, err_msg=k)
+
+
+@pytest.mark.parametrize("algo,batch,seed", [("DQNAgent", 32, 21), ("PerDuelingDoubleDQNAgent", 32, 22),
+                                             ("DoubleDQNAgent", 48, 23)])
+def test_gpu_hybrid84_implicit_convs_all_algorithms(algo, batch, seed):
+    """The implicit-GEMM conv path (conv_ig.hip) under every algorithm: two forward streams
+    (DQNAgent: online(s), target(s')), the linear head, PER (IS weights through the conv
+    backward), a batch that is no multiple of the row tiles."""
+    from parity import assert_grad_close
+    from test_gpu_engine import compare_state
+    cap, n_fill = 200, 150
+    oracle, eng = make_hybrid_pair(algo, batch, cap, n_fill, seed, micro_chw=(4, 84, 84))
+    per = algo.startswith("Per")
+    loose = {k: torch.zeros_like(v, dtype=torch.bool) for k, v in oracle.online.items()}
+    for step in range(2):
+        rec = oracle.train_step()
+        eng.learn_step(soft_update=True)
+        torch.cuda.synchronize()
+        eng.check_device_error()
+        idx = eng.batch_idx.cpu().numpy().astype(np.int64) + (cap - 1 if per else 0)
+        assert np.array_equal(idx, rec.positions), f"step {step}: sampled indices differ"
+        q = eng.q.cpu()
+        np.testing.assert_allclose(q[0].numpy(), rec.q_online.numpy(), atol=1e-5, rtol=1e-5)
+        np.testing.assert_allclose(q[2].numpy(), rec.q_target_next.numpy(), atol=1e-5, rtol=1e-5)
+        assert abs(eng.loss() - rec.loss) <= 1e-5 * max(1.0, abs(rec.loss))
+        g = eng.param_views(eng.grads[:-1])
+        for k, ref in rec.grads.items():
+            got = g[k].cpu()
+            assert_grad_close(got, ref, k)
+            loose[k] |= (got - ref).abs() > 1e-3 * ref.abs()
+        # weights at 1e-5, except (capped, counted) entries whose gradient differed by > 0.1 %
+        # (Adam's lr * g / |g| step, see test_gpu_engine.compare_state)
+        compare_state(oracle, eng, loose=loose)

@@ -10,7 +10,7 @@ from collections import defaultdict
 
 
 def short(name):
-    name = re.sub(r"\(.*$", "", name)
+    name = re.sub(r"\(dqnx::[A-Za-z]*Args\).*$", "", name).replace("void ", "")
     return name.replace("dqnx::", "").replace("(anonymous namespace)::", "")
 
 
