@@ -167,6 +167,9 @@ static bool fwd_big_mode() {
 
 static inline uint64_t align_up(uint64_t x, uint64_t a) { return (x + a - 1) / a * a; }
 
+// head split-K slabs padded to 4 floats, so every slab stride allows the float4 Adam pass
+static inline int64_t head_pstride(const NetPlan& np) { return (int64_t)align_up((uint64_t)np.head_params, 4); }
+
 // ---- implicit-GEMM conv geometry (conv_ig.hip) ----
 // Row tile of TR class rows (full width) on a BM-row workgroup tile: the BM of 256 / 128 / 64
 // wasting the fewest padded rows, the larger on ties ((4,84,84) convs 1/2: 3 x 84 rows on 256;
@@ -474,7 +477,7 @@ int layout(dqnx_engine* e) {
         const uint64_t lp = (uint64_t)np.dense[l].out * np.dense[l].in + np.dense[l].out;
         e->ws_part[l] = sub((uint64_t)e->slices[l] * lp * 4);
     }
-    e->ws_head_part = sub((uint64_t)e->slices[L - 1] * np.head_params * 4);
+    e->ws_head_part = sub((uint64_t)e->slices[L - 1] * head_pstride(np) * 4);
     e->ws_dhead = sub((uint64_t)e->Bl * 16 * 4);
     e->ws_raw = sub((uint64_t)3 * e->Bl * 16 * 4);
     e->ws_trans = sub((uint64_t)e->Bl * 16);
@@ -684,7 +687,7 @@ KStep adam_kstep(dqnx_engine* e, int flags) {
         AdamSegment& sg = aa.seg[aa.nseg++];
         sg.off = np.head_off;
         sg.partial = at<float>(e, e->ws_head_part);
-        sg.pstride = np.head_params;
+        sg.pstride = head_pstride(np);
         sg.S = e->slices[L - 1];
         part_elems += (double)sg.S * sg.pstride;
     }
@@ -949,7 +952,7 @@ void build_fused_steps(dqnx_engine* e, int flags, int32_t* idx, int32_t* phys, s
             h.in = np.F;
             h.out = np.NH;
             h.partial = at<float>(e, e->ws_head_part);
-            h.pstride = np.head_params;
+            h.pstride = head_pstride(np);
             h.head_kind = c.net.head;
             h.A = A;
             flops += 2.0 * Bl * np.NH * (np.F + 1.0);
@@ -1401,7 +1404,7 @@ std::vector<KStep> build_learn_steps(dqnx_engine* e, int key) {
             h.in = np.F;
             h.out = np.NH;
             h.partial = at<float>(e, e->ws_head_part);
-            h.pstride = np.head_params;
+            h.pstride = head_pstride(np);
             h.head_kind = c.net.head;
             h.A = A;
             flops += 2.0 * Bl * np.NH * (np.F + 1.0);

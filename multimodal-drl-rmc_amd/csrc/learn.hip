@@ -702,11 +702,12 @@ __global__ __launch_bounds__(256) void k_adam(AdamArgs a) {
         if (a.mode == 2) {
             gsum = a.grads[e];
         } else {
-            int sgi = 0;
+            // the element's segment by static-index selects (a kernel-argument array indexed by a
+            // per-lane value would be copied to scratch)
+            AdamSegment sg = a.seg[0];
 #pragma unroll
             for (int q = 1; q < kMaxSeg; q++)
-                if (q < a.nseg && e >= a.seg[q].off) sgi = q;
-            const AdamSegment sg = a.seg[sgi];
+                if (q < a.nseg && e >= a.seg[q].off) sg = a.seg[q];
             const float* pp = sg.partial + (e - sg.off);
             float pv[8];
 #pragma unroll
@@ -737,7 +738,7 @@ __global__ __launch_bounds__(256) void k_adam(AdamArgs a) {
         if (a.soft) a.target[e] = tg;
 #pragma unroll
         for (int l = 0; l < 3; l++) {   // the blocked copies of a dense-layer weight
-            if (l >= a.nblk) break;
+            if (l >= a.nblk) continue;
             const AdamArgs::BlkLayer& L = a.blk[l];
             const int64_t le64 = e - L.woff;
             if (le64 < 0 || le64 >= (int64_t)L.out * L.in) continue;
@@ -762,6 +763,102 @@ __global__ __launch_bounds__(256) void k_adam(AdamArgs a) {
         if (threadIdx.x == 0) {
             const float loss = s / (float)a.batch_global;
             a.grads[P] = loss;     // all-reduced with the gradient under DP
+            a.ctrl->loss = loss;
+        }
+    }
+    if (a.mode == 2 && blockIdx.x == 0 && threadIdx.x == 0) a.ctrl->loss = a.grads[P];
+}
+
+// k_adam on float4s: every segment offset / slab stride a multiple of 4 and no blocked copies
+// (launch_adam checks); 4 consecutive elements per thread per pass, so a thread keeps 4x the
+// bytes in flight of the scalar kernel (the (4,84,84) variant updates 29 M parameters).  The
+// same per-element arithmetic, the same fixed slab order.
+__global__ __launch_bounds__(256) void k_adam4(AdamArgs a) {
+    if (a.mtc && blockIdx.x == gridDim.x - 1) {
+        mt_cache_extend(a.mtc, a.mtc_blocks);
+        return;
+    }
+    const int64_t P = a.n_params, P4 = (P + 3) >> 2;
+    const int64_t stride = (int64_t)(gridDim.x - (a.mtc ? 1 : 0)) * blockDim.x;
+    float step_size = 0.f, bc2s = 1.f;
+    if (a.mode != 0) {
+        step_size = a.ctrl->adam_step_size;
+        bc2s = a.ctrl->adam_bc2_sqrt;
+    }
+    for (int64_t e4 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e4 < P4; e4 += stride) {
+        const int64_t e = e4 << 2;
+        const int nv = (int)min((int64_t)4, P - e);   // 4 except in the last vector
+        float4 m = make_float4(0.f, 0.f, 0.f, 0.f), v = m, p = m, tg = m, g = m;
+        auto ld = [&](const float* base) {   // the last vector may be partial (no dynamic indexing)
+            if (nv == 4) return ld4(base + e);
+            return make_float4(base[e], nv > 1 ? base[e + 1] : 0.f, nv > 2 ? base[e + 2] : 0.f, 0.f);
+        };
+        auto st = [&](float* base, const float4& x) {
+            if (nv == 4) {
+                *reinterpret_cast<float4*>(base + e) = x;
+                return;
+            }
+            base[e] = x.x;
+            if (nv > 1) base[e + 1] = x.y;
+            if (nv > 2) base[e + 2] = x.z;
+        };
+        if (a.mode != 0) {
+            m = ld(a.m);
+            v = ld(a.v);
+            p = ld(a.p);
+            if (a.soft) tg = ld(a.target);
+        }
+        if (a.mode == 2) {
+            g = ld(a.grads);
+        } else {
+            AdamSegment sg = a.seg[0];
+#pragma unroll
+            for (int q = 1; q < kMaxSeg; q++)
+                if (q < a.nseg && e >= a.seg[q].off) sg = a.seg[q];
+            const float* pp = sg.partial + (e - sg.off) - e;   // ld() adds e back
+            float4 pv[4];
+            for (int u0 = 0; u0 < sg.S; u0 += 4) {   // 4 slabs in flight per round trip
+#pragma unroll
+                for (int u = 0; u < 4; u++)
+                    pv[u] = (u0 + u < sg.S) ? ld(pp + (int64_t)(u0 + u) * sg.pstride) : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+                for (int u = 0; u < 4; u++) {
+                    if (u0 + u >= sg.S) break;
+                    if (u0 + u == 0) {
+                        g = pv[0];
+                    } else {
+                        g.x += pv[u].x; g.y += pv[u].y; g.z += pv[u].z; g.w += pv[u].w;
+                    }
+                }
+            }
+            st(a.grads, g);
+        }
+        if (a.mode == 0) continue;
+        auto upd = [&](float& mk, float& vk, float& pk, float& tk, float gk) {
+            mk = fmaf(a.w1, gk - mk, mk);
+            vk = vk * a.beta2;
+            vk = vk + (a.c2 * gk) * gk;
+            const float denom = sqrtf(vk) / bc2s + a.eps;
+            pk = pk + (step_size * mk) / denom;
+            if (a.soft) tk = a.tau * pk + a.one_minus_tau * tk;
+        };
+        upd(m.x, v.x, p.x, tg.x, g.x);
+        upd(m.y, v.y, p.y, tg.y, g.y);
+        upd(m.z, v.z, p.z, tg.z, g.z);
+        upd(m.w, v.w, p.w, tg.w, g.w);
+        st(a.m, m);
+        st(a.v, v);
+        st(a.p, p);
+        if (a.soft) st(a.target, tg);
+    }
+    if (a.mode != 2 && blockIdx.x == 0 && threadIdx.x < 64 && a.loss_partial) {   // one wave, fixed order
+        float s = 0.f;
+        for (int j = threadIdx.x; j < a.n_loss_partial; j += 64) s += a.loss_partial[j];
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) s += __shfl_xor(s, o);
+        if (threadIdx.x == 0) {
+            const float loss = s / (float)a.batch_global;
+            a.grads[P] = loss;
             a.ctrl->loss = loss;
         }
     }
@@ -925,12 +1022,28 @@ int launch_head(const HeadArgs& a, int act, hipStream_t s) {
     return DQNX_OK;
 }
 
+// the float4 kernel when every segment is 4-aligned (offsets, slab strides, pointers) and no
+// blocked copies ride along; DQNX_ADAM_VEC=0 keeps the scalar kernel
+static bool adam_vec_ok(const AdamArgs& a) {
+    if (const char* v = getenv("DQNX_ADAM_VEC"))
+        if (atoi(v) == 0) return false;
+    if (a.nblk) return false;
+    auto al = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
+    if (!al(a.p) || !al(a.m) || !al(a.v) || !al(a.grads) || (a.target && !al(a.target))) return false;
+    for (int i = 0; i < a.nseg; i++)
+        if (a.seg[i].off % 4 || (a.mode != 2 && (a.seg[i].pstride % 4 || !al(a.seg[i].partial)))) return false;
+    return true;
+}
+
 int launch_adam(const AdamArgs& a, hipStream_t s) {
-    int blocks = (int)((a.n_params + 255) / 256);
+    const bool vec = adam_vec_ok(a);
+    const int64_t items = vec ? (a.n_params + 3) / 4 : a.n_params;
+    int blocks = (int)((items + 255) / 256);
     if (blocks > 2048) blocks = 2048;
     if (blocks < 1) blocks = 1;
     if (a.mtc) blocks++;   // + the sampler-cache workgroup
-    hipLaunchKernelGGL(k_adam, dim3(blocks), dim3(256), 0, s, a);
+    if (vec) hipLaunchKernelGGL(k_adam4, dim3(blocks), dim3(256), 0, s, a);
+    else hipLaunchKernelGGL(k_adam, dim3(blocks), dim3(256), 0, s, a);
     DQNX_HIP_CHECK(hipGetLastError());
     return DQNX_OK;
 }
