@@ -61,7 +61,7 @@ struct StageRegs {
     float4 v[VEC ? NQ : 1];
     float f[VEC ? 1 : NQS];
 
-    __device__ __forceinline__ void load(const CigSource& S, const Stage& st, int NR, int WP, int CB) {
+    __device__ __forceinline__ void load(const CigSource& S, const Stage& st, int NR, int WP, int CB, int RS = 1) {
         const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
         if (VEC) {
             const int q4s = CB == 64 ? 4 : CB == 32 ? 3 : CB == 16 ? 2 : (CB == 8 ? 1 : 0);   // log2(CB / 4)
@@ -74,7 +74,7 @@ struct StageRegs {
                 const int rr = li / lpr, h = li - rr * lpr;
                 const int j = 64 * h + lane;
                 const int cc = j >> q4s, q = j & ((1 << q4s) - 1);
-                const int r = st.r0 + rr, w = st.c0 + cc;
+                const int r = st.r0 + rr * RS, w = st.c0 + cc;
                 v[u] = make_float4(0.f, 0.f, 0.f, 0.f);
                 if (li < nlines && j < per_line && r >= 0 && r < S.H && w >= 0 && w < S.W)
                     v[u] = ld4(st.srcb + (int64_t)(r * S.W + w) * S.pstride + st.ch0 + 4 * q);
@@ -88,7 +88,7 @@ struct StageRegs {
                 const int ch = li / (NR * lpr), rem = li - ch * (NR * lpr);
                 const int rr = rem / lpr, h = rem - rr * lpr;
                 const int cc = 64 * h + lane;
-                const int r = st.r0 + rr, w = st.c0 + cc;
+                const int r = st.r0 + rr * RS, w = st.c0 + cc;
                 f[u] = 0.f;
                 if (li < nlines && cc < WP && r >= 0 && r < S.H && w >= 0 && w < S.W)
                     f[u] = st.srcb[(int64_t)(r * S.W + w) * S.pstride + (int64_t)(st.ch0 + ch) * S.cstride];
@@ -169,17 +169,20 @@ __global__ __launch_bounds__(256, 2) void k_conv_ig(ConvIgArgs a) {
         }
         return T;
     };
-    auto stage_of = [&](int T, int cbk) {
+    const int ngrp = a.ngrp, nstage = ncb * ngrp;   // stage s = (channel block, row group)
+    auto stage_of = [&](int T, int s) {
         int z, cl, b, tile;
         decode(T, z, cl, b, tile);
         const CigClass& K = a.cls[cl];
-        return Stage{image_base(a.src, z, b), tile * a.TR * a.RM + K.rmin, K.cmin, cbk * CB};
+        const int cbk = s / ngrp, grp = s - cbk * ngrp;
+        return Stage{image_base(a.src, z, b), tile * a.TR * a.SRM + K.rmin + grp, K.cmin, cbk * CB};
     };
+    auto nr_of = [&](int s) { return ngrp > 1 ? a.gnr[s % ngrp] : a.NR; };
 
     int T = next_valid(blockIdx.x);
     if (T >= total) return;
     StageRegs<VEC> pre;   // the next band, loaded while the current one is multiplied
-    pre.load(a.src, stage_of(T, 0), a.NR, a.WP, CB);
+    pre.load(a.src, stage_of(T, 0), nr_of(0), a.WP, CB, a.RS);
     while (true) {
         int z, cl, b, tile;
         decode(T, z, cl, b, tile);
@@ -230,30 +233,39 @@ __global__ __launch_bounds__(256, 2) void k_conv_ig(ConvIgArgs a) {
                     acc[tm][tn] = mfma16x16x4(bq[tn].w, av[tm][3], acc[tm][tn]);
                 }
         };
-        const int ntaps = K.ntaps;
-        // chunk r of a block = (tap, sub): A at band4[ppos + toff*CS/4 + 4*sub + g], weights
-        // at wtap*C + block*CB + 16*sub + 4g (uniform integer math, no table loads)
+        // stage s = (channel block cbk, row group grp): taps i = gi0 + ii*gdi (ii < gni), all j;
+        // chunk r of a stage = (tap, sub): A at band4[ppos + toff*CS/4 + 4*sub + g], weights at
+        // wtap*C + cbk*CB + 16*sub + 4g (uniform integer math, no table loads)
         const int nsub_s = C4 ? 0 : (CB == 64 ? 2 : CB == 32 ? 1 : 0);
-        const int per_blk = C4 ? (ntaps + 3) >> 2 : ntaps << nsub_s;
-        auto chunk = [&](int cbk, int r, int& aoff4, int& woff, bool& bv) {
+        int cbk = 0, gi0 = K.i0, gdi = K.di, gni = K.ni, ntaps = K.ntaps, per_blk = 0;
+        auto set_stage = [&](int s) {
+            cbk = s / ngrp;
+            const int grp = s - cbk * ngrp;
+            gi0 = ngrp > 1 ? grp : K.i0;
+            gdi = ngrp > 1 ? a.SRM : K.di;
+            gni = ngrp > 1 ? a.gni[grp] : K.ni;
+            ntaps = gni * K.nj;
+            per_blk = C4 ? (ntaps + 3) >> 2 : ntaps << nsub_s;
+        };
+        auto chunk = [&](int r, int& aoff4, int& woff, bool& bv) {
             if (C4) {   // lane group g: tap 4r + g, its 4 channels
                 const int t = 4 * r + g;
                 bv = t < ntaps;
                 const int ii = t / K.nj, jj = t - ii * K.nj;
                 aoff4 = bv ? (K.o0 + ii * K.oi + jj * K.oj) * CS4 : 0;
-                woff = ((K.i0 + ii * K.di) * K.kw + K.j0 + jj * K.dj) * 4;
+                woff = ((gi0 + ii * gdi) * K.kw + K.j0 + jj * K.dj) * 4;
             } else {
                 const int ti = r >> nsub_s, sub = r & ((1 << nsub_s) - 1);
                 const int ii = ti / K.nj, jj = ti - ii * K.nj;
                 bv = true;
                 aoff4 = (K.o0 + ii * K.oi + jj * K.oj) * CS4 + 4 * sub + g;
-                woff = ((K.i0 + ii * K.di) * K.kw + K.j0 + jj * K.dj) * C + cbk * CB + 16 * sub + 4 * g;
+                woff = ((gi0 + ii * gdi) * K.kw + K.j0 + jj * K.dj) * C + cbk * CB + 16 * sub + 4 * g;
             }
         };
-        auto bload = [&](int cbk, int r, float4 (&bb)[TN]) {
+        auto bload = [&](int r, float4 (&bb)[TN]) {
             int aoff4, woff;
             bool bv;
-            chunk(cbk, r, aoff4, woff, bv);
+            chunk(r, aoff4, woff, bv);
 #pragma unroll
             for (int tn = 0; tn < TN; tn++) bb[tn] = (bv && !(a.exp & 2)) ? ld4(wrow[tn] + woff) : make_float4(0.f, 0.f, 0.f, 0.f);
             if (a.exp & 2) {
@@ -264,11 +276,11 @@ __global__ __launch_bounds__(256, 2) void k_conv_ig(ConvIgArgs a) {
         // one chunk: the next chunk's weights into `nxt` while `cur` is multiplied (two named
         // register sets, chunk loop unrolled by 2: no copies, so the wait for `cur` does not
         // also wait for the prefetch)
-        auto step = [&](int cbk, int r, const float4 (&cur)[TN], float4 (&nxt)[TN]) {
+        auto step = [&](int r, const float4 (&cur)[TN], float4 (&nxt)[TN]) {
             int aoff4, woff;
             bool bv;
-            chunk(cbk, r, aoff4, woff, bv);
-            if (r + 1 < per_blk) bload(cbk, r + 1, nxt);
+            chunk(r, aoff4, woff, bv);
+            if (r + 1 < per_blk) bload(r + 1, nxt);
             // keep the prefetch at the top of the chunk: under register pressure the scheduler
             // otherwise sinks it below the MFMAs, exposing the L2 latency at every chunk
             __builtin_amdgcn_sched_barrier(0);
@@ -282,22 +294,23 @@ __global__ __launch_bounds__(256, 2) void k_conv_ig(ConvIgArgs a) {
                 mma(av, cur);
             }
         };
-        for (int cbk = 0; cbk < ncb; cbk++) {
+        for (int s = 0; s < nstage; s++) {
+            set_stage(s);
             float4 b0[TN], b1[TN];
-            bload(cbk, 0, b0);
-            __syncthreads();   // the previous block's A reads are done
-            if (!(a.exp & 1)) pre.store(band, a.NR, a.WP, CB, a.CS);
+            bload(0, b0);
+            __syncthreads();   // the previous stage's A reads are done
+            if (!(a.exp & 1)) pre.store(band, nr_of(s), a.WP, CB, a.CS);
             __syncthreads();
             if (!(a.exp & 1)) {
-                if (cbk + 1 < ncb) pre.load(a.src, stage_of(T, cbk + 1), a.NR, a.WP, CB);
-                else if (Tn < total) pre.load(a.src, stage_of(Tn, 0), a.NR, a.WP, CB);
+                if (s + 1 < nstage) pre.load(a.src, stage_of(T, s + 1), nr_of(s + 1), a.WP, CB, a.RS);
+                else if (Tn < total) pre.load(a.src, stage_of(Tn, 0), nr_of(0), a.WP, CB, a.RS);
             }
             int r = 0;
             for (; r + 1 < per_blk; r += 2) {
-                step(cbk, r, b0, b1);
-                step(cbk, r + 1, b1, b0);
+                step(r, b0, b1);
+                step(r + 1, b1, b0);
             }
-            if (r < per_blk) step(cbk, r, b0, b1);
+            if (r < per_blk) step(r, b0, b1);
         }
 
         // epilogue: lane holds pixel q = (wm*TM + tm)*16 + i16, channels n = (wn*TN + tn)*16 + 4g + r.

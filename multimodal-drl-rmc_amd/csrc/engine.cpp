@@ -200,8 +200,10 @@ static bool cig_stage_fits(int NR, int WP, int CB, bool vec) {
 }
 static int cig_cb(int C, int NR, int WP, bool vec) {
     if (C == 4) return 4;
+    size_t cap = 50 * 1024;   // DQNX_CIG_LDS_KB: band budget (a larger band means fewer workgroups per CU)
+    if (const char* v = getenv("DQNX_CIG_LDS_KB")) cap = (size_t)atoi(v) * 1024;
     for (int cb : {64, 32})
-        if (C % cb == 0 && (size_t)NR * WP * (cb + 4) * 4 <= 50 * 1024 && cig_stage_fits(NR, WP, cb, vec)) return cb;
+        if (C % cb == 0 && (size_t)NR * WP * (cb + 4) * 4 <= cap && cig_stage_fits(NR, WP, cb, vec)) return cb;
     return 16;
 }
 static int cig_cs(int CB) { return CB == 4 ? 4 : CB + 4; }
@@ -213,24 +215,40 @@ static bool cig_fwd_geom(const ConvPlan& cp, int Bl, bool first, ConvIgArgs& a) 
     if (!conv_ig_supported(cp.Co, a.BM, cp.Ci)) return false;
     a.Bl = Bl;
     a.nclass = 1;
-    a.RM = cp.sh;
     a.CM = cp.sw;
     a.WP = (cp.Wo - 1) * cp.sw + cp.kw;
-    a.NR = (a.TR - 1) * cp.sh + cp.kh;
+    a.SRM = cp.sh;
+    CigClass& k = a.cls[0];
+    k.ni = cp.kh; k.nj = cp.kw; k.i0 = k.j0 = 0; k.di = k.dj = 1; k.kw = cp.kw;
+    k.o0 = 0; k.oi = a.WP; k.oj = 1;
+    const char* gv = getenv("DQNX_CIG_GROUPS");   // 0: stride-2 forwards stage all rows at once
+    if (cp.sh == 2 && cp.Ci != 4 && !(gv && atoi(gv) == 0)) {   // row-parity groups: band rows compact, one group per parity
+        a.ngrp = 2;
+        a.RM = 1;
+        a.RS = 2;
+        a.NR = 0;
+        for (int p = 0; p < 2; p++) {
+            a.gni[p] = p < cp.kh ? (cp.kh - 1 - p) / 2 + 1 : 0;
+            a.gnr[p] = a.TR + std::max(a.gni[p], 1) - 1;
+            a.NR = std::max(a.NR, a.gnr[p]);
+        }
+    } else {
+        a.ngrp = 1;
+        a.RM = cp.sh;
+        a.RS = 1;
+        a.NR = (a.TR - 1) * cp.sh + cp.kh;
+    }
     a.N = cp.Co;
     const bool vec = cp.Ci != 4 && !first;   // the first conv stages CHW ring rows
     a.CB = cig_cb(cp.Ci, a.NR, a.WP, vec);
     a.CS = cig_cs(a.CB);
     if (!cig_stage_fits(a.NR, a.WP, a.CB, vec)) return false;
-    CigClass& k = a.cls[0];
     k.Hq = cp.Ho;
     k.Wq = cp.Wo;
     k.tiles = (cp.Ho + a.TR - 1) / a.TR;
     k.ntaps = cp.kh * cp.kw;
     k.rmin = -cp.ph;
     k.cmin = -cp.pw;
-    k.ni = cp.kh; k.nj = cp.kw; k.i0 = k.j0 = 0; k.di = k.dj = 1; k.kw = cp.kw;
-    k.o0 = 0; k.oi = a.WP; k.oj = 1;
     a.maxtiles = k.tiles;
     a.Kw = cp.kh * cp.kw * cp.Ci;
     a.ymul = a.xmul = 1;
@@ -238,7 +256,7 @@ static bool cig_fwd_geom(const ConvPlan& cp, int Bl, bool first, ConvIgArgs& a) 
     a.src.H = cp.Hi;
     a.src.W = cp.Wi;
     a.src.C = cp.Ci;
-    return conv_ig_lds_bytes(a) <= 64 * 1024;
+    return conv_ig_lds_bytes(a) <= 160 * 1024;
 }
 
 // data gradient of conv cp (into the previous conv's NHWC dZ): one class per output phase
@@ -252,6 +270,7 @@ static bool cig_dx_geom(const ConvPlan& cp, int Bl, bool last, ConvIgArgs& a) {
     if (!conv_ig_supported(cp.Ci, a.BM, cp.Co)) return false;
     a.Bl = Bl;
     a.RM = a.CM = 1;
+    a.SRM = a.RS = a.ngrp = 1;
     int nr = 0, wp = 0;
     for (int pa = 0; pa < cp.sh; pa++)
         for (int pc = 0; pc < cp.sw; pc++) {
@@ -298,7 +317,7 @@ static bool cig_dx_geom(const ConvPlan& cp, int Bl, bool last, ConvIgArgs& a) {
     a.src.W = cp.Wo;
     a.src.C = cp.Co;
     a.nstreams = 1;
-    return conv_ig_lds_bytes(a) <= 64 * 1024;
+    return conv_ig_lds_bytes(a) <= 160 * 1024;
 }
 
 // weight gradient of conv cp: row groups of RB output rows (X band <= 64 KB, pixel chunks as

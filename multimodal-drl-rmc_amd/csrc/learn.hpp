@@ -420,7 +420,13 @@ struct CigSource {
 enum { CIG_EPI_NHWC = 0, CIG_EPI_FLAT = 1, CIG_EPI_DX = 2 };
 struct ConvIgArgs {
     int nstreams, Bl, nclass, maxtiles;
-    int TR, RM, CM, NR, WP;   // tile = TR class rows; band NR x WP source pixels
+    int TR, RM, CM, NR, WP;   // tile = TR class rows; band NR x WP source pixels; RM band rows per class row
+    // source rows per class row (SRM) and the staging row step (RS).  A stride-2 forward stages its
+    // band in two row-parity groups (ngrp 2: group p holds source rows r0 + p + 2k compactly, gnr[p]
+    // of them, and the taps i = p + 2 ii, ii < gni[p]), so every stage reads whole pixels (all
+    // channels of a 128-B line at once) and each source row once
+    int SRM, RS, ngrp;
+    int gnr[2], gni[2];
     int BM, act;              // tile rows (64 / 128 / 256; TR * Wq <= BM), activation
     int exp;                  // DQNX_CIG_EXP timing experiments (wrong results): 1 no band staging,
                               // 2 no weight loads, 4 no epilogue stores, 8 no MFMA

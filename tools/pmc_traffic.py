@@ -24,13 +24,25 @@ NAMES = [   # (substring of the HIP kernel name, bench step name)
     ("k_per_update", "per_update"),
     ("k_per_prep", "per_update_prep"),
     ("k_per_prop", "per_update_prop"),
+    # (4,84,84) variant, implicit-GEMM convs (conv_ig.hip)
+    ("k_conv_perm", "conv_perm"),
+    ("k_conv_ig<4, 2, 4, true, 0, false>", "conv_fwd_c1"),
+    ("k_conv_ig<8, 2, 2, false, 0, true>", "conv_fwd_c2"),
+    ("k_conv_ig<4, 2, 2, false, 1, true>", "conv_fwd_c3"),
+    ("k_conv_ig<4, 2, 2, false, 2, true>", "conv_dx_c3"),
+    ("k_conv_ig<4, 2, 4, false, 2, true>", "conv_dx_c2"),
+    ("k_conv_dw_ig<3, 2, false>", "conv_dw_c1"),
+    ("k_unflatten_tiled", "unflatten"),
+    ("k_linear_fwd_reduce", "linear_fwd_l1_reduce"),
+    ("k_adam4", "adam_fused"),
 ]
 
 
 # kernels launched more than once per step under one name: bench step names in dispatch order
 CYCLES = [
     ("k_im2col_lds", ["im2col_c1", "im2col_c2", "im2col_c3"]),   # (4,84,84) variant
-    ("k_linear_fwd_big<1, true, 128, 64", ["conv_fwd_c2", "conv_fwd_c3"]),
+    ("k_linear_fwd_big<1, true, 128, 64", ["conv_fwd_c2", "conv_fwd_c3"]),   # explicit path
+    ("k_conv_dw_ig<9, 4, true>", ["conv_dw_c3", "conv_dw_c2"]),              # implicit path, last conv first
 ]
 
 
