@@ -39,7 +39,7 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(REPO, "multimodal-drl-rmc_amd"))
 
 from dqn import _capi as C  # noqa: E402
-from dqn.data_parallel import GraphedDPStep, dp_learn_step  # noqa: E402
+from dqn.data_parallel import GraphedDPStep, dp_learn_step, dp_learn_step_bucketed  # noqa: E402
 from dqn.engine import LearnEngine, hybrid_spec, mlp_spec  # noqa: E402
 
 PEAK_FP32_MFMA_TFLOPS = 157.3   # MI355X_MICROARCH.md: F32 matrix, dense
@@ -81,6 +81,8 @@ def parse():
                    help="N > 1, uniform replay: each rank draws its own rows from its own MT stream (plain data "
                         "parallelism; NOT the reference's random.sample semantics)")
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--no-buckets", action="store_true",
+                   help="conv nets under DP: one gradient all-reduce instead of per-layer buckets")
     p.add_argument("--cpu-seconds", type=float, default=6.0, help="seconds per CPU-baseline leg")
     p.add_argument("--no-kernel-timing", action="store_true")
     p.add_argument("--no-extras", action="store_true",
@@ -321,9 +323,13 @@ def timed_steps(step, steps, dist, device):
 def run_learner(args, eng, world, backend, steps, warmup, dist, device):
     """Warm up, then time `steps` learn steps (single GPU: the engine's graph; DP: the whole DP
     step as one HIP graph over RCCL).  Returns (seconds, dp_graph)."""
+    # conv nets exchange per-layer gradient buckets on a side stream, overlapped with the rest of
+    # the backward (dp_learn_step_bucketed); the MLP's 428 KB gradient stays one all-reduce
+    bucketed = world > 1 and args.net != "mlp" and not args.no_buckets
+
     def step():
         if world > 1:   # shard compute, RCCL all-reduce (+ PER |delta| all-gather), replicated Adam
-            dp_learn_step(eng, soft_update=True)
+            (dp_learn_step_bucketed if bucketed else dp_learn_step)(eng, soft_update=True)
         else:
             eng.learn_step(soft_update=True, prefetch=args.prefetch)
     for _ in range(warmup):
@@ -335,7 +341,7 @@ def run_learner(args, eng, world, backend, steps, warmup, dist, device):
         # the whole DP step (shard kernels + RCCL all-reduce + Adam) as one replayed graph: the
         # eager loop is host-bound (3 launches + a collective call per ~50 us step).  RCCL
         # collectives are capturable; gloo's are host calls and never are.
-        g = GraphedDPStep(eng, soft_update=True)
+        g = GraphedDPStep(eng, soft_update=True, bucketed=bucketed)
         g()   # one untimed replay
         torch.cuda.synchronize()
         dp_graph = True
@@ -556,7 +562,9 @@ def main():
                 "batch_per_gpu": Bl, "global_batch": Bg, "replay_capacity": args.capacity,
                 "parallelism": f"dp{world}", "graphs": not args.no_graphs, "prefetch_sampling": args.prefetch,
                 "sampling": "rank-local" if local else "global (reference-exact random.sample on every rank)",
-                "dp_step": ("one HIP graph" if dp_graph else "eager") if world > 1 else None,
+                "dp_step": ((("one HIP graph" if dp_graph else "eager")
+                             + (", per-layer gradient buckets" if args.net != "mlp" and not args.no_buckets else ""))
+                            if world > 1 else None),
                 "compute": args.compute,
             },
             "roofline": roofline,

@@ -249,6 +249,21 @@ int dqnx_rng_get(dqnx_engine* e, int32_t which, uint32_t* state625, void* stream
 int dqnx_learn_step(dqnx_engine* e, int32_t flags, void* stream);
 /* Adam (+ optional soft update) from DQNX_BUF_GRADS: second half of a GRADS_ONLY step. */
 int dqnx_apply_grads(dqnx_engine* e, int32_t flags, void* stream);
+/* ---- bucketed data-parallel step (conv nets) -----------------------
+ * The DQNX_STEP_GRADS_ONLY step cut where a layer's weight gradient is complete, so the caller
+ * can all-reduce a finished bucket (on a side stream) while the engine runs the rest of the
+ * backward, and apply Adam to it before the last bucket arrives.  Bucket 0 = dense layers +
+ * Q head + the loss slot (done after the dense backward), then one bucket per conv, last conv
+ * first; an MLP has one bucket.  Each bucket is a contiguous range of DQNX_BUF_GRADS /
+ * DQNX_BUF_PARAMS.  Enqueue dqnx_learn_step_bucket for b = 0, 1, ... in order on one stream;
+ * dqnx_apply_grads_bucket(b) after bucket b's all-reduce (bucket 0's also applies the PER tree
+ * update).  Together they equal dqnx_learn_step(GRADS_ONLY) + dqnx_apply_grads, bit for bit.
+ * Replaces the single all-reduce of dqn/data_parallel.py's unbucketed step (no reference call
+ * site: the reference trains on one device). */
+int dqnx_dp_bucket_count(dqnx_engine* e, int32_t* n);
+int dqnx_dp_bucket_info(dqnx_engine* e, int32_t bucket, int64_t* first, int64_t* count);
+int dqnx_learn_step_bucket(dqnx_engine* e, int32_t flags, int32_t bucket, void* stream);
+int dqnx_apply_grads_bucket(dqnx_engine* e, int32_t flags, int32_t bucket, void* stream);
 /* Agent.update_target_network (R:dqn/agent.py:101-110): soft (tau*n_env) or hard copy. */
 int dqnx_soft_update(dqnx_engine* e, void* stream);
 int dqnx_hard_update(dqnx_engine* e, void* stream);

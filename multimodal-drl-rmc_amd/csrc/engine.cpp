@@ -673,7 +673,7 @@ void fill_blk_layers(dqnx_engine* e, AdamArgs& aa) {
 }
 
 // Gradient reduction (fixed-order sum of the split-K slabs) + Adam (+ soft update).
-KStep adam_kstep(dqnx_engine* e, int flags) {
+KStep adam_kstep(dqnx_engine* e, int flags, AdamArgs* args_out = nullptr) {
     const dqnx_config& c = e->cfg;
     const NetPlan& np = e->np;
     const int L = (int)np.dense.size();
@@ -733,6 +733,7 @@ KStep adam_kstep(dqnx_engine* e, int flags) {
     aa.loss_partial = at<float>(e, e->ws_loss_part);
     aa.n_loss_partial = e->tiles;
     aa.batch_global = e->Bg;
+    aa.with_loss = 1;
     fill_blk_layers(e, aa);
     if (e->mtc_blocks && !(flags & DQNX_STEP_GIVEN_INDICES)) {   // keep the sampler's MT blocks ahead
         aa.mtc = at<uint32_t>(e, e->ws_mtc);
@@ -745,8 +746,10 @@ KStep adam_kstep(dqnx_engine* e, int flags) {
     k.bytes = 4.0 * (part_elems + P + (aa.mode ? 6.0 * P + (aa.soft ? 2.0 * P : 0.0) : 0.0));
     k.flops = aa.mode ? 12.0 * P : 0.0;
     k.run = [=](hipStream_t s) { return launch_adam(aa, s); };
+    if (args_out) *args_out = aa;
     return k;
 }
+
 
 // Blocked weight copies for the fused plan (relayout.hpp), rebuilt by spare workgroups of
 // the sampler launch at the start of every step.
@@ -1764,6 +1767,7 @@ int enqueue_apply(dqnx_engine* e, int flags, hipStream_t s) {
     aa.beta2d = c.beta2;
     aa.lrd = c.lr;
     aa.batch_global = e->Bg;
+    aa.with_loss = 1;
     fill_blk_layers(e, aa);
     return launch_adam(aa, s);
 }
@@ -1814,6 +1818,61 @@ const std::vector<KStep>& steps_for(dqnx_engine* e, int key) {
     auto it = e->steps_cache.find(key);
     if (it == e->steps_cache.end()) it = e->steps_cache.emplace(key, build_learn_steps(e, key)).first;
     return it->second;
+}
+
+// ---- bucketed DP step (conv nets): the GRADS_ONLY step cut where a layer's
+// weight gradient is complete.  Bucket 0 = dense layers + head + the loss slot (complete after
+// the dense backward), then one bucket per conv, last conv first; each a contiguous flat range,
+// so the caller all-reduces bucket b while the engine computes the remaining backward.
+struct DpBucket {
+    int k0, k1;              // kernels [k0, k1) of the GRADS_ONLY plan
+    int64_t first, count;    // parameter range [first, first + count) (bucket 0: + the loss slot)
+};
+
+int dp_buckets(dqnx_engine* e, std::vector<DpBucket>& out) {
+    out.clear();
+    const NetPlan& np = e->np;
+    const int NC = (int)np.conv.size();
+    const std::vector<KStep>& ks = steps_for(e, DQNX_STEP_GRADS_ONLY);
+    const int nk = (int)ks.size() - 1;   // the last kernel is the whole-gradient slab sum
+    auto find = [&](const std::string& nm, int from) {
+        for (int k = from; k < nk; k++)
+            if (ks[k].name == nm) return k;
+        return -1;
+    };
+    if (NC == 0) {
+        out.push_back({0, nk, 0, np.P});
+        return DQNX_OK;
+    }
+    int cut = find("unflatten", 0);
+    if (cut < 0) return set_error(DQNX_EUNSUPPORTED, "dp buckets: no conv backward in the plan");
+    out.push_back({0, cut, np.dense[0].off, np.P - np.dense[0].off});
+    for (int l = NC - 1; l >= 0; l--) {
+        // the bucket closes after the last kernel that READS this conv's weights: the implicit
+        // path's data gradient reads the permuted copy made at the step's start, so its bucket
+        // closes at the dW kernel; the explicit path's dX GEMM (conv_dx / conv_dxs / the level
+        // kernel's dx role) reads the live weights, which the bucket's Adam must not update first
+        const std::string tag = "_c" + std::to_string(l + 1);
+        int k = -1;
+        if (e->conv_ig) {
+            k = find("conv_dw" + tag, cut);
+        } else {
+            for (int q = cut; q < nk; q++) {
+                const std::string& nm = ks[q].name;
+                if (nm.rfind("conv_", 0) == 0 && nm.size() > tag.size() &&
+                    nm.compare(nm.size() - tag.size(), tag.size(), tag) == 0)
+                    k = q;
+            }
+        }
+        if (k < 0) return set_error(DQNX_EUNSUPPORTED, "dp buckets: no weight gradient kernel for conv %d", l + 1);
+        const ConvPlan& cp = np.conv[l];
+        out.push_back({cut, k + 1, cp.off, (int64_t)cp.Co * cp.K + cp.Co});
+        cut = k + 1;
+    }
+    if (cut != nk) {   // kernels after conv 1's dW (none in either conv path) go with the last bucket
+        out.back().k1 = nk;
+    }
+    return DQNX_OK;
 }
 
 }  // namespace
@@ -2414,6 +2473,87 @@ int dqnx_apply_grads(dqnx_engine* e, int32_t flags, void* stream) {
     if (rc) return rc;
     const int key = 0x100 | (flags & DQNX_STEP_SOFT_UPDATE);
     return run_graphed(e, key, (hipStream_t)stream, [&](hipStream_t s) { return enqueue_apply(e, key, s); });
+}
+
+int dqnx_dp_bucket_count(dqnx_engine* e, int32_t* n) {
+    int rc = check_bound(e);
+    if (rc) return rc;
+    if (!n) return set_error(DQNX_EINVAL, "null argument");
+    std::vector<DpBucket> b;
+    rc = dp_buckets(e, b);
+    if (rc) return rc;
+    *n = (int32_t)b.size();
+    return DQNX_OK;
+}
+
+int dqnx_dp_bucket_info(dqnx_engine* e, int32_t bucket, int64_t* first, int64_t* count) {
+    int rc = check_bound(e);
+    if (rc) return rc;
+    std::vector<DpBucket> b;
+    rc = dp_buckets(e, b);
+    if (rc) return rc;
+    if (bucket < 0 || bucket >= (int32_t)b.size()) return set_error(DQNX_EINVAL, "bucket %d out of range", bucket);
+    if (first) *first = b[bucket].first;
+    if (count) *count = b[bucket].count + (bucket == 0 ? 1 : 0);   // bucket 0 carries the loss slot
+    return DQNX_OK;
+}
+
+int dqnx_learn_step_bucket(dqnx_engine* e, int32_t flags, int32_t bucket, void* stream) {
+    int rc = check_bound(e);
+    if (rc) return rc;
+    hipStream_t s = (hipStream_t)stream;
+    if (flags & (DQNX_STEP_PREFETCH | DQNX_STEP_GIVEN_INDICES))
+        return set_error(DQNX_EUNSUPPORTED, "bucketed steps sample their own minibatch, without prefetch");
+    if (e->pf_valid) return set_error(DQNX_ESTATE, "a prefetched minibatch is pending");
+    std::vector<DpBucket> b;
+    rc = dp_buckets(e, b);
+    if (rc) return rc;
+    if (bucket < 0 || bucket >= (int32_t)b.size()) return set_error(DQNX_EINVAL, "bucket %d out of range", bucket);
+    if (bucket == 0 && e->ring_size < e->Bs)
+        return set_error(DQNX_EINVAL, "Sample larger than population: %lld < %d", (long long)e->ring_size, e->Bs);
+    // the plan of a plain GRADS_ONLY step (blocked-weight rebuild as that step decides)
+    const int key = DQNX_STEP_GRADS_ONLY | ((e->bwd_plan == 2 && (e->wblk_dirty || !adam_keeps_blk(e))) ? KEY_RELAYOUT : 0);
+    const std::vector<KStep>& ks = steps_for(e, key);
+    const std::vector<KStep>& k0 = steps_for(e, DQNX_STEP_GRADS_ONLY);
+    if (ks.size() != k0.size()) return set_error(DQNX_ESTATE, "dp buckets: plan mismatch");
+    rc = enqueue_range(ks, b[bucket].k0, b[bucket].k1, s);
+    if (rc) return rc;
+    if (bucket == 0) e->wblk_dirty = false;
+    AdamArgs aa;
+    adam_kstep(e, DQNX_STEP_GRADS_ONLY, &aa);   // mode 0: this bucket's slab sums into DQNX_BUF_GRADS
+    aa.e0 = b[bucket].first;
+    aa.n_params = b[bucket].first + b[bucket].count;
+    aa.with_loss = bucket == 0;
+    if (bucket != 0) {
+        aa.loss_partial = nullptr;
+        aa.mtc = nullptr;
+    }
+    return launch_adam(aa, s);
+}
+
+int dqnx_apply_grads_bucket(dqnx_engine* e, int32_t flags, int32_t bucket, void* stream) {
+    int rc = check_bound(e);
+    if (rc) return rc;
+    hipStream_t s = (hipStream_t)stream;
+    std::vector<DpBucket> b;
+    rc = dp_buckets(e, b);
+    if (rc) return rc;
+    if (bucket < 0 || bucket >= (int32_t)b.size()) return set_error(DQNX_EINVAL, "bucket %d out of range", bucket);
+    const dqnx_config& c = e->cfg;
+    if (bucket == 0 && c.algo == DQNX_ALGO_PER_DOUBLE) {   // the tree update, once per step
+        rc = enqueue_per_update(e, at<int32_t>(e, e->off[DQNX_BUF_BATCH_IDX]), s);
+        if (rc) return rc;
+    }
+    AdamArgs aa;
+    adam_kstep(e, DQNX_STEP_GRADS_ONLY, &aa);
+    aa.mode = 2;
+    aa.soft = (flags & DQNX_STEP_SOFT_UPDATE) ? 1 : 0;
+    aa.loss_partial = nullptr;
+    aa.mtc = nullptr;
+    aa.e0 = b[bucket].first;
+    aa.n_params = b[bucket].first + b[bucket].count;
+    aa.with_loss = bucket == 0;
+    return launch_adam(aa, s);
 }
 
 int dqnx_soft_update(dqnx_engine* e, void* stream) {

@@ -689,7 +689,7 @@ __global__ __launch_bounds__(256) void k_adam(AdamArgs a) {
         step_size = a.ctrl->adam_step_size;
         bc2s = a.ctrl->adam_bc2_sqrt;
     }
-    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < P; e += stride) {
+    for (int64_t e = a.e0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < P; e += stride) {
         // every load of this element is issued before the first use (one round trip)
         float m = 0.f, v = 0.f, p = 0.f, tg = 0.f;
         if (a.mode != 0) {
@@ -766,7 +766,7 @@ __global__ __launch_bounds__(256) void k_adam(AdamArgs a) {
             a.ctrl->loss = loss;
         }
     }
-    if (a.mode == 2 && blockIdx.x == 0 && threadIdx.x == 0) a.ctrl->loss = a.grads[P];
+    if (a.mode == 2 && a.with_loss && blockIdx.x == 0 && threadIdx.x == 0) a.ctrl->loss = a.grads[P];
 }
 
 // k_adam on float4s: every segment offset / slab stride a multiple of 4 and no blocked copies
@@ -778,14 +778,14 @@ __global__ __launch_bounds__(256) void k_adam4(AdamArgs a) {
         mt_cache_extend(a.mtc, a.mtc_blocks);
         return;
     }
-    const int64_t P = a.n_params, P4 = (P + 3) >> 2;
+    const int64_t P = a.n_params, P4 = (P + 3) >> 2;   // e0 is a multiple of 4 (launch_adam)
     const int64_t stride = (int64_t)(gridDim.x - (a.mtc ? 1 : 0)) * blockDim.x;
     float step_size = 0.f, bc2s = 1.f;
     if (a.mode != 0) {
         step_size = a.ctrl->adam_step_size;
         bc2s = a.ctrl->adam_bc2_sqrt;
     }
-    for (int64_t e4 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e4 < P4; e4 += stride) {
+    for (int64_t e4 = (a.e0 >> 2) + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e4 < P4; e4 += stride) {
         const int64_t e = e4 << 2;
         const int nv = (int)min((int64_t)4, P - e);   // 4 except in the last vector
         float4 m = make_float4(0.f, 0.f, 0.f, 0.f), v = m, p = m, tg = m, g = m;
@@ -862,7 +862,7 @@ __global__ __launch_bounds__(256) void k_adam4(AdamArgs a) {
             a.ctrl->loss = loss;
         }
     }
-    if (a.mode == 2 && blockIdx.x == 0 && threadIdx.x == 0) a.ctrl->loss = a.grads[P];
+    if (a.mode == 2 && a.with_loss && blockIdx.x == 0 && threadIdx.x == 0) a.ctrl->loss = a.grads[P];
 }
 
 __global__ void k_soft_update(float* __restrict__ target, const float* __restrict__ p, int64_t n, float tau,
@@ -1027,7 +1027,7 @@ int launch_head(const HeadArgs& a, int act, hipStream_t s) {
 static bool adam_vec_ok(const AdamArgs& a) {
     if (const char* v = getenv("DQNX_ADAM_VEC"))
         if (atoi(v) == 0) return false;
-    if (a.nblk) return false;
+    if (a.nblk || a.e0 % 4) return false;
     auto al = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
     if (!al(a.p) || !al(a.m) || !al(a.v) || !al(a.grads) || (a.target && !al(a.target))) return false;
     for (int i = 0; i < a.nseg; i++)
@@ -1037,7 +1037,7 @@ static bool adam_vec_ok(const AdamArgs& a) {
 
 int launch_adam(const AdamArgs& a, hipStream_t s) {
     const bool vec = adam_vec_ok(a);
-    const int64_t items = vec ? (a.n_params + 3) / 4 : a.n_params;
+    const int64_t items = vec ? (a.n_params - a.e0 + 3) / 4 : a.n_params - a.e0;
     int blocks = (int)((items + 255) / 256);
     if (blocks > 2048) blocks = 2048;
     if (blocks < 1) blocks = 1;

@@ -136,7 +136,9 @@ struct AdamArgs {
     int nseg;
     int mode;              // 0 partials->grads, 1 partials->grads+adam, 2 grads->adam
     int soft;
-    int64_t n_params;
+    int64_t n_params;      // elements [e0, n_params) are processed (e0 = 0 except for DP buckets)
+    int64_t e0;
+    int with_loss;         // the range ends at the loss slot grads[n_params] (mode 2: publish it)
     float* p;
     float* m;
     float* v;

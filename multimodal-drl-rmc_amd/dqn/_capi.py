@@ -84,7 +84,8 @@ EXPORTS = [
     "dqnx_learn_kernel_count", "dqnx_learn_kernel_info", "dqnx_learn_step_timed", "dqnx_learn_step_omit", "dqnx_events_create",
     "dqnx_events_destroy", "dqnx_event_elapsed", "dqnx_debug_stamps",
     "dqnx_per_sample", "dqnx_per_update_priorities", "dqnx_set_agent_step", "dqnx_act", "dqnx_act_scratch_bytes",
-    "dqnx_params_modified",
+    "dqnx_params_modified", "dqnx_dp_bucket_count", "dqnx_dp_bucket_info", "dqnx_learn_step_bucket",
+    "dqnx_apply_grads_bucket",
 ]
 
 _lib = None
@@ -123,6 +124,10 @@ def lib():
         "dqnx_rng_get": ([vp, I32, P(ctypes.c_uint32), vp], ctypes.c_int),
         "dqnx_learn_step": ([vp, I32, vp], ctypes.c_int),
         "dqnx_apply_grads": ([vp, I32, vp], ctypes.c_int),
+        "dqnx_dp_bucket_count": ([vp, P(I32)], ctypes.c_int),
+        "dqnx_dp_bucket_info": ([vp, I32, P(I64), P(I64)], ctypes.c_int),
+        "dqnx_learn_step_bucket": ([vp, I32, I32, vp], ctypes.c_int),
+        "dqnx_apply_grads_bucket": ([vp, I32, I32, vp], ctypes.c_int),
         "dqnx_soft_update": ([vp, vp], ctypes.c_int),
         "dqnx_hard_update": ([vp, vp], ctypes.c_int),
         "dqnx_sample_scratch_bytes": ([I64, I32], ctypes.c_uint64),

@@ -38,11 +38,53 @@ def exchange(engine, group=None):
     """The exchange step between the shard gradients and the optimizer."""
     dist.all_reduce(engine.grads, op=dist.ReduceOp.SUM, group=group)
     if engine.per_abs_td.numel():
-        world = engine.world_size
-        b0, b1 = shard_bounds(engine.batch, world, engine.rank)
-        parts = list(engine.per_abs_td.chunk(world))
-        mine = engine.per_abs_td[b0:b1].clone()
-        dist.all_gather(parts, mine, group=group)
+        _gather_abs_td(engine, group)
+
+
+def dp_learn_step_bucketed(engine, soft_update: bool = True, group=None, comm_stream=None):
+    """The data-parallel step with per-layer gradient buckets (conv nets).  The engine's backward
+    completes the gradient in buckets (engine.dp_buckets(): dense layers + head + loss first, then
+    each conv, last conv first); bucket b's all-reduce and its Adam run on `comm_stream` while the
+    engine computes bucket b+1's backward on the current stream.  No parameter the remaining
+    backward reads is updated early: a conv's data gradient reads the permuted weight copy made at
+    the start of the step, and dF was computed before bucket 0 closed.  Equal, bit for bit, to
+    dp_learn_step: the same kernels, the same sums, the same per-element all-reduce.
+
+    On CPU tensors (gloo rehearsals) the buckets run in the same order on one thread."""
+    buckets = engine.dp_buckets()
+    cuda = engine.grads.is_cuda
+    main = torch.cuda.current_stream(engine.grads.device) if cuda else None
+    comm = (comm_stream or torch.cuda.Stream(engine.grads.device)) if cuda else None
+    for b, (first, count) in enumerate(buckets):
+        engine.learn_step_bucket(b)                   # on the main stream
+        if cuda:
+            comm.wait_stream(main)
+            ctx = torch.cuda.stream(comm)
+        else:
+            ctx = _nullctx()
+        with ctx:
+            dist.all_reduce(engine.grads[first:first + count], op=dist.ReduceOp.SUM, group=group)
+            if b == 0 and engine.per_abs_td.numel():
+                _gather_abs_td(engine, group)
+            engine.apply_grads_bucket(b, soft_update=soft_update)
+    if cuda:
+        main.wait_stream(comm)
+
+
+class _nullctx:
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        return False
+
+
+def _gather_abs_td(engine, group):
+    world = engine.world_size
+    b0, b1 = shard_bounds(engine.batch, world, engine.rank)
+    parts = list(engine.per_abs_td.chunk(world))
+    mine = engine.per_abs_td[b0:b1].clone()
+    dist.all_gather(parts, mine, group=group)
 
 
 class GraphedDPStep:
@@ -58,13 +100,17 @@ class GraphedDPStep:
     off: its kernels become nodes of this graph.
     """
 
-    def __init__(self, engine, soft_update: bool = True, group=None):
+    def __init__(self, engine, soft_update: bool = True, group=None, bucketed: bool = False):
         self.engine = engine
         engine.set_graphs(False)
         self.graph = torch.cuda.CUDAGraph()
+        self.comm = torch.cuda.Stream(engine.grads.device) if bucketed else None
         torch.cuda.synchronize()
         with torch.cuda.graph(self.graph):
-            dp_learn_step(engine, soft_update=soft_update, group=group)
+            if bucketed:   # the side stream forks and joins inside the capture
+                dp_learn_step_bucketed(engine, soft_update=soft_update, group=group, comm_stream=self.comm)
+            else:
+                dp_learn_step(engine, soft_update=soft_update, group=group)
         torch.cuda.synchronize()
 
     def __call__(self):

@@ -369,6 +369,28 @@ class LearnEngine:
         C.check(self.L.dqnx_apply_grads(self.h, C.STEP_SOFT_UPDATE if soft_update else 0, self.stream()),
                 "apply_grads")
 
+    # ---- bucketed data-parallel step (dqn.data_parallel.dp_learn_step_bucketed) ----
+    def dp_buckets(self):
+        """[(first, count)] flat ranges of `grads` / `params`, in the order the backward completes
+        them: dense layers + head (+ the loss slot) first, then the convs, last conv first."""
+        n = ctypes.c_int32()
+        C.check(self.L.dqnx_dp_bucket_count(self.h, ctypes.byref(n)), "dp_bucket_count")
+        out = []
+        for b in range(n.value):
+            f, c = ctypes.c_int64(), ctypes.c_int64()
+            C.check(self.L.dqnx_dp_bucket_info(self.h, b, ctypes.byref(f), ctypes.byref(c)), "dp_bucket_info")
+            out.append((f.value, c.value))
+        return out
+
+    def learn_step_bucket(self, bucket: int):
+        """The part of a GRADS_ONLY learn step that completes `bucket`'s gradient."""
+        C.check(self.L.dqnx_learn_step_bucket(self.h, 0, int(bucket), self.stream()), "learn_step_bucket")
+
+    def apply_grads_bucket(self, bucket: int, soft_update=False):
+        """Adam (+ soft update) of `bucket`'s parameters from `grads` (bucket 0: + the PER tree update)."""
+        C.check(self.L.dqnx_apply_grads_bucket(self.h, C.STEP_SOFT_UPDATE if soft_update else 0, int(bucket),
+                                               self.stream()), "apply_grads_bucket")
+
     def soft_update(self):
         C.check(self.L.dqnx_soft_update(self.h, self.stream()), "soft_update")
 

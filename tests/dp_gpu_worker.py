@@ -11,7 +11,7 @@ REPO = os.path.dirname(HERE)
 sys.path[:0] = [REPO, os.path.join(REPO, "multimodal-drl-rmc_amd")]
 
 from dqn import engine as E  # noqa: E402
-from dqn.data_parallel import dp_learn_step  # noqa: E402
+from dqn.data_parallel import dp_learn_step, dp_learn_step_bucketed  # noqa: E402
 from oracle import ref as O  # noqa: E402  (test data + initial weights only)
 
 
@@ -20,28 +20,43 @@ CASES = {
     "small": (284, 64, 1000, 700, 9),
     "c3": (284, 4096, 60000, 60000, 29),      # configs[3]: global minibatch 4096
 }
+# two-stream conv nets (micro grid, global batch, capacity, fill, seed): the bucketed DP step
+HYB_CASES = {
+    "hyb": ((2, 27, 5), 64, 1000, 700, 13),
+    "hyb84": ((4, 84, 84), 32, 200, 150, 17),
+}
+
+
+def make_spec(case, head):
+    if case in HYB_CASES:
+        chw = HYB_CASES[case][0]
+        return E.hybrid_spec(8, head, micro_chw=chw), O.hybrid_spec(8, head, micro_chw=chw), HYB_CASES[case][1:]
+    obs_dim, batch, cap, fill, seed = CASES[case]
+    return E.mlp_spec(obs_dim, 8, head), O.mlp_spec(obs_dim, 8, head), (batch, cap, fill, seed)
 
 
 def main():
-    """argv: rank world algo out_dir [sampling=global|local] [case=small|c3] [compute=fp32|bf16]"""
+    """argv: rank world algo out_dir [sampling=global|local] [case=small|c3|hyb|hyb84] [compute=fp32|bf16]
+    [mode=plain|bucketed]"""
     rank, world, algo, out = int(sys.argv[1]), int(sys.argv[2]), sys.argv[3], sys.argv[4]
     local = len(sys.argv) > 5 and sys.argv[5] == "local"
     case = sys.argv[6] if len(sys.argv) > 6 else "small"
     compute = sys.argv[7] if len(sys.argv) > 7 else "fp32"
+    bucketed = len(sys.argv) > 8 and sys.argv[8] == "bucketed"
     backend = os.environ.get("DQNX_TEST_BACKEND", "gloo")
     torch.cuda.set_device(0)
     dist.init_process_group(backend, rank=rank, world_size=world)
-    obs_dim, batch, cap, fill, seed = CASES[case]
     head = O.algo_spec_head(algo)
-    eng = E.LearnEngine(E.mlp_spec(obs_dim, 8, head), algo, batch, cap, world_size=world, rank=rank,
+    espec, ospec, (batch, cap, fill, seed) = make_spec(case, head)
+    eng = E.LearnEngine(espec, algo, batch, cap, world_size=world, rank=rank,
                         local_sampling=local, compute_dtype=compute)
-    eng.load_params(O.reference_init(O.mlp_spec(obs_dim, 8, head), seed))
-    eng.push(*O.synth_transitions(fill, obs_dim, 8, seed=seed + 100))
+    eng.load_params(O.reference_init(ospec, seed))
+    eng.push(*O.synth_transitions(fill, ospec.obs_dim, 8, seed=seed + 100))
     eng.set_rng(0, O.py_state_to_array(__import__("random").Random(seed + (rank if local else 0)).getstate()))
     eng.set_rng(1, O.np_state_to_array(np.random.RandomState(seed).get_state()))
     losses, pos = [], []
     for _ in range(3):
-        dp_learn_step(eng, soft_update=True)
+        (dp_learn_step_bucketed if bucketed else dp_learn_step)(eng, soft_update=True)
         torch.cuda.synchronize()
         eng.check_device_error()
         losses.append(float(eng.grads[-1].item()))

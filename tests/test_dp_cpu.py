@@ -107,3 +107,71 @@ def test_dp_world2_matches_single_process(tmp_path, algo):
             np.testing.assert_allclose(z["tree"], ref.replay.replay_buffer.tree, rtol=1e-6, atol=1e-6)
     for k in ref.online:   # replicas stay bitwise identical across ranks
         assert np.array_equal(r0["on_" + k], r1["on_" + k])
+
+
+class BucketedOracleShardEngine(OracleShardEngine):
+    """The bucket surface of LearnEngine (dp_buckets / learn_step_bucket / apply_grads_bucket)
+    over the oracle shard: bucket b's gradient range is published only by learn_step_bucket(b),
+    so an all-reduce that ran early, twice or over the wrong range changes the result; the full
+    update is applied when the last bucket's apply arrives.  The call order is logged."""
+
+    def __init__(self, learner, world, rank):
+        super().__init__(learner, world, rank)
+        sizes = [v.numel() for v in learner.online.values()]
+        # reverse layer order, like the engine: the last tensors (head) + the loss slot first
+        cut1 = self.P - sum(sizes[-2:])
+        cut2 = sizes[0] + sizes[1]
+        self.buckets = [(cut1, self.P - cut1 + 1), (cut2, cut1 - cut2), (0, cut2)]
+        self.full = None
+        self.log = []
+
+    def dp_buckets(self):
+        return list(self.buckets)
+
+    def learn_step_bucket(self, b):
+        self.log.append(("learn", b))
+        if b == 0:
+            self.grads.zero_()
+            self.learn_step(grads_only=True)
+            self.full = self.grads.clone()
+            self.grads.zero_()
+        f, c = self.buckets[b]
+        self.grads[f:f + c] = self.full[f:f + c]
+
+    def apply_grads_bucket(self, b, soft_update=True):
+        self.log.append(("apply", b))
+        if b == len(self.buckets) - 1:
+            self.apply_grads(soft_update=soft_update)
+
+
+def bucket_worker(rank, world, port, algo, out_dir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.set_num_threads(1)
+    from dqn.data_parallel import dp_learn_step, dp_learn_step_bucketed
+    plain = OracleShardEngine(make_learner(algo), world, rank)
+    buck = BucketedOracleShardEngine(make_learner(algo), world, rank)
+    for _ in range(3):
+        dp_learn_step(plain, soft_update=True)
+        dp_learn_step_bucketed(buck, soft_update=True)
+    np.savez(os.path.join(out_dir, f"b{rank}.npz"),
+             plain=torch.cat([v.reshape(-1) for v in plain.L.online.values()]).numpy(),
+             buck=torch.cat([v.reshape(-1) for v in buck.L.online.values()]).numpy(),
+             plain_t=torch.cat([v.reshape(-1) for v in plain.L.target.values()]).numpy(),
+             buck_t=torch.cat([v.reshape(-1) for v in buck.L.target.values()]).numpy(),
+             log=np.array([[0 if k == "learn" else 1, b] for k, b in buck.log]))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("algo", ALGOS)
+def test_bucketed_dp_step_order_and_identity(tmp_path, algo):
+    """dqn.data_parallel.dp_learn_step_bucketed on 2 gloo ranks: buckets are completed, all-reduced
+    and applied in order 0, 1, 2 (learn_step_bucket(b) before apply_grads_bucket(b), before
+    learn_step_bucket(b+1)), and the result equals the single all-reduce step exactly."""
+    port = free_port()
+    mp.spawn(bucket_worker, args=(2, port, algo, str(tmp_path)), nprocs=2, join=True)
+    for r in range(2):
+        z = np.load(tmp_path / f"b{r}.npz")
+        assert np.array_equal(z["plain"], z["buck"]) and np.array_equal(z["plain_t"], z["buck_t"])
+        want = [[k, b] for _ in range(3) for b in range(3) for k in (0, 1)]
+        assert z["log"].tolist() == want

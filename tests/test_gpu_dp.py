@@ -14,10 +14,10 @@ pytestmark = pytest.mark.gpu
 HERE = os.path.dirname(os.path.abspath(__file__))
 
 
-def run_ranks(tmp_path, world, algo, sampling="global", case="small", compute="fp32", timeout=300):
+def run_ranks(tmp_path, world, algo, sampling="global", case="small", compute="fp32", timeout=300, mode="plain"):
     env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(free_port()))
     procs = [subprocess.Popen([sys.executable, os.path.join(HERE, "dp_gpu_worker.py"), str(r), str(world), algo,
-                               str(tmp_path), sampling, case, compute], env=env) for r in range(world)]
+                               str(tmp_path), sampling, case, compute, mode], env=env) for r in range(world)]
     for p in procs:
         assert p.wait(timeout=timeout) == 0
     return [np.load(tmp_path / f"rank{r}.npz") for r in range(world)]
@@ -157,3 +157,42 @@ def test_gpu_dp_world2_bf16_matches_bf16_oracle(tmp_path):
         np.testing.assert_allclose(z[r]["losses"], [x.loss for x in recs], rtol=LOSS_RTOL, atol=1e-6)
         np.testing.assert_allclose(z[r]["params"], flat_on, atol=W_ATOL, rtol=0)
     assert np.array_equal(z[0]["params"], z[1]["params"]) and np.array_equal(z[0]["tree"], z[1]["tree"])
+
+
+@pytest.mark.parametrize("case,algo", [("hyb", "DuelingDoubleDQNAgent"), ("hyb", "PerDuelingDoubleDQNAgent"),
+                                       ("hyb84", "DuelingDoubleDQNAgent")])
+def test_gpu_dp_bucketed_equals_unbucketed(tmp_path, case, algo):
+    """Conv nets: dp_learn_step_bucketed (dense + head bucket, then one bucket per conv, last conv
+    first; each all-reduced and Adam-applied on a side stream while the remaining backward runs)
+    leaves the ranks bit-identical to the single all-reduce step, and the losses follow the
+    single-process oracle on the whole minibatch."""
+    import random
+    sys.path.insert(0, HERE)
+    from dp_gpu_worker import HYB_CASES
+    (tmp_path / "plain").mkdir()
+    (tmp_path / "bucketed").mkdir()
+    zp = run_ranks(tmp_path / "plain", 2, algo, case=case)
+    zb = run_ranks(tmp_path / "bucketed", 2, algo, case=case, mode="bucketed")
+    for r in range(2):
+        for k in ("losses", "positions", "params", "target", "tree"):
+            assert np.array_equal(zp[r][k], zb[r][k]), (r, k)
+    chw, batch, cap, fill, seed = HYB_CASES[case]
+    spec = O.hybrid_spec(8, O.algo_spec_head(algo), micro_chw=chw)
+    ref = O.OracleLearner(spec, algo, batch, cap, seed=seed, params=O.reference_init(spec, seed), per_pow="cr")
+    O.fill_replay(ref, *O.synth_transitions(fill, spec.obs_dim, 8, seed=seed + 100))
+    ref.py_state = O.py_state_to_array(random.Random(seed).getstate())
+    ref.np_state = O.np_state_to_array(np.random.RandomState(seed).get_state())
+    recs = [ref.train_step() for _ in range(3)]
+    np.testing.assert_allclose(zb[0]["losses"], [x.loss for x in recs], rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("net", ["hybrid", "hybrid84"])
+def test_gpu_graphed_bucketed_dp_step(net):
+    """GraphedDPStep(bucketed=True): the bucketed step with its side-stream collectives and Adam
+    captured into one HIP graph (world 1 over RCCL) equals eager bucketed and unbucketed steps and
+    the single-GPU learn step, bit for bit (tools/dp_bucket_check.py asserts it)."""
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(free_port()))
+    r = subprocess.run([sys.executable, os.path.join(os.path.dirname(HERE), "tools", "dp_bucket_check.py"), net],
+                       env=env, capture_output=True, text=True, timeout=280)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    assert "all equal: True" in r.stdout, r.stdout[-2000:]
