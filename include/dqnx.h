@@ -118,7 +118,11 @@ typedef struct dqnx_config {
     double per_eps, per_alpha, per_max_priority;
     double per_beta_start, per_beta_end, per_beta_steps;   /* beta = interp(step,[0,steps],[start,end]) */
     int32_t compute_dtype;     /* dqnx_compute_dtype (ABI 2) */
-    int32_t reserved1;
+    int32_t per_numpy121;      /* PER tree arithmetic of the reference's pinned numpy 1.21: 0 (default) =
+                                  numpy >= 2 (NEP 50: `change` and the ancestor sums in float64, exact);
+                                  1 = numpy 1.21 value-based casting: update_batch_priorities' float32
+                                  `change` and float32-rounded ancestor sums, applied in update order
+                                  (R:dqn/utils/sum_tree.py:18, 31-32; R:bin/environment.yml pins 1.21) */
 } dqnx_config;
 
 /* Fill cfg with the reference's HYPER_PARAMS defaults for the given network. */

@@ -392,7 +392,7 @@ struct dqnx_engine {
     uint64_t total = 0;
     // workspace sub-regions (byte offsets from the arena base)
     uint64_t ws_phys = 0, ws_pool = 0, ws_xobs = 0, ws_head_part = 0, ws_loss_part = 0, ws_stage = 0;
-    uint64_t ws_adam_tab = 0, ws_stamps = 0, ws_dhead = 0, ws_raw = 0, ws_trans = 0, ws_gtab = 0, ws_mtc = 0, ws_per_ticket = 0, ws_per_wl = 0, ws_per_wp = 0, ws_per_winit = 0, ws_per_last = 0;
+    uint64_t ws_adam_tab = 0, ws_stamps = 0, ws_dhead = 0, ws_raw = 0, ws_trans = 0, ws_gtab = 0, ws_mtc = 0, ws_per_ticket = 0, ws_per_wl = 0, ws_per_wp = 0, ws_per_winit = 0, ws_per_last = 0, ws_per_wchg = 0;
     // fused plan: fragment-blocked weight copies [online fwd | target fwd | online chain] per layer
     uint64_t ws_wblk[2][FUSED_MAX_L] = {{0}}, ws_wblkT[FUSED_MAX_L] = {0};
     std::vector<uint64_t> ws_H, ws_dZ, ws_part;
@@ -517,6 +517,7 @@ int layout(dqnx_engine* e) {
         e->ws_per_wp = sub((uint64_t)PER_CHUNK * 4);
         e->ws_per_winit = sub((uint64_t)PER_CHUNK * 8);
         e->ws_per_last = sub((uint64_t)c.capacity * 8);
+        e->ws_per_wchg = sub((uint64_t)PER_CHUNK * 4);
     }
     e->ws_loss_part = sub((uint64_t)e->tiles * 4);
     e->stage_rows = 1024;
@@ -606,6 +607,8 @@ PerUpdateArgs per_update_args(dqnx_engine* e) {
     ua.winit = at<double>(e, e->ws_per_winit);
     ua.last = at<uint64_t>(e, e->ws_per_last);
     ua.epoch = at<uint32_t>(e, e->ws_per_ticket) + 16;
+    ua.numpy121 = c.per_numpy121;
+    ua.wchg = at<float>(e, e->ws_per_wchg);
     return ua;
 }
 
@@ -1938,6 +1941,10 @@ int dqnx_engine_create(const dqnx_config* cfg, dqnx_engine** out) {
     if (rc) { delete e; return rc; }
     const dqnx_config& c = e->cfg;
     if (c.algo < DQNX_ALGO_DQN || c.algo > DQNX_ALGO_PER_DOUBLE) { delete e; return set_error(DQNX_EINVAL, "bad algo"); }
+    if (c.algo == DQNX_ALGO_PER_DOUBLE && c.per_numpy121) {
+        rc = per_numpy121_init();
+        if (rc) { delete e; return rc; }
+    }
     if (c.algo == DQNX_ALGO_PER_DOUBLE) {
         // exact float64 tree sums need cap <= 2^20 (see per.hip); one sampler workgroup <= PER_MAX_B
         if (c.capacity > ((int64_t)1 << 20)) { delete e; return set_error(DQNX_EUNSUPPORTED, "PER capacity > 2^20"); }

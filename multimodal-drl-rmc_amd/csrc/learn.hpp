@@ -289,6 +289,10 @@ struct PerUpdateArgs {
     double* winit;            // [PER_CHUNK] the leaf's value before the chunk
     uint64_t* last;           // [cap] (epoch << 32 | i) of the latest item writing the slot
     uint32_t* epoch;          // chunk counter (tags `last`; zero after reset, like `last`)
+    // numpy 1.21 arithmetic (dqnx_config.per_numpy121, mode 0 only): `change` and every
+    // ancestor sum rounded to float32, applied in update order (k_per_chain)
+    int32_t numpy121;
+    float* wchg;              // [PER_CHUNK] float32 change of item i
 };
 
 // ---- two-stream hybrid network data movement (conv.hip) ----
@@ -487,6 +491,7 @@ int launch_col2im(const Col2imArgs& a, int act, hipStream_t s);
 
 int launch_per_sample(const PerSampleArgs& a, hipStream_t s);
 int launch_per_update(const PerUpdateArgs& a, hipStream_t s);
+int per_numpy121_init();
 
 int launch_linear_fwd(const FwdArgs& args, int nprob, int act, bool vecb, hipStream_t s);
 // large-K dense layers (the (4,84,84) variant's 56,462 -> 512): 128x128 tiles, split-K

@@ -580,6 +580,95 @@ __global__ __launch_bounds__(PER_GT) void k_per_prop(PerUpdateArgs a) {
         if (topd[node] != 0.0) atomicAdd(&a.tree[node], topd[node]);
 }
 
+// ---------------------------------------------------------------------------------------
+// numpy 1.21 mode (dqnx_config.per_numpy121).  update_batch_priorities hands SumTree.update a
+// float32 (1,) array per sample (R:dqn/replay_memory.py:95-98); under numpy < 2's value-based
+// casting `change = priority - tree[i]` and `tree[parent] += change` (R:dqn/utils/sum_tree.py:
+// 18, 31-32) are computed in float32 (the float64 scalar is cast down), so the ancestors hold
+// float32-rounded running sums and the ORDER of the updates matters.  Every node's sequence of
+// additions is independent of every other node's, so:
+//   k_per_chain<true>  (one workgroup): items sorted by (leaf, item); per leaf, in item order,
+//                      change = f32(p - previous value of the leaf); the final p is written;
+//   k_per_chain<false> (one workgroup per tree depth): items sorted by (ancestor at that depth,
+//                      item); per ancestor, in item order, v = f32(f32(v) + change).
+// Sorting is an LDS bitonic sort of (node << 13 | item) keys; a node's chain is one thread's
+// sequential loop (the root's is the whole batch: B dependent adds).  The leaf max/min tracking
+// (k_per_update) is unchanged: comparisons and leaves are the same under both numpy versions.
+// ---------------------------------------------------------------------------------------
+constexpr int PER_CHAIN_NT = 1024;
+
+__device__ __forceinline__ void chain_sort(unsigned long long* keys, int N2) {
+    for (int k = 2; k <= N2; k <<= 1)
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            for (int i = threadIdx.x; i < N2; i += PER_CHAIN_NT) {
+                const int ixj = i ^ j;
+                if (ixj > i) {
+                    const unsigned long long x = keys[i], y = keys[ixj];
+                    if ((x > y) == ((i & k) == 0)) {
+                        keys[i] = y;
+                        keys[ixj] = x;
+                    }
+                }
+            }
+            __syncthreads();
+        }
+}
+
+template <bool LEAF>
+__global__ __launch_bounds__(PER_CHAIN_NT) void k_per_chain(PerUpdateArgs a) {
+    extern __shared__ unsigned long long keys[];   // [N2], then (ancestor pass) [n] float changes
+    const int n = a.n, tid = threadIdx.x;
+    int N2 = 1;
+    while (N2 < n) N2 <<= 1;
+    float* chg = reinterpret_cast<float*>(keys + N2);
+    const int depth = blockIdx.x;   // ancestor pass: the tree depth this workgroup owns
+    for (int u = tid; u < N2; u += PER_CHAIN_NT) {
+        unsigned long long k = ~0ull;
+        if (u < n) {
+            int64_t node = a.wl[u];
+            if (!LEAF) {
+                const int dn = 63 - __clzll((unsigned long long)(node + 1));   // depth of the leaf
+                node = dn > depth ? ((node + 1) >> (dn - depth)) - 1 : -1;
+                chg[u] = a.wchg[u];
+            }
+            if (node >= 0) k = ((unsigned long long)node << 13) | (unsigned)u;
+        }
+        keys[u] = k;
+    }
+    __syncthreads();
+    chain_sort(keys, N2);
+    for (int i = tid; i < n; i += PER_CHAIN_NT) {
+        const unsigned long long k = keys[i];
+        if (k == ~0ull) continue;
+        const int64_t node = (int64_t)(k >> 13);
+        if (i > 0 && (int64_t)(keys[i - 1] >> 13) == node) continue;   // not the start of a chain
+        if (LEAF) {
+            float prev = (float)a.winit[(int)(k & 8191u)];   // the leaf before this chunk
+            for (int j = i; j < n && (int64_t)(keys[j] >> 13) == node; j++) {
+                const int u = (int)(keys[j] & 8191u);
+                const float p = a.wp[u];
+                a.wchg[u] = p - prev;   // float32 subtraction
+                prev = p;
+            }
+            a.tree[node] = (double)prev;
+        } else {
+            float v = (float)a.tree[node];
+            for (int j = i; j < n && (int64_t)(keys[j] >> 13) == node; j++) v = v + chg[(int)(keys[j] & 8191u)];
+            a.tree[node] = (double)v;
+        }
+    }
+}
+
+// the ancestor pass needs up to 96 KB of dynamic LDS: raise the limit once, outside any
+// stream capture (dqnx_engine_create with per_numpy121)
+int per_numpy121_init() {
+    DQNX_HIP_CHECK(hipFuncSetAttribute((const void*)k_per_chain<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       PER_CHUNK * 12));
+    DQNX_HIP_CHECK(hipFuncSetAttribute((const void*)k_per_chain<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       PER_CHUNK * 12));
+    return DQNX_OK;
+}
+
 int launch_per_sample(const PerSampleArgs& a, hipStream_t s) {
     if (a.Bg < 1 || a.Bg > PER_MAX_B) return set_error(DQNX_EUNSUPPORTED, "PER batch %d outside [1, %d]", a.Bg, PER_MAX_B);
     const int G = (a.Bg + PER_SNT - 1) / PER_SNT;
@@ -594,7 +683,17 @@ int launch_per_update(const PerUpdateArgs& a, hipStream_t s) {
     const int g = (a.n + PER_GT - 1) / PER_GT;
     hipLaunchKernelGGL(k_per_prep, dim3(g), dim3(PER_GT), 0, s, a);
     hipLaunchKernelGGL(k_per_update, dim3(1), dim3(PER_NT), 0, s, a);
-    hipLaunchKernelGGL(k_per_prop, dim3(g), dim3(PER_GT), 0, s, a);
+    if (a.numpy121 && a.mode == 0) {   // float32 change / ancestor sums in update order
+        int N2 = 1;
+        while (N2 < a.n) N2 <<= 1;
+        int depths = 0;   // internal depths 0 .. (deepest leaf depth - 1)
+        while (((int64_t)1 << (depths + 1)) <= 2 * a.cap - 1) depths++;
+        hipLaunchKernelGGL(k_per_chain<true>, dim3(1), dim3(PER_CHAIN_NT), (size_t)N2 * 8, s, a);
+        if (depths > 0)
+            hipLaunchKernelGGL(k_per_chain<false>, dim3(depths), dim3(PER_CHAIN_NT), (size_t)N2 * 8 + (size_t)a.n * 4, s, a);
+    } else {
+        hipLaunchKernelGGL(k_per_prop, dim3(g), dim3(PER_GT), 0, s, a);
+    }
     DQNX_HIP_CHECK(hipGetLastError());
     return DQNX_OK;
 }

@@ -61,7 +61,7 @@ class Config(ctypes.Structure):
         ("local_sampling", I32), ("per_eps", ctypes.c_double), ("per_alpha", ctypes.c_double),
         ("per_max_priority", ctypes.c_double), ("per_beta_start", ctypes.c_double),
         ("per_beta_end", ctypes.c_double), ("per_beta_steps", ctypes.c_double),
-        ("compute_dtype", I32), ("reserved1", I32),
+        ("compute_dtype", I32), ("per_numpy121", I32),
     ]
 
 

@@ -58,6 +58,17 @@ def _obs_dim(input_dim) -> int:
     return int(input_dim)
 
 
+def _per_numpy121() -> bool:
+    """The SumTree arithmetic the reference would run with under THIS interpreter's numpy: the
+    reference's float32 priorities make `change` and the ancestor sums float32 under numpy < 2's
+    value-based casting (its pinned 1.21) and float64 under numpy >= 2 (NEP 50).
+    DQNX_PER_NUMPY121=0/1 overrides."""
+    v = os.environ.get("DQNX_PER_NUMPY121")
+    if v is not None:
+        return v not in ("", "0")
+    return int(np.__version__.split(".")[0]) < 2
+
+
 def _check_optim_loss(network):
     """The engine implements torch.optim.Adam (default betas / eps, no weight decay, no amsgrad)
     and nn.SmoothL1Loss (beta 1).  network_config may name others (R:env/custom_env/macro with
@@ -122,7 +133,7 @@ class Agent:
         self._build()
 
     # -- composition (R:dqn/agent.py:275-320) ------------------------------------------
-    def _build(self):
+    def _build(self):   # noqa: C901
         cls = type(self)._network_cls
         # same construction order as the reference: online, then target (torch RNG stream)
         self.online_network = cls(self.device, self.lr, self.nn_conf_func, self.input_dim, self.output_dim,
@@ -135,7 +146,8 @@ class Agent:
         self.engine = LearnEngine(spec, type(self).__name__, self.batch_size, self.buffer_size, gamma=self.gamma,
                                   lr=self.lr, tau=self.target_soft_update_tau, n_env=self.n_env, device=self.device,
                                   eps_dec=self.epsilon_decay,
-                                  compute_dtype=os.environ.get("DQNX_COMPUTE_DTYPE", "fp32"))
+                                  compute_dtype=os.environ.get("DQNX_COMPUTE_DTYPE", "fp32"),
+                                  per_numpy121=_per_numpy121())
         self.online_network.bind_flat(self.engine.param_views(self.engine.params), self.engine.params, spec,
                                       engine=self.engine)
         self.target_network.bind_flat(self.engine.param_views(self.engine.target_params), self.engine.target_params,

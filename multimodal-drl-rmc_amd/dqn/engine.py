@@ -209,7 +209,9 @@ class LearnEngine:
 
     def __init__(self, spec: NetSpec, algo: str, batch: int, capacity: int, gamma=0.99, lr=1e-4,
                  tau=1e-3, n_env=1, world_size=1, rank=0, device=None, graphs=True, eps_dec=2e6,
-                 local_sampling=False, compute_dtype="fp32"):
+                 local_sampling=False, compute_dtype="fp32", per_numpy121=False):
+        """per_numpy121: PER SumTree arithmetic of the reference's pinned numpy 1.21 (float32
+        `change` and float32-rounded ancestor sums, in update order) instead of numpy >= 2's."""
         if not torch.cuda.is_available():
             raise RuntimeError("libdqnx needs a ROCm GPU (MI355X / gfx950); there is no CPU fallback")
         self.L = C.lib()
@@ -227,6 +229,7 @@ class LearnEngine:
         if compute_dtype not in ("fp32", "bf16"):
             raise ValueError(f"compute_dtype must be 'fp32' or 'bf16', got {compute_dtype!r}")
         cfg.compute_dtype = C.DQNX_COMPUTE_BF16 if compute_dtype == "bf16" else C.DQNX_COMPUTE_FP32
+        cfg.per_numpy121 = 1 if per_numpy121 else 0
         self.compute_dtype = compute_dtype
         self.cfg = cfg
         h = ctypes.c_void_p()

@@ -316,9 +316,18 @@ class NaiveReplay:
 
 
 class SumTree:
-    """SumTree (R:dqn/utils/sum_tree.py:4-73), numpy>=2 float64 semantics."""
+    """SumTree (R:dqn/utils/sum_tree.py:4-73), numpy>=2 float64 semantics by default.
 
-    def __init__(self, capacity: int):
+    numpy121=True restates the reference's pinned numpy 1.21 (R:bin/environment.yml) for the
+    float32 (1,)-array priorities update_batch_priorities passes (R:dqn/replay_memory.py:95-98):
+    value-based casting casts the float64 tree scalar down, so `change = priority - tree[i]`
+    (:18) and `tree[parent] += change` (:31-32) are float32 operations whose results are stored
+    back into the float64 tree.  Pushes (float64 scalar priorities, :34-40) stay float64 under
+    both versions.  numpy 1.21 is not installed here: this mode is a restatement of the casting
+    rules (parity unpinned against a numpy 1.21 run)."""
+
+    def __init__(self, capacity: int, numpy121: bool = False):
+        self.numpy121 = numpy121
         self.capacity = capacity
         self.tree = np.zeros(2 * capacity - 1)
         self.data = [None] * capacity
@@ -327,11 +336,16 @@ class SumTree:
         self.max_priority_index = capacity - 1
         self.min_priority_index = capacity - 1
 
-    def update(self, tree_index: int, priority: float):        # :15-32
+    def update(self, tree_index: int, priority: float, f32: bool = False):   # :15-32
         tree = self.tree
         max_p, min_p = tree[self.max_priority_index], tree[self.min_priority_index]
-        priority = float(priority)
-        change = priority - tree[tree_index]
+        f32 = f32 and self.numpy121
+        if f32:   # numpy 1.21: float32 array minus float64 scalar -> float32
+            priority = float(np.float32(priority))
+            change = np.float32(np.float32(priority) - np.float32(tree[tree_index]))
+        else:
+            priority = float(priority)
+            change = priority - tree[tree_index]
         tree[tree_index] = priority
         lo, hi = self.capacity - 1, self.capacity + self.size - 1
         if priority >= max_p:
@@ -344,7 +358,10 @@ class SumTree:
             self.min_priority_index = int(np.argmin(tree[lo:hi])) + lo
         while tree_index != 0:
             tree_index = (tree_index - 1) // 2
-            tree[tree_index] += change
+            if f32:   # float64 scalar + float32 array -> float32, stored into the float64 tree
+                tree[tree_index] = float(np.float32(np.float32(tree[tree_index]) + change))
+            else:
+                tree[tree_index] += change
 
     def add(self, priority: float, data):                      # :34-40
         tree_index = self.data_pointer + self.capacity - 1
@@ -385,11 +402,12 @@ class SumTree:
 class PerReplay:
     """ReplayMemoryPrioritized (R:dqn/replay_memory.py:43-98)."""
 
-    def __init__(self, buffer_size: int, batch_size: int, eps_dec: float, pow_mode: str = "numpy"):
+    def __init__(self, buffer_size: int, batch_size: int, eps_dec: float, pow_mode: str = "numpy",
+                 numpy121: bool = False):
         self.pow_mode = pow_mode
         self.batch_size = batch_size
         self.buffer_size = buffer_size
-        self.replay_buffer = SumTree(buffer_size)
+        self.replay_buffer = SumTree(buffer_size, numpy121=numpy121)
         self.epsilon = 0.0001
         self.alpha = 0.6
         self.beta_start = 0.4
@@ -441,8 +459,8 @@ class PerReplay:
 
     def update_batch_priorities(self, tree_indices, abs_td_errors_np):  # :94-98
         pr = self.priorities(abs_td_errors_np).reshape(-1)
-        for i, p in zip(tree_indices, pr):
-            self.replay_buffer.update(int(i), float(p))
+        for i, p in zip(tree_indices, pr):   # float32 (1,) arrays in the reference
+            self.replay_buffer.update(int(i), float(p), f32=True)
 
 
 def transitions_to_tensor(transitions):
@@ -512,7 +530,7 @@ class OracleLearner:
     def __init__(self, spec: NetSpec, algo: str, batch_size: int, buffer_size: int,
                  lr=1e-4, gamma=0.99, tau=1e-3, n_env=1, soft_update=True,
                  update_target_frequency=30000, eps_dec=2e6, seed=0, params=None, per_pow="numpy",
-                 compute="fp32"):
+                 compute="fp32", per_numpy121=False):
         assert algo in ALGOS and compute in ("fp32", "bf16")
         self.bf16 = compute == "bf16"
         self.spec, self.algo = spec, algo
@@ -528,7 +546,7 @@ class OracleLearner:
         self.adam_step = 0
         self.step = 0
         self.per = algo == "PerDuelingDoubleDQNAgent"
-        self.replay = PerReplay(buffer_size, batch_size, eps_dec, per_pow) if self.per \
+        self.replay = PerReplay(buffer_size, batch_size, eps_dec, per_pow, per_numpy121) if self.per \
             else NaiveReplay(buffer_size, batch_size)
         self.py_state = py_state_to_array(random.getstate())
         self.np_state = np_state_to_array(np.random.get_state())

@@ -43,9 +43,9 @@ def assert_tree_equal(eng, st: O.SumTree, exact=True):
                                                                          st.min_priority_index)
 
 
-def per_engine(obs_dim, batch, cap, graphs=True):
+def per_engine(obs_dim, batch, cap, graphs=True, numpy121=False):
     E = _E()
-    return E.LearnEngine(E.mlp_spec(obs_dim, 8, "dueling"), ALGO, batch, cap, graphs=graphs)
+    return E.LearnEngine(E.mlp_spec(obs_dim, 8, "dueling"), ALGO, batch, cap, graphs=graphs, per_numpy121=numpy121)
 
 
 def test_gpu_per_push_matches_sumtree_add():
@@ -208,3 +208,77 @@ def test_gpu_per_graph_and_eager_identical():
     torch.cuda.synchronize()
     assert torch.equal(e1.params, e2.params)
     assert torch.equal(e1.sumtree, e2.sumtree)
+
+
+@pytest.mark.parametrize("cap,fill,n,rounds", [(500, 300, 64, 40), (20000, 20000, 5000, 3), (30000, 30000, 12000, 2)])
+def test_gpu_per_numpy121_updates_match_float32_semantics(cap, fill, n, rounds):
+    """per_numpy121: update_batch_priorities with the reference's pinned numpy 1.21 arithmetic
+    (float32 `change`, float32-rounded ancestor sums, in update order; oracle SumTree(numpy121))
+    -- duplicates, rescans, pushes between rounds (float64 under both versions), chunked
+    launches; the tree compared with ==.  The numpy >= 2 tree differs from it (checked), so the
+    mode is not a no-op."""
+    eng = per_engine(14, 32, cap, numpy121=True)
+    rep = O.PerReplay(cap, 32, 2e6, "cr", numpy121=True)
+    ref2 = O.PerReplay(cap, 32, 2e6, "cr")
+    data = O.synth_transitions(fill, 14, 8, seed=16)
+    eng.push(*data)
+    list(rep.store_transitions(*data))
+    list(ref2.store_transitions(*data))
+    rng = np.random.default_rng(17)
+    st = rep.replay_buffer
+    for r in range(rounds):
+        slots = rng.integers(0, fill, size=n).astype(np.int32)
+        slots[rng.integers(0, n, size=n // 8)] = slots[0]                   # duplicates
+        absd = (rng.random(n).astype(np.float32) * np.float32(3.0)) ** 3
+        k = rng.integers(0, n, size=2)
+        slots[k[0]] = st.max_priority_index - (cap - 1)                     # lower the max leaf
+        absd[k[0]] = np.float32(1e-3)
+        slots[k[1]] = st.min_priority_index - (cap - 1)                     # raise the min leaf
+        absd[k[1]] = np.float32(5.0)
+        eng.per_update_priorities(torch.from_numpy(slots), torch.from_numpy(absd))
+        idx = (slots.astype(np.int64) + cap - 1).tolist()
+        rep.update_batch_priorities(idx, absd.reshape(-1, 1))
+        ref2.update_batch_priorities(idx, absd.reshape(-1, 1))
+        torch.cuda.synchronize()
+        assert_tree_equal(eng, st)
+        if r == 0:
+            extra = O.synth_transitions(17, 14, 8, seed=100 + r)               # a push between rounds
+            eng.push(*extra)
+            list(rep.store_transitions(*extra))
+            list(ref2.store_transitions(*extra))
+            torch.cuda.synchronize()
+            assert_tree_equal(eng, st)
+    assert not np.array_equal(st.tree, ref2.replay_buffer.tree)
+
+
+def test_gpu_per_numpy121_learn_steps_match_oracle():
+    """PerDuelingDoubleDQNAgent learn steps in numpy 1.21 mode against the oracle in the same
+    mode: sampled leaves (the descent reads the float32-rounded sums), IS weights through the
+    loss, the tree after every step's priority update."""
+    E = _E()
+    cap, fill, batch, seed = 3000, 2500, 256, 23
+    spec = O.mlp_spec(14, 8, "dueling")
+    init = O.reference_init(spec, seed)
+    oracle = O.OracleLearner(spec, ALGO, batch, cap, seed=seed, params=init, per_pow="cr", per_numpy121=True)
+    data = O.synth_transitions(fill, 14, 8, seed=seed + 100)
+    O.fill_replay(oracle, *data)
+    eng = E.LearnEngine(E.mlp_spec(14, 8, "dueling"), ALGO, batch, cap, per_numpy121=True)
+    eng.load_params(init)
+    eng.push(*data)
+    import random
+    random.seed(seed + 7)
+    st = O.py_state_to_array()
+    oracle.py_state = st.copy()
+    eng.set_rng(0, st)
+    np.random.seed(seed + 11)
+    nps = O.np_state_to_array()
+    oracle.np_state = nps.copy()
+    eng.set_rng(1, nps)
+    for step in range(4):
+        rec = oracle.train_step()
+        eng.learn_step(soft_update=True)
+        torch.cuda.synchronize()
+        eng.check_device_error()
+        assert np.array_equal(eng.batch_idx.cpu().numpy().astype(np.int64) + cap - 1, rec.positions), step
+        assert abs(eng.loss() - rec.loss) <= 1e-5 * max(1.0, abs(rec.loss))
+        assert_tree_equal(eng, oracle.replay.replay_buffer, exact=False)
