@@ -61,6 +61,15 @@ __device__ __forceinline__ T gld(const T* p) {
 }
 
 
+// Raw buffer descriptor for a wave-uniform base (bytes = the range; offsets at or past it read 0)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t wave_rsrc(const float* base, uint32_t bytes) {
+    const uint64_t b = (uint64_t)base;
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)b);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(b >> 32));
+    return __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)hi << 32) | lo), 0,
+                                             __builtin_amdgcn_readfirstlane(bytes), 0x00020000);
+}
+
 // XCD-aware block remap (CDNA guide T1): blocks are dealt round-robin over the 8 XCDs, so
 // hand XCD x a CONTIGUOUS range of tiles (bijective for any total).  Speed only: placement
 // never affects results.

@@ -656,6 +656,33 @@ bool adam_keeps_blk(const dqnx_engine* e) {
     return true;
 }
 
+// Fused plan, fp32: every dW over the full (local) minibatch + Adam + blocked copies in one
+// launch (k_dw_adam16) instead of split-K slabs + the Adam pass, up to 2048 rows per GPU.
+// Measured on MI355X, MLP-284: B = 1024 step 46.8 -> 43.7 us (dW + Adam 8.5 + 5.1 -> 10.6 us);
+// at B = 4096 the slabs win (18.7 + 6.7 vs 26.3 us: the full-K tiles re-read dZ and X from L2
+// per 16 x 16 tile, the split-K slices spread the rows over more workgroups).
+// DQNX_DW_ADAM16=0 / 1 forces the slab plan / this kernel.  GRADS_ONLY steps run it in
+// gradient mode (so world-1 DP equals the single-GPU step bitwise).
+bool dw_adam16_on(const dqnx_engine* e, int flags) {
+    (void)flags;
+    if (e->bwd_plan != 2 || e->fplan.bf16) return false;
+    if (const char* v = getenv("DQNX_DW_ADAM16")) {
+        if (atoi(v) == 0) return false;
+    } else if (e->Bl > 2048) {
+        return false;
+    }
+    for (const LayerPlan& lp : e->np.dense)
+        if (lp.out % 16) return false;   // chain blocks tile `out` by 16
+    return e->np.NH <= 16;
+}
+
+// the weight update of a step with these flags keeps the fused plan's blocked copies current
+static bool blk_kept(const dqnx_engine* e, int flags) {
+    // (a GRADS_ONLY step: the update is dqnx_apply_grads' Adam pass)
+    if (flags & DQNX_STEP_GRADS_ONLY) return adam_keeps_blk(e);
+    return adam_keeps_blk(e) || dw_adam16_on(e, flags);
+}
+
 void fill_blk_layers(dqnx_engine* e, AdamArgs& aa) {
     aa.nblk = 0;
     if (!adam_keeps_blk(e)) return;
@@ -982,6 +1009,78 @@ void build_fused_steps(dqnx_engine* e, int flags, int32_t* idx, int32_t* phys, s
             h.A = A;
             flops += 2.0 * Bl * np.NH * (np.F + 1.0);
             bytes += 4.0 * (16.0 * Bl + Bl * np.F + ba.dw_slices * (double)np.head_params);
+        }
+        if (dw_adam16_on(e, flags)) {   // full-minibatch 16 x 16 tiles + Adam + blocked copies
+            DwAdam16Args da;
+            memset(&da, 0, sizeof(da));
+            int tiles = 0;
+            auto add = [&](const DwProblem& p, int64_t poff, int l) {
+                DwAdam16Layer& d = da.L[da.nl++];
+                d.dZ = p.dZ;
+                d.ldz = p.ldz;
+                d.X = p.X;
+                d.ldx = p.ldx;
+                d.in = p.in;
+                d.out = p.out;
+                d.poff = poff;
+                d.head_kind = p.head_kind;
+                d.A = p.A;
+                d.ti = (p.in + 15) / 16;
+                d.t0 = tiles;
+                tiles += d.ti * ((p.out + 15) / 16);
+                if (l >= 0) {
+                    d.fwd_online = at<float>(e, e->ws_wblk[0][l]);
+                    d.fwd_target = at<float>(e, e->ws_wblk[1][l]);
+                    d.chain = l >= 1 ? at<float>(e, e->ws_wblkT[l]) : nullptr;
+                    d.nch_fwd = e->fplan.kpad[l] / 16;
+                    d.nch_chain = np.dense[l].out / 16;
+                }
+            };
+            for (int q = 0; q < ba.ndw; q++) {   // dense layers last-first, then the head
+                const int l = q < L ? L - 1 - q : -1;
+                add(ba.dw[q], l >= 0 ? np.dense[l].off : np.head_off, l);
+            }
+            AdamArgs aa;
+            adam_kstep(e, flags, &aa);
+            da.tiles = tiles;
+            da.Bl = e->Bl;
+            da.mode = aa.mode;
+            da.soft = aa.soft;
+            da.n_params = np.P;
+            da.p = aa.p;
+            da.m = aa.m;
+            da.v = aa.v;
+            da.grads = aa.grads;
+            da.target = aa.target;
+            da.ctrl = aa.ctrl;
+            da.w1 = aa.w1;
+            da.beta2 = aa.beta2;
+            da.c2 = aa.c2;
+            da.eps = aa.eps;
+            da.tau = aa.tau;
+            da.one_minus_tau = aa.one_minus_tau;
+            da.loss_partial = aa.loss_partial;
+            da.n_loss_partial = aa.n_loss_partial;
+            da.batch_global = aa.batch_global;
+            da.mtc = aa.mtc;
+            da.mtc_blocks = aa.mtc_blocks;
+            da.stamps = at<int64_t>(e, e->ws_stamps);
+            const double P = (double)np.P;
+            KStep k;
+            k.name = da.mode ? "dw_adam16" : "dw16_grads";
+            k.flops = flops + (da.mode ? 12.0 * P : 0.0);
+            // dZ / X rows once; p, m, v read and written, grads written (+ target read and
+            // written); the blocked copies: fwd online (+ fwd target), chain for l >= 1
+            double ops = Bl * (16.0 + np.F), blk = 0;
+            for (int l = 0; l < L; l++) {
+                const double w = (double)np.dense[l].out * np.dense[l].in;
+                ops += Bl * (np.dense[l].out + np.dense[l].in);
+                blk += w * (da.soft ? 2.0 : 1.0) + (l >= 1 ? w : 0.0);
+            }
+            k.bytes = 4.0 * (ops + (da.mode ? 7.0 * P + (da.soft ? 2.0 * P : 0.0) + blk : P));
+            k.run = [=](hipStream_t s) { return launch_dw_adam16(da, s); };
+            ks.push_back(k);
+            return;
         }
         if (e->fplan.bf16) {   // bf16 operands, fp32 slabs: the same Adam pass follows
             dw_bf16_grid(ba);
@@ -1837,13 +1936,17 @@ int dp_buckets(dqnx_engine* e, std::vector<DpBucket>& out) {
     const NetPlan& np = e->np;
     const int NC = (int)np.conv.size();
     const std::vector<KStep>& ks = steps_for(e, DQNX_STEP_GRADS_ONLY);
-    const int nk = (int)ks.size() - 1;   // the last kernel is the whole-gradient slab sum
+    // the last kernel is the whole-gradient slab sum, or (fused plan, k_dw_adam16 in gradient
+    // mode) the kernel that writes the gradient itself
+    const bool direct = ks.back().name == "dw16_grads";
+    const int nk = (int)ks.size() - (direct ? 0 : 1);
     auto find = [&](const std::string& nm, int from) {
         for (int k = from; k < nk; k++)
             if (ks[k].name == nm) return k;
         return -1;
     };
-    if (NC == 0) {
+    if (NC == 0 || direct) {
+        if (direct && NC) return set_error(DQNX_EUNSUPPORTED, "dp buckets: fused dW plan with convs");
         out.push_back({0, nk, 0, np.P});
         return DQNX_OK;
     }
@@ -2318,7 +2421,7 @@ int dqnx_learn_step(dqnx_engine* e, int32_t flags, void* stream) {
     const int base = flags & (DQNX_STEP_SOFT_UPDATE | DQNX_STEP_GIVEN_INDICES | DQNX_STEP_GRADS_ONLY);
     if (!prefetch && !e->pf_valid) {
         // the weights changed outside the Adam pass: this step's sampler launch rebuilds the copies
-        const int key = base | ((e->bwd_plan == 2 && (e->wblk_dirty || !adam_keeps_blk(e))) ? KEY_RELAYOUT : 0);
+        const int key = base | ((e->bwd_plan == 2 && (e->wblk_dirty || !blk_kept(e, base))) ? KEY_RELAYOUT : 0);
         const std::vector<KStep>& ks = steps_for(e, key);
         rc = run_graphed(e, key, s, [&](hipStream_t cs) { return enqueue_range(ks, 0, (int)ks.size(), cs); });
         if (!rc) e->wblk_dirty = false;
@@ -2479,6 +2582,7 @@ int dqnx_apply_grads(dqnx_engine* e, int32_t flags, void* stream) {
     int rc = check_bound(e);
     if (rc) return rc;
     const int key = 0x100 | (flags & DQNX_STEP_SOFT_UPDATE);
+    if (!adam_keeps_blk(e)) e->wblk_dirty = true;   // this Adam pass leaves the blocked copies behind
     return run_graphed(e, key, (hipStream_t)stream, [&](hipStream_t s) { return enqueue_apply(e, key, s); });
 }
 
@@ -2519,13 +2623,14 @@ int dqnx_learn_step_bucket(dqnx_engine* e, int32_t flags, int32_t bucket, void* 
     if (bucket == 0 && e->ring_size < e->Bs)
         return set_error(DQNX_EINVAL, "Sample larger than population: %lld < %d", (long long)e->ring_size, e->Bs);
     // the plan of a plain GRADS_ONLY step (blocked-weight rebuild as that step decides)
-    const int key = DQNX_STEP_GRADS_ONLY | ((e->bwd_plan == 2 && (e->wblk_dirty || !adam_keeps_blk(e))) ? KEY_RELAYOUT : 0);
+    const int key = DQNX_STEP_GRADS_ONLY | ((e->bwd_plan == 2 && (e->wblk_dirty || !blk_kept(e, DQNX_STEP_GRADS_ONLY))) ? KEY_RELAYOUT : 0);
     const std::vector<KStep>& ks = steps_for(e, key);
     const std::vector<KStep>& k0 = steps_for(e, DQNX_STEP_GRADS_ONLY);
     if (ks.size() != k0.size()) return set_error(DQNX_ESTATE, "dp buckets: plan mismatch");
     rc = enqueue_range(ks, b[bucket].k0, b[bucket].k1, s);
     if (rc) return rc;
     if (bucket == 0) e->wblk_dirty = false;
+    if (ks.back().name == "dw16_grads") return DQNX_OK;   // it wrote the gradient and the loss
     AdamArgs aa;
     adam_kstep(e, DQNX_STEP_GRADS_ONLY, &aa);   // mode 0: this bucket's slab sums into DQNX_BUF_GRADS
     aa.e0 = b[bucket].first;
@@ -2551,6 +2656,7 @@ int dqnx_apply_grads_bucket(dqnx_engine* e, int32_t flags, int32_t bucket, void*
         rc = enqueue_per_update(e, at<int32_t>(e, e->off[DQNX_BUF_BATCH_IDX]), s);
         if (rc) return rc;
     }
+    if (!adam_keeps_blk(e)) e->wblk_dirty = true;
     AdamArgs aa;
     adam_kstep(e, DQNX_STEP_GRADS_ONLY, &aa);
     aa.mode = 2;

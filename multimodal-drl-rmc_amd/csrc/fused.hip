@@ -67,13 +67,6 @@ __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(
 // touching memory (the prefetch overrun past the last chunk needs no branch).
 constexpr uint32_t kOOB = 0x80000000u;
 
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t wave_rsrc(const float* base, uint32_t bytes) {
-    const uint64_t b = (uint64_t)base;
-    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)b);
-    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(b >> 32));
-    return __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)hi << 32) | lo), 0,
-                                             __builtin_amdgcn_readfirstlane(bytes), 0x00020000);
-}
 __device__ __forceinline__ float4 bld4(__amdgpu_buffer_rsrc_t r, uint32_t off) {
     const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
     return make_float4(__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z), __uint_as_float(v.w));

@@ -865,6 +865,206 @@ __global__ __launch_bounds__(256) void k_adam4(AdamArgs a) {
     if (a.mode == 2 && a.with_loss && blockIdx.x == 0 && threadIdx.x == 0) a.ctrl->loss = a.grads[P];
 }
 
+// =====================================================================================
+// Fused plan, fp32: weight gradients + Adam (+ soft update, + blocked copies) in one launch.
+// One 512-thread workgroup per 16 x 16 parameter tile of a dense layer or the head; its 8 waves
+// split the minibatch, every wave streams its rows of dZ and X straight into MFMA operands
+// (an element of either feeds exactly one v_mfma_f32_16x16x4_f32 of a 16 x 16 tile, so nothing
+// is staged in LDS), and the 8 partial tiles are summed through LDS in wave order: the gradient
+// is final inside the workgroup (deterministic, no split-K slabs, no separate optimizer pass).
+// Tiles with i-block 0 also sum dZ's column (the bias).  The epilogue is k_adam's per-element
+// arithmetic, and writes the tile's fwd- / chain-blocked copies (one 16 x 16 block each), so
+// the next step's forward needs no rebuild.  Reference: loss.backward() + optimizer.step()
+// (R:dqn/agent.py:224-226), soft update R:dqn/agent.py:105-110.
+// =====================================================================================
+__device__ __forceinline__ int64_t dw16_index(const DwAdam16Layer& d, int row, int col) {
+    if (d.head_kind < 0) return d.poff + ((col < d.in) ? (int64_t)row * d.in + col : (int64_t)d.out * d.in + row);
+    return d.poff + ((col < d.in) ? (int64_t)head_w_off(d.head_kind, row, d.in) + col
+                                  : (int64_t)head_b_off(d.head_kind, row, d.in, d.A));
+}
+
+template <int DW16_NW, int U>   // waves per tile; k-steps (4 rows each) per register set, two sets in flight
+__global__ __launch_bounds__(64 * DW16_NW) void k_dw_adam16(DwAdam16Args a) {
+    __shared__ floatx4 red[DW16_NW][64];
+    __shared__ float redb[DW16_NW][64];
+    const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int i = lane & 15, g = lane >> 4;
+    if (a.mtc && (int)blockIdx.x == a.tiles) {   // the extra workgroup: sampler cache for the next step
+        mt_cache_extend(a.mtc, a.mtc_blocks);
+        return;
+    }
+    DQNX_STAMP(a.stamps, 56);
+    const int T = xcd_remap(blockIdx.x, a.tiles);
+    // the tile's layer: every first-tile index read at once, then one (scalar) load of the layer
+    // (a chain of per-layer selects serialises a kernel-argument round trip per layer)
+    int li = 0;
+#pragma unroll
+    for (int q = 1; q <= DQNX_MAX_DENSE; q++) li += (q < a.nl && T >= a.L[q].t0) ? 1 : 0;
+    li = __builtin_amdgcn_readfirstlane(li);
+    const DwAdam16Layer d = a.L[li];
+    const int t = T - d.t0;
+    const int ob = t / d.ti, ib = t - ob * d.ti;
+    const int o0 = ob * 16, i0 = ib * 16;
+
+    // (0) this thread's parameters: slot q = tid + j NT of the tile's 256 weights (q < 256) and
+    //     16 biases (q = 256 + row, tiles with ib == 0), with their optimizer state, fetched
+    //     before the K loop so the latency hides under it
+    constexpr int NT = 64 * DW16_NW, NS = (272 + NT - 1) / NT;
+    int row[NS], col[NS];
+    bool own[NS];
+    int64_t e[NS];
+    float p[NS], m[NS], v[NS], tg[NS];
+#pragma unroll
+    for (int j = 0; j < NS; j++) {
+        const int q = tid + j * NT;
+        if (q < 256) {
+            row[j] = o0 + (q >> 4);
+            col[j] = i0 + (q & 15);
+            own[j] = row[j] < d.out && col[j] < d.in;
+        } else {
+            row[j] = o0 + q - 256;
+            col[j] = d.in;
+            own[j] = ib == 0 && q < 272 && row[j] < d.out;
+        }
+        e[j] = own[j] ? dw16_index(d, row[j], col[j]) : 0;
+        p[j] = m[j] = v[j] = tg[j] = 0.f;
+        if (own[j] && a.mode) {
+            p[j] = gld(a.p + e[j]);
+            m[j] = gld(a.m + e[j]);
+            v[j] = gld(a.v + e[j]);
+            if (a.soft) tg[j] = gld(a.target + e[j]);
+        }
+    }
+    const float step_size = gld(&a.ctrl->adam_step_size), bc2s = gld(&a.ctrl->adam_bc2_sqrt);
+    DQNX_STAMP(a.stamps, 57);
+
+    // (1) dW tile = dZ[:, o0:o0+16]^T X[:, i0:i0+16] over this wave's rows; lane (i, g) supplies
+    //     dZ[b][o0 + i] and X[b][i0 + i] of row b = 4 s + g at k-step s.  Loads go through
+    //     wave-uniform buffer descriptors bounded at Bl rows: rows past the batch read zero
+    //     without a branch.  Columns past the layer are clamped (their accumulator rows /
+    //     columns are never stored).  A wave owns a multiple of 2U k-steps, so the loop has no
+    //     tail.
+    const int nsteps = (a.Bl + 3) >> 2;
+    const int spw = ((nsteps + DW16_NW - 1) / DW16_NW + 2 * U - 1) / (2 * U) * (2 * U);
+    const int s0 = wid * spw;
+    const int iters = s0 < nsteps ? spw / (2 * U) : 0;
+    const __amdgpu_buffer_rsrc_t zr = wave_rsrc(d.dZ, (uint32_t)a.Bl * d.ldz * 4u);
+    const __amdgpu_buffer_rsrc_t xr = wave_rsrc(d.X, (uint32_t)a.Bl * d.ldx * 4u);
+    uint32_t zo = (uint32_t)((4 * s0 + g) * d.ldz + min(o0 + i, d.out - 1)) * 4u;
+    uint32_t xo = (uint32_t)((4 * s0 + g) * d.ldx + min(i0 + i, d.in - 1)) * 4u;
+    const uint32_t zs = 16u * d.ldz, xs = 16u * d.ldx;   // bytes per k-step (4 rows)
+    floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+    float bs = 0.f;
+    float za[U], xa[U], zb[U], xb[U];
+    auto load = [&](float* z, float* x) {
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            z[u] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(zr, zo + u * zs, 0, 0));
+            x[u] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xr, xo + u * xs, 0, 0));
+        }
+        zo += U * zs;
+        xo += U * xs;
+    };
+    auto comp = [&](const float* z, const float* x) {
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            acc = mfma16x16x4(z[u], x[u], acc);
+            bs += z[u];
+        }
+    };
+    if (iters > 0) {
+        load(za, xa);
+        for (int it = 0;; it++) {
+            load(zb, xb);
+            __builtin_amdgcn_sched_barrier(0);
+            comp(za, xa);
+            __builtin_amdgcn_sched_barrier(0);
+            if (it + 1 == iters) {   // (wave-uniform) no prefetch past the wave's rows
+                comp(zb, xb);
+                break;
+            }
+            load(za, xa);
+            __builtin_amdgcn_sched_barrier(0);
+            comp(zb, xb);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    }
+    DQNX_STAMP(a.stamps, 58);
+    red[wid][lane] = acc;
+    redb[wid][lane] = bs;
+    __syncthreads();
+
+    DQNX_STAMP(a.stamps, 59);
+    // (2) fixed-order sum of the wave partials, then k_adam's per-element update
+#pragma unroll
+    for (int j = 0; j < NS; j++) {
+        if (!own[j]) continue;
+        const int q = tid + j * NT;
+        float gsum;
+        if (q < 256) {
+            const float* rf = reinterpret_cast<const float*>(&red[0][0]);
+            const int rr = q >> 4, off = ((rr >> 2) * 16 + (q & 15)) * 4 + (rr & 3);
+            gsum = rf[off];
+#pragma unroll
+            for (int w = 1; w < DW16_NW; w++) gsum += rf[w * 256 + off];
+        } else {   // bias: lanes (i = row, g = 0..3) of every wave, wave-major
+            const int rr = q - 256;
+            gsum = redb[0][rr];
+#pragma unroll
+            for (int k = 1; k < 4 * DW16_NW; k++) gsum += redb[k >> 2][(k & 3) * 16 + rr];
+        }
+        a.grads[e[j]] = gsum;
+        if (!a.mode) continue;
+        float mk = fmaf(a.w1, gsum - m[j], m[j]);
+        float vk = v[j] * a.beta2;
+        vk = vk + (a.c2 * gsum) * gsum;
+        const float denom = sqrtf(vk) / bc2s + a.eps;
+        const float pk = p[j] + (step_size * mk) / denom;
+        a.m[e[j]] = mk;
+        a.v[e[j]] = vk;
+        a.p[e[j]] = pk;
+        float tk = 0.f;
+        if (a.soft) {
+            tk = a.tau * pk + a.one_minus_tau * tg[j];
+            a.target[e[j]] = tk;
+        }
+        if (q < 256 && d.fwd_online) {   // the tile's blocks of the forward / dZ-chain copies
+            const int64_t pf = blk_pos(row[j], col[j], d.nch_fwd, false);
+            d.fwd_online[pf] = pk;
+            if (a.soft) d.fwd_target[pf] = tk;
+            if (d.chain) d.chain[blk_pos(col[j], row[j], d.nch_chain, false)] = pk;
+        }
+    }
+    DQNX_STAMP(a.stamps, 60);
+    if (T == 0 && wid == DW16_NW - 1 && a.loss_partial) {   // one wave, k_adam's fixed order
+        float s = 0.f;
+        for (int j = lane; j < a.n_loss_partial; j += 64) s += a.loss_partial[j];
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) s += __shfl_xor(s, o);
+        if (lane == 0) {
+            const float loss = s / (float)a.batch_global;
+            a.grads[a.n_params] = loss;
+            a.ctrl->loss = loss;
+        }
+    }
+}
+
+int launch_dw_adam16(const DwAdam16Args& a, hipStream_t s) {
+    static const int var = getenv("DQNX_DW16_VAR") ? atoi(getenv("DQNX_DW16_VAR")) : 0;
+    const dim3 grid(a.tiles + (a.mtc ? 1 : 0));
+    switch (var) {   // measurement variants (waves per tile, k-steps per register set)
+        case 1: hipLaunchKernelGGL((k_dw_adam16<4, 8>), grid, dim3(256), 0, s, a); break;
+        case 2: hipLaunchKernelGGL((k_dw_adam16<16, 4>), grid, dim3(1024), 0, s, a); break;
+        case 3: hipLaunchKernelGGL((k_dw_adam16<8, 4>), grid, dim3(512), 0, s, a); break;
+        case 4: hipLaunchKernelGGL((k_dw_adam16<4, 16>), grid, dim3(256), 0, s, a); break;
+        case 5: hipLaunchKernelGGL((k_dw_adam16<8, 16>), grid, dim3(512), 0, s, a); break;
+        case 6: hipLaunchKernelGGL((k_dw_adam16<16, 8>), grid, dim3(1024), 0, s, a); break;
+        default: hipLaunchKernelGGL((k_dw_adam16<8, 8>), grid, dim3(512), 0, s, a); break;
+    }
+    DQNX_HIP_CHECK(hipGetLastError());
+    return DQNX_OK;
+}
+
 __global__ void k_soft_update(float* __restrict__ target, const float* __restrict__ p, int64_t n, float tau,
                               float omt) {
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;

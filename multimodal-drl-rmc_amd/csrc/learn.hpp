@@ -202,6 +202,49 @@ struct DwAdamArgs {
     double beta1d, beta2d, lrd;
 };
 
+// Fused plan (fp32): every weight gradient over the FULL minibatch on 16 x 16 parameter tiles,
+// then Adam, the soft update and the fragment-blocked weight copies of the tile, in one launch
+// (k_dw_adam16, learn.hip).  A tile is exactly one 16 x 16 block of the fwd- and chain-blocked
+// copies (relayout.hpp).
+struct DwAdam16Layer {
+    const float* dZ;       // [Bl][ldz]
+    int ldz;
+    const float* X;        // [Bl][ldx] layer input rows (stream 0)
+    int ldx;
+    int in, out;
+    int64_t poff;          // flat offset of W ([out][in]; the bias follows, or the head layout)
+    int head_kind;         // -1 plain Linear, else dqnx_head_kind
+    int A;
+    int ti;                // 16-column blocks along `in`
+    int t0;                // first tile of this layer in the grid
+    float* fwd_online;     // fwd-blocked copies (null: the layer has none)
+    float* fwd_target;
+    float* chain;          // chain-blocked online copy (null: none)
+    int nch_fwd, nch_chain;   // kpad / 16, out / 16
+};
+struct DwAdam16Args {
+    DwAdam16Layer L[DQNX_MAX_DENSE + 1];
+    int nl;
+    int tiles;             // parameter tiles (+ 1 workgroup for the MT cache when mtc)
+    int Bl;
+    int mode;              // 0: gradients (+ loss) only, the DP all-reduce and Adam pass follow; 1: + Adam
+    int soft;
+    int64_t n_params;
+    float* p;
+    float* m;
+    float* v;
+    float* grads;          // [n_params + 1] (last = loss)
+    float* target;
+    dqnx_ctrl* ctrl;
+    float w1, beta2, c2, eps, tau, one_minus_tau;
+    const float* loss_partial;
+    int n_loss_partial;
+    int batch_global;
+    uint32_t* mtc;
+    int mtc_blocks;
+    int64_t* stamps;       // diagnostic builds (-DDQNX_STAMPS): slots 56..61
+};
+
 struct PushArgs {
     const float* obs;
     const float* next_obs;
@@ -510,6 +553,7 @@ bool head_supported(int F);
 int launch_adam(const AdamArgs& a, hipStream_t s);
 void dw_adam_grid(DwAdamArgs& a);
 int launch_dw_adam(const DwAdamArgs& a, hipStream_t s);
+int launch_dw_adam16(const DwAdam16Args& a, hipStream_t s);
 // acting path (act.hip): Network.actions for MLP nets, one launch
 constexpr int kActMaxDense = DQNX_MAX_DENSE;
 constexpr size_t kActMaxLds = 64 * 1024;

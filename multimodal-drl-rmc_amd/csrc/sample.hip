@@ -118,8 +118,14 @@ int sample_hash_slots(int32_t k) {
     return hs > 0 ? hs : global_hash_slots(k);
 }
 
+// smallest k routed to the fast sampler (DQNX_SAMPLER_FAST_MIN overrides, for measurements)
+static int fast_min_k() {
+    static const int v = getenv("DQNX_SAMPLER_FAST_MIN") ? atoi(getenv("DQNX_SAMPLER_FAST_MIN")) : SAMPLE_FAST_MIN_K;
+    return v;
+}
+
 int mt_cache_target_blocks(int32_t k, int64_t n) {
-    if (k < SAMPLE_FAST_MIN_K || k > SAMPLE_FAST_MAX_K || n <= k) return 0;   // the fast path only
+    if (k < fast_min_k() || k > SAMPLE_FAST_MAX_K || n <= k) return 0;   // the fast path only
     // the fast sampler's word estimate (sample_pipe.hpp) at population n, from a fully consumed
     // state block; + the state block itself
     int bits = 0;
@@ -142,7 +148,7 @@ int launch_sample_uniform(const SampleArgs& a_in, hipStream_t s) {
     a.test_flags = getenv("DQNX_SAMPLER_FORCE_FALLBACK") ? 1 : 0;
     const dim3 grid(1 + a.rl_blocks);
     const int lhs = lds_hash_slots(a.k);
-    if (a.k <= SAMPLE_FAST_MAX_K && (a.k >= SAMPLE_FAST_MIN_K || getenv("DQNX_SAMPLER_FAST") || a.test_flags) &&
+    if (a.k <= SAMPLE_FAST_MAX_K && (a.k >= fast_min_k() || getenv("DQNX_SAMPLER_FAST") || a.test_flags) &&
         !getenv("DQNX_SAMPLER_OLD")) {
         hipLaunchKernelGGL(k_sample_fast, grid, dim3(SAMPLE_FAST_NT), 0, s, a);
     } else if (lhs > 0) {

@@ -175,6 +175,20 @@ def test_gpu_learn_fused_backward_plan_matches_oracle(monkeypatch, algo, obs_dim
     _check_learn(*make_pair(algo, obs_dim, batch, capacity, n_fill, seed))
 
 
+@pytest.mark.parametrize("dw16,algo,obs_dim,batch,capacity,n_fill,seed", [
+    ("0", "DuelingDoubleDQNAgent", 284, 256, 3000, 3000, 61),    # split-K slabs + Adam pass
+    ("0", "DQNAgent", 14, 100, 500, 300, 62),
+    ("1", "DuelingDoubleDQNAgent", 284, 4096, 60000, 60000, 63),   # full-K tiles past 2048 rows
+    ("1", "DoubleDQNAgent", 284, 1000, 20000, 20000, 64),          # ragged K tail
+])
+def test_gpu_learn_dw_plans_match_oracle(monkeypatch, dw16, algo, obs_dim, batch, capacity, n_fill, seed):
+    """Both weight-gradient routes of the fused plan: k_dw_adam16 (full-minibatch 16 x 16 tiles,
+    Adam and the blocked copies in one launch; default up to 2048 rows) and the split-K slabs +
+    Adam pass (default beyond), each forced at a batch where the other is the default."""
+    monkeypatch.setenv("DQNX_DW_ADAM16", dw16)
+    _check_learn(*make_pair(algo, obs_dim, batch, capacity, n_fill, seed))
+
+
 @pytest.mark.parametrize("algo,obs_dim,batch,capacity,n_fill,seed", [
     ("DQNAgent", 14, 32, 500, 300, 23),
     ("DoubleDQNAgent", 284, 256, 3000, 3000, 24),
@@ -276,15 +290,17 @@ def _check_learn(oracle, eng):
     assert np.array_equal(eng.get_rng(0), oracle.py_state)
 
 
-@pytest.mark.parametrize("adam_blk", ["0", "1"])
+@pytest.mark.parametrize("adam_blk,dw16", [("0", "1"), ("0", "0"), ("1", "0")])
 @pytest.mark.parametrize("compute", ["fp32", "bf16"])
-def test_gpu_weights_written_from_host_are_used(monkeypatch, compute, adam_blk):
+def test_gpu_weights_written_from_host_are_used(monkeypatch, compute, adam_blk, dw16):
     """The fused plan keeps fragment-blocked weight copies current from the Adam pass; weights
     written from the host (a checkpoint load through load_params / state_dict views, hard or
     soft updates) must reach the next step's forward (DQNX_STEP relayout after
     dqnx_params_modified).  Checked by loading fresh weights mid-run into engine and oracle,
-    with the copies rebuilt every step (default) and maintained by Adam (DQNX_ADAM_BLK=1)."""
+    with the copies maintained by k_dw_adam16 (default), rebuilt every step (slab plan) and
+    maintained by the slab plan's Adam pass (DQNX_ADAM_BLK=1)."""
     monkeypatch.setenv("DQNX_ADAM_BLK", adam_blk)
+    monkeypatch.setenv("DQNX_DW_ADAM16", dw16)
     o, e = make_pair("DuelingDoubleDQNAgent", 284, 256, 3000, 3000, 27)
     if compute == "bf16":   # bf16: only that the host-written weights are the ones used
         E = _engine_mod()

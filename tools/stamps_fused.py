@@ -50,3 +50,8 @@ for step in range(6):
           + ", ".join(f"{ph[j]} {s[j + 1] - s[j]}" for j in range(7)))
     print(f"step {step}: fwd total {prev and (max(x for x in f if x) - f[0])} cyc: {fw}")
     print(f"         head_bwd total {max(x for x in h if x) - h[0]} cyc: {hw}")
+    d = s[56:61]
+    if all(d):
+        ph = ["prologue", "K loop", "reduce+barrier", "epilogue"]
+        print(f"         dw_adam16 (block 0) total {d[4] - d[0]} cyc: "
+              + ", ".join(f"{ph[j]} {d[j + 1] - d[j]}" for j in range(4)))
