@@ -46,6 +46,11 @@ for step in range(6):
             hw.append((40 + j, h[j] - prev))
             prev = h[j]
     ph = ["loads+clear", "cache/twist", "seen bits", "contended", "ballots", "scan", "out+cache"]
+    if s[15] > s[0] and s[15] - s[0] < 10**7:   # multi-pass body (k below the fast path)
+        body = ["state+clear", "twists", "insert", "scan", "out+pass"]
+        print(f"step {step}: sampler (multi-pass) total {s[15] - s[0]} cyc: "
+              + ", ".join(f"{body[j]} {s[j + 1] - s[j]}" for j in range(5)) + f", end {s[15] - s[5]}"
+              + f" (twisted blocks {s[16] // 100}, from the cache {s[16] % 100})")
     print(f"step {step}: sampler total {s[7] - s[0]} cyc (nb {s[8]}, cached {s[9]}): "
           + ", ".join(f"{ph[j]} {s[j + 1] - s[j]}" for j in range(7)))
     print(f"step {step}: fwd total {prev and (max(x for x in f if x) - f[0])} cyc: {fw}")
