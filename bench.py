@@ -87,6 +87,9 @@ def parse():
     p.add_argument("--no-kernel-timing", action="store_true")
     p.add_argument("--no-extras", action="store_true",
                    help="skip the secondary measurements (configs3_n1 / projection_w8 / weak)")
+    p.add_argument("--chain", type=int, default=1,
+                   help="N = 1: learn steps per engine call (dqnx_learn_steps: one graph, each step's "
+                        "minibatch drawn inside the previous step's last launch); 1 = one Agent.learn() per call")
     p.add_argument("--prefetch", action="store_true",
                    help="overlap the next step's replay sampling with this step's compute on a "
                         "side stream (measured slower at batch 1024: cross-stream event waits)")
@@ -301,14 +304,21 @@ def make_engine(args, spec, batch_global, world, rank, device, local=False):
     return eng
 
 
-def timed_steps(step, steps, dist, device):
-    """`steps` steps bracketed by barrier + synchronize on both sides; max over ranks (s)."""
+def timed_steps(step, steps, dist, device, chain=1):
+    """`steps` steps bracketed by barrier + synchronize on both sides; max over ranks (s).
+    chain > 1: step(c) runs c learn steps per call (steps // chain calls + the remainder)."""
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(steps):
-        step()
+    if chain > 1:
+        for _ in range(steps // chain):
+            step(chain)
+        if steps % chain:
+            step(steps % chain)
+    else:
+        for _ in range(steps):
+            step()
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
@@ -327,13 +337,17 @@ def run_learner(args, eng, world, backend, steps, warmup, dist, device):
     # the backward (dp_learn_step_bucketed); the MLP's 428 KB gradient stays one all-reduce
     bucketed = world > 1 and args.net != "mlp" and not args.no_buckets
 
-    def step():
+    chain = args.chain if world == 1 else 1
+
+    def step(count=1):
         if world > 1:   # shard compute, RCCL all-reduce (+ PER |delta| all-gather), replicated Adam
             (dp_learn_step_bucketed if bucketed else dp_learn_step)(eng, soft_update=True)
+        elif chain > 1:
+            eng.learn_steps(count, soft_update=True)
         else:
             eng.learn_step(soft_update=True, prefetch=args.prefetch)
     for _ in range(warmup):
-        step()
+        step(chain)
     torch.cuda.synchronize()
     eng.check_device_error()
     dp_graph = False
@@ -346,7 +360,9 @@ def run_learner(args, eng, world, backend, steps, warmup, dist, device):
         torch.cuda.synchronize()
         dp_graph = True
         step = g
-    el = timed_steps(step, steps, dist, device)
+    el = timed_steps(step, steps, dist, device, chain)
+    if args.prefetch and world == 1 and chain == 1:
+        eng.learn_step(soft_update=True)   # consume the minibatch drawn ahead (no draw pending after)
     if dp_graph:
         eng.set_graphs(True)   # later kernel timing replays the engine's own graphs
     eng.check_device_error()
@@ -561,6 +577,7 @@ def main():
                 "algo": args.algo, "net": net_name(args),
                 "batch_per_gpu": Bl, "global_batch": Bg, "replay_capacity": args.capacity,
                 "parallelism": f"dp{world}", "graphs": not args.no_graphs, "prefetch_sampling": args.prefetch,
+                "steps_per_call": args.chain if world == 1 else 1,
                 "sampling": "rank-local" if local else "global (reference-exact random.sample on every rank)",
                 "dp_step": ((("one HIP graph" if dp_graph else "eager")
                              + (", per-layer gradient buckets" if args.net != "mlp" and not args.no_buckets else ""))

@@ -243,14 +243,23 @@ int dqnx_rng_get(dqnx_engine* e, int32_t which, uint32_t* state625, void* stream
 #define DQNX_STEP_SOFT_UPDATE 0x1   /* fuse the tau soft update into the Adam pass */
 #define DQNX_STEP_GIVEN_INDICES 0x2 /* skip sampling: use DQNX_BUF_BATCH_IDX as written by caller */
 #define DQNX_STEP_GRADS_ONLY 0x4    /* stop after writing DQNX_BUF_GRADS (DP: all-reduce, then apply) */
-#define DQNX_STEP_PREFETCH 0x8      /* pure learning loops: also draw the NEXT step's minibatch on a
-                                       forked graph branch, overlapped with this step's compute.
+#define DQNX_STEP_PREFETCH 0x8      /* pure learning loops: also draw the NEXT step's minibatch,
+                                       overlapped with this step's compute (fused MLP plan: by one
+                                       more workgroup of the last launch; per-layer plan: on a
+                                       side stream).
                                        Results are bit-identical to sequential steps; while a
                                        prefetched minibatch is pending, dqnx_replay_push and
                                        dqnx_rng_set return DQNX_ESTATE and dqnx_rng_get already
                                        reflects the prefetched draw.  A step without the flag
                                        consumes the pending minibatch. */
 int dqnx_learn_step(dqnx_engine* e, int32_t flags, void* stream);
+/* `count` (1..256) consecutive learn steps, bitwise equal to `count` dqnx_learn_step(flags) calls
+ * (flags: 0 or DQNX_STEP_SOFT_UPDATE).  Replaces a loop of Agent.learn() +
+ * update_target_network() with no host work in between (R:train.py:99-101 repeated, e.g. several
+ * gradient steps per environment step).  Uniform replay on the fused MLP plan runs them as ONE
+ * graph in which step i's last launch also draws step i+1's minibatch; other configurations
+ * run the steps one by one.  Nothing is pending afterwards. */
+int dqnx_learn_steps(dqnx_engine* e, int32_t flags, int32_t count, void* stream);
 /* Adam (+ optional soft update) from DQNX_BUF_GRADS: second half of a GRADS_ONLY step. */
 int dqnx_apply_grads(dqnx_engine* e, int32_t flags, void* stream);
 /* ---- bucketed data-parallel step (conv nets) -----------------------

@@ -427,6 +427,8 @@ struct dqnx_engine {
     FusedFwdArgs fplan;     // LDS geometry of the fused plan (valid when bwd_plan == 2)
     int fsplit = 1;         // layer-1 column parts of the split forward (1: one forward launch)
     bool pf_valid = false;   // a prefetched minibatch for the next step sits in slot pf_slot
+    bool pf_inlaunch = false;   // ... drawn by the previous step's k_dw_adam16 launch (fused plan)
+    hipStream_t pf_stream = nullptr;   // ... on this stream
     int pf_slot = 0;
 };
 
@@ -816,7 +818,8 @@ RelayoutArgs relayout_args(dqnx_engine* e, int* blocks) {
 
 // Fused MLP plan (bwd_plan 2): forward of every layer + head in one launch, head / TD /
 // dZ chain in one launch, every dW in one split-K launch, then the Adam pass.
-void build_fused_steps(dqnx_engine* e, int flags, int32_t* idx, int32_t* phys, std::vector<KStep>& ks) {
+void build_fused_steps(dqnx_engine* e, int flags, int32_t* idx, int32_t* phys, std::vector<KStep>& ks,
+                       const SampleArgs* sample_next) {
     const dqnx_config& c = e->cfg;
     const NetPlan& np = e->np;
     const int L = (int)np.dense.size();
@@ -1065,6 +1068,15 @@ void build_fused_steps(dqnx_engine* e, int flags, int32_t* idx, int32_t* phys, s
             da.mtc = aa.mtc;
             da.mtc_blocks = aa.mtc_blocks;
             da.stamps = at<int64_t>(e, e->ws_stamps);
+            if (sample_next) {   // + the next step's minibatch (in-launch prefetch)
+                da.with_sample = 1;
+                da.samp = *sample_next;
+                da.samp.mtc = nullptr;
+                da.samp.mtc_blocks = 0;
+                da.samp.stamps = nullptr;
+                da.mtc = nullptr;
+                da.mtc_blocks = 0;
+            }
             const double P = (double)np.P;
             KStep k;
             k.name = da.mode ? "dw_adam16" : "dw16_grads";
@@ -1107,6 +1119,41 @@ void build_fused_steps(dqnx_engine* e, int flags, int32_t* idx, int32_t* phys, s
 // buffer pair; KEY_RELAYOUT = the sampler launch also rebuilds the fused plan's blocked weight
 // copies (only after the weights changed outside the Adam pass, which keeps them current).
 constexpr int KEY_RELAYOUT = 0x40;
+// KEY_SAMPLE_NEXT = no sampler launch at the front (the minibatch in `slot` was drawn by the
+// previous step); the last launch draws the next step's minibatch into slot ^ 1 (in-launch prefetch)
+constexpr int KEY_SAMPLE_NEXT = 0x80;
+
+SampleArgs uniform_sample_args(dqnx_engine* e, int32_t* idx, int32_t* phys) {
+    dqnx_ctrl* ctrl = ctrl_of(e);
+    SampleArgs sa;
+    memset(&sa, 0, sizeof(sa));
+    sa.state = ctrl->py_mt;
+    sa.n_dev = &ctrl->ring_size;
+    sa.k = e->Bs;
+    sa.setsize = e->setsize;
+    sa.out = idx;
+    sa.err = &ctrl->error;
+    sa.pool = at<int32_t>(e, e->ws_pool);
+    sa.phys_out = phys;
+    sa.shard_begin = e->shard_begin;
+    sa.shard_len = e->Bl;
+    sa.wptr_dev = &ctrl->ring_wptr;
+    sa.capacity = e->cfg.capacity;
+    sa.stamps = at<int64_t>(e, e->ws_stamps);
+    sa.gtab = sample_table_bytes(e->Bs) ? at<unsigned long long>(e, e->ws_gtab) : nullptr;
+    sa.mtc = at<uint32_t>(e, e->ws_mtc);
+    sa.mtc_blocks = e->mtc_blocks;
+    return sa;
+}
+
+// The fused plan's last launch can host the next step's sampler: uniform replay, the engine draws
+// its own indices, k_dw_adam16 is the update kernel and k takes the multi-pass sampler body
+bool inlaunch_prefetch_ok(const dqnx_engine* e, int flags) {
+    if (getenv("DQNX_PF_SIDE")) return false;   // measurements: the side-stream pipeline instead
+    return e->cfg.algo != DQNX_ALGO_PER_DOUBLE && !(flags & DQNX_STEP_GIVEN_INDICES) && dw_adam16_on(e, flags) &&
+           e->Bs <= DW16_SAMPLE_MAX_K && e->mtc_blocks == 0;
+}
+
 std::vector<KStep> build_learn_steps(dqnx_engine* e, int key) {
     const int flags = key & 0x3f;
     const int slot = (key >> 8) & 1;
@@ -1149,27 +1196,10 @@ std::vector<KStep> build_learn_steps(dqnx_engine* e, int key) {
             return launch_idx_to_phys(idx, phys, e->shard_begin, e->Bl, ctrl, c.capacity, &rl, rl_blocks, s);
         };
         ks.push_back(k);
-    } else {
-        SampleArgs sa;
-        memset(&sa, 0, sizeof(sa));
-        sa.state = ctrl->py_mt;
-        sa.n_dev = &ctrl->ring_size;
-        sa.k = e->Bs;
-        sa.setsize = e->setsize;
-        sa.out = idx;
-        sa.err = &ctrl->error;
-        sa.pool = at<int32_t>(e, e->ws_pool);
-        sa.phys_out = phys;
-        sa.shard_begin = e->shard_begin;
-        sa.shard_len = e->Bl;
-        sa.wptr_dev = &ctrl->ring_wptr;
-        sa.capacity = c.capacity;
-        sa.stamps = at<int64_t>(e, e->ws_stamps);
+    } else if (!(key & KEY_SAMPLE_NEXT)) {
+        SampleArgs sa = uniform_sample_args(e, idx, phys);
         sa.rl = rl;
         sa.rl_blocks = rl_blocks;
-        sa.gtab = sample_table_bytes(e->Bs) ? at<unsigned long long>(e, e->ws_gtab) : nullptr;
-        sa.mtc = at<uint32_t>(e, e->ws_mtc);
-        sa.mtc_blocks = e->mtc_blocks;
         KStep k;
         k.name = "sample_uniform";
         k.bytes = 2.0 * 625 * 4 + 4.0 * e->Bs + 4.0 * Bl;
@@ -1178,7 +1208,12 @@ std::vector<KStep> build_learn_steps(dqnx_engine* e, int key) {
     }
 
     if (e->bwd_plan == 2) {
-        build_fused_steps(e, flags, idx, phys, ks);
+        SampleArgs nxt;
+        const bool sample_next = (key & KEY_SAMPLE_NEXT) != 0;
+        if (sample_next)
+            nxt = uniform_sample_args(e, at<int32_t>(e, e->off[DQNX_BUF_BATCH_IDX]) + (size_t)(slot ^ 1) * e->Bg,
+                                      at<int32_t>(e, e->ws_phys) + (size_t)(slot ^ 1) * e->Bl);
+        build_fused_steps(e, flags, idx, phys, ks, sample_next ? &nxt : nullptr);
         return ks;
     }
 
@@ -2265,6 +2300,7 @@ int dqnx_engine_reset(dqnx_engine* e, void* stream) {
     e->ring_size = 0;
     e->ring_wptr = 0;
     e->pf_valid = false;
+    e->pf_inlaunch = false;
     e->wblk_dirty = true;
     return DQNX_OK;
 }
@@ -2377,7 +2413,8 @@ int dqnx_rng_get(dqnx_engine* e, int32_t which, uint32_t* state625, void* stream
     if (!state625 || (which != DQNX_RNG_PY && which != DQNX_RNG_NP)) return set_error(DQNX_EINVAL, "bad argument");
     hipStream_t s = (hipStream_t)stream;
     const uint32_t* src = which == DQNX_RNG_PY ? ctrl_of(e)->py_mt : ctrl_of(e)->np_mt;
-    if (e->pf_valid) DQNX_HIP_CHECK(hipStreamWaitEvent(s, e->ev_sampled[e->pf_slot], 0));
+    if (e->pf_valid && e->pf_inlaunch) DQNX_HIP_CHECK(hipStreamSynchronize(e->pf_stream));
+    else if (e->pf_valid) DQNX_HIP_CHECK(hipStreamWaitEvent(s, e->ev_sampled[e->pf_slot], 0));
     DQNX_HIP_CHECK(hipMemcpyAsync(state625, src, 625 * 4, hipMemcpyDeviceToHost, s));
     DQNX_HIP_CHECK(hipStreamSynchronize(s));
     return DQNX_OK;
@@ -2405,20 +2442,69 @@ static int pf_sample(dqnx_engine* e, int base, int slot) {
                        [&](hipStream_t cs) { return enqueue_range(ks, 0, 1, cs); });
 }
 
+// In-launch prefetch (fused plan): step t computes on slot cur, and its k_dw_adam16 launch draws
+// step t+1's minibatch into slot cur ^ 1 with one more workgroup.  Same stream, so ordering is
+// the launch order: the draw reads the MT state only after step t-1's draw wrote it, and step t+1
+// reads the slot after the launch that filled it.  Results are bitwise those of sequential steps
+// (the sample depends only on the MT state and the ring, which push / rng_set refuse to change
+// while a minibatch is pending).
+static int learn_step_inlaunch(dqnx_engine* e, int base, bool prefetch, hipStream_t s) {
+    int rc = DQNX_OK;
+    if (e->pf_valid && s != e->pf_stream) {   // the pending draw was enqueued on another stream
+        DQNX_HIP_CHECK(hipStreamSynchronize(e->pf_stream));
+    }
+    if (!e->pf_valid) {   // prologue: this step's minibatch by the sampler launch (+ relayout if dirty)
+        const int key0 = base | (e->wblk_dirty ? KEY_RELAYOUT : 0);
+        const std::vector<KStep>& ks0 = steps_for(e, key0);
+        rc = run_graphed(e, 0x80000 | key0, s, [&](hipStream_t cs) { return enqueue_range(ks0, 0, 1, cs); });
+        if (rc) return rc;
+        e->wblk_dirty = false;
+        e->pf_slot = 0;
+        e->pf_valid = true;
+        e->pf_inlaunch = true;
+    } else if (e->wblk_dirty) {   // weights written by the host while a minibatch is pending
+        int blocks = 0;
+        RelayoutArgs rl = relayout_args(e, &blocks);
+        rc = launch_idx_to_phys(nullptr, nullptr, 0, 0, ctrl_of(e), e->cfg.capacity, &rl, blocks, s);
+        if (rc) return rc;
+        e->wblk_dirty = false;
+    }
+    const int cur = e->pf_slot;
+    const int key = base | (cur << 8) | (prefetch ? KEY_SAMPLE_NEXT : 0);
+    const std::vector<KStep>& ks = steps_for(e, key);
+    rc = run_graphed(e, key | 0x20000, s,
+                     [&](hipStream_t cs) { return enqueue_range(ks, prefetch ? 0 : 1, (int)ks.size(), cs); });
+    if (rc) return rc;
+    if (!prefetch) {   // consumed the pending minibatch; nothing drawn ahead
+        e->pf_valid = false;
+        e->pf_inlaunch = false;
+        return DQNX_OK;
+    }
+    e->pf_slot = cur ^ 1;
+    e->pf_stream = s;   // dqnx_rng_get synchronises it (an event record per step cost ~10 us of queue time)
+    return DQNX_OK;
+}
+
 int dqnx_learn_step(dqnx_engine* e, int32_t flags, void* stream) {
     int rc = check_bound(e);
     if (rc) return rc;
     hipStream_t s = (hipStream_t)stream;
     if (e->cfg.algo == DQNX_ALGO_PER_DOUBLE && (flags & DQNX_STEP_GIVEN_INDICES))
         return set_error(DQNX_EUNSUPPORTED, "PER learn step samples its own minibatch");
-    // PER: step t+1's sample depends on step t's priority update, so nothing is drawn ahead
-    // Fused plan: the sampler launch also rebuilds the blocked weight copies, which must see
-    // this step's weights, so it cannot run a step ahead either.
+    // PER: step t+1's sample depends on step t's priority update, so nothing is drawn ahead.
+    // Fused plan: the last launch of step t (k_dw_adam16) hosts step t+1's sampler workgroup
+    // (in-launch prefetch, same stream, no events); where it cannot (k past the multi-pass
+    // sampler, slab plan), nothing is drawn ahead.  Per-layer plan: a side-stream pipeline.
+    const int base = flags & (DQNX_STEP_SOFT_UPDATE | DQNX_STEP_GIVEN_INDICES | DQNX_STEP_GRADS_ONLY);
+    const bool inl = e->bwd_plan == 2 && inlaunch_prefetch_ok(e, base);
     const bool prefetch = (flags & DQNX_STEP_PREFETCH) && !(flags & DQNX_STEP_GIVEN_INDICES) &&
-                          e->cfg.algo != DQNX_ALGO_PER_DOUBLE && e->bwd_plan != 2;
+                          e->cfg.algo != DQNX_ALGO_PER_DOUBLE && (e->bwd_plan != 2 || inl);
     if (e->ring_size < e->Bs && !(flags & DQNX_STEP_GIVEN_INDICES) && !e->pf_valid)
         return set_error(DQNX_EINVAL, "Sample larger than population: %lld < %d", (long long)e->ring_size, e->Bs);
-    const int base = flags & (DQNX_STEP_SOFT_UPDATE | DQNX_STEP_GIVEN_INDICES | DQNX_STEP_GRADS_ONLY);
+    if (e->pf_valid && (flags & DQNX_STEP_GIVEN_INDICES))
+        return set_error(DQNX_ESTATE, "given-indices step while a prefetched minibatch is pending");
+    if (e->pf_valid && e->pf_inlaunch) return learn_step_inlaunch(e, base, prefetch, s);
+    if (prefetch && inl) return learn_step_inlaunch(e, base, true, s);
     if (!prefetch && !e->pf_valid) {
         // the weights changed outside the Adam pass: this step's sampler launch rebuilds the copies
         const int key = base | ((e->bwd_plan == 2 && (e->wblk_dirty || !blk_kept(e, base))) ? KEY_RELAYOUT : 0);
@@ -2459,6 +2545,45 @@ int dqnx_learn_step(dqnx_engine* e, int32_t flags, void* stream) {
     DQNX_HIP_CHECK(hipEventRecord(e->ev_sampled[nxt], e->side_stream));
     e->pf_slot = nxt;
     return DQNX_OK;
+}
+
+// `count` consecutive learn steps as ONE graph (pure learning loops, e.g. several learn steps
+// per environment step): the first step's minibatch is drawn by the sampler launch, every
+// later one by the previous step's k_dw_adam16 launch (in-launch prefetch), the last step draws
+// nothing ahead.  Bitwise equal to `count` dqnx_learn_step calls, and nothing is pending after
+// the call.  Configurations without the in-launch sampler (PER, the slab / per-layer plans,
+// k past the multi-pass sampler) run the steps one by one.
+int dqnx_learn_steps(dqnx_engine* e, int32_t flags, int32_t count, void* stream) {
+    int rc = check_bound(e);
+    if (rc) return rc;
+    if (count < 1 || count > 256) return set_error(DQNX_EINVAL, "learn_steps: count %d not in [1, 256]", count);
+    if (flags & (DQNX_STEP_PREFETCH | DQNX_STEP_GIVEN_INDICES | DQNX_STEP_GRADS_ONLY))
+        return set_error(DQNX_EINVAL, "learn_steps: flags may only hold DQNX_STEP_SOFT_UPDATE");
+    hipStream_t s = (hipStream_t)stream;
+    const int base = flags & DQNX_STEP_SOFT_UPDATE;
+    if (e->pf_valid || !(e->bwd_plan == 2 && inlaunch_prefetch_ok(e, base))) {
+        for (int i = 0; i < count; i++) {
+            rc = dqnx_learn_step(e, base, stream);
+            if (rc) return rc;
+        }
+        return DQNX_OK;
+    }
+    if (e->ring_size < e->Bs)
+        return set_error(DQNX_EINVAL, "Sample larger than population: %lld < %d", (long long)e->ring_size, e->Bs);
+    const int first = base | (e->wblk_dirty ? KEY_RELAYOUT : 0);
+    rc = run_graphed(e, 0x40000000 | (count << 12) | first, s, [&](hipStream_t cs) {
+        const std::vector<KStep>& k0 = steps_for(e, first);   // slot 0: sampler (+ relayout) + step
+        int r = enqueue_range(k0, 0, 1, cs);
+        for (int i = 0; i < count && !r; i++) {
+            const int slot = i & 1;
+            const bool last = i == count - 1;
+            const std::vector<KStep>& ks = steps_for(e, base | (slot << 8) | (last ? 0 : KEY_SAMPLE_NEXT));
+            r = enqueue_range(ks, last ? 1 : 0, (int)ks.size(), cs);
+        }
+        return r;
+    });
+    if (!rc) e->wblk_dirty = false;
+    return rc;
 }
 
 int dqnx_learn_kernel_count(dqnx_engine* e, int32_t flags, int32_t* n) {

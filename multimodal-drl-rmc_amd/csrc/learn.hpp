@@ -202,6 +202,44 @@ struct DwAdamArgs {
     double beta1d, beta2d, lrd;
 };
 
+struct PushArgs {
+    const float* obs;
+    const float* next_obs;
+    const int32_t* act;
+    const float* rew;
+    const uint8_t* done;
+    int n, obs_dim, stride;
+    int64_t wptr, capacity, new_size, new_wptr;
+    float* ring_obs;
+    float* ring_next;
+    int32_t* ring_act;
+    float* ring_rew;
+    float* ring_done;
+    dqnx_ctrl* ctrl;
+};
+
+struct SampleArgs {
+    uint32_t* state;          // [625]
+    const int64_t* n_dev;     // population size from device (ring size) or null
+    int64_t n_val;
+    int32_t k;
+    int64_t setsize;
+    int32_t* out;             // [k] logical positions
+    int32_t* err;             // sticky error word
+    int32_t* pool;            // pool-branch scratch [>= setsize]
+    // optional: physical ring slots of the local shard  phys = (wptr - size + j) mod cap
+    int32_t* phys_out;        // [shard_len] or null
+    int32_t shard_begin, shard_len;
+    const int64_t* wptr_dev;
+    int64_t capacity;
+    int64_t* stamps;          // diagnostic builds (-DDQNX_STAMPS)
+    RelayoutArgs rl;          // fused plan: blocked weight copies, built by blocks 1.. of the launch
+    int rl_blocks;
+    unsigned long long* gtab; // k too large for an LDS table: sample_table_bytes(k) of global scratch
+    int test_flags;           // tests only (DQNX_SAMPLER_FORCE_FALLBACK): 1 = take the fast path's fallback
+    uint32_t* mtc;            // MT block cache (mt_cache_words), or null: [0] = blocks held, [64 + 624 b + o]
+    int mtc_blocks;           // blocks the cache is kept at (the state's block + its successors)
+};
 // Fused plan (fp32): every weight gradient over the FULL minibatch on 16 x 16 parameter tiles,
 // then Adam, the soft update and the fragment-blocked weight copies of the tile, in one launch
 // (k_dw_adam16, learn.hip).  A tile is exactly one 16 x 16 block of the fwd- and chain-blocked
@@ -243,46 +281,14 @@ struct DwAdam16Args {
     uint32_t* mtc;
     int mtc_blocks;
     int64_t* stamps;       // diagnostic builds (-DDQNX_STAMPS): slots 56..61
+    // in-launch prefetch (DQNX_STEP_PREFETCH, uniform replay, k <= DW16_SAMPLE_MAX_K): one more
+    // workgroup (index tiles) draws the NEXT step's minibatch with the uniform sampler's body
+    int with_sample;
+    SampleArgs samp;
 };
+constexpr int DW16_SAMPLE_HS = 4096;     // LDS hash slots of that workgroup's sampler (32 KiB)
+constexpr int DW16_SAMPLE_MAX_K = 2048;  // k it serves (table <= 3/4 full: k + one pass of words)
 
-struct PushArgs {
-    const float* obs;
-    const float* next_obs;
-    const int32_t* act;
-    const float* rew;
-    const uint8_t* done;
-    int n, obs_dim, stride;
-    int64_t wptr, capacity, new_size, new_wptr;
-    float* ring_obs;
-    float* ring_next;
-    int32_t* ring_act;
-    float* ring_rew;
-    float* ring_done;
-    dqnx_ctrl* ctrl;
-};
-
-struct SampleArgs {
-    uint32_t* state;          // [625]
-    const int64_t* n_dev;     // population size from device (ring size) or null
-    int64_t n_val;
-    int32_t k;
-    int64_t setsize;
-    int32_t* out;             // [k] logical positions
-    int32_t* err;             // sticky error word
-    int32_t* pool;            // pool-branch scratch [>= setsize]
-    // optional: physical ring slots of the local shard  phys = (wptr - size + j) mod cap
-    int32_t* phys_out;        // [shard_len] or null
-    int32_t shard_begin, shard_len;
-    const int64_t* wptr_dev;
-    int64_t capacity;
-    int64_t* stamps;          // diagnostic builds (-DDQNX_STAMPS)
-    RelayoutArgs rl;          // fused plan: blocked weight copies, built by blocks 1.. of the launch
-    int rl_blocks;
-    unsigned long long* gtab; // k too large for an LDS table: sample_table_bytes(k) of global scratch
-    int test_flags;           // tests only (DQNX_SAMPLER_FORCE_FALLBACK): 1 = take the fast path's fallback
-    uint32_t* mtc;            // MT block cache (mt_cache_words), or null: [0] = blocks held, [64 + 624 b + o]
-    int mtc_blocks;           // blocks the cache is kept at (the state's block + its successors)
-};
 // MT block cache: the state block of the uniform sampler and its twisted successors, kept ahead
 // by the Adam launch of the previous step (k_adam's extra workgroup), so the next sample reads the
 // blocks it consumes instead of twisting them on its critical path.  Valid by construction: cache

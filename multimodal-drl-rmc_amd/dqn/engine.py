@@ -368,6 +368,15 @@ class LearnEngine:
         if self.cfg.algo == C.DQNX_ALGO_PER_DOUBLE:   # every PER learn step samples: step += n_env
             self.agent_step += self.cfg.n_env
 
+    def learn_steps(self, count: int, soft_update=False):
+        """`count` consecutive learn steps in one call (dqnx_learn_steps): bitwise equal to
+        `count` learn_step(soft_update) calls; one graph on the fused MLP plan, with every step's
+        minibatch after the first drawn inside the previous step's last launch."""
+        C.check(self.L.dqnx_learn_steps(self.h, C.STEP_SOFT_UPDATE if soft_update else 0, int(count),
+                                        self.stream()), "learn_steps")
+        if self.cfg.algo == C.DQNX_ALGO_PER_DOUBLE:
+            self.agent_step += self.cfg.n_env * int(count)
+
     def apply_grads(self, soft_update=False):
         C.check(self.L.dqnx_apply_grads(self.h, C.STEP_SOFT_UPDATE if soft_update else 0, self.stream()),
                 "apply_grads")

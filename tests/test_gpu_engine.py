@@ -408,19 +408,24 @@ def test_gpu_learn_golden(golden):
             np.testing.assert_allclose(got, ref, atol=1e-5, rtol=0, err_msg=f"{nm} {k}")
 
 
-def test_gpu_prefetch_mode_bit_identical(monkeypatch):
+@pytest.mark.parametrize("plan,batch", [("0", 256), ("fused", 256), ("fused", 1024), ("fused", 2048)])
+def test_gpu_prefetch_mode_bit_identical(monkeypatch, plan, batch):
     """DQNX_STEP_PREFETCH draws step t+1's minibatch during step t: same results, bitwise.
-    (Per-layer plan: the fused plan rebuilds its blocked weights in the sampler launch and
-    never samples ahead.)"""
-    monkeypatch.setenv("DQNX_BWD_PLAN", "0")
-    o1, e1 = make_pair("DuelingDoubleDQNAgent", 284, 256, 3000, 3000, 21)
-    o2, e2 = make_pair("DuelingDoubleDQNAgent", 284, 256, 3000, 3000, 21)
-    for _ in range(5):
+    Per-layer plan: a side-stream pipeline.  Fused plan: step t's k_dw_adam16 launch hosts step
+    t+1's sampler workgroup (in-launch prefetch; B=2048 is its largest k)."""
+    if plan == "0":
+        monkeypatch.setenv("DQNX_BWD_PLAN", "0")
+    n = max(3000, 2 * batch)
+    o1, e1 = make_pair("DuelingDoubleDQNAgent", 284, batch, n, n, 21)
+    o2, e2 = make_pair("DuelingDoubleDQNAgent", 284, batch, n, n, 21)
+    for _ in range(6):
         e1.learn_step(soft_update=True)
-    for _ in range(4):
+    for _ in range(5):
         e2.learn_step(soft_update=True, prefetch=True)
     e2.learn_step(soft_update=True)     # consumes the pending minibatch
     torch.cuda.synchronize()
+    e1.check_device_error()
+    e2.check_device_error()
     assert torch.equal(e1.params, e2.params)
     assert torch.equal(e1.target_params, e2.target_params)
     assert np.array_equal(e1.get_rng(0), e2.get_rng(0))
@@ -428,9 +433,66 @@ def test_gpu_prefetch_mode_bit_identical(monkeypatch):
     e2.push(*O.synth_transitions(4, 284, 8, seed=3))
 
 
-def test_gpu_push_refused_with_pending_prefetch(monkeypatch):
+@pytest.mark.parametrize("algo,batch,count,n_fill", [
+    ("DuelingDoubleDQNAgent", 1024, 1, 4000),
+    ("DuelingDoubleDQNAgent", 1024, 2, 4000),
+    ("DuelingDoubleDQNAgent", 1024, 7, 4000),
+    ("DQNAgent", 256, 4, 3000),
+    ("DuelingDoubleDQNAgent", 1024, 3, 3000),     # n <= setsize: the pool branch in-launch
+    ("PerDuelingDoubleDQNAgent", 256, 3, 3000),   # no in-launch sampler: steps one by one
+])
+def test_gpu_learn_steps_equal_single_steps(algo, batch, count, n_fill):
+    """dqnx_learn_steps(count) == count x dqnx_learn_step, bitwise (weights, target, Adam state,
+    loss, RNG), with host-side weight writes before the call (relayout in the graph's sampler)."""
+    o1, e1 = make_pair(algo, 284, batch, max(n_fill, 3000), n_fill, 31)
+    o2, e2 = make_pair(algo, 284, batch, max(n_fill, 3000), n_fill, 31)
+    for rnd in range(2):
+        for _ in range(count):
+            e1.learn_step(soft_update=True)
+        e2.learn_steps(count, soft_update=True)
+        torch.cuda.synchronize()
+        e1.check_device_error()
+        e2.check_device_error()
+        assert torch.equal(e1.params, e2.params), rnd
+        assert torch.equal(e1.target_params, e2.target_params), rnd
+        assert torch.equal(e1.adam_m, e2.adam_m) and torch.equal(e1.adam_v, e2.adam_v), rnd
+        assert e1.loss() == e2.loss()
+        assert np.array_equal(e1.get_rng(0), e2.get_rng(0))
+        if algo.startswith("Per"):
+            assert np.array_equal(e1.get_rng(1), e2.get_rng(1))
+        new = O.reference_init(O.mlp_spec(284, 8, O.algo_spec_head(algo)), 50 + rnd)
+        e1.load_params(new)
+        e2.load_params(new)
+    # nothing is pending afterwards: pushes are allowed
+    e2.push(*O.synth_transitions(4, 284, 8, seed=3))
+
+
+def test_gpu_prefetch_fused_weights_written_while_pending():
+    """Fused plan, in-launch prefetch: host-side weight writes (load_params) while a minibatch is
+    pending rebuild the blocked copies before the next step, and the step matches a sequential
+    engine that got the same write."""
+    o1, e1 = make_pair("DuelingDoubleDQNAgent", 284, 1024, 4000, 4000, 23)
+    o2, e2 = make_pair("DuelingDoubleDQNAgent", 284, 1024, 4000, 4000, 23)
+    e1.learn_step(soft_update=True)
+    e2.learn_step(soft_update=True, prefetch=True)
+    new = O.reference_init(O.mlp_spec(284, 8, "dueling"), 99)
+    e1.load_params(new)
+    e2.load_params(new)
+    for _ in range(2):
+        e1.learn_step(soft_update=True)
+    e2.learn_step(soft_update=True, prefetch=True)
+    e2.learn_step(soft_update=True)
+    torch.cuda.synchronize()
+    assert torch.equal(e1.params, e2.params)
+    assert torch.equal(e1.target_params, e2.target_params)
+    assert abs(e1.loss() - e2.loss()) == 0.0
+
+
+@pytest.mark.parametrize("plan", ["0", "fused"])
+def test_gpu_push_refused_with_pending_prefetch(monkeypatch, plan):
     from dqn import _capi as C
-    monkeypatch.setenv("DQNX_BWD_PLAN", "0")
+    if plan == "0":
+        monkeypatch.setenv("DQNX_BWD_PLAN", "0")
     o, e = make_pair("DuelingDoubleDQNAgent", 14, 32, 500, 300, 22)
     e.learn_step(prefetch=True)
     with pytest.raises(C.DqnxError):
