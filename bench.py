@@ -71,7 +71,10 @@ def parse():
     p.add_argument("--net", default="mlp", choices=["mlp", "hybrid", "hybrid84"],
                    help="mlp: MLP-284 (configs[1]/[3]/[4]); hybrid: TwoStreamHybridNetwork on the (2,27,5) grid; "
                         "hybrid84: the stacked (4,84,84) occupancy-grid CNN variant (configs[2])")
-    p.add_argument("--no-graphs", action="store_true")
+    p.add_argument("--graphs", action="store_true",
+                   help="replay every learn step as a captured HIP graph (default: eager launches, 3-4 us per "
+                        "step faster on MI355X / ROCm 7.2: each hipGraphLaunch adds ~8.5 us between graphs)")
+    p.add_argument("--no-graphs", action="store_true", help="(the default; kept for old command lines)")
     p.add_argument("--no-dp-graph", action="store_true",
                    help="N > 1: launch the learn graph, the all-reduce and Adam separately each step "
                         "instead of replaying them as one captured HIP graph")
@@ -90,12 +93,14 @@ def parse():
     p.add_argument("--chain", type=int, default=1,
                    help="N = 1: learn steps per engine call (dqnx_learn_steps: one graph, each step's "
                         "minibatch drawn inside the previous step's last launch); 1 = one Agent.learn() per call")
-    p.add_argument("--prefetch", action="store_true",
-                   help="overlap the next step's replay sampling with this step's compute on a "
-                        "side stream (measured slower at batch 1024: cross-stream event waits)")
+    p.add_argument("--no-prefetch", action="store_true",
+                   help="N = 1, uniform replay: do not draw step t+1's minibatch inside step t's last launch "
+                        "(DQNX_STEP_PREFETCH; on by default for this pure learning loop)")
+    p.add_argument("--prefetch", action="store_true", help="(the default; kept for old command lines)")
     a = p.parse_args()
     if a.capacity is None:
         a.capacity = 100_000 if a.net == "hybrid84" else 1_000_000
+    a.prefetch = not a.no_prefetch
     return a
 
 
@@ -297,7 +302,7 @@ def set_rngs(eng, per, rank_seed=0):
 
 def make_engine(args, spec, batch_global, world, rank, device, local=False):
     eng = LearnEngine(spec, args.algo, batch_global, args.capacity, world_size=world, rank=rank, device=device,
-                      graphs=not args.no_graphs, local_sampling=local, compute_dtype=args.compute)
+                      graphs=args.graphs, local_sampling=local, compute_dtype=args.compute)
     eng.load_params(init_params(spec, 0))
     fill_ring(eng, args.capacity, spec.obs_dim, args.actions, device, seed=0)
     set_rngs(eng, args.algo.startswith("Per"), rank if local else 0)
@@ -351,7 +356,7 @@ def run_learner(args, eng, world, backend, steps, warmup, dist, device):
     torch.cuda.synchronize()
     eng.check_device_error()
     dp_graph = False
-    if world > 1 and backend == "nccl" and not args.no_dp_graph and not args.no_graphs:
+    if world > 1 and backend == "nccl" and not args.no_dp_graph:
         # the whole DP step (shard kernels + RCCL all-reduce + Adam) as one replayed graph: the
         # eager loop is host-bound (3 launches + a collective call per ~50 us step).  RCCL
         # collectives are capturable; gloo's are host calls and never are.
@@ -364,7 +369,7 @@ def run_learner(args, eng, world, backend, steps, warmup, dist, device):
     if args.prefetch and world == 1 and chain == 1:
         eng.learn_step(soft_update=True)   # consume the minibatch drawn ahead (no draw pending after)
     if dp_graph:
-        eng.set_graphs(True)   # later kernel timing replays the engine's own graphs
+        eng.set_graphs(args.graphs)   # GraphedDPStep switched the engine's own graphs off
     eng.check_device_error()
     return el, dp_graph
 
@@ -530,6 +535,8 @@ def main():
     kernels = []
     if not args.no_kernel_timing:
         flags = C.STEP_GRADS_ONLY if world > 1 else C.STEP_SOFT_UPDATE
+        if world == 1 and args.prefetch:   # the plan the timed loop ran (steady state: no sampler launch)
+            flags |= C.STEP_PREFETCH
         ks = kernel_times(eng, flags, count=50, reps=5)
         dom = max(ks, key=lambda k: k[1])
         # re-time the dominant kernel with more steps per sample
@@ -576,7 +583,7 @@ def main():
                 "workload": workload_name(args, world),
                 "algo": args.algo, "net": net_name(args),
                 "batch_per_gpu": Bl, "global_batch": Bg, "replay_capacity": args.capacity,
-                "parallelism": f"dp{world}", "graphs": not args.no_graphs, "prefetch_sampling": args.prefetch,
+                "parallelism": f"dp{world}", "graphs": args.graphs, "prefetch_sampling": args.prefetch and world == 1 and not per,
                 "steps_per_call": args.chain if world == 1 else 1,
                 "sampling": "rank-local" if local else "global (reference-exact random.sample on every rank)",
                 "dp_step": ((("one HIP graph" if dp_graph else "eager")

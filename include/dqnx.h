@@ -196,7 +196,10 @@ int dqnx_engine_bind(dqnx_engine* e, void* arena, uint64_t bytes);
 int dqnx_params_modified(dqnx_engine* e);
 /* Zero Adam moments, ring state, tree, control block (params untouched); stream-ordered. */
 int dqnx_engine_reset(dqnx_engine* e, void* stream);
-/* Use hipGraph capture/replay for learn steps (default on). */
+/* Use hipGraph capture/replay for learn steps (default OFF: measured on MI355X / ROCm 7.2, every
+ * hipGraphLaunch leaves ~8.5 us between the previous graph's last kernel and its first one, while
+ * back-to-back kernel launches on one stream leave ~0; eager steps are 3-4 us faster at every
+ * configuration measured -- MLP B=1024 / 4096, PER, bf16 B=8192, two-stream). */
 int dqnx_engine_set_graphs(dqnx_engine* e, int32_t enabled);
 
 /* ---- replay ring: replaces ReplayMemoryNaive/Prioritized.store_transitions
@@ -301,13 +304,16 @@ int dqnx_act(const dqnx_net_desc* net, const float* params, const float* obs, in
  * A learn step is an ordered list of kernel launches (sample, linear_fwd_l1.., head_td_loss,
  * linear_bwd_lL..l1, adam_fused).  dqnx_learn_step_timed runs one whole step exactly like
  * dqnx_learn_step but records ev_start/ev_stop (hipEvent_t) around kernel `kernel_index`
- * on `stream` (the sub-ranges before/after it are graph-replayed separately). */
+ * on `stream` (the sub-ranges before/after it are graph-replayed separately).
+ * kernel_count / kernel_info / step_omit with DQNX_STEP_PREFETCH describe the steady-state step
+ * of a prefetching loop where the in-launch prefetch applies (no sampler launch; the last
+ * launch, "dw_adam16+sample", also draws the next minibatch). */
 int dqnx_learn_kernel_count(dqnx_engine* e, int32_t flags, int32_t* n);
 int dqnx_learn_kernel_info(dqnx_engine* e, int32_t flags, int32_t index, char* name, int32_t name_len,
                            double* algorithmic_flops, double* algorithmic_bytes);
 int dqnx_learn_step_timed(dqnx_engine* e, int32_t flags, int32_t kernel_index, void* ev_start, void* ev_stop,
                           void* stream);
-/* Timing aid (bench.py roofline): one learn step, graph-launched, with kernel
+/* Timing aid (bench.py roofline): one learn step (graph-launched when graphs are on), with kernel
  * `omit_index` (as numbered by dqnx_learn_kernel_info; -1 = none) left out.  Engine state
  * afterwards is meant for timing only. */
 int dqnx_learn_step_omit(dqnx_engine* e, int32_t flags, int32_t omit_index, void* stream);

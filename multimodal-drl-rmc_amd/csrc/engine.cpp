@@ -408,7 +408,7 @@ struct dqnx_engine {
     int stage_rows = 0;
     char* arena = nullptr;
     int64_t ring_size = 0, ring_wptr = 0;   // host mirror of the ring state (pushes are host-driven)
-    bool graphs = true;
+    bool graphs = false;   // eager launches by default (dqnx_engine_set_graphs)
     std::map<int, hipGraphExec_t> graph_cache;
     hipStream_t capture_stream = nullptr;
     std::map<int, std::vector<KStep>> steps_cache;
@@ -1079,7 +1079,8 @@ void build_fused_steps(dqnx_engine* e, int flags, int32_t* idx, int32_t* phys, s
             }
             const double P = (double)np.P;
             KStep k;
-            k.name = da.mode ? "dw_adam16" : "dw16_grads";
+            k.name = sample_next ? (da.mode ? "dw_adam16+sample" : "dw16_grads+sample")
+                                 : (da.mode ? "dw_adam16" : "dw16_grads");
             k.flops = flops + (da.mode ? 12.0 * P : 0.0);
             // dZ / X rows once; p, m, v read and written, grads written (+ target read and
             // written); the blocked copies: fwd online (+ fwd target), chain for l >= 1
@@ -2586,11 +2587,20 @@ int dqnx_learn_steps(dqnx_engine* e, int32_t flags, int32_t count, void* stream)
     return rc;
 }
 
+// The plan the timing entry points describe: flags & 7, and with DQNX_STEP_PREFETCH (where the
+// in-launch prefetch applies) the steady-state step of a prefetching loop -- no sampler launch,
+// the last launch draws the next minibatch (into slot 1; timing runs leave the state stale).
+static int timing_key(const dqnx_engine* e, int32_t flags) {
+    const int base = flags & 7;
+    if ((flags & DQNX_STEP_PREFETCH) && e->bwd_plan == 2 && inlaunch_prefetch_ok(e, base)) return base | KEY_SAMPLE_NEXT;
+    return base;
+}
+
 int dqnx_learn_kernel_count(dqnx_engine* e, int32_t flags, int32_t* n) {
     int rc = check_bound(e);
     if (rc) return rc;
     if (!n) return set_error(DQNX_EINVAL, "null argument");
-    *n = (int32_t)steps_for(e, flags & 7).size();
+    *n = (int32_t)steps_for(e, timing_key(e, flags)).size();
     return DQNX_OK;
 }
 
@@ -2598,7 +2608,7 @@ int dqnx_learn_kernel_info(dqnx_engine* e, int32_t flags, int32_t i, char* name,
                            double* bytes) {
     int rc = check_bound(e);
     if (rc) return rc;
-    const std::vector<KStep>& ks = steps_for(e, flags & 7);
+    const std::vector<KStep>& ks = steps_for(e, timing_key(e, flags));
     if (i < 0 || i >= (int32_t)ks.size()) return set_error(DQNX_EINVAL, "kernel index %d out of range", i);
     if (name && name_len > 0) snprintf(name, (size_t)name_len, "%s", ks[i].name.c_str());
     if (flops) *flops = ks[i].flops;
@@ -2641,7 +2651,7 @@ int dqnx_learn_step_omit(dqnx_engine* e, int32_t flags, int32_t omit_index, void
     if (e->pf_valid) return set_error(DQNX_ESTATE, "timing step with a prefetched minibatch pending");
     if (e->ring_size < e->Bs && !(flags & DQNX_STEP_GIVEN_INDICES))
         return set_error(DQNX_EINVAL, "Sample larger than population: %lld < %d", (long long)e->ring_size, e->Bs);
-    const int base = flags & 7;
+    const int base = timing_key(e, flags);
     const std::vector<KStep>& ks = steps_for(e, base);
     const int n = (int)ks.size();
     if (omit_index < -1 || omit_index >= n) return set_error(DQNX_EINVAL, "kernel index out of range");

@@ -208,9 +208,11 @@ class LearnEngine:
     """One agent's learn-step engine on one GPU (one process per GPU under DP)."""
 
     def __init__(self, spec: NetSpec, algo: str, batch: int, capacity: int, gamma=0.99, lr=1e-4,
-                 tau=1e-3, n_env=1, world_size=1, rank=0, device=None, graphs=True, eps_dec=2e6,
+                 tau=1e-3, n_env=1, world_size=1, rank=0, device=None, graphs=False, eps_dec=2e6,
                  local_sampling=False, compute_dtype="fp32", per_numpy121=False):
-        """per_numpy121: PER SumTree arithmetic of the reference's pinned numpy 1.21 (float32
+        """graphs: replay each learn step as a captured HIP graph (off by default: eager launches
+        measured 3-4 us faster per step, include/dqnx.h dqnx_engine_set_graphs).
+        per_numpy121: PER SumTree arithmetic of the reference's pinned numpy 1.21 (float32
         `change` and float32-rounded ancestor sums, in update order) instead of numpy >= 2's."""
         if not torch.cuda.is_available():
             raise RuntimeError("libdqnx needs a ROCm GPU (MI355X / gfx950); there is no CPU fallback")

@@ -408,8 +408,9 @@ def test_gpu_learn_golden(golden):
             np.testing.assert_allclose(got, ref, atol=1e-5, rtol=0, err_msg=f"{nm} {k}")
 
 
-@pytest.mark.parametrize("plan,batch", [("0", 256), ("fused", 256), ("fused", 1024), ("fused", 2048)])
-def test_gpu_prefetch_mode_bit_identical(monkeypatch, plan, batch):
+@pytest.mark.parametrize("plan,batch,graphs", [("0", 256, True), ("fused", 256, True), ("fused", 1024, True),
+                                               ("fused", 1024, False), ("fused", 2048, True)])
+def test_gpu_prefetch_mode_bit_identical(monkeypatch, plan, batch, graphs):
     """DQNX_STEP_PREFETCH draws step t+1's minibatch during step t: same results, bitwise.
     Per-layer plan: a side-stream pipeline.  Fused plan: step t's k_dw_adam16 launch hosts step
     t+1's sampler workgroup (in-launch prefetch; B=2048 is its largest k)."""
@@ -417,7 +418,7 @@ def test_gpu_prefetch_mode_bit_identical(monkeypatch, plan, batch):
         monkeypatch.setenv("DQNX_BWD_PLAN", "0")
     n = max(3000, 2 * batch)
     o1, e1 = make_pair("DuelingDoubleDQNAgent", 284, batch, n, n, 21)
-    o2, e2 = make_pair("DuelingDoubleDQNAgent", 284, batch, n, n, 21)
+    o2, e2 = make_pair("DuelingDoubleDQNAgent", 284, batch, n, n, 21, graphs=graphs)
     for _ in range(6):
         e1.learn_step(soft_update=True)
     for _ in range(5):
