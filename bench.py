@@ -344,13 +344,19 @@ def run_learner(args, eng, world, backend, steps, warmup, dist, device):
 
     chain = args.chain if world == 1 else 1
 
+    # pure learning loop, uniform replay: step t+1's minibatch is drawn inside step t's forward launch
+    prefetch = args.prefetch and not args.algo.startswith("Per") and not bucketed
+
     def step(count=1):
         if world > 1:   # shard compute, RCCL all-reduce (+ PER |delta| all-gather), replicated Adam
-            (dp_learn_step_bucketed if bucketed else dp_learn_step)(eng, soft_update=True)
+            if bucketed:
+                dp_learn_step_bucketed(eng, soft_update=True)
+            else:
+                dp_learn_step(eng, soft_update=True, prefetch=prefetch)
         elif chain > 1:
             eng.learn_steps(count, soft_update=True)
         else:
-            eng.learn_step(soft_update=True, prefetch=args.prefetch)
+            eng.learn_step(soft_update=True, prefetch=prefetch)
     for _ in range(warmup):
         step(chain)
     torch.cuda.synchronize()
@@ -360,14 +366,17 @@ def run_learner(args, eng, world, backend, steps, warmup, dist, device):
         # the whole DP step (shard kernels + RCCL all-reduce + Adam) as one replayed graph: the
         # eager loop is host-bound (3 launches + a collective call per ~50 us step).  RCCL
         # collectives are capturable; gloo's are host calls and never are.
-        g = GraphedDPStep(eng, soft_update=True, bucketed=bucketed)
+        g = GraphedDPStep(eng, soft_update=True, bucketed=bucketed, prefetch=prefetch)
         g()   # one untimed replay
         torch.cuda.synchronize()
         dp_graph = True
         step = g
     el = timed_steps(step, steps, dist, device, chain)
-    if args.prefetch and world == 1 and chain == 1:
-        eng.learn_step(soft_update=True)   # consume the minibatch drawn ahead (no draw pending after)
+    if prefetch and chain == 1:   # consume the minibatch drawn ahead (no draw pending after)
+        if world > 1:
+            dp_learn_step(eng, soft_update=True)
+        else:
+            eng.learn_step(soft_update=True)
     if dp_graph:
         eng.set_graphs(args.graphs)   # GraphedDPStep switched the engine's own graphs off
     eng.check_device_error()
@@ -467,22 +476,32 @@ def single_gpu_extras(args, spec, device):
     W = 8
     eng = make_engine(args, spec, Bg, W, 0, device)
 
-    def shard_step():   # what each rank runs around the all-reduce
-        eng.learn_step(grads_only=True)
+    def shard_step(prefetch=args.prefetch):   # what each rank runs around the all-reduce
+        eng.learn_step(grads_only=True, prefetch=prefetch)
         eng.apply_grads(soft_update=True)
     for _ in range(args.warmup):
         shard_step()
     el = timed_steps(shard_step, steps, None, device)
+    shard_step(prefetch=False)   # consume the pending draw
+    seq = {}
+    if args.prefetch:   # the same shard step with the sampler launch on the critical path
+        for _ in range(args.warmup):
+            shard_step(prefetch=False)
+        el_seq = timed_steps(lambda: shard_step(prefetch=False), steps, None, device)
+        seq = {"shard_step_us_sampler_launch": el_seq / steps * 1e6}
     ks = kernel_times(eng, C.STEP_GRADS_ONLY, count=50, reps=3)
     samp = next((k[1] for k in ks if k[0] == "sample_uniform"), None)
-    out["projection_w8"] = {
+    kpf = kernel_times(eng, C.STEP_GRADS_ONLY | C.STEP_PREFETCH, count=50, reps=3) if args.prefetch else []
+    out["projection_w8"] = dict({
         "rows_per_rank": Bg // W, "global_batch": Bg, "shard_step_us": el / steps * 1e6,
+        "prefetch_sampling": args.prefetch,
         "global_sampling_us": samp,
         "tr_per_s_without_allreduce": Bg / (el / steps),
         "kernels": [{"kernel": k[0], "avg_us": k[1]} for k in ks],
-        "note": "rank 0 of world_size 8 on one GPU: sampler (all 4096 draws) + 512-row shard + grad reduce + "
-                "Adam/soft update (two graph launches); add the RCCL all-reduce of the 428 KB gradient for the "
-                "8-GPU step"}
+        "kernels_prefetch": [{"kernel": k[0], "avg_us": k[1]} for k in kpf],
+        "note": "rank 0 of world_size 8 on one GPU: 512-row shard + grad reduce + Adam/soft update, the global "
+                "4096-draw sampler inside the forward launch (prefetch) or as its own launch; add the RCCL "
+                "all-reduce of the 428 KB gradient for the 8-GPU step"}, **seq)
     del eng
     torch.cuda.empty_cache()
     return out
@@ -535,7 +554,7 @@ def main():
     kernels = []
     if not args.no_kernel_timing:
         flags = C.STEP_GRADS_ONLY if world > 1 else C.STEP_SOFT_UPDATE
-        if world == 1 and args.prefetch:   # the plan the timed loop ran (steady state: no sampler launch)
+        if args.prefetch and not per:   # the plan the timed loop ran (steady state: no sampler launch)
             flags |= C.STEP_PREFETCH
         ks = kernel_times(eng, flags, count=50, reps=5)
         dom = max(ks, key=lambda k: k[1])
@@ -583,7 +602,7 @@ def main():
                 "workload": workload_name(args, world),
                 "algo": args.algo, "net": net_name(args),
                 "batch_per_gpu": Bl, "global_batch": Bg, "replay_capacity": args.capacity,
-                "parallelism": f"dp{world}", "graphs": args.graphs, "prefetch_sampling": args.prefetch and world == 1 and not per,
+                "parallelism": f"dp{world}", "graphs": args.graphs, "prefetch_sampling": args.prefetch and not per and (world == 1 or args.net == "mlp"),
                 "steps_per_call": args.chain if world == 1 else 1,
                 "sampling": "rank-local" if local else "global (reference-exact random.sample on every rank)",
                 "dp_step": ((("one HIP graph" if dp_graph else "eager")

@@ -256,6 +256,10 @@ int dqnx_rng_get(dqnx_engine* e, int32_t which, uint32_t* state625, void* stream
                                        reflects the prefetched draw.  A step without the flag
                                        consumes the pending minibatch. */
 int dqnx_learn_step(dqnx_engine* e, int32_t flags, void* stream);
+/* Draw the first minibatch of a prefetching loop now (no-op when a draw is pending or the
+ * configuration does not draw ahead), so that the next DQNX_STEP_PREFETCH step can be captured
+ * into a caller's graph without its prologue (dqn.data_parallel.GraphedDPStep). */
+int dqnx_prefetch_begin(dqnx_engine* e, int32_t flags, void* stream);
 /* `count` (1..256) consecutive learn steps, bitwise equal to `count` dqnx_learn_step(flags) calls
  * (flags: 0 or DQNX_STEP_SOFT_UPDATE).  Replaces a loop of Agent.learn() +
  * update_target_network() with no host work in between (R:train.py:99-101 repeated, e.g. several

@@ -866,8 +866,13 @@ void build_fused_steps(dqnx_engine* e, int flags, int32_t* idx, int32_t* phys, s
             fa.wblk[1][l] = at<float>(e, e->ws_wblk[1][l]);
         }
         fa.stamps = at<int64_t>(e, e->ws_stamps);
+        if (sample_next) {   // + the next step's minibatch into the staging slot (in-launch prefetch)
+            fa.samp_hs = fwd_sample_hs(sample_next->k);
+            fa.samp = *sample_next;
+            fa.samp.stamps = nullptr;
+        }
         KStep k;
-        k.name = "mlp_fwd";
+        k.name = sample_next ? "mlp_fwd+sample" : "mlp_fwd";
         k.flops = nstreams * Bl * (body_flops + 2.0 * np.NH * np.F);
         // gathered rows in, stream-0 rows + activations + raw heads out, online + target weights
         double hsum = 0;
@@ -1068,19 +1073,19 @@ void build_fused_steps(dqnx_engine* e, int flags, int32_t* idx, int32_t* phys, s
             da.mtc = aa.mtc;
             da.mtc_blocks = aa.mtc_blocks;
             da.stamps = at<int64_t>(e, e->ws_stamps);
-            if (sample_next) {   // + the next step's minibatch (in-launch prefetch)
-                da.with_sample = 1;
-                da.samp = *sample_next;
-                da.samp.mtc = nullptr;
-                da.samp.mtc_blocks = 0;
-                da.samp.stamps = nullptr;
-                da.mtc = nullptr;
+            if (sample_next) {   // the staged minibatch becomes the compute slot's (in-launch prefetch)
+                da.pf_idx_src = sample_next->out;
+                da.pf_idx_dst = idx;
+                da.pf_nidx = e->Bg;
+                da.pf_phys_src = sample_next->phys_out;
+                da.pf_phys_dst = phys;
+                da.pf_nphys = e->Bl;
+                da.mtc = nullptr;   // the forward's sampler body draws from the MT state itself
                 da.mtc_blocks = 0;
             }
             const double P = (double)np.P;
             KStep k;
-            k.name = sample_next ? (da.mode ? "dw_adam16+sample" : "dw16_grads+sample")
-                                 : (da.mode ? "dw_adam16" : "dw16_grads");
+            k.name = da.mode ? "dw_adam16" : "dw16_grads";
             k.flops = flops + (da.mode ? 12.0 * P : 0.0);
             // dZ / X rows once; p, m, v read and written, grads written (+ target read and
             // written); the blocked copies: fwd online (+ fwd target), chain for l >= 1
@@ -1120,8 +1125,9 @@ void build_fused_steps(dqnx_engine* e, int flags, int32_t* idx, int32_t* phys, s
 // buffer pair; KEY_RELAYOUT = the sampler launch also rebuilds the fused plan's blocked weight
 // copies (only after the weights changed outside the Adam pass, which keeps them current).
 constexpr int KEY_RELAYOUT = 0x40;
-// KEY_SAMPLE_NEXT = no sampler launch at the front (the minibatch in `slot` was drawn by the
-// previous step); the last launch draws the next step's minibatch into slot ^ 1 (in-launch prefetch)
+// KEY_SAMPLE_NEXT (in-launch prefetch; the compute slot is 0): no sampler launch at the front (slot
+// 0 holds the minibatch the previous step drew); one more workgroup of the forward launch draws the
+// next step's minibatch into the staging slot 1, and the last launch copies it over slot 0
 constexpr int KEY_SAMPLE_NEXT = 0x80;
 
 SampleArgs uniform_sample_args(dqnx_engine* e, int32_t* idx, int32_t* phys) {
@@ -1147,12 +1153,13 @@ SampleArgs uniform_sample_args(dqnx_engine* e, int32_t* idx, int32_t* phys) {
     return sa;
 }
 
-// The fused plan's last launch can host the next step's sampler: uniform replay, the engine draws
-// its own indices, k_dw_adam16 is the update kernel and k takes the multi-pass sampler body
+// The fused plan's forward launch can host the next step's sampler workgroup: uniform replay, the
+// engine draws its own indices, k_dw_adam16 (which does the slot copy) is the update kernel, and k
+// fits the multi-pass sampler body's LDS table
 bool inlaunch_prefetch_ok(const dqnx_engine* e, int flags) {
     if (getenv("DQNX_PF_SIDE")) return false;   // measurements: the side-stream pipeline instead
     return e->cfg.algo != DQNX_ALGO_PER_DOUBLE && !(flags & DQNX_STEP_GIVEN_INDICES) && dw_adam16_on(e, flags) &&
-           e->Bs <= DW16_SAMPLE_MAX_K && e->mtc_blocks == 0;
+           e->Bs <= FWD_SAMPLE_MAX_K && e->fsplit <= 1 && !e->fplan.bf16;
 }
 
 std::vector<KStep> build_learn_steps(dqnx_engine* e, int key) {
@@ -1211,9 +1218,9 @@ std::vector<KStep> build_learn_steps(dqnx_engine* e, int key) {
     if (e->bwd_plan == 2) {
         SampleArgs nxt;
         const bool sample_next = (key & KEY_SAMPLE_NEXT) != 0;
-        if (sample_next)
-            nxt = uniform_sample_args(e, at<int32_t>(e, e->off[DQNX_BUF_BATCH_IDX]) + (size_t)(slot ^ 1) * e->Bg,
-                                      at<int32_t>(e, e->ws_phys) + (size_t)(slot ^ 1) * e->Bl);
+        if (sample_next)   // the staging slot (the compute slot is slot 0)
+            nxt = uniform_sample_args(e, at<int32_t>(e, e->off[DQNX_BUF_BATCH_IDX]) + (size_t)e->Bg,
+                                      at<int32_t>(e, e->ws_phys) + (size_t)e->Bl);
         build_fused_steps(e, flags, idx, phys, ks, sample_next ? &nxt : nullptr);
         return ks;
     }
@@ -2449,20 +2456,26 @@ static int pf_sample(dqnx_engine* e, int base, int slot) {
 // reads the slot after the launch that filled it.  Results are bitwise those of sequential steps
 // (the sample depends only on the MT state and the ring, which push / rng_set refuse to change
 // while a minibatch is pending).
+static int inlaunch_prologue(dqnx_engine* e, int base, hipStream_t s) {
+    const int key0 = base | (e->wblk_dirty ? KEY_RELAYOUT : 0);
+    const std::vector<KStep>& ks0 = steps_for(e, key0);
+    int rc = run_graphed(e, 0x80000 | key0, s, [&](hipStream_t cs) { return enqueue_range(ks0, 0, 1, cs); });
+    if (rc) return rc;
+    e->wblk_dirty = false;
+    e->pf_valid = true;
+    e->pf_inlaunch = true;
+    e->pf_stream = s;
+    return DQNX_OK;
+}
+
 static int learn_step_inlaunch(dqnx_engine* e, int base, bool prefetch, hipStream_t s) {
     int rc = DQNX_OK;
     if (e->pf_valid && s != e->pf_stream) {   // the pending draw was enqueued on another stream
         DQNX_HIP_CHECK(hipStreamSynchronize(e->pf_stream));
     }
     if (!e->pf_valid) {   // prologue: this step's minibatch by the sampler launch (+ relayout if dirty)
-        const int key0 = base | (e->wblk_dirty ? KEY_RELAYOUT : 0);
-        const std::vector<KStep>& ks0 = steps_for(e, key0);
-        rc = run_graphed(e, 0x80000 | key0, s, [&](hipStream_t cs) { return enqueue_range(ks0, 0, 1, cs); });
+        rc = inlaunch_prologue(e, base, s);
         if (rc) return rc;
-        e->wblk_dirty = false;
-        e->pf_slot = 0;
-        e->pf_valid = true;
-        e->pf_inlaunch = true;
     } else if (e->wblk_dirty) {   // weights written by the host while a minibatch is pending
         int blocks = 0;
         RelayoutArgs rl = relayout_args(e, &blocks);
@@ -2470,8 +2483,7 @@ static int learn_step_inlaunch(dqnx_engine* e, int base, bool prefetch, hipStrea
         if (rc) return rc;
         e->wblk_dirty = false;
     }
-    const int cur = e->pf_slot;
-    const int key = base | (cur << 8) | (prefetch ? KEY_SAMPLE_NEXT : 0);
+    const int key = base | (prefetch ? KEY_SAMPLE_NEXT : 0);
     const std::vector<KStep>& ks = steps_for(e, key);
     rc = run_graphed(e, key | 0x20000, s,
                      [&](hipStream_t cs) { return enqueue_range(ks, prefetch ? 0 : 1, (int)ks.size(), cs); });
@@ -2481,7 +2493,6 @@ static int learn_step_inlaunch(dqnx_engine* e, int base, bool prefetch, hipStrea
         e->pf_inlaunch = false;
         return DQNX_OK;
     }
-    e->pf_slot = cur ^ 1;
     e->pf_stream = s;   // dqnx_rng_get synchronises it (an event record per step cost ~10 us of queue time)
     return DQNX_OK;
 }
@@ -2550,7 +2561,7 @@ int dqnx_learn_step(dqnx_engine* e, int32_t flags, void* stream) {
 
 // `count` consecutive learn steps as ONE graph (pure learning loops, e.g. several learn steps
 // per environment step): the first step's minibatch is drawn by the sampler launch, every
-// later one by the previous step's k_dw_adam16 launch (in-launch prefetch), the last step draws
+// later one by the previous step's forward launch (in-launch prefetch), the last step draws
 // nothing ahead.  Bitwise equal to `count` dqnx_learn_step calls, and nothing is pending after
 // the call.  Configurations without the in-launch sampler (PER, the slab / per-layer plans,
 // k past the multi-pass sampler) run the steps one by one.
@@ -2576,9 +2587,8 @@ int dqnx_learn_steps(dqnx_engine* e, int32_t flags, int32_t count, void* stream)
         const std::vector<KStep>& k0 = steps_for(e, first);   // slot 0: sampler (+ relayout) + step
         int r = enqueue_range(k0, 0, 1, cs);
         for (int i = 0; i < count && !r; i++) {
-            const int slot = i & 1;
             const bool last = i == count - 1;
-            const std::vector<KStep>& ks = steps_for(e, base | (slot << 8) | (last ? 0 : KEY_SAMPLE_NEXT));
+            const std::vector<KStep>& ks = steps_for(e, base | (last ? 0 : KEY_SAMPLE_NEXT));
             r = enqueue_range(ks, last ? 1 : 0, (int)ks.size(), cs);
         }
         return r;
@@ -2594,6 +2604,17 @@ static int timing_key(const dqnx_engine* e, int32_t flags) {
     const int base = flags & 7;
     if ((flags & DQNX_STEP_PREFETCH) && e->bwd_plan == 2 && inlaunch_prefetch_ok(e, base)) return base | KEY_SAMPLE_NEXT;
     return base;
+}
+
+int dqnx_prefetch_begin(dqnx_engine* e, int32_t flags, void* stream) {
+    int rc = check_bound(e);
+    if (rc) return rc;
+    const int base = flags & (DQNX_STEP_SOFT_UPDATE | DQNX_STEP_GRADS_ONLY);
+    if (e->pf_valid || e->cfg.algo == DQNX_ALGO_PER_DOUBLE || !(e->bwd_plan == 2 && inlaunch_prefetch_ok(e, base)))
+        return DQNX_OK;   // a draw is pending already, or this configuration does not draw ahead
+    if (e->ring_size < e->Bs)
+        return set_error(DQNX_EINVAL, "Sample larger than population: %lld < %d", (long long)e->ring_size, e->Bs);
+    return inlaunch_prologue(e, base, (hipStream_t)stream);
 }
 
 int dqnx_learn_kernel_count(dqnx_engine* e, int32_t flags, int32_t* n) {

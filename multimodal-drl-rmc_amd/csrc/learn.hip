@@ -16,7 +16,6 @@
 #include "gemm_sk.hpp"
 #include "learn.hpp"
 #include "mt.hpp"
-#include "sample_body.hpp"
 
 namespace dqnx {
 
@@ -884,42 +883,22 @@ __device__ __forceinline__ int64_t dw16_index(const DwAdam16Layer& d, int row, i
                                   : (int64_t)head_b_off(d.head_kind, row, d.in, d.A));
 }
 
-template <int NW>
-struct Dw16Red {
-    floatx4 red[NW][64];
-    float redb[NW][64];
-};
-template <int NW, bool SAMP>   // SAMP: the launch also hosts the next step's sampler workgroup
-struct Dw16Lds {
-    union {
-        Dw16Red<NW> r;
-        SampleLds<64 * NW, DW16_SAMPLE_HS> s;
-    };
-};
-template <int NW>
-struct Dw16Lds<NW, false> {
-    Dw16Red<NW> r;
-};
-
-template <int DW16_NW, int U, bool SAMP>   // waves per tile; k-steps (4 rows each) per register set, two
-__global__ __launch_bounds__(64 * DW16_NW) void k_dw_adam16(DwAdam16Args a) {   // sets in flight
-    __shared__ Dw16Lds<DW16_NW, SAMP> S;
-    auto& red = S.r.red;
-    auto& redb = S.r.redb;
+template <int DW16_NW, int U>   // waves per tile; k-steps (4 rows each) per register set, two sets in flight
+__global__ __launch_bounds__(64 * DW16_NW) void k_dw_adam16(DwAdam16Args a) {
+    __shared__ floatx4 red[DW16_NW][64];
+    __shared__ float redb[DW16_NW][64];
     const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int i = lane & 15, g = lane >> 4;
-    if constexpr (SAMP) {
-        // step t+1's random.sample (R:dqn/replay_memory.py:38-39) into the other (idx, phys) slot:
-        // it depends only on the MT state and the ring size, which nothing in this step changes
-        if ((int)blockIdx.x == a.tiles) {
-            sample_uniform_body<64 * DW16_NW, DW16_SAMPLE_HS>(a.samp, S.s, S.s.tab);
-            return;
-        }
-    } else {
-        if (a.mtc && (int)blockIdx.x == a.tiles) {   // the extra workgroup: sampler cache for the next step
+    if ((int)blockIdx.x >= a.tiles) {   // extra workgroups: sampler cache, then the staged-minibatch copy
+        if (a.mtc && (int)blockIdx.x == a.tiles) {
             mt_cache_extend(a.mtc, a.mtc_blocks);
-            return;
+        } else {
+            // in-launch prefetch: the forward launch drew the next minibatch into the staging slot;
+            // nothing after this launch reads the compute slot of this step, so it takes the new one
+            for (int q = tid; q < a.pf_nidx; q += blockDim.x) a.pf_idx_dst[q] = a.pf_idx_src[q];
+            for (int q = tid; q < a.pf_nphys; q += blockDim.x) a.pf_phys_dst[q] = a.pf_phys_src[q];
         }
+        return;
     }
     DQNX_STAMP(a.stamps, 56);
     const int T = xcd_remap(blockIdx.x, a.tiles);
@@ -1079,23 +1058,15 @@ __global__ __launch_bounds__(64 * DW16_NW) void k_dw_adam16(DwAdam16Args a) {   
 
 int launch_dw_adam16(const DwAdam16Args& a, hipStream_t s) {
     static const int var = getenv("DQNX_DW16_VAR") ? atoi(getenv("DQNX_DW16_VAR")) : 0;
-    if (a.with_sample) {   // + the next step's sampler workgroup (no MT-cache workgroup: k < the fast path)
-        if (a.mtc || a.samp.k > DW16_SAMPLE_MAX_K || a.samp.rl_blocks)
-            return set_error(DQNX_EINVAL, "dw_adam16: in-launch sampler needs k <= %d, no cache / relayout",
-                             DW16_SAMPLE_MAX_K);
-        hipLaunchKernelGGL((k_dw_adam16<8, 8, true>), dim3(a.tiles + 1), dim3(512), 0, s, a);
-        DQNX_HIP_CHECK(hipGetLastError());
-        return DQNX_OK;
-    }
-    const dim3 grid(a.tiles + (a.mtc ? 1 : 0));
+    const dim3 grid(a.tiles + (a.mtc ? 1 : 0) + (a.pf_nidx > 0 ? 1 : 0));
     switch (var) {   // measurement variants (waves per tile, k-steps per register set)
-        case 1: hipLaunchKernelGGL((k_dw_adam16<4, 8, false>), grid, dim3(256), 0, s, a); break;
-        case 2: hipLaunchKernelGGL((k_dw_adam16<16, 4, false>), grid, dim3(1024), 0, s, a); break;
-        case 3: hipLaunchKernelGGL((k_dw_adam16<8, 4, false>), grid, dim3(512), 0, s, a); break;
-        case 4: hipLaunchKernelGGL((k_dw_adam16<4, 16, false>), grid, dim3(256), 0, s, a); break;
-        case 5: hipLaunchKernelGGL((k_dw_adam16<8, 16, false>), grid, dim3(512), 0, s, a); break;
-        case 6: hipLaunchKernelGGL((k_dw_adam16<16, 8, false>), grid, dim3(1024), 0, s, a); break;
-        default: hipLaunchKernelGGL((k_dw_adam16<8, 8, false>), grid, dim3(512), 0, s, a); break;
+        case 1: hipLaunchKernelGGL((k_dw_adam16<4, 8>), grid, dim3(256), 0, s, a); break;
+        case 2: hipLaunchKernelGGL((k_dw_adam16<16, 4>), grid, dim3(1024), 0, s, a); break;
+        case 3: hipLaunchKernelGGL((k_dw_adam16<8, 4>), grid, dim3(512), 0, s, a); break;
+        case 4: hipLaunchKernelGGL((k_dw_adam16<4, 16>), grid, dim3(256), 0, s, a); break;
+        case 5: hipLaunchKernelGGL((k_dw_adam16<8, 16>), grid, dim3(512), 0, s, a); break;
+        case 6: hipLaunchKernelGGL((k_dw_adam16<16, 8>), grid, dim3(1024), 0, s, a); break;
+        default: hipLaunchKernelGGL((k_dw_adam16<8, 8>), grid, dim3(512), 0, s, a); break;
     }
     DQNX_HIP_CHECK(hipGetLastError());
     return DQNX_OK;

@@ -281,13 +281,15 @@ struct DwAdam16Args {
     uint32_t* mtc;
     int mtc_blocks;
     int64_t* stamps;       // diagnostic builds (-DDQNX_STAMPS): slots 56..61
-    // in-launch prefetch (DQNX_STEP_PREFETCH, uniform replay, k <= DW16_SAMPLE_MAX_K): one more
-    // workgroup (index tiles) draws the NEXT step's minibatch with the uniform sampler's body
-    int with_sample;
-    SampleArgs samp;
+    // in-launch prefetch (DQNX_STEP_PREFETCH): one more workgroup copies the minibatch the forward
+    // launch drew into the staging slot over this step's (pf_nidx = 0: none)
+    const int32_t* pf_idx_src;
+    int32_t* pf_idx_dst;
+    int pf_nidx;
+    const int32_t* pf_phys_src;
+    int32_t* pf_phys_dst;
+    int pf_nphys;
 };
-constexpr int DW16_SAMPLE_HS = 4096;     // LDS hash slots of that workgroup's sampler (32 KiB)
-constexpr int DW16_SAMPLE_MAX_K = 2048;  // k it serves (table <= 3/4 full: k + one pass of words)
 
 // MT block cache: the state block of the uniform sampler and its twisted successors, kept ahead
 // by the Adam launch of the previous step (k_adam's extra workgroup), so the next sample reads the
@@ -414,7 +416,22 @@ struct FusedFwdArgs {
     int kpad[FUSED_MAX_L];       // layer inputs zero padded to kpad (blocked copies): fp32 a multiple of 64, bf16 of 32
     const float* wblk[2][FUSED_MAX_L];   // fragment-blocked W_l of the online / target net (relayout.hpp)
     int64_t* stamps;             // diagnostic builds (-DDQNX_STAMPS): slots 24..39
+    // in-launch prefetch (DQNX_STEP_PREFETCH, uniform replay): one more workgroup (the last)
+    // draws the NEXT step's minibatch into the staging slot with the multi-pass sampler body, on
+    // a CU the row tiles leave idle (samp_hs = its LDS hash slots; 0 = no sampler workgroup)
+    int samp_hs;
+    SampleArgs samp;
 };
+// The forward's sampler workgroup (512 threads): k <= 2048 passes of 3 MT blocks into a 4096-slot
+// table (40 KB of LDS, no more than the forward's own tiles); k <= FWD_SAMPLE_MAX_K one pass of 9
+// blocks into 16384 slots (150 KB: one workgroup per CU, as the forward runs at the shard sizes
+// that use it), so k = 4096 takes one pass instead of three
+constexpr int FWD_SAMPLE_MAX_K = 4608;
+__host__ __device__ constexpr int fwd_sample_ahead(int k) { return k <= 2048 ? 2 : 8; }
+__host__ __device__ constexpr int fwd_sample_hs(int k) { return k <= 2048 ? 4096 : 16384; }
+// LDS of that workgroup: the sampler's MT blocks / scan words, then the hash table (8-byte slots)
+__host__ __device__ constexpr int fwd_sample_tab_off(int k) { return (((fwd_sample_ahead(k) + 1) * 624 + 16) * 4 + 63) / 64 * 64; }
+__host__ __device__ constexpr int fwd_sample_lds_bytes(int k) { return fwd_sample_tab_off(k) + 8 * fwd_sample_hs(k); }
 struct HeadBwdArgs {
     int L, Bl, A, NH, F, head_kind, algo;
     int nsplit;                  // workgroups per 16-sample tile (split the last dZ's columns)

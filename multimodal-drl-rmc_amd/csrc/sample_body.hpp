@@ -25,18 +25,20 @@ __device__ __forceinline__ uint32_t hash_u32(uint32_t x) {
     return x;
 }
 
-// threads -> MT blocks twisted ahead per pass and words per thread per pass
-// ((624 * (1 + AHEAD)) / NT rounded up)
+// threads -> MT blocks twisted ahead per pass (AH; default 4 at 1024 threads, 2 below) and words
+// per thread per pass ((624 * (1 + AH)) / NT rounded up)
 template <int NT>
+constexpr int sample_default_ahead() { return NT >= 1024 ? 4 : 2; }
+template <int NT, int AH = sample_default_ahead<NT>()>
 struct SampleShape {
     static_assert(NT >= 256 && NT % 64 == 0, "the twist needs >= 227 threads");
-    static constexpr int AHEAD = NT >= 1024 ? 4 : 2;
+    static constexpr int AHEAD = AH;
     static constexpr int WPT = (624 * (1 + AHEAD) + NT - 1) / NT;
 };
 
-template <int NT>
+template <int NT, int AH = sample_default_ahead<NT>()>
 struct SampleLdsBase {
-    uint32_t blk[SampleShape<NT>::AHEAD + 1][624];   // [0] current block, [1..] twisted ahead
+    uint32_t blk[AH + 1][624];   // [0] current block, [1..] twisted ahead
     int wave_tot[NT / 64];
     int s_final;
 };
@@ -46,10 +48,10 @@ struct SampleLds : SampleLdsBase<NT> {
 };
 
 // `tab`: HS slots in LDS, or (k too large for LDS) in global memory, used by this one workgroup
-template <int NT, int HS>
-__device__ __forceinline__ void sample_uniform_body(const SampleArgs& a, SampleLdsBase<NT>& S,
+template <int NT, int HS, int AH = sample_default_ahead<NT>()>
+__device__ __forceinline__ void sample_uniform_body(const SampleArgs& a, SampleLdsBase<NT, AH>& S,
                                                     unsigned long long* tab) {
-    constexpr int NW = NT / 64, AHEAD = SampleShape<NT>::AHEAD, WPT = SampleShape<NT>::WPT;
+    constexpr int NW = NT / 64, AHEAD = SampleShape<NT, AH>::AHEAD, WPT = SampleShape<NT, AH>::WPT;
     auto& blk = S.blk;
     int* wave_tot = S.wave_tot;
     int& s_final = S.s_final;

@@ -26,10 +26,16 @@ def shard_bounds(batch: int, world: int, rank: int):
     return rank * per, (rank + 1) * per
 
 
-def dp_learn_step(engine, soft_update: bool = True, group=None):
+def dp_learn_step(engine, soft_update: bool = True, group=None, prefetch: bool = False):
     """One data-parallel learn step (+ soft target update) on `engine` (a LearnEngine built
-    with world_size / rank).  Collectives are enqueued on the current stream."""
-    engine.learn_step(grads_only=True)
+    with world_size / rank).  Collectives are enqueued on the current stream.
+    prefetch=True (pure learning loops, uniform replay): the shard's forward launch also draws the
+    NEXT step's global minibatch (DQNX_STEP_PREFETCH), so the O(B_global) sampler leaves the
+    critical path; a step with prefetch=False consumes the pending draw."""
+    if prefetch:
+        engine.learn_step(grads_only=True, prefetch=True)
+    else:
+        engine.learn_step(grads_only=True)
     exchange(engine, group)
     engine.apply_grads(soft_update=soft_update)
 
@@ -100,17 +106,23 @@ class GraphedDPStep:
     off: its kernels become nodes of this graph.
     """
 
-    def __init__(self, engine, soft_update: bool = True, group=None, bucketed: bool = False):
+    def __init__(self, engine, soft_update: bool = True, group=None, bucketed: bool = False, prefetch: bool = False):
+        """prefetch=True: capture the prefetching step (each replay computes on the minibatch the
+        previous one drew and draws the next; see dp_learn_step).  The first draw is made here,
+        before the capture; run one dp_learn_step(prefetch=False) after the last replay to
+        consume the pending draw."""
         self.engine = engine
         engine.set_graphs(False)
         self.graph = torch.cuda.CUDAGraph()
         self.comm = torch.cuda.Stream(engine.grads.device) if bucketed else None
+        if prefetch and not bucketed:
+            engine.prefetch_prologue()
         torch.cuda.synchronize()
         with torch.cuda.graph(self.graph):
             if bucketed:   # the side stream forks and joins inside the capture
                 dp_learn_step_bucketed(engine, soft_update=soft_update, group=group, comm_stream=self.comm)
             else:
-                dp_learn_step(engine, soft_update=soft_update, group=group)
+                dp_learn_step(engine, soft_update=soft_update, group=group, prefetch=prefetch)
         torch.cuda.synchronize()
 
     def __call__(self):

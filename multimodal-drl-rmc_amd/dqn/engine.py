@@ -370,6 +370,11 @@ class LearnEngine:
         if self.cfg.algo == C.DQNX_ALGO_PER_DOUBLE:   # every PER learn step samples: step += n_env
             self.agent_step += self.cfg.n_env
 
+    def prefetch_prologue(self, grads_only=True):
+        """Draw the first minibatch of a prefetching loop now (dqnx_prefetch_begin)."""
+        C.check(self.L.dqnx_prefetch_begin(self.h, C.STEP_GRADS_ONLY if grads_only else 0, self.stream()),
+                "prefetch_begin")
+
     def learn_steps(self, count: int, soft_update=False):
         """`count` consecutive learn steps in one call (dqnx_learn_steps): bitwise equal to
         `count` learn_step(soft_update) calls; one graph on the fused MLP plan, with every step's

@@ -98,12 +98,13 @@ def test_gpu_dp_world2_rank_local_sampling(tmp_path):
 def test_gpu_graphed_dp_step_matches_eager(algo):
     """dqn.data_parallel.GraphedDPStep (learn kernels + RCCL all-reduce + Adam captured as one
     HIP graph) continues exactly like eager dp_learn_step calls (world 1 over RCCL, one GPU),
-    and both equal the single-GPU learn step; the script asserts it."""
+    and both equal the single-GPU learn step; so does the graphed prefetching DP step (the next
+    global minibatch drawn inside the forward launch); the script asserts it."""
     env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(free_port()))
     r = subprocess.run([sys.executable, os.path.join(os.path.dirname(HERE), "tools", "dp_graph_check.py"), algo, "256"],
                        env=env, capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
-    assert "graphed == eager: True; dp == single: True" in r.stdout, r.stdout[-2000:]
+    assert "graphed == eager: True; dp == single: True; prefetch == eager: True" in r.stdout, r.stdout[-2000:]
 
 
 @pytest.mark.parametrize("world", [2, 8])

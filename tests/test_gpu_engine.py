@@ -468,6 +468,38 @@ def test_gpu_learn_steps_equal_single_steps(algo, batch, count, n_fill):
     e2.push(*O.synth_transitions(4, 284, 8, seed=3))
 
 
+@pytest.mark.parametrize("world,k", [(8, 4096), (4, 4096), (2, 2048)])
+def test_gpu_prefetch_dp_shard_step_bit_identical(world, k):
+    """configs[3] shard step (rank 0 of `world`, global minibatch k): the next GLOBAL minibatch
+    drawn inside the forward launch (the 8192-slot sampler table at k = 4096) gives the same
+    gradients and weights as the sampler launch, bitwise."""
+    E = _engine_mod()
+    ospec = O.mlp_spec(284, 8, "dueling")
+    init = O.reference_init(ospec, 41)
+    data = O.synth_transitions(12000, 284, 8, seed=141)
+    engines = []
+    for _ in range(2):
+        eng = E.LearnEngine(E.mlp_spec(284, 8, "dueling"), "DuelingDoubleDQNAgent", k, 12000,
+                            world_size=world, rank=0)
+        eng.load_params(init)
+        eng.push(*data)
+        random.seed(48)
+        eng.set_rng(0, O.py_state_to_array())
+        engines.append(eng)
+    e1, e2 = engines
+    for i in range(4):
+        e1.learn_step(grads_only=True)
+        e1.apply_grads(soft_update=True)
+        e2.learn_step(grads_only=True, prefetch=i < 3)
+        e2.apply_grads(soft_update=True)
+    torch.cuda.synchronize()
+    e1.check_device_error()
+    e2.check_device_error()
+    assert torch.equal(e1.grads, e2.grads)
+    assert torch.equal(e1.params, e2.params) and torch.equal(e1.target_params, e2.target_params)
+    assert np.array_equal(e1.get_rng(0), e2.get_rng(0))
+
+
 def test_gpu_prefetch_fused_weights_written_while_pending():
     """Fused plan, in-launch prefetch: host-side weight writes (load_params) while a minibatch is
     pending rebuild the blocked copies before the next step, and the step matches a sequential

@@ -70,9 +70,24 @@ for _ in range(N):
     c.learn_step(soft_update=True)
 torch.cuda.synchronize()
 single_ms = (time.perf_counter() - t0) / N * 1e3
+# the prefetching DP step (next global minibatch drawn inside the forward launch), graphed
+d = make()
+for _ in range(3):
+    dp_learn_step(d, prefetch=True)
+gp = GraphedDPStep(d, prefetch=True)
+torch.cuda.synchronize()
+t0 = time.perf_counter()
+for _ in range(N - 1):
+    gp()
+torch.cuda.synchronize()
+pf_ms = (time.perf_counter() - t0) / (N - 1) * 1e3
+dp_learn_step(d)   # consumes the pending draw: N + 3 steps in all, like the others
+torch.cuda.synchronize()
 same = torch.equal(a.params, b.params) and torch.equal(a.target_params, b.target_params)
 same_single = torch.equal(a.params, c.params)
+same_pf = torch.equal(a.params, d.params) and torch.equal(a.target_params, d.target_params)
 print(f"{algo} B={B}: eager dp step {eager_ms * 1e3:.1f} us, graphed dp step {graph_ms * 1e3:.1f} us, "
-      f"single-GPU learn step {single_ms * 1e3:.1f} us; graphed == eager: {same}; dp == single: {same_single}")
+      f"graphed prefetching dp step {pf_ms * 1e3:.1f} us, single-GPU learn step {single_ms * 1e3:.1f} us; "
+      f"graphed == eager: {same}; dp == single: {same_single}; prefetch == eager: {same_pf}")
 dist.destroy_process_group()
-assert same and same_single
+assert same and same_single and same_pf
