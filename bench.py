@@ -75,6 +75,10 @@ def parse():
                    help="replay every learn step as a captured HIP graph (default: eager launches, 3-4 us per "
                         "step faster on MI355X / ROCm 7.2: each hipGraphLaunch adds ~8.5 us between graphs)")
     p.add_argument("--no-graphs", action="store_true", help="(the default; kept for old command lines)")
+    p.add_argument("--dp-graph-steps", type=int, default=4,
+                   help="N > 1: DP steps captured back to back into the one replayed graph (every hipGraphLaunch "
+                        "leaves ~8.5 us before its first kernel); the timed K steps are K // this replays plus "
+                        "the remainder as eager steps")
     p.add_argument("--no-dp-graph", action="store_true",
                    help="N > 1: launch the learn graph, the all-reduce and Adam separately each step "
                         "instead of replaying them as one captured HIP graph")
@@ -335,20 +339,21 @@ def timed_steps(step, steps, dist, device, chain=1):
     return el
 
 
-def run_learner(args, eng, world, backend, steps, warmup, dist, device):
+def run_learner(args, eng, world, backend, steps, warmup, dist, device, dp=None):
     """Warm up, then time `steps` learn steps (single GPU: the engine's graph; DP: the whole DP
     step as one HIP graph over RCCL).  Returns (seconds, dp_graph)."""
     # conv nets exchange per-layer gradient buckets on a side stream, overlapped with the rest of
     # the backward (dp_learn_step_bucketed); the MLP's 428 KB gradient stays one all-reduce
-    bucketed = world > 1 and args.net != "mlp" and not args.no_buckets
+    dp = world > 1 if dp is None else dp   # the data-parallel step (DQNX_BENCH_FORCE_DP: also at world 1)
+    bucketed = dp and args.net != "mlp" and not args.no_buckets
 
-    chain = args.chain if world == 1 else 1
+    chain = args.chain if not dp else 1
 
     # pure learning loop, uniform replay: step t+1's minibatch is drawn inside step t's forward launch
     prefetch = args.prefetch and not args.algo.startswith("Per") and not bucketed
 
     def step(count=1):
-        if world > 1:   # shard compute, RCCL all-reduce (+ PER |delta| all-gather), replicated Adam
+        if dp:   # shard compute, RCCL all-reduce (+ PER |delta| all-gather), replicated Adam
             if bucketed:
                 dp_learn_step_bucketed(eng, soft_update=True)
             else:
@@ -362,18 +367,26 @@ def run_learner(args, eng, world, backend, steps, warmup, dist, device):
     torch.cuda.synchronize()
     eng.check_device_error()
     dp_graph = False
-    if world > 1 and backend == "nccl" and not args.no_dp_graph:
+    if dp and backend == "nccl" and not args.no_dp_graph:
         # the whole DP step (shard kernels + RCCL all-reduce + Adam) as one replayed graph: the
         # eager loop is host-bound (3 launches + a collective call per ~50 us step).  RCCL
         # collectives are capturable; gloo's are host calls and never are.
-        g = GraphedDPStep(eng, soft_update=True, bucketed=bucketed, prefetch=prefetch)
+        gs = max(1, args.dp_graph_steps)
+        g = GraphedDPStep(eng, soft_update=True, bucketed=bucketed, prefetch=prefetch, steps=gs)
         g()   # one untimed replay
         torch.cuda.synchronize()
         dp_graph = True
-        step = g
+        eager_step = step
+
+        def step(count=1):   # count steps: whole replays, the remainder eagerly
+            for _ in range(count // gs):
+                g()
+            for _ in range(count % gs):
+                eager_step()
+        chain = gs
     el = timed_steps(step, steps, dist, device, chain)
-    if prefetch and chain == 1:   # consume the minibatch drawn ahead (no draw pending after)
-        if world > 1:
+    if prefetch and (dp or chain == 1):   # consume the minibatch drawn ahead (none pending after)
+        if dp:
             dp_learn_step(eng, soft_update=True)
         else:
             eng.learn_step(soft_update=True)
@@ -520,7 +533,10 @@ def main():
     device = torch.device("cuda", dev_index)
     dist = None
     backend = None
-    if world > 1:
+    # DQNX_BENCH_FORCE_DP=1 (rehearsal on a one-GPU box): the N > 1 code path -- process group,
+    # GraphedDPStep over RCCL, global-batch sharding -- at world size 1
+    dpmode = world > 1 or os.environ.get("DQNX_BENCH_FORCE_DP") == "1"
+    if dpmode:
         import torch.distributed as dist
         backend = os.environ.get("DQNX_DIST_BACKEND", "nccl")   # nccl = RCCL over xGMI
         if backend == "nccl":
@@ -530,7 +546,7 @@ def main():
 
     spec = make_spec(args)
     per = args.algo.startswith("Per")
-    if world == 1:
+    if not dpmode:
         Bg = args.batch or 1024
         scaling = "strong"
     elif args.scaling == "strong":
@@ -542,9 +558,9 @@ def main():
     if Bg % world:
         raise SystemExit(f"global batch {Bg} is not a multiple of {world} ranks")
     Bl = Bg // world
-    local = world > 1 and args.local_sampling and not per
+    local = dpmode and args.local_sampling and not per
     eng = make_engine(args, spec, Bg, world, rank, device, local=local)
-    el, dp_graph = run_learner(args, eng, world, backend, args.steps, args.warmup, dist, device)
+    el, dp_graph = run_learner(args, eng, world, backend, args.steps, args.warmup, dist, device, dp=dpmode)
     loss = eng.loss()
     ms_per_step = el / args.steps * 1e3
     value = Bg * args.steps / el
@@ -553,7 +569,7 @@ def main():
     roofline = None
     kernels = []
     if not args.no_kernel_timing:
-        flags = C.STEP_GRADS_ONLY if world > 1 else C.STEP_SOFT_UPDATE
+        flags = C.STEP_GRADS_ONLY if dpmode else C.STEP_SOFT_UPDATE
         if args.prefetch and not per:   # the plan the timed loop ran (steady state: no sampler launch)
             flags |= C.STEP_PREFETCH
         ks = kernel_times(eng, flags, count=50, reps=5)
@@ -568,17 +584,17 @@ def main():
     if not args.no_extras and args.net == "mlp" and not per and args.compute == "fp32":
         del eng
         torch.cuda.empty_cache()
-        if world == 1:
+        if not dpmode:
             extras = single_gpu_extras(args, spec, device)
         elif scaling == "strong":   # the weak-scaling companion line: 4096 rows per rank
             weng = make_engine(args, spec, 4096 * world, world, rank, device, local=local)
-            wel, _ = run_learner(args, weng, world, backend, args.steps, args.warmup, dist, device)
+            wel, _ = run_learner(args, weng, world, backend, args.steps, args.warmup, dist, device, dp=dpmode)
             extras["weak"] = {"value": 4096 * world * args.steps / wel, "ms_per_step": wel / args.steps * 1e3,
                               "batch_per_gpu": 4096, "global_batch": 4096 * world}
             del weng
 
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and not dpmode and not args.no_cpu_baseline:
         try:
             cpu = cpu_baseline(args, Bg)
         except Exception as ex:  # the baseline must never hide the GPU number
@@ -603,11 +619,11 @@ def main():
                 "algo": args.algo, "net": net_name(args),
                 "batch_per_gpu": Bl, "global_batch": Bg, "replay_capacity": args.capacity,
                 "parallelism": f"dp{world}", "graphs": args.graphs, "prefetch_sampling": args.prefetch and not per and (world == 1 or args.net == "mlp"),
-                "steps_per_call": args.chain if world == 1 else 1,
+                "steps_per_call": args.chain if not dpmode else 1,
                 "sampling": "rank-local" if local else "global (reference-exact random.sample on every rank)",
-                "dp_step": ((("one HIP graph" if dp_graph else "eager")
+                "dp_step": (((f"one HIP graph per {args.dp_graph_steps} steps" if dp_graph else "eager")
                              + (", per-layer gradient buckets" if args.net != "mlp" and not args.no_buckets else ""))
-                            if world > 1 else None),
+                            if dpmode else None),
                 "compute": args.compute,
             },
             "roofline": roofline,

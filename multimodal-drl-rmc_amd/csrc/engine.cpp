@@ -427,7 +427,8 @@ struct dqnx_engine {
     FusedFwdArgs fplan;     // LDS geometry of the fused plan (valid when bwd_plan == 2)
     int fsplit = 1;         // layer-1 column parts of the split forward (1: one forward launch)
     bool pf_valid = false;   // a prefetched minibatch for the next step sits in slot pf_slot
-    bool pf_inlaunch = false;   // ... drawn by the previous step's k_dw_adam16 launch (fused plan)
+    bool pf_inlaunch = false;   // ... drawn by the previous step's forward launch (fused plan)
+    int n_cu = 256;             // compute units of the device (hipDeviceAttributeMultiprocessorCount)
     hipStream_t pf_stream = nullptr;   // ... on this stream
     int pf_slot = 0;
 };
@@ -867,7 +868,10 @@ void build_fused_steps(dqnx_engine* e, int flags, int32_t* idx, int32_t* phys, s
         }
         fa.stamps = at<int64_t>(e, e->ws_stamps);
         if (sample_next) {   // + the next step's minibatch into the staging slot (in-launch prefetch)
-            fa.samp_hs = fwd_sample_hs(sample_next->k);
+            // the one-pass shape only when the row tiles leave a CU idle (its LDS allows one
+            // workgroup per CU); else the 3-block passes, whose LDS keeps two per CU
+            const int wgs = fa.tiles * nstreams + 1;
+            fa.samp_shape = sample_next->k <= 2048 ? 1 : (wgs <= e->n_cu ? 3 : 2);
             fa.samp = *sample_next;
             fa.samp.stamps = nullptr;
         }
@@ -1117,6 +1121,21 @@ void build_fused_steps(dqnx_engine* e, int flags, int32_t* idx, int32_t* phys, s
             k.run = [=](hipStream_t s) { return launch_bwd_level(ba, act, s); };
             ks.push_back(k);
         }
+        if (sample_next) {   // the Adam launch's last workgroup takes the staged minibatch over
+            AdamArgs aa;
+            KStep k = adam_kstep(e, flags, &aa);
+            aa.pf_idx_src = sample_next->out;
+            aa.pf_idx_dst = idx;
+            aa.pf_nidx = e->Bg;
+            aa.pf_phys_src = sample_next->phys_out;
+            aa.pf_phys_dst = phys;
+            aa.pf_nphys = e->Bl;
+            aa.mtc = nullptr;   // the forward's sampler body draws from the MT state itself
+            aa.mtc_blocks = 0;
+            k.run = [=](hipStream_t s) { return launch_adam(aa, s); };
+            ks.push_back(k);
+            return;
+        }
         ks.push_back(adam_kstep(e, flags));
     }
 }
@@ -1154,12 +1173,13 @@ SampleArgs uniform_sample_args(dqnx_engine* e, int32_t* idx, int32_t* phys) {
 }
 
 // The fused plan's forward launch can host the next step's sampler workgroup: uniform replay, the
-// engine draws its own indices, k_dw_adam16 (which does the slot copy) is the update kernel, and k
-// fits the multi-pass sampler body's LDS table
+// engine draws its own indices, the whole forward is one launch, and k fits the multi-pass sampler
+// body's LDS table.  The step's last launch (k_dw_adam16, or the slab plan's Adam pass) copies the
+// staged minibatch over the compute slot.
 bool inlaunch_prefetch_ok(const dqnx_engine* e, int flags) {
     if (getenv("DQNX_PF_SIDE")) return false;   // measurements: the side-stream pipeline instead
-    return e->cfg.algo != DQNX_ALGO_PER_DOUBLE && !(flags & DQNX_STEP_GIVEN_INDICES) && dw_adam16_on(e, flags) &&
-           e->Bs <= FWD_SAMPLE_MAX_K && e->fsplit <= 1 && !e->fplan.bf16;
+    return e->bwd_plan == 2 && e->cfg.algo != DQNX_ALGO_PER_DOUBLE && !(flags & DQNX_STEP_GIVEN_INDICES) &&
+           e->Bs <= FWD_SAMPLE_MAX_K && e->fsplit <= 1;
 }
 
 std::vector<KStep> build_learn_steps(dqnx_engine* e, int key) {
@@ -2264,6 +2284,10 @@ int dqnx_engine_bind(dqnx_engine* e, void* arena, uint64_t bytes) {
     drop_graphs(e);
     e->arena = (char*)arena;
     e->wblk_dirty = true;
+    int dev = 0, cus = 0;   // the current device's compute units (plans that size grids to the chip)
+    if (hipGetDevice(&dev) == hipSuccess &&
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && cus > 0)
+        e->n_cu = cus;
     return DQNX_OK;
 }
 
@@ -2456,6 +2480,14 @@ static int pf_sample(dqnx_engine* e, int base, int slot) {
 // reads the slot after the launch that filled it.  Results are bitwise those of sequential steps
 // (the sample depends only on the MT state and the ring, which push / rng_set refuse to change
 // while a minibatch is pending).
+// The fused plan's blocked weight copies rebuilt by a launch of their own (a step whose minibatch
+// was drawn ahead has no sampler launch whose spare workgroups would do it)
+static int enqueue_relayout(dqnx_engine* e, hipStream_t s) {
+    int blocks = 0;
+    RelayoutArgs rl = relayout_args(e, &blocks);
+    return launch_idx_to_phys(nullptr, nullptr, 0, 0, ctrl_of(e), e->cfg.capacity, &rl, blocks, s);
+}
+
 static int inlaunch_prologue(dqnx_engine* e, int base, hipStream_t s) {
     const int key0 = base | (e->wblk_dirty ? KEY_RELAYOUT : 0);
     const std::vector<KStep>& ks0 = steps_for(e, key0);
@@ -2476,10 +2508,8 @@ static int learn_step_inlaunch(dqnx_engine* e, int base, bool prefetch, hipStrea
     if (!e->pf_valid) {   // prologue: this step's minibatch by the sampler launch (+ relayout if dirty)
         rc = inlaunch_prologue(e, base, s);
         if (rc) return rc;
-    } else if (e->wblk_dirty) {   // weights written by the host while a minibatch is pending
-        int blocks = 0;
-        RelayoutArgs rl = relayout_args(e, &blocks);
-        rc = launch_idx_to_phys(nullptr, nullptr, 0, 0, ctrl_of(e), e->cfg.capacity, &rl, blocks, s);
+    } else if (e->wblk_dirty) {   // weights changed outside a blocked-copy-keeping update
+        rc = enqueue_relayout(e, s);
         if (rc) return rc;
         e->wblk_dirty = false;
     }
@@ -2488,6 +2518,9 @@ static int learn_step_inlaunch(dqnx_engine* e, int base, bool prefetch, hipStrea
     rc = run_graphed(e, key | 0x20000, s,
                      [&](hipStream_t cs) { return enqueue_range(ks, prefetch ? 0 : 1, (int)ks.size(), cs); });
     if (rc) return rc;
+    // the slab plan's Adam pass (and a GRADS_ONLY step's later dqnx_apply_grads) leaves the blocked
+    // copies behind: the next step rebuilds them first (with no sampler launch to host it)
+    if (!blk_kept(e, base)) e->wblk_dirty = true;
     if (!prefetch) {   // consumed the pending minibatch; nothing drawn ahead
         e->pf_valid = false;
         e->pf_inlaunch = false;
@@ -2522,7 +2555,7 @@ int dqnx_learn_step(dqnx_engine* e, int32_t flags, void* stream) {
         const int key = base | ((e->bwd_plan == 2 && (e->wblk_dirty || !blk_kept(e, base))) ? KEY_RELAYOUT : 0);
         const std::vector<KStep>& ks = steps_for(e, key);
         rc = run_graphed(e, key, s, [&](hipStream_t cs) { return enqueue_range(ks, 0, (int)ks.size(), cs); });
-        if (!rc) e->wblk_dirty = false;
+        if (!rc) e->wblk_dirty = !blk_kept(e, base);   // stale again after an update that does not keep them
         return rc;
     }
     rc = pf_events(e);
@@ -2586,14 +2619,16 @@ int dqnx_learn_steps(dqnx_engine* e, int32_t flags, int32_t count, void* stream)
     rc = run_graphed(e, 0x40000000 | (count << 12) | first, s, [&](hipStream_t cs) {
         const std::vector<KStep>& k0 = steps_for(e, first);   // slot 0: sampler (+ relayout) + step
         int r = enqueue_range(k0, 0, 1, cs);
+        const bool kept = blk_kept(e, base);
         for (int i = 0; i < count && !r; i++) {
             const bool last = i == count - 1;
+            if (i > 0 && !kept) r = enqueue_relayout(e, cs);   // the previous step's Adam left them behind
             const std::vector<KStep>& ks = steps_for(e, base | (last ? 0 : KEY_SAMPLE_NEXT));
-            r = enqueue_range(ks, last ? 1 : 0, (int)ks.size(), cs);
+            if (!r) r = enqueue_range(ks, last ? 1 : 0, (int)ks.size(), cs);
         }
         return r;
     });
-    if (!rc) e->wblk_dirty = false;
+    if (!rc) e->wblk_dirty = !blk_kept(e, base);
     return rc;
 }
 

@@ -288,30 +288,28 @@ __global__ __launch_bounds__(FT) void k_mlp_fwd(FusedFwdArgs a) {
     // LDS tile b: pointer arithmetic on `lds` keeps the LDS address space visible to the
     // compiler (ds_read, not flat loads that share the vmcnt counter with the W stream)
 #define FBUF(b) (lds + ((b) ? a.buf0 : 0))
-    if (a.samp_hs && (int)blockIdx.x == (int)gridDim.x - 1) {
+    if (a.samp_shape && blockIdx.x == 0) {   // (dispatched first: it starts even when the grid exceeds the chip)
         // in-launch prefetch: the next step's random.sample (R:dqn/replay_memory.py:38-39) into the
         // staging slot.  It reads only the MT state and the ring's size / write pointer, which no
         // kernel of this step writes (the replay push is refused while a draw is pending).
-        static_assert(sizeof(SampleLdsBase<FT, fwd_sample_ahead(2048)>) <= (size_t)fwd_sample_tab_off(2048) &&
-                      sizeof(SampleLdsBase<FT, fwd_sample_ahead(4096)>) <= (size_t)fwd_sample_tab_off(4096),
-                      "sampler LDS layout");
-        if (a.samp_hs == fwd_sample_hs(2048)) {
-            constexpr int AH = fwd_sample_ahead(2048);
-            sample_uniform_body<FT, fwd_sample_hs(2048), AH>(
-                a.samp, *reinterpret_cast<SampleLdsBase<FT, AH>*>(lds),
-                reinterpret_cast<unsigned long long*>(reinterpret_cast<char*>(lds) + fwd_sample_tab_off(2048)));
-        } else {
-            constexpr int AH = fwd_sample_ahead(4096);
-            sample_uniform_body<FT, fwd_sample_hs(4096), AH>(
-                a.samp, *reinterpret_cast<SampleLdsBase<FT, AH>*>(lds),
-                reinterpret_cast<unsigned long long*>(reinterpret_cast<char*>(lds) + fwd_sample_tab_off(4096)));
-        }
+#define FWD_SAMPLER(SH)                                                                              \
+        do {                                                                                         \
+            constexpr int AH = fwd_sample_ahead(SH);                                                 \
+            static_assert(sizeof(SampleLdsBase<FT, AH>) <= (size_t)fwd_sample_tab_off(SH), "layout"); \
+            sample_uniform_body<FT, fwd_sample_hs(SH), AH>(                                          \
+                a.samp, *reinterpret_cast<SampleLdsBase<FT, AH>*>(lds),                               \
+                reinterpret_cast<unsigned long long*>(reinterpret_cast<char*>(lds) + fwd_sample_tab_off(SH))); \
+        } while (0)
+        if (a.samp_shape == 1) FWD_SAMPLER(1);
+        else if (a.samp_shape == 2) FWD_SAMPLER(2);
+        else FWD_SAMPLER(3);
+#undef FWD_SAMPLER
         return;
     }
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int i = lane & 15, g = lane >> 4;
     const int nsp = PH == 1 ? a.csplit : 1;
-    const int T0 = xcd_remap(blockIdx.x, a.tiles * a.nstreams * nsp);
+    const int T0 = xcd_remap((int)blockIdx.x - (a.samp_shape ? 1 : 0), a.tiles * a.nstreams * nsp);
     const int part = T0 % nsp, T = T0 / nsp;   // the parts of one row tile are neighbours (one XCD)
     const int z = T / a.tiles, tile = T - z * a.tiles;
     const int s = a.stream_of[z];
@@ -967,12 +965,13 @@ static void allow_lds(K kern, size_t bytes) {
 int launch_fused_fwd(const FusedFwdArgs& a, int act, hipStream_t s) {
     if (a.phase != 0 && (a.L < 2 || a.mr != 1 || (a.phase == 1 && (a.csplit < 1 || a.out[0] % (16 * a.csplit)))))
         return set_error(DQNX_EUNSUPPORTED, "split forward: L >= 2, 16-row tiles, layer 1 width / parts a multiple of 16");
-    if (a.samp_hs && (a.phase != 0 || a.samp_hs != fwd_sample_hs(a.samp.k) || a.samp.k > FWD_SAMPLE_MAX_K))
+    if (a.samp_shape && (a.phase != 0 || a.samp_shape > 3 || a.samp.k > FWD_SAMPLE_MAX_K ||
+                         (a.samp_shape == 1 && a.samp.k > 2048)))
         return set_error(DQNX_EUNSUPPORTED, "forward sampler workgroup: whole forward, k <= %d", FWD_SAMPLE_MAX_K);
-    const dim3 grid(a.tiles * a.nstreams * (a.phase == 1 ? a.csplit : 1) + (a.samp_hs ? 1 : 0)), block(FT);
+    const dim3 grid(a.tiles * a.nstreams * (a.phase == 1 ? a.csplit : 1) + (a.samp_shape ? 1 : 0)), block(FT);
     size_t shm = (size_t)(a.buf0 + a.buf1) * 4;
     if (shm < (size_t)DQNX_FUSED_LDS_MIN) shm = DQNX_FUSED_LDS_MIN;
-    if (a.samp_hs && shm < (size_t)fwd_sample_lds_bytes(a.samp.k)) shm = fwd_sample_lds_bytes(a.samp.k);
+    if (a.samp_shape && shm < (size_t)fwd_sample_lds_bytes(a.samp_shape)) shm = fwd_sample_lds_bytes(a.samp_shape);
 #define FUSED_FWD_MR(ACTV, NLV, BFV, MRV, PHV)                                                       \
     do {                                                                                             \
         if (shm > 64 * 1024) allow_lds(k_mlp_fwd<ACTV, NLV, BFV, MRV, PHV>, 160 * 1024);             \

@@ -677,13 +677,26 @@ __device__ __forceinline__ void blk_store(float* base, int64_t pos, float v, boo
     else base[pos] = v;
 }
 
-__global__ __launch_bounds__(256) void k_adam(AdamArgs a) {
-    if (a.mtc && blockIdx.x == gridDim.x - 1) {   // the extra workgroup: sampler cache for the next step
+// The Adam launch's extra workgroups, after the element blocks: the sampler's MT block cache
+// (a.mtc), then the in-launch prefetch's copy of the staged minibatch over the compute slot
+// (a.pf_nidx > 0; every reader of the step's minibatch ran in earlier launches).
+__device__ __forceinline__ int adam_extra_count(const AdamArgs& a) { return (a.mtc ? 1 : 0) + (a.pf_nidx > 0 ? 1 : 0); }
+__device__ __forceinline__ bool adam_extra_wg(const AdamArgs& a) {
+    const int first = (int)gridDim.x - adam_extra_count(a);
+    if ((int)blockIdx.x < first) return false;
+    if (a.mtc && (int)blockIdx.x == first) {
         mt_cache_extend(a.mtc, a.mtc_blocks);
-        return;
+    } else {
+        for (int q = threadIdx.x; q < a.pf_nidx; q += blockDim.x) a.pf_idx_dst[q] = a.pf_idx_src[q];
+        for (int q = threadIdx.x; q < a.pf_nphys; q += blockDim.x) a.pf_phys_dst[q] = a.pf_phys_src[q];
     }
+    return true;
+}
+
+__global__ __launch_bounds__(256) void k_adam(AdamArgs a) {
+    if (adam_extra_wg(a)) return;   // the sampler-cache / staged-minibatch workgroups
     const int64_t P = a.n_params;
-    const int64_t stride = (int64_t)(gridDim.x - (a.mtc ? 1 : 0)) * blockDim.x;
+    const int64_t stride = (int64_t)(gridDim.x - adam_extra_count(a)) * blockDim.x;
     float step_size = 0.f, bc2s = 1.f;
     if (a.mode != 0) {   // this step's scalars, stored by the head kernel (adam_advance)
         step_size = a.ctrl->adam_step_size;
@@ -774,12 +787,9 @@ __global__ __launch_bounds__(256) void k_adam(AdamArgs a) {
 // bytes in flight of the scalar kernel (the (4,84,84) variant updates 29 M parameters).  The
 // same per-element arithmetic, the same fixed slab order.
 __global__ __launch_bounds__(256) void k_adam4(AdamArgs a) {
-    if (a.mtc && blockIdx.x == gridDim.x - 1) {
-        mt_cache_extend(a.mtc, a.mtc_blocks);
-        return;
-    }
+    if (adam_extra_wg(a)) return;   // the sampler-cache / staged-minibatch workgroups
     const int64_t P = a.n_params, P4 = (P + 3) >> 2;   // e0 is a multiple of 4 (launch_adam)
-    const int64_t stride = (int64_t)(gridDim.x - (a.mtc ? 1 : 0)) * blockDim.x;
+    const int64_t stride = (int64_t)(gridDim.x - adam_extra_count(a)) * blockDim.x;
     float step_size = 0.f, bc2s = 1.f;
     if (a.mode != 0) {
         step_size = a.ctrl->adam_step_size;
@@ -1249,6 +1259,7 @@ int launch_adam(const AdamArgs& a, hipStream_t s) {
     if (blocks > 2048) blocks = 2048;
     if (blocks < 1) blocks = 1;
     if (a.mtc) blocks++;   // + the sampler-cache workgroup
+    if (a.pf_nidx > 0) blocks++;   // + the staged-minibatch copy
     if (vec) hipLaunchKernelGGL(k_adam4, dim3(blocks), dim3(256), 0, s, a);
     else hipLaunchKernelGGL(k_adam, dim3(blocks), dim3(256), 0, s, a);
     DQNX_HIP_CHECK(hipGetLastError());

@@ -166,6 +166,14 @@ struct AdamArgs {
         float* chain;      // chain-blocked online W_l (l >= 1) or null
     } blk[3];
     int blk_bf16;
+    // in-launch prefetch: the minibatch the forward drew into the staging slot replaces this
+    // step's (one more workgroup; pf_nidx = 0: none)
+    const int32_t* pf_idx_src;
+    int32_t* pf_idx_dst;
+    int pf_nidx;
+    const int32_t* pf_phys_src;
+    int32_t* pf_phys_dst;
+    int pf_nphys;
 };
 
 // Full-K weight gradients of every layer + Adam (+ soft update) in one launch.
@@ -418,20 +426,25 @@ struct FusedFwdArgs {
     int64_t* stamps;             // diagnostic builds (-DDQNX_STAMPS): slots 24..39
     // in-launch prefetch (DQNX_STEP_PREFETCH, uniform replay): one more workgroup (the last)
     // draws the NEXT step's minibatch into the staging slot with the multi-pass sampler body, on
-    // a CU the row tiles leave idle (samp_hs = its LDS hash slots; 0 = no sampler workgroup)
-    int samp_hs;
+    // a CU the row tiles leave idle (samp_shape: its LDS shape, fwd_sample_*; 0 = no sampler workgroup)
+    int samp_shape;
     SampleArgs samp;
 };
-// The forward's sampler workgroup (512 threads): k <= 2048 passes of 3 MT blocks into a 4096-slot
-// table (40 KB of LDS, no more than the forward's own tiles); k <= FWD_SAMPLE_MAX_K one pass of 9
-// blocks into 16384 slots (150 KB: one workgroup per CU, as the forward runs at the shard sizes
-// that use it), so k = 4096 takes one pass instead of three
+// The forward's sampler workgroup (512 threads), three LDS shapes (FusedFwdArgs::samp_shape):
+//   1: k <= 2048, passes of 3 MT blocks into a 4096-slot table (40 KB, no more than the forward's
+//      own tiles);
+//   2: k <= FWD_SAMPLE_MAX_K, passes of 3 blocks into 8192 slots (72 KB: two forward workgroups per
+//      CU still fit, for grids larger than the chip);
+//   3: k <= FWD_SAMPLE_MAX_K, ONE pass of 9 blocks into 16384 slots (150 KB: one workgroup per CU,
+//      only when the forward's grid leaves a CU idle), so k = 4096 takes one pass instead of three
 constexpr int FWD_SAMPLE_MAX_K = 4608;
-__host__ __device__ constexpr int fwd_sample_ahead(int k) { return k <= 2048 ? 2 : 8; }
-__host__ __device__ constexpr int fwd_sample_hs(int k) { return k <= 2048 ? 4096 : 16384; }
+__host__ __device__ constexpr int fwd_sample_ahead(int shape) { return shape == 3 ? 8 : 2; }
+__host__ __device__ constexpr int fwd_sample_hs(int shape) { return shape == 1 ? 4096 : shape == 2 ? 8192 : 16384; }
 // LDS of that workgroup: the sampler's MT blocks / scan words, then the hash table (8-byte slots)
-__host__ __device__ constexpr int fwd_sample_tab_off(int k) { return (((fwd_sample_ahead(k) + 1) * 624 + 16) * 4 + 63) / 64 * 64; }
-__host__ __device__ constexpr int fwd_sample_lds_bytes(int k) { return fwd_sample_tab_off(k) + 8 * fwd_sample_hs(k); }
+__host__ __device__ constexpr int fwd_sample_tab_off(int shape) {
+    return (((fwd_sample_ahead(shape) + 1) * 624 + 16) * 4 + 63) / 64 * 64;
+}
+__host__ __device__ constexpr int fwd_sample_lds_bytes(int shape) { return fwd_sample_tab_off(shape) + 8 * fwd_sample_hs(shape); }
 struct HeadBwdArgs {
     int L, Bl, A, NH, F, head_kind, algo;
     int nsplit;                  // workgroups per 16-sample tile (split the last dZ's columns)

@@ -106,11 +106,16 @@ class GraphedDPStep:
     off: its kernels become nodes of this graph.
     """
 
-    def __init__(self, engine, soft_update: bool = True, group=None, bucketed: bool = False, prefetch: bool = False):
+    def __init__(self, engine, soft_update: bool = True, group=None, bucketed: bool = False, prefetch: bool = False,
+                 steps: int = 1):
         """prefetch=True: capture the prefetching step (each replay computes on the minibatch the
         previous one drew and draws the next; see dp_learn_step).  The first draw is made here,
         before the capture; run one dp_learn_step(prefetch=False) after the last replay to
-        consume the pending draw."""
+        consume the pending draw.
+        steps: DP steps captured back to back into the one graph (a replay = `steps` steps).
+        Every hipGraphLaunch leaves ~8.5 us before its first kernel on MI355X / ROCm 7.2; inside
+        a graph consecutive kernels start back to back."""
+        self.steps = int(steps)
         self.engine = engine
         engine.set_graphs(False)
         self.graph = torch.cuda.CUDAGraph()
@@ -119,10 +124,11 @@ class GraphedDPStep:
             engine.prefetch_prologue()
         torch.cuda.synchronize()
         with torch.cuda.graph(self.graph):
-            if bucketed:   # the side stream forks and joins inside the capture
-                dp_learn_step_bucketed(engine, soft_update=soft_update, group=group, comm_stream=self.comm)
-            else:
-                dp_learn_step(engine, soft_update=soft_update, group=group, prefetch=prefetch)
+            for _ in range(self.steps):
+                if bucketed:   # the side stream forks and joins inside the capture
+                    dp_learn_step_bucketed(engine, soft_update=soft_update, group=group, comm_stream=self.comm)
+                else:
+                    dp_learn_step(engine, soft_update=soft_update, group=group, prefetch=prefetch)
         torch.cuda.synchronize()
 
     def __call__(self):

@@ -203,3 +203,19 @@ def test_gpu_bf16_graph_and_eager_identical():
         torch.cuda.synchronize()
         outs.append(eng.params.clone())
     assert torch.equal(outs[0], outs[1])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("batch", [1024, 4096])
+def test_gpu_bf16_prefetch_bit_identical(batch):
+    """bf16 compute with the in-launch prefetch (the bf16 forward hosts the next step's sampler
+    workgroup; the slab plan's Adam pass copies the staged minibatch and the blocked bf16 copies
+    are rebuilt by a launch of their own): bitwise equal to sequential steps."""
+    _, _, e1 = make_bf16_pair("DuelingDoubleDQNAgent", 284, batch, 3 * batch, 3 * batch, 61, graphs=False)
+    _, _, e2 = make_bf16_pair("DuelingDoubleDQNAgent", 284, batch, 3 * batch, 3 * batch, 61, graphs=False)
+    for i in range(4):
+        e1.learn_step(soft_update=True)
+        e2.learn_step(soft_update=True, prefetch=i < 3)
+    torch.cuda.synchronize()
+    assert torch.equal(e1.params, e2.params) and torch.equal(e1.target_params, e2.target_params)
+    assert np.array_equal(e1.get_rng(0), e2.get_rng(0))

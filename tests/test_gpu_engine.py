@@ -409,7 +409,7 @@ def test_gpu_learn_golden(golden):
 
 
 @pytest.mark.parametrize("plan,batch,graphs", [("0", 256, True), ("fused", 256, True), ("fused", 1024, True),
-                                               ("fused", 1024, False), ("fused", 2048, True)])
+                                               ("fused", 1024, False), ("fused", 2048, True), ("fused", 4096, False)])
 def test_gpu_prefetch_mode_bit_identical(monkeypatch, plan, batch, graphs):
     """DQNX_STEP_PREFETCH draws step t+1's minibatch during step t: same results, bitwise.
     Per-layer plan: a side-stream pipeline.  Fused plan: step t's k_dw_adam16 launch hosts step
@@ -435,6 +435,7 @@ def test_gpu_prefetch_mode_bit_identical(monkeypatch, plan, batch, graphs):
 
 
 @pytest.mark.parametrize("algo,batch,count,n_fill", [
+    ("DuelingDoubleDQNAgent", 4096, 3, 9000),     # slab plan: Adam pass copies, relayout launches
     ("DuelingDoubleDQNAgent", 1024, 1, 4000),
     ("DuelingDoubleDQNAgent", 1024, 2, 4000),
     ("DuelingDoubleDQNAgent", 1024, 7, 4000),
@@ -468,10 +469,11 @@ def test_gpu_learn_steps_equal_single_steps(algo, batch, count, n_fill):
     e2.push(*O.synth_transitions(4, 284, 8, seed=3))
 
 
-@pytest.mark.parametrize("world,k", [(8, 4096), (4, 4096), (2, 2048)])
+@pytest.mark.parametrize("world,k", [(8, 4096), (4, 4096), (2, 4096), (2, 2048), (1, 4096)])
 def test_gpu_prefetch_dp_shard_step_bit_identical(world, k):
     """configs[3] shard step (rank 0 of `world`, global minibatch k): the next GLOBAL minibatch
-    drawn inside the forward launch (the 8192-slot sampler table at k = 4096) gives the same
+    drawn inside the forward launch (k = 4096: one-pass 16384-slot table while the grid leaves a CU
+    idle, 8192-slot passes at 2048 rows per rank; k = 2048: 4096 slots) gives the same
     gradients and weights as the sampler launch, bitwise."""
     E = _engine_mod()
     ospec = O.mlp_spec(284, 8, "dueling")

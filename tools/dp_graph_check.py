@@ -82,12 +82,27 @@ for _ in range(N - 1):
 torch.cuda.synchronize()
 pf_ms = (time.perf_counter() - t0) / (N - 1) * 1e3
 dp_learn_step(d)   # consumes the pending draw: N + 3 steps in all, like the others
+# ... and 4 prefetching steps per graph replay
+e = make()
+for _ in range(2):
+    dp_learn_step(e, prefetch=True)
+g4 = GraphedDPStep(e, prefetch=True, steps=4)
+torch.cuda.synchronize()
+t0 = time.perf_counter()
+for _ in range(N // 4):
+    g4()
+torch.cuda.synchronize()
+pf4_ms = (time.perf_counter() - t0) / N * 1e3
+dp_learn_step(e)   # 2 + N + 1 steps
+torch.cuda.synchronize()
 torch.cuda.synchronize()
 same = torch.equal(a.params, b.params) and torch.equal(a.target_params, b.target_params)
 same_single = torch.equal(a.params, c.params)
 same_pf = torch.equal(a.params, d.params) and torch.equal(a.target_params, d.target_params)
+same_pf4 = torch.equal(a.params, e.params) and torch.equal(a.target_params, e.target_params)
 print(f"{algo} B={B}: eager dp step {eager_ms * 1e3:.1f} us, graphed dp step {graph_ms * 1e3:.1f} us, "
-      f"graphed prefetching dp step {pf_ms * 1e3:.1f} us, single-GPU learn step {single_ms * 1e3:.1f} us; "
-      f"graphed == eager: {same}; dp == single: {same_single}; prefetch == eager: {same_pf}")
+      f"graphed prefetching dp step {pf_ms * 1e3:.1f} us (4 per replay: {pf4_ms * 1e3:.1f} us), single-GPU learn step "
+      f"{single_ms * 1e3:.1f} us; graphed == eager: {same}; dp == single: {same_single}; prefetch == eager: "
+      f"{same_pf and same_pf4}")
 dist.destroy_process_group()
-assert same and same_single and same_pf
+assert same and same_single and same_pf and same_pf4
