@@ -449,7 +449,8 @@ def roofline_of(args, kern, batch_tag):
     pmc_path = os.path.join(REPO, "profiles", f"pmc_traffic_{args.net}_b{batch_tag}{tag}.json")
     if os.path.exists(pmc_path):
         try:
-            traffic = json.load(open(pmc_path)).get(nm, {}).get("hbm_bytes_per_launch")
+            pmc = json.load(open(pmc_path))   # keyed by kernel ("mlp_fwd+sample" is the k_mlp_fwd launch)
+            traffic = pmc.get(nm, pmc.get(nm.split("+")[0], {})).get("hbm_bytes_per_launch")
         except Exception:
             traffic = None
     sec = us * 1e-6
