@@ -867,6 +867,8 @@ void build_fused_steps(dqnx_engine* e, int flags, int32_t* idx, int32_t* phys, s
             fa.wblk[1][l] = at<float>(e, e->ws_wblk[1][l]);
         }
         fa.stamps = at<int64_t>(e, e->ws_stamps);
+        fa.adam_ctrl = ctrl;   // (the head kernel below gets no ctrl: the forward stores the scalars)
+        fa.ab = adam_bias_args(e);
         if (sample_next) {   // + the next step's minibatch into the staging slot (in-launch prefetch)
             // the one-pass shape only when the row tiles leave a CU idle (its LDS allows one
             // workgroup per CU); else the 3-block passes, whose LDS keeps two per CU
@@ -954,7 +956,7 @@ void build_fused_steps(dqnx_engine* e, int flags, int32_t* idx, int32_t* phys, s
         ha.td = at<float>(e, e->off[DQNX_BUF_TD]);
         ha.dhead = at<float>(e, e->ws_dhead);
         ha.loss_partial = at<float>(e, e->ws_loss_part);
-        ha.ctrl = ctrl;
+        ha.ctrl = nullptr;   // the forward launch stores the step's Adam scalars
         for (int l = 1; l < L; l++) ha.wblkT[l] = at<float>(e, e->ws_wblkT[l]);
         ha.ab = adam_bias_args(e);
         ha.stamps = at<int64_t>(e, e->ws_stamps);

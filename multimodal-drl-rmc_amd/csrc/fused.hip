@@ -321,6 +321,9 @@ __global__ __launch_bounds__(FT) void k_mlp_fwd(FusedFwdArgs a) {
     const int coff = PH == 1 ? part * (a.out[0] / nsp) : 0;   // layer-1 columns of this part
 
     DQNX_STAMP(a.stamps, 24);
+    // the step's Adam scalars for the update launch: a dependent ctrl -> table chain on the last
+    // thread of one workgroup, hidden under that workgroup's gather
+    if (PH != 2 && a.adam_ctrl && T0 == a.tiles * a.nstreams * nsp - 1 && tid == FT - 1) adam_advance(a.adam_ctrl, a.ab);
     float4 wb[FNB][FPF][2];
     WStream ws;
     WaveCols c = wave_cols(PH == 1 ? a.out[0] / nsp : a.out[LB]);

@@ -429,6 +429,10 @@ struct FusedFwdArgs {
     // a CU the row tiles leave idle (samp_shape: its LDS shape, fwd_sample_*; 0 = no sampler workgroup)
     int samp_shape;
     SampleArgs samp;
+    // this step's Adam scalars (adam_advance), stored by one otherwise idle thread while its
+    // workgroup gathers, off the head kernel's critical path (null: the head kernel stores them)
+    dqnx_ctrl* adam_ctrl;
+    AdamBias ab;
 };
 // The forward's sampler workgroup (512 threads), three LDS shapes (FusedFwdArgs::samp_shape):
 //   1: k <= 2048, passes of 3 MT blocks into a 4096-slot table (40 KB, no more than the forward's
