@@ -893,10 +893,11 @@ __device__ __forceinline__ int64_t dw16_index(const DwAdam16Layer& d, int row, i
                                   : (int64_t)head_b_off(d.head_kind, row, d.in, d.A));
 }
 
-template <int DW16_NW, int U>   // waves per tile; k-steps (4 rows each) per register set, two sets in flight
+// R: 16-row blocks of W per workgroup (a tile is 16 R x 16; every X element loaded feeds R MFMAs)
+template <int DW16_NW, int U, int R>   // waves per tile; k-steps (4 rows each) per register set, two sets in flight
 __global__ __launch_bounds__(64 * DW16_NW) void k_dw_adam16(DwAdam16Args a) {
-    __shared__ floatx4 red[DW16_NW][64];
-    __shared__ float redb[DW16_NW][64];
+    __shared__ floatx4 red[DW16_NW][R][64];
+    __shared__ float redb[DW16_NW][R][64];
     const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int i = lane & 15, g = lane >> 4;
     if ((int)blockIdx.x >= a.tiles) {   // extra workgroups: sampler cache, then the staged-minibatch copy
@@ -921,12 +922,12 @@ __global__ __launch_bounds__(64 * DW16_NW) void k_dw_adam16(DwAdam16Args a) {
     const DwAdam16Layer d = a.L[li];
     const int t = T - d.t0;
     const int ob = t / d.ti, ib = t - ob * d.ti;
-    const int o0 = ob * 16, i0 = ib * 16;
+    const int o0 = ob * 16 * R, i0 = ib * 16;
 
-    // (0) this thread's parameters: slot q = tid + j NT of the tile's 256 weights (q < 256) and
-    //     16 biases (q = 256 + row, tiles with ib == 0), with their optimizer state, fetched
+    // (0) this thread's parameters: slot q = tid + j NT of the tile's 256 R weights (q < 256 R) and
+    //     16 R biases (q = 256 R + row, tiles with ib == 0), with their optimizer state, fetched
     //     before the K loop so the latency hides under it
-    constexpr int NT = 64 * DW16_NW, NS = (272 + NT - 1) / NT;
+    constexpr int NW_ = 256 * R, NT = 64 * DW16_NW, NS = (NW_ + 16 * R + NT - 1) / NT;
     int row[NS], col[NS];
     bool own[NS];
     int64_t e[NS];
@@ -934,14 +935,14 @@ __global__ __launch_bounds__(64 * DW16_NW) void k_dw_adam16(DwAdam16Args a) {
 #pragma unroll
     for (int j = 0; j < NS; j++) {
         const int q = tid + j * NT;
-        if (q < 256) {
+        if (q < NW_) {
             row[j] = o0 + (q >> 4);
             col[j] = i0 + (q & 15);
             own[j] = row[j] < d.out && col[j] < d.in;
         } else {
-            row[j] = o0 + q - 256;
+            row[j] = o0 + q - NW_;
             col[j] = d.in;
-            own[j] = ib == 0 && q < 272 && row[j] < d.out;
+            own[j] = ib == 0 && q < NW_ + 16 * R && row[j] < d.out;
         }
         e[j] = own[j] ? dw16_index(d, row[j], col[j]) : 0;
         p[j] = m[j] = v[j] = tg[j] = 0.f;
@@ -967,27 +968,39 @@ __global__ __launch_bounds__(64 * DW16_NW) void k_dw_adam16(DwAdam16Args a) {
     const int iters = s0 < nsteps ? spw / (2 * U) : 0;
     const __amdgpu_buffer_rsrc_t zr = wave_rsrc(d.dZ, (uint32_t)a.Bl * d.ldz * 4u);
     const __amdgpu_buffer_rsrc_t xr = wave_rsrc(d.X, (uint32_t)a.Bl * d.ldx * 4u);
-    uint32_t zo = (uint32_t)((4 * s0 + g) * d.ldz + min(o0 + i, d.out - 1)) * 4u;
+    uint32_t zo[R];
+#pragma unroll
+    for (int r = 0; r < R; r++) zo[r] = (uint32_t)((4 * s0 + g) * d.ldz + min(o0 + 16 * r + i, d.out - 1)) * 4u;
     uint32_t xo = (uint32_t)((4 * s0 + g) * d.ldx + min(i0 + i, d.in - 1)) * 4u;
     const uint32_t zs = 16u * d.ldz, xs = 16u * d.ldx;   // bytes per k-step (4 rows)
-    floatx4 acc = {0.f, 0.f, 0.f, 0.f};
-    float bs = 0.f;
-    float za[U], xa[U], zb[U], xb[U];
-    auto load = [&](float* z, float* x) {
+    floatx4 acc[R];
+    float bs[R];
+#pragma unroll
+    for (int r = 0; r < R; r++) {
+        acc[r] = floatx4{0.f, 0.f, 0.f, 0.f};
+        bs[r] = 0.f;
+    }
+    float za[R][U], xa[U], zb[R][U], xb[U];
+    auto load = [&](float (*z)[U], float* x) {
 #pragma unroll
         for (int u = 0; u < U; u++) {
-            z[u] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(zr, zo + u * zs, 0, 0));
+#pragma unroll
+            for (int r = 0; r < R; r++)
+                z[r][u] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(zr, zo[r] + u * zs, 0, 0));
             x[u] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xr, xo + u * xs, 0, 0));
         }
-        zo += U * zs;
+#pragma unroll
+        for (int r = 0; r < R; r++) zo[r] += U * zs;
         xo += U * xs;
     };
-    auto comp = [&](const float* z, const float* x) {
+    auto comp = [&](const float (*z)[U], const float* x) {
 #pragma unroll
-        for (int u = 0; u < U; u++) {
-            acc = mfma16x16x4(z[u], x[u], acc);
-            bs += z[u];
-        }
+        for (int u = 0; u < U; u++)
+#pragma unroll
+            for (int r = 0; r < R; r++) {
+                acc[r] = mfma16x16x4(z[r][u], x[u], acc[r]);
+                bs[r] += z[r][u];
+            }
     };
     if (iters > 0) {
         load(za, xa);
@@ -1007,8 +1020,11 @@ __global__ __launch_bounds__(64 * DW16_NW) void k_dw_adam16(DwAdam16Args a) {
         }
     }
     DQNX_STAMP(a.stamps, 58);
-    red[wid][lane] = acc;
-    redb[wid][lane] = bs;
+#pragma unroll
+    for (int r = 0; r < R; r++) {
+        red[wid][r][lane] = acc[r];
+        redb[wid][r][lane] = bs[r];
+    }
     __syncthreads();
 
     DQNX_STAMP(a.stamps, 59);
@@ -1018,17 +1034,17 @@ __global__ __launch_bounds__(64 * DW16_NW) void k_dw_adam16(DwAdam16Args a) {
         if (!own[j]) continue;
         const int q = tid + j * NT;
         float gsum;
-        if (q < 256) {
-            const float* rf = reinterpret_cast<const float*>(&red[0][0]);
-            const int rr = q >> 4, off = ((rr >> 2) * 16 + (q & 15)) * 4 + (rr & 3);
+        if (q < NW_) {   // row block r = q / 256 of the tile; the same order for every R
+            const float* rf = reinterpret_cast<const float*>(&red[0][0][0]) + (q >> 8) * 256;
+            const int qq = q & 255, rr = qq >> 4, off = ((rr >> 2) * 16 + (qq & 15)) * 4 + (rr & 3);
             gsum = rf[off];
 #pragma unroll
-            for (int w = 1; w < DW16_NW; w++) gsum += rf[w * 256 + off];
+            for (int w = 1; w < DW16_NW; w++) gsum += rf[w * 256 * R + off];
         } else {   // bias: lanes (i = row, g = 0..3) of every wave, wave-major
-            const int rr = q - 256;
-            gsum = redb[0][rr];
+            const int rb = (q - NW_) >> 4, rr = (q - NW_) & 15;
+            gsum = redb[0][rb][rr];
 #pragma unroll
-            for (int k = 1; k < 4 * DW16_NW; k++) gsum += redb[k >> 2][(k & 3) * 16 + rr];
+            for (int k = 1; k < 4 * DW16_NW; k++) gsum += redb[k >> 2][rb][(k & 3) * 16 + rr];
         }
         a.grads[e[j]] = gsum;
         if (!a.mode) continue;
@@ -1045,7 +1061,7 @@ __global__ __launch_bounds__(64 * DW16_NW) void k_dw_adam16(DwAdam16Args a) {
             tk = a.tau * pk + a.one_minus_tau * tg[j];
             a.target[e[j]] = tk;
         }
-        if (q < 256 && d.fwd_online) {   // the tile's blocks of the forward / dZ-chain copies
+        if (q < NW_ && d.fwd_online) {   // the tile's blocks of the forward / dZ-chain copies
             const int64_t pf = blk_pos(row[j], col[j], d.nch_fwd, false);
             d.fwd_online[pf] = pk;
             if (a.soft) d.fwd_target[pf] = tk;
@@ -1069,14 +1085,20 @@ __global__ __launch_bounds__(64 * DW16_NW) void k_dw_adam16(DwAdam16Args a) {
 int launch_dw_adam16(const DwAdam16Args& a, hipStream_t s) {
     static const int var = getenv("DQNX_DW16_VAR") ? atoi(getenv("DQNX_DW16_VAR")) : 0;
     const dim3 grid(a.tiles + (a.mtc ? 1 : 0) + (a.pf_nidx > 0 ? 1 : 0));
+    if (a.rows16 == 2) {
+        hipLaunchKernelGGL((k_dw_adam16<8, 8, 2>), grid, dim3(512), 0, s, a);
+        DQNX_HIP_CHECK(hipGetLastError());
+        return DQNX_OK;
+    }
+    if (a.rows16 != 1) return set_error(DQNX_EINVAL, "dw_adam16: %d row blocks per tile", a.rows16);
     switch (var) {   // measurement variants (waves per tile, k-steps per register set)
-        case 1: hipLaunchKernelGGL((k_dw_adam16<4, 8>), grid, dim3(256), 0, s, a); break;
-        case 2: hipLaunchKernelGGL((k_dw_adam16<16, 4>), grid, dim3(1024), 0, s, a); break;
-        case 3: hipLaunchKernelGGL((k_dw_adam16<8, 4>), grid, dim3(512), 0, s, a); break;
-        case 4: hipLaunchKernelGGL((k_dw_adam16<4, 16>), grid, dim3(256), 0, s, a); break;
-        case 5: hipLaunchKernelGGL((k_dw_adam16<8, 16>), grid, dim3(512), 0, s, a); break;
-        case 6: hipLaunchKernelGGL((k_dw_adam16<16, 8>), grid, dim3(1024), 0, s, a); break;
-        default: hipLaunchKernelGGL((k_dw_adam16<8, 8>), grid, dim3(512), 0, s, a); break;
+        case 1: hipLaunchKernelGGL((k_dw_adam16<4, 8, 1>), grid, dim3(256), 0, s, a); break;
+        case 2: hipLaunchKernelGGL((k_dw_adam16<16, 4, 1>), grid, dim3(1024), 0, s, a); break;
+        case 3: hipLaunchKernelGGL((k_dw_adam16<8, 4, 1>), grid, dim3(512), 0, s, a); break;
+        case 4: hipLaunchKernelGGL((k_dw_adam16<4, 16, 1>), grid, dim3(256), 0, s, a); break;
+        case 5: hipLaunchKernelGGL((k_dw_adam16<8, 16, 1>), grid, dim3(512), 0, s, a); break;
+        case 6: hipLaunchKernelGGL((k_dw_adam16<16, 8, 1>), grid, dim3(1024), 0, s, a); break;
+        default: hipLaunchKernelGGL((k_dw_adam16<8, 8, 1>), grid, dim3(512), 0, s, a); break;
     }
     DQNX_HIP_CHECK(hipGetLastError());
     return DQNX_OK;

@@ -262,7 +262,7 @@ struct DwAdam16Layer {
     int head_kind;         // -1 plain Linear, else dqnx_head_kind
     int A;
     int ti;                // 16-column blocks along `in`
-    int t0;                // first tile of this layer in the grid
+    int t0;                // first tile of this layer in the grid (tiles: ti x ceil(out / (16 rows16)))
     float* fwd_online;     // fwd-blocked copies (null: the layer has none)
     float* fwd_target;
     float* chain;          // chain-blocked online copy (null: none)
@@ -272,6 +272,7 @@ struct DwAdam16Args {
     DwAdam16Layer L[DQNX_MAX_DENSE + 1];
     int nl;
     int tiles;             // parameter tiles (+ 1 workgroup for the MT cache when mtc)
+    int rows16;            // 16-row blocks of W per tile (1: 16 x 16 tiles; 2: 32 x 16)
     int Bl;
     int mode;              // 0: gradients (+ loss) only, the DP all-reduce and Adam pass follow; 1: + Adam
     int soft;

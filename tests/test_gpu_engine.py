@@ -502,6 +502,29 @@ def test_gpu_prefetch_dp_shard_step_bit_identical(world, k):
     assert np.array_equal(e1.get_rng(0), e2.get_rng(0))
 
 
+@pytest.mark.parametrize("algo,batch", [("DuelingDoubleDQNAgent", 1024), ("DQNAgent", 200),
+                                        ("PerDuelingDoubleDQNAgent", 512)])
+def test_gpu_dw16_row_pair_tiles_bit_identical(monkeypatch, algo, batch):
+    """k_dw_adam16 on 32 x 16 tiles (the default: two 16-row blocks of W share each X load) sums
+    every gradient in the same order as the 16 x 16 tiles (DQNX_DW16_R=1): weights, target, Adam
+    state and gradients are bitwise equal."""
+    monkeypatch.setenv("DQNX_DW16_R", "1")
+    o1, e1 = make_pair(algo, 284, batch, 3000, 3000, 81)
+    for _ in range(3):
+        e1.learn_step(soft_update=True)   # (the plan is built at the first step)
+    torch.cuda.synchronize()
+    monkeypatch.delenv("DQNX_DW16_R")
+    o2, e2 = make_pair(algo, 284, batch, 3000, 3000, 81)
+    for _ in range(3):
+        e2.learn_step(soft_update=True)
+    torch.cuda.synchronize()
+    e1.check_device_error()
+    e2.check_device_error()
+    assert torch.equal(e1.grads, e2.grads)
+    assert torch.equal(e1.params, e2.params) and torch.equal(e1.target_params, e2.target_params)
+    assert torch.equal(e1.adam_m, e2.adam_m) and torch.equal(e1.adam_v, e2.adam_v)
+
+
 def test_gpu_prefetch_fused_weights_written_while_pending():
     """Fused plan, in-launch prefetch: host-side weight writes (load_params) while a minibatch is
     pending rebuild the blocked copies before the next step, and the step matches a sequential
