@@ -392,6 +392,7 @@ struct dqnx_engine {
     uint64_t total = 0;
     // workspace sub-regions (byte offsets from the arena base)
     uint64_t ws_phys = 0, ws_pool = 0, ws_xobs = 0, ws_head_part = 0, ws_loss_part = 0, ws_stage = 0;
+    uint64_t ws_npc = 0;   // numpy MT block cache (PER, fused plan)
     uint64_t ws_adam_tab = 0, ws_stamps = 0, ws_dhead = 0, ws_raw = 0, ws_trans = 0, ws_gtab = 0, ws_mtc = 0, ws_per_ticket = 0, ws_per_wl = 0, ws_per_wp = 0, ws_per_winit = 0, ws_per_last = 0, ws_per_wchg = 0;
     // fused plan: fragment-blocked weight copies [online fwd | target fwd | online chain] per layer
     uint64_t ws_wblk[2][FUSED_MAX_L] = {{0}}, ws_wblkT[FUSED_MAX_L] = {0};
@@ -515,6 +516,10 @@ int layout(dqnx_engine* e) {
     e->ws_adam_tab = sub((uint64_t)kAdamTable * 2 * 4);
     e->ws_stamps = sub(64 * 8);
     e->ws_per_ticket = sub(64);   // k_per_sample arrival counter (zero between launches); [16]: PER chunk epoch
+    // numpy MT block cache: only where the fused forward launch keeps it extended
+    if (c.algo == DQNX_ALGO_PER_DOUBLE && e->bwd_plan == 2 && e->fsplit <= 1 && !getenv("DQNX_NO_NP_CACHE") &&
+        np_cache_blocks(e->Bg) <= NPC_MAX_BLOCKS)
+        e->ws_npc = sub((uint64_t)np_cache_words() * 4);
     if (c.algo == DQNX_ALGO_PER_DOUBLE) {   // k_per_prep / k_per_update / k_per_prop hand-offs
         e->ws_per_wl = sub((uint64_t)PER_CHUNK * 4);
         e->ws_per_wp = sub((uint64_t)PER_CHUNK * 4);
@@ -591,6 +596,7 @@ PerSampleArgs per_sample_args(dqnx_engine* e, int32_t* idx, int32_t* phys) {
     pa.n_env = c.n_env;
     pa.stamps = at<int64_t>(e, e->ws_stamps);
     pa.ticket = at<int32_t>(e, e->ws_per_ticket);
+    pa.npc = e->ws_npc ? at<uint32_t>(e, e->ws_npc) : nullptr;   // extended by the fused forward
     return pa;
 }
 
@@ -868,6 +874,11 @@ void build_fused_steps(dqnx_engine* e, int flags, int32_t* idx, int32_t* phys, s
         }
         fa.stamps = at<int64_t>(e, e->ws_stamps);
         fa.adam_ctrl = ctrl;   // (the head kernel below gets no ctrl: the forward stores the scalars)
+        if (e->ws_npc && c.algo == DQNX_ALGO_PER_DOUBLE && !(e->fsplit > 1 && L >= 2 && fa.mr == 1)) {
+            fa.npc = at<uint32_t>(e, e->ws_npc);   // the next PER sample's MT blocks, twisted ahead
+            fa.np_state = ctrl->np_mt;
+            fa.npc_blocks = np_cache_blocks(e->Bg);
+        }
         fa.ab = adam_bias_args(e);
         if (sample_next) {   // + the next step's minibatch into the staging slot (in-launch prefetch)
             // the one-pass shape only when the row tiles leave a CU idle (its LDS allows one

@@ -288,6 +288,10 @@ __global__ __launch_bounds__(FT) void k_mlp_fwd(FusedFwdArgs a) {
     // LDS tile b: pointer arithmetic on `lds` keeps the LDS address space visible to the
     // compiler (ds_read, not flat loads that share the vmcnt counter with the W stream)
 #define FBUF(b) (lds + ((b) ? a.buf0 : 0))
+    if (a.npc && blockIdx.x == 0) {   // PER: the next sample's numpy MT blocks, twisted ahead on their own CU
+        np_cache_extend(a.npc, a.np_state, a.npc_blocks, reinterpret_cast<uint32_t*>(lds));
+        return;
+    }
     if (a.samp_shape && blockIdx.x == 0) {   // (dispatched first: it starts even when the grid exceeds the chip)
         // in-launch prefetch: the next step's random.sample (R:dqn/replay_memory.py:38-39) into the
         // staging slot.  It reads only the MT state and the ring's size / write pointer, which no
@@ -309,7 +313,7 @@ __global__ __launch_bounds__(FT) void k_mlp_fwd(FusedFwdArgs a) {
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int i = lane & 15, g = lane >> 4;
     const int nsp = PH == 1 ? a.csplit : 1;
-    const int T0 = xcd_remap((int)blockIdx.x - (a.samp_shape ? 1 : 0), a.tiles * a.nstreams * nsp);
+    const int T0 = xcd_remap((int)blockIdx.x - ((a.samp_shape || a.npc) ? 1 : 0), a.tiles * a.nstreams * nsp);
     const int part = T0 % nsp, T = T0 / nsp;   // the parts of one row tile are neighbours (one XCD)
     const int z = T / a.tiles, tile = T - z * a.tiles;
     const int s = a.stream_of[z];
@@ -971,10 +975,13 @@ int launch_fused_fwd(const FusedFwdArgs& a, int act, hipStream_t s) {
     if (a.samp_shape && (a.phase != 0 || a.samp_shape > 3 || a.samp.k > FWD_SAMPLE_MAX_K ||
                          (a.samp_shape == 1 && a.samp.k > 2048)))
         return set_error(DQNX_EUNSUPPORTED, "forward sampler workgroup: whole forward, k <= %d", FWD_SAMPLE_MAX_K);
-    const dim3 grid(a.tiles * a.nstreams * (a.phase == 1 ? a.csplit : 1) + (a.samp_shape ? 1 : 0)), block(FT);
+    if (a.npc && (a.samp_shape || a.phase == 2 || a.npc_blocks > NPC_MAX_BLOCKS))
+        return set_error(DQNX_EUNSUPPORTED, "forward MT-cache workgroup: not with the sampler workgroup / phase 2");
+    const dim3 grid(a.tiles * a.nstreams * (a.phase == 1 ? a.csplit : 1) + ((a.samp_shape || a.npc) ? 1 : 0)), block(FT);
     size_t shm = (size_t)(a.buf0 + a.buf1) * 4;
     if (shm < (size_t)DQNX_FUSED_LDS_MIN) shm = DQNX_FUSED_LDS_MIN;
     if (a.samp_shape && shm < (size_t)fwd_sample_lds_bytes(a.samp_shape)) shm = fwd_sample_lds_bytes(a.samp_shape);
+    if (a.npc && shm < (size_t)(2 * 624 + 2) * 4) shm = (2 * 624 + 2) * 4;
 #define FUSED_FWD_MR(ACTV, NLV, BFV, MRV, PHV)                                                       \
     do {                                                                                             \
         if (shm > 64 * 1024) allow_lds(k_mlp_fwd<ACTV, NLV, BFV, MRV, PHV>, 160 * 1024);             \

@@ -327,7 +327,16 @@ struct PerSampleArgs {
     int rl_blocks;
     int64_t* stamps;          // diagnostic builds (-DDQNX_STAMPS): slots 0..7
     int32_t* ticket;          // arrival counter of the sampling workgroups, zero between launches
+    uint32_t* npc;            // numpy MT block cache (np_cache_words; null: twist every block here)
 };
+// numpy MT block cache (PER, fused plan): [0] blocks held, [1] block the state moved to in the last
+// sample (the extension shifts the cache down by it), [64 + 624 b + o] block b (0 = the state block).
+// PER sampling consumes 2 Bg words; without the cache every sampling workgroup twists all of those
+// blocks in sequence (26 at Bg = 8192).  One extra workgroup of the forward launch (which runs
+// after the sample) twists the next sample's blocks ahead, off the critical path.
+constexpr int NPC_MAX_BLOCKS = 29;   // (624 + 2 PER_MAX_B - 1) / 624 + 1 at PER_MAX_B = 8192
+constexpr int64_t np_cache_words() { return 64 + (int64_t)NPC_MAX_BLOCKS * 624; }
+__host__ __device__ constexpr int np_cache_blocks(int Bg) { return (624 + 2 * Bg - 1) / 624 + 1; }
 
 // PER priority writes with SumTree.update's sequential semantics (R:dqn/utils/sum_tree.py:15-32):
 // mode 0 = update_batch_priorities (R:dqn/replay_memory.py:94-98),
@@ -434,6 +443,10 @@ struct FusedFwdArgs {
     // workgroup gathers, off the head kernel's critical path (null: the head kernel stores them)
     dqnx_ctrl* adam_ctrl;
     AdamBias ab;
+    // PER: block 0 (dispatched first) twists the numpy MT block cache ahead for the next sample
+    uint32_t* npc;
+    const uint32_t* np_state;   // ctrl->np_mt (the state the cache must start from)
+    int npc_blocks;
 };
 // The forward's sampler workgroup (512 threads), three LDS shapes (FusedFwdArgs::samp_shape):
 //   1: k <= 2048, passes of 3 MT blocks into a 4096-slot table (40 KB, no more than the forward's

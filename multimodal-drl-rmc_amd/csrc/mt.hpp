@@ -55,4 +55,47 @@ __device__ __forceinline__ void mt_twist_into(const uint32_t* old, uint32_t* nw)
     __syncthreads();
 }
 
+// numpy MT block cache (learn.hpp, PerSampleArgs::npc): drop the blocks the last sample moved
+// past, then twist forward until `target` blocks are held.  One workgroup (>= 227 threads);
+// `mb` = LDS [2][624] + 2 ints.  Runs in a launch after the sample (no other reader or writer).
+__device__ __forceinline__ void np_cache_extend(uint32_t* npc, const uint32_t* state, int target, uint32_t* mb) {
+    const int tid = threadIdx.x, nt = blockDim.x;
+    int* hdr = reinterpret_cast<int*>(mb + 2 * 624);
+    uint32_t* blocks = npc + 64;
+    if (tid == 0) {
+        hdr[0] = (int)npc[0];
+        hdr[1] = (int)npc[1];
+    }
+    __syncthreads();
+    int cnt = hdr[0];
+    const int sh = hdr[1];
+    if (cnt <= 0 || sh >= cnt) {   // nothing usable: start again from the state block
+        for (int j = tid; j < 624; j += nt) {
+            const uint32_t x = state[j];
+            mb[j] = x;
+            blocks[j] = x;
+        }
+        cnt = 1;
+    } else {
+        // block b <- block b + sh in increasing b: a block is read before any lower block is written
+        for (int b = 0; b < cnt - sh; b++)
+            for (int j = tid; j < 624; j += nt) blocks[(int64_t)b * 624 + j] = blocks[(int64_t)(b + sh) * 624 + j];
+        cnt -= sh;
+        __syncthreads();   // (this thread's stores above are visible to its own loads; others' by the barrier)
+        __threadfence_block();
+        for (int j = tid; j < 624; j += nt) mb[j] = blocks[(int64_t)(cnt - 1) * 624 + j];
+    }
+    __syncthreads();
+    int cur = 0;
+    for (int b = cnt; b < target; b++) {
+        mt_twist_into(mb + cur * 624, mb + (cur ^ 1) * 624);   // ends with a barrier
+        cur ^= 1;
+        for (int j = tid; j < 624; j += nt) blocks[(int64_t)b * 624 + j] = mb[cur * 624 + j];
+    }
+    if (tid == 0) {
+        npc[0] = (uint32_t)(target > cnt ? target : cnt);
+        npc[1] = 0u;
+    }
+}
+
 }  // namespace dqnx

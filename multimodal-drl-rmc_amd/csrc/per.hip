@@ -53,7 +53,7 @@ __global__ __launch_bounds__(PER_SNT) void k_per_sample(PerSampleArgs a) {
     __shared__ uint32_t words[2 * PER_SNT];
     __shared__ int64_t s_step;
     __shared__ uint32_t s_pos;
-    __shared__ int s_last;
+    __shared__ int s_last, s_ccnt;
     const int G = (a.Bg + PER_SNT - 1) / PER_SNT;
     if ((int)blockIdx.x >= G) {   // spare workgroups: blocked weight copies for the fused plan
         relayout_run(a.rl, blockIdx.x - G, gridDim.x - G);
@@ -69,6 +69,7 @@ __global__ __launch_bounds__(PER_SNT) void k_per_sample(PerSampleArgs a) {
     }
     const int64_t size = a.ctrl->ring_size;
     const int64_t min_idx = a.ctrl->per_min_idx;
+    bool cmis = false;
     {   // every load in flight before the first LDS write (a plain loop waits on each one)
         constexpr int NQ = (PER_STOP + 2 * PER_SNT - 1) / (2 * PER_SNT);
         double2 tv[NQ];
@@ -79,7 +80,21 @@ __global__ __launch_bounds__(PER_SNT) void k_per_sample(PerSampleArgs a) {
             tv[q] = j + 1 < len ? *reinterpret_cast<const double2*>(a.tree + j)
                                 : make_double2(j < len ? a.tree[j] : 0.0, 0.0);
         }
-        for (int j = tid; j < 624; j += PER_SNT) mtb[0][j] = a.ctrl->np_mt[j];
+        constexpr int NJ = (624 + PER_SNT - 1) / PER_SNT;
+        uint32_t sw[NJ], cwv[NJ];
+#pragma unroll
+        for (int u = 0; u < NJ; u++) {   // the state block, and the cache's block 0 to check it against
+            const int j = tid + u * PER_SNT < 624 ? tid + u * PER_SNT : 623;
+            sw[u] = a.ctrl->np_mt[j];
+            cwv[u] = a.npc ? a.npc[64 + j] : 0u;
+        }
+#pragma unroll
+        for (int u = 0; u < NJ; u++) {
+            if (tid + u * PER_SNT < 624) {
+                mtb[0][tid + u * PER_SNT] = sw[u];
+                cmis |= sw[u] != cwv[u];
+            }
+        }
 #pragma unroll
         for (int q = 0; q < NQ; q++) {
             const int j = 2 * (tid + q * PER_SNT);
@@ -90,9 +105,10 @@ __global__ __launch_bounds__(PER_SNT) void k_per_sample(PerSampleArgs a) {
     if (tid == 0) {
         s_pos = a.ctrl->np_mt[624];
         s_step = a.ctrl->agent_step;
+        s_ccnt = a.npc ? (int)a.npc[0] : 0;
     }
     const double prob_min = a.tree[min_idx] / total;
-    __syncthreads();   // the fields written back below are in LDS now
+    const bool cache_mismatch = __syncthreads_or(cmis ? 1 : 0) != 0;   // (the fields written back below are in LDS)
     if (tid == 0) {
         __threadfence();
         s_last = atomicAdd(a.ticket, 1) == G - 1;
@@ -104,20 +120,28 @@ __global__ __launch_bounds__(PER_SNT) void k_per_sample(PerSampleArgs a) {
     // the words of np.random.uniform calls i = 0..Bg-1: legacy double = 2 words each
     const int W = 2 * a.Bg;
     const int w0 = 2 * grp * PER_SNT, w1 = min(W, w0 + 2 * PER_SNT);
+    // the block holding the last word (0 = the state block) and the index just past it
+    const int bfin = ((int)pos + W - 1) / 624;
+    const uint32_t nxfin = (uint32_t)(((int)pos + W - 1) % 624 + 1);
+    const bool cached = a.npc && !cache_mismatch && s_ccnt >= bfin + 1;
     bool twisted = false;
     int cur = 0;
-    for (int done = 0; done < W;) {
-        if (pos >= 624) {
-            mt_twist_into(mtb[cur], mtb[cur ^ 1]);   // ends with a barrier
-            cur ^= 1;
-            pos = 0;
-            twisted = true;
+    if (cached) {   // word w of the call sits at cache position pos + w (blocks are contiguous)
+        for (int w = w0 + tid; w < w1; w += PER_SNT) words[w - w0] = mt_temper(a.npc[64 + pos + w]);
+    } else {
+        for (int done = 0; done < W;) {
+            if (pos >= 624) {
+                mt_twist_into(mtb[cur], mtb[cur ^ 1]);   // ends with a barrier
+                cur ^= 1;
+                pos = 0;
+                twisted = true;
+            }
+            const int take = min(624 - (int)pos, W - done);
+            const int lo = max(done, w0), hi = min(done + take, w1);
+            for (int w = lo + tid; w < hi; w += PER_SNT) words[w - w0] = mt_temper(mtb[cur][pos + (w - done)]);
+            done += take;
+            pos += (uint32_t)take;
         }
-        const int take = min(624 - (int)pos, W - done);
-        const int lo = max(done, w0), hi = min(done + take, w1);
-        for (int w = lo + tid; w < hi; w += PER_SNT) words[w - w0] = mt_temper(mtb[cur][pos + (w - done)]);
-        done += take;
-        pos += (uint32_t)take;
     }
 
     // beta = np.interp(step, [0, beta_inc], [beta_start, beta_end]) (numpy arr_interp, 2 points)
@@ -202,10 +226,17 @@ __global__ __launch_bounds__(PER_SNT) void k_per_sample(PerSampleArgs a) {
     }
     DQNX_STAMP(a.stamps, 3);
     if (s_last) {   // every other workgroup has read the old state: write the advanced one
-        if (twisted)
-            for (int j = tid; j < 624; j += PER_SNT) a.ctrl->np_mt[j] = mtb[cur][j];
+        if (cached) {   // cache block bfin; the next extension drops the blocks before it
+            if (bfin > 0)
+                for (int j = tid; j < 624; j += PER_SNT) a.ctrl->np_mt[j] = a.npc[64 + 624 * bfin + j];
+            if (tid == 0) a.npc[1] = (uint32_t)bfin;
+        } else {
+            if (twisted)
+                for (int j = tid; j < 624; j += PER_SNT) a.ctrl->np_mt[j] = mtb[cur][j];
+            if (tid == 0 && a.npc) a.npc[0] = 0u;   // the extension restarts from the new state
+        }
         if (tid == 0) {
-            a.ctrl->np_mt[624] = pos;
+            a.ctrl->np_mt[624] = cached ? nxfin : pos;
             a.ctrl->per_beta = beta;
             a.ctrl->agent_step = step + a.n_env;   // the caller's agent.step advances once per learn
             *a.ticket = 0;

@@ -282,3 +282,32 @@ def test_gpu_per_numpy121_learn_steps_match_oracle():
         assert np.array_equal(eng.batch_idx.cpu().numpy().astype(np.int64) + cap - 1, rec.positions), step
         assert abs(eng.loss() - rec.loss) <= 1e-5 * max(1.0, abs(rec.loss))
         assert_tree_equal(eng, oracle.replay.replay_buffer, exact=False)
+
+
+@pytest.mark.parametrize("batch,cap", [(256, 5000), (1024, 20000), (8192, 40000)])
+def test_gpu_per_np_cache_bit_identical(monkeypatch, batch, cap):
+    """The numpy MT block cache (the next PER sample's blocks twisted ahead by one workgroup of the
+    forward launch) gives the same leaves, IS weights, RNG state, tree and weights as twisting in
+    the sampler (DQNX_NO_NP_CACHE=1), across learn steps and after the host replaces the state."""
+    monkeypatch.setenv("DQNX_NO_NP_CACHE", "1")
+    _, e1 = make_per_pair(284, batch, cap, cap, 91)
+    monkeypatch.delenv("DQNX_NO_NP_CACHE")
+    _, e2 = make_per_pair(284, batch, cap, cap, 91)
+    for rnd in range(2):
+        for _ in range(4):
+            e1.learn_step(soft_update=True)
+            e2.learn_step(soft_update=True)
+        torch.cuda.synchronize()
+        e1.check_device_error()
+        e2.check_device_error()
+        assert torch.equal(e1.batch_idx, e2.batch_idx), rnd
+        assert torch.equal(e1.is_weights, e2.is_weights), rnd
+        assert np.array_equal(e1.get_rng(1), e2.get_rng(1)), rnd
+        assert torch.equal(e1.sumtree, e2.sumtree), rnd
+        assert torch.equal(e1.params, e2.params) and torch.equal(e1.target_params, e2.target_params), rnd
+        np.random.seed(500 + rnd)   # a new state from the host: the cache no longer matches
+        st = O.np_state_to_array()
+        if rnd == 0:
+            st[624] = 624            # ... and one whose next word needs a twist
+        e1.set_rng(1, st)
+        e2.set_rng(1, st)
