@@ -328,6 +328,7 @@ struct PerSampleArgs {
     int64_t* stamps;          // diagnostic builds (-DDQNX_STAMPS): slots 0..7
     int32_t* ticket;          // arrival counter of the sampling workgroups, zero between launches
     uint32_t* npc;            // numpy MT block cache (np_cache_words; null: twist every block here)
+    int spw;                  // samples (descents) per workgroup
 };
 // numpy MT block cache (PER, fused plan): [0] blocks held, [1] block the state moved to in the last
 // sample (the extension shifts the cache down by it), [64 + 624 b + o] block b (0 = the state block).

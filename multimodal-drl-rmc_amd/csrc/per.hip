@@ -54,7 +54,8 @@ __global__ __launch_bounds__(PER_SNT) void k_per_sample(PerSampleArgs a) {
     __shared__ int64_t s_step;
     __shared__ uint32_t s_pos;
     __shared__ int s_last, s_ccnt;
-    const int G = (a.Bg + PER_SNT - 1) / PER_SNT;
+    const int spw = a.spw;   // samples per workgroup (<= PER_SNT; all PER_SNT threads load and twist)
+    const int G = (a.Bg + spw - 1) / spw;
     if ((int)blockIdx.x >= G) {   // spare workgroups: blocked weight copies for the fused plan
         relayout_run(a.rl, blockIdx.x - G, gridDim.x - G);
         return;
@@ -119,7 +120,7 @@ __global__ __launch_bounds__(PER_SNT) void k_per_sample(PerSampleArgs a) {
 
     // the words of np.random.uniform calls i = 0..Bg-1: legacy double = 2 words each
     const int W = 2 * a.Bg;
-    const int w0 = 2 * grp * PER_SNT, w1 = min(W, w0 + 2 * PER_SNT);
+    const int w0 = 2 * grp * spw, w1 = min(W, w0 + 2 * spw);
     // the block holding the last word (0 = the state block) and the index just past it
     const int bfin = ((int)pos + W - 1) / 624;
     const uint32_t nxfin = (uint32_t)(((int)pos + W - 1) % 624 + 1);
@@ -158,8 +159,8 @@ __global__ __launch_bounds__(PER_SNT) void k_per_sample(PerSampleArgs a) {
     __syncthreads();
     DQNX_STAMP(a.stamps, 2);
 
-    const int i = grp * PER_SNT + tid;
-    if (i < a.Bg) {
+    const int i = grp * spw + tid;
+    if (tid < spw && i < a.Bg) {
         // legacy_double: (a >> 5, b >> 6) -> [0, 1); uniform = low + (high - low) * u
         const uint32_t wa = words[2 * tid] >> 5, wb = words[2 * tid + 1] >> 6;
         const double u = ((double)wa * 67108864.0 + (double)wb) / 9007199254740992.0;
@@ -702,7 +703,8 @@ int per_numpy121_init() {
 
 int launch_per_sample(const PerSampleArgs& a, hipStream_t s) {
     if (a.Bg < 1 || a.Bg > PER_MAX_B) return set_error(DQNX_EUNSUPPORTED, "PER batch %d outside [1, %d]", a.Bg, PER_MAX_B);
-    const int G = (a.Bg + PER_SNT - 1) / PER_SNT;
+    if (a.spw < 1 || a.spw > PER_SNT) return set_error(DQNX_EINVAL, "PER samples per workgroup %d", a.spw);
+    const int G = (a.Bg + a.spw - 1) / a.spw;
     hipLaunchKernelGGL(k_per_sample, dim3(G + a.rl_blocks), dim3(PER_SNT), 0, s, a);
     DQNX_HIP_CHECK(hipGetLastError());
     return DQNX_OK;
