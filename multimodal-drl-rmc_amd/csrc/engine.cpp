@@ -852,6 +852,12 @@ void build_fused_steps(dqnx_engine* e, int flags, int32_t* idx, int32_t* phys, s
         body_flops += 2.0 * np.dense[l].in * np.dense[l].out;
         wbytes += (e->fplan.bf16 ? 2.0 : 4.0) * np.dense[l].in * np.dense[l].out + 4.0 * np.dense[l].out;
     }
+    // row tile t of every stream (and the head's tile t) on XCD t % 8: the head kernel then reads
+    // the forward's outputs from its own XCD's L2 (16-row tiles, tiles % 8 == 0).  Measured at
+    // B=1024: head_bwd 7.2 -> 6.6 us, the forward unchanged; DQNX_XCD_ROWS=0 keeps xcd_remap's order
+    const int ftiles = (e->Bl + 15) / 16;
+    const bool xcd_rows = !(getenv("DQNX_XCD_ROWS") && atoi(getenv("DQNX_XCD_ROWS")) == 0) && e->fplan.mr == 1 &&
+                          ftiles % 8 == 0 && !(e->fsplit > 1 && L >= 2);
     // 2. forward (R:dqn/agent.py:209-214 / 172-173 streams, R:dqn/network.py:61-65, 90-96)
     {
         FusedFwdArgs fa = e->fplan;
@@ -882,6 +888,7 @@ void build_fused_steps(dqnx_engine* e, int flags, int32_t* idx, int32_t* phys, s
             fa.wblk[1][l] = at<float>(e, e->ws_wblk[1][l]);
         }
         fa.stamps = at<int64_t>(e, e->ws_stamps);
+        fa.xcd_rows = xcd_rows ? 1 : 0;
         fa.adam_ctrl = ctrl;   // (the head kernel below gets no ctrl: the forward stores the scalars)
         if (e->ws_npc && c.algo == DQNX_ALGO_PER_DOUBLE && !(e->fsplit > 1 && L >= 2 && fa.mr == 1)) {
             fa.npc = at<uint32_t>(e, e->ws_npc);   // the next PER sample's MT blocks, twisted ahead
@@ -977,6 +984,8 @@ void build_fused_steps(dqnx_engine* e, int flags, int32_t* idx, int32_t* phys, s
         ha.dhead = at<float>(e, e->ws_dhead);
         ha.loss_partial = at<float>(e, e->ws_loss_part);
         ha.ctrl = nullptr;   // the forward launch stores the step's Adam scalars
+        ha.xcd_rows = xcd_rows ? 1 : 0;
+        ha.xcd_shift = (sample_next || (e->ws_npc && c.algo == DQNX_ALGO_PER_DOUBLE)) ? 1 : 0;   // forward's block 0
         for (int l = 1; l < L; l++) ha.wblkT[l] = at<float>(e, e->ws_wblkT[l]);
         ha.ab = adam_bias_args(e);
         ha.stamps = at<int64_t>(e, e->ws_stamps);

@@ -313,9 +313,16 @@ __global__ __launch_bounds__(FT) void k_mlp_fwd(FusedFwdArgs a) {
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int i = lane & 15, g = lane >> 4;
     const int nsp = PH == 1 ? a.csplit : 1;
-    const int T0 = xcd_remap((int)blockIdx.x - ((a.samp_shape || a.npc) ? 1 : 0), a.tiles * a.nstreams * nsp);
-    const int part = T0 % nsp, T = T0 / nsp;   // the parts of one row tile are neighbours (one XCD)
-    const int z = T / a.tiles, tile = T - z * a.tiles;
+    const int bid = (int)blockIdx.x - ((a.samp_shape || a.npc) ? 1 : 0);
+    const int T0 = xcd_remap(bid, a.tiles * a.nstreams * nsp);
+    int part = T0 % nsp, T = T0 / nsp;   // the parts of one row tile are neighbours (one XCD)
+    int z = T / a.tiles, tile = T - z * a.tiles;
+    if (PH == 0 && a.xcd_rows) {   // row tile t of every stream on XCD t % 8 (tiles % 8 == 0)
+        const int tp = a.tiles >> 3, L = bid >> 3;
+        z = L / tp;
+        tile = (L - z * tp) * 8 + (bid & 7);
+        part = 0;
+    }
     const int s = a.stream_of[z];
     const int tgt = s == 2 ? 1 : 0;
     const int b0 = tile * RW, nb = min(RW, a.Bl - b0);
@@ -531,7 +538,12 @@ __global__ __launch_bounds__(FT) void k_head_bwd(HeadBwdArgs a) {
     const int i = lane & 15, g = lane >> 4;
     // nsplit workgroups per 16-sample tile: each recomputes the (cheap) head part and takes
     // 1/nsplit of the columns of the LAST dZ of the chain (dZ_1, the widest)
-    const int tile = blockIdx.x / a.nsplit, part = blockIdx.x - tile * a.nsplit;
+    int tile = blockIdx.x / a.nsplit, part = blockIdx.x - tile * a.nsplit;
+    if (a.xcd_rows) {   // tile t on the XCD whose L2 holds the forward's outputs of row tile t
+        const int xh = blockIdx.x & 7, k = blockIdx.x >> 3;
+        tile = (k / a.nsplit) * 8 + ((xh - a.xcd_shift) & 7);
+        part = k - (k / a.nsplit) * a.nsplit;
+    }
     const bool lead = part == 0;
     const int b0 = tile * 16, nb = min(16, a.Bl - b0);
     const int A = a.A, NH = a.NH, F = a.F;

@@ -442,6 +442,7 @@ struct FusedFwdArgs {
     SampleArgs samp;
     // this step's Adam scalars (adam_advance), stored by one otherwise idle thread while its
     // workgroup gathers, off the head kernel's critical path (null: the head kernel stores them)
+    int xcd_rows;                // row tile t of every stream on XCD t % 8 (the head kernel follows)
     dqnx_ctrl* adam_ctrl;
     AdamBias ab;
     // PER: block 0 (dispatched first) twists the numpy MT block cache ahead for the next sample
@@ -467,6 +468,8 @@ __host__ __device__ constexpr int fwd_sample_lds_bytes(int shape) { return fwd_s
 struct HeadBwdArgs {
     int L, Bl, A, NH, F, head_kind, algo;
     int nsplit;                  // workgroups per 16-sample tile (split the last dZ's columns)
+    int xcd_rows;                // tile t's workgroups on the XCD the forward ran row tile t on
+    int xcd_shift;               // ... whose workgroups the forward's extra block 0 shifted by one
     int bf16;                    // DQNX_COMPUTE_BF16: dZ chain on bf16 operands (LDS tiles + wblkT)
     int in[FUSED_MAX_L], out[FUSED_MAX_L];
     int64_t woff[FUSED_MAX_L], head_off;

@@ -525,6 +525,28 @@ def test_gpu_dw16_row_pair_tiles_bit_identical(monkeypatch, algo, batch):
     assert torch.equal(e1.adam_m, e2.adam_m) and torch.equal(e1.adam_v, e2.adam_v)
 
 
+@pytest.mark.parametrize("algo,batch,prefetch", [("DuelingDoubleDQNAgent", 1024, True),
+                                                 ("DuelingDoubleDQNAgent", 512, False),
+                                                 ("PerDuelingDoubleDQNAgent", 1024, False)])
+def test_gpu_xcd_row_mapping_bit_identical(monkeypatch, algo, batch, prefetch):
+    """The XCD-aligned row tiles (default: row tile t of every stream and the head's tile t on XCD
+    t % 8) only move workgroups: results are bitwise those of xcd_remap's order (DQNX_XCD_ROWS=0)."""
+    monkeypatch.setenv("DQNX_XCD_ROWS", "0")
+    o1, e1 = make_pair(algo, 284, batch, 3000, 3000, 83)
+    for i in range(3):
+        e1.learn_step(soft_update=True, prefetch=prefetch and i < 2)
+    torch.cuda.synchronize()
+    monkeypatch.delenv("DQNX_XCD_ROWS")
+    o2, e2 = make_pair(algo, 284, batch, 3000, 3000, 83)
+    for i in range(3):
+        e2.learn_step(soft_update=True, prefetch=prefetch and i < 2)
+    torch.cuda.synchronize()
+    e1.check_device_error()
+    e2.check_device_error()
+    assert torch.equal(e1.q, e2.q) and torch.equal(e1.td, e2.td)
+    assert torch.equal(e1.params, e2.params) and torch.equal(e1.target_params, e2.target_params)
+
+
 def test_gpu_prefetch_fused_weights_written_while_pending():
     """Fused plan, in-launch prefetch: host-side weight writes (load_params) while a minibatch is
     pending rebuild the blocked copies before the next step, and the step matches a sequential
