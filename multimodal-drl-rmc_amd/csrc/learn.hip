@@ -1086,7 +1086,11 @@ int launch_dw_adam16(const DwAdam16Args& a, hipStream_t s) {
     static const int var = getenv("DQNX_DW16_VAR") ? atoi(getenv("DQNX_DW16_VAR")) : 0;
     const dim3 grid(a.tiles + (a.mtc ? 1 : 0) + (a.pf_nidx > 0 ? 1 : 0));
     if (a.rows16 == 2) {
-        hipLaunchKernelGGL((k_dw_adam16<8, 8, 2>), grid, dim3(512), 0, s, a);
+        switch (var) {   // measurement variants (waves per tile, k-steps per register set)
+            case 7: hipLaunchKernelGGL((k_dw_adam16<16, 4, 2>), grid, dim3(1024), 0, s, a); break;
+            case 8: hipLaunchKernelGGL((k_dw_adam16<8, 4, 2>), grid, dim3(512), 0, s, a); break;
+            default: hipLaunchKernelGGL((k_dw_adam16<8, 8, 2>), grid, dim3(512), 0, s, a); break;
+        }
         DQNX_HIP_CHECK(hipGetLastError());
         return DQNX_OK;
     }
