@@ -677,14 +677,14 @@ __device__ __forceinline__ void blk_store(float* base, int64_t pos, float v, boo
     else base[pos] = v;
 }
 
-// The Adam launch's extra workgroups, after the element blocks: the sampler's MT block cache
-// (a.mtc), then the in-launch prefetch's copy of the staged minibatch over the compute slot
-// (a.pf_nidx > 0; every reader of the step's minibatch ran in earlier launches).
+// The Adam launch's extra workgroups, BEFORE the element blocks (dispatched first, so they overlap
+// the element pass instead of trailing it: at B=4096 the trailing copy cost ~4 us): the sampler's
+// MT block cache (a.mtc), then the in-launch prefetch's copy of the staged minibatch over the
+// compute slot (a.pf_nidx > 0; every reader of the step's minibatch ran in earlier launches).
 __device__ __forceinline__ int adam_extra_count(const AdamArgs& a) { return (a.mtc ? 1 : 0) + (a.pf_nidx > 0 ? 1 : 0); }
 __device__ __forceinline__ bool adam_extra_wg(const AdamArgs& a) {
-    const int first = (int)gridDim.x - adam_extra_count(a);
-    if ((int)blockIdx.x < first) return false;
-    if (a.mtc && (int)blockIdx.x == first) {
+    if ((int)blockIdx.x >= adam_extra_count(a)) return false;
+    if (a.mtc && blockIdx.x == 0) {
         mt_cache_extend(a.mtc, a.mtc_blocks);
     } else {
         for (int q = threadIdx.x; q < a.pf_nidx; q += blockDim.x) a.pf_idx_dst[q] = a.pf_idx_src[q];
@@ -695,6 +695,7 @@ __device__ __forceinline__ bool adam_extra_wg(const AdamArgs& a) {
 
 __global__ __launch_bounds__(256) void k_adam(AdamArgs a) {
     if (adam_extra_wg(a)) return;   // the sampler-cache / staged-minibatch workgroups
+    const int eb = (int)blockIdx.x - adam_extra_count(a);   // element block
     const int64_t P = a.n_params;
     const int64_t stride = (int64_t)(gridDim.x - adam_extra_count(a)) * blockDim.x;
     float step_size = 0.f, bc2s = 1.f;
@@ -702,7 +703,7 @@ __global__ __launch_bounds__(256) void k_adam(AdamArgs a) {
         step_size = a.ctrl->adam_step_size;
         bc2s = a.ctrl->adam_bc2_sqrt;
     }
-    for (int64_t e = a.e0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < P; e += stride) {
+    for (int64_t e = a.e0 + (int64_t)eb * blockDim.x + threadIdx.x; e < P; e += stride) {
         // every load of this element is issued before the first use (one round trip)
         float m = 0.f, v = 0.f, p = 0.f, tg = 0.f;
         if (a.mode != 0) {
@@ -768,7 +769,7 @@ __global__ __launch_bounds__(256) void k_adam(AdamArgs a) {
             if (L.chain) blk_store(L.chain, blk_pos(q, r, L.out / (bf ? 32 : 16), bf), p, bf);
         }
     }
-    if (a.mode != 2 && blockIdx.x == 0 && threadIdx.x < 64 && a.loss_partial) {   // one wave, fixed order
+    if (a.mode != 2 && eb == 0 && threadIdx.x < 64 && a.loss_partial) {   // one wave, fixed order
         float s = 0.f;
         for (int j = threadIdx.x; j < a.n_loss_partial; j += 64) s += a.loss_partial[j];
 #pragma unroll
@@ -779,7 +780,7 @@ __global__ __launch_bounds__(256) void k_adam(AdamArgs a) {
             a.ctrl->loss = loss;
         }
     }
-    if (a.mode == 2 && a.with_loss && blockIdx.x == 0 && threadIdx.x == 0) a.ctrl->loss = a.grads[P];
+    if (a.mode == 2 && a.with_loss && eb == 0 && threadIdx.x == 0) a.ctrl->loss = a.grads[P];
 }
 
 // k_adam on float4s: every segment offset / slab stride a multiple of 4 and no blocked copies
@@ -788,6 +789,7 @@ __global__ __launch_bounds__(256) void k_adam(AdamArgs a) {
 // same per-element arithmetic, the same fixed slab order.
 __global__ __launch_bounds__(256) void k_adam4(AdamArgs a) {
     if (adam_extra_wg(a)) return;   // the sampler-cache / staged-minibatch workgroups
+    const int eb = (int)blockIdx.x - adam_extra_count(a);   // element block
     const int64_t P = a.n_params, P4 = (P + 3) >> 2;   // e0 is a multiple of 4 (launch_adam)
     const int64_t stride = (int64_t)(gridDim.x - adam_extra_count(a)) * blockDim.x;
     float step_size = 0.f, bc2s = 1.f;
@@ -795,7 +797,7 @@ __global__ __launch_bounds__(256) void k_adam4(AdamArgs a) {
         step_size = a.ctrl->adam_step_size;
         bc2s = a.ctrl->adam_bc2_sqrt;
     }
-    for (int64_t e4 = (a.e0 >> 2) + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e4 < P4; e4 += stride) {
+    for (int64_t e4 = (a.e0 >> 2) + (int64_t)eb * blockDim.x + threadIdx.x; e4 < P4; e4 += stride) {
         const int64_t e = e4 << 2;
         const int nv = (int)min((int64_t)4, P - e);   // 4 except in the last vector
         float4 m = make_float4(0.f, 0.f, 0.f, 0.f), v = m, p = m, tg = m, g = m;
@@ -861,7 +863,7 @@ __global__ __launch_bounds__(256) void k_adam4(AdamArgs a) {
         st(a.p, p);
         if (a.soft) st(a.target, tg);
     }
-    if (a.mode != 2 && blockIdx.x == 0 && threadIdx.x < 64 && a.loss_partial) {   // one wave, fixed order
+    if (a.mode != 2 && eb == 0 && threadIdx.x < 64 && a.loss_partial) {   // one wave, fixed order
         float s = 0.f;
         for (int j = threadIdx.x; j < a.n_loss_partial; j += 64) s += a.loss_partial[j];
 #pragma unroll
@@ -872,7 +874,7 @@ __global__ __launch_bounds__(256) void k_adam4(AdamArgs a) {
             a.ctrl->loss = loss;
         }
     }
-    if (a.mode == 2 && a.with_loss && blockIdx.x == 0 && threadIdx.x == 0) a.ctrl->loss = a.grads[P];
+    if (a.mode == 2 && a.with_loss && eb == 0 && threadIdx.x == 0) a.ctrl->loss = a.grads[P];
 }
 
 // =====================================================================================
