@@ -701,9 +701,13 @@ static bool blk_kept(const dqnx_engine* e, int flags) {
     return adam_keeps_blk(e) || dw_adam16_on(e, flags);
 }
 
-void fill_blk_layers(dqnx_engine* e, AdamArgs& aa) {
+// force: this Adam pass writes the blocked copies although the engine does not keep them by
+// default (a prefetching step has no sampler launch whose spare workgroups would rebuild them)
+void fill_blk_layers(dqnx_engine* e, AdamArgs& aa, bool force = false) {
     aa.nblk = 0;
-    if (!adam_keeps_blk(e)) return;
+    if (!adam_keeps_blk(e) && !(force && e->bwd_plan == 2)) return;
+    for (const LayerPlan& lp : e->np.dense)
+        if ((int64_t)lp.out * lp.in >= ((int64_t)1 << 24)) return;
     const NetPlan& np = e->np;
     aa.blk_bf16 = e->fplan.bf16 ? 1 : 0;
     for (int l = 0; l < (int)np.dense.size() && l < 3; l++) {
@@ -1168,6 +1172,7 @@ void build_fused_steps(dqnx_engine* e, int flags, int32_t* idx, int32_t* phys, s
             aa.pf_nphys = e->Bl;
             aa.mtc = nullptr;   // the forward's sampler body draws from the MT state itself
             aa.mtc_blocks = 0;
+            fill_blk_layers(e, aa, true);   // ... and the next step has no sampler launch to rebuild them
             k.run = [=](hipStream_t s) { return launch_adam(aa, s); };
             ks.push_back(k);
             return;
@@ -1939,6 +1944,7 @@ int enqueue_range(const std::vector<KStep>& ks, int a, int b, hipStream_t s) {
 }
 
 int enqueue_apply(dqnx_engine* e, int flags, hipStream_t s) {
+    const bool keep_blk = (flags & 0x200) != 0;   // (a prefetched minibatch is pending: no sampler launch next)
     const dqnx_config& c = e->cfg;
     if (c.algo == DQNX_ALGO_PER_DOUBLE) {   // priorities from the all-gathered |delta| (DP)
         int rc = enqueue_per_update(e, at<int32_t>(e, e->off[DQNX_BUF_BATCH_IDX]), s);
@@ -1969,7 +1975,7 @@ int enqueue_apply(dqnx_engine* e, int flags, hipStream_t s) {
     aa.lrd = c.lr;
     aa.batch_global = e->Bg;
     aa.with_loss = 1;
-    fill_blk_layers(e, aa);
+    fill_blk_layers(e, aa, keep_blk);
     return launch_adam(aa, s);
 }
 
@@ -2556,7 +2562,9 @@ static int learn_step_inlaunch(dqnx_engine* e, int base, bool prefetch, hipStrea
     if (rc) return rc;
     // the slab plan's Adam pass (and a GRADS_ONLY step's later dqnx_apply_grads) leaves the blocked
     // copies behind: the next step rebuilds them first (with no sampler launch to host it)
-    if (!blk_kept(e, base)) e->wblk_dirty = true;
+    // (a prefetching step's update keeps them: k_dw_adam16 always, the slab plan's Adam pass when it
+    // draws ahead; a GRADS_ONLY step's dqnx_apply_grads decides for itself)
+    if (!blk_kept(e, base) && !(prefetch && !(base & DQNX_STEP_GRADS_ONLY))) e->wblk_dirty = true;
     if (!prefetch) {   // consumed the pending minibatch; nothing drawn ahead
         e->pf_valid = false;
         e->pf_inlaunch = false;
@@ -2658,7 +2666,7 @@ int dqnx_learn_steps(dqnx_engine* e, int32_t flags, int32_t count, void* stream)
         const bool kept = blk_kept(e, base);
         for (int i = 0; i < count && !r; i++) {
             const bool last = i == count - 1;
-            if (i > 0 && !kept) r = enqueue_relayout(e, cs);   // the previous step's Adam left them behind
+            (void)kept;   // every step before the last draws ahead, and its update keeps the copies
             const std::vector<KStep>& ks = steps_for(e, base | (last ? 0 : KEY_SAMPLE_NEXT));
             if (!r) r = enqueue_range(ks, last ? 1 : 0, (int)ks.size(), cs);
         }
@@ -2808,9 +2816,16 @@ int dqnx_event_elapsed(void* start, void* stop, float* ms) {
 int dqnx_apply_grads(dqnx_engine* e, int32_t flags, void* stream) {
     int rc = check_bound(e);
     if (rc) return rc;
-    const int key = 0x100 | (flags & DQNX_STEP_SOFT_UPDATE);
-    if (!adam_keeps_blk(e)) e->wblk_dirty = true;   // this Adam pass leaves the blocked copies behind
-    return run_graphed(e, key, (hipStream_t)stream, [&](hipStream_t s) { return enqueue_apply(e, key, s); });
+    // with an in-launch prefetch pending the next step has no sampler launch: this pass writes the
+    // fused plan's blocked copies itself (measured 2.4-2.6 us per DP shard step faster than a
+    // relayout launch); otherwise the next sampler launch rebuilds them for free
+    const bool keep = e->bwd_plan == 2 && e->pf_valid && e->pf_inlaunch;
+    const int key = 0x100 | (flags & DQNX_STEP_SOFT_UPDATE) | (keep ? 0x200 : 0);
+    const int rc2 = run_graphed(e, key, (hipStream_t)stream, [&](hipStream_t s) { return enqueue_apply(e, key, s); });
+    if (rc2) return rc2;
+    if (keep) e->wblk_dirty = false;                          // every blocked copy rewritten from the new weights
+    else if (!adam_keeps_blk(e)) e->wblk_dirty = true;        // this Adam pass leaves the blocked copies behind
+    return DQNX_OK;
 }
 
 int dqnx_dp_bucket_count(dqnx_engine* e, int32_t* n) {
