@@ -404,6 +404,8 @@ class LearnEngine:
     def learn_step_bucket(self, bucket: int):
         """The part of a GRADS_ONLY learn step that completes `bucket`'s gradient."""
         C.check(self.L.dqnx_learn_step_bucket(self.h, 0, int(bucket), self.stream()), "learn_step_bucket")
+        if bucket == 0 and self.cfg.algo == C.DQNX_ALGO_PER_DOUBLE:   # bucket 0 samples: step += n_env
+            self.agent_step += self.cfg.n_env
 
     def apply_grads_bucket(self, bucket: int, soft_update=False):
         """Adam (+ soft update) of `bucket`'s parameters from `grads` (bucket 0: + the PER tree update)."""

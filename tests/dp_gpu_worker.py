@@ -19,6 +19,7 @@ from oracle import ref as O  # noqa: E402  (test data + initial weights only)
 CASES = {
     "small": (284, 64, 1000, 700, 9),
     "c3": (284, 4096, 60000, 60000, 29),      # configs[3]: global minibatch 4096
+    "c5": (284, 8192, 40000, 40000, 31),      # configs[4]: PER + bf16, global minibatch 8192
 }
 # two-stream conv nets (micro grid, global batch, capacity, fill, seed): the bucketed DP step
 HYB_CASES = {
@@ -54,16 +55,22 @@ def main():
     eng.push(*O.synth_transitions(fill, ospec.obs_dim, 8, seed=seed + 100))
     eng.set_rng(0, O.py_state_to_array(__import__("random").Random(seed + (rank if local else 0)).getstate()))
     eng.set_rng(1, O.np_state_to_array(np.random.RandomState(seed).get_state()))
-    losses, pos = [], []
+    losses, pos, trees, absd, maxmin = [], [], [], [], []
     for _ in range(3):
         (dp_learn_step_bucketed if bucketed else dp_learn_step)(eng, soft_update=True)
         torch.cuda.synchronize()
         eng.check_device_error()
         losses.append(float(eng.grads[-1].item()))
         pos.append(eng.batch_idx.cpu().numpy().copy())
+        if eng.per_abs_td.numel():   # per step: the all-gathered |delta| and the tree it produced
+            c = eng.ctrl()
+            trees.append(eng.sumtree.cpu().numpy())
+            absd.append(eng.per_abs_td.cpu().numpy())
+            maxmin.append((int(c.per_max_idx), int(c.per_min_idx)))
+    extra = dict(step_trees=np.stack(trees), step_absd=np.stack(absd), step_maxmin=np.array(maxmin)) if trees else {}
     np.savez(os.path.join(out, f"rank{rank}.npz"), losses=np.array(losses), positions=np.stack(pos),
              params=eng.params.cpu().numpy(), target=eng.target_params.cpu().numpy(),
-             tree=eng.sumtree.cpu().numpy())
+             tree=eng.sumtree.cpu().numpy(), **extra)
     dist.destroy_process_group()
 
 

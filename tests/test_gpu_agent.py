@@ -15,38 +15,50 @@ from refnets import agent_kwargs, hybrid_network_config, mse_network_config, rms
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("algo,obs_dim,batch,buffer,n_fill,net", [
-    ("DQNAgent", 14, 32, 500, 300, "mlp"),
-    ("DuelingDoubleDQNAgent", 284, 64, 1000, 700, "mlp"),
-    ("PerDuelingDoubleDQNAgent", 284, 64, 1000, 700, "mlp"),
+@pytest.mark.parametrize("algo,obs_dim,batch,buffer,n_fill,net,n_env", [
+    ("DQNAgent", 14, 32, 500, 300, "mlp", 1),
+    ("DuelingDoubleDQNAgent", 284, 64, 1000, 700, "mlp", 1),
+    ("PerDuelingDoubleDQNAgent", 284, 64, 1000, 700, "mlp", 1),
     # the reference's HEAD configuration: DuelingDoubleDQNAgent on env/dqn_config.network_config
     # (TwoStreamHybridNetwork), as bin/train.sh launches it (R:train.py:24, R:bin/train.sh:5)
-    ("DuelingDoubleDQNAgent", 284, 64, 1000, 700, "hybrid"),
-    ("PerDuelingDoubleDQNAgent", 284, 32, 500, 300, "hybrid"),
+    ("DuelingDoubleDQNAgent", 284, 64, 1000, 700, "hybrid", 1),
+    ("PerDuelingDoubleDQNAgent", 284, 32, 500, 300, "hybrid", 1),
+    # -n_env 2 (R:train.py:120): two rows per store_transitions / choose_actions, soft update with
+    # tau*n_env (R:dqn/agent.py:105-110), PER beta at step*n_env (R:dqn/agent.py:247); a ring
+    # that wraps during the loop (uniform) and a buffer filled to capacity (PER)
+    ("DuelingDoubleDQNAgent", 284, 64, 706, 700, "mlp", 2),
+    ("PerDuelingDoubleDQNAgent", 284, 64, 700, 700, "mlp", 2),
+    ("DQNAgent", 14, 32, 500, 300, "mlp", 3),
+    ("PerDuelingDoubleDQNAgent", 284, 32, 500, 300, "hybrid", 2),
 ])
-def test_gpu_agent_train_loop_matches_oracle(tmp_path, algo, obs_dim, batch, buffer, n_fill, net):
+def test_gpu_agent_train_loop_matches_oracle(tmp_path, algo, obs_dim, batch, buffer, n_fill, net, n_env):
     seed = 17
     torch.manual_seed(seed)
     over = {"nn_conf_func": hybrid_network_config} if net == "hybrid" else {}
-    agent = getattr(Agents, algo)(**agent_kwargs(algo, obs_dim, batch, buffer, tmp_path, **over))
+    agent = getattr(Agents, algo)(**agent_kwargs(algo, obs_dim, batch, buffer, tmp_path, n_env=n_env, **over))
     head = O.algo_spec_head(algo)
     spec = O.hybrid_spec(8, head) if net == "hybrid" else O.mlp_spec(obs_dim, 8, head)
     init = O.reference_init(spec, seed)
     for k, v in agent.online_network.state_dict().items():
         assert torch.equal(v.cpu(), init[k]), k
-    oracle = O.OracleLearner(spec, algo, batch, buffer, seed=seed, params=init, per_pow="cr")
+    oracle = O.OracleLearner(spec, algo, batch, buffer, seed=seed, params=init, per_pow="cr", n_env=n_env)
 
-    obs, act, rew, done, nobs = O.synth_transitions(n_fill + 8, obs_dim, 8, seed=seed)
-    for i in range(n_fill):   # init_replay_memory_buffer: one env step (n_env = 1) at a time
-        agent.store_transitions(obs[i:i + 1], [int(act[i])], [float(rew[i])], [bool(done[i])], nobs[i:i + 1], None)
-    O.fill_replay(oracle, obs[:n_fill], act[:n_fill], rew[:n_fill], done[:n_fill], nobs[:n_fill])
+    steps = 4
+    obs, act, rew, done, nobs = O.synth_transitions(n_fill + steps * n_env, obs_dim, 8, seed=seed)
+    for i in range(0, n_fill, n_env):   # init_replay_memory_buffer: n_env rows per env step (R:train.py:63-81)
+        j = min(i + n_env, n_fill)
+        rows = (obs[i:j], [int(a) for a in act[i:j]], [float(r) for r in rew[i:j]], [bool(d) for d in done[i:j]],
+                nobs[i:j])
+        agent.store_transitions(*rows, None)
+        oracle.store_transitions(*rows)
 
     random.seed(seed)
     np.random.seed(seed)
-    for t in range(4):
+    for t in range(steps):
         agent.step = t
         agent.epsilon_start = 0.5          # mix greedy and random actions
-        x = obs[n_fill + t:n_fill + t + 1]
+        lo, hi = n_fill + t * n_env, n_fill + (t + 1) * n_env
+        x = obs[lo:hi]
         s0 = random.getstate()
         actions = agent.choose_actions(x)
         s1 = random.getstate()
@@ -57,6 +69,10 @@ def test_gpu_agent_train_loop_matches_oracle(tmp_path, algo, obs_dim, batch, buf
             if random.random() <= agent.epsilon():
                 ref_actions[i] = random.randint(0, 7)
         assert random.getstate() == s1 and actions == ref_actions
+        if n_env > 1:   # the env step's n_env transitions reach the replay before learn() (R:train.py:93-99)
+            rows = (x, list(actions), [float(r) for r in rew[lo:hi]], [bool(d) for d in done[lo:hi]], nobs[lo:hi])
+            agent.store_transitions(*rows, None)
+            oracle.store_transitions(*rows)
 
         oracle.py_state = O.py_state_to_array()
         oracle.np_state = O.np_state_to_array()

@@ -29,6 +29,32 @@ def free_port():
         return s.getsockname()[1]
 
 
+def oracle_steps_exact_tree(ref, z, steps=3):
+    """Step the oracle `steps` times next to a PER DP run whose per-step trees / all-gathered |delta|
+    the ranks saved (tests/dp_gpu_worker.py), checking the tree EXACTLY after every step: the
+    oracle's SumTree snapshot, updated in order with the ENGINE's |delta| (which agrees with the
+    oracle's only to the forward's rounding), must equal every rank's tree bit for bit, max / min
+    indices included; the oracle continues from that tree, so the next step samples the same
+    leaves (as tests/test_gpu_bf16.py does on one GPU).  Returns the step records."""
+    import copy
+    recs = []
+    for step in range(steps):
+        t = ref.replay.replay_buffer
+        snap = copy.copy(t)
+        snap.tree, snap.data = t.tree.copy(), list(t.data)
+        rec = ref.train_step()
+        recs.append(rec)
+        ref.replay.replay_buffer = snap
+        absd = z[0]["step_absd"][step]
+        ref.replay.update_batch_priorities(rec.positions.tolist(), absd.reshape(-1, 1))
+        for r, zr in enumerate(z):
+            assert np.array_equal(zr["step_absd"][step], absd), (r, step)
+            bad = np.nonzero(zr["step_trees"][step] != snap.tree)[0]
+            assert bad.size == 0, f"rank {r} step {step}: {bad.size} tree nodes differ, first {bad[:5]}"
+            assert tuple(zr["step_maxmin"][step]) == (snap.max_priority_index, snap.min_priority_index), (r, step)
+    return recs
+
+
 @pytest.mark.parametrize("algo", ["DuelingDoubleDQNAgent", "PerDuelingDoubleDQNAgent"])
 def test_gpu_dp_world2_matches_oracle(tmp_path, algo):
     env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(free_port()))
@@ -43,10 +69,10 @@ def test_gpu_dp_world2_matches_oracle(tmp_path, algo):
     import random
     ref.py_state = O.py_state_to_array(random.Random(seed).getstate())
     ref.np_state = O.np_state_to_array(np.random.RandomState(seed).get_state())
-    recs = [ref.train_step() for _ in range(3)]
+    z0, z1 = (np.load(tmp_path / f"rank{r}.npz") for r in (0, 1))
+    recs = oracle_steps_exact_tree(ref, [z0, z1]) if ref.per else [ref.train_step() for _ in range(3)]
     flat_on = np.concatenate([v.reshape(-1).numpy() for v in ref.online.values()])
     flat_tg = np.concatenate([v.reshape(-1).numpy() for v in ref.target.values()])
-    z0, z1 = (np.load(tmp_path / f"rank{r}.npz") for r in (0, 1))
     for z in (z0, z1):
         got = z["positions"].astype(np.int64) + (cap - 1 if ref.per else 0)
         assert np.array_equal(got, np.stack([np.asarray(r.positions) for r in recs]))
@@ -54,7 +80,7 @@ def test_gpu_dp_world2_matches_oracle(tmp_path, algo):
         np.testing.assert_allclose(z["params"], flat_on, atol=1e-5, rtol=0)
         np.testing.assert_allclose(z["target"], flat_tg, atol=1e-5, rtol=0)
         if ref.per:
-            np.testing.assert_allclose(z["tree"], ref.replay.replay_buffer.tree, rtol=1e-6, atol=1e-4)
+            np.testing.assert_allclose(z["step_absd"][-1], recs[-1].abs_td.reshape(-1), rtol=1e-5, atol=1e-5)
     assert np.array_equal(z0["params"], z1["params"]) and np.array_equal(z0["tree"], z1["tree"])
 
 
@@ -151,13 +177,48 @@ def test_gpu_dp_world2_bf16_matches_bf16_oracle(tmp_path):
     O.fill_replay(emu, *O.synth_transitions(fill, obs_dim, 8, seed=seed + 100))
     emu.py_state = O.py_state_to_array(random.Random(seed).getstate())
     emu.np_state = O.np_state_to_array(np.random.RandomState(seed).get_state())
-    recs = [emu.train_step() for _ in range(3)]
+    recs = oracle_steps_exact_tree(emu, z)
     flat_on = np.concatenate([v.reshape(-1).numpy() for v in emu.online.values()])
     for r in range(2):
         assert np.array_equal(z[r]["positions"].astype(np.int64) + cap - 1, np.stack([x.positions for x in recs]))
         np.testing.assert_allclose(z[r]["losses"], [x.loss for x in recs], rtol=LOSS_RTOL, atol=1e-6)
         np.testing.assert_allclose(z[r]["params"], flat_on, atol=W_ATOL, rtol=0)
     assert np.array_equal(z[0]["params"], z[1]["params"]) and np.array_equal(z[0]["tree"], z[1]["tree"])
+
+
+def test_gpu_dp_world8_per_bf16_global_batch_8192(tmp_path):
+    """configs[4] as its 8-GPU split: PerDuelingDoubleDQNAgent, bf16 compute, global minibatch 8192
+    sharded over 8 ranks (1024 rows each), every rank sampling the same 8192 leaves from its tree
+    replica (R:dqn/replay_memory.py:69-92), one gradient all-reduce, one all-gather of |delta| and
+    the ordered priority update on every replica (R:dqn/replay_memory.py:94-98).  Against the
+    oracle's bf16 emulation on the whole minibatch: leaves and the numpy RNG bit-exact, the tree
+    bit-exact after every step (oracle_steps_exact_tree), loss / weights within the bf16
+    tolerances of tests/test_gpu_bf16.py.  The ranks share the box's one GPU over gloo."""
+    import random
+    sys.path.insert(0, HERE)
+    from dp_gpu_worker import CASES
+    from test_gpu_bf16 import LOSS_RTOL, W_ATOL, _close
+    algo, world = "PerDuelingDoubleDQNAgent", 8
+    z = run_ranks(tmp_path, world, algo, case="c5", compute="bf16", timeout=600)
+    obs_dim, batch, cap, fill, seed = CASES["c5"]
+    spec = O.mlp_spec(obs_dim, 8, O.algo_spec_head(algo))
+    emu = O.OracleLearner(spec, algo, batch, cap, seed=seed, params=O.reference_init(spec, seed), per_pow="cr",
+                          compute="bf16")
+    O.fill_replay(emu, *O.synth_transitions(fill, obs_dim, 8, seed=seed + 100))
+    emu.py_state = O.py_state_to_array(random.Random(seed).getstate())
+    emu.np_state = O.np_state_to_array(np.random.RandomState(seed).get_state())
+    recs = oracle_steps_exact_tree(emu, z)
+    flat_on = np.concatenate([v.reshape(-1).numpy() for v in emu.online.values()])
+    flat_tg = np.concatenate([v.reshape(-1).numpy() for v in emu.target.values()])
+    for r in range(world):
+        assert np.array_equal(z[r]["positions"].astype(np.int64) + cap - 1, np.stack([x.positions for x in recs])), r
+        np.testing.assert_allclose(z[r]["losses"], [x.loss for x in recs], rtol=LOSS_RTOL, atol=1e-6)
+        np.testing.assert_allclose(z[r]["params"], flat_on, atol=W_ATOL, rtol=0)
+        np.testing.assert_allclose(z[r]["target"], flat_tg, atol=W_ATOL, rtol=0)
+        for k in ("params", "target", "tree"):   # replicas stay bitwise identical
+            assert np.array_equal(z[r][k], z[0][k]), (r, k)
+    for step, rec in enumerate(recs):   # the gathered |delta| of the whole minibatch vs the emulation
+        _close(z[0]["step_absd"][step], rec.abs_td.reshape(-1), "|delta|")
 
 
 @pytest.mark.parametrize("case,algo", [("hyb", "DuelingDoubleDQNAgent"), ("hyb", "PerDuelingDoubleDQNAgent"),

@@ -98,7 +98,8 @@ def test_gpu_hybrid_learn_golden():
         np.testing.assert_allclose(got, ref, atol=1e-5, rtol=0, err_msg=k)
 
 
-@pytest.mark.parametrize("batch,fwd_big,conv_ig", [(64, "1", "1"), (128, "1", "1"), (128, "1", "0"), (128, "0", "0")])
+@pytest.mark.parametrize("batch,fwd_big,conv_ig", [(64, "1", "1"), (128, "1", "1"), (128, "1", "0"), (128, "0", "0"),
+                                             (256, "1", "1")])
 def test_gpu_hybrid84_learn_matches_oracle(monkeypatch, batch, fwd_big, conv_ig):
     """The stacked (4,84,84) variant (BASELINE configs[2]).  conv_ig=1 (the default): the
     implicit-GEMM convs of conv_ig.hip (forward with F written by the last conv, phase-split data
@@ -108,12 +109,14 @@ def test_gpu_hybrid84_learn_matches_oracle(monkeypatch, batch, fwd_big, conv_ig)
     k_conv_dw_big tiles; with DQNX_FWD_BIG=0 the conv dX runs as the split conv_dxs level beside
     the big dW.  Tolerances are those of the (2,27,5) cases, with the
     gradient check scale-relative (the 56,462-term sums differ from torch's CPU order by a few
-    ulps of the largest terms)."""
+    ulps of the largest terms).  B=256 is the bench's batch (configs[2]): the default implicit
+    path with the split-K count of the 56,462-wide dense layer chosen for 256 rows per GPU."""
     E = _E()
     from parity import assert_grad_close
     monkeypatch.setenv("DQNX_FWD_BIG", fwd_big)
     monkeypatch.setenv("DQNX_CONV_IG", conv_ig)
-    algo, cap, n_fill, seed = "DuelingDoubleDQNAgent", 200, 150, 8
+    algo, seed = "DuelingDoubleDQNAgent", 8
+    cap, n_fill = (200, 150) if batch < 256 else (400, 350)
     ospec = O.hybrid_spec(8, "dueling", micro_chw=(4, 84, 84))
     init = O.reference_init(ospec, seed)
     oracle = O.OracleLearner(ospec, algo, batch, cap, seed=seed, params=init)
