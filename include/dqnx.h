@@ -149,7 +149,6 @@ typedef struct dqnx_ctrl {
 /* device error codes written to dqnx_ctrl.error */
 #define DQNX_DEVERR_SAMPLE_TOO_LARGE 1   /* random.sample: k > n (ValueError) */
 #define DQNX_DEVERR_EMPTY_TREE 2         /* PER sample with total priority 0 */
-#define DQNX_DEVERR_SAMPLER_STUCK 3      /* internal: a sampler wait exceeded its bound (never expected) */
 
 /* ---- engine lifetime --------------------------------------------------------------- */
 typedef struct dqnx_engine dqnx_engine;
@@ -256,6 +255,12 @@ int dqnx_rng_get(dqnx_engine* e, int32_t which, uint32_t* state625, void* stream
                                        reflects the prefetched draw.  A step without the flag
                                        consumes the pending minibatch. */
 int dqnx_learn_step(dqnx_engine* e, int32_t flags, void* stream);
+/* Same-stream rule for DQNX_STEP_PREFETCH: the engine remembers the stream of the step that
+ * left a draw pending; dqnx_rng_get synchronises THAT stream, and a later step on another
+ * stream synchronises it first.  A caller that captures prefetching steps into its own graph
+ * (dqn.data_parallel.GraphedDPStep) must replay the graph on the capture's stream or call
+ * dqnx_prefetch_stream() with the replay stream before dqnx_rng_get. */
+int dqnx_prefetch_stream(dqnx_engine* e, void* stream);
 /* Draw the first minibatch of a prefetching loop now (no-op when a draw is pending or the
  * configuration does not draw ahead), so that the next DQNX_STEP_PREFETCH step can be captured
  * into a caller's graph without its prologue (dqn.data_parallel.GraphedDPStep). */
@@ -326,10 +331,13 @@ int dqnx_events_create(int32_t n, void** events);      /* hipEventCreate x n */
 int dqnx_events_destroy(int32_t n, void** events);
 int dqnx_event_elapsed(void* start, void* stop, float* ms);   /* synchronises `stop` */
 
-/* ---- sampler (test hook / building block): random.sample positions on device.
+/* ---- sampler (test hook): random.sample positions on device.
  * R:dqn/replay_memory.py:38-39.  mt625: device uint32[625] (advanced in place);
  * n: population size; k: sample size; out: device int32[k].  scratch: device buffer of
- * dqnx_sample_scratch_bytes(n, k) bytes.  err: device int32 (set to 1 if k > n). */
+ * dqnx_sample_scratch_bytes(n, k) bytes.  err: device int32 (set to 1 if k > n).
+ * BLOCKING and not capturable: it stages n into `scratch` from a host stack value and
+ * synchronises `stream` before the launch.  Learn steps never call it (their samplers read the
+ * ring size from the control block, stream-ordered). */
 uint64_t dqnx_sample_scratch_bytes(int64_t n, int32_t k);
 int dqnx_sample_uniform(uint32_t* mt625, int64_t n, int32_t k, int32_t* out, void* scratch,
                         int32_t* err, void* stream);

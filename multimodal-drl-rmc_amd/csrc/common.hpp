@@ -2,6 +2,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "../../include/dqnx.h"
 
@@ -99,4 +100,24 @@ __device__ __forceinline__ int xcd_remap(int L, int total) {
 namespace dqnx {
 int set_error(int code, const char* fmt, ...);
 int set_hip_error(hipError_t e, const char* expr, const char* file, int line);
+
+// Host-side plan knobs (read when a plan is built, so tests can switch them per engine).
+//  * route_knob / route_flag: choose between alternative kernel routes that are ALL parity-tested
+//    (bitwise equal to the default, or within the stated tolerance of the same reference
+//    arithmetic); the tests force each route through the environment.
+//  * tuning_knob / tuning_flag: measurement-only parameters (tile, occupancy and threshold sweeps).
+//    The shipped library uses the measured defaults; only the diagnostic build
+//    (`make tuning`, -DDQNX_TUNING) reads them from the environment.
+inline int route_knob(const char* name, int dflt) {
+    const char* v = getenv(name);
+    return v ? atoi(v) : dflt;
+}
+inline bool route_flag(const char* name) { return getenv(name) != nullptr; }
+#ifdef DQNX_TUNING
+inline int tuning_knob(const char* name, int dflt) { return route_knob(name, dflt); }
+inline bool tuning_flag(const char* name) { return route_flag(name); }
+#else
+inline int tuning_knob(const char*, int dflt) { return dflt; }
+inline bool tuning_flag(const char*) { return false; }
+#endif
 }  // namespace dqnx

@@ -313,8 +313,7 @@ static dim3 grid_for(int64_t total) {
 int im2col_mode() {
     static int mode = -1;   // DQNX_IM2COL: 0 = flat/row kernels only, 1 = LDS band kernel where it fits (default)
     if (mode < 0) {
-        const char* e = getenv("DQNX_IM2COL");
-        mode = e ? atoi(e) : 1;
+        mode = tuning_knob("DQNX_IM2COL", 1);
     }
     return mode;
 }

@@ -267,11 +267,7 @@ __global__ __launch_bounds__(256, 2) void k_conv_ig(ConvIgArgs a) {
             bool bv;
             chunk(r, aoff4, woff, bv);
 #pragma unroll
-            for (int tn = 0; tn < TN; tn++) bb[tn] = (bv && !(a.exp & 2)) ? ld4(wrow[tn] + woff) : make_float4(0.f, 0.f, 0.f, 0.f);
-            if (a.exp & 2) {
-#pragma unroll
-                for (int tn = 0; tn < TN; tn++) bb[tn] = make_float4(woff * 1e-9f, 0.f, 1.f, (float)tn);
-            }
+            for (int tn = 0; tn < TN; tn++) bb[tn] = bv ? ld4(wrow[tn] + woff) : make_float4(0.f, 0.f, 0.f, 0.f);
         };
         // one chunk: the next chunk's weights into `nxt` while `cur` is multiplied (two named
         // register sets, chunk loop unrolled by 2: no copies, so the wait for `cur` does not
@@ -287,24 +283,17 @@ __global__ __launch_bounds__(256, 2) void k_conv_ig(ConvIgArgs a) {
             floatx4 av[TM];
 #pragma unroll
             for (int tm = 0; tm < TM; tm++) av[tm] = band4[ppos4[tm] + aoff4];
-            if (a.exp & 8) {
-#pragma unroll
-                for (int tm = 0; tm < TM; tm++) acc[tm][0][0] += av[tm][0] + cur[0].y;
-            } else {
-                mma(av, cur);
-            }
+            mma(av, cur);
         };
         for (int s = 0; s < nstage; s++) {
             set_stage(s);
             float4 b0[TN], b1[TN];
             bload(0, b0);
             __syncthreads();   // the previous stage's A reads are done
-            if (!(a.exp & 1)) pre.store(band, nr_of(s), a.WP, CB, a.CS);
+            pre.store(band, nr_of(s), a.WP, CB, a.CS);
             __syncthreads();
-            if (!(a.exp & 1)) {
-                if (s + 1 < nstage) pre.load(a.src, stage_of(T, s + 1), nr_of(s + 1), a.WP, CB, a.RS);
-                else if (Tn < total) pre.load(a.src, stage_of(Tn, 0), nr_of(0), a.WP, CB, a.RS);
-            }
+            if (s + 1 < nstage) pre.load(a.src, stage_of(T, s + 1), nr_of(s + 1), a.WP, CB, a.RS);
+            else if (Tn < total) pre.load(a.src, stage_of(Tn, 0), nr_of(0), a.WP, CB, a.RS);
             int r = 0;
             for (; r + 1 < per_blk; r += 2) {
                 step(r, b0, b1);
@@ -338,8 +327,7 @@ __global__ __launch_bounds__(256, 2) void k_conv_ig(ConvIgArgs a) {
                         const float v = acc[tm][tn][r], hv = (&h[tn].x)[r];
                         d[r] = relu ? (hv > 0.f ? v : 0.f) : (hv > 0.f ? v : v * (hv + 1.f));
                     }
-                    if (!(a.exp & 4) || d[0] == 12345.f)
-                        *reinterpret_cast<float4*>(outb + o + (wn * TN + tn) * 16 + 4 * g) = make_float4(d[0], d[1], d[2], d[3]);
+                    *reinterpret_cast<float4*>(outb + o + (wn * TN + tn) * 16 + 4 * g) = make_float4(d[0], d[1], d[2], d[3]);
                 }
             }
         } else {
@@ -364,7 +352,6 @@ __global__ __launch_bounds__(256, 2) void k_conv_ig(ConvIgArgs a) {
                         v[r] = x > 0.f ? x : (relu ? 0.f : __expf(x) - 1.f);
                     }
                     const int n0 = (wn * TN + tn) * 16 + 4 * g;
-                    if ((a.exp & 4) && v[0] != 12345.f) continue;
                     if (EPI == CIG_EPI_NHWC) {
                         *reinterpret_cast<float4*>(outb + q * a.opix + n0) = make_float4(v[0], v[1], v[2], v[3]);
                     } else {   // CHW flatten: consecutive lanes on consecutive pixels of a channel row
@@ -572,7 +559,7 @@ int persistent_grid(const void* fn, size_t lds, int64_t tiles) {
             occ_cache[{fn, lds}] = occ;
         }
     }
-    if (const char* v = getenv("DQNX_CIG_OCC")) occ = std::max(1, atoi(v));
+    occ = std::max(1, tuning_knob("DQNX_CIG_OCC", occ));
     return (int)std::max<int64_t>(1, std::min<int64_t>(tiles, (int64_t)occ * cus));
 }
 

@@ -154,15 +154,13 @@ constexpr int BWD_TILE = 32;   // k_bwd_level dW tile edge (DQNX_BWD_BM = DQNX_B
 // k_bwd_level's 32x32 role
 // (environment knobs are read when a plan is built, so tests can switch them per engine)
 static bool conv_dw_big(int64_t rows, int K) {
-    const char* v = getenv("DQNX_CONV_DW_BIG");
-    const int mode = v ? atoi(v) : 1;
+    const int mode = tuning_knob("DQNX_CONV_DW_BIG", 1);
     return mode != 0 && rows >= 65536 && K >= 127;
 }
 
 // DQNX_FWD_BIG=0 keeps every dense forward on the 16x64-tile kernel (A/B measurements)
 static bool fwd_big_mode() {
-    const char* v = getenv("DQNX_FWD_BIG");
-    return v ? atoi(v) != 0 : true;
+    return route_knob("DQNX_FWD_BIG", 1) != 0;
 }
 
 static inline uint64_t align_up(uint64_t x, uint64_t a) { return (x + a - 1) / a * a; }
@@ -201,7 +199,7 @@ static bool cig_stage_fits(int NR, int WP, int CB, bool vec) {
 static int cig_cb(int C, int NR, int WP, bool vec) {
     if (C == 4) return 4;
     size_t cap = 50 * 1024;   // DQNX_CIG_LDS_KB: band budget (a larger band means fewer workgroups per CU)
-    if (const char* v = getenv("DQNX_CIG_LDS_KB")) cap = (size_t)atoi(v) * 1024;
+    cap = (size_t)tuning_knob("DQNX_CIG_LDS_KB", 50) * 1024;
     for (int cb : {64, 32})
         if (C % cb == 0 && (size_t)NR * WP * (cb + 4) * 4 <= cap && cig_stage_fits(NR, WP, cb, vec)) return cb;
     return 16;
@@ -221,8 +219,8 @@ static bool cig_fwd_geom(const ConvPlan& cp, int Bl, bool first, ConvIgArgs& a) 
     CigClass& k = a.cls[0];
     k.ni = cp.kh; k.nj = cp.kw; k.i0 = k.j0 = 0; k.di = k.dj = 1; k.kw = cp.kw;
     k.o0 = 0; k.oi = a.WP; k.oj = 1;
-    const char* gv = getenv("DQNX_CIG_GROUPS");   // 0: stride-2 forwards stage all rows at once
-    if (cp.sh == 2 && cp.Ci != 4 && !(gv && atoi(gv) == 0)) {   // row-parity groups: band rows compact, one group per parity
+    // DQNX_CIG_GROUPS=0 (tuning): stride-2 forwards stage all rows at once
+    if (cp.sh == 2 && cp.Ci != 4 && tuning_knob("DQNX_CIG_GROUPS", 1) != 0) {   // row-parity groups: band rows compact, one group per parity
         a.ngrp = 2;
         a.RM = 1;
         a.RS = 2;
@@ -252,7 +250,6 @@ static bool cig_fwd_geom(const ConvPlan& cp, int Bl, bool first, ConvIgArgs& a) 
     a.maxtiles = k.tiles;
     a.Kw = cp.kh * cp.kw * cp.Ci;
     a.ymul = a.xmul = 1;
-    if (const char* v = getenv("DQNX_CIG_EXP")) a.exp = atoi(v);
     a.src.H = cp.Hi;
     a.src.W = cp.Wi;
     a.src.C = cp.Ci;
@@ -312,7 +309,6 @@ static bool cig_dx_geom(const ConvPlan& cp, int Bl, bool last, ConvIgArgs& a) {
     a.Kw = cp.kh * cp.kw * cp.Co;
     a.ymul = cp.sh;
     a.xmul = cp.sw;
-    if (const char* v = getenv("DQNX_CIG_EXP")) a.exp = atoi(v);
     a.src.H = cp.Ho;
     a.src.W = cp.Wo;
     a.src.C = cp.Co;
@@ -356,8 +352,7 @@ static bool cig_dw_geom(const ConvPlan& cp, int Bl, bool first, ConvDwIgArgs& d)
 // implicit-GEMM convs for every conv of a large micro grid (DQNX_CONV_IG=0: explicit path)
 static bool conv_ig_plan(const NetPlan& np, int Bl) {
     if (np.conv.empty()) return false;
-    const char* v = getenv("DQNX_CONV_IG");
-    if (v && atoi(v) == 0) return false;
+    if (route_knob("DQNX_CONV_IG", 1) == 0) return false;
     if ((int64_t)np.conv[0].Hi * np.conv[0].Wi < 1024) return false;   // the (2,27,5) grid keeps the explicit kernels
     for (size_t l = 0; l < np.conv.size(); l++) {
         ConvIgArgs f;
@@ -486,7 +481,7 @@ int layout(dqnx_engine* e) {
     e->ws_phys = sub((uint64_t)2 * e->Bl * 4);
     e->ws_pool = sub((uint64_t)(e->setsize + 64) * 4);
     e->ws_gtab = sub(sample_table_bytes(e->Bs));   // 0 unless the minibatch exceeds the LDS tables
-    e->mtc_blocks = (e->bwd_plan == 2 && c.algo != DQNX_ALGO_PER_DOUBLE && !getenv("DQNX_NO_MT_CACHE"))
+    e->mtc_blocks = (e->bwd_plan == 2 && c.algo != DQNX_ALGO_PER_DOUBLE && !tuning_flag("DQNX_NO_MT_CACHE"))
                         ? mt_cache_target_blocks(e->Bs, c.capacity) : 0;
     e->ws_mtc = sub((uint64_t)mt_cache_words() * 4);   // always valid for the sampler's loads
     e->ws_xobs = sub((uint64_t)e->Bl * e->stride * 4);
@@ -517,7 +512,7 @@ int layout(dqnx_engine* e) {
     e->ws_stamps = sub(64 * 8);
     e->ws_per_ticket = sub(64);   // k_per_sample arrival counter (zero between launches); [16]: PER chunk epoch
     // numpy MT block cache: only where the fused forward launch keeps it extended
-    if (c.algo == DQNX_ALGO_PER_DOUBLE && e->bwd_plan == 2 && e->fsplit <= 1 && !getenv("DQNX_NO_NP_CACHE") &&
+    if (c.algo == DQNX_ALGO_PER_DOUBLE && e->bwd_plan == 2 && e->fsplit <= 1 && !route_flag("DQNX_NO_NP_CACHE") &&
         np_cache_blocks(e->Bg) <= NPC_MAX_BLOCKS)
         e->ws_npc = sub((uint64_t)np_cache_words() * 4);
     if (c.algo == DQNX_ALGO_PER_DOUBLE) {   // k_per_prep / k_per_update / k_per_prop hand-offs
@@ -602,8 +597,8 @@ PerSampleArgs per_sample_args(dqnx_engine* e, int32_t* idx, int32_t* phys) {
     // (measured on MI355X: B=1024 per_sample 17.3 / 14.8 / 13.5 us at 256 / 128 / 64 per workgroup,
     // step 68.2 -> 63.2 us; bf16 B=8192 step 120.0 / 116.6 / 117.9 us)
     pa.spw = e->Bg <= 2048 ? 64 : 128;
-    if (const char* v = getenv("DQNX_PER_SPW")) {
-        const int x = atoi(v);
+    {
+        const int x = tuning_knob("DQNX_PER_SPW", pa.spw);
         if (x == 64 || x == 128 || x == 256) pa.spw = x;
     }
     return pa;
@@ -667,8 +662,7 @@ AdamBias adam_bias_args(dqnx_engine* e) {
 // keeps the per-step rebuild.  (Adam's row/column split needs out * in < 2^24.)
 bool adam_keeps_blk(const dqnx_engine* e) {
     if (e->bwd_plan != 2) return false;
-    const char* v = getenv("DQNX_ADAM_BLK");
-    if (!v || atoi(v) == 0) return false;
+    if (route_knob("DQNX_ADAM_BLK", 0) == 0) return false;
     for (const LayerPlan& lp : e->np.dense)
         if ((int64_t)lp.out * lp.in >= ((int64_t)1 << 24)) return false;
     return true;
@@ -684,8 +678,8 @@ bool adam_keeps_blk(const dqnx_engine* e) {
 bool dw_adam16_on(const dqnx_engine* e, int flags) {
     (void)flags;
     if (e->bwd_plan != 2 || e->fplan.bf16) return false;
-    if (const char* v = getenv("DQNX_DW_ADAM16")) {
-        if (atoi(v) == 0) return false;
+    if (route_flag("DQNX_DW_ADAM16")) {
+        if (route_knob("DQNX_DW_ADAM16", 1) == 0) return false;
     } else if (e->Bl > 2048) {
         return false;
     }
@@ -860,7 +854,7 @@ void build_fused_steps(dqnx_engine* e, int flags, int32_t* idx, int32_t* phys, s
     // the forward's outputs from its own XCD's L2 (16-row tiles, tiles % 8 == 0).  Measured at
     // B=1024: head_bwd 7.2 -> 6.6 us, the forward unchanged; DQNX_XCD_ROWS=0 keeps xcd_remap's order
     const int ftiles = (e->Bl + 15) / 16;
-    const bool xcd_rows = !(getenv("DQNX_XCD_ROWS") && atoi(getenv("DQNX_XCD_ROWS")) == 0) && e->fplan.mr == 1 &&
+    const bool xcd_rows = route_knob("DQNX_XCD_ROWS", 1) != 0 && e->fplan.mr == 1 &&
                           ftiles % 8 == 0 && !(e->fsplit > 1 && L >= 2);
     // 2. forward (R:dqn/agent.py:209-214 / 172-173 streams, R:dqn/network.py:61-65, 90-96)
     {
@@ -954,8 +948,8 @@ void build_fused_steps(dqnx_engine* e, int flags, int32_t* idx, int32_t* phys, s
         // 6.0 us with 4 parts; B=4096 best unsplit (9.2 vs 9.5 with 2, 13.8 with 4)
         for (int v : {4, 2})
             if (ha.nsplit == 1 && L >= 2 && np.dense[0].out % (v * 16) == 0 && e->tiles * v <= 256) ha.nsplit = v;
-        if (const char* ns = getenv("DQNX_HEAD_SPLIT")) {
-            const int v = atoi(ns);
+        if (route_flag("DQNX_HEAD_SPLIT")) {
+            const int v = route_knob("DQNX_HEAD_SPLIT", 1);
             if (v == 1 || ((v == 2 || v == 4) && L >= 2 && np.dense[0].out % (v * 16) == 0)) ha.nsplit = v;
         }
         ha.A = A;
@@ -1064,7 +1058,7 @@ void build_fused_steps(dqnx_engine* e, int flags, int32_t* idx, int32_t* phys, s
             // 32 x 16 tiles: every X element loaded feeds two MFMAs, half the workgroups (216 at
             // MLP-284: one per CU).  Measured at B=1024: 11.8 -> 10.35 us in context, bitwise equal
             // to the 16 x 16 tiles (DQNX_DW16_R=1 selects those)
-            const int rows16 = getenv("DQNX_DW16_R") && atoi(getenv("DQNX_DW16_R")) == 1 ? 1 : 2;
+            const int rows16 = route_knob("DQNX_DW16_R", 2) == 1 ? 1 : 2;
             da.rows16 = rows16;
             auto add = [&](const DwProblem& p, int64_t poff, int l) {
                 DwAdam16Layer& d = da.L[da.nl++];
@@ -1218,7 +1212,7 @@ SampleArgs uniform_sample_args(dqnx_engine* e, int32_t* idx, int32_t* phys) {
 // body's LDS table.  The step's last launch (k_dw_adam16, or the slab plan's Adam pass) copies the
 // staged minibatch over the compute slot.
 bool inlaunch_prefetch_ok(const dqnx_engine* e, int flags) {
-    if (getenv("DQNX_PF_SIDE")) return false;   // measurements: the side-stream pipeline instead
+    if (tuning_flag("DQNX_PF_SIDE")) return false;   // measurements: the side-stream pipeline instead
     return e->bwd_plan == 2 && e->cfg.algo != DQNX_ALGO_PER_DOUBLE && !(flags & DQNX_STEP_GIVEN_INDICES) &&
            e->Bs <= FWD_SAMPLE_MAX_K && e->fsplit <= 1;
 }
@@ -1502,7 +1496,7 @@ std::vector<KStep> build_learn_steps(dqnx_engine* e, int key) {
         const uint64_t part_floats = (uint64_t)e->slices[l] * ((uint64_t)lp.out * lp.in + lp.out);
         int kchunk = 0;
         const int ksplit = fwd_big_ksplit(e->Bl, lp.out, lp.in, np_, (int64_t)part_floats, &kchunk);
-        const int big_min_k = getenv("DQNX_FWD_BIG_MINK") ? atoi(getenv("DQNX_FWD_BIG_MINK")) : 8192;
+        const int big_min_k = tuning_knob("DQNX_FWD_BIG_MINK", 8192);
         if ((l > 0 || NC) && lp.in >= big_min_k && e->Bl >= 64 && fwd_big_mode() &&
             (uint64_t)ksplit * np_ * e->Bl * lp.out <= part_floats) {
             fa.ksplit = ksplit;
@@ -2147,7 +2141,7 @@ int dqnx_engine_create(const dqnx_config* cfg, dqnx_engine** out) {
     e->cfg = *cfg;
     int rc = plan_net(&cfg->net, e->np);
     if (rc) { delete e; return rc; }
-    const dqnx_config& c = e->cfg;
+    const dqnx_config c = *cfg;   // a copy: the error paths below read it after `delete e`
     if (c.algo < DQNX_ALGO_DQN || c.algo > DQNX_ALGO_PER_DOUBLE) { delete e; return set_error(DQNX_EINVAL, "bad algo"); }
     if (c.algo == DQNX_ALGO_PER_DOUBLE && c.per_numpy121) {
         rc = per_numpy121_init();
@@ -2162,7 +2156,11 @@ int dqnx_engine_create(const dqnx_config* cfg, dqnx_engine** out) {
         { delete e; return set_error(DQNX_EINVAL, "batch must be a positive multiple of world_size"); }
     if (c.capacity <= 0 || c.capacity >= ((int64_t)1 << 31)) { delete e; return set_error(DQNX_EINVAL, "capacity out of range"); }
     if (e->np.NH > 16) { delete e; return set_error(DQNX_EUNSUPPORTED, "head with more than 16 outputs"); }
-    if (!head_supported(e->np.F)) { delete e; return set_error(DQNX_EUNSUPPORTED, "head input width %d not in {64,128,256}", e->np.F); }
+    if (!head_supported(e->np.F)) {
+        const int F = e->np.F;   // (read before the delete: found by the ASan plan check)
+        delete e;
+        return set_error(DQNX_EUNSUPPORTED, "head input width %d not in {64,128,256}", F);
+    }
     for (size_t l = 0; l < e->np.dense.size(); l++)
         if (e->np.dense[l].out % 4) { delete e; return set_error(DQNX_EUNSUPPORTED, "hidden widths must be multiples of 4"); }
     if (sample_hash_slots(c.batch) < 0) { delete e; return set_error(DQNX_EUNSUPPORTED, "batch too large for the sampler"); }
@@ -2181,8 +2179,8 @@ int dqnx_engine_create(const dqnx_config* cfg, dqnx_engine** out) {
         const bool bf = c.compute_dtype == DQNX_COMPUTE_BF16;
         const bool fused_ok = c.net.kind == DQNX_NET_MLP && fused_fwd_plan(fp, c.net.obs_dim, bf, 1);
         e->bwd_plan = fused_ok ? 2 : 0;
-        if (const char* bp = getenv("DQNX_BWD_PLAN")) {
-            const int want = atoi(bp);
+        if (route_flag("DQNX_BWD_PLAN")) {
+            const int want = route_knob("DQNX_BWD_PLAN", 2);
             if (want == 0 || (want == 1 && c.net.kind == DQNX_NET_MLP) || (want == 2 && fused_ok)) e->bwd_plan = want;
         }
         if (bf && e->bwd_plan != 2) {   // bf16 lives in the fused MLP kernels only
@@ -2211,7 +2209,7 @@ int dqnx_engine_create(const dqnx_config* cfg, dqnx_engine** out) {
         if (e->fplan.bf16)
             for (int cand : {4, 2})
                 if (mr == 1 && ((e->Bl + 16 * cand - 1) / (16 * cand)) * nst >= 256) mr = cand;
-        if (const char* v = getenv("DQNX_FWD_MR")) mr = atoi(v);
+        mr = route_knob("DQNX_FWD_MR", mr);
         FusedFwdArgs trial = e->fplan;
         if (mr != 1 && fused_fwd_plan(trial, c.net.obs_dim, e->fplan.bf16 != 0, mr)) e->fplan = trial;
         // opt-in (DQNX_FWD_SPLIT=2|4): layer 1 in a launch of its own over 2 or 4 column parts
@@ -2219,8 +2217,8 @@ int dqnx_engine_create(const dqnx_config* cfg, dqnx_engine** out) {
         // 15.7 us for the whole one-launch forward; step 47.7 vs 45.2 us): the weight bytes
         // streamed from L2 stay the same in total, so more workgroups do not help
         if (e->fplan.mr == 1 && e->np.dense.size() >= 2) {
-            if (const char* v = getenv("DQNX_FWD_SPLIT")) {
-                const int w = atoi(v);
+            if (route_flag("DQNX_FWD_SPLIT")) {
+                const int w = route_knob("DQNX_FWD_SPLIT", 1);
                 if (w <= 1) e->fsplit = 1;
                 else if (e->np.dense[0].out % (16 * w) == 0) e->fsplit = w;
             }
@@ -2231,7 +2229,7 @@ int dqnx_engine_create(const dqnx_config* cfg, dqnx_engine** out) {
     e->slices.assign(L, 1);
     e->kslice.assign(L, e->Bl);
     int dw_rows = 256;   // minibatch rows per split-K slice of the weight gradients
-    if (const char* v = getenv("DQNX_DW_ROWS")) dw_rows = std::max(16, atoi(v));
+    dw_rows = std::max(16, tuning_knob("DQNX_DW_ROWS", dw_rows));
     for (int l = 0; l < L; l++) {
         int S = e->Bl / dw_rows;
         if (S < 1) S = 1;
@@ -2248,7 +2246,7 @@ int dqnx_engine_create(const dqnx_config* cfg, dqnx_engine** out) {
     // conv dW workgroups to aim for: the (4,84,84) conv 1 ([32 x 37] tile grid 2 x 1) had only
     // 64 workgroups at the old 32-slice cap; DQNX_CONV_DW_WGS=0 restores that rule
     int dw_wgs = 1024;
-    if (const char* v = getenv("DQNX_CONV_DW_WGS")) dw_wgs = std::max(0, atoi(v));
+    dw_wgs = std::max(0, tuning_knob("DQNX_CONV_DW_WGS", dw_wgs));
     for (int l = 0; l < NC; l++) {   // split-K over the conv's output pixels (b, ho, wo)
         const ConvPlan& cq = e->np.conv[l];
         const int rows = e->Bl * cq.Ho * cq.Wo;
@@ -2810,6 +2808,12 @@ int dqnx_event_elapsed(void* start, void* stop, float* ms) {
     if (!start || !stop || !ms) return set_error(DQNX_EINVAL, "null argument");
     DQNX_HIP_CHECK(hipEventSynchronize((hipEvent_t)stop));
     DQNX_HIP_CHECK(hipEventElapsedTime(ms, (hipEvent_t)start, (hipEvent_t)stop));
+    return DQNX_OK;
+}
+
+int dqnx_prefetch_stream(dqnx_engine* e, void* stream) {
+    if (!e) return set_error(DQNX_EINVAL, "null engine");
+    e->pf_stream = (hipStream_t)stream;   // where replays of a captured prefetching step run
     return DQNX_OK;
 }
 

@@ -1085,7 +1085,7 @@ __global__ __launch_bounds__(64 * DW16_NW) void k_dw_adam16(DwAdam16Args a) {
 }
 
 int launch_dw_adam16(const DwAdam16Args& a, hipStream_t s) {
-    static const int var = getenv("DQNX_DW16_VAR") ? atoi(getenv("DQNX_DW16_VAR")) : 0;
+    static const int var = tuning_knob("DQNX_DW16_VAR", 0);
     const dim3 grid(a.tiles + (a.mtc ? 1 : 0) + (a.pf_nidx > 0 ? 1 : 0));
     if (a.rows16 == 2) {
         switch (var) {   // measurement variants (waves per tile, k-steps per register set)
@@ -1270,8 +1270,7 @@ int launch_head(const HeadArgs& a, int act, hipStream_t s) {
 // the float4 kernel when every segment is 4-aligned (offsets, slab strides, pointers) and no
 // blocked copies ride along; DQNX_ADAM_VEC=0 keeps the scalar kernel
 static bool adam_vec_ok(const AdamArgs& a) {
-    if (const char* v = getenv("DQNX_ADAM_VEC"))
-        if (atoi(v) == 0) return false;
+    if (tuning_knob("DQNX_ADAM_VEC", 1) == 0) return false;
     if (a.nblk || a.e0 % 4) return false;
     auto al = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
     if (!al(a.p) || !al(a.m) || !al(a.v) || !al(a.grads) || (a.target && !al(a.target))) return false;

@@ -535,8 +535,6 @@ struct ConvIgArgs {
     int SRM, RS, ngrp;
     int gnr[2], gni[2];
     int BM, act;              // tile rows (64 / 128 / 256; TR * Wq <= BM), activation
-    int exp;                  // DQNX_CIG_EXP timing experiments (wrong results): 1 no band staging,
-                              // 2 no weight loads, 4 no epilogue stores, 8 no MFMA
     int N, CB, CS;            // GEMM columns, channels staged per pass, LDS floats per pixel
     CigSource src;
     CigClass cls[4];

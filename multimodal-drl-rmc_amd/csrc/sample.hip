@@ -120,7 +120,7 @@ int sample_hash_slots(int32_t k) {
 
 // smallest k routed to the fast sampler (DQNX_SAMPLER_FAST_MIN overrides, for measurements)
 static int fast_min_k() {
-    static const int v = getenv("DQNX_SAMPLER_FAST_MIN") ? atoi(getenv("DQNX_SAMPLER_FAST_MIN")) : SAMPLE_FAST_MIN_K;
+    static const int v = tuning_knob("DQNX_SAMPLER_FAST_MIN", SAMPLE_FAST_MIN_K);
     return v;
 }
 
@@ -145,11 +145,11 @@ uint64_t sample_table_bytes(int32_t k) {
 
 int launch_sample_uniform(const SampleArgs& a_in, hipStream_t s) {
     SampleArgs a = a_in;
-    a.test_flags = getenv("DQNX_SAMPLER_FORCE_FALLBACK") ? 1 : 0;
+    a.test_flags = route_flag("DQNX_SAMPLER_FORCE_FALLBACK") ? 1 : 0;
     const dim3 grid(1 + a.rl_blocks);
     const int lhs = lds_hash_slots(a.k);
-    if (a.k <= SAMPLE_FAST_MAX_K && (a.k >= fast_min_k() || getenv("DQNX_SAMPLER_FAST") || a.test_flags) &&
-        !getenv("DQNX_SAMPLER_OLD")) {
+    if (a.k <= SAMPLE_FAST_MAX_K && (a.k >= fast_min_k() || route_flag("DQNX_SAMPLER_FAST") || a.test_flags) &&
+        !route_flag("DQNX_SAMPLER_OLD")) {
         hipLaunchKernelGGL(k_sample_fast, grid, dim3(SAMPLE_FAST_NT), 0, s, a);
     } else if (lhs > 0) {
         switch (lhs) {

@@ -114,7 +114,10 @@ class GraphedDPStep:
         consume the pending draw.
         steps: DP steps captured back to back into the one graph (a replay = `steps` steps).
         Every hipGraphLaunch leaves ~8.5 us before its first kernel on MI355X / ROCm 7.2; inside
-        a graph consecutive kernels start back to back."""
+        a graph consecutive kernels start back to back.
+        Replays run on the caller's current stream; with prefetch each replay re-points the
+        engine's pending-draw stream there (dqnx_prefetch_stream), so dqnx_rng_get waits on the
+        stream that holds the draw."""
         self.steps = int(steps)
         self.engine = engine
         engine.set_graphs(False)
@@ -130,6 +133,14 @@ class GraphedDPStep:
                 else:
                     dp_learn_step(engine, soft_update=soft_update, group=group, prefetch=prefetch)
         torch.cuda.synchronize()
+        # the captured steps recorded torch's capture stream as the pending draw's stream; replays
+        # run on the caller's current stream, which dqnx_rng_get must synchronise instead
+        self._prefetch = prefetch and not bucketed
 
     def __call__(self):
         self.graph.replay()
+        if self._prefetch:
+            import ctypes
+            from . import _capi as C
+            C.check(C.lib().dqnx_prefetch_stream(self.engine.h, ctypes.c_void_p(
+                torch.cuda.current_stream(self.engine.grads.device).cuda_stream)), "prefetch_stream")
