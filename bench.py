@@ -472,6 +472,9 @@ def roofline_of(args, kern, batch_tag):
                 **common)
 
 
+ALLREDUCE_EST_US = 20.0   # assumed RCCL all-reduce of the 428 KB MLP-284 gradient over 8 xGMI-linked GPUs
+
+
 def single_gpu_extras(args, spec, device):
     """configs[3] points measured on this one GPU:
     * configs3_n1: the learn step at the global minibatch 4096 (strong-scaling N = 1 point);
@@ -516,9 +519,76 @@ def single_gpu_extras(args, spec, device):
         "note": "rank 0 of world_size 8 on one GPU: 512-row shard + grad reduce + Adam/soft update, the global "
                 "4096-draw sampler inside the forward launch (prefetch) or as its own launch; add the RCCL "
                 "all-reduce of the 428 KB gradient for the 8-GPU step"}, **seq)
+    # Amdahl bound of 8-GPU strong scaling at global 4096: the one-GPU step
+    # over 8 x (the shard step + an all-reduce estimate).  The all-reduce term is an assumption
+    # (RCCL ring over xGMI, 428 KB fp32 gradient: latency-dominated), not a measurement.
+    t1 = out["configs3_n1"]["ms_per_step"] * 1e3
+    shard = out["projection_w8"]["shard_step_us"]
+    out["projection_w8"]["efficiency_bound"] = {
+        "without_allreduce": t1 / (W * shard),
+        "with_allreduce": t1 / (W * (shard + ALLREDUCE_EST_US)),
+        "allreduce_estimate_us": ALLREDUCE_EST_US, "one_gpu_step_us": t1}
     del eng
     torch.cuda.empty_cache()
     return out
+
+
+def dropin_loop(args, device, batch=1024, iters=200, warmup=20):
+    """The drop-in path a reference user runs (R:train.py:88-108): `Agents.DuelingDoubleDQNAgent`
+    on the macro-lane MLP, one env row per iteration (n_env = 1):
+    choose_actions -> store_transitions -> learn -> update_target_network, timed per call on
+    the host clock (learn() ends with the RNG hand-back, which synchronises the stream).
+    The replay is pre-filled through the engine (synthetic rows, like the headline line)."""
+    import tempfile
+
+    import torch.optim as optim
+    from dqn import Agents
+
+    class Box:
+        shape = (args.obs_dim,)
+
+    def net_conf(space):   # R:env/custom_env/macro with lane/dqn_config.py:58-104 (MLP, ReLU, Adam)
+        act = nn.ReLU()
+        return (nn.Sequential(nn.Linear(space.shape[0], 256), act, nn.Linear(256, 128), act), 128, optim.Adam,
+                nn.SmoothL1Loss)
+    tmp = tempfile.mkdtemp(prefix="dqnx_dropin_")
+    agent = Agents.DuelingDoubleDQNAgent(
+        n_env=1, lr=1e-4, gamma=0.99, epsilon_start=1.0, epsilon_min=0.05, epsilon_decay=2e6,
+        epsilon_exp_decay=False, nn_conf_func=net_conf, input_dim=Box(), output_dim=args.actions,
+        batch_size=batch, min_buffer_size=batch, buffer_size=args.capacity, update_target_frequency=30000,
+        target_soft_update=True, target_soft_update_tau=1e-3, save_frequency=10 ** 9, log_frequency=10 ** 9,
+        save_dir=tmp + "/", log_dir=tmp + "/", load=False, algo="DuelingDoubleDQNAgent", gpu=str(device.index or 0))
+    fill_ring(agent.engine, min(args.capacity, 100_000), args.obs_dim, args.actions, device, seed=0)
+    rng = np.random.default_rng(0)
+    obs = rng.random((iters + warmup + 1, args.obs_dim), dtype=np.float32)
+    random.seed(1234)
+    phases = {"choose_actions": 0.0, "store_transitions": 0.0, "learn": 0.0, "update_target_network": 0.0}
+    t_all = 0.0
+    for t in range(iters + warmup):
+        agent.step = t
+        t0 = time.perf_counter()
+        a = agent.choose_actions(obs[t:t + 1])
+        t1 = time.perf_counter()
+        agent.store_transitions(obs[t:t + 1], a, [0.5], [False], obs[t + 1:t + 2], None)
+        t2 = time.perf_counter()
+        agent.learn()
+        t3 = time.perf_counter()
+        agent.update_target_network()
+        torch.cuda.synchronize(device)
+        t4 = time.perf_counter()
+        if t >= warmup:
+            phases["choose_actions"] += t1 - t0
+            phases["store_transitions"] += t2 - t1
+            phases["learn"] += t3 - t2
+            phases["update_target_network"] += t4 - t3
+            t_all += t4 - t0
+    del agent
+    torch.cuda.empty_cache()
+    return {"us_per_iteration": t_all / iters * 1e6, "batch": batch, "n_env": 1, "iterations": iters,
+            "learn_tr_per_s": batch * iters / t_all,
+            "phases_us": {k: v / iters * 1e6 for k, v in phases.items()},
+            "note": "Agents.DuelingDoubleDQNAgent through the R:train.py:88-108 call sequence on the MLP-284 "
+                    "macro-lane net; host-clock per call, the stream synchronised at the end of every iteration"}
 
 
 def main():
@@ -587,6 +657,10 @@ def main():
         torch.cuda.empty_cache()
         if not dpmode:
             extras = single_gpu_extras(args, spec, device)
+            try:
+                extras["dropin_loop"] = dropin_loop(args, device)
+            except Exception as ex:   # an extra must never hide the headline number
+                log(f"dropin loop failed: {ex!r}")
         elif scaling == "strong":   # the weak-scaling companion line: 4096 rows per rank
             weng = make_engine(args, spec, 4096 * world, world, rank, device, local=local)
             wel, _ = run_learner(args, weng, world, backend, args.steps, args.warmup, dist, device, dp=dpmode)

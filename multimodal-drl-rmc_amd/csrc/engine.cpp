@@ -364,6 +364,23 @@ static bool conv_ig_plan(const NetPlan& np, int Bl) {
     return true;
 }
 
+// the micro-CNN geometry of a two-stream net (micro.hip): every conv 3x3 with padding 1
+static bool micro_geom(const NetPlan& np, MicroConv* c) {
+    const int NC = (int)np.conv.size();
+    if (NC < 2 || NC > MICRO_MAX_CONV) return false;
+    for (int l = 0; l < NC; l++) {
+        const ConvPlan& cp = np.conv[l];
+        if (cp.kh != 3 || cp.kw != 3 || cp.ph != 1 || cp.pw != 1) return false;
+        MicroConv& m = c[l];
+        memset(&m, 0, sizeof(m));
+        m.Ci = cp.Ci; m.Hi = cp.Hi; m.Wi = cp.Wi; m.Co = cp.Co; m.Ho = cp.Ho; m.Wo = cp.Wo;
+        m.sh = cp.sh; m.sw = cp.sw;
+        m.woff = cp.off;
+        m.cs = cp.Co + 8;
+    }
+    return true;
+}
+
 struct KStep {
     std::string name;
     double flops = 0, bytes = 0;
@@ -396,11 +413,18 @@ struct dqnx_engine {
     // dZ [M][Co], split-K partial slabs; dense input F [3][Bl][strideF] and its gradient
     std::vector<uint64_t> ws_col, ws_Hc, ws_dZc, ws_cpart;
     std::vector<int> cslices, ckslice;
-    uint64_t ws_F = 0, ws_dF = 0, ws_dcol = 0;
+    uint64_t ws_F = 0, ws_dF = 0, ws_dcol = 0, ws_fpart = 0;
+    int f1_ksplit = 0, f1_kchunk = 0;   // conv nets' dense 1 forward: split-K slabs (0: the 16 x 64 kernel)
     // implicit-GEMM convs (conv_ig.hip): no column matrices; permuted weight copies per conv
     // ([co][tap][ci] online / target, [ci][tap][co] online), the last conv writes F directly
     bool conv_ig = false;
     std::vector<uint64_t> ws_wperm0, ws_wperm1, ws_wpermT;
+    // micro-CNN plan (micro.hip): the reference HEAD net's convs on a small grid, activations on
+    // chip (forward: S samples per workgroup; data gradients: dx_S; weight gradients: dw plan)
+    bool micro = false;
+    int micro_S = 1, micro_lds = 0, micro_dx_S = 1, micro_dx_lds = 0;
+    int micro_lds_d[MICRO_MAX_CONV] = {0, 0, 0};
+    MicroDwArgs micro_dw;
     int stage_rows = 0;
     char* arena = nullptr;
     int64_t ring_size = 0, ring_wptr = 0;   // host mirror of the ring state (pushes are host-driven)
@@ -538,12 +562,13 @@ int layout(dqnx_engine* e) {
         const ConvPlan& cp = np.conv[l];
         const uint64_t M = (uint64_t)e->Bl * cp.Ho * cp.Wo;
         const bool last = l == NC - 1;
-        if (!e->conv_ig) e->ws_col[l] = sub(3 * M * cp.Kstride * 4);
-        if (!(e->conv_ig && last)) e->ws_Hc[l] = sub(3 * M * cp.Co * 4);   // the implicit path's last conv writes F
+        if (!e->conv_ig && !e->micro) e->ws_col[l] = sub(3 * M * cp.Kstride * 4);
+        // the implicit path's last conv writes F; the micro plan keeps stream 0's outputs only
+        if (!((e->conv_ig || e->micro) && last)) e->ws_Hc[l] = sub((e->micro ? 1 : 3) * M * cp.Co * 4);
         e->ws_dZc[l] = sub(M * cp.Co * 4);
         e->ws_cpart[l] = sub((uint64_t)e->cslices[l] * ((uint64_t)cp.Co * cp.K + cp.Co) * 4);
-        if (!e->conv_ig && l > 0 && M * cp.K * 4 > dcol_max) dcol_max = M * cp.K * 4;
-        if (e->conv_ig) {
+        if (!e->conv_ig && !e->micro && l > 0 && M * cp.K * 4 > dcol_max) dcol_max = M * cp.K * 4;
+        if (e->conv_ig || e->micro) {
             e->ws_wperm0[l] = sub((uint64_t)cp.Co * cp.K * 4);
             e->ws_wperm1[l] = sub((uint64_t)cp.Co * cp.K * 4);
             if (l > 0) e->ws_wpermT[l] = sub((uint64_t)cp.Co * cp.K * 4);
@@ -552,6 +577,7 @@ int layout(dqnx_engine* e) {
     if (NC) {
         e->ws_F = sub((uint64_t)3 * e->Bl * np.strideF * 4);
         e->ws_dF = sub((uint64_t)e->Bl * np.dense[0].in * 4);
+        if (e->f1_ksplit) e->ws_fpart = sub((uint64_t)e->f1_ksplit * 3 * e->Bl * np.dense[0].out * 4);
         if (dcol_max) e->ws_dcol = sub(dcol_max);
     }
     cur = align_up(cur, 256);
@@ -1365,7 +1391,80 @@ std::vector<KStep> build_learn_steps(dqnx_engine* e, int key) {
             ks.push_back(k);
         }
     }
-    if (!e->conv_ig) {
+    // micro-CNN plan: conv weights of the step in the kernels' layouts, then ONE launch for every
+    // conv of every stream (micro.hip)
+    MicroConv mconv[MICRO_MAX_CONV];
+    if (NC && e->micro) {
+        micro_geom(np, mconv);
+        int x0 = 0, zero = 0;
+        micro_fwd_layout(mconv, NC, e->micro_S, &x0, &zero);
+        ConvPermArgs pa;
+        memset(&pa, 0, sizeof(pa));
+        double pbytes = 0;
+        for (int l = 1; l < NC; l++) {   // conv 1 reads the torch layout directly
+            const ConvPlan& cp = np.conv[l];
+            pa.job[pa.njobs++] = ConvPermJob{params + cp.off, at<float>(e, e->ws_wperm0[l]), cp.Co, cp.Ci, 9, 0};
+            pa.job[pa.njobs++] = ConvPermJob{tparams + cp.off, at<float>(e, e->ws_wperm1[l]), cp.Co, cp.Ci, 9, 0};
+            pa.job[pa.njobs++] = ConvPermJob{params + cp.off, at<float>(e, e->ws_wpermT[l]), cp.Co, cp.Ci, 9, 1};
+            mconv[l].wp[0] = at<float>(e, e->ws_wperm0[l]);
+            mconv[l].wp[1] = at<float>(e, e->ws_wperm1[l]);
+            mconv[l].wT = at<float>(e, e->ws_wpermT[l]);
+            pbytes += 8.0 * cp.Co * cp.K * 3;
+        }
+        for (int l = 0; l < NC; l++) {
+            mconv[l].hc = l + 1 < NC ? at<float>(e, e->ws_Hc[l]) : nullptr;
+            mconv[l].dz = at<float>(e, e->ws_dZc[l]);
+        }
+        {
+            KStep k;
+            k.name = "conv_perm";
+            k.bytes = pbytes;
+            k.run = [=](hipStream_t s) { return launch_conv_perm(pa, s); };
+            ks.push_back(k);
+        }
+        MicroFwdArgs ma;
+        memset(&ma, 0, sizeof(ma));
+        for (int l = 0; l < NC; l++) ma.c[l] = mconv[l];
+        ma.nc = NC;
+        ma.Bl = e->Bl;
+        ma.S = e->micro_S;
+        ma.groups = (e->Bl + ma.S - 1) / ma.S;
+        int z = 0;
+        for (int st = 0; st < 3; st++) {
+            if (st == 1 && !dbl) continue;
+            ma.stream_of[z] = st;
+            ma.F[z] = at<float>(e, e->ws_F) + (int64_t)st * e->Bl * np.strideF;
+            z++;
+        }
+        ma.nstreams = z;
+        ma.params = params;
+        ma.tparams = tparams;
+        ma.ring_obs = ring_obs;
+        ma.ring_next = ring_next;
+        ma.ring_stride = e->stride;
+        ma.macro_len = np.macro_len;
+        ma.phys = phys;
+        ma.strideF = np.strideF;
+        const ConvPlan& cl = np.conv[NC - 1];
+        ma.flat_cols = cl.Co * cl.Ho * cl.Wo;
+        ma.x0 = x0;
+        ma.zero = zero;
+        ma.lds_floats = e->micro_lds;
+        double flops = 0, bytes = 0;
+        for (int l = 0; l < NC; l++) {
+            const ConvPlan& cp = np.conv[l];
+            flops += 2.0 * nstreams * Bl * cp.Ho * cp.Wo * (double)cp.Co * cp.K;
+            bytes += 4.0 * 2.0 * (cp.Co * (double)cp.K + cp.Co) + (l + 1 < NC ? 4.0 * Bl * cp.Ho * cp.Wo * cp.Co : 0.0);
+        }
+        bytes += 4.0 * nstreams * Bl * (np.conv[0].Ci * np.conv[0].Hi * np.conv[0].Wi + np.strideF);
+        KStep k;
+        k.name = "micro_fwd";
+        k.flops = flops;
+        k.bytes = bytes;
+        k.run = [=](hipStream_t s) { return launch_micro_fwd(ma, s); };
+        ks.push_back(k);
+    }
+    if (!e->conv_ig && !e->micro) {
     // 2a. two-stream micro CNN (R:env/dqn_config.py:92-101, forward :126-133): im2col + MFMA GEMM
     for (int l = 0; l < NC; l++) {
         const ConvPlan cp = np.conv[l];
@@ -1496,6 +1595,19 @@ std::vector<KStep> build_learn_steps(dqnx_engine* e, int key) {
         const uint64_t part_floats = (uint64_t)e->slices[l] * ((uint64_t)lp.out * lp.in + lp.out);
         int kchunk = 0;
         const int ksplit = fwd_big_ksplit(e->Bl, lp.out, lp.in, np_, (int64_t)part_floats, &kchunk);
+        if (l == 0 && NC && e->f1_ksplit) {
+            fa.ksplit = e->f1_ksplit;
+            fa.kchunk = e->f1_kchunk;
+            fa.partial = at<float>(e, e->ws_fpart);
+            k.run = [=](hipStream_t s) { return launch_linear_fwd_split(fa, np_, act, vecb, s); };
+            ks.push_back(k);
+            KStep kr;
+            kr.name = k.name + "_reduce";
+            kr.bytes = 4.0 * ((double)fa.ksplit + 1) * np_ * Bl * lp.out;
+            kr.run = [=](hipStream_t s) { return launch_linear_fwd_reduce(fa, np_, act, s); };
+            ks.push_back(kr);
+            continue;
+        }
         const int big_min_k = tuning_knob("DQNX_FWD_BIG_MINK", 8192);
         if ((l > 0 || NC) && lp.in >= big_min_k && e->Bl >= 64 && fwd_big_mode() &&
             (uint64_t)ksplit * np_ * e->Bl * lp.out <= part_floats) {
@@ -1720,8 +1832,58 @@ std::vector<KStep> build_learn_steps(dqnx_engine* e, int key) {
             ks.push_back(k);
         }
     }
+    // 4b''. micro-CNN backward: data gradients of every conv (one launch, stream 0), then every
+    //       conv's weight gradient as split-K slabs (one launch)
+    if (NC && e->micro) {
+        MicroDxArgs xa;
+        memset(&xa, 0, sizeof(xa));
+        for (int l = 0; l < NC; l++) xa.c[l] = mconv[l];
+        xa.nc = NC;
+        xa.Bl = e->Bl;
+        xa.S = e->micro_dx_S;
+        xa.groups = (e->Bl + xa.S - 1) / xa.S;
+        xa.dF = at<float>(e, e->ws_dF);
+        xa.ldf = np.dense[0].in;
+        micro_dx_layout(mconv, NC, xa.S, xa.lds_d, &xa.zero);
+        micro_dx_waves(xa);
+        xa.lds_floats = e->micro_dx_lds;
+        double xf = 0, xb = 0;
+        for (int l = 1; l < NC; l++) {
+            const ConvPlan& cp = np.conv[l];
+            xf += 2.0 * Bl * cp.Ho * cp.Wo * (double)cp.Co * cp.K;
+            xb += 4.0 * (Bl * cp.Ho * cp.Wo * (double)cp.Co + 2.0 * Bl * cp.Hi * cp.Wi * cp.Ci + cp.Co * (double)cp.K);
+        }
+        KStep kx;
+        kx.name = "micro_dx";
+        kx.flops = xf;
+        kx.bytes = xb;
+        kx.run = [=](hipStream_t s) { return launch_micro_dx(xa, s); };
+        ks.push_back(kx);
+        MicroDwArgs da = e->micro_dw;
+        da.ring_obs = ring_obs;
+        da.stamps = at<int64_t>(e, e->ws_stamps);
+        da.phys = phys;
+        da.ring_stride = e->stride;
+        da.macro_len = np.macro_len;
+        double wf = 0, wb = 0;
+        for (int l = 0; l < NC; l++) {
+            const ConvPlan& cp = np.conv[l];
+            MicroDwLayer& L = da.L[l];
+            L.D = at<float>(e, e->ws_dZc[l]);
+            L.X = l > 0 ? at<float>(e, e->ws_Hc[l - 1]) : nullptr;
+            L.partial = at<float>(e, e->ws_cpart[l]);
+            wf += 2.0 * Bl * cp.Ho * cp.Wo * (double)cp.Co * (cp.K + 1.0);
+            wb += 4.0 * (Bl * cp.Ho * cp.Wo * (double)cp.Co + Bl * (double)cp.Ci * cp.Hi * cp.Wi + (double)L.slices * L.pstride);
+        }
+        KStep kw;
+        kw.name = "micro_dw";
+        kw.flops = wf;
+        kw.bytes = wb;
+        kw.run = [=](hipStream_t s) { return launch_micro_dw(da, s); };
+        ks.push_back(kw);
+    }
     // 4b. micro CNN backward: unflatten dF, then per conv (last first) dW + dX columns, col2im
-    if (NC && !e->conv_ig) {
+    if (NC && !e->conv_ig && !e->micro) {
         {
             const ConvPlan cl = np.conv[NC - 1];
             UnflattenArgs ua;
@@ -2049,6 +2211,13 @@ int dp_buckets(dqnx_engine* e, std::vector<DpBucket>& out) {
         out.push_back({0, nk, 0, np.P});
         return DQNX_OK;
     }
+    if (e->micro) {   // micro-CNN plan: every conv's gradient comes out of one launch (micro_dw)
+        const int kx = find("micro_dx", 0), kw = find("micro_dw", 0);
+        if (kx < 0 || kw < kx) return set_error(DQNX_EUNSUPPORTED, "dp buckets: no micro conv backward in the plan");
+        out.push_back({0, kx, np.dense[0].off, np.P - np.dense[0].off});
+        out.push_back({kx, nk, np.conv[0].off, np.dense[0].off - np.conv[0].off});
+        return DQNX_OK;
+    }
     int cut = find("unflatten", 0);
     if (cut < 0) return set_error(DQNX_EUNSUPPORTED, "dp buckets: no conv backward in the plan");
     out.push_back({0, cut, np.dense[0].off, np.P - np.dense[0].off});
@@ -2243,6 +2412,36 @@ int dqnx_engine_create(const dqnx_config* cfg, dqnx_engine** out) {
     e->cslices.assign(NC, 1);
     e->ckslice.assign(NC, 1);
     e->conv_ig = conv_ig_plan(e->np, e->Bl);
+    if (NC && route_knob("DQNX_MICRO_CNN", 1) != 0) {   // DQNX_MICRO_CNN=0 keeps the per-layer conv kernels
+        MicroConv mc[MICRO_MAX_CONV];
+        const int nst = c.algo == DQNX_ALGO_DQN ? 2 : 3;
+        int S = 0, lf = 0, dS = 0, dlf = 0, lds_d[MICRO_MAX_CONV];
+        if (micro_geom(e->np, mc) && micro_plan(mc, NC, e->Bl, nst, e->n_cu, &S, &lf) &&
+            micro_dx_plan(mc, NC, e->Bl, &dS, lds_d, &dlf)) {
+            MicroDwArgs& d = e->micro_dw;
+            memset(&d, 0, sizeof(d));
+            d.nc = NC;
+            d.Bl = e->Bl;
+            for (int l = 0; l < NC; l++) {
+                MicroDwLayer& L = d.L[l];
+                L.Ci = mc[l].Ci; L.Hi = mc[l].Hi; L.Wi = mc[l].Wi; L.Co = mc[l].Co; L.Ho = mc[l].Ho; L.Wo = mc[l].Wo;
+                L.sh = mc[l].sh; L.sw = mc[l].sw;
+            }
+            if (micro_dw_plan(d, e->n_cu) == DQNX_OK) {
+                e->micro = true;
+                e->conv_ig = false;
+                e->micro_S = S;
+                e->micro_lds = lf;
+                e->micro_dx_S = dS;
+                e->micro_dx_lds = dlf;
+                for (int l = 0; l < NC; l++) e->micro_lds_d[l] = lds_d[l];
+            }
+        }
+    }
+    if (NC && route_knob("DQNX_FWD_SPLIT", 1) != 0) {   // dense 1 (K = F) as 64 x 64 split-K tiles
+        const int nst = c.algo == DQNX_ALGO_DQN ? 2 : 3;
+        e->f1_ksplit = fwd_split_ksplit(e->Bl, e->np.dense[0].out, e->np.dense[0].in, nst, e->n_cu, &e->f1_kchunk);
+    }
     // conv dW workgroups to aim for: the (4,84,84) conv 1 ([32 x 37] tile grid 2 x 1) had only
     // 64 workgroups at the old 32-slice cap; DQNX_CONV_DW_WGS=0 restores that rule
     int dw_wgs = 1024;
@@ -2266,6 +2465,7 @@ int dqnx_engine_create(const dqnx_config* cfg, dqnx_engine** out) {
             cig_dw_geom(cq, e->Bl, l == 0, d);
             e->cslices[l] = d.slices;
         }
+        if (e->micro) e->cslices[l] = e->micro_dw.L[l].slices;   // sample slices of k_micro_dw
         if (e->np.conv[l].Co % 4) { delete e; return set_error(DQNX_EUNSUPPORTED, "conv channels must be multiples of 4"); }
     }
     layout(e);

@@ -131,10 +131,10 @@ __global__ __launch_bounds__(256) void k_linear_fwd(FwdArgs args) {
 // into C.  A 128-row tile loads each weight K-slab once per 128 rows instead of once per 16.
 // The per-element accumulation order (K ascending, 16-deep MFMA chunks) is the one of the
 // 16x64 kernel, so both give bit-identical outputs.
-template <int ACT, bool VECB, int BM, int BN, int WM>
+template <int ACT, bool VECB, int BM, int BN, int WM, int KT = FWD_BIG_KT>
 __global__ __launch_bounds__(256) void k_linear_fwd_big(FwdArgs args) {
     constexpr int WN = 4 / WM;
-    using G = TileGemm<BM, BN, FWD_BIG_KT, WM, WN, L_ROWS_K, L_ROWS_K, true, VECB>;
+    using G = TileGemm<BM, BN, KT, WM, WN, L_ROWS_K, L_ROWS_K, true, VECB>;
     constexpr int TM = G::TM, TN = G::TN;
     __shared__ __attribute__((aligned(16))) float lds[G::LDS_FLOATS];
     const int M = args.M, N = args.N, K = args.K;
@@ -723,20 +723,26 @@ __global__ __launch_bounds__(256) void k_adam(AdamArgs a) {
             for (int q = 1; q < kMaxSeg; q++)
                 if (q < a.nseg && e >= a.seg[q].off) sg = a.seg[q];
             const float* pp = sg.partial + (e - sg.off);
-            float pv[8];
+            // fixed-order sum of the slabs: slab 0, then 16 / 4 / 1 per round trip, every load of a
+            // round unconditional
+            const int64_t ps = sg.pstride;
+            gsum = pp[0];
+            int u = 1;
+            for (; u + 16 <= sg.S; u += 16) {
+                float pv[16];
 #pragma unroll
-            for (int u = 0; u < 8; u++) pv[u] = (u < sg.S) ? pp[(int64_t)u * sg.pstride] : 0.f;
-            gsum = pv[0];                               // fixed-order sum of the slabs
+                for (int j = 0; j < 16; j++) pv[j] = pp[(int64_t)(u + j) * ps];
 #pragma unroll
-            for (int u = 1; u < 8; u++)
-                if (u < sg.S) gsum += pv[u];
-            for (int u0 = 8; u0 < sg.S; u0 += 8) {   // 8 loads in flight per round trip
-#pragma unroll
-                for (int u = 0; u < 8; u++) pv[u] = (u0 + u < sg.S) ? pp[(int64_t)(u0 + u) * sg.pstride] : 0.f;
-#pragma unroll
-                for (int u = 0; u < 8; u++)
-                    if (u0 + u < sg.S) gsum += pv[u];
+                for (int j = 0; j < 16; j++) gsum += pv[j];
             }
+            for (; u + 4 <= sg.S; u += 4) {
+                float pv[4];
+#pragma unroll
+                for (int j = 0; j < 4; j++) pv[j] = pp[(int64_t)(u + j) * ps];
+#pragma unroll
+                for (int j = 0; j < 4; j++) gsum += pv[j];
+            }
+            for (; u < sg.S; u++) gsum += pp[(int64_t)u * ps];
             a.grads[e] = gsum;
         }
         if (a.mode == 0) continue;
@@ -828,18 +834,43 @@ __global__ __launch_bounds__(256) void k_adam4(AdamArgs a) {
             for (int q = 1; q < kMaxSeg; q++)
                 if (q < a.nseg && e >= a.seg[q].off) sg = a.seg[q];
             const float* pp = sg.partial + (e - sg.off) - e;   // ld() adds e back
-            float4 pv[4];
-            for (int u0 = 0; u0 < sg.S; u0 += 4) {   // 4 slabs in flight per round trip
+            if (nv == 4) {
+                // slab 0, then 16 / 4 / 1 slabs per round trip, every load of a round unconditional
+                // (a conditional load would make the compiler wait for all of them before the
+                // first add); the conv nets' micro dW writes ~100 slabs, a dense layer 1
+                const float* q4 = pp + e;
+                const int64_t ps = sg.pstride;
+                g = ld4(q4);
+                int u = 1;
+                for (; u + 16 <= sg.S; u += 16) {
+                    float4 pv[16];
 #pragma unroll
-                for (int u = 0; u < 4; u++)
-                    pv[u] = (u0 + u < sg.S) ? ld(pp + (int64_t)(u0 + u) * sg.pstride) : make_float4(0.f, 0.f, 0.f, 0.f);
+                    for (int j = 0; j < 16; j++) pv[j] = ld4(q4 + (int64_t)(u + j) * ps);
 #pragma unroll
-                for (int u = 0; u < 4; u++) {
-                    if (u0 + u >= sg.S) break;
-                    if (u0 + u == 0) {
-                        g = pv[0];
+                    for (int j = 0; j < 16; j++) {
+                        g.x += pv[j].x; g.y += pv[j].y; g.z += pv[j].z; g.w += pv[j].w;
+                    }
+                }
+                for (; u + 4 <= sg.S; u += 4) {
+                    float4 pv[4];
+#pragma unroll
+                    for (int j = 0; j < 4; j++) pv[j] = ld4(q4 + (int64_t)(u + j) * ps);
+#pragma unroll
+                    for (int j = 0; j < 4; j++) {
+                        g.x += pv[j].x; g.y += pv[j].y; g.z += pv[j].z; g.w += pv[j].w;
+                    }
+                }
+                for (; u < sg.S; u++) {
+                    const float4 x = ld4(q4 + (int64_t)u * ps);
+                    g.x += x.x; g.y += x.y; g.z += x.z; g.w += x.w;
+                }
+            } else {   // the last, partial vector
+                for (int u = 0; u < sg.S; u++) {
+                    const float4 x = ld(pp + (int64_t)u * sg.pstride);
+                    if (u == 0) {
+                        g = x;
                     } else {
-                        g.x += pv[u].x; g.y += pv[u].y; g.z += pv[u].z; g.w += pv[u].w;
+                        g.x += x.x; g.y += x.y; g.z += x.z; g.w += x.w;
                     }
                 }
             }
@@ -1200,6 +1231,36 @@ int launch_linear_fwd_big(const FwdArgs& args, int nprob, int act, bool vecb, hi
     if (a2.ksplit == 1 && args.N <= 32) launch_fwd_big_t<128, 32, 4>(a2, act, vecb, s);
     else if (a2.ksplit == 1 && args.N <= 64) launch_fwd_big_t<128, 64, 2>(a2, act, vecb, s);
     else launch_fwd_big_t<FWD_BIG_BM, FWD_BIG_BN, 2>(a2, act, vecb, s);
+    DQNX_HIP_CHECK(hipGetLastError());
+    return DQNX_OK;
+}
+
+constexpr int FWD_SPLIT_T = 64, FWD_SPLIT_KT = 64;
+int fwd_split_ksplit(int M, int N, int K, int nprob, int n_cu, int* kchunk) {
+    const int tiles = ((N + FWD_SPLIT_T - 1) / FWD_SPLIT_T) * ((M + FWD_SPLIT_T - 1) / FWD_SPLIT_T) * nprob;
+    const int Kpad = (K + 3) & ~3;
+    // slabs: whole KT passes (a slab's last pass must not run into the next slab's K range)
+    int S = std::max(1, std::min(2 * n_cu / tiles, Kpad / (2 * FWD_SPLIT_KT)));
+    int kc = (Kpad + S - 1) / S;
+    kc = (kc + FWD_SPLIT_KT - 1) / FWD_SPLIT_KT * FWD_SPLIT_KT;
+    S = (Kpad + kc - 1) / kc;
+    *kchunk = kc;
+    return S;
+}
+
+int launch_linear_fwd_split(const FwdArgs& args, int nprob, int act, bool vecb, hipStream_t s) {
+    FwdArgs a2 = args;
+    a2.nprob = nprob;
+    constexpr int T = FWD_SPLIT_T, KT = FWD_SPLIT_KT;
+    const int tiles = ((a2.N + T - 1) / T) * ((a2.M + T - 1) / T) * nprob;
+    const dim3 grid(tiles * a2.ksplit);
+    if (act == DQNX_ACT_RELU) {
+        if (vecb) hipLaunchKernelGGL((k_linear_fwd_big<DQNX_ACT_RELU, true, T, T, 2, KT>), grid, dim3(256), 0, s, a2);
+        else hipLaunchKernelGGL((k_linear_fwd_big<DQNX_ACT_RELU, false, T, T, 2, KT>), grid, dim3(256), 0, s, a2);
+    } else {
+        if (vecb) hipLaunchKernelGGL((k_linear_fwd_big<DQNX_ACT_ELU, true, T, T, 2, KT>), grid, dim3(256), 0, s, a2);
+        else hipLaunchKernelGGL((k_linear_fwd_big<DQNX_ACT_ELU, false, T, T, 2, KT>), grid, dim3(256), 0, s, a2);
+    }
     DQNX_HIP_CHECK(hipGetLastError());
     return DQNX_OK;
 }

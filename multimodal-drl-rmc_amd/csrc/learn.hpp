@@ -583,6 +583,78 @@ struct ConvPermArgs {
 int launch_conv_perm(const ConvPermArgs& a, hipStream_t s);
 int launch_unflatten_tiled(const UnflattenArgs& a, hipStream_t s);
 
+// ---- micro-CNN plan (micro.hip): the reference HEAD net's convs on its small micro grid
+//      (TwoStreamHybridNetwork, R:env/dqn_config.py:66-143: 3x3 convs, padding 1, ELU) with the
+//      whole per-sample activations on chip -- no column matrices, no flatten / col2im launches ----
+constexpr int MICRO_MAX_CONV = 3;
+struct MicroConv {
+    int Ci, Hi, Wi, Co, Ho, Wo, sh, sw;
+    int64_t woff;              // flat offset of W [Co][Ci][3][3] (the bias follows)
+    const float* wp[2];        // l >= 1: [Co][9][Ci] copies of the online / target W (k_conv_perm mode 0)
+    const float* wT;           // l >= 1: [Ci][9][Co] copy of the online W (mode 1, data gradient)
+    int cs;                    // LDS floats per pixel of this conv's output image (Co + 8: b128 reads conflict-free)
+    int lds;                   // LDS float offset of this conv's output images [S][Ho*Wo][cs]
+    float* hc;                 // l < nc - 1: stream-0 output (ELU applied), NHWC [Bl][Ho*Wo][Co]
+    float* dz;                 // stream-0 dZ of this conv's output (ELU' applied), NHWC [Bl][Ho*Wo][Co]
+};
+struct MicroFwdArgs {
+    MicroConv c[MICRO_MAX_CONV];
+    int nc, Bl, S, groups;     // samples per workgroup, workgroups per stream
+    int nstreams, stream_of[3];
+    const float* params;
+    const float* tparams;
+    const float* ring_obs;
+    const float* ring_next;
+    int ring_stride, macro_len;
+    const int32_t* phys;
+    float* F[3];               // per grid slice: [Bl][strideF] = cat(flatten_CHW(last conv), macro), zero padded
+    int strideF, flat_cols;
+    int x0;                    // LDS float offset of the input images [S][Ci*Hi*Wi] (CHW, as in the ring row)
+    int zero;                  // LDS float offset of 16 zeros (out-of-range taps read them)
+    int lds_floats;
+};
+struct MicroDxArgs {           // data gradients, last conv down to conv 2's input (stream 0)
+    MicroConv c[MICRO_MAX_CONV];
+    int nc, Bl, S, groups;
+    const float* dF;           // [Bl][ldf] CHW-flatten dZ of the last conv (ELU' applied by the dense dx role)
+    int ldf;
+    int lds_d[MICRO_MAX_CONV]; // LDS float offset of each conv's dZ images [S][Ho*Wo][c.cs]
+    int zero;
+    int lds_floats;
+    int wasg[MICRO_MAX_CONV][4];   // per level, per wave: sub-pixel phase | first tile << 4 | tiles << 12
+};
+struct MicroDwLayer {
+    int Ci, Hi, Wi, Co, Ho, Wo, sh, sw;
+    const float* D;            // dZ NHWC [Bl][Ho*Wo][Co] (stream 0)
+    const float* X;            // input NHWC [Bl][Hi*Wi][Ci] (l >= 1), null for conv 1 (CHW ring rows)
+    float* partial;            // [slices][Co*Ci*9 + Co], torch order [co][ci][i][j] then the bias
+    int64_t pstride;
+    int spw, slices, wg0;      // samples per slice, slices, first workgroup of this conv
+    int G;                     // samples per LDS stage (the next stage's loads in flight)
+    int skip;                  // tuning builds only: workgroups of this conv return at once (timing)
+    int nct;                   // column tiles: Ci/16 ci tiles (l >= 1), ceil(Ci*9/16) (conv 1, torch column order)
+    int wo_mul;                // q / Wo == (q * wo_mul) >> 16 for every pixel q < Ho*Wo + 4 (host-checked)
+};
+struct MicroDwArgs {
+    MicroDwLayer L[MICRO_MAX_CONV];
+    int nc, Bl, wgs;
+    const float* ring_obs;     // conv 1 input: the micro grid of the gathered obs rows
+    const int32_t* phys;
+    int ring_stride, macro_len;
+    int lds_floats;
+    int64_t* stamps;           // diagnostic builds (-DDQNX_STAMPS): slots 24..39 (conv 1 workgroup 0)
+};
+// plans (host): false if the net is outside what the micro kernels implement
+bool micro_plan(const MicroConv* convs, int nc, int Bl, int nstreams, int n_cu, int* S, int* lds_floats);
+bool micro_dx_plan(const MicroConv* convs, int nc, int Bl, int* S, int* lds_d, int* lds_floats);
+void micro_dx_waves(MicroDxArgs& a);   // fills wasg (after micro_dx_plan accepted the net)
+int micro_dw_plan(MicroDwArgs& a, int n_cu);
+int micro_fwd_layout(MicroConv* c, int nc, int S, int* x0, int* zero);        // sets c[l].lds; LDS floats
+int micro_dx_layout(const MicroConv* c, int nc, int S, int* lds_d, int* zero); // LDS floats   // fills spw / slices / wg0 / cs / lds; returns slices per conv via a
+int launch_micro_fwd(const MicroFwdArgs& a, hipStream_t s);
+int launch_micro_dx(const MicroDxArgs& a, hipStream_t s);
+int launch_micro_dw(const MicroDwArgs& a, hipStream_t s);
+
 int launch_im2col(const Im2colArgs& a, hipStream_t s);
 int launch_flatten_concat(const FlattenArgs& a, hipStream_t s);
 int launch_unflatten(const UnflattenArgs& a, hipStream_t s);
@@ -597,6 +669,10 @@ int launch_linear_fwd(const FwdArgs& args, int nprob, int act, bool vecb, hipStr
 constexpr int FWD_BIG_BM = 128, FWD_BIG_BN = 128, FWD_BIG_KT = 32;
 int fwd_big_ksplit(int M, int N, int K, int nprob, int64_t partial_floats, int* kchunk);
 int launch_linear_fwd_big(const FwdArgs& args, int nprob, int act, bool vecb, hipStream_t s);
+// conv nets' dense 1 (M = Bl rows per stream, K = F): 64 x 64 tiles split over K into slabs
+// (about two workgroups per CU), reduced in slab order by launch_linear_fwd_reduce
+int fwd_split_ksplit(int M, int N, int K, int nprob, int n_cu, int* kchunk);
+int launch_linear_fwd_split(const FwdArgs& args, int nprob, int act, bool vecb, hipStream_t s);
 int launch_linear_fwd_reduce(const FwdArgs& args, int nprob, int act, hipStream_t s);
 int conv_dx_big_tiles(int Bl, int in);
 int conv_dw_big_tiles(int in, int out);

@@ -72,6 +72,16 @@ def test_gpu_hybrid_learn_matches_oracle(algo, batch, cap, n_fill, seed):
             np.testing.assert_allclose(tg[k].cpu().numpy(), oracle.target[k].numpy(), atol=1e-5, rtol=0, err_msg=k)
 
 
+@pytest.mark.parametrize("micro", ["1", "0"])
+def test_gpu_hybrid_conv_routes_match_oracle(monkeypatch, micro):
+    """The (2,27,5) HEAD net's two conv routes against the oracle: the micro-CNN plan (micro.hip,
+    the default: every conv of every stream in one forward launch, the phase-split data gradients
+    and the sample-sliced weight gradients in two more) and the per-layer explicit plan
+    (DQNX_MICRO_CNN=0: im2col + GEMM, col2im).  PER at a batch that is no multiple of anything."""
+    monkeypatch.setenv("DQNX_MICRO_CNN", micro)
+    test_gpu_hybrid_learn_matches_oracle("PerDuelingDoubleDQNAgent", 100, 1000, 700, 31)
+
+
 def test_gpu_hybrid_learn_golden():
     """Against the reference's own hybrid DuelingDouble steps (tests/golden/make_golden.py)."""
     E = _E()
