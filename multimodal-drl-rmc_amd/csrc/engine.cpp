@@ -1237,11 +1237,16 @@ SampleArgs uniform_sample_args(dqnx_engine* e, int32_t* idx, int32_t* phys) {
 // engine draws its own indices, the whole forward is one launch, and k fits the multi-pass sampler
 // body's LDS table.  The step's last launch (k_dw_adam16, or the slab plan's Adam pass) copies the
 // staged minibatch over the compute slot.
+// The micro-CNN plan's forward launch hosts it the same way (k_micro_fwd block 0, k <= 2048), and
+// its Adam / gradient-reduce launch copies the staged minibatch.
 bool inlaunch_prefetch_ok(const dqnx_engine* e, int flags) {
     if (tuning_flag("DQNX_PF_SIDE")) return false;   // measurements: the side-stream pipeline instead
-    return e->bwd_plan == 2 && e->cfg.algo != DQNX_ALGO_PER_DOUBLE && !(flags & DQNX_STEP_GIVEN_INDICES) &&
-           e->Bs <= FWD_SAMPLE_MAX_K && e->fsplit <= 1;
+    if (e->cfg.algo == DQNX_ALGO_PER_DOUBLE || (flags & DQNX_STEP_GIVEN_INDICES)) return false;
+    if (e->bwd_plan == 2) return e->Bs <= FWD_SAMPLE_MAX_K && e->fsplit <= 1;
+    return e->bwd_plan == 0 && e->micro && e->Bs <= MICRO_SAMPLE_MAX_K;
 }
+// the fused plan's blocked weight copies need a rebuild launch before the next step
+static bool relayout_due(const dqnx_engine* e) { return e->bwd_plan == 2 && e->wblk_dirty; }
 
 std::vector<KStep> build_learn_steps(dqnx_engine* e, int key) {
     const int flags = key & 0x3f;
@@ -1450,6 +1455,12 @@ std::vector<KStep> build_learn_steps(dqnx_engine* e, int key) {
         ma.x0 = x0;
         ma.zero = zero;
         ma.lds_floats = e->micro_lds;
+        if (key & KEY_SAMPLE_NEXT) {   // + the next step's minibatch into the staging slot (in-launch prefetch)
+            ma.samp_on = 1;
+            ma.samp = uniform_sample_args(e, at<int32_t>(e, e->off[DQNX_BUF_BATCH_IDX]) + (size_t)e->Bg,
+                                          at<int32_t>(e, e->ws_phys) + (size_t)e->Bl);
+            ma.samp.stamps = nullptr;
+        }
         double flops = 0, bytes = 0;
         for (int l = 0; l < NC; l++) {
             const ConvPlan& cp = np.conv[l];
@@ -1458,7 +1469,7 @@ std::vector<KStep> build_learn_steps(dqnx_engine* e, int key) {
         }
         bytes += 4.0 * nstreams * Bl * (np.conv[0].Ci * np.conv[0].Hi * np.conv[0].Wi + np.strideF);
         KStep k;
-        k.name = "micro_fwd";
+        k.name = ma.samp_on ? "micro_fwd+sample" : "micro_fwd";
         k.flops = flops;
         k.bytes = bytes;
         k.run = [=](hipStream_t s) { return launch_micro_fwd(ma, s); };
@@ -1986,8 +1997,24 @@ std::vector<KStep> build_learn_steps(dqnx_engine* e, int key) {
         }
     }
 
-    // 5. gradient reduction + Adam (+ soft update)
-    ks.push_back(adam_kstep(e, flags));
+    // 5. gradient reduction + Adam (+ soft update); with the in-launch prefetch its extra workgroup
+    //    copies the staged minibatch over the compute slot (every reader of slot 0 ran before)
+    if (key & KEY_SAMPLE_NEXT) {
+        AdamArgs aa;
+        KStep k = adam_kstep(e, flags, &aa);
+        aa.pf_idx_src = at<int32_t>(e, e->off[DQNX_BUF_BATCH_IDX]) + (size_t)e->Bg;
+        aa.pf_idx_dst = idx;
+        aa.pf_nidx = e->Bg;
+        aa.pf_phys_src = at<int32_t>(e, e->ws_phys) + (size_t)e->Bl;
+        aa.pf_phys_dst = phys;
+        aa.pf_nphys = e->Bl;
+        aa.mtc = nullptr;   // the forward's sampler body draws from the MT state itself
+        aa.mtc_blocks = 0;
+        k.run = [=](hipStream_t s) { return launch_adam(aa, s); };
+        ks.push_back(k);
+    } else {
+        ks.push_back(adam_kstep(e, flags));
+    }
     } else {
     // 4. dZ of levels below L-1 (deeper MLPs only; the head kernel produced dZ_L and dZ_{L-1})
     for (int l = L - 2; l >= 1; l--) {
@@ -2729,7 +2756,7 @@ static int enqueue_relayout(dqnx_engine* e, hipStream_t s) {
 }
 
 static int inlaunch_prologue(dqnx_engine* e, int base, hipStream_t s) {
-    const int key0 = base | (e->wblk_dirty ? KEY_RELAYOUT : 0);
+    const int key0 = base | (relayout_due(e) ? KEY_RELAYOUT : 0);
     const std::vector<KStep>& ks0 = steps_for(e, key0);
     int rc = run_graphed(e, 0x80000 | key0, s, [&](hipStream_t cs) { return enqueue_range(ks0, 0, 1, cs); });
     if (rc) return rc;
@@ -2748,7 +2775,7 @@ static int learn_step_inlaunch(dqnx_engine* e, int base, bool prefetch, hipStrea
     if (!e->pf_valid) {   // prologue: this step's minibatch by the sampler launch (+ relayout if dirty)
         rc = inlaunch_prologue(e, base, s);
         if (rc) return rc;
-    } else if (e->wblk_dirty) {   // weights changed outside a blocked-copy-keeping update
+    } else if (relayout_due(e)) {   // weights changed outside a blocked-copy-keeping update
         rc = enqueue_relayout(e, s);
         if (rc) return rc;
         e->wblk_dirty = false;
@@ -2783,7 +2810,7 @@ int dqnx_learn_step(dqnx_engine* e, int32_t flags, void* stream) {
     // (in-launch prefetch, same stream, no events); where it cannot (k past the multi-pass
     // sampler, slab plan), nothing is drawn ahead.  Per-layer plan: a side-stream pipeline.
     const int base = flags & (DQNX_STEP_SOFT_UPDATE | DQNX_STEP_GIVEN_INDICES | DQNX_STEP_GRADS_ONLY);
-    const bool inl = e->bwd_plan == 2 && inlaunch_prefetch_ok(e, base);
+    const bool inl = inlaunch_prefetch_ok(e, base);
     const bool prefetch = (flags & DQNX_STEP_PREFETCH) && !(flags & DQNX_STEP_GIVEN_INDICES) &&
                           e->cfg.algo != DQNX_ALGO_PER_DOUBLE && (e->bwd_plan != 2 || inl);
     if (e->ring_size < e->Bs && !(flags & DQNX_STEP_GIVEN_INDICES) && !e->pf_valid)
@@ -2848,7 +2875,7 @@ int dqnx_learn_steps(dqnx_engine* e, int32_t flags, int32_t count, void* stream)
         return set_error(DQNX_EINVAL, "learn_steps: flags may only hold DQNX_STEP_SOFT_UPDATE");
     hipStream_t s = (hipStream_t)stream;
     const int base = flags & DQNX_STEP_SOFT_UPDATE;
-    if (e->pf_valid || !(e->bwd_plan == 2 && inlaunch_prefetch_ok(e, base))) {
+    if (e->pf_valid || !inlaunch_prefetch_ok(e, base)) {
         for (int i = 0; i < count; i++) {
             rc = dqnx_learn_step(e, base, stream);
             if (rc) return rc;
@@ -2857,7 +2884,7 @@ int dqnx_learn_steps(dqnx_engine* e, int32_t flags, int32_t count, void* stream)
     }
     if (e->ring_size < e->Bs)
         return set_error(DQNX_EINVAL, "Sample larger than population: %lld < %d", (long long)e->ring_size, e->Bs);
-    const int first = base | (e->wblk_dirty ? KEY_RELAYOUT : 0);
+    const int first = base | (relayout_due(e) ? KEY_RELAYOUT : 0);
     rc = run_graphed(e, 0x40000000 | (count << 12) | first, s, [&](hipStream_t cs) {
         const std::vector<KStep>& k0 = steps_for(e, first);   // slot 0: sampler (+ relayout) + step
         int r = enqueue_range(k0, 0, 1, cs);
@@ -2879,7 +2906,7 @@ int dqnx_learn_steps(dqnx_engine* e, int32_t flags, int32_t count, void* stream)
 // the last launch draws the next minibatch (into slot 1; timing runs leave the state stale).
 static int timing_key(const dqnx_engine* e, int32_t flags) {
     const int base = flags & 7;
-    if ((flags & DQNX_STEP_PREFETCH) && e->bwd_plan == 2 && inlaunch_prefetch_ok(e, base)) return base | KEY_SAMPLE_NEXT;
+    if ((flags & DQNX_STEP_PREFETCH) && inlaunch_prefetch_ok(e, base)) return base | KEY_SAMPLE_NEXT;
     return base;
 }
 
@@ -2887,7 +2914,7 @@ int dqnx_prefetch_begin(dqnx_engine* e, int32_t flags, void* stream) {
     int rc = check_bound(e);
     if (rc) return rc;
     const int base = flags & (DQNX_STEP_SOFT_UPDATE | DQNX_STEP_GRADS_ONLY);
-    if (e->pf_valid || e->cfg.algo == DQNX_ALGO_PER_DOUBLE || !(e->bwd_plan == 2 && inlaunch_prefetch_ok(e, base)))
+    if (e->pf_valid || e->cfg.algo == DQNX_ALGO_PER_DOUBLE || !inlaunch_prefetch_ok(e, base))
         return DQNX_OK;   // a draw is pending already, or this configuration does not draw ahead
     if (e->ring_size < e->Bs)
         return set_error(DQNX_EINVAL, "Sample larger than population: %lld < %d", (long long)e->ring_size, e->Bs);

@@ -728,6 +728,17 @@ __global__ __launch_bounds__(256) void k_adam(AdamArgs a) {
             const int64_t ps = sg.pstride;
             gsum = pp[0];
             int u = 1;
+            if (sg.S >= ADAM_WIDE_MIN_S) {   // k_adam4's wide order: 8 strided partials, then its xor butterfly
+                float part[8];
+#pragma unroll
+                for (int j = 0; j < 8; j++) {
+                    float t = pp[(int64_t)j * ps];
+                    for (int w = j + 8; w < sg.S; w += 8) t += pp[(int64_t)w * ps];
+                    part[j] = t;
+                }
+                gsum = ((part[0] + part[4]) + (part[2] + part[6])) + ((part[1] + part[5]) + (part[3] + part[7]));
+                u = sg.S;
+            }
             for (; u + 16 <= sg.S; u += 16) {
                 float pv[16];
 #pragma unroll
@@ -793,32 +804,133 @@ __global__ __launch_bounds__(256) void k_adam(AdamArgs a) {
 // (launch_adam checks); 4 consecutive elements per thread per pass, so a thread keeps 4x the
 // bytes in flight of the scalar kernel (the (4,84,84) variant updates 29 M parameters).  The
 // same per-element arithmetic, the same fixed slab order.
+//
+// Wide segments (a.wide_end > e0: the leading segments with many split-K slabs, i.e. the micro
+// CNN's conv weight gradients, 24..128 slabs at the HEAD net's B=256): ADAM_WIDE lanes share one
+// float4, lane j summing slabs j, j + ADAM_WIDE, ... in order, then a fixed xor butterfly over the
+// lanes (every lane ends with the same bits).  One round trip of slab loads instead of S / 16
+// dependent rounds: the slab sum of conv 2 (128 slabs) was the launch's critical path.
+static_assert(ADAM_WIDE == 8, "k_adam's scalar wide sum assumes 8 lanes");
+__device__ __forceinline__ void adam4_update(const AdamArgs& a, int64_t e, int nv, float4 g, float4 m, float4 v,
+                                             float4 p, float4 tg, float step_size, float bc2s, bool store_g) {
+    auto st = [&](float* base, const float4& x) {
+        if (nv == 4) {
+            *reinterpret_cast<float4*>(base + e) = x;
+            return;
+        }
+        base[e] = x.x;
+        if (nv > 1) base[e + 1] = x.y;
+        if (nv > 2) base[e + 2] = x.z;
+    };
+    if (store_g) st(a.grads, g);
+    if (a.mode == 0) return;
+    auto upd = [&](float& mk, float& vk, float& pk, float& tk, float gk) {
+        mk = fmaf(a.w1, gk - mk, mk);
+        vk = vk * a.beta2;
+        vk = vk + (a.c2 * gk) * gk;
+        const float denom = sqrtf(vk) / bc2s + a.eps;
+        pk = pk + (step_size * mk) / denom;
+        if (a.soft) tk = a.tau * pk + a.one_minus_tau * tk;
+    };
+    upd(m.x, v.x, p.x, tg.x, g.x);
+    upd(m.y, v.y, p.y, tg.y, g.y);
+    upd(m.z, v.z, p.z, tg.z, g.z);
+    upd(m.w, v.w, p.w, tg.w, g.w);
+    st(a.m, m);
+    st(a.v, v);
+    st(a.p, p);
+    if (a.soft) st(a.target, tg);
+}
+
+__device__ __forceinline__ AdamSegment adam_segment_of(const AdamArgs& a, int64_t e) {
+    // static-index selects (a kernel-argument array indexed by a per-lane value goes to scratch)
+    AdamSegment sg = a.seg[0];
+#pragma unroll
+    for (int q = 1; q < kMaxSeg; q++)
+        if (q < a.nseg && e >= a.seg[q].off) sg = a.seg[q];
+    return sg;
+}
+
 __global__ __launch_bounds__(256) void k_adam4(AdamArgs a) {
     if (adam_extra_wg(a)) return;   // the sampler-cache / staged-minibatch workgroups
     const int eb = (int)blockIdx.x - adam_extra_count(a);   // element block
     const int64_t P = a.n_params, P4 = (P + 3) >> 2;   // e0 is a multiple of 4 (launch_adam)
-    const int64_t stride = (int64_t)(gridDim.x - adam_extra_count(a)) * blockDim.x;
+    if (eb == 0) {
+        if (a.mode != 2 && threadIdx.x < 64 && a.loss_partial) {   // one wave, fixed order
+            float s = 0.f;
+            for (int j = threadIdx.x; j < a.n_loss_partial; j += 64) s += a.loss_partial[j];
+#pragma unroll
+            for (int o = 32; o >= 1; o >>= 1) s += __shfl_xor(s, o);
+            if (threadIdx.x == 0) {
+                const float loss = s / (float)a.batch_global;
+                a.grads[P] = loss;
+                a.ctrl->loss = loss;
+            }
+        }
+        if (a.mode == 2 && a.with_loss && threadIdx.x == 0) a.ctrl->loss = a.grads[P];
+    }
     float step_size = 0.f, bc2s = 1.f;
     if (a.mode != 0) {
         step_size = a.ctrl->adam_step_size;
         bc2s = a.ctrl->adam_bc2_sqrt;
     }
-    for (int64_t e4 = (a.e0 >> 2) + (int64_t)eb * blockDim.x + threadIdx.x; e4 < P4; e4 += stride) {
+    const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+    const int64_t w0 = a.e0 >> 2, w4 = a.wide_end > a.e0 ? ((a.wide_end - a.e0) >> 2) : 0;
+    const int wide_blocks = (int)((w4 * ADAM_WIDE + 255) / 256);
+    if (eb < wide_blocks) {   // ---- wide segments: ADAM_WIDE lanes per float4 ----
+        const int64_t gid = (int64_t)eb * 256 + threadIdx.x;
+        const int64_t e4 = w0 + gid / ADAM_WIDE;
+        const int j = (int)(gid % ADAM_WIDE);
+        const bool live = e4 < w0 + w4;
+        const int64_t e = (live ? e4 : w0) << 2;
+        float4 m = z4, v = z4, p = z4, tg = z4;
+        if (a.mode != 0 && j == 0 && live) {
+            m = ld4(a.m + e);
+            v = ld4(a.v + e);
+            p = ld4(a.p + e);
+            if (a.soft) tg = ld4(a.target + e);
+        }
+        const AdamSegment sg = adam_segment_of(a, e);
+        const float* q4 = sg.partial + (e - sg.off);
+        const int64_t ps = sg.pstride;
+        float4 g = z4;
+        const int cnt = live && j < sg.S ? (sg.S - j + ADAM_WIDE - 1) / ADAM_WIDE : 0;   // slabs j, j + W, ...
+        for (int u0 = 0; u0 < cnt; u0 += 16) {
+            float4 pv[16];
+#pragma unroll
+            for (int q = 0; q < 16; q++) {   // addresses clamped to slab j: the loads stay unconditional
+                const int u = u0 + q < cnt ? u0 + q : 0;
+                pv[q] = ld4(q4 + (int64_t)(j + u * ADAM_WIDE) * ps);
+            }
+#pragma unroll
+            for (int q = 0; q < 16; q++) {
+                if (u0 + q >= cnt) break;
+                if (u0 + q == 0) {
+                    g = pv[q];
+                } else {
+                    g.x += pv[q].x; g.y += pv[q].y; g.z += pv[q].z; g.w += pv[q].w;
+                }
+            }
+        }
+#pragma unroll
+        for (int o = ADAM_WIDE / 2; o >= 1; o >>= 1) {   // (x + y == y + x: all lanes agree)
+            g.x += __shfl_xor(g.x, o);
+            g.y += __shfl_xor(g.y, o);
+            g.z += __shfl_xor(g.z, o);
+            g.w += __shfl_xor(g.w, o);
+        }
+        if (j == 0 && live) adam4_update(a, e, 4, g, m, v, p, tg, step_size, bc2s, true);
+        return;
+    }
+    const int nb = eb - wide_blocks;
+    const int64_t stride = (int64_t)(gridDim.x - adam_extra_count(a) - wide_blocks) * blockDim.x;
+    for (int64_t e4 = w0 + w4 + (int64_t)nb * blockDim.x + threadIdx.x; e4 < P4; e4 += stride) {
         const int64_t e = e4 << 2;
         const int nv = (int)min((int64_t)4, P - e);   // 4 except in the last vector
-        float4 m = make_float4(0.f, 0.f, 0.f, 0.f), v = m, p = m, tg = m, g = m;
+        float4 m = z4, v = z4, p = z4, tg = z4, g = z4;
         auto ld = [&](const float* base) {   // the last vector may be partial (no dynamic indexing)
             if (nv == 4) return ld4(base + e);
             return make_float4(base[e], nv > 1 ? base[e + 1] : 0.f, nv > 2 ? base[e + 2] : 0.f, 0.f);
-        };
-        auto st = [&](float* base, const float4& x) {
-            if (nv == 4) {
-                *reinterpret_cast<float4*>(base + e) = x;
-                return;
-            }
-            base[e] = x.x;
-            if (nv > 1) base[e + 1] = x.y;
-            if (nv > 2) base[e + 2] = x.z;
         };
         if (a.mode != 0) {
             m = ld(a.m);
@@ -829,15 +941,12 @@ __global__ __launch_bounds__(256) void k_adam4(AdamArgs a) {
         if (a.mode == 2) {
             g = ld(a.grads);
         } else {
-            AdamSegment sg = a.seg[0];
-#pragma unroll
-            for (int q = 1; q < kMaxSeg; q++)
-                if (q < a.nseg && e >= a.seg[q].off) sg = a.seg[q];
+            const AdamSegment sg = adam_segment_of(a, e);
             const float* pp = sg.partial + (e - sg.off) - e;   // ld() adds e back
             if (nv == 4) {
                 // slab 0, then 16 / 4 / 1 slabs per round trip, every load of a round unconditional
                 // (a conditional load would make the compiler wait for all of them before the
-                // first add); the conv nets' micro dW writes ~100 slabs, a dense layer 1
+                // first add)
                 const float* q4 = pp + e;
                 const int64_t ps = sg.pstride;
                 g = ld4(q4);
@@ -874,38 +983,9 @@ __global__ __launch_bounds__(256) void k_adam4(AdamArgs a) {
                     }
                 }
             }
-            st(a.grads, g);
         }
-        if (a.mode == 0) continue;
-        auto upd = [&](float& mk, float& vk, float& pk, float& tk, float gk) {
-            mk = fmaf(a.w1, gk - mk, mk);
-            vk = vk * a.beta2;
-            vk = vk + (a.c2 * gk) * gk;
-            const float denom = sqrtf(vk) / bc2s + a.eps;
-            pk = pk + (step_size * mk) / denom;
-            if (a.soft) tk = a.tau * pk + a.one_minus_tau * tk;
-        };
-        upd(m.x, v.x, p.x, tg.x, g.x);
-        upd(m.y, v.y, p.y, tg.y, g.y);
-        upd(m.z, v.z, p.z, tg.z, g.z);
-        upd(m.w, v.w, p.w, tg.w, g.w);
-        st(a.m, m);
-        st(a.v, v);
-        st(a.p, p);
-        if (a.soft) st(a.target, tg);
+        adam4_update(a, e, nv, g, m, v, p, tg, step_size, bc2s, a.mode != 2);
     }
-    if (a.mode != 2 && eb == 0 && threadIdx.x < 64 && a.loss_partial) {   // one wave, fixed order
-        float s = 0.f;
-        for (int j = threadIdx.x; j < a.n_loss_partial; j += 64) s += a.loss_partial[j];
-#pragma unroll
-        for (int o = 32; o >= 1; o >>= 1) s += __shfl_xor(s, o);
-        if (threadIdx.x == 0) {
-            const float loss = s / (float)a.batch_global;
-            a.grads[P] = loss;
-            a.ctrl->loss = loss;
-        }
-    }
-    if (a.mode == 2 && a.with_loss && eb == 0 && threadIdx.x == 0) a.ctrl->loss = a.grads[P];
 }
 
 // =====================================================================================
@@ -1340,12 +1420,25 @@ static bool adam_vec_ok(const AdamArgs& a) {
     return true;
 }
 
-int launch_adam(const AdamArgs& a, hipStream_t s) {
+int launch_adam(const AdamArgs& a_in, hipStream_t s) {
+    AdamArgs a = a_in;
     const bool vec = adam_vec_ok(a);
-    const int64_t items = vec ? (a.n_params - a.e0 + 3) / 4 : a.n_params - a.e0;
+    // the wide prefix (k_adam4): the leading segments of the range with >= ADAM_WIDE_MIN_S slabs
+    a.wide_end = 0;
+    if (vec && a.mode != 2) {
+        int q = 0;
+        while (q + 1 < a.nseg && a.seg[q + 1].off <= a.e0) q++;
+        int64_t end = a.e0;
+        for (; q < a.nseg && a.seg[q].S >= ADAM_WIDE_MIN_S; q++) end = q + 1 < a.nseg ? a.seg[q + 1].off : a.n_params;
+        if (end > a.n_params) end = a.n_params;
+        if (end > a.e0 && end % 4 == 0) a.wide_end = end;
+    }
+    const int64_t wide4 = a.wide_end > a.e0 ? (a.wide_end - a.e0) / 4 : 0;
+    const int64_t items = vec ? (a.n_params - a.e0 + 3) / 4 - wide4 : a.n_params - a.e0;
     int blocks = (int)((items + 255) / 256);
     if (blocks > 2048) blocks = 2048;
     if (blocks < 1) blocks = 1;
+    blocks += (int)((wide4 * 8 + 255) / 256);   // ADAM_WIDE lanes per wide float4
     if (a.mtc) blocks++;   // + the sampler-cache workgroup
     if (a.pf_nidx > 0) blocks++;   // + the staged-minibatch copy
     if (vec) hipLaunchKernelGGL(k_adam4, dim3(blocks), dim3(256), 0, s, a);

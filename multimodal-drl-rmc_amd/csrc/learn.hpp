@@ -124,6 +124,8 @@ struct HeadArgs {
 };
 
 constexpr int kMaxSeg = 10;
+constexpr int ADAM_WIDE = 8;          // k_adam4: lanes per float4 of a wide segment
+constexpr int ADAM_WIDE_MIN_S = 24;   // k_adam4: segments with this many split-K slabs or more take the wide path
 constexpr int kAdamTable = 1 << 20;   // precomputed Adam bias corrections (steps 1..2^20)
 struct AdamSegment {
     int64_t off;           // first flat element of the segment
@@ -138,6 +140,7 @@ struct AdamArgs {
     int soft;
     int64_t n_params;      // elements [e0, n_params) are processed (e0 = 0 except for DP buckets)
     int64_t e0;
+    int64_t wide_end;      // k_adam4: [e0, wide_end) = segments summed by ADAM_WIDE lanes per float4 (launch_adam)
     int with_loss;         // the range ends at the loss slot grads[n_params] (mode 2: publish it)
     float* p;
     float* m;
@@ -458,6 +461,7 @@ struct FusedFwdArgs {
 //   3: k <= FWD_SAMPLE_MAX_K, ONE pass of 9 blocks into 16384 slots (150 KB: one workgroup per CU,
 //      only when the forward's grid leaves a CU idle), so k = 4096 takes one pass instead of three
 constexpr int FWD_SAMPLE_MAX_K = 4608;
+constexpr int MICRO_SAMPLE_MAX_K = 2048;   // k_micro_fwd's sampler workgroup (256 threads, 4096 slots)
 __host__ __device__ constexpr int fwd_sample_ahead(int shape) { return shape == 3 ? 8 : 2; }
 __host__ __device__ constexpr int fwd_sample_hs(int shape) { return shape == 1 ? 4096 : shape == 2 ? 8192 : 16384; }
 // LDS of that workgroup: the sampler's MT blocks / scan words, then the hash table (8-byte slots)
@@ -612,6 +616,10 @@ struct MicroFwdArgs {
     int x0;                    // LDS float offset of the input images [S][Ci*Hi*Wi] (CHW, as in the ring row)
     int zero;                  // LDS float offset of 16 zeros (out-of-range taps read them)
     int lds_floats;
+    // in-launch prefetch: block 0 (dispatched first) draws the NEXT step's minibatch into the
+    // staging slot with the 256-thread sampler body (k <= 2048: 3-block passes into 4096 LDS slots)
+    int samp_on;
+    SampleArgs samp;
 };
 struct MicroDxArgs {           // data gradients, last conv down to conv 2's input (stream 0)
     MicroConv c[MICRO_MAX_CONV];

@@ -24,6 +24,7 @@
 // Every contraction is v_mfma_f32_16x16x4_f32 (an exact fp32 fmaf chain, MI355X_MICROARCH.md §F32);
 // sums run in a fixed order (no atomics): results are bitwise reproducible run to run.
 #include "learn.hpp"
+#include "sample_body.hpp"
 
 namespace dqnx {
 
@@ -553,11 +554,26 @@ __device__ __forceinline__ void micro_conv(const MicroFwdArgs& a, const MicroCon
     }
 }
 
+// the sampler workgroup's LDS: the 3-block MT window, then a 4096-slot (value, position) table
+constexpr int MICRO_SAMP_AH = 2, MICRO_SAMP_HS = 4096;
+constexpr int MICRO_SAMP_TAB = ((int)sizeof(SampleLdsBase<MTH, MICRO_SAMP_AH>) + 63) / 64 * 64;
+constexpr int MICRO_SAMP_LDS = MICRO_SAMP_TAB + 8 * MICRO_SAMP_HS;
+
 template <int NC>
 __global__ __launch_bounds__(MTH, 3) void k_micro_fwd(MicroFwdArgs a) {   // 3 waves per SIMD: 3 workgroups per CU
     extern __shared__ __attribute__((aligned(16))) float lds[];
+    if (a.samp_on && blockIdx.x == 0) {
+        // in-launch prefetch: the next step's random.sample (R:dqn/replay_memory.py:38-39) into the
+        // staging slot.  It reads only the MT state and the ring's size / write pointer, which no
+        // kernel of this step writes (push / rng_set are refused while a draw is pending).
+        sample_uniform_body<MTH, MICRO_SAMP_HS, MICRO_SAMP_AH>(
+            a.samp, *reinterpret_cast<SampleLdsBase<MTH, MICRO_SAMP_AH>*>(lds),
+            reinterpret_cast<unsigned long long*>(reinterpret_cast<char*>(lds) + MICRO_SAMP_TAB));
+        return;
+    }
+    const int bid = (int)blockIdx.x - (a.samp_on ? 1 : 0);
     const int tid = threadIdx.x, wid = tid >> 6;
-    const int z = blockIdx.x / a.groups, grp = blockIdx.x - z * a.groups;
+    const int z = bid / a.groups, grp = bid - z * a.groups;
     const int s = a.stream_of[z];
     const int tgt = s == 2 ? 1 : 0;
     const bool keep = s == 0;
@@ -619,8 +635,11 @@ __global__ __launch_bounds__(MTH, 3) void k_micro_fwd(MicroFwdArgs a) {   // 3 w
 }
 
 int launch_micro_fwd(const MicroFwdArgs& a, hipStream_t s) {
-    const dim3 grid(a.nstreams * a.groups);
-    const size_t lds = (size_t)a.lds_floats * 4;
+    if (a.samp_on && a.samp.k > MICRO_SAMPLE_MAX_K)
+        return set_error(DQNX_EUNSUPPORTED, "micro forward sampler workgroup: k <= %d", MICRO_SAMPLE_MAX_K);
+    const dim3 grid(a.nstreams * a.groups + (a.samp_on ? 1 : 0));
+    size_t lds = (size_t)a.lds_floats * 4;
+    if (a.samp_on && lds < (size_t)MICRO_SAMP_LDS) lds = MICRO_SAMP_LDS;
     if (a.nc == 3) hipLaunchKernelGGL(k_micro_fwd<3>, grid, dim3(MTH), lds, s, a);
     else hipLaunchKernelGGL(k_micro_fwd<2>, grid, dim3(MTH), lds, s, a);
     DQNX_HIP_CHECK(hipGetLastError());

@@ -188,3 +188,27 @@ def test_gpu_hybrid84_implicit_convs_all_algorithms(algo, batch, seed):
         # weights at 1e-5, except (capped, counted) entries whose gradient differed by > 0.1 %
         # (Adam's lr * g / |g| step, see test_gpu_engine.compare_state)
         compare_state(oracle, eng, loose=loose)
+
+
+@pytest.mark.parametrize("algo,batch,grads_only", [("DuelingDoubleDQNAgent", 256, False), ("DQNAgent", 100, False),
+                                                   ("DuelingDoubleDQNAgent", 256, True)])
+def test_gpu_hybrid_inlaunch_prefetch_bit_identical(algo, batch, grads_only):
+    """The HEAD net's micro-CNN plan under DQNX_STEP_PREFETCH: k_micro_fwd's block 0 draws step
+    t+1's minibatch into the staging slot and the step's last launch (Adam, or the gradient reduce
+    of a GRADS_ONLY step) copies it over the compute slot.  Bitwise equal to sequential steps: Q,
+    gradients, weights, the sampled indices and the RNG state."""
+    o1, e1 = make_hybrid_pair(algo, batch, 3000, 2500, 61)
+    o2, e2 = make_hybrid_pair(algo, batch, 3000, 2500, 61)
+    for i in range(5):
+        e1.learn_step(soft_update=not grads_only, grads_only=grads_only)
+        e2.learn_step(soft_update=not grads_only, grads_only=grads_only, prefetch=i < 4)
+        if grads_only:
+            e1.apply_grads(soft_update=True)
+            e2.apply_grads(soft_update=True)
+    torch.cuda.synchronize()
+    e1.check_device_error()
+    e2.check_device_error()
+    assert torch.equal(e1.batch_idx, e2.batch_idx)
+    assert torch.equal(e1.q, e2.q) and torch.equal(e1.grads, e2.grads)
+    assert torch.equal(e1.params, e2.params) and torch.equal(e1.target_params, e2.target_params)
+    assert np.array_equal(e1.get_rng(0), e2.get_rng(0))
