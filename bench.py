@@ -458,14 +458,17 @@ def roofline_of(args, kern, batch_tag):
     hbm_ach = by / sec / 1e9
     mfma_frac = mfma_ach / peak_mfma
     hbm_frac = hbm_ach / PEAK_HBM_GBS
-    # the bounding roof by the kernel's intensity, taken over the MEASURED HBM traffic when the
-    # PMC passes exist (algorithmic bytes otherwise), against the dtype's ridge point
     ridge = peak_mfma * 1e12 / (PEAK_HBM_GBS * 1e9)
     intensity = fl / (traffic or by) if (traffic or by) else 0.0
+    # the bound from the measured limiter: a kernel is HBM-bound only when its MEASURED traffic (PMC,
+    # else its algorithmic bytes) streams at >= half the HBM peak or it does no math; otherwise its
+    # roof is the MFMA peak of the compute dtype, whatever bounds it below that (LDS, L2->VGPR, latency:
+    # DESIGN.md section 3), and `frac` says how far below it runs
+    hbm_measured_frac = ((traffic or by) / sec / 1e9) / PEAK_HBM_GBS
     common = {"traffic": traffic, "kernel": nm, "avg_us": us, "algorithmic_flops": fl, "algorithmic_bytes": by,
-              "mfma_frac": mfma_frac, "hbm_frac": hbm_frac, "intensity_flop_per_byte": intensity,
-              "ridge_flop_per_byte": ridge}
-    if fl > 0 and intensity > ridge:
+              "mfma_frac": mfma_frac, "hbm_frac": hbm_frac, "hbm_measured_frac": hbm_measured_frac,
+              "intensity_flop_per_byte": intensity, "ridge_flop_per_byte": ridge}
+    if fl > 0 and hbm_measured_frac < 0.5:
         return dict({"bound": "mfma", "achieved": mfma_ach, "peak": peak_mfma, "unit": "TFLOP/s",
                      "frac": mfma_frac}, **common)
     return dict({"bound": "hbm", "achieved": hbm_ach, "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": hbm_frac},
@@ -473,6 +476,35 @@ def roofline_of(args, kern, batch_tag):
 
 
 ALLREDUCE_EST_US = 20.0   # assumed RCCL all-reduce of the 428 KB MLP-284 gradient over 8 xGMI-linked GPUs
+
+
+def graphed_shard_steps(eng, args, steps, device, prefetch=None):
+    """`steps` GRADS_ONLY shard steps (+ apply_grads) replayed --dp-graph-steps per captured graph, as
+    GraphedDPStep runs them under torchrun (the collective left out).  Returns (seconds, steps per graph)."""
+    prefetch = args.prefetch if prefetch is None else prefetch
+    gs = max(1, args.dp_graph_steps)
+    eng.set_graphs(False)
+    if prefetch:
+        eng.prefetch_prologue()
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        for _ in range(gs):
+            eng.learn_step(grads_only=True, prefetch=prefetch)
+            eng.apply_grads(soft_update=True)
+    for _ in range(max(2, args.warmup // gs)):
+        g.replay()
+    n = max(1, steps // gs)
+    el = timed_steps(lambda: g.replay(), n, None, device)
+    if prefetch:   # the replays ran on this stream: dqnx_rng_get / the next step wait on it
+        C.check(C.lib().dqnx_prefetch_stream(eng.h, eng.stream()), "prefetch_stream")
+        eng.learn_step(grads_only=True)   # consume the pending draw
+        eng.apply_grads(soft_update=True)
+    torch.cuda.synchronize()
+    eng.check_device_error()
+    eng.set_graphs(args.graphs)
+    del g
+    return el * steps / (n * gs), gs
 
 
 def single_gpu_extras(args, spec, device):
@@ -498,8 +530,11 @@ def single_gpu_extras(args, spec, device):
         eng.apply_grads(soft_update=True)
     for _ in range(args.warmup):
         shard_step()
-    el = timed_steps(shard_step, steps, None, device)
+    el_eager = timed_steps(shard_step, steps, None, device)
     shard_step(prefetch=False)   # consume the pending draw
+    # the way the N > 1 bench runs it: --dp-graph-steps shard steps per replayed graph (GraphedDPStep
+    # without the collective)
+    el, gs = graphed_shard_steps(eng, args, steps, device)
     seq = {}
     if args.prefetch:   # the same shard step with the sampler launch on the critical path
         for _ in range(args.warmup):
@@ -511,14 +546,16 @@ def single_gpu_extras(args, spec, device):
     kpf = kernel_times(eng, C.STEP_GRADS_ONLY | C.STEP_PREFETCH, count=50, reps=3) if args.prefetch else []
     out["projection_w8"] = dict({
         "rows_per_rank": Bg // W, "global_batch": Bg, "shard_step_us": el / steps * 1e6,
+        "shard_step_us_eager": el_eager / steps * 1e6, "steps_per_graph": gs,
         "prefetch_sampling": args.prefetch,
         "global_sampling_us": samp,
         "tr_per_s_without_allreduce": Bg / (el / steps),
         "kernels": [{"kernel": k[0], "avg_us": k[1]} for k in ks],
         "kernels_prefetch": [{"kernel": k[0], "avg_us": k[1]} for k in kpf],
         "note": "rank 0 of world_size 8 on one GPU: 512-row shard + grad reduce + Adam/soft update, the global "
-                "4096-draw sampler inside the forward launch (prefetch) or as its own launch; add the RCCL "
-                "all-reduce of the 428 KB gradient for the 8-GPU step"}, **seq)
+                "4096-draw sampler inside the forward launch (prefetch) or as its own launch, replayed "
+                f"{gs} steps per captured graph like the N>1 bench (shard_step_us_eager: one host call per "
+                "launch); add the RCCL all-reduce of the 428 KB gradient for the 8-GPU step"}, **seq)
     # Amdahl bound of 8-GPU strong scaling at global 4096: the one-GPU step
     # over 8 x (the shard step + an all-reduce estimate).  The all-reduce term is an assumption
     # (RCCL ring over xGMI, 428 KB fp32 gradient: latency-dominated), not a measurement.
@@ -533,11 +570,83 @@ def single_gpu_extras(args, spec, device):
     return out
 
 
+def head_net_extra(args, device):
+    """The reference's HEAD net (TwoStreamHybridNetwork on the (2,27,5) grid + 14 macro features,
+    R:env/dqn_config.py:66-193, the net bin/train.sh trains), DuelingDouble fp32, B=256, in the same
+    learning loop as the headline (eager, in-launch prefetch), with its dominant kernel's roofline."""
+    import copy
+    a = copy.copy(args)
+    a.net, a.batch = "hybrid", 256
+    spec = make_spec(a)
+    eng = make_engine(a, spec, 256, 1, 0, device)
+    steps = max(args.steps, 100)
+    el, _ = run_learner(a, eng, 1, None, steps, args.warmup, None, device)
+    flags = C.STEP_SOFT_UPDATE | (C.STEP_PREFETCH if a.prefetch else 0)
+    ks = kernel_times(eng, flags, count=50, reps=3)
+    dom = max(ks, key=lambda k: k[1])
+    dom = kernel_times(eng, flags, count=100, reps=5, only={dom[0]})[0]
+    out = {"value": 256 * steps / el, "unit": "transitions/s", "ms_per_step": el / steps * 1e3, "batch": 256,
+           "net": net_name(a), "algo": a.algo, "dtype": "fp32",
+           "kernels": [{"kernel": k[0], "avg_us": (dom[1] if k[0] == dom[0] else k[1])} for k in ks],
+           "roofline": roofline_of(a, dom, 256)}
+    del eng
+    torch.cuda.empty_cache()
+    return out
+
+
+def c5_projection(args, device):
+    """configs[4] (PER + DuelingDouble, bf16 compute, global minibatch 8192): the one-GPU step, and
+    the rank-0 shard step of a world_size = 8 engine (1024 rows; the replicated O(B_global) PER
+    sampler and tree update included, the |delta| all-gather and gradient all-reduce not)."""
+    import copy
+    a = copy.copy(args)
+    a.algo, a.compute = "PerDuelingDoubleDQNAgent", "bf16"
+    spec = make_spec(a)
+    Bg, W = 8192, 8
+    steps = max(args.steps // 2, 50)
+    eng = make_engine(a, spec, Bg, 1, 0, device)
+    el1, _ = run_learner(a, eng, 1, None, steps, args.warmup, None, device)
+    del eng
+    torch.cuda.empty_cache()
+    eng = make_engine(a, spec, Bg, W, 0, device)
+
+    def shard_step():
+        eng.learn_step(grads_only=True)
+        eng.apply_grads(soft_update=True)   # Adam + the PER tree update of all 8192 |delta|
+    for _ in range(args.warmup):
+        shard_step()
+    el_eager = timed_steps(shard_step, steps, None, device)
+    el, gs = graphed_shard_steps(eng, a, steps, device, prefetch=False)
+    ks = kernel_times(eng, C.STEP_GRADS_ONLY, count=30, reps=3)
+    del eng
+    torch.cuda.empty_cache()
+    # (replayed graphs of the PER shard step measure ~3x slower than eager launches on ROCm 7.2, while
+    # a kernel trace of the same replays shows the kernels back to back at the eager rate: the faster
+    # of the two is the projection, both are reported)
+    t1, shard_g, shard_e = el1 / steps * 1e6, el / steps * 1e6, el_eager / steps * 1e6
+    shard = min(shard_g, shard_e)
+    return {"one_gpu_step_us": t1, "one_gpu_value": Bg * steps / el1, "rows_per_rank": Bg // W,
+            "shard_step_us": shard, "shard_step_us_eager": shard_e, "shard_step_us_graph": shard_g,
+            "steps_per_graph": gs,
+            "tr_per_s_without_collectives": Bg / (shard * 1e-6),
+            "kernels": [{"kernel": k[0], "avg_us": k[1]} for k in ks],
+            "efficiency_bound": {"without_collectives": t1 / (W * shard),
+                                 "with_allreduce": t1 / (W * (shard + ALLREDUCE_EST_US)),
+                                 "allreduce_estimate_us": ALLREDUCE_EST_US},
+            "note": "rank 0 of world_size 8 on one GPU: the 1024-row shard's GRADS_ONLY step (every rank draws the "
+                    "same global 8192 PER sample) + apply_grads (Adam, soft update, the ordered priority update "
+                    "of all 8192 |delta| on every tree replica); add the |delta| all-gather (32 KB) and the "
+                    "428 KB gradient all-reduce for the 8-GPU step"}
+
+
 def dropin_loop(args, device, batch=1024, iters=200, warmup=20):
     """The drop-in path a reference user runs (R:train.py:88-108): `Agents.DuelingDoubleDQNAgent`
     on the macro-lane MLP, one env row per iteration (n_env = 1):
-    choose_actions -> store_transitions -> learn -> update_target_network, timed per call on
-    the host clock (learn() ends with the RNG hand-back, which synchronises the stream).
+    choose_actions -> store_transitions -> learn -> update_target_network, timed per call on the
+    host clock, the stream synchronised only before the clock stops (as in train.py, where the next
+    choose_actions waits for the GPU).  `deferred` (the default Agent): learn() is recorded and
+    launched by update_target_network with the soft update fused, RNG hand-back through pinned
+    buffers; `synchronous`: DQNX_AGENT_DEFER=0 (learn() launches and reads the RNG back itself).
     The replay is pre-filled through the engine (synthetic rows, like the headline line)."""
     import tempfile
 
@@ -551,44 +660,64 @@ def dropin_loop(args, device, batch=1024, iters=200, warmup=20):
         act = nn.ReLU()
         return (nn.Sequential(nn.Linear(space.shape[0], 256), act, nn.Linear(256, 128), act), 128, optim.Adam,
                 nn.SmoothL1Loss)
-    tmp = tempfile.mkdtemp(prefix="dqnx_dropin_")
-    agent = Agents.DuelingDoubleDQNAgent(
-        n_env=1, lr=1e-4, gamma=0.99, epsilon_start=1.0, epsilon_min=0.05, epsilon_decay=2e6,
-        epsilon_exp_decay=False, nn_conf_func=net_conf, input_dim=Box(), output_dim=args.actions,
-        batch_size=batch, min_buffer_size=batch, buffer_size=args.capacity, update_target_frequency=30000,
-        target_soft_update=True, target_soft_update_tau=1e-3, save_frequency=10 ** 9, log_frequency=10 ** 9,
-        save_dir=tmp + "/", log_dir=tmp + "/", load=False, algo="DuelingDoubleDQNAgent", gpu=str(device.index or 0))
-    fill_ring(agent.engine, min(args.capacity, 100_000), args.obs_dim, args.actions, device, seed=0)
-    rng = np.random.default_rng(0)
-    obs = rng.random((iters + warmup + 1, args.obs_dim), dtype=np.float32)
-    random.seed(1234)
-    phases = {"choose_actions": 0.0, "store_transitions": 0.0, "learn": 0.0, "update_target_network": 0.0}
-    t_all = 0.0
-    for t in range(iters + warmup):
-        agent.step = t
-        t0 = time.perf_counter()
-        a = agent.choose_actions(obs[t:t + 1])
-        t1 = time.perf_counter()
-        agent.store_transitions(obs[t:t + 1], a, [0.5], [False], obs[t + 1:t + 2], None)
-        t2 = time.perf_counter()
-        agent.learn()
-        t3 = time.perf_counter()
-        agent.update_target_network()
+
+    def run(defer):
+        os.environ["DQNX_AGENT_DEFER"] = "1" if defer else "0"
+        tmp = tempfile.mkdtemp(prefix="dqnx_dropin_")
+        agent = Agents.DuelingDoubleDQNAgent(
+            n_env=1, lr=1e-4, gamma=0.99, epsilon_start=1.0, epsilon_min=0.05, epsilon_decay=2e6,
+            epsilon_exp_decay=False, nn_conf_func=net_conf, input_dim=Box(), output_dim=args.actions,
+            batch_size=batch, min_buffer_size=batch, buffer_size=args.capacity, update_target_frequency=30000,
+            target_soft_update=True, target_soft_update_tau=1e-3, save_frequency=10 ** 9, log_frequency=10 ** 9,
+            save_dir=tmp + "/", log_dir=tmp + "/", load=False, algo="DuelingDoubleDQNAgent",
+            gpu=str(device.index or 0))
+        fill_ring(agent.engine, min(args.capacity, 100_000), args.obs_dim, args.actions, device, seed=0)
+        rng = np.random.default_rng(0)
+        obs = rng.random((iters + warmup + 1, args.obs_dim), dtype=np.float32)
+        random.seed(1234)
+        phases = {"choose_actions": 0.0, "store_transitions": 0.0, "learn": 0.0, "update_target_network": 0.0}
+        t_start = None
+        for t in range(iters + warmup):
+            if t == warmup:
+                agent.flush()
+                torch.cuda.synchronize(device)
+                t_start = time.perf_counter()
+            agent.step = t
+            t0 = time.perf_counter()
+            a = agent.choose_actions(obs[t:t + 1])
+            t1 = time.perf_counter()
+            agent.store_transitions(obs[t:t + 1], a, [0.5], [False], obs[t + 1:t + 2], None)
+            t2 = time.perf_counter()
+            agent.learn()
+            t3 = time.perf_counter()
+            agent.update_target_network()
+            t4 = time.perf_counter()
+            if t >= warmup:
+                phases["choose_actions"] += t1 - t0
+                phases["store_transitions"] += t2 - t1
+                phases["learn"] += t3 - t2
+                phases["update_target_network"] += t4 - t3
+        agent.flush()
         torch.cuda.synchronize(device)
-        t4 = time.perf_counter()
-        if t >= warmup:
-            phases["choose_actions"] += t1 - t0
-            phases["store_transitions"] += t2 - t1
-            phases["learn"] += t3 - t2
-            phases["update_target_network"] += t4 - t3
-            t_all += t4 - t0
-    del agent
-    torch.cuda.empty_cache()
-    return {"us_per_iteration": t_all / iters * 1e6, "batch": batch, "n_env": 1, "iterations": iters,
-            "learn_tr_per_s": batch * iters / t_all,
-            "phases_us": {k: v / iters * 1e6 for k, v in phases.items()},
-            "note": "Agents.DuelingDoubleDQNAgent through the R:train.py:88-108 call sequence on the MLP-284 "
-                    "macro-lane net; host-clock per call, the stream synchronised at the end of every iteration"}
+        t_all = time.perf_counter() - t_start
+        del agent
+        torch.cuda.empty_cache()
+        return {"us_per_iteration": t_all / iters * 1e6, "learn_tr_per_s": batch * iters / t_all,
+                "phases_us": {k: v / iters * 1e6 for k, v in phases.items()}}
+
+    saved = os.environ.get("DQNX_AGENT_DEFER")
+    try:
+        sync = run(False)
+        dfr = run(True)
+    finally:
+        if saved is None:
+            os.environ.pop("DQNX_AGENT_DEFER", None)
+        else:
+            os.environ["DQNX_AGENT_DEFER"] = saved
+    return dict(dfr, batch=batch, n_env=1, iterations=iters, synchronous=sync,
+                note="Agents.DuelingDoubleDQNAgent through the R:train.py:88-108 call sequence on the MLP-284 "
+                     "macro-lane net; host clock per call; the top-level numbers are the default (deferred) "
+                     "agent, `synchronous` the DQNX_AGENT_DEFER=0 one")
 
 
 def main():
@@ -657,10 +786,13 @@ def main():
         torch.cuda.empty_cache()
         if not dpmode:
             extras = single_gpu_extras(args, spec, device)
-            try:
-                extras["dropin_loop"] = dropin_loop(args, device)
-            except Exception as ex:   # an extra must never hide the headline number
-                log(f"dropin loop failed: {ex!r}")
+            for name, fn in (("head_net", head_net_extra), ("configs4_projection_w8", c5_projection),
+                             ("dropin_loop", dropin_loop)):
+                try:
+                    extras[name] = fn(args, device)
+                except Exception as ex:   # an extra must never hide the headline number
+                    log(f"{name} failed: {ex!r}")
+                torch.cuda.empty_cache()
         elif scaling == "strong":   # the weak-scaling companion line: 4096 rows per rank
             weng = make_engine(args, spec, 4096 * world, world, rank, device, local=local)
             wel, _ = run_learner(args, weng, world, backend, args.steps, args.warmup, dist, device, dp=dpmode)

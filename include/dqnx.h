@@ -235,6 +235,14 @@ enum dqnx_rng { DQNX_RNG_PY = 0, DQNX_RNG_NP = 1 };
 int dqnx_rng_set(dqnx_engine* e, int32_t which, const uint32_t* state625, void* stream);
 /* Download 625 words; synchronises the stream. */
 int dqnx_rng_get(dqnx_engine* e, int32_t which, uint32_t* state625, void* stream);
+/* The same two copies, stream-ordered and WITHOUT a synchronisation: `state625` must be pinned
+ * (page-locked) host memory that the caller keeps unchanged (set) / does not read (get) until the
+ * copy has executed (e.g. an event recorded after it).  The drop-in Agent uses them to hand the
+ * sampler's RNG to and from Python's global `random` / numpy state without a host round trip per
+ * learn() (dqn/agent.py).  Same argument checks as dqnx_rng_set / dqnx_rng_get; refused while a
+ * prefetched minibatch is pending. */
+int dqnx_rng_set_async(dqnx_engine* e, int32_t which, const uint32_t* state625, void* stream);
+int dqnx_rng_get_async(dqnx_engine* e, int32_t which, uint32_t* state625, void* stream);
 
 /* ---- the learn step: replaces Agent.learn() (R:dqn/agent.py:166-185 / 204-226 /
  *      245-272) and, with DQNX_STEP_SOFT_UPDATE, the following

@@ -444,6 +444,9 @@ struct dqnx_engine {
     int bwd_plan = 0;
     int mtc_blocks = 0;     // uniform sampler's MT block cache (fused plan only; 0 = off)
     bool wblk_dirty = true; // the fused plan's blocked weight copies must be rebuilt before the next step
+    // the micro-CNN plan's permuted conv weight copies (k_conv_perm) are stale: the next step launches
+    // conv_perm (an Adam pass that writes them -- adam_writes_perms -- makes them current)
+    bool perm_dirty = true;
     FusedFwdArgs fplan;     // LDS geometry of the fused plan (valid when bwd_plan == 2)
     int fsplit = 1;         // layer-1 column parts of the split forward (1: one forward launch)
     bool pf_valid = false;   // a prefetched minibatch for the next step sits in slot pf_slot
@@ -744,6 +747,17 @@ void fill_blk_layers(dqnx_engine* e, AdamArgs& aa, bool force = false) {
     }
 }
 
+// The Adam launch of a plan step; one that writes the micro plan's permuted conv copies marks them
+// current when it is enqueued (launch order = execution order on the step's stream)
+static std::function<int(hipStream_t)> adam_run(dqnx_engine* e, const AdamArgs& aa) {
+    const bool perms = adam_writes_perms(aa);
+    return [=](hipStream_t s) {
+        const int rc = launch_adam(aa, s);
+        if (!rc && perms) e->perm_dirty = false;
+        return rc;
+    };
+}
+
 // Gradient reduction (fixed-order sum of the split-K slabs) + Adam (+ soft update).
 KStep adam_kstep(dqnx_engine* e, int flags, AdamArgs* args_out = nullptr) {
     const dqnx_config& c = e->cfg;
@@ -764,6 +778,7 @@ KStep adam_kstep(dqnx_engine* e, int flags, AdamArgs* args_out = nullptr) {
         sg.partial = at<float>(e, e->ws_cpart[l]);
         sg.pstride = (int64_t)cp.Co * cp.K + cp.Co;
         sg.S = e->cslices[l];
+        sg.wide = sg.S >= ADAM_WIDE_MIN_S || e->micro;   // micro plan: every conv (its permuted copies)
         part_elems += (double)sg.S * sg.pstride;
     }
     for (int l = 0; l < L; l++) {
@@ -772,6 +787,7 @@ KStep adam_kstep(dqnx_engine* e, int flags, AdamArgs* args_out = nullptr) {
         sg.partial = at<float>(e, e->ws_part[l]);
         sg.pstride = (int64_t)np.dense[l].out * np.dense[l].in + np.dense[l].out;
         sg.S = e->slices[l];
+        sg.wide = sg.S >= ADAM_WIDE_MIN_S;
         part_elems += (double)sg.S * sg.pstride;
     }
     {
@@ -780,6 +796,7 @@ KStep adam_kstep(dqnx_engine* e, int flags, AdamArgs* args_out = nullptr) {
         sg.partial = at<float>(e, e->ws_head_part);
         sg.pstride = head_pstride(np);
         sg.S = e->slices[L - 1];
+        sg.wide = sg.S >= ADAM_WIDE_MIN_S;
         part_elems += (double)sg.S * sg.pstride;
     }
     aa.mode = (flags & DQNX_STEP_GRADS_ONLY) ? 0 : 1;
@@ -811,13 +828,26 @@ KStep adam_kstep(dqnx_engine* e, int flags, AdamArgs* args_out = nullptr) {
         aa.mtc = at<uint32_t>(e, e->ws_mtc);
         aa.mtc_blocks = e->mtc_blocks;
     }
+    if (e->micro && aa.mode == 1) {   // the permuted copies of convs 2.. next to the updated weights
+        for (int l = 1; l < NC && aa.nperm < 2; l++) {
+            const ConvPlan& cp = np.conv[l];
+            AdamArgs::PermLayer& P = aa.perm[aa.nperm++];
+            P.woff = cp.off;
+            P.Co = cp.Co;
+            P.Ci = cp.Ci;
+            P.p0 = at<float>(e, e->ws_wperm0[l]);
+            P.p1 = at<float>(e, e->ws_wperm1[l]);
+            P.pT = at<float>(e, e->ws_wpermT[l]);
+        }
+        if (NC - 1 > 2) aa.nperm = 0;
+    }
     KStep k;
     k.name = aa.mode ? "adam_fused" : "grad_reduce";
     const double P = (double)np.P;
     // read partials; write g; Adam: read p,m,v (+target), write p,m,v (+target)
     k.bytes = 4.0 * (part_elems + P + (aa.mode ? 6.0 * P + (aa.soft ? 2.0 * P : 0.0) : 0.0));
     k.flops = aa.mode ? 12.0 * P : 0.0;
-    k.run = [=](hipStream_t s) { return launch_adam(aa, s); };
+    k.run = adam_run(e, aa);
     if (args_out) *args_out = aa;
     return k;
 }
@@ -1424,7 +1454,14 @@ std::vector<KStep> build_learn_steps(dqnx_engine* e, int key) {
             KStep k;
             k.name = "conv_perm";
             k.bytes = pbytes;
-            k.run = [=](hipStream_t s) { return launch_conv_perm(pa, s); };
+            // eager: only while the copies are stale (the last step's Adam pass wrote them otherwise);
+            // a captured graph always holds the launch (its replays may follow any update)
+            k.run = [=](hipStream_t s) {
+                hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+                DQNX_HIP_CHECK(hipStreamIsCapturing(s, &cs));
+                if (!e->perm_dirty && cs == hipStreamCaptureStatusNone) return (int)DQNX_OK;
+                return launch_conv_perm(pa, s);
+            };
             ks.push_back(k);
         }
         MicroFwdArgs ma;
@@ -2010,7 +2047,7 @@ std::vector<KStep> build_learn_steps(dqnx_engine* e, int key) {
         aa.pf_nphys = e->Bl;
         aa.mtc = nullptr;   // the forward's sampler body draws from the MT state itself
         aa.mtc_blocks = 0;
-        k.run = [=](hipStream_t s) { return launch_adam(aa, s); };
+        k.run = adam_run(e, aa);
         ks.push_back(k);
     } else {
         ks.push_back(adam_kstep(e, flags));
@@ -2539,6 +2576,7 @@ int dqnx_engine_obs_stride(const dqnx_engine* e, int32_t* stride) {
 
 int dqnx_params_modified(dqnx_engine* e) {
     if (!e) return set_error(DQNX_EINVAL, "null engine");
+    e->perm_dirty = true;
     e->wblk_dirty = true;
     return DQNX_OK;
 }
@@ -2550,6 +2588,7 @@ int dqnx_engine_bind(dqnx_engine* e, void* arena, uint64_t bytes) {
     if (((uintptr_t)arena) % 256) return set_error(DQNX_EINVAL, "arena must be 256-byte aligned");
     drop_graphs(e);
     e->arena = (char*)arena;
+    e->perm_dirty = true;
     e->wblk_dirty = true;
     int dev = 0, cus = 0;   // the current device's compute units (plans that size grids to the chip)
     if (hipGetDevice(&dev) == hipSuccess &&
@@ -2716,6 +2755,27 @@ int dqnx_rng_get(dqnx_engine* e, int32_t which, uint32_t* state625, void* stream
     else if (e->pf_valid) DQNX_HIP_CHECK(hipStreamWaitEvent(s, e->ev_sampled[e->pf_slot], 0));
     DQNX_HIP_CHECK(hipMemcpyAsync(state625, src, 625 * 4, hipMemcpyDeviceToHost, s));
     DQNX_HIP_CHECK(hipStreamSynchronize(s));
+    return DQNX_OK;
+}
+
+int dqnx_rng_set_async(dqnx_engine* e, int32_t which, const uint32_t* state625, void* stream) {
+    int rc = check_bound(e);
+    if (rc) return rc;
+    if (!state625 || (which != DQNX_RNG_PY && which != DQNX_RNG_NP)) return set_error(DQNX_EINVAL, "bad argument");
+    if (state625[624] > 624) return set_error(DQNX_EINVAL, "MT index must be <= 624");
+    if (e->pf_valid) return set_error(DQNX_ESTATE, "rng_set while a prefetched minibatch is pending");
+    uint32_t* dst = which == DQNX_RNG_PY ? ctrl_of(e)->py_mt : ctrl_of(e)->np_mt;
+    DQNX_HIP_CHECK(hipMemcpyAsync(dst, state625, 625 * 4, hipMemcpyHostToDevice, (hipStream_t)stream));
+    return DQNX_OK;
+}
+
+int dqnx_rng_get_async(dqnx_engine* e, int32_t which, uint32_t* state625, void* stream) {
+    int rc = check_bound(e);
+    if (rc) return rc;
+    if (!state625 || (which != DQNX_RNG_PY && which != DQNX_RNG_NP)) return set_error(DQNX_EINVAL, "bad argument");
+    if (e->pf_valid) return set_error(DQNX_ESTATE, "rng_get_async while a prefetched minibatch is pending");
+    const uint32_t* src = which == DQNX_RNG_PY ? ctrl_of(e)->py_mt : ctrl_of(e)->np_mt;
+    DQNX_HIP_CHECK(hipMemcpyAsync(state625, src, 625 * 4, hipMemcpyDeviceToHost, (hipStream_t)stream));
     return DQNX_OK;
 }
 
@@ -3054,6 +3114,7 @@ int dqnx_apply_grads(dqnx_engine* e, int32_t flags, void* stream) {
     const int key = 0x100 | (flags & DQNX_STEP_SOFT_UPDATE) | (keep ? 0x200 : 0);
     const int rc2 = run_graphed(e, key, (hipStream_t)stream, [&](hipStream_t s) { return enqueue_apply(e, key, s); });
     if (rc2) return rc2;
+    e->perm_dirty = true;   // (mode 2: the conv weights change without their permuted copies)
     if (keep) e->wblk_dirty = false;                          // every blocked copy rewritten from the new weights
     else if (!adam_keeps_blk(e)) e->wblk_dirty = true;        // this Adam pass leaves the blocked copies behind
     return DQNX_OK;
@@ -3129,6 +3190,7 @@ int dqnx_apply_grads_bucket(dqnx_engine* e, int32_t flags, int32_t bucket, void*
         rc = enqueue_per_update(e, at<int32_t>(e, e->off[DQNX_BUF_BATCH_IDX]), s);
         if (rc) return rc;
     }
+    e->perm_dirty = true;
     if (!adam_keeps_blk(e)) e->wblk_dirty = true;
     AdamArgs aa;
     adam_kstep(e, DQNX_STEP_GRADS_ONLY, &aa);
@@ -3145,6 +3207,7 @@ int dqnx_apply_grads_bucket(dqnx_engine* e, int32_t flags, int32_t bucket, void*
 int dqnx_soft_update(dqnx_engine* e, void* stream) {
     int rc = check_bound(e);
     if (rc) return rc;
+    e->perm_dirty = true;
     e->wblk_dirty = true;   // the target copies change outside the Adam pass
     const float tau = (float)((double)e->cfg.tau * e->cfg.n_env);
     const float omt = (float)(1.0 - (double)e->cfg.tau * e->cfg.n_env);
@@ -3155,6 +3218,7 @@ int dqnx_soft_update(dqnx_engine* e, void* stream) {
 int dqnx_hard_update(dqnx_engine* e, void* stream) {
     int rc = check_bound(e);
     if (rc) return rc;
+    e->perm_dirty = true;
     e->wblk_dirty = true;
     DQNX_HIP_CHECK(hipMemcpyAsync(e->arena + e->off[DQNX_BUF_TARGET_PARAMS], e->arena + e->off[DQNX_BUF_PARAMS],
                                   (size_t)e->np.P * 4, hipMemcpyDeviceToDevice, (hipStream_t)stream));

@@ -728,7 +728,7 @@ __global__ __launch_bounds__(256) void k_adam(AdamArgs a) {
             const int64_t ps = sg.pstride;
             gsum = pp[0];
             int u = 1;
-            if (sg.S >= ADAM_WIDE_MIN_S) {   // k_adam4's wide order: 8 strided partials, then its xor butterfly
+            if (sg.wide) {   // k_adam4's wide order: 8 strided partials, then its xor butterfly
                 float part[8];
 #pragma unroll
                 for (int j = 0; j < 8; j++) {
@@ -811,19 +811,8 @@ __global__ __launch_bounds__(256) void k_adam(AdamArgs a) {
 // lanes (every lane ends with the same bits).  One round trip of slab loads instead of S / 16
 // dependent rounds: the slab sum of conv 2 (128 slabs) was the launch's critical path.
 static_assert(ADAM_WIDE == 8, "k_adam's scalar wide sum assumes 8 lanes");
-__device__ __forceinline__ void adam4_update(const AdamArgs& a, int64_t e, int nv, float4 g, float4 m, float4 v,
-                                             float4 p, float4 tg, float step_size, float bc2s, bool store_g) {
-    auto st = [&](float* base, const float4& x) {
-        if (nv == 4) {
-            *reinterpret_cast<float4*>(base + e) = x;
-            return;
-        }
-        base[e] = x.x;
-        if (nv > 1) base[e + 1] = x.y;
-        if (nv > 2) base[e + 2] = x.z;
-    };
-    if (store_g) st(a.grads, g);
-    if (a.mode == 0) return;
+__device__ __forceinline__ void adam4_compute(const AdamArgs& a, const float4& g, float4& m, float4& v, float4& p,
+                                              float4& tg, float step_size, float bc2s) {
     auto upd = [&](float& mk, float& vk, float& pk, float& tk, float gk) {
         mk = fmaf(a.w1, gk - mk, mk);
         vk = vk * a.beta2;
@@ -836,6 +825,21 @@ __device__ __forceinline__ void adam4_update(const AdamArgs& a, int64_t e, int n
     upd(m.y, v.y, p.y, tg.y, g.y);
     upd(m.z, v.z, p.z, tg.z, g.z);
     upd(m.w, v.w, p.w, tg.w, g.w);
+}
+__device__ __forceinline__ void adam4_update(const AdamArgs& a, int64_t e, int nv, float4 g, float4 m, float4 v,
+                                             float4& p, float4& tg, float step_size, float bc2s, bool store_g) {
+    auto st = [&](float* base, const float4& x) {
+        if (nv == 4) {
+            *reinterpret_cast<float4*>(base + e) = x;
+            return;
+        }
+        base[e] = x.x;
+        if (nv > 1) base[e + 1] = x.y;
+        if (nv > 2) base[e + 2] = x.z;
+    };
+    if (store_g) st(a.grads, g);
+    if (a.mode == 0) return;
+    adam4_compute(a, g, m, v, p, tg, step_size, bc2s);
     st(a.m, m);
     st(a.v, v);
     st(a.p, p);
@@ -884,11 +888,14 @@ __global__ __launch_bounds__(256) void k_adam4(AdamArgs a) {
         const bool live = e4 < w0 + w4;
         const int64_t e = (live ? e4 : w0) << 2;
         float4 m = z4, v = z4, p = z4, tg = z4;
-        if (a.mode != 0 && j == 0 && live) {
+        const bool perms = a.mode == 1 && a.nperm > 0;
+        // with the permuted copies every lane of the group loads the operands (one transaction per
+        // group) and computes the same update, so the stores below spread over the 8 lanes
+        if (a.mode != 0 && (j == 0 || perms) && live) {
             m = ld4(a.m + e);
             v = ld4(a.v + e);
             p = ld4(a.p + e);
-            if (a.soft) tg = ld4(a.target + e);
+            if (a.soft || perms) tg = ld4(a.target + e);
         }
         const AdamSegment sg = adam_segment_of(a, e);
         const float* q4 = sg.partial + (e - sg.off);
@@ -919,7 +926,38 @@ __global__ __launch_bounds__(256) void k_adam4(AdamArgs a) {
             g.z += __shfl_xor(g.z, o);
             g.w += __shfl_xor(g.w, o);
         }
-        if (j == 0 && live) adam4_update(a, e, 4, g, m, v, p, tg, step_size, bc2s, true);
+        if (live && !perms) {
+            if (j == 0) adam4_update(a, e, 4, g, m, v, p, tg, step_size, bc2s, true);
+        } else if (live) {
+            // every lane: the same update; lane j < 4 writes element j's three permuted copies, lanes
+            // 4..7 the float4s of grads / m / v / p (+ target)
+            adam4_compute(a, g, m, v, p, tg, step_size, bc2s);
+            if (j < 4) {
+                const float pv = j == 0 ? p.x : j == 1 ? p.y : j == 2 ? p.z : p.w;
+                const float tv = j == 0 ? tg.x : j == 1 ? tg.y : j == 2 ? tg.z : tg.w;
+#pragma unroll
+                for (int l = 0; l < 2; l++) {
+                    if (l >= a.nperm) continue;
+                    const AdamArgs::PermLayer& L = a.perm[l];
+                    const int K = L.Ci * 9;
+                    const int64_t le = e + j - L.woff;
+                    if (le < 0 || le >= (int64_t)L.Co * K) continue;   // (a layer's bias is not permuted)
+                    const int co = (int)le / K, r = (int)le - co * K, ci = r / 9, t = r - ci * 9;
+                    L.p0[(co * 9 + t) * L.Ci + ci] = pv;
+                    L.p1[(co * 9 + t) * L.Ci + ci] = tv;
+                    L.pT[(ci * 9 + t) * L.Co + co] = pv;
+                }
+            } else if (j == 4) {
+                *reinterpret_cast<float4*>(a.grads + e) = g;
+                *reinterpret_cast<float4*>(a.m + e) = m;
+            } else if (j == 5) {
+                *reinterpret_cast<float4*>(a.v + e) = v;
+            } else if (j == 6) {
+                *reinterpret_cast<float4*>(a.p + e) = p;
+            } else if (a.soft) {
+                *reinterpret_cast<float4*>(a.target + e) = tg;
+            }
+        }
         return;
     }
     const int nb = eb - wide_blocks;
@@ -1420,8 +1458,18 @@ static bool adam_vec_ok(const AdamArgs& a) {
     return true;
 }
 
+bool adam_writes_perms(const AdamArgs& a) {
+    if (a.nperm <= 0 || a.mode != 1 || a.e0 != 0 || !adam_vec_ok(a)) return false;
+    int64_t end = 0;   // the wide prefix must cover every perm layer
+    for (int q = 0; q < a.nseg && a.seg[q].wide; q++) end = q + 1 < a.nseg ? a.seg[q + 1].off : a.n_params;
+    for (int l = 0; l < a.nperm; l++)
+        if (a.perm[l].woff + (int64_t)a.perm[l].Co * a.perm[l].Ci * 9 > end) return false;
+    return end % 4 == 0;
+}
+
 int launch_adam(const AdamArgs& a_in, hipStream_t s) {
     AdamArgs a = a_in;
+    if (!adam_writes_perms(a)) a.nperm = 0;
     const bool vec = adam_vec_ok(a);
     // the wide prefix (k_adam4): the leading segments of the range with >= ADAM_WIDE_MIN_S slabs
     a.wide_end = 0;
@@ -1429,7 +1477,7 @@ int launch_adam(const AdamArgs& a_in, hipStream_t s) {
         int q = 0;
         while (q + 1 < a.nseg && a.seg[q + 1].off <= a.e0) q++;
         int64_t end = a.e0;
-        for (; q < a.nseg && a.seg[q].S >= ADAM_WIDE_MIN_S; q++) end = q + 1 < a.nseg ? a.seg[q + 1].off : a.n_params;
+        for (; q < a.nseg && a.seg[q].wide; q++) end = q + 1 < a.nseg ? a.seg[q + 1].off : a.n_params;
         if (end > a.n_params) end = a.n_params;
         if (end > a.e0 && end % 4 == 0) a.wide_end = end;
     }

@@ -132,6 +132,7 @@ struct AdamSegment {
     const float* partial;  // slab 0 of the segment's partials
     int64_t pstride;       // elements between slabs
     int S;                 // number of slabs
+    int wide;              // summed ADAM_WIDE-strided (k_adam4's wide path; the scalar kernel the same order)
 };
 struct AdamArgs {
     AdamSegment seg[kMaxSeg];
@@ -177,7 +178,19 @@ struct AdamArgs {
     const int32_t* pf_phys_src;
     int32_t* pf_phys_dst;
     int pf_nphys;
+    // micro-CNN plan: the permuted weight copies of convs 2.. (k_conv_perm's layouts) written next to
+    // every updated conv weight by the wide path (mode 1), so the next step needs no conv_perm launch
+    int nperm;
+    struct PermLayer {
+        int64_t woff;      // flat offset of W [Co][Ci][3][3]
+        int Co, Ci;
+        float* p0;         // [Co][9][Ci] online
+        float* p1;         // [Co][9][Ci] target
+        float* pT;         // [Ci][9][Co] online
+    } perm[2];
 };
+// launch_adam writes AdamArgs::perm (the float4 kernel's wide path covers every perm layer)
+bool adam_writes_perms(const AdamArgs& a);
 
 // Full-K weight gradients of every layer + Adam (+ soft update) in one launch.
 struct DwAdamProblem {

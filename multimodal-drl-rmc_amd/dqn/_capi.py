@@ -79,7 +79,7 @@ EXPORTS = [
     "dqnx_net_param_count", "dqnx_net_param_info", "dqnx_config_defaults", "dqnx_engine_create",
     "dqnx_engine_destroy", "dqnx_engine_arena_bytes", "dqnx_engine_buffer", "dqnx_engine_obs_stride",
     "dqnx_engine_bind", "dqnx_engine_reset", "dqnx_engine_set_graphs", "dqnx_replay_push", "dqnx_rng_set",
-    "dqnx_rng_get", "dqnx_learn_step", "dqnx_learn_steps", "dqnx_prefetch_begin", "dqnx_prefetch_stream", "dqnx_apply_grads", "dqnx_soft_update", "dqnx_hard_update",
+    "dqnx_rng_get", "dqnx_rng_set_async", "dqnx_rng_get_async", "dqnx_learn_step", "dqnx_learn_steps", "dqnx_prefetch_begin", "dqnx_prefetch_stream", "dqnx_apply_grads", "dqnx_soft_update", "dqnx_hard_update",
     "dqnx_sample_scratch_bytes", "dqnx_sample_uniform", "dqnx_last_error", "dqnx_abi_version",
     "dqnx_learn_kernel_count", "dqnx_learn_kernel_info", "dqnx_learn_step_timed", "dqnx_learn_step_omit", "dqnx_events_create",
     "dqnx_events_destroy", "dqnx_event_elapsed", "dqnx_debug_stamps",
@@ -122,6 +122,8 @@ def lib():
         "dqnx_replay_push": ([vp, vp, vp, vp, vp, vp, I32, I32, vp], ctypes.c_int),
         "dqnx_rng_set": ([vp, I32, P(ctypes.c_uint32), vp], ctypes.c_int),
         "dqnx_rng_get": ([vp, I32, P(ctypes.c_uint32), vp], ctypes.c_int),
+        "dqnx_rng_set_async": ([vp, I32, vp, vp], ctypes.c_int),
+        "dqnx_rng_get_async": ([vp, I32, vp, vp], ctypes.c_int),
         "dqnx_learn_step": ([vp, I32, vp], ctypes.c_int),
         "dqnx_learn_steps": ([vp, I32, I32, vp], ctypes.c_int),
         "dqnx_prefetch_begin": ([vp, I32, vp], ctypes.c_int),

@@ -19,6 +19,18 @@ Host-visible RNG semantics are the reference's.
 * PER's `np.random.uniform` continues numpy's global legacy stream.
 Both are handed to the engine before the step and taken back after it, so
 `choose_actions`' ε-greedy draws interleave exactly as in the reference.
+
+The train.py loop without host round trips (R:train.py:88-108: choose_actions ->
+store_transitions -> learn -> update_target_network -> log -> save_model): `learn()` records the
+step and returns; the step is launched by the next agent call -- by `update_target_network()`
+as ONE launch sequence with the soft update fused into the Adam pass (what
+`update_target_network` would do next anyway), otherwise as a plain learn step.  The RNG state
+goes to the device and comes back through pinned buffers without a synchronisation; it is
+installed into Python's `random` (numpy's global state under PER) at the next agent call that
+needs it (`choose_actions`, `learn`, or `flush()`).  The results are bitwise those of the eager
+order.  The contract this adds: code that draws from `random` / `np.random` or reads the
+networks' parameters between `learn()` and the next agent method must call `agent.flush()`
+first.  DQNX_AGENT_DEFER=0 restores the synchronous learn().
 """
 from __future__ import annotations
 
@@ -155,6 +167,11 @@ class Agent:
         self.replay_memory_buffer = self._make_replay()
         self._learn_steps = 0          # learn() calls since the last log (throughput metric)
         self._learn_t0 = time.time()
+        self._defer = os.environ.get("DQNX_AGENT_DEFER", "1") != "0"
+        self._learn_pending = False    # learn() recorded, not launched yet
+        self._rng_pending = False      # the advanced sampler RNG is on its way back (pinned buffer)
+        self.engine.launch_hook = self._launch_pending
+        self.engine.settle_hook = self.flush
         self.update_target_network(force=True)
 
     def _make_replay(self):
@@ -172,6 +189,7 @@ class Agent:
 
     def store_transitions(self, obses, actions, rews, dones, new_obses, infos):
         """R:dqn/agent.py:80-84."""
+        self._launch_pending()   # a recorded learn step samples the ring as it was at learn()
         for i in self.replay_memory_buffer.store_transitions(obses, actions, rews, dones, new_obses):
             if infos:
                 self.ep_info_buffer.append({'r': infos[i]['r'], 'l': infos[i]['l']})
@@ -185,20 +203,66 @@ class Agent:
         return np.interp(self.step * self.n_env, [0, self.epsilon_decay], [self.epsilon_start, self.epsilon_min])
 
     def choose_actions(self, obses):
-        actions = self.online_network.actions(obses)
+        self._launch_pending()
+        actions = self.online_network.actions(obses)   # (waits for the stream: the learn step ran)
+        self.flush()                                   # the sampler's RNG back into `random` first
         for i in range(len(actions)):
             if random.random() <= self.epsilon():
                 actions[i] = random.randint(0, self.output_dim - 1)
         return actions
 
     # -- learning ----------------------------------------------------------------------
+    # RNG stream the sampler consumes: CPython's global `random` (uniform replay)
+    _rng_which = C.DQNX_RNG_PY
+
+    def _rng_to_engine(self):
+        if self._rng_which == C.DQNX_RNG_PY:
+            self.engine.set_rng_async(C.DQNX_RNG_PY, random.getstate()[1])
+        else:
+            st = np.random.get_state()
+            self.engine.set_rng_async(C.DQNX_RNG_NP, np.append(np.asarray(st[1], dtype=np.uint32), np.uint32(st[2])))
+
+    def _rng_from_engine(self):
+        a = self.engine.rng_async_out
+        if self._rng_which == C.DQNX_RNG_PY:
+            v, _, g = random.getstate()
+            random.setstate((v, tuple(a.tolist()), g))
+        else:
+            st = np.random.get_state()
+            np.random.set_state((st[0], a[:624].copy(), int(a[624]), st[3], st[4]))
+
+    def _pre_learn(self):
+        """Per-algorithm host bookkeeping before the step is launched (PER: the beta step)."""
+
+    def _launch_learn(self, soft_update):
+        e = self.engine
+        self._pre_learn()
+        self._rng_to_engine()                # async H2D from pinned memory
+        e.learn_step(soft_update=soft_update)
+        e.get_rng_async(self._rng_which)     # async D2H + event
+        self._learn_pending = False
+        self._rng_pending = True
+
+    def _launch_pending(self, soft_update=False):
+        if self._learn_pending:
+            self._launch_learn(soft_update)
+
+    def flush(self):
+        """Launch a recorded learn step and install the advanced sampler RNG into Python's global
+        state (waits for the step).  Agent methods call it where they need it."""
+        self._launch_pending()
+        if self._rng_pending:
+            self.engine.rng_wait()
+            self._rng_from_engine()
+            self._rng_pending = False
+
     def learn(self):
         """One learn step on the engine (R:dqn/agent.py:166-185 / 204-226 / 245-272)."""
-        e = self.engine
-        e.set_py_state_from_global()
-        e.learn_step(soft_update=False)
-        e.get_py_state_to_global()       # synchronises the stream
+        self.flush()
+        self._learn_pending = True
         self._count_learn()
+        if not self._defer:
+            self.flush()
 
     def _count_learn(self):
         self._learn_steps += 1
@@ -213,8 +277,14 @@ class Agent:
         return rate
 
     def update_target_network(self, force=False):
-        """R:dqn/agent.py:101-110."""
-        if (not self.target_soft_update and self.step % (self.update_target_frequency // self.n_env) == 0) or force:
+        """R:dqn/agent.py:101-110.  Right after learn() (train.py's order) the soft update rides in
+        the learn step's Adam pass (DQNX_STEP_SOFT_UPDATE: the same arithmetic, bitwise)."""
+        hard = (not self.target_soft_update and self.step % (self.update_target_frequency // self.n_env) == 0) or force
+        if self._learn_pending and self.target_soft_update and not hard:
+            self._launch_learn(soft_update=True)
+            return
+        self._launch_pending()
+        if hard:
             self.engine.hard_update()
         elif self.target_soft_update:
             self.engine.soft_update()
@@ -222,6 +292,7 @@ class Agent:
     # -- checkpoints / logging (R:dqn/agent.py:112-147) ---------------------------------
     def load_model(self):
         import os
+        self.flush()
         if self.load and os.path.exists(self.save_path):
             print()
             print("Resume training from " + self.save_path + "...")
@@ -235,6 +306,7 @@ class Agent:
 
     def save_model(self):
         if self.step % self.save_frequency == 0 and self.step > self.resume_step:
+            self.flush()
             print()
             print("Saving model...")
             T.cuda.synchronize(self.device)
@@ -244,6 +316,7 @@ class Agent:
 
     def log(self):
         if self.step % self.log_frequency == 0 and self.step > self.resume_step:
+            self.flush()
             rew_mean, len_mean = self.info_mean('r'), self.info_mean('l')
             print()
             print('Step: ', self.step * self.n_env, ' (' + str(self.step) + 'x' + str(self.n_env) + ')')
@@ -276,18 +349,23 @@ class PerDoubleAgent(Agent):
 
     _reduction = "none"
 
+    _rng_which = C.DQNX_RNG_NP   # np.random.uniform (R:dqn/replay_memory.py:76-80)
+
     def _make_replay(self):
         return ReplayMemoryPrioritized(self.buffer_size, self.batch_size, self.epsilon_decay, engine=self.engine)
 
     def learn(self):
-        e = self.engine
-        step = self.step * self.n_env                      # R:dqn/agent.py:247
-        if step != e.agent_step:                          # any other sampler call moved it too
-            e.set_agent_step(step)
-        e.set_np_state_from_global()
-        e.learn_step(soft_update=False)                   # advances the engine's step by n_env
-        e.get_np_state_to_global()
+        self.flush()
+        self._learn_step_at = self.step * self.n_env      # R:dqn/agent.py:247 (the step of THIS learn)
+        self._learn_pending = True
         self._count_learn()
+        if not self._defer:
+            self.flush()
+
+    def _pre_learn(self):
+        e = self.engine
+        if self._learn_step_at != e.agent_step:           # any other sampler call moved it too
+            e.set_agent_step(self._learn_step_at)
 
 
 class DQNAgent(SimpleAgent):

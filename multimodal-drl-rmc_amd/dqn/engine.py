@@ -270,6 +270,19 @@ class LearnEngine:
         self.ring_size = 0
         self.ring_wptr = 0
         self.agent_step = 0      # host mirror of dqnx_ctrl.agent_step (PER beta schedule)
+        # set by a drop-in Agent that records learn() steps for launch at its next call: `launch_hook`
+        # launches a recorded step (host reads of engine memory follow it in stream order),
+        # `settle_hook` also installs the sampler's advanced RNG into the global state (host draws)
+        self.launch_hook = None
+        self.settle_hook = None
+
+    def launch_recorded(self):
+        if self.launch_hook is not None:
+            self.launch_hook()
+
+    def settle(self):
+        if self.settle_hook is not None:
+            self.settle_hook()
 
     # ---- plumbing ------------------------------------------------------------------
     def buffer(self, which) -> Tuple[int, int]:
@@ -332,15 +345,49 @@ class LearnEngine:
         else:
             obs = np.ascontiguousarray(obs, dtype=np.float32).reshape(-1, self.spec.obs_dim)
             next_obs = np.ascontiguousarray(next_obs, dtype=np.float32).reshape(-1, self.spec.obs_dim)
-            act = np.ascontiguousarray(act, dtype=np.int32).reshape(-1)
-            rew = np.ascontiguousarray(rew, dtype=np.float32).reshape(-1)
-            done = np.ascontiguousarray(np.asarray(done).astype(bool), dtype=np.uint8).reshape(-1)
             n = obs.shape[0]
-            C.check(self.L.dqnx_replay_push(self.h, obs.ctypes.data, act.ctypes.data, rew.ctypes.data,
-                                            done.ctypes.data, next_obs.ctypes.data, n, 0, self.stream()),
-                    "replay_push")
+            if n <= self.PINNED_PUSH_ROWS:   # the env loop's n_env rows: one pinned H2D, no host wait
+                self._push_pinned(obs, act, rew, done, next_obs)
+            else:
+                act = np.ascontiguousarray(act, dtype=np.int32).reshape(-1)
+                rew = np.ascontiguousarray(rew, dtype=np.float32).reshape(-1)
+                done = np.ascontiguousarray(np.asarray(done).astype(bool), dtype=np.uint8).reshape(-1)
+                C.check(self.L.dqnx_replay_push(self.h, obs.ctypes.data, act.ctypes.data, rew.ctypes.data,
+                                                done.ctypes.data, next_obs.ctypes.data, n, 0, self.stream()),
+                        "replay_push")
         self.ring_wptr = (self.ring_wptr + n) % self.capacity
         self.ring_size = min(self.ring_size + n, self.capacity)
+
+    PINNED_PUSH_ROWS = 256
+
+    def _push_pinned(self, obs, act, rew, done, next_obs):
+        """Small host pushes (Agent.store_transitions): obs | next_obs | act | rew | done packed into
+        one pinned block, one async H2D into a device staging block, then dqnx_replay_push from device
+        memory (stream-ordered: no host synchronisation; the pinned block is reused once the event
+        after its previous copy has passed)."""
+        n, D = obs.shape
+        nb = ((8 * n * D + 8 * n + n) + 15) // 16 * 16
+        if getattr(self, "_push_pin", None) is None or self._push_pin.numel() < nb:
+            cap = max(nb, ((8 * 16 * D + 8 * 16 + 16) + 15) // 16 * 16)
+            self._push_pin = torch.empty(cap, dtype=torch.uint8).pin_memory()
+            self._push_dev = torch.empty(cap, dtype=torch.uint8, device=self.device)
+            self._push_ev = torch.cuda.Event()
+            self._push_ev_live = False
+        if self._push_ev_live:
+            self._push_ev.synchronize()
+        h = self._push_pin.numpy()
+        o1, o2, o3, o4 = 4 * n * D, 8 * n * D, 8 * n * D + 4 * n, 8 * n * D + 8 * n
+        h[:o1].view(np.float32)[:] = obs.reshape(-1)
+        h[o1:o2].view(np.float32)[:] = next_obs.reshape(-1)
+        h[o2:o3].view(np.int32)[:] = np.asarray(act).reshape(-1)
+        h[o3:o4].view(np.float32)[:] = np.asarray(rew, dtype=np.float32).reshape(-1)
+        h[o4:o4 + n] = np.asarray(done).reshape(-1).astype(bool)
+        self._push_dev[:nb].copy_(self._push_pin[:nb], non_blocking=True)
+        self._push_ev.record(torch.cuda.current_stream(self.device))
+        self._push_ev_live = True
+        b = self._push_dev.data_ptr()
+        C.check(self.L.dqnx_replay_push(self.h, b, b + o2, b + o3, b + o4, b + o1, n, 1, self.stream()),
+                "replay_push")
 
     # ---- RNG -------------------------------------------------------------------------
     def set_rng(self, which: int, state625: np.ndarray):
@@ -354,6 +401,40 @@ class LearnEngine:
         C.check(self.L.dqnx_rng_get(self.h, which, a.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)),
                                     self.stream()), "rng_get")
         return a
+
+    # asynchronous RNG hand-off (dqnx_rng_set_async / _get_async through pinned buffers): the drop-in
+    # Agent's learn() installs Python's / numpy's state and reads the advanced one back without a
+    # host round trip; `rng_wait()` (an event after the download) before reading `rng_async_out`
+    def _rng_pinned(self):
+        if getattr(self, "_rng_pin", None) is None:
+            self._rng_pin = (torch.empty(625, dtype=torch.int32).pin_memory(),
+                             torch.empty(625, dtype=torch.int32).pin_memory())
+            self._rng_ev = torch.cuda.Event()
+            self._rng_ev_live = False
+        return self._rng_pin
+
+    def set_rng_async(self, which: int, state625) -> None:
+        src, _ = self._rng_pinned()
+        self.rng_wait()                    # the previous copies out of / into the pinned buffers ran
+        src.numpy().view(np.uint32)[:] = state625
+        C.check(self.L.dqnx_rng_set_async(self.h, which, ctypes.c_void_p(src.data_ptr()), self.stream()),
+                "rng_set_async")
+
+    def get_rng_async(self, which: int) -> None:
+        _, dst = self._rng_pinned()
+        C.check(self.L.dqnx_rng_get_async(self.h, which, ctypes.c_void_p(dst.data_ptr()), self.stream()),
+                "rng_get_async")
+        self._rng_ev.record(torch.cuda.current_stream(self.device))
+        self._rng_ev_live = True
+
+    def rng_wait(self):
+        if getattr(self, "_rng_ev_live", False):
+            self._rng_ev.synchronize()
+            self._rng_ev_live = False
+
+    @property
+    def rng_async_out(self) -> np.ndarray:
+        return self._rng_pinned()[1].numpy().view(np.uint32)
 
     # ---- steps -----------------------------------------------------------------------
     def set_graphs(self, on: bool):
@@ -458,6 +539,7 @@ class LearnEngine:
 
     def ctrl(self) -> C.Ctrl:
         """Snapshot of the device control block (synchronises)."""
+        self.launch_recorded()
         raw = self.ctrl_bytes.cpu().numpy().tobytes()
         return C.Ctrl.from_buffer_copy(raw[:ctypes.sizeof(C.Ctrl)])
 

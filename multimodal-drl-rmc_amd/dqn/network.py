@@ -73,6 +73,8 @@ class Network(nn.Module):
         """Greedy actions through dqnx_act: obs staged through pinned memory, one launch, the
         actions copied back and the stream synchronised once (the caller needs a list)."""
         spec, flat = self._native_act()
+        if self._engine is not None:
+            self._engine.launch_recorded()   # the agent's recorded learn step updates these weights first
         x = T.as_tensor(obses, dtype=T.float32)
         n = x.shape[0]
         x = x.reshape(n, -1)
@@ -142,7 +144,14 @@ class Network(nn.Module):
         self.load_state_dict({k: T.as_tensor(v, device=self.device) for k, v in params.items()})
         return step, episode_count, rew_mean, len_mean
 
+    def state_dict(self, *args, **kwargs):
+        if self._engine is not None:   # an agent's recorded learn step lands first (stream order)
+            self._engine.launch_recorded()
+        return super().state_dict(*args, **kwargs)
+
     def load_state_dict(self, state_dict, *args, **kwargs):
+        if self._engine is not None:
+            self._engine.launch_recorded()
         out = super().load_state_dict(state_dict, *args, **kwargs)
         if self._engine is not None:   # written into the engine's buffer: refresh its derived layouts
             self._engine.params_modified()

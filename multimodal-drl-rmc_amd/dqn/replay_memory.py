@@ -46,6 +46,7 @@ class RingView:
 
     def rows(self, slots):
         e = self.engine
+        e.launch_recorded()
         s = torch.as_tensor(np.asarray(slots, dtype=np.int64), device=e.device)
         D = e.spec.obs_dim
         obs = e.ring_obs.index_select(0, s)[:, :D].cpu().numpy()
@@ -72,6 +73,7 @@ class SumTreeView:
 
     @property
     def tree(self) -> np.ndarray:
+        self.engine.launch_recorded()
         return self.engine.sumtree.cpu().numpy()
 
     @property
@@ -121,6 +123,7 @@ class ReplayMemory:
         """Push the n_env transitions (host arrays) and yield the indices whose `done` is set
         (R:dqn/replay_memory.py:30-36 / 56-67)."""
         n = len(actions)
+        self.engine.launch_recorded()   # a recorded learn step samples the ring as it was at learn()
         if n:
             self.engine.push(np.asarray(obses, dtype=np.float32).reshape(n, -1),
                              np.asarray(actions).reshape(n), np.asarray(rews, dtype=np.float32).reshape(n),
@@ -143,6 +146,7 @@ class ReplayMemoryNaive(ReplayMemory):
     def sample_transitions(self, step=None):
         # random.sample over a sequence only uses its length to draw positions, so sampling
         # range(len) consumes the global stream exactly like sampling the deque
+        self.engine.settle()
         pos = random.sample(range(len(self.replay_buffer)), self.batch_size)
         return self.replay_buffer.rows([self.replay_buffer.slot(p) for p in pos])
 
@@ -165,6 +169,7 @@ class ReplayMemoryPrioritized(ReplayMemory):
         """(is_weights, tree_indices, transitions) drawn from numpy's global RandomState,
         which is advanced exactly as the reference's np.random.uniform calls would."""
         e = self.engine
+        e.settle()
         e.set_np_state_from_global()
         e.set_agent_step(int(step))
         e.per_sample()
@@ -179,6 +184,7 @@ class ReplayMemoryPrioritized(ReplayMemory):
 
     def update_batch_priorities(self, tree_indices, abs_td_errors_np):
         e = self.engine
+        e.launch_recorded()
         slots = torch.as_tensor(np.asarray(tree_indices, dtype=np.int64) - (e.capacity - 1), dtype=torch.int32)
         absd = torch.as_tensor(np.asarray(abs_td_errors_np, dtype=np.float32).reshape(-1))
         e.per_update_priorities(slots, absd)

@@ -81,6 +81,7 @@ def test_gpu_agent_train_loop_matches_oracle(tmp_path, algo, obs_dim, batch, buf
         agent.update_target_network()
         rec = oracle.learn()
         oracle.update_target_network()
+        agent.flush()   # the advanced sampler RNG reaches the global state at the next agent call
         torch.cuda.synchronize()
         assert np.array_equal(np.asarray(random.getstate()[1], dtype=np.uint32), oracle.py_state)
         assert np.array_equal(O.np_state_to_array(), oracle.np_state)
@@ -182,3 +183,42 @@ def test_gpu_agent_drives_gymnasium_env_through_adapter(tmp_path):
         ro, ra, rr, rd, rno = ring[i]
         assert np.array_equal(ro, o) and ra == a and rr == np.float32(r) and rd == d and np.array_equal(rno, no), i
     assert agent.episode_count == sum(1 for s in seen if s[3])
+
+
+@pytest.mark.parametrize("algo,soft", [("DuelingDoubleDQNAgent", True), ("DuelingDoubleDQNAgent", False),
+                                       ("PerDuelingDoubleDQNAgent", True), ("DQNAgent", True)])
+def test_gpu_agent_deferred_learn_bit_identical(tmp_path, monkeypatch, algo, soft):
+    """learn() records the step and the next agent call launches it (update_target_network with the
+    soft update fused into the Adam pass; RNG hand-back through pinned buffers, installed lazily):
+    bitwise the synchronous learn() (DQNX_AGENT_DEFER=0) over a train.py loop, hard target updates
+    (every 3 steps) included, the global RNG states after every iteration and the logged loss."""
+    runs = []
+    for defer in ("0", "1"):
+        monkeypatch.setenv("DQNX_AGENT_DEFER", defer)
+        torch.manual_seed(5)
+        agent = getattr(Agents, algo)(**agent_kwargs(algo, 284, 64, 1000, tmp_path, target_soft_update=soft,
+                                                     update_target_frequency=3))
+        obs, act, rew, done, nobs = O.synth_transitions(800, 284, 8, seed=9)
+        for i in range(700):
+            agent.store_transitions(obs[i:i + 1], [int(act[i])], [float(rew[i])], [bool(done[i])], nobs[i:i + 1],
+                                    None)
+        random.seed(3)
+        np.random.seed(3)
+        states = []
+        for t in range(8):
+            agent.step = t
+            agent.epsilon_start = 0.5
+            a = agent.choose_actions(obs[700 + t:701 + t])
+            agent.store_transitions(obs[700 + t:701 + t], a, [float(rew[700 + t])], [False], nobs[700 + t:701 + t], None)
+            agent.learn()
+            agent.update_target_network()
+            states.append((a, random.getstate() if defer == "0" else None))
+        agent.flush()
+        torch.cuda.synchronize()
+        runs.append((agent, states, random.getstate(), np.random.get_state()[1].copy(), agent.engine.loss()))
+    (a0, s0, r0, n0, l0), (a1, s1, r1, n1, l1) = runs
+    assert [x[0] for x in s0] == [x[0] for x in s1]
+    assert r0 == r1 and np.array_equal(n0, n1) and l0 == l1
+    assert torch.equal(a0.engine.params, a1.engine.params)
+    assert torch.equal(a0.engine.target_params, a1.engine.target_params)
+    assert torch.equal(a0.engine.adam_m, a1.engine.adam_m)

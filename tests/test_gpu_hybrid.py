@@ -20,7 +20,7 @@ def _E():
     return E
 
 
-def make_hybrid_pair(algo, batch, cap, n_fill, seed, graphs=True, micro_chw=(2, 27, 5)):
+def make_hybrid_pair(algo, batch, cap, n_fill, seed, graphs=False, micro_chw=(2, 27, 5)):
     E = _E()
     head = O.algo_spec_head(algo)
     ospec = O.hybrid_spec(8, head, micro_chw=micro_chw)
@@ -212,3 +212,39 @@ def test_gpu_hybrid_inlaunch_prefetch_bit_identical(algo, batch, grads_only):
     assert torch.equal(e1.q, e2.q) and torch.equal(e1.grads, e2.grads)
     assert torch.equal(e1.params, e2.params) and torch.equal(e1.target_params, e2.target_params)
     assert np.array_equal(e1.get_rng(0), e2.get_rng(0))
+
+
+@pytest.mark.parametrize("algo", ["DuelingDoubleDQNAgent", "PerDuelingDoubleDQNAgent"])
+def test_gpu_hybrid_adam_written_conv_copies_bit_identical(algo):
+    """Eager micro-CNN steps skip the conv_perm launch while the permuted conv weight copies are
+    current: the previous step's Adam pass wrote them next to every updated conv weight (wide slab
+    path).  Against an engine replaying graphs (which always launch conv_perm): bitwise equal through
+    hard / soft updates, a direct parameter write (+ params_modified) and a data-parallel style
+    GRADS_ONLY step + apply_grads, each of which leaves the copies stale."""
+    o1, e1 = make_hybrid_pair(algo, 64, 1000, 700, 71, graphs=False)
+    o2, e2 = make_hybrid_pair(algo, 64, 1000, 700, 71, graphs=True)
+
+    def both(fn):
+        fn(e1)
+        fn(e2)
+    for i in range(7):
+        both(lambda e: e.learn_step(soft_update=True))
+        if i == 1:
+            both(lambda e: e.hard_update())
+        if i == 2:
+            both(lambda e: e.soft_update())
+        if i == 3:   # a host-side write through the torch views
+            def poke(e):
+                v = e.param_views(e.params)
+                k = next(k for k in v if "cnn_stream.2.weight" in k)
+                v[k].mul_(0.5)
+                e.params_modified()
+            both(poke)
+        if i == 4:
+            both(lambda e: e.learn_step(grads_only=True))
+            both(lambda e: e.apply_grads(soft_update=True))
+    torch.cuda.synchronize()
+    e1.check_device_error()
+    e2.check_device_error()
+    assert torch.equal(e1.q, e2.q) and torch.equal(e1.grads, e2.grads)
+    assert torch.equal(e1.params, e2.params) and torch.equal(e1.target_params, e2.target_params)
