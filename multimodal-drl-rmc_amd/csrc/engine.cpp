@@ -2195,6 +2195,59 @@ int enqueue_apply(dqnx_engine* e, int flags, hipStream_t s) {
     aa.lrd = c.lr;
     aa.batch_global = e->Bg;
     aa.with_loss = 1;
+    if (keep_blk && dw_adam16_on(e, DQNX_STEP_GRADS_ONLY) && route_knob("DQNX_APPLY_TILES", 1) != 0) {
+        // fused plan: k_dw_adam16 in apply mode -- 32 x 16 parameter tiles, the same per-element
+        // update as k_adam, and each tile's blocked copies as (near-)contiguous blocks instead of
+        // k_adam's per-element scattered stores (the DP shard step's last launch)
+        DwAdam16Args da;
+        memset(&da, 0, sizeof(da));
+        const NetPlan& np = e->np;
+        const int L = (int)np.dense.size();
+        da.rows16 = 2;
+        int tiles = 0;
+        for (int q = 0; q <= L; q++) {   // dense layers last-first, then the head (any tiling: elementwise)
+            const int l = q < L ? L - 1 - q : -1;
+            DwAdam16Layer& d = da.L[da.nl++];
+            d.in = l >= 0 ? np.dense[l].in : np.F;
+            d.out = l >= 0 ? np.dense[l].out : np.NH;
+            d.poff = l >= 0 ? np.dense[l].off : np.head_off;
+            d.head_kind = l >= 0 ? -1 : c.net.head;
+            d.A = c.net.n_actions;
+            d.ti = (d.in + 15) / 16;
+            d.t0 = tiles;
+            tiles += d.ti * ((d.out + 31) / 32);
+            if (l >= 0) {
+                d.fwd_online = at<float>(e, e->ws_wblk[0][l]);
+                d.fwd_target = at<float>(e, e->ws_wblk[1][l]);
+                d.chain = l >= 1 ? at<float>(e, e->ws_wblkT[l]) : nullptr;
+                d.nch_fwd = e->fplan.kpad[l] / 16;
+                d.nch_chain = np.dense[l].out / 16;
+            }
+            d.dZ = aa.grads;   // (no K loop: never read)
+            d.X = aa.grads;
+            d.ldz = d.ldx = 1;
+        }
+        da.tiles = tiles;
+        da.Bl = 0;
+        da.mode = 3;
+        da.soft = aa.soft;
+        da.n_params = np.P;
+        da.p = aa.p;
+        da.m = aa.m;
+        da.v = aa.v;
+        da.grads = aa.grads;
+        da.target = aa.target;
+        da.ctrl = aa.ctrl;
+        da.w1 = aa.w1;
+        da.beta2 = aa.beta2;
+        da.c2 = aa.c2;
+        da.eps = aa.eps;
+        da.tau = aa.tau;
+        da.one_minus_tau = aa.one_minus_tau;
+        da.batch_global = e->Bg;
+        da.stamps = at<int64_t>(e, e->ws_stamps);
+        return launch_dw_adam16(da, s);
+    }
     fill_blk_layers(e, aa, keep_blk);
     return launch_adam(aa, s);
 }

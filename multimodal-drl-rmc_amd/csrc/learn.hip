@@ -1082,10 +1082,12 @@ __global__ __launch_bounds__(64 * DW16_NW) void k_dw_adam16(DwAdam16Args a) {
     int row[NS], col[NS];
     bool own[NS];
     int64_t e[NS];
-    float p[NS], m[NS], v[NS], tg[NS];
+    float p[NS], m[NS], v[NS], tg[NS], ga[NS];
+    const bool apply = a.mode == 3;   // the gradient is in `grads` already (all-reduced): no K loop
 #pragma unroll
     for (int j = 0; j < NS; j++) {
         const int q = tid + j * NT;
+        ga[j] = 0.f;
         if (q < NW_) {
             row[j] = o0 + (q >> 4);
             col[j] = i0 + (q & 15);
@@ -1102,6 +1104,7 @@ __global__ __launch_bounds__(64 * DW16_NW) void k_dw_adam16(DwAdam16Args a) {
             m[j] = gld(a.m + e[j]);
             v[j] = gld(a.v + e[j]);
             if (a.soft) tg[j] = gld(a.target + e[j]);
+            if (apply) ga[j] = gld(a.grads + e[j]);
         }
     }
     const float step_size = gld(&a.ctrl->adam_step_size), bc2s = gld(&a.ctrl->adam_bc2_sqrt);
@@ -1113,7 +1116,7 @@ __global__ __launch_bounds__(64 * DW16_NW) void k_dw_adam16(DwAdam16Args a) {
     //     without a branch.  Columns past the layer are clamped (their accumulator rows /
     //     columns are never stored).  A wave owns a multiple of 2U k-steps, so the loop has no
     //     tail.
-    const int nsteps = (a.Bl + 3) >> 2;
+    const int nsteps = apply ? 0 : (a.Bl + 3) >> 2;
     const int spw = ((nsteps + DW16_NW - 1) / DW16_NW + 2 * U - 1) / (2 * U) * (2 * U);
     const int s0 = wid * spw;
     const int iters = s0 < nsteps ? spw / (2 * U) : 0;
@@ -1185,7 +1188,9 @@ __global__ __launch_bounds__(64 * DW16_NW) void k_dw_adam16(DwAdam16Args a) {
         if (!own[j]) continue;
         const int q = tid + j * NT;
         float gsum;
-        if (q < NW_) {   // row block r = q / 256 of the tile; the same order for every R
+        if (apply) {
+            gsum = ga[j];
+        } else if (q < NW_) {   // row block r = q / 256 of the tile; the same order for every R
             const float* rf = reinterpret_cast<const float*>(&red[0][0][0]) + (q >> 8) * 256;
             const int qq = q & 255, rr = qq >> 4, off = ((rr >> 2) * 16 + (qq & 15)) * 4 + (rr & 3);
             gsum = rf[off];
@@ -1197,7 +1202,7 @@ __global__ __launch_bounds__(64 * DW16_NW) void k_dw_adam16(DwAdam16Args a) {
 #pragma unroll
             for (int k = 1; k < 4 * DW16_NW; k++) gsum += redb[k >> 2][rb][(k & 3) * 16 + rr];
         }
-        a.grads[e[j]] = gsum;
+        if (!apply) a.grads[e[j]] = gsum;
         if (!a.mode) continue;
         float mk = fmaf(a.w1, gsum - m[j], m[j]);
         float vk = v[j] * a.beta2;
@@ -1220,7 +1225,8 @@ __global__ __launch_bounds__(64 * DW16_NW) void k_dw_adam16(DwAdam16Args a) {
         }
     }
     DQNX_STAMP(a.stamps, 60);
-    if (T == 0 && wid == DW16_NW - 1 && a.loss_partial) {   // one wave, k_adam's fixed order
+    if (apply && T == 0 && tid == 0) a.ctrl->loss = a.grads[a.n_params];   // (the all-reduced loss slot)
+    if (!apply && T == 0 && wid == DW16_NW - 1 && a.loss_partial) {   // one wave, k_adam's fixed order
         float s = 0.f;
         for (int j = lane; j < a.n_loss_partial; j += 64) s += a.loss_partial[j];
 #pragma unroll

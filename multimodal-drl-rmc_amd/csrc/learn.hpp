@@ -290,7 +290,8 @@ struct DwAdam16Args {
     int tiles;             // parameter tiles (+ 1 workgroup for the MT cache when mtc)
     int rows16;            // 16-row blocks of W per tile (1: 16 x 16 tiles; 2: 32 x 16)
     int Bl;
-    int mode;              // 0: gradients (+ loss) only, the DP all-reduce and Adam pass follow; 1: + Adam
+    int mode;              // 0: gradients (+ loss) only, the DP all-reduce and Adam pass follow; 1: + Adam;
+                           // 3: Adam from `grads` (dqnx_apply_grads after the all-reduce: no K loop)
     int soft;
     int64_t n_params;
     float* p;

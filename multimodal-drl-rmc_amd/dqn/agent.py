@@ -217,17 +217,19 @@ class Agent:
 
     def _rng_to_engine(self):
         if self._rng_which == C.DQNX_RNG_PY:
-            self.engine.set_rng_async(C.DQNX_RNG_PY, random.getstate()[1])
+            st = random.getstate()
+            self._py_state_meta = st   # (version, -, gauss_next): restored around the new words
+            self.engine.set_rng_async(C.DQNX_RNG_PY, st[1])
         else:
             st = np.random.get_state()
             self.engine.set_rng_async(C.DQNX_RNG_NP, np.append(np.asarray(st[1], dtype=np.uint32), np.uint32(st[2])))
 
     def _rng_from_engine(self):
-        a = self.engine.rng_async_out
         if self._rng_which == C.DQNX_RNG_PY:
-            v, _, g = random.getstate()
-            random.setstate((v, tuple(a.tolist()), g))
+            v, _, g = self._py_state_meta
+            random.setstate((v, self.engine.rng_async_out_tuple(), g))
         else:
+            a = self.engine.rng_async_out
             st = np.random.get_state()
             np.random.set_state((st[0], a[:624].copy(), int(a[624]), st[3], st[4]))
 

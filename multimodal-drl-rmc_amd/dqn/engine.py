@@ -11,6 +11,7 @@ from __future__ import annotations
 
 import ctypes
 import random
+import struct
 from dataclasses import dataclass
 from typing import Optional, Sequence, Tuple
 
@@ -411,12 +412,18 @@ class LearnEngine:
                              torch.empty(625, dtype=torch.int32).pin_memory())
             self._rng_ev = torch.cuda.Event()
             self._rng_ev_live = False
+            self._rng_pin_np = tuple(t.numpy().view(np.uint32) for t in self._rng_pin)
         return self._rng_pin
 
     def set_rng_async(self, which: int, state625) -> None:
+        """state625: 625 words -- a numpy array, or a tuple of Python ints (random.getstate()[1],
+        packed straight into the pinned buffer: no 625-object numpy conversion)."""
         src, _ = self._rng_pinned()
         self.rng_wait()                    # the previous copies out of / into the pinned buffers ran
-        src.numpy().view(np.uint32)[:] = state625
+        if isinstance(state625, tuple):
+            struct.pack_into("625I", self._rng_pin_np[0], 0, *state625)
+        else:
+            self._rng_pin_np[0][:] = state625
         C.check(self.L.dqnx_rng_set_async(self.h, which, ctypes.c_void_p(src.data_ptr()), self.stream()),
                 "rng_set_async")
 
@@ -434,7 +441,13 @@ class LearnEngine:
 
     @property
     def rng_async_out(self) -> np.ndarray:
-        return self._rng_pinned()[1].numpy().view(np.uint32)
+        self._rng_pinned()
+        return self._rng_pin_np[1]
+
+    def rng_async_out_tuple(self) -> tuple:
+        """The downloaded 625 words as a tuple of Python ints (random.setstate's format)."""
+        self._rng_pinned()
+        return struct.unpack("625I", self._rng_pin_np[1].tobytes())
 
     # ---- steps -----------------------------------------------------------------------
     def set_graphs(self, on: bool):

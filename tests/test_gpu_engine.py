@@ -579,3 +579,36 @@ def test_gpu_push_refused_with_pending_prefetch(monkeypatch, plan):
         e.push(*O.synth_transitions(2, 14, 8, seed=1))
     e.learn_step()
     torch.cuda.synchronize()
+
+
+@pytest.mark.parametrize("world,k", [(8, 4096), (1, 1024), (2, 1024)])
+def test_gpu_apply_grads_tiles_bit_identical(monkeypatch, world, k):
+    """dqnx_apply_grads on the fused plan with a prefetched minibatch pending (the DP shard step):
+    k_dw_adam16 in apply mode (32 x 16 tiles, blocked copies per tile, the default) against k_adam's
+    per-element pass (DQNX_APPLY_TILES=0): the same update and blocked copies, so every later step
+    is bitwise equal too."""
+    E = _engine_mod()
+    ospec = O.mlp_spec(284, 8, "dueling")
+    init = O.reference_init(ospec, 43)
+    data = O.synth_transitions(9000, 284, 8, seed=143)
+    engines = []
+    for tiles in ("0", "1"):
+        monkeypatch.setenv("DQNX_APPLY_TILES", tiles)
+        eng = E.LearnEngine(E.mlp_spec(284, 8, "dueling"), "DuelingDoubleDQNAgent", k, 9000,
+                            world_size=world, rank=0)
+        eng.load_params(init)
+        eng.push(*data)
+        random.seed(49)
+        eng.set_rng(0, O.py_state_to_array())
+        for i in range(4):
+            eng.learn_step(grads_only=True, prefetch=i < 3)
+            eng.apply_grads(soft_update=True)
+        torch.cuda.synchronize()
+        eng.check_device_error()
+        engines.append(eng)
+    e1, e2 = engines
+    assert torch.equal(e1.q, e2.q) and torch.equal(e1.grads, e2.grads)
+    assert torch.equal(e1.params, e2.params) and torch.equal(e1.target_params, e2.target_params)
+    assert torch.equal(e1.adam_m, e2.adam_m) and torch.equal(e1.adam_v, e2.adam_v)
+    assert e1.loss() == e2.loss()
+
