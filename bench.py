@@ -101,6 +101,9 @@ def parse():
                    help="N = 1, uniform replay: do not draw step t+1's minibatch inside step t's last launch "
                         "(DQNX_STEP_PREFETCH; on by default for this pure learning loop)")
     p.add_argument("--prefetch", action="store_true", help="(the default; kept for old command lines)")
+    p.add_argument("--per-numpy121", action="store_true",
+                   help="PER: the SumTree arithmetic of the reference's pinned numpy 1.21 (float32 change and "
+                        "ancestor sums in update order, k_per_chain) instead of numpy >= 2's float64")
     a = p.parse_args()
     if a.capacity is None:
         a.capacity = 100_000 if a.net == "hybrid84" else 1_000_000
@@ -306,7 +309,8 @@ def set_rngs(eng, per, rank_seed=0):
 
 def make_engine(args, spec, batch_global, world, rank, device, local=False):
     eng = LearnEngine(spec, args.algo, batch_global, args.capacity, world_size=world, rank=rank, device=device,
-                      graphs=args.graphs, local_sampling=local, compute_dtype=args.compute)
+                      graphs=args.graphs, local_sampling=local, compute_dtype=args.compute,
+                      per_numpy121=getattr(args, "per_numpy121", False))
     eng.load_params(init_params(spec, 0))
     fill_ring(eng, args.capacity, spec.obs_dim, args.actions, device, seed=0)
     set_rngs(eng, args.algo.startswith("Per"), rank if local else 0)

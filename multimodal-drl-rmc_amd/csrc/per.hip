@@ -648,8 +648,12 @@ __device__ __forceinline__ void chain_sort(unsigned long long* keys, int N2) {
 
 template <bool LEAF>
 __global__ __launch_bounds__(PER_CHAIN_NT) void k_per_chain(PerUpdateArgs a) {
-    extern __shared__ unsigned long long keys[];   // [N2], then (ancestor pass) [n] float changes
-    const int n = a.n, tid = threadIdx.x;
+    // LDS: keys [N2] (u64), then chg [n] (float; the ancestor pass reuses it for the chain starts),
+    // then schg [n] (the changes in sorted order)
+    extern __shared__ unsigned long long keys[];
+    __shared__ int wave_cnt[PER_CHAIN_NT / 64];
+    __shared__ int s_nst;
+    const int n = a.n, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     int N2 = 1;
     while (N2 < n) N2 <<= 1;
     float* chg = reinterpret_cast<float*>(keys + N2);
@@ -669,12 +673,12 @@ __global__ __launch_bounds__(PER_CHAIN_NT) void k_per_chain(PerUpdateArgs a) {
     }
     __syncthreads();
     chain_sort(keys, N2);
-    for (int i = tid; i < n; i += PER_CHAIN_NT) {
-        const unsigned long long k = keys[i];
-        if (k == ~0ull) continue;
-        const int64_t node = (int64_t)(k >> 13);
-        if (i > 0 && (int64_t)(keys[i - 1] >> 13) == node) continue;   // not the start of a chain
-        if (LEAF) {
+    if (LEAF) {
+        for (int i = tid; i < n; i += PER_CHAIN_NT) {
+            const unsigned long long k = keys[i];
+            if (k == ~0ull) continue;
+            const int64_t node = (int64_t)(k >> 13);
+            if (i > 0 && (int64_t)(keys[i - 1] >> 13) == node) continue;   // not the start of a chain
             float prev = (float)a.winit[(int)(k & 8191u)];   // the leaf before this chunk
             for (int j = i; j < n && (int64_t)(keys[j] >> 13) == node; j++) {
                 const int u = (int)(keys[j] & 8191u);
@@ -683,21 +687,114 @@ __global__ __launch_bounds__(PER_CHAIN_NT) void k_per_chain(PerUpdateArgs a) {
                 prev = p;
             }
             a.tree[node] = (double)prev;
-        } else {
-            float v = (float)a.tree[node];
-            for (int j = i; j < n && (int64_t)(keys[j] >> 13) == node; j++) v = v + chg[(int)(keys[j] & 8191u)];
-            a.tree[node] = (double)v;
         }
+        return;
+    }
+    // ---- ancestor pass ----
+    // (1) the changes in sorted (node, item) order; (2) the chain starts, compacted in order (a block
+    // scan over 8 consecutive positions per thread); (3) a WAVE per chain: 64 sorted changes per round
+    // in the lanes, the node's float32 running sum carried through them in item order by readlane
+    // (v = f32(v + change), the reference's sequence), so a chain costs ~2 instructions per update
+    // instead of a dependent LDS round trip per update (the root's chain is the whole batch)
+    float* schg = chg + n;
+    for (int i = tid; i < n; i += PER_CHAIN_NT) {
+        const unsigned long long k = keys[i];
+        schg[i] = k == ~0ull ? 0.f : chg[(int)(k & 8191u)];
+    }
+    __syncthreads();
+    constexpr int IPT = PER_CHUNK / PER_CHAIN_NT;   // positions per thread in the scan
+    int flags = 0, cnt = 0;
+#pragma unroll
+    for (int q = 0; q < IPT; q++) {
+        const int i = tid * IPT + q;
+        bool st = false;
+        if (i < n) {
+            const unsigned long long k = keys[i];
+            st = k != ~0ull && (i == 0 || (keys[i - 1] >> 13) != (k >> 13));
+        }
+        flags |= st ? (1 << q) : 0;
+        cnt += st ? 1 : 0;
+    }
+    int incl = cnt;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(incl, o);
+        if (lane >= o) incl += y;
+    }
+    if (lane == 63) wave_cnt[wid] = incl;
+    __syncthreads();   // (every schg / chg read above is done before the starts overwrite chg)
+    int before = incl - cnt, total = 0;
+#pragma unroll
+    for (int w = 0; w < PER_CHAIN_NT / 64; w++) {
+        const int c = wave_cnt[w];
+        before += w < wid ? c : 0;
+        total += c;
+    }
+    int* starts = reinterpret_cast<int*>(chg);
+#pragma unroll
+    for (int q = 0; q < IPT; q++)
+        if (flags & (1 << q)) starts[before++] = tid * IPT + q;
+    int nvalid = 0;   // positions holding a key (the no-ancestor keys sort last)
+    if (tid == 0) s_nst = total;
+    __syncthreads();
+    const int nst = s_nst;
+    {   // nvalid: the first position past the last valid key (binary search, every thread alike)
+        int lo = 0, hi = n;
+        while (lo < hi) {
+            const int m = (lo + hi) >> 1;
+            if (keys[m] != ~0ull) lo = m + 1;
+            else hi = m;
+        }
+        nvalid = lo;
+    }
+    // short chains (deep levels: thousands of 1-3 update chains): a thread each, every tree value of
+    // the thread's chains loaded before the first walk
+    constexpr int LONG = 128, CPT = PER_CHUNK / PER_CHAIN_NT;
+    {
+        int c0[CPT], c1[CPT];
+        int64_t nd[CPT];
+        double tv[CPT];
+#pragma unroll
+        for (int k = 0; k < CPT; k++) {
+            const int c = tid + k * PER_CHAIN_NT;
+            c0[k] = c < nst ? starts[c] : 0;
+            c1[k] = c < nst ? (c + 1 < nst ? starts[c + 1] : nvalid) : 0;
+            if (c1[k] - c0[k] >= LONG) c1[k] = c0[k];   // a wave's below
+            nd[k] = (int64_t)(keys[c0[k]] >> 13);
+            tv[k] = c1[k] > c0[k] ? a.tree[nd[k]] : 0.0;
+        }
+#pragma unroll
+        for (int k = 0; k < CPT; k++) {
+            if (c1[k] <= c0[k]) continue;
+            float v = (float)tv[k];
+            for (int j = c0[k]; j < c1[k]; j++) v = v + schg[j];
+            a.tree[nd[k]] = (double)v;
+        }
+    }
+    // long chains (the top levels; the root's is the whole batch): a wave each, 64 sorted changes per
+    // round in the lanes, the running sum carried through them in item order by readlane
+    for (int c = wid; c < nst; c += PER_CHAIN_NT / 64) {
+        const int s0 = starts[c], e0 = c + 1 < nst ? starts[c + 1] : nvalid;
+        if (e0 - s0 < LONG) continue;
+        const int64_t node = (int64_t)(keys[s0] >> 13);
+        float v = (float)a.tree[node];
+        for (int j0 = s0; j0 < e0; j0 += 64) {
+            const int len = min(64, e0 - j0);
+            const float cv = lane < len ? schg[j0 + lane] : 0.f;
+            const int cvi = __float_as_int(cv);
+            for (int q = 0; q < len; q++) v = v + __int_as_float(__builtin_amdgcn_readlane(cvi, q));
+        }
+        if (lane == 0) a.tree[node] = (double)v;
     }
 }
 
-// the ancestor pass needs up to 96 KB of dynamic LDS: raise the limit once, outside any
+// the ancestor pass needs up to 128 KB of dynamic LDS: raise the limit once, outside any
 // stream capture (dqnx_engine_create with per_numpy121)
 int per_numpy121_init() {
     DQNX_HIP_CHECK(hipFuncSetAttribute((const void*)k_per_chain<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                       PER_CHUNK * 12));
+                                       PER_CHUNK * 16));
     DQNX_HIP_CHECK(hipFuncSetAttribute((const void*)k_per_chain<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                       PER_CHUNK * 12));
+                                       PER_CHUNK * 16));
     return DQNX_OK;
 }
 
@@ -723,7 +820,7 @@ int launch_per_update(const PerUpdateArgs& a, hipStream_t s) {
         while (((int64_t)1 << (depths + 1)) <= 2 * a.cap - 1) depths++;
         hipLaunchKernelGGL(k_per_chain<true>, dim3(1), dim3(PER_CHAIN_NT), (size_t)N2 * 8, s, a);
         if (depths > 0)
-            hipLaunchKernelGGL(k_per_chain<false>, dim3(depths), dim3(PER_CHAIN_NT), (size_t)N2 * 8 + (size_t)a.n * 4, s, a);
+            hipLaunchKernelGGL(k_per_chain<false>, dim3(depths), dim3(PER_CHAIN_NT), (size_t)N2 * 8 + (size_t)a.n * 8, s, a);
     } else {
         hipLaunchKernelGGL(k_per_prop, dim3(g), dim3(PER_GT), 0, s, a);
     }
