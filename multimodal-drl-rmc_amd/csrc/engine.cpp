@@ -886,6 +886,19 @@ RelayoutArgs relayout_args(dqnx_engine* e, int* blocks) {
     return r;
 }
 
+// The single-GPU PER step's SumTree update split over the launches that run anyway (round 3): the
+// head kernel does k_per_prep's work, the weight-gradient launch (k_dw_adam16 on 32 x 16 tiles, or
+// k_dw_bf16) runs k_per_prop's workgroups, leaving the order-dependent k_per_update launch.  Not
+// under DP (the |delta| of other shards arrive by all-gather), not in numpy-1.21 mode (k_per_chain),
+// not on the fp32 slab plan.  DQNX_PER_FUSED=0: the three launches.
+bool dw_adam16_on(const dqnx_engine* e, int flags);
+static bool per_fused_update(const dqnx_engine* e, int flags) {
+    if (e->cfg.algo != DQNX_ALGO_PER_DOUBLE || (flags & DQNX_STEP_GRADS_ONLY) || e->cfg.per_numpy121) return false;
+    if (e->bwd_plan != 2 || e->Bg > PER_CHUNK || route_knob("DQNX_PER_FUSED", 1) == 0) return false;
+    if (e->fplan.bf16) return true;
+    return dw_adam16_on(e, flags) && route_knob("DQNX_DW16_R", 2) == 2;
+}
+
 // Fused MLP plan (bwd_plan 2): forward of every layer + head in one launch, head / TD /
 // dZ chain in one launch, every dW in one split-K launch, then the Adam pass.
 void build_fused_steps(dqnx_engine* e, int flags, int32_t* idx, int32_t* phys, std::vector<KStep>& ks,
@@ -1043,6 +1056,14 @@ void build_fused_steps(dqnx_engine* e, int flags, int32_t* idx, int32_t* phys, s
         for (int l = 1; l < L; l++) ha.wblkT[l] = at<float>(e, e->ws_wblkT[l]);
         ha.ab = adam_bias_args(e);
         ha.stamps = at<int64_t>(e, e->ws_stamps);
+        if (per_fused_update(e, flags)) {   // the single-GPU PER step: k_per_prep's work per sample here
+            ha.pp = per_update_args(e);
+            ha.pp.mode = 0;
+            ha.pp.n = e->Bg;
+            ha.pp.slots = idx;
+            ha.pp.abs_td = at<float>(e, e->off[DQNX_BUF_PER_ABS_TD]);
+            ha.pp_on = 1;
+        }
         KStep k;
         k.name = "head_bwd";
         double dzf = 2.0 * Bl * 16 * np.F, dzb = 0;
@@ -1056,12 +1077,25 @@ void build_fused_steps(dqnx_engine* e, int flags, int32_t* idx, int32_t* phys, s
         k.run = [=](hipStream_t s) { return launch_head_bwd(ha, act, s); };
         ks.push_back(k);
     }
-    // 3b. PER priorities (single GPU; under DP after the all-gather, in dqnx_apply_grads)
+    // 3b. PER priorities (single GPU; under DP after the all-gather, in dqnx_apply_grads).  Fused:
+    //     the head kernel did k_per_prep's work, the gradient launch below runs k_per_prop's
+    //     workgroups beside its tiles, so only the order-dependent tracking launch remains here
+    PerUpdateArgs pua;
+    const bool per_fused = per_fused_update(e, flags);
+    if (per_fused) {
+        pua = per_update_args(e);
+        pua.mode = 0;
+        pua.n = e->Bg;
+        pua.slots = idx;
+        pua.abs_td = at<float>(e, e->off[DQNX_BUF_PER_ABS_TD]);
+        pua.skip = PER_SKIP_PREP | PER_SKIP_PROP;
+    }
     if (c.algo == DQNX_ALGO_PER_DOUBLE && !(flags & DQNX_STEP_GRADS_ONLY)) {
         KStep k;
         k.name = "per_update";
         k.bytes = e->Bg * (4.0 + 4.0 + 8.0 * 2.0 * 21.0);
-        k.run = [=](hipStream_t s) { return enqueue_per_update(e, idx, s); };
+        if (per_fused) k.run = [=](hipStream_t s) { return launch_per_update(pua, s); };
+        else k.run = [=](hipStream_t s) { return enqueue_per_update(e, idx, s); };
         ks.push_back(k);
     }
     // 4. every weight gradient: split-K slabs of dZ_l^T [X_l | 1] and dHead^T [H_L | 1]
@@ -1177,6 +1211,10 @@ void build_fused_steps(dqnx_engine* e, int flags, int32_t* idx, int32_t* phys, s
                 da.mtc = nullptr;   // the forward's sampler body draws from the MT state itself
                 da.mtc_blocks = 0;
             }
+            if (per_fused) {
+                da.pprop = pua;
+                da.pprop_wgs = (e->Bg + 511) / 512;
+            }
             const double P = (double)np.P;
             KStep k;
             k.name = da.mode ? "dw_adam16" : "dw16_grads";
@@ -1196,6 +1234,10 @@ void build_fused_steps(dqnx_engine* e, int flags, int32_t* idx, int32_t* phys, s
         }
         if (e->fplan.bf16) {   // bf16 operands, fp32 slabs: the same Adam pass follows
             dw_bf16_grid(ba);
+            if (per_fused) {
+                ba.pprop = pua;
+                ba.pprop_wgs = (e->Bg + 255) / 256;
+            }
             KStep k;
             k.name = "dw_all";
             k.flops = flops;
@@ -2166,7 +2208,22 @@ int enqueue_range(const std::vector<KStep>& ks, int a, int b, hipStream_t s) {
 int enqueue_apply(dqnx_engine* e, int flags, hipStream_t s) {
     const bool keep_blk = (flags & 0x200) != 0;   // (a prefetched minibatch is pending: no sampler launch next)
     const dqnx_config& c = e->cfg;
-    if (c.algo == DQNX_ALGO_PER_DOUBLE) {   // priorities from the all-gathered |delta| (DP)
+    // priorities from the all-gathered |delta| (DP); k_per_prop's workgroups ride in the Adam launch
+    // below (DQNX_PER_FUSED=0: its own launch)
+    PerUpdateArgs pua;
+    memset(&pua, 0, sizeof(pua));
+    const bool prop_in_adam = c.algo == DQNX_ALGO_PER_DOUBLE && !c.per_numpy121 && e->Bg <= PER_CHUNK &&
+                              route_knob("DQNX_PER_FUSED", 1) != 0;
+    if (prop_in_adam) {
+        pua = per_update_args(e);
+        pua.mode = 0;
+        pua.n = e->Bg;
+        pua.slots = at<int32_t>(e, e->off[DQNX_BUF_BATCH_IDX]);
+        pua.abs_td = at<float>(e, e->off[DQNX_BUF_PER_ABS_TD]);
+        pua.skip = PER_SKIP_PROP;
+        int rc = launch_per_update(pua, s);
+        if (rc) return rc;
+    } else if (c.algo == DQNX_ALGO_PER_DOUBLE) {
         int rc = enqueue_per_update(e, at<int32_t>(e, e->off[DQNX_BUF_BATCH_IDX]), s);
         if (rc) return rc;
     }
@@ -2246,9 +2303,17 @@ int enqueue_apply(dqnx_engine* e, int flags, hipStream_t s) {
         da.one_minus_tau = aa.one_minus_tau;
         da.batch_global = e->Bg;
         da.stamps = at<int64_t>(e, e->ws_stamps);
+        if (prop_in_adam) {
+            da.pprop = pua;
+            da.pprop_wgs = (e->Bg + 511) / 512;
+        }
         return launch_dw_adam16(da, s);
     }
     fill_blk_layers(e, aa, keep_blk);
+    if (prop_in_adam) {
+        aa.pprop = pua;
+        aa.pprop_wgs = (e->Bg + 255) / 256;
+    }
     return launch_adam(aa, s);
 }
 

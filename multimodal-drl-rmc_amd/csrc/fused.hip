@@ -26,6 +26,7 @@
 // activation tile is shared by all waves and lives in LDS (row stride = 8 mod 64 floats:
 // conflict-free ds_read_b128 fragments, MI355X_MICROARCH.md §LDS).
 #include "learn.hpp"
+#include "per_common.hpp"
 #include "sample_body.hpp"
 
 namespace dqnx {
@@ -682,6 +683,7 @@ __global__ __launch_bounds__(FT) void k_head_bwd(HeadBwdArgs a) {
                 a.td[a.Bl + gb] = qa;
                 a.td[2 * a.Bl + gb] = zabs;
                 if (a.abs_td_out) a.abs_td_out[gb] = zabs;
+                if (a.pp_on) per_prep_item(a.pp, gb, zabs);   // SumTree.update bookkeeping of this sample
             }
         }
     }
@@ -834,6 +836,19 @@ __global__ __launch_bounds__(256) void k_dw_bf16(BwdArgs a) {
     const int i = lane & 15, g = lane >> 4;
     const int wm = wid >> 1, wn = wid & 1;
     int b = blockIdx.x;
+    {   // workgroups past the tiles: k_per_prop's (single-GPU PER step; independent of the gradients)
+        int tiles = 0;
+        for (int p = 0; p < a.ndw; p++) tiles += a.dw[p].blocks;
+        if (b >= tiles) {
+            if constexpr (sizeof(lds) >= PER_TOP * sizeof(double)) {
+                per_prop_block(a.pprop, (b - tiles) * 256, reinterpret_cast<double*>(lds));
+            } else {
+                __shared__ double topd[PER_TOP];
+                per_prop_block(a.pprop, (b - tiles) * 256, topd);
+            }
+            return;
+        }
+    }
     int p = 0;
     while (p + 1 < a.ndw && b >= a.dw[p].blocks) { b -= a.dw[p].blocks; p++; }
     const DwProblem& d = a.dw[p];
@@ -916,7 +931,7 @@ void dw_bf16_grid(BwdArgs& a) {
 }
 
 int launch_dw_bf16(const BwdArgs& a, hipStream_t s) {
-    int blocks = 0;
+    int blocks = a.pprop_wgs;   // (k_per_prop's workgroups: 256 updates each, after the tiles)
     for (int p = 0; p < a.ndw; p++) blocks += a.dw[p].blocks;
     for (int p = 0; p < a.ndw; p++)   // 16-byte row loads
         if (a.dw[p].ldx % 4 || a.dw[p].ldz % 4)

@@ -15,6 +15,7 @@
 #include "gemm_lds.hpp"
 #include "gemm_sk.hpp"
 #include "learn.hpp"
+#include "per_common.hpp"
 #include "mt.hpp"
 
 namespace dqnx {
@@ -681,10 +682,16 @@ __device__ __forceinline__ void blk_store(float* base, int64_t pos, float v, boo
 // the element pass instead of trailing it: at B=4096 the trailing copy cost ~4 us): the sampler's
 // MT block cache (a.mtc), then the in-launch prefetch's copy of the staged minibatch over the
 // compute slot (a.pf_nidx > 0; every reader of the step's minibatch ran in earlier launches).
-__device__ __forceinline__ int adam_extra_count(const AdamArgs& a) { return (a.mtc ? 1 : 0) + (a.pf_nidx > 0 ? 1 : 0); }
+__device__ __forceinline__ int adam_extra_count(const AdamArgs& a) {
+    return (a.mtc ? 1 : 0) + (a.pf_nidx > 0 ? 1 : 0) + a.pprop_wgs;
+}
 __device__ __forceinline__ bool adam_extra_wg(const AdamArgs& a) {
     if ((int)blockIdx.x >= adam_extra_count(a)) return false;
-    if (a.mtc && blockIdx.x == 0) {
+    const int x = (int)blockIdx.x - (a.mtc ? 1 : 0) - (a.pf_nidx > 0 ? 1 : 0);
+    if (x >= 0) {   // k_per_prop's workgroups (the tree; independent of the parameter update)
+        __shared__ double topd[PER_TOP];
+        per_prop_block(a.pprop, x * blockDim.x, topd);
+    } else if (a.mtc && blockIdx.x == 0) {
         mt_cache_extend(a.mtc, a.mtc_blocks);
     } else {
         for (int q = threadIdx.x; q < a.pf_nidx; q += blockDim.x) a.pf_idx_dst[q] = a.pf_idx_src[q];
@@ -1051,8 +1058,12 @@ __global__ __launch_bounds__(64 * DW16_NW) void k_dw_adam16(DwAdam16Args a) {
     __shared__ float redb[DW16_NW][R][64];
     const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int i = lane & 15, g = lane >> 4;
-    if ((int)blockIdx.x >= a.tiles) {   // extra workgroups: sampler cache, then the staged-minibatch copy
-        if (a.mtc && (int)blockIdx.x == a.tiles) {
+    if ((int)blockIdx.x >= a.tiles) {   // extra workgroups: sampler cache, the staged-minibatch copy, PER prop
+        const int x = (int)blockIdx.x - a.tiles - (a.mtc ? 1 : 0) - (a.pf_nidx > 0 ? 1 : 0);
+        if (x >= 0) {   // k_per_prop's body over 64 * DW16_NW updates (the red table as its LDS)
+            if constexpr (sizeof(red) >= PER_TOP * sizeof(double))   // (launch_dw_adam16: 32 x 16 tiles only)
+                per_prop_block(a.pprop, x * 64 * DW16_NW, reinterpret_cast<double*>(&red[0][0][0]));
+        } else if (a.mtc && (int)blockIdx.x == a.tiles) {
             mt_cache_extend(a.mtc, a.mtc_blocks);
         } else {
             // in-launch prefetch: the forward launch drew the next minibatch into the staging slot;
@@ -1241,7 +1252,9 @@ __global__ __launch_bounds__(64 * DW16_NW) void k_dw_adam16(DwAdam16Args a) {
 
 int launch_dw_adam16(const DwAdam16Args& a, hipStream_t s) {
     static const int var = tuning_knob("DQNX_DW16_VAR", 0);
-    const dim3 grid(a.tiles + (a.mtc ? 1 : 0) + (a.pf_nidx > 0 ? 1 : 0));
+    if (a.pprop_wgs && (a.rows16 != 2 || var != 0))
+        return set_error(DQNX_EUNSUPPORTED, "dw_adam16: PER prop workgroups with the default 32 x 16 tiles only");
+    const dim3 grid(a.tiles + (a.mtc ? 1 : 0) + (a.pf_nidx > 0 ? 1 : 0) + a.pprop_wgs);
     if (a.rows16 == 2) {
         switch (var) {   // measurement variants (waves per tile, k-steps per register set)
             case 7: hipLaunchKernelGGL((k_dw_adam16<16, 4, 2>), grid, dim3(1024), 0, s, a); break;
@@ -1495,6 +1508,7 @@ int launch_adam(const AdamArgs& a_in, hipStream_t s) {
     blocks += (int)((wide4 * 8 + 255) / 256);   // ADAM_WIDE lanes per wide float4
     if (a.mtc) blocks++;   // + the sampler-cache workgroup
     if (a.pf_nidx > 0) blocks++;   // + the staged-minibatch copy
+    blocks += a.pprop_wgs;         // + k_per_prop's workgroups (256 updates each)
     if (vec) hipLaunchKernelGGL(k_adam4, dim3(blocks), dim3(256), 0, s, a);
     else hipLaunchKernelGGL(k_adam, dim3(blocks), dim3(256), 0, s, a);
     DQNX_HIP_CHECK(hipGetLastError());

@@ -43,6 +43,36 @@ __device__ __forceinline__ void adam_advance(dqnx_ctrl* ctrl, const AdamBias& b)
     ctrl->adam_bc2_sqrt = bc;
 }
 
+// PER priority writes with SumTree.update's sequential semantics (R:dqn/utils/sum_tree.py:15-32):
+// mode 0 = update_batch_priorities (R:dqn/replay_memory.py:94-98),
+// mode 1 = store_transitions' adds at the current max priority (R:dqn/replay_memory.py:56-67).
+struct PerUpdateArgs {
+    double* tree;
+    int64_t cap;
+    dqnx_ctrl* ctrl;          // per_max_idx / per_min_idx (read + written)
+    int32_t mode;
+    int32_t n;                // updates in this launch (<= PER_CHUNK)
+    const int32_t* slots;     // mode 0: [n] ring slots, in batch order
+    const float* abs_td;      // mode 0: [n] |targets - q(s,a)|
+    int64_t wptr, size;       // mode 1: ring write pointer / size before this chunk (mode 0 reads ctrl)
+    float eps, alpha, pmax;   // numpy float32 arithmetic on the python-float constants
+    int64_t* stamps;          // diagnostic builds (-DDQNX_STAMPS): slots 56..63
+    // workspace shared by the three launches of one chunk (k_per_prep, k_per_update, k_per_prop)
+    int32_t* wl;              // [PER_CHUNK] leaf (tree index) of item i
+    float* wp;                // [PER_CHUNK] its new priority
+    double* winit;            // [PER_CHUNK] the leaf's value before the chunk
+    uint64_t* last;           // [cap] (epoch << 32 | i) of the latest item writing the slot
+    uint32_t* epoch;          // chunk counter (tags `last`; zero after reset, like `last`)
+    // numpy 1.21 arithmetic (dqnx_config.per_numpy121, mode 0 only): `change` and every
+    // ancestor sum rounded to float32, applied in update order (k_per_chain)
+    int32_t numpy121;
+    float* wchg;              // [PER_CHUNK] float32 change of item i
+    // single-GPU PER learn step: k_per_prep's work done by the head kernel for its samples
+    // (PER_SKIP_PREP) and k_per_prop's workgroups run beside the weight-gradient tiles (PER_SKIP_PROP)
+    int32_t skip;
+};
+constexpr int PER_SKIP_PREP = 1, PER_SKIP_PROP = 2;
+
 struct FwdProblem {
     const float* A;        // dense rows, or the replay ring (layer 1, phys != null)
     int lda;
@@ -92,6 +122,8 @@ struct BwdArgs {
     int ndw;
     int Bl, kslice, dw_slices;
     int dx_blocks, dx_grid_x;
+    int pprop_wgs;         // k_dw_bf16: + workgroups running k_per_prop's body (single-GPU PER step)
+    PerUpdateArgs pprop;
 };
 
 struct HeadArgs {
@@ -180,6 +212,8 @@ struct AdamArgs {
     int pf_nphys;
     // micro-CNN plan: the permuted weight copies of convs 2.. (k_conv_perm's layouts) written next to
     // every updated conv weight by the wide path (mode 1), so the next step needs no conv_perm launch
+    int pprop_wgs;         // + workgroups running k_per_prop's body (DP apply: after the all-gathered update)
+    PerUpdateArgs pprop;
     int nperm;
     struct PermLayer {
         int64_t woff;      // flat offset of W [Co][Ci][3][3]
@@ -315,6 +349,8 @@ struct DwAdam16Args {
     const int32_t* pf_phys_src;
     int32_t* pf_phys_dst;
     int pf_nphys;
+    int pprop_wgs;         // + workgroups running k_per_prop's body (single-GPU PER step; 0: none)
+    PerUpdateArgs pprop;
 };
 
 // MT block cache: the state block of the uniform sampler and its twisted successors, kept ahead
@@ -356,31 +392,6 @@ constexpr int NPC_MAX_BLOCKS = 29;   // (624 + 2 PER_MAX_B - 1) / 624 + 1 at PER
 constexpr int64_t np_cache_words() { return 64 + (int64_t)NPC_MAX_BLOCKS * 624; }
 __host__ __device__ constexpr int np_cache_blocks(int Bg) { return (624 + 2 * Bg - 1) / 624 + 1; }
 
-// PER priority writes with SumTree.update's sequential semantics (R:dqn/utils/sum_tree.py:15-32):
-// mode 0 = update_batch_priorities (R:dqn/replay_memory.py:94-98),
-// mode 1 = store_transitions' adds at the current max priority (R:dqn/replay_memory.py:56-67).
-struct PerUpdateArgs {
-    double* tree;
-    int64_t cap;
-    dqnx_ctrl* ctrl;          // per_max_idx / per_min_idx (read + written)
-    int32_t mode;
-    int32_t n;                // updates in this launch (<= PER_CHUNK)
-    const int32_t* slots;     // mode 0: [n] ring slots, in batch order
-    const float* abs_td;      // mode 0: [n] |targets - q(s,a)|
-    int64_t wptr, size;       // mode 1: ring write pointer / size before this chunk (mode 0 reads ctrl)
-    float eps, alpha, pmax;   // numpy float32 arithmetic on the python-float constants
-    int64_t* stamps;          // diagnostic builds (-DDQNX_STAMPS): slots 56..63
-    // workspace shared by the three launches of one chunk (k_per_prep, k_per_update, k_per_prop)
-    int32_t* wl;              // [PER_CHUNK] leaf (tree index) of item i
-    float* wp;                // [PER_CHUNK] its new priority
-    double* winit;            // [PER_CHUNK] the leaf's value before the chunk
-    uint64_t* last;           // [cap] (epoch << 32 | i) of the latest item writing the slot
-    uint32_t* epoch;          // chunk counter (tags `last`; zero after reset, like `last`)
-    // numpy 1.21 arithmetic (dqnx_config.per_numpy121, mode 0 only): `change` and every
-    // ancestor sum rounded to float32, applied in update order (k_per_chain)
-    int32_t numpy121;
-    float* wchg;              // [PER_CHUNK] float32 change of item i
-};
 
 // ---- two-stream hybrid network data movement (conv.hip) ----
 struct Im2colArgs {
@@ -511,6 +522,8 @@ struct HeadBwdArgs {
     const float* wblkT[FUSED_MAX_L];     // chain-blocked online W_l, l >= 1 (relayout.hpp)
     AdamBias ab;
     int64_t* stamps;             // diagnostic builds (-DDQNX_STAMPS): slots 40..55
+    int pp_on;                   // single-GPU PER: k_per_prep's work for this kernel's samples
+    PerUpdateArgs pp;
 };
 bool fused_fwd_plan(FusedFwdArgs& a, int obs_dim, bool bf16, int mr);   // fills sx/sh/buf/kpad; false if unsupported
 int fused_wblk_bytes(bool bf16, int rows, int kpad);          // one blocked weight copy

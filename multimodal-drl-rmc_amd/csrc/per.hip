@@ -16,12 +16,12 @@
 // argmax/argmin rescans -- follow SumTree.update step by step (see k_per_update).
 #include "learn.hpp"
 #include "mt.hpp"
+#include "per_common.hpp"
 
 namespace dqnx {
 
 constexpr int PER_NT = 1024;   // threads of the one-workgroup tracking kernel (256 x 32 items measured
                                // slower: serial per-item LDS lookups, strided LDS stores)
-constexpr int PER_TOP = 2047;            // nodes of depth <= 10, accumulated in LDS by k_per_update
 constexpr int PER_IPT = PER_CHUNK / PER_NT;
 
 // ---------------------------------------------------------------------------------------
@@ -346,16 +346,6 @@ __device__ int64_t block_arg_extreme(const double* tree, int64_t base, int64_t n
     return ri;
 }
 
-// numpy: np.power(np.minimum(abs_td + eps, 1.0), alpha) on float32 (python floats are cast to
-// float32).  The power is correctly rounded (float64 pow rounded once), which is what glibc's
-// powf returns except in rare hard cases; numpy >= 1.22 on AVX-512 hosts may use SVML
-// instead (within 1 ulp).  See DESIGN.md.
-__device__ __forceinline__ float per_priority(float d, float eps, float alpha, float pmax) {
-    float x = d + eps;
-    x = (x > pmax) ? pmax : x;   // NaN propagates like np.minimum
-    return (float)pow((double)x, (double)alpha);
-}
-
 __device__ __forceinline__ uint32_t leaf_hash(uint32_t x) {
     x ^= x >> 16; x *= 0x7feb352du; x ^= x >> 15; x *= 0x846ca68bu; x ^= x >> 16;
     return x;
@@ -384,21 +374,19 @@ __device__ __forceinline__ uint32_t leaf_hash(uint32_t x) {
 //   (final - old) to the ancestors: float64 atomics, the top levels first summed per
 //   workgroup in LDS.  Order-free: every addition is exact (file header).
 // ---------------------------------------------------------------------------------------
-constexpr int PER_GT = 256;   // threads per workgroup of the grid launches
 
 __global__ __launch_bounds__(PER_GT) void k_per_prep(PerUpdateArgs a) {
     const int i = blockIdx.x * PER_GT + threadIdx.x;
     if (i >= a.n) return;
     const int64_t base = a.cap - 1;
-    const int64_t slot = a.mode == 0 ? (int64_t)a.slots[i] : (a.wptr + i) % a.cap;
-    const int32_t L = (int32_t)(slot + base);
-    float p;
     if (a.mode == 0) {
-        p = per_priority(a.abs_td[i], a.eps, a.alpha, a.pmax);
-    } else {   // store_transitions: max_priority, or max_priority_high if 0
-        const double mv = a.tree[a.ctrl->per_max_idx];
-        p = (mv == 0.0) ? a.pmax : (float)mv;
+        per_prep_item(a, i, a.abs_td[i]);
+        return;
     }
+    const int64_t slot = (a.wptr + i) % a.cap;   // store_transitions: max_priority, or max_priority_high if 0
+    const int32_t L = (int32_t)(slot + base);
+    const double mv = a.tree[a.ctrl->per_max_idx];
+    const float p = (mv == 0.0) ? a.pmax : (float)mv;
     a.wl[i] = L;
     a.wp[i] = p;
     a.winit[i] = a.tree[L];
@@ -585,31 +573,7 @@ __global__ __launch_bounds__(PER_NT) void k_per_update(PerUpdateArgs a) {
 
 __global__ __launch_bounds__(PER_GT) void k_per_prop(PerUpdateArgs a) {
     __shared__ double topd[PER_TOP];
-    const int tid = threadIdx.x;
-    for (int h = tid; h < PER_TOP; h += PER_GT) topd[h] = 0.0;
-    __syncthreads();
-    const int i = blockIdx.x * PER_GT + tid;
-    const int64_t base = a.cap - 1;
-    if (i < a.n) {
-        const int64_t L = a.wl[i];
-        const uint64_t tag = ((uint64_t)*a.epoch << 32) | (uint32_t)i;
-        if (a.last[L - base] == tag) {   // the slot's final value
-            const double fin = (double)a.wp[i];
-            a.tree[L] = fin;
-            const double delta = fin - a.winit[i];
-            if (delta != 0.0) {
-                int64_t node = L;
-                while (node > 0) {
-                    node = (node - 1) >> 1;
-                    if (node < PER_TOP) atomicAdd(&topd[node], delta);
-                    else atomicAdd(&a.tree[node], delta);
-                }
-            }
-        }
-    }
-    __syncthreads();
-    for (int node = tid; node < PER_TOP && node < base; node += PER_GT)
-        if (topd[node] != 0.0) atomicAdd(&a.tree[node], topd[node]);
+    per_prop_block(a, blockIdx.x * PER_GT, topd);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -811,7 +775,9 @@ int launch_per_update(const PerUpdateArgs& a, hipStream_t s) {
     if (a.n < 0 || a.n > PER_CHUNK) return set_error(DQNX_EINVAL, "PER update chunk %d > %d", a.n, PER_CHUNK);
     if (a.n == 0) return DQNX_OK;
     const int g = (a.n + PER_GT - 1) / PER_GT;
-    hipLaunchKernelGGL(k_per_prep, dim3(g), dim3(PER_GT), 0, s, a);
+    if ((a.skip & PER_SKIP_PREP) && (a.mode != 0 || a.numpy121))
+        return set_error(DQNX_EINVAL, "PER update: the prep pass is hosted only for mode 0 without numpy121");
+    if (!(a.skip & PER_SKIP_PREP)) hipLaunchKernelGGL(k_per_prep, dim3(g), dim3(PER_GT), 0, s, a);
     hipLaunchKernelGGL(k_per_update, dim3(1), dim3(PER_NT), 0, s, a);
     if (a.numpy121 && a.mode == 0) {   // float32 change / ancestor sums in update order
         int N2 = 1;
@@ -821,7 +787,7 @@ int launch_per_update(const PerUpdateArgs& a, hipStream_t s) {
         hipLaunchKernelGGL(k_per_chain<true>, dim3(1), dim3(PER_CHAIN_NT), (size_t)N2 * 8, s, a);
         if (depths > 0)
             hipLaunchKernelGGL(k_per_chain<false>, dim3(depths), dim3(PER_CHAIN_NT), (size_t)N2 * 8 + (size_t)a.n * 8, s, a);
-    } else {
+    } else if (!(a.skip & PER_SKIP_PROP)) {
         hipLaunchKernelGGL(k_per_prop, dim3(g), dim3(PER_GT), 0, s, a);
     }
     DQNX_HIP_CHECK(hipGetLastError());

@@ -311,3 +311,42 @@ def test_gpu_per_np_cache_bit_identical(monkeypatch, batch, cap):
             st[624] = 624            # ... and one whose next word needs a twist
         e1.set_rng(1, st)
         e2.set_rng(1, st)
+
+
+@pytest.mark.parametrize("batch,compute,cap,world", [(1024, "fp32", 20000, 1), (8192, "bf16", 40000, 1),
+                                                     (300, "fp32", 2000, 1), (2048, "fp32", 9000, 1),
+                                                     (8192, "bf16", 40000, 8), (1024, "fp32", 20000, 2)])
+def test_gpu_per_fused_update_bit_identical(monkeypatch, batch, compute, cap, world):
+    """The single-GPU PER step with the SumTree update spread over the launches that run anyway (the
+    head kernel does k_per_prep's work per sample, the gradient launch runs k_per_prop's workgroups
+    beside its tiles; the default) against the three update launches (DQNX_PER_FUSED=0): the same
+    leaves, tree, tracked max / min indices, IS weights, sampled indices and weights, bitwise, over
+    several steps (each step samples from the tree the previous one updated).  world > 1: rank 0's
+    GRADS_ONLY step + dqnx_apply_grads, whose Adam launch runs k_per_prop's workgroups."""
+    E = _E()
+    ospec = O.mlp_spec(284, 8, "dueling")
+    init = O.reference_init(ospec, 63)
+    data = O.synth_transitions(cap, 284, 8, seed=163)
+    runs = []
+    for fused in ("0", "1"):
+        monkeypatch.setenv("DQNX_PER_FUSED", fused)
+        eng = E.LearnEngine(E.mlp_spec(284, 8, "dueling"), ALGO, batch, cap, compute_dtype=compute,
+                            world_size=world, rank=0)
+        eng.load_params(init)
+        eng.push(*data)
+        np.random.seed(64)
+        eng.set_rng(1, O.np_state_to_array())
+        for t in range(4):
+            eng.set_agent_step(t)
+            if world > 1:
+                eng.learn_step(grads_only=True)
+                eng.apply_grads(soft_update=True)
+            else:
+                eng.learn_step(soft_update=True)
+        torch.cuda.synchronize()
+        eng.check_device_error()
+        runs.append((eng, tree_state(eng)))
+    (e0, (t0, mx0, mn0)), (e1, (t1, mx1, mn1)) = runs
+    assert np.array_equal(t0, t1) and mx0 == mx1 and mn0 == mn1
+    assert torch.equal(e0.batch_idx, e1.batch_idx) and torch.equal(e0.is_weights, e1.is_weights)
+    assert torch.equal(e0.params, e1.params) and torch.equal(e0.target_params, e1.target_params)

@@ -11,7 +11,15 @@ import os
 import sys
 from collections import defaultdict
 
-NAMES = [   # (substring of the HIP kernel name, bench step name)
+NAMES = [   # (substring of the HIP kernel name, bench step name); the first match wins
+    # the HEAD net's micro-CNN plan (micro.hip) and its ELU dense layers
+    ("k_micro_fwd", "micro_fwd"),
+    ("k_micro_dx", "micro_dx"),
+    ("k_micro_dw", "micro_dw"),
+    ("k_linear_fwd_big<1, false, 64, 64, 2, 64>", "linear_fwd_l1"),
+    ("k_linear_fwd<1, true, false>", "linear_fwd_l2"),
+    ("k_bwd_level<1, true>", "linear_bwd_l2"),
+    ("k_bwd_level<1, false>", "linear_bwd_l1"),
     ("k_mlp_fwd", "mlp_fwd"),
     ("k_head_bwd", "head_bwd"),
     ("k_linear_fwd<0, true, true>", "linear_fwd_l1"),
