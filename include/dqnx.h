@@ -149,6 +149,7 @@ typedef struct dqnx_ctrl {
 /* device error codes written to dqnx_ctrl.error */
 #define DQNX_DEVERR_SAMPLE_TOO_LARGE 1   /* random.sample: k > n (ValueError) */
 #define DQNX_DEVERR_EMPTY_TREE 2         /* PER sample with total priority 0 */
+#define DQNX_DEVERR_PER_HANDOFF 3        /* internal: a PER update hand-off inside one launch timed out */
 
 /* ---- engine lifetime --------------------------------------------------------------- */
 typedef struct dqnx_engine dqnx_engine;

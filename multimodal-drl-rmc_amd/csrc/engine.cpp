@@ -537,7 +537,8 @@ int layout(dqnx_engine* e) {
     }
     e->ws_adam_tab = sub((uint64_t)kAdamTable * 2 * 4);
     e->ws_stamps = sub(64 * 8);
-    e->ws_per_ticket = sub(64);   // k_per_sample arrival counter (zero between launches); [16]: PER chunk epoch
+    e->ws_per_ticket = sub(128);   // k_per_sample arrival counter (zero between launches); [16]: PER chunk
+                                   // epoch; [20..21]: the in-launch tracking -> prop hand-off words
     // numpy MT block cache: only where the fused forward launch keeps it extended
     if (c.algo == DQNX_ALGO_PER_DOUBLE && e->bwd_plan == 2 && e->fsplit <= 1 && !route_flag("DQNX_NO_NP_CACHE") &&
         np_cache_blocks(e->Bg) <= NPC_MAX_BLOCKS)
@@ -649,6 +650,7 @@ PerUpdateArgs per_update_args(dqnx_engine* e) {
     ua.winit = at<double>(e, e->ws_per_winit);
     ua.last = at<uint64_t>(e, e->ws_per_last);
     ua.epoch = at<uint32_t>(e, e->ws_per_ticket) + 16;
+    ua.sync = at<uint32_t>(e, e->ws_per_ticket) + 20;
     ua.numpy121 = c.per_numpy121;
     ua.wchg = at<float>(e, e->ws_per_wchg);
     return ua;
@@ -890,13 +892,19 @@ RelayoutArgs relayout_args(dqnx_engine* e, int* blocks) {
 // head kernel does k_per_prep's work, the weight-gradient launch (k_dw_adam16 on 32 x 16 tiles, or
 // k_dw_bf16) runs k_per_prop's workgroups, leaving the order-dependent k_per_update launch.  Not
 // under DP (the |delta| of other shards arrive by all-gather), not in numpy-1.21 mode (k_per_chain),
-// not on the fp32 slab plan.  DQNX_PER_FUSED=0: the three launches.
+// not on the fp32 slab plan.  DQNX_PER_FUSED=0: the three launches.  With the tracking in the
+// gradient launch too (per_track_inlaunch, the default) no PER launch is left: k_dw_adam16 runs
+// the tracking workgroup and its prop workgroups wait for it in the same launch; k_dw_bf16 runs
+// the tracking workgroup and the Adam launch after it the prop workgroups.
 bool dw_adam16_on(const dqnx_engine* e, int flags);
 static bool per_fused_update(const dqnx_engine* e, int flags) {
     if (e->cfg.algo != DQNX_ALGO_PER_DOUBLE || (flags & DQNX_STEP_GRADS_ONLY) || e->cfg.per_numpy121) return false;
     if (e->bwd_plan != 2 || e->Bg > PER_CHUNK || route_knob("DQNX_PER_FUSED", 1) == 0) return false;
     if (e->fplan.bf16) return true;
     return dw_adam16_on(e, flags) && route_knob("DQNX_DW16_R", 2) == 2;
+}
+static bool per_track_inlaunch(const dqnx_engine* e, int flags) {
+    return per_fused_update(e, flags) && route_knob("DQNX_PER_TRACK_INLAUNCH", 1) != 0;
 }
 
 // Fused MLP plan (bwd_plan 2): forward of every layer + head in one launch, head / TD /
@@ -1082,6 +1090,7 @@ void build_fused_steps(dqnx_engine* e, int flags, int32_t* idx, int32_t* phys, s
     //     workgroups beside its tiles, so only the order-dependent tracking launch remains here
     PerUpdateArgs pua;
     const bool per_fused = per_fused_update(e, flags);
+    const bool per_track = per_track_inlaunch(e, flags);
     if (per_fused) {
         pua = per_update_args(e);
         pua.mode = 0;
@@ -1090,7 +1099,7 @@ void build_fused_steps(dqnx_engine* e, int flags, int32_t* idx, int32_t* phys, s
         pua.abs_td = at<float>(e, e->off[DQNX_BUF_PER_ABS_TD]);
         pua.skip = PER_SKIP_PREP | PER_SKIP_PROP;
     }
-    if (c.algo == DQNX_ALGO_PER_DOUBLE && !(flags & DQNX_STEP_GRADS_ONLY)) {
+    if (c.algo == DQNX_ALGO_PER_DOUBLE && !(flags & DQNX_STEP_GRADS_ONLY) && !per_track) {
         KStep k;
         k.name = "per_update";
         k.bytes = e->Bg * (4.0 + 4.0 + 8.0 * 2.0 * 21.0);
@@ -1214,6 +1223,7 @@ void build_fused_steps(dqnx_engine* e, int flags, int32_t* idx, int32_t* phys, s
             if (per_fused) {
                 da.pprop = pua;
                 da.pprop_wgs = (e->Bg + 511) / 512;
+                da.ptrack = per_track ? 1 : 0;
             }
             const double P = (double)np.P;
             KStep k;
@@ -1234,9 +1244,10 @@ void build_fused_steps(dqnx_engine* e, int flags, int32_t* idx, int32_t* phys, s
         }
         if (e->fplan.bf16) {   // bf16 operands, fp32 slabs: the same Adam pass follows
             dw_bf16_grid(ba);
-            if (per_fused) {
+            if (per_fused) {   // tracking in this launch, prop in the Adam launch; or prop here
                 ba.pprop = pua;
-                ba.pprop_wgs = (e->Bg + 255) / 256;
+                ba.ptrack = per_track ? 1 : 0;
+                ba.pprop_wgs = per_track ? 0 : (e->Bg + 255) / 256;
             }
             KStep k;
             k.name = "dw_all";
@@ -1265,7 +1276,20 @@ void build_fused_steps(dqnx_engine* e, int flags, int32_t* idx, int32_t* phys, s
             aa.mtc = nullptr;   // the forward's sampler body draws from the MT state itself
             aa.mtc_blocks = 0;
             fill_blk_layers(e, aa, true);   // ... and the next step has no sampler launch to rebuild them
+            if (per_track) {
+                aa.pprop = pua;
+                aa.pprop_wgs = (e->Bg + 255) / 256;
+            }
             k.run = [=](hipStream_t s) { return launch_adam(aa, s); };
+            ks.push_back(k);
+            return;
+        }
+        if (per_track) {   // the prop workgroups after the gradient launch's tracking
+            AdamArgs aa;
+            KStep k = adam_kstep(e, flags, &aa);
+            aa.pprop = pua;
+            aa.pprop_wgs = (e->Bg + 255) / 256;
+            k.run = adam_run(e, aa);
             ks.push_back(k);
             return;
         }

@@ -44,7 +44,10 @@ constexpr int FT = 64 * FW;
 #endif
 constexpr int FPF = DQNX_FPF;   // 16-deep chunks per group
 constexpr int FNB = DQNX_FNB;   // register sets: FNB-1 groups of W in flight ahead of the MFMAs
-constexpr int FGQ = 6;     // float4 gather slots per thread (input tile <= FGQ * FT float4)
+constexpr int FGQ = 6;
+#ifndef DQNX_BF16_TRACK_IPT
+#define DQNX_BF16_TRACK_IPT 8   // PER tracking items per thread in k_dw_bf16 (its VGPR budget: 8 -> 96)
+#endif     // float4 gather slots per thread (input tile <= FGQ * FT float4)
 
 __host__ __device__ __forceinline__ int fused_stride(int K) { return ((K + 63) & ~63) + 8; }
 __host__ __device__ __forceinline__ int fused_groups(int K) { return (K + 16 * FPF - 1) / (16 * FPF); }
@@ -835,7 +838,14 @@ __global__ __launch_bounds__(256) void k_dw_bf16(BwdArgs a) {
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int i = lane & 15, g = lane >> 4;
     const int wm = wid >> 1, wn = wid & 1;
-    int b = blockIdx.x;
+    if (a.ptrack && blockIdx.x == 0) {   // k_per_update's tracking (single-GPU PER step; dispatched
+        // first so it starts under any grid size; its prop workgroups run in the Adam launch)
+        static_assert(sizeof(lds) >= sizeof(PerTrackLds<256>), "tracking scratch");
+        auto& tl = *reinterpret_cast<PerTrackLds<256>*>(lds);
+        per_track_block<256, DQNX_BF16_TRACK_IPT>(a.pprop, tl);
+        return;
+    }
+    int b = (int)blockIdx.x - a.ptrack;
     {   // workgroups past the tiles: k_per_prop's (single-GPU PER step; independent of the gradients)
         int tiles = 0;
         for (int p = 0; p < a.ndw; p++) tiles += a.dw[p].blocks;
@@ -931,7 +941,9 @@ void dw_bf16_grid(BwdArgs& a) {
 }
 
 int launch_dw_bf16(const BwdArgs& a, hipStream_t s) {
-    int blocks = a.pprop_wgs;   // (k_per_prop's workgroups: 256 updates each, after the tiles)
+    int blocks = a.pprop_wgs + a.ptrack;   // (+ k_per_prop's workgroups: 256 updates each, after the
+                                            // tiles; + the tracking workgroup, block 0)
+    if (a.ptrack && a.pprop.n > PER_CHUNK) return set_error(DQNX_EINVAL, "dw_bf16: PER tracking chunk %d", a.pprop.n);
     for (int p = 0; p < a.ndw; p++) blocks += a.dw[p].blocks;
     for (int p = 0; p < a.ndw; p++)   // 16-byte row loads
         if (a.dw[p].ldx % 4 || a.dw[p].ldz % 4)

@@ -1058,12 +1058,22 @@ __global__ __launch_bounds__(64 * DW16_NW) void k_dw_adam16(DwAdam16Args a) {
     __shared__ float redb[DW16_NW][R][64];
     const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int i = lane & 15, g = lane >> 4;
-    if ((int)blockIdx.x >= a.tiles) {   // extra workgroups: sampler cache, the staged-minibatch copy, PER prop
-        const int x = (int)blockIdx.x - a.tiles - (a.mtc ? 1 : 0) - (a.pf_nidx > 0 ? 1 : 0);
+    if ((int)blockIdx.x >= a.tiles) {   // extra workgroups: PER tracking, sampler cache, the staged-minibatch copy, PER prop
+        const int x = (int)blockIdx.x - a.tiles - a.ptrack - (a.mtc ? 1 : 0) - (a.pf_nidx > 0 ? 1 : 0);
         if (x >= 0) {   // k_per_prop's body over 64 * DW16_NW updates (the red table as its LDS)
-            if constexpr (sizeof(red) >= PER_TOP * sizeof(double))   // (launch_dw_adam16: 32 x 16 tiles only)
+            if constexpr (sizeof(red) >= PER_TOP * sizeof(double)) {   // (launch_dw_adam16: 32 x 16 tiles only)
+                if (a.ptrack) per_prop_wait(a.pprop);   // the tracking workgroup of this launch first
                 per_prop_block(a.pprop, x * 64 * DW16_NW, reinterpret_cast<double*>(&red[0][0][0]));
-        } else if (a.mtc && (int)blockIdx.x == a.tiles) {
+                if (a.ptrack) per_prop_finish(a.pprop, a.pprop_wgs);
+            }
+        } else if (a.ptrack && (int)blockIdx.x == a.tiles) {   // k_per_update's tracking (dispatched
+            // right after the tiles, before the prop workgroups that wait for it)
+            if constexpr (sizeof(red) >= sizeof(PerTrackLds<64 * DW16_NW>)) {
+                auto& tl = *reinterpret_cast<PerTrackLds<64 * DW16_NW>*>(&red[0][0][0]);
+                per_track_block<64 * DW16_NW, 4>(a.pprop, tl);
+                per_track_publish(a.pprop);
+            }
+        } else if (a.mtc && (int)blockIdx.x == a.tiles + a.ptrack) {
             mt_cache_extend(a.mtc, a.mtc_blocks);
         } else {
             // in-launch prefetch: the forward launch drew the next minibatch into the staging slot;
@@ -1252,9 +1262,11 @@ __global__ __launch_bounds__(64 * DW16_NW) void k_dw_adam16(DwAdam16Args a) {
 
 int launch_dw_adam16(const DwAdam16Args& a, hipStream_t s) {
     static const int var = tuning_knob("DQNX_DW16_VAR", 0);
-    if (a.pprop_wgs && (a.rows16 != 2 || var != 0))
-        return set_error(DQNX_EUNSUPPORTED, "dw_adam16: PER prop workgroups with the default 32 x 16 tiles only");
-    const dim3 grid(a.tiles + (a.mtc ? 1 : 0) + (a.pf_nidx > 0 ? 1 : 0) + a.pprop_wgs);
+    if ((a.pprop_wgs || a.ptrack) && (a.rows16 != 2 || var != 0))
+        return set_error(DQNX_EUNSUPPORTED, "dw_adam16: PER workgroups with the default 32 x 16 tiles only");
+    if (a.ptrack && (a.pprop.n > PER_CHUNK || !a.pprop.sync || a.pprop_wgs < 1))
+        return set_error(DQNX_EINVAL, "dw_adam16: PER tracking workgroup needs its prop workgroups and hand-off words");
+    const dim3 grid(a.tiles + a.ptrack + (a.mtc ? 1 : 0) + (a.pf_nidx > 0 ? 1 : 0) + a.pprop_wgs);
     if (a.rows16 == 2) {
         switch (var) {   // measurement variants (waves per tile, k-steps per register set)
             case 7: hipLaunchKernelGGL((k_dw_adam16<16, 4, 2>), grid, dim3(1024), 0, s, a); break;

@@ -70,8 +70,11 @@ struct PerUpdateArgs {
     // single-GPU PER learn step: k_per_prep's work done by the head kernel for its samples
     // (PER_SKIP_PREP) and k_per_prop's workgroups run beside the weight-gradient tiles (PER_SKIP_PROP)
     int32_t skip;
+    // the tracking workgroup -> prop workgroups hand-off inside one launch (k_dw_adam16 hosting
+    // both): [0] tracking done, [1] prop workgroups finished (the last one zeroes both)
+    uint32_t* sync;
 };
-constexpr int PER_SKIP_PREP = 1, PER_SKIP_PROP = 2;
+constexpr int PER_SKIP_PREP = 1, PER_SKIP_PROP = 2, PER_SKIP_TRACK = 4;
 
 struct FwdProblem {
     const float* A;        // dense rows, or the replay ring (layer 1, phys != null)
@@ -123,6 +126,7 @@ struct BwdArgs {
     int Bl, kslice, dw_slices;
     int dx_blocks, dx_grid_x;
     int pprop_wgs;         // k_dw_bf16: + workgroups running k_per_prop's body (single-GPU PER step)
+    int ptrack;            // k_dw_bf16: + block 0 running k_per_update's tracking (its prop in the Adam launch)
     PerUpdateArgs pprop;
 };
 
@@ -350,6 +354,8 @@ struct DwAdam16Args {
     int32_t* pf_phys_dst;
     int pf_nphys;
     int pprop_wgs;         // + workgroups running k_per_prop's body (single-GPU PER step; 0: none)
+    int ptrack;            // + one workgroup running k_per_update's tracking first; the prop
+                           //   workgroups then wait for it (pprop.sync)
     PerUpdateArgs pprop;
 };
 

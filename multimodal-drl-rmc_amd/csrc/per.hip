@@ -22,7 +22,6 @@ namespace dqnx {
 
 constexpr int PER_NT = 1024;   // threads of the one-workgroup tracking kernel (256 x 32 items measured
                                // slower: serial per-item LDS lookups, strided LDS stores)
-constexpr int PER_IPT = PER_CHUNK / PER_NT;
 
 // ---------------------------------------------------------------------------------------
 // sample_transitions (R:dqn/replay_memory.py:69-92): stratified proportional sampling.
@@ -245,107 +244,6 @@ __global__ __launch_bounds__(PER_SNT) void k_per_sample(PerSampleArgs a) {
     }
 }
 
-// ---------------------------------------------------------------------------------------
-// block scan / reduce helpers (PER_NT threads)
-// ---------------------------------------------------------------------------------------
-constexpr int PER_NW = PER_NT / 64;
-
-// running max / min priority and the latest index at which each was (re)taken, scanned
-// together: one pair of barriers for all four
-struct Track {
-    float mx, mn;
-    int lx, ln;
-};
-__device__ __forceinline__ Track track_op(const Track& a, const Track& b) {
-    return Track{fmaxf(a.mx, b.mx), fminf(a.mn, b.mn), a.lx > b.lx ? a.lx : b.lx, a.ln > b.ln ? a.ln : b.ln};
-}
-__device__ __forceinline__ Track track_shfl_up(const Track& t, int d) {
-    return Track{__shfl_up(t.mx, d, 64), __shfl_up(t.mn, d, 64), __shfl_up(t.lx, d, 64), __shfl_up(t.ln, d, 64)};
-}
-// exclusive scan over threads (thread order) and the block total; every thread must call
-__device__ Track track_scan(const Track& v, Track* sh, Track* total) {
-    const Track ident{-INFINITY, INFINITY, -1, -1};
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    Track x = v;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const Track y = track_shfl_up(x, d);
-        if (lane >= d) x = track_op(y, x);
-    }
-    if (lane == 63) sh[wid] = x;
-    __syncthreads();
-    Track carry = ident, tot = ident;
-#pragma unroll
-    for (int w = 0; w < PER_NW; w++) {
-        if (w == wid) carry = tot;
-        tot = track_op(tot, sh[w]);
-    }
-    Track prev = track_shfl_up(x, 1);
-    if (lane == 0) prev = ident;
-    __syncthreads();
-    *total = tot;
-    return track_op(carry, prev);
-}
-
-__device__ __forceinline__ int block_min_int(int v, int* sh) {
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-#pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) {
-        const int o = __shfl_xor(v, d, 64);
-        v = o < v ? o : v;
-    }
-    if (lane == 0) sh[wid] = v;
-    __syncthreads();
-    int r = sh[0];
-#pragma unroll
-    for (int w = 1; w < PER_NW; w++) r = sh[w] < r ? sh[w] : r;
-    __syncthreads();
-    return r;
-}
-
-// first index of the max (want_max) or min over leaves [base, base + n): np.argmax / np.argmin
-__device__ int64_t block_arg_extreme(const double* tree, int64_t base, int64_t n, bool want_max, double* shv,
-                                     int64_t* shi, double* out_val) {
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    double bv = want_max ? -INFINITY : INFINITY;
-    int64_t bi = INT64_MAX;
-    for (int64_t j = threadIdx.x; j < n; j += blockDim.x) {
-        const double v = tree[base + j];
-        if (want_max ? (v > bv) : (v < bv)) {   // strided ascending j: first occurrence kept
-            bv = v;
-            bi = j;
-        }
-    }
-#pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) {
-        const double ov = __shfl_xor(bv, d, 64);
-        const int64_t oi = __shfl_xor(bi, d, 64);
-        const bool better = want_max ? (ov > bv || (ov == bv && oi < bi)) : (ov < bv || (ov == bv && oi < bi));
-        if (better) {
-            bv = ov;
-            bi = oi;
-        }
-    }
-    if (lane == 0) {
-        shv[wid] = bv;
-        shi[wid] = bi;
-    }
-    __syncthreads();
-    double rv = shv[0];
-    int64_t ri = shi[0];
-    for (int w = 1; w < (int)(blockDim.x >> 6); w++) {
-        const bool better = want_max ? (shv[w] > rv || (shv[w] == rv && shi[w] < ri))
-                                     : (shv[w] < rv || (shv[w] == rv && shi[w] < ri));
-        if (better) {
-            rv = shv[w];
-            ri = shi[w];
-        }
-    }
-    __syncthreads();
-    *out_val = rv;
-    return ri;
-}
-
 __device__ __forceinline__ uint32_t leaf_hash(uint32_t x) {
     x ^= x >> 16; x *= 0x7feb352du; x ^= x >> 15; x *= 0x846ca68bu; x ^= x >> 16;
     return x;
@@ -395,180 +293,9 @@ __global__ __launch_bounds__(PER_GT) void k_per_prep(PerUpdateArgs a) {
 }
 
 __global__ __launch_bounds__(PER_NT) void k_per_update(PerUpdateArgs a) {
-    __shared__ int32_t Ls[PER_CHUNK];
-    __shared__ float Ps[PER_CHUNK];
-    __shared__ Track sht[PER_NW];
-    __shared__ int shi[PER_NW];
-    __shared__ double shd[PER_NW];
-    __shared__ int64_t shl[PER_NW];
-    __shared__ int s_mx_i, s_mn_i, s_resx, s_resn;
-    __shared__ float s_mx_v, s_mn_v;
-
-    const int tid = threadIdx.x;
-    DQNX_STAMP(a.stamps, 56);
-    const int n = a.n;
-    const int64_t base = a.cap - 1;
-    float pv[PER_IPT];
-    int32_t lv[PER_IPT];
-    // the tracked max / min leaves first (a dependent pair of round trips)
-    int mx_i = (int)a.ctrl->per_max_idx, mn_i = (int)a.ctrl->per_min_idx;
-    float mx_v = (float)a.tree[mx_i], mn_v = (float)a.tree[mn_i];
-    // PER_IPT consecutive items per thread (scan order): 16-byte loads (the workspace holds
-    // PER_CHUNK items, so the tail past n stays in bounds and is masked below)
-    static_assert(PER_IPT % 4 == 0, "16-byte loads");
-    {
-        const int4* wl4 = reinterpret_cast<const int4*>(a.wl) + (PER_IPT / 4) * tid;
-        const float4* wp4 = reinterpret_cast<const float4*>(a.wp) + (PER_IPT / 4) * tid;
-        int4 l4[PER_IPT / 4];
-        float4 p4[PER_IPT / 4];
-#pragma unroll
-        for (int q = 0; q < PER_IPT / 4; q++) {
-            l4[q] = wl4[q];
-            p4[q] = wp4[q];
-        }
-#pragma unroll
-        for (int q = 0; q < PER_IPT / 4; q++) {
-            lv[4 * q] = l4[q].x; lv[4 * q + 1] = l4[q].y; lv[4 * q + 2] = l4[q].z; lv[4 * q + 3] = l4[q].w;
-            pv[4 * q] = p4[q].x; pv[4 * q + 1] = p4[q].y; pv[4 * q + 2] = p4[q].z; pv[4 * q + 3] = p4[q].w;
-        }
-    }
-    DQNX_STAMP(a.stamps, 8);
-#pragma unroll
-    for (int k = 0; k < PER_IPT; k++) {
-        const int i = tid * PER_IPT + k;
-        if (i < n) {
-            Ls[i] = lv[k];
-            Ps[i] = pv[k];
-        } else {
-            lv[k] = -1;
-            pv[k] = 0.f;
-        }
-    }
-    DQNX_STAMP(a.stamps, 9);
-    DQNX_STAMP(a.stamps, 10);
-    __syncthreads();
-    DQNX_STAMP(a.stamps, 57);
-    DQNX_STAMP(a.stamps, 58);
-
-    // ---- max / min index tracking, sequential semantics ----
-    int s = 0;
-    while (true) {
-        // pass 1: the thread's max / min (for the scan)
-        Track own{-INFINITY, INFINITY, -1, -1};
-#pragma unroll
-        for (int k = 0; k < PER_IPT; k++) {
-            const int i = tid * PER_IPT + k;
-            if (i >= s && i < n) {
-                own.mx = fmaxf(own.mx, pv[k]);
-                own.mn = fminf(own.mn, pv[k]);
-            }
-        }
-        Track totv;
-        DQNX_STAMP(a.stamps, 11);
-        const Track exv = track_scan(own, sht, &totv);
-        DQNX_STAMP(a.stamps, 12);
-        // pass 2: which items (re)take the max / min, given the running values BEFORE each
-        Track ownl{-INFINITY, INFINITY, -1, -1};
-        {
-            float rmx = fmaxf(mx_v, exv.mx), rmn = fminf(mn_v, exv.mn);
-#pragma unroll
-            for (int k = 0; k < PER_IPT; k++) {
-                const int i = tid * PER_IPT + k;
-                if (i >= s && i < n) {
-                    if (pv[k] >= rmx) ownl.lx = i;
-                    if (pv[k] <= rmn) ownl.ln = i;
-                    rmx = fmaxf(rmx, pv[k]);
-                    rmn = fminf(rmn, pv[k]);
-                }
-            }
-        }
-        Track totl;
-        DQNX_STAMP(a.stamps, 13);
-        const Track exl = track_scan(ownl, sht, &totl);
-        DQNX_STAMP(a.stamps, 14);
-        // pass 3: the first item that rewrites the current max / min leaf without retaking it
-        int lastx = exl.lx, lastn = exl.ln;
-        int mytrig = n;
-        int cxb = 0, cnb = 0;
-        float tp = 0.f, bx = 0.f, bn = 0.f;
-        {
-            float rmx = fmaxf(mx_v, exv.mx), rmn = fminf(mn_v, exv.mn);
-#pragma unroll
-            for (int k = 0; k < PER_IPT; k++) {
-                const int i = tid * PER_IPT + k;
-                if (i >= s && i < n) {
-                    const bool fx = pv[k] >= rmx, fn = pv[k] <= rmn;
-                    const int curx = lastx >= 0 ? Ls[lastx] : mx_i;   // max_idx before update i
-                    const int curn = lastn >= 0 ? Ls[lastn] : mn_i;
-                    const bool trig = (!fx && lv[k] == curx) || (!fn && lv[k] == curn);
-                    if (trig && mytrig == n) {
-                        mytrig = i;
-                        cxb = curx;
-                        cnb = curn;
-                        tp = pv[k];
-                        bx = rmx;
-                        bn = rmn;
-                    }
-                    if (fx) lastx = i;
-                    if (fn) lastn = i;
-                    rmx = fmaxf(rmx, pv[k]);
-                    rmn = fminf(rmn, pv[k]);
-                }
-            }
-        }
-        DQNX_STAMP(a.stamps, 15);
-        if (!__syncthreads_or(mytrig < n)) {   // no rescan left: fold the scans into the state
-            if (totl.lx >= 0) mx_i = Ls[totl.lx];
-            if (totl.ln >= 0) mn_i = Ls[totl.ln];
-            mx_v = fmaxf(mx_v, totv.mx);
-            mn_v = fminf(mn_v, totv.mn);
-            break;
-        }
-        const int istar = block_min_int(mytrig, shi);
-        if (mytrig == istar) {   // the owner of the first trigger applies that update
-            const float p = tp;
-            const int L = Ls[istar];
-            s_resx = 0;
-            s_resn = 0;
-            if (p >= bx) { s_mx_i = L; s_mx_v = p; }
-            else if (L == cxb) s_resx = 1;
-            else { s_mx_i = cxb; s_mx_v = bx; }
-            if (p <= bn) { s_mn_i = L; s_mn_v = p; }
-            else if (L == cnb) s_resn = 1;
-            else { s_mn_i = cnb; s_mn_v = bn; }
-        }
-        __syncthreads();
-        // leaves as they stand after update istar (earlier segments were written already)
-        if (tid == 0)
-            for (int j = s; j <= istar; j++) a.tree[Ls[j]] = (double)Ps[j];
-        __threadfence_block();
-        __syncthreads();
-        const int64_t sz = a.mode == 1 ? min(a.size + istar + 1, a.cap) : a.ctrl->ring_size;
-        if (s_resx) {
-            double v;
-            const int64_t j = block_arg_extreme(a.tree, base, sz, true, shd, shl, &v);
-            if (tid == 0) { s_mx_i = (int)(j + base); s_mx_v = (float)v; }
-        }
-        if (s_resn) {
-            double v;
-            const int64_t j = block_arg_extreme(a.tree, base, sz, false, shd, shl, &v);
-            if (tid == 0) { s_mn_i = (int)(j + base); s_mn_v = (float)v; }
-        }
-        __syncthreads();
-        mx_i = s_mx_i;
-        mx_v = s_mx_v;
-        mn_i = s_mn_i;
-        mn_v = s_mn_v;
-        s = istar + 1;
-        __syncthreads();
-    }
-    DQNX_STAMP(a.stamps, 59);
-    if (tid == 0) {
-        a.ctrl->per_max_idx = mx_i;
-        a.ctrl->per_min_idx = mn_i;
-        *a.epoch += 1u;   // the chunk k_per_prep tagged; k_per_prop reads it back
-    }
-    DQNX_STAMP(a.stamps, 61);
+    __shared__ PerTrackLds<PER_NT> sh;
+    // one super-chunk; the leaf lookups instead of the carried leaves (128 VGPRs at 1024 threads)
+    per_track_block<PER_NT, PER_CHUNK / PER_NT, false>(a, sh);
 }
 
 __global__ __launch_bounds__(PER_GT) void k_per_prop(PerUpdateArgs a) {

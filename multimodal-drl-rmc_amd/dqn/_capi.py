@@ -33,6 +33,7 @@ STEP_GRADS_ONLY = 0x4
 STEP_PREFETCH = 0x8
 DEVERR_SAMPLE_TOO_LARGE = 1
 DEVERR_EMPTY_TREE = 2
+DEVERR_PER_HANDOFF = 3
 
 I32 = ctypes.c_int32
 I64 = ctypes.c_int64

@@ -565,5 +565,7 @@ class LearnEngine:
             raise ValueError("Sample larger than population or is negative")
         if err == C.DEVERR_EMPTY_TREE:
             raise RuntimeError("libdqnx: PER sample from a SumTree with total priority 0")
+        if err == C.DEVERR_PER_HANDOFF:
+            raise RuntimeError("libdqnx: PER tree update hand-off timed out inside a launch (internal error)")
         if err:
             raise RuntimeError(f"libdqnx device error {err}")

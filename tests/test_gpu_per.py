@@ -313,23 +313,33 @@ def test_gpu_per_np_cache_bit_identical(monkeypatch, batch, cap):
         e2.set_rng(1, st)
 
 
-@pytest.mark.parametrize("batch,compute,cap,world", [(1024, "fp32", 20000, 1), (8192, "bf16", 40000, 1),
-                                                     (300, "fp32", 2000, 1), (2048, "fp32", 9000, 1),
-                                                     (8192, "bf16", 40000, 8), (1024, "fp32", 20000, 2)])
-def test_gpu_per_fused_update_bit_identical(monkeypatch, batch, compute, cap, world):
+@pytest.mark.parametrize("batch,compute,cap,world,dw16", [
+    (1024, "fp32", 20000, 1, None), (8192, "bf16", 40000, 1, None), (300, "fp32", 2000, 1, None),
+    (2048, "fp32", 9000, 1, None), (2048, "fp32", 2500, 1, None), (512, "bf16", 1500, 1, None),
+    (4096, "fp32", 6000, 1, "1"), (8192, "bf16", 40000, 8, None), (1024, "fp32", 20000, 2, None)])
+def test_gpu_per_fused_update_bit_identical(monkeypatch, batch, compute, cap, world, dw16):
     """The single-GPU PER step with the SumTree update spread over the launches that run anyway (the
     head kernel does k_per_prep's work per sample, the gradient launch runs k_per_prop's workgroups
     beside its tiles; the default) against the three update launches (DQNX_PER_FUSED=0): the same
     leaves, tree, tracked max / min indices, IS weights, sampled indices and weights, bitwise, over
     several steps (each step samples from the tree the previous one updated).  world > 1: rank 0's
-    GRADS_ONLY step + dqnx_apply_grads, whose Adam launch runs k_per_prop's workgroups."""
+    GRADS_ONLY step + dqnx_apply_grads, whose Adam launch runs k_per_prop's workgroups.  Three
+    modes: the three launches, prep / prop fused with the tracking launch kept
+    (DQNX_PER_TRACK_INLAUNCH=0), and the default with the tracking workgroup in the gradient launch
+    (k_dw_adam16: its prop workgroups wait for it in the same launch; k_dw_bf16: the Adam launch
+    runs the prop).  Small trees against large batches (cap 2500 / 1500) resample the tracked max /
+    min leaves, so the rescans run; B=4096 on k_dw_adam16 (DQNX_DW_ADAM16=1) and B=8192 on k_dw_bf16
+    take the tracking in several super-chunks."""
     E = _E()
     ospec = O.mlp_spec(284, 8, "dueling")
     init = O.reference_init(ospec, 63)
     data = O.synth_transitions(cap, 284, 8, seed=163)
+    if dw16:
+        monkeypatch.setenv("DQNX_DW_ADAM16", dw16)
     runs = []
-    for fused in ("0", "1"):
+    for fused, track in (("0", "0"), ("1", "0"), ("1", "1")):
         monkeypatch.setenv("DQNX_PER_FUSED", fused)
+        monkeypatch.setenv("DQNX_PER_TRACK_INLAUNCH", track)
         eng = E.LearnEngine(E.mlp_spec(284, 8, "dueling"), ALGO, batch, cap, compute_dtype=compute,
                             world_size=world, rank=0)
         eng.load_params(init)
@@ -346,7 +356,8 @@ def test_gpu_per_fused_update_bit_identical(monkeypatch, batch, compute, cap, wo
         torch.cuda.synchronize()
         eng.check_device_error()
         runs.append((eng, tree_state(eng)))
-    (e0, (t0, mx0, mn0)), (e1, (t1, mx1, mn1)) = runs
-    assert np.array_equal(t0, t1) and mx0 == mx1 and mn0 == mn1
-    assert torch.equal(e0.batch_idx, e1.batch_idx) and torch.equal(e0.is_weights, e1.is_weights)
-    assert torch.equal(e0.params, e1.params) and torch.equal(e0.target_params, e1.target_params)
+    e0, (t0, mx0, mn0) = runs[0]
+    for mode, (e1, (t1, mx1, mn1)) in enumerate(runs[1:], 1):
+        assert np.array_equal(t0, t1) and mx0 == mx1 and mn0 == mn1, mode
+        assert torch.equal(e0.batch_idx, e1.batch_idx) and torch.equal(e0.is_weights, e1.is_weights), mode
+        assert torch.equal(e0.params, e1.params) and torch.equal(e0.target_params, e1.target_params), mode

@@ -1,7 +1,6 @@
 """Diagnostic: s_memtime phase stamps (block 0, thread 0) of the PER kernels (libdqnx_stamps.so).
 k_per_sample: 0 start, 1 top/MT loaded, 2 words + beta, 3 descents done.
-k_per_update (last chunk of the step): 56 start, 57 items loaded, 58 (same), 59 max/min
-tracking, 61 end."""
+k_per_update (last chunk of the step): 56 start, 57 items loaded, 59 max/min tracking, 61 end."""
 import os
 import random
 import sys
@@ -34,7 +33,5 @@ for step in range(5):
     C.check(C.lib().dqnx_debug_stamps(eng.h, out, eng.stream()), "stamps")
     s = list(out)
     ps = [s[j + 1] - s[j] for j in range(3)]
-    pu = [s[57] - s[56], s[59] - s[58], s[61] - s[59]]
-    det = [s[8] - s[56], s[9] - s[8], s[10] - s[9], s[57] - s[10], s[11] - s[58], s[12] - s[11], s[13] - s[12],
-           s[14] - s[13], s[15] - s[14], s[59] - s[15]]
-    print(f"step {step}: per_sample cyc {ps} total {s[3] - s[0]}; per_update cyc {pu} total {s[61] - s[56]}; detail {det}")
+    pu = [s[57] - s[56], s[59] - s[57], s[61] - s[59]]
+    print(f"step {step}: per_sample cyc {ps} total {s[3] - s[0]}; per_update cyc {pu} total {s[61] - s[56]}")
