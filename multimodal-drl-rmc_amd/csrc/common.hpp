@@ -85,8 +85,14 @@ __device__ __forceinline__ int xcd_remap(int L, int total) {
     do {                                                                             \
         if ((ptr) && blockIdx.x == 0 && threadIdx.x == 0) (ptr)[i] = (int64_t)__builtin_amdgcn_s_memtime(); \
     } while (0)
+// thread 0 of whichever workgroup runs it (a role hosted by one workgroup of a launch)
+#define DQNX_STAMP_WG(ptr, i)                                                         \
+    do {                                                                             \
+        if ((ptr) && threadIdx.x == 0) (ptr)[i] = (int64_t)__builtin_amdgcn_s_memtime(); \
+    } while (0)
 #else
 #define DQNX_STAMP(ptr, i) do { } while (0)
+#define DQNX_STAMP_WG(ptr, i) do { } while (0)
 #endif
 
 }  // namespace dqnx

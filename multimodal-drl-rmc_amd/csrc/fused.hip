@@ -45,8 +45,20 @@ constexpr int FT = 64 * FW;
 constexpr int FPF = DQNX_FPF;   // 16-deep chunks per group
 constexpr int FNB = DQNX_FNB;   // register sets: FNB-1 groups of W in flight ahead of the MFMAs
 constexpr int FGQ = 6;
+// The PER tracking workgroup hosted by k_dw_bf16 must not raise the tiles' register budget: 4 items
+// per thread without the carried leaves stays within the 80 VGPRs of 6 waves / SIMD (8 items with
+// them took 96-101 VGPRs, 4 waves / SIMD, and dw_all 23 -> 27.5 us at B=8192)
 #ifndef DQNX_BF16_TRACK_IPT
-#define DQNX_BF16_TRACK_IPT 8   // PER tracking items per thread in k_dw_bf16 (its VGPR budget: 8 -> 96)
+#define DQNX_BF16_TRACK_IPT 4
+#endif
+#ifndef DQNX_BF16_TRACK_CARRY
+#define DQNX_BF16_TRACK_CARRY false
+#endif
+#ifndef DQNX_BF16_TRACK_PF
+#define DQNX_BF16_TRACK_PF false
+#endif
+#ifndef DQNX_DWB_WAVES
+#define DQNX_DWB_WAVES 6
 #endif     // float4 gather slots per thread (input tile <= FGQ * FT float4)
 
 __host__ __device__ __forceinline__ int fused_stride(int K) { return ((K + 63) & ~63) + 8; }
@@ -826,7 +838,7 @@ __device__ __forceinline__ void dwb_store(uint32_t* dst,
 
 // BT x BT output tile (32 or 64), 4 waves of (BT/32) x (BT/32) 16x16 tiles, KT samples per pass.
 template <int BT, int KT>
-__global__ __launch_bounds__(256) void k_dw_bf16(BwdArgs a) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DQNX_DWB_WAVES))) void k_dw_bf16(BwdArgs a) {
     static_assert(BT == 32 || BT == 64, "tile");
     static_assert(KT % 32 == 0, "whole MFMA chunks");
     constexpr int T = BT / 32, SD = DwbShape<KT>::SD;
@@ -840,9 +852,12 @@ __global__ __launch_bounds__(256) void k_dw_bf16(BwdArgs a) {
     const int wm = wid >> 1, wn = wid & 1;
     if (a.ptrack && blockIdx.x == 0) {   // k_per_update's tracking (single-GPU PER step; dispatched
         // first so it starts under any grid size; its prop workgroups run in the Adam launch)
-        static_assert(sizeof(lds) >= sizeof(PerTrackLds<256>), "tracking scratch");
+        // LDS: the scan scratch, then the super-chunk leaves (double buffered) for the lookups
+        constexpr int LSH = 2 * 256 * DQNX_BF16_TRACK_IPT;
+        static_assert(sizeof(lds) >= sizeof(PerTrackLds<256>) + 4 * LSH + 16, "tracking scratch");
         auto& tl = *reinterpret_cast<PerTrackLds<256>*>(lds);
-        per_track_block<256, DQNX_BF16_TRACK_IPT>(a.pprop, tl);
+        int32_t* lsh = reinterpret_cast<int32_t*>(lds) + ((sizeof(PerTrackLds<256>) + 15) / 16) * 4;
+        per_track_block<256, DQNX_BF16_TRACK_IPT, DQNX_BF16_TRACK_CARRY, DQNX_BF16_TRACK_PF>(a.pprop, tl, lsh);
         return;
     }
     int b = (int)blockIdx.x - a.ptrack;
