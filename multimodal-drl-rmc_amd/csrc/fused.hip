@@ -54,9 +54,6 @@ constexpr int FGQ = 6;
 #ifndef DQNX_BF16_TRACK_CARRY
 #define DQNX_BF16_TRACK_CARRY false
 #endif
-#ifndef DQNX_BF16_TRACK_PF
-#define DQNX_BF16_TRACK_PF false
-#endif
 #ifndef DQNX_DWB_WAVES
 #define DQNX_DWB_WAVES 6
 #endif     // float4 gather slots per thread (input tile <= FGQ * FT float4)
@@ -852,12 +849,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DQNX_DWB_WA
     const int wm = wid >> 1, wn = wid & 1;
     if (a.ptrack && blockIdx.x == 0) {   // k_per_update's tracking (single-GPU PER step; dispatched
         // first so it starts under any grid size; its prop workgroups run in the Adam launch)
-        // LDS: the scan scratch, then the super-chunk leaves (double buffered) for the lookups
-        constexpr int LSH = 2 * 256 * DQNX_BF16_TRACK_IPT;
-        static_assert(sizeof(lds) >= sizeof(PerTrackLds<256>) + 4 * LSH + 16, "tracking scratch");
+        static_assert(sizeof(lds) >= sizeof(PerTrackLds<256>), "tracking scratch");
         auto& tl = *reinterpret_cast<PerTrackLds<256>*>(lds);
-        int32_t* lsh = reinterpret_cast<int32_t*>(lds) + ((sizeof(PerTrackLds<256>) + 15) / 16) * 4;
-        per_track_block<256, DQNX_BF16_TRACK_IPT, DQNX_BF16_TRACK_CARRY, DQNX_BF16_TRACK_PF>(a.pprop, tl, lsh);
+        per_track_block<256, DQNX_BF16_TRACK_IPT, DQNX_BF16_TRACK_CARRY>(a.pprop, tl);
         return;
     }
     int b = (int)blockIdx.x - a.ptrack;

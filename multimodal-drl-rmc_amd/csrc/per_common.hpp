@@ -243,12 +243,9 @@ __device__ int64_t block_arg_extreme(const double* tree, int64_t base, int64_t n
 // scanned with the state the previous one left: the same sequential semantics.  Ends by storing
 // the tracked indices and advancing the chunk epoch (thread 0).
 // CARRY: each retaking update's leaf rides in the scans (no dependent hand-off lookups; more
-// registers: the 1024-thread k_per_update keeps the lookups to stay within 128 VGPRs).  Without it,
-// lsh (2 * NT * IPT ints of LDS, or null) holds the super-chunk's leaves for the lookups, double
-// buffered by super-chunk parity (the scans' barriers order the writes before the reads).  PF: the
-// next super-chunk's items are loaded while the current one is scanned.
-template <int NT, int IPT, bool CARRY = true, bool PF = false>
-__device__ void per_track_block(const PerUpdateArgs& a, PerTrackLds<NT>& sh, int32_t* lsh = nullptr) {
+// registers: the 1024-thread k_per_update keeps the lookups to stay within 128 VGPRs).
+template <int NT, int IPT, bool CARRY = true>
+__device__ void per_track_block(const PerUpdateArgs& a, PerTrackLds<NT>& sh) {
     static_assert(IPT % 4 == 0 && PER_CHUNK % (NT * IPT) == 0, "16-byte loads inside the PER_CHUNK hand-off");
     constexpr int NW = NT / 64, SC = NT * IPT;
     const int tid = threadIdx.x;
@@ -260,34 +257,20 @@ __device__ void per_track_block(const PerUpdateArgs& a, PerTrackLds<NT>& sh, int
     int mx_i = (int)a.ctrl->per_max_idx, mn_i = (int)a.ctrl->per_min_idx;
     float mx_v = (float)a.tree[mx_i], mn_v = (float)a.tree[mn_i];
     int w = 0;   // updates [0, w) are written to the leaves (by the rescans so far)
-    // IPT consecutive items per thread (scan order); the tail past n is masked below
-    int4 l4[IPT / 4];
-    float4 p4[IPT / 4];
-    auto fetch = [&](int c) {
-        const int4* wl4 = reinterpret_cast<const int4*>(a.wl + c) + (IPT / 4) * tid;
-        const float4* wp4 = reinterpret_cast<const float4*>(a.wp + c) + (IPT / 4) * tid;
-#pragma unroll
-        for (int q = 0; q < IPT / 4; q++) {
-            l4[q] = wl4[q];
-            p4[q] = wp4[q];
-        }
-    };
-    if (PF) fetch(0);
     for (int c0 = 0; c0 < n; c0 += SC) {
         float pv[IPT];
         int32_t lv[IPT];
-        if (!PF) fetch(c0);
+        {   // IPT consecutive items per thread (scan order); the tail past n is masked below
+            const int4* wl4 = reinterpret_cast<const int4*>(a.wl + c0) + (IPT / 4) * tid;
+            const float4* wp4 = reinterpret_cast<const float4*>(a.wp + c0) + (IPT / 4) * tid;
 #pragma unroll
-        for (int q = 0; q < IPT / 4; q++) {
-            lv[4 * q] = l4[q].x; lv[4 * q + 1] = l4[q].y; lv[4 * q + 2] = l4[q].z; lv[4 * q + 3] = l4[q].w;
-            pv[4 * q] = p4[q].x; pv[4 * q + 1] = p4[q].y; pv[4 * q + 2] = p4[q].z; pv[4 * q + 3] = p4[q].w;
+            for (int q = 0; q < IPT / 4; q++) {
+                const int4 l4 = wl4[q];
+                const float4 p4 = wp4[q];
+                lv[4 * q] = l4.x; lv[4 * q + 1] = l4.y; lv[4 * q + 2] = l4.z; lv[4 * q + 3] = l4.w;
+                pv[4 * q] = p4.x; pv[4 * q + 1] = p4.y; pv[4 * q + 2] = p4.z; pv[4 * q + 3] = p4.w;
+            }
         }
-        int32_t* lb = lsh ? lsh + ((c0 / SC) & 1) * SC : nullptr;
-        if (!CARRY && lsh) {
-#pragma unroll
-            for (int q = 0; q < IPT / 4; q++) reinterpret_cast<int4*>(lb)[(IPT / 4) * tid + q] = l4[q];
-        }
-        if (PF && c0 + SC < n) fetch(c0 + SC);   // in flight during this super-chunk's scans
 #pragma unroll
         for (int k = 0; k < IPT; k++) {
             if (c0 + tid * IPT + k >= n) {
@@ -331,8 +314,8 @@ __device__ void per_track_block(const PerUpdateArgs& a, PerTrackLds<NT>& sh, int
             // pass 3: the first item that rewrites the current max / min leaf without retaking it.
             // max_idx before update i is the leaf of the latest retaking item before it (the
             // thread's own item once one of its items retook), else the state entering the scan
-            int curx = exl.lx >= 0 ? (CARRY ? exl.Lx : (lb ? lb[exl.lx - c0] : a.wl[exl.lx])) : mx_i;
-            int curn = exl.ln >= 0 ? (CARRY ? exl.Ln : (lb ? lb[exl.ln - c0] : a.wl[exl.ln])) : mn_i;
+            int curx = exl.lx >= 0 ? (CARRY ? exl.Lx : a.wl[exl.lx]) : mx_i;
+            int curn = exl.ln >= 0 ? (CARRY ? exl.Ln : a.wl[exl.ln]) : mn_i;
             int mytrig = n;
             int cxb = 0, cnb = 0, tl = 0;
             float tp = 0.f, bx = 0.f, bn = 0.f;
@@ -361,8 +344,8 @@ __device__ void per_track_block(const PerUpdateArgs& a, PerTrackLds<NT>& sh, int
                 }
             }
             if (!__syncthreads_or(mytrig < n)) {   // no rescan left: fold the scans into the state
-                if (totl.lx >= 0) mx_i = CARRY ? totl.Lx : (lb ? lb[totl.lx - c0] : a.wl[totl.lx]);
-                if (totl.ln >= 0) mn_i = CARRY ? totl.Ln : (lb ? lb[totl.ln - c0] : a.wl[totl.ln]);
+                if (totl.lx >= 0) mx_i = CARRY ? totl.Lx : a.wl[totl.lx];
+                if (totl.ln >= 0) mn_i = CARRY ? totl.Ln : a.wl[totl.ln];
                 mx_v = fmaxf(mx_v, totv.mx);
                 mn_v = fminf(mn_v, totv.mn);
                 break;
