@@ -598,6 +598,39 @@ def head_net_extra(args, device):
     return out
 
 
+def configs2_extra(args, device):
+    """configs[2] as BASELINE.json states it: the stacked 4x84x84 occupancy-grid CNN encoder + dueling
+    head (TwoStreamHybridNetwork on a (4,84,84) micro grid, R:env/dqn_config.py:97-143: the class is
+    shape-generic), DuelingDouble fp32, B=256, replay capacity 1e5 resident in HBM (113 KB rows), in the
+    same learning loop as the headline, with its dominant kernel's roofline (traffic from the committed
+    PMC passes) and the oracle's CPU baseline on a 2e3-transition deque (a 1e5 host deque of these rows
+    would need 22.6 GB)."""
+    import copy
+    a = copy.copy(args)
+    a.net, a.batch, a.capacity = "hybrid84", 256, 100_000
+    spec = make_spec(a)
+    eng = make_engine(a, spec, 256, 1, 0, device)
+    steps = max(args.steps, 20)
+    el, _ = run_learner(a, eng, 1, None, steps, max(2, min(args.warmup, 5)), None, device)
+    flags = C.STEP_SOFT_UPDATE | (C.STEP_PREFETCH if a.prefetch else 0)
+    ks = kernel_times(eng, flags, count=6, reps=3)
+    dom = max(ks, key=lambda k: k[1])
+    dom = kernel_times(eng, flags, count=20, reps=5, only={dom[0]})[0]
+    out = {"value": 256 * steps / el, "unit": "transitions/s", "ms_per_step": el / steps * 1e3, "steps": steps,
+           "batch": 256, "replay_capacity": a.capacity, "net": net_name(a), "algo": a.algo, "dtype": "fp32",
+           "workload": workload_name(a, 1),
+           "kernels": [{"kernel": k[0], "avg_us": (dom[1] if k[0] == dom[0] else k[1])} for k in ks],
+           "roofline": roofline_of(a, dom, 256)}
+    del eng
+    torch.cuda.empty_cache()
+    if not args.no_cpu_baseline:
+        try:
+            out["cpu_baseline"] = cpu_baseline(a, 256)
+        except Exception as ex:   # the baseline must never hide the GPU number
+            log(f"configs2 cpu baseline failed: {ex!r}")
+    return out
+
+
 def c5_projection(args, device):
     """configs[4] (PER + DuelingDouble, bf16 compute, global minibatch 8192): the one-GPU step, and
     the rank-0 shard step of a world_size = 8 engine (1024 rows; the replicated O(B_global) PER
@@ -790,8 +823,8 @@ def main():
         torch.cuda.empty_cache()
         if not dpmode:
             extras = single_gpu_extras(args, spec, device)
-            for name, fn in (("head_net", head_net_extra), ("configs4_projection_w8", c5_projection),
-                             ("dropin_loop", dropin_loop)):
+            for name, fn in (("head_net", head_net_extra), ("configs2", configs2_extra),
+                             ("configs4_projection_w8", c5_projection), ("dropin_loop", dropin_loop)):
                 try:
                     extras[name] = fn(args, device)
                 except Exception as ex:   # an extra must never hide the headline number

@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define DQNX_ABI_VERSION 2
+#define DQNX_ABI_VERSION 3
 
 /* ---- status codes ---------------------------------------------------------------- */
 #define DQNX_OK 0
@@ -244,6 +244,28 @@ int dqnx_rng_get(dqnx_engine* e, int32_t which, uint32_t* state625, void* stream
  * prefetched minibatch is pending. */
 int dqnx_rng_set_async(dqnx_engine* e, int32_t which, const uint32_t* state625, void* stream);
 int dqnx_rng_get_async(dqnx_engine* e, int32_t which, uint32_t* state625, void* stream);
+
+/* The whole control block (both RNG states, ring size, loss, sticky error, ...) into PINNED host memory
+ * (sizeof(dqnx_ctrl) bytes), stream-ordered and without a synchronisation: the drop-in Agent reads it
+ * back after each launched learn step and checks the sticky error and its RNG mirror (below) at its
+ * next synchronisation point, so a device error reaches the caller without a host round trip per step. */
+int dqnx_ctrl_get_async(dqnx_engine* e, void* dst, void* stream);
+
+/* ---- host-side RNG stream mirror (host only, no device work) -----------------------------------
+ * The reference draws the minibatch inside Agent.learn() from the interpreter's global generators
+ * (R:dqn/replay_memory.py:38-39 random.sample; :79-80 np.random.uniform once per sample), so the
+ * caller's `random` / `np.random` have moved on when learn() returns.  The device sampler draws the
+ * minibatch; these tell the host how far that draw moves the stream, so the Agent advances its global
+ * generator at learn() time without waiting for the GPU (R:dqn/agent.py:204-226 stays synchronous
+ * from the caller's view) and checks the device's returned state against `out625` later.
+ * dqnx_rng_sample_words: the 32-bit words CPython's random.sample(population of n, k) consumes from
+ *   `state625` (its _randbelow rejections and the set branch's duplicate redraws depend on the values,
+ *   so the stream is walked); `out625` (may be NULL) receives the state after the draw.  k > n returns
+ *   DQNX_EINVAL with random.sample's ValueError message.
+ * dqnx_rng_advance: `out625` = `state625` advanced by `words` MT19937 outputs (numpy's legacy uniform
+ *   takes two per draw). */
+int dqnx_rng_sample_words(const uint32_t* state625, int64_t n, int32_t k, uint32_t* out625, int64_t* words);
+int dqnx_rng_advance(const uint32_t* state625, int64_t words, uint32_t* out625);
 
 /* ---- the learn step: replaces Agent.learn() (R:dqn/agent.py:166-185 / 204-226 /
  *      245-272) and, with DQNX_STEP_SOFT_UPDATE, the following

@@ -538,7 +538,7 @@ int layout(dqnx_engine* e) {
     e->ws_adam_tab = sub((uint64_t)kAdamTable * 2 * 4);
     e->ws_stamps = sub(64 * 8);
     e->ws_per_ticket = sub(128);   // k_per_sample arrival counter (zero between launches); [16]: PER chunk
-                                   // epoch; [20..21]: the in-launch tracking -> prop hand-off words
+                                   // epoch; [20]: the in-launch tracking -> prop hand-off word
     // numpy MT block cache: only where the fused forward launch keeps it extended
     if (c.algo == DQNX_ALGO_PER_DOUBLE && e->bwd_plan == 2 && e->fsplit <= 1 && !route_flag("DQNX_NO_NP_CACHE") &&
         np_cache_blocks(e->Bg) <= NPC_MAX_BLOCKS)
@@ -2563,6 +2563,15 @@ int dqnx_engine_create(const dqnx_config* cfg, dqnx_engine** out) {
             return set_error(DQNX_EUNSUPPORTED, "bf16 compute needs the fused MLP plan (MLP, widths multiple of 64 <= 256, <= 3 layers)");
         }
     }
+    {   // the current device's compute units: the plans below size their grids (and the conv dW /
+        // dense-1 split-K slab counts, hence their fixed summation order) from it.  Without a visible
+        // device (host-only plan checks) the MI355X's 256 stays.
+        int dev = 0, cus = 0;
+        if (hipGetDevice(&dev) == hipSuccess &&
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && cus > 0)
+            e->n_cu = cus;
+        (void)hipGetLastError();
+    }
     e->Bg = c.batch;
     e->Bl = c.batch / c.world_size;
     e->local_sampling = c.local_sampling && c.world_size > 1;
@@ -2644,7 +2653,7 @@ int dqnx_engine_create(const dqnx_config* cfg, dqnx_engine** out) {
             }
         }
     }
-    if (NC && route_knob("DQNX_FWD_SPLIT", 1) != 0) {   // dense 1 (K = F) as 64 x 64 split-K tiles
+    if (NC && route_knob("DQNX_F1_SPLITK", 1) != 0) {   // dense 1 (K = F) as 64 x 64 split-K tiles
         const int nst = c.algo == DQNX_ALGO_DQN ? 2 : 3;
         e->f1_ksplit = fwd_split_ksplit(e->Bl, e->np.dense[0].out, e->np.dense[0].in, nst, e->n_cu, &e->f1_kchunk);
     }
@@ -2732,10 +2741,6 @@ int dqnx_engine_bind(dqnx_engine* e, void* arena, uint64_t bytes) {
     e->arena = (char*)arena;
     e->perm_dirty = true;
     e->wblk_dirty = true;
-    int dev = 0, cus = 0;   // the current device's compute units (plans that size grids to the chip)
-    if (hipGetDevice(&dev) == hipSuccess &&
-        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && cus > 0)
-        e->n_cu = cus;
     return DQNX_OK;
 }
 
@@ -2782,6 +2787,7 @@ int dqnx_engine_reset(dqnx_engine* e, void* stream) {
     e->pf_valid = false;
     e->pf_inlaunch = false;
     e->wblk_dirty = true;
+    e->perm_dirty = true;   // the workspace memset above zeroed the permuted conv weight copies too
     return DQNX_OK;
 }
 
@@ -2918,6 +2924,14 @@ int dqnx_rng_get_async(dqnx_engine* e, int32_t which, uint32_t* state625, void* 
     if (e->pf_valid) return set_error(DQNX_ESTATE, "rng_get_async while a prefetched minibatch is pending");
     const uint32_t* src = which == DQNX_RNG_PY ? ctrl_of(e)->py_mt : ctrl_of(e)->np_mt;
     DQNX_HIP_CHECK(hipMemcpyAsync(state625, src, 625 * 4, hipMemcpyDeviceToHost, (hipStream_t)stream));
+    return DQNX_OK;
+}
+
+int dqnx_ctrl_get_async(dqnx_engine* e, void* dst, void* stream) {
+    int rc = check_bound(e);
+    if (rc) return rc;
+    if (!dst) return set_error(DQNX_EINVAL, "null argument");
+    DQNX_HIP_CHECK(hipMemcpyAsync(dst, ctrl_of(e), sizeof(dqnx_ctrl), hipMemcpyDeviceToHost, (hipStream_t)stream));
     return DQNX_OK;
 }
 

@@ -738,8 +738,8 @@ __global__ __launch_bounds__(256) void k_adam(AdamArgs a) {
             if (sg.wide) {   // k_adam4's wide order: 8 strided partials, then its xor butterfly
                 float part[8];
 #pragma unroll
-                for (int j = 0; j < 8; j++) {
-                    float t = pp[(int64_t)j * ps];
+                for (int j = 0; j < 8; j++) {   // lanes past the segment's slabs add zeros, as in k_adam4
+                    float t = j < sg.S ? pp[(int64_t)j * ps] : 0.f;
                     for (int w = j + 8; w < sg.S; w += 8) t += pp[(int64_t)w * ps];
                     part[j] = t;
                 }
@@ -1062,9 +1062,9 @@ __global__ __launch_bounds__(64 * DW16_NW) void k_dw_adam16(DwAdam16Args a) {
         const int x = (int)blockIdx.x - a.tiles - a.ptrack - (a.mtc ? 1 : 0) - (a.pf_nidx > 0 ? 1 : 0);
         if (x >= 0) {   // k_per_prop's body over 64 * DW16_NW updates (the red table as its LDS)
             if constexpr (sizeof(red) >= PER_TOP * sizeof(double)) {   // (launch_dw_adam16: 32 x 16 tiles only)
-                if (a.ptrack) per_prop_wait(a.pprop);   // the tracking workgroup of this launch first
+                if (a.ptrack) per_prop_wait(a.pprop, x * 64 * DW16_NW);   // the tracking workgroup of this launch first
                 per_prop_block(a.pprop, x * 64 * DW16_NW, reinterpret_cast<double*>(&red[0][0][0]));
-                if (a.ptrack) per_prop_finish(a.pprop, a.pprop_wgs);
+                DQNX_STAMP_WG(a.pprop.stamps, 52);
             }
         } else if (a.ptrack && (int)blockIdx.x == a.tiles) {   // k_per_update's tracking (dispatched
             // right after the tiles, before the prop workgroups that wait for it)

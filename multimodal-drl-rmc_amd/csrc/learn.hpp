@@ -71,7 +71,7 @@ struct PerUpdateArgs {
     // (PER_SKIP_PREP) and k_per_prop's workgroups run beside the weight-gradient tiles (PER_SKIP_PROP)
     int32_t skip;
     // the tracking workgroup -> prop workgroups hand-off inside one launch (k_dw_adam16 hosting
-    // both): [0] tracking done, [1] prop workgroups finished (the last one zeroes both)
+    // both): the chunk epoch the tracking workgroup last advanced to (per_track_publish)
     uint32_t* sync;
 };
 constexpr int PER_SKIP_PREP = 1, PER_SKIP_PROP = 2, PER_SKIP_TRACK = 4;

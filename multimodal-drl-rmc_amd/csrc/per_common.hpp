@@ -67,22 +67,28 @@ __device__ __forceinline__ void per_prop_block(const PerUpdateArgs& a, int i0, d
 }
 
 // In-launch hand-off when one launch hosts the tracking workgroup and the prop workgroups
-// (k_dw_adam16): the tracking workgroup publishes when it is done; the prop workgroups,
-// dispatched after it (so it is resident or finished while they wait), spin on that word; the
-// last prop workgroup to finish zeroes both words for the next launch.  The wait is bounded: past
-// ~2^21 sleeps the prop workgroups go on with DQNX_DEVERR_PER_HANDOFF in ctrl.error (a broken
-// launch shape reports instead of hanging the queue).
+// (k_dw_adam16): the tracking workgroup publishes the chunk epoch it has just advanced to; the prop
+// workgroups, dispatched after it (so it is resident or finished while they wait), spin until the
+// word holds THEIR chunk's epoch, which they read from the latest-writer tag the head kernel left on
+// the slot of their first update (epoch + 1 in the high word, per_prep_item).  A publish is tied to
+// its launch, so nothing needs resetting between launches and a publish that arrives late (after a
+// timed-out wait) can never satisfy the next launch's wait.  The wait is bounded: past ~2^21 sleeps
+// the prop workgroups go on with DQNX_DEVERR_PER_HANDOFF in ctrl.error (a broken launch shape
+// reports instead of hanging the queue; their tag check then writes no leaf, and the Agent raises).
 __device__ __forceinline__ void per_track_publish(const PerUpdateArgs& a) {
     __syncthreads();
     if (threadIdx.x == 0) {   // after thread 0's leaf / ctrl / epoch stores (per_track_block)
+        const uint32_t ep = *(volatile uint32_t*)a.epoch;   // thread 0 advanced it
         __threadfence();
-        __hip_atomic_store(a.sync, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(a.sync, ep, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
-__device__ __forceinline__ void per_prop_wait(const PerUpdateArgs& a) {
-    if (threadIdx.x == 0) {
+__device__ __forceinline__ void per_prop_wait(const PerUpdateArgs& a, int i0) {
+    if (threadIdx.x == 0 && i0 < a.n) {
+        const int64_t slot = (int64_t)a.wl[i0] - (a.cap - 1);
+        const uint32_t want = (uint32_t)(a.last[slot] >> 32);   // written by the previous launch
         uint32_t spins = 0;
-        while (__hip_atomic_load(a.sync, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == 0u) {
+        while (__hip_atomic_load(a.sync, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) != want) {
             __builtin_amdgcn_s_sleep(4);
             if (++spins == (1u << 21)) {
                 __hip_atomic_store(&a.ctrl->error, (int32_t)DQNX_DEVERR_PER_HANDOFF, __ATOMIC_RELAXED,
@@ -94,14 +100,6 @@ __device__ __forceinline__ void per_prop_wait(const PerUpdateArgs& a) {
     __syncthreads();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     DQNX_STAMP_WG(a.stamps, 51);
-}
-__device__ __forceinline__ void per_prop_finish(const PerUpdateArgs& a, int nprop) {
-    __syncthreads();
-    DQNX_STAMP_WG(a.stamps, 52);
-    if (threadIdx.x == 0 && atomicAdd(a.sync + 1, 1u) == (uint32_t)nprop - 1) {
-        __hip_atomic_store(a.sync + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(a.sync, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
 }
 
 // ---------------------------------------------------------------------------------------

@@ -86,7 +86,7 @@ EXPORTS = [
     "dqnx_events_destroy", "dqnx_event_elapsed", "dqnx_debug_stamps",
     "dqnx_per_sample", "dqnx_per_update_priorities", "dqnx_set_agent_step", "dqnx_act", "dqnx_act_scratch_bytes",
     "dqnx_params_modified", "dqnx_dp_bucket_count", "dqnx_dp_bucket_info", "dqnx_learn_step_bucket",
-    "dqnx_apply_grads_bucket",
+    "dqnx_apply_grads_bucket", "dqnx_ctrl_get_async", "dqnx_rng_sample_words", "dqnx_rng_advance",
 ]
 
 _lib = None
@@ -154,6 +154,9 @@ def lib():
         "dqnx_set_agent_step": ([vp, I64, vp], ctypes.c_int),
         "dqnx_act": ([P(NetDesc), vp, vp, I32, vp, vp, vp, ctypes.c_uint64, vp], ctypes.c_int),
         "dqnx_act_scratch_bytes": ([P(NetDesc), I32], ctypes.c_uint64),
+        "dqnx_ctrl_get_async": ([vp, vp, vp], ctypes.c_int),
+        "dqnx_rng_sample_words": ([vp, I64, I32, vp, P(I64)], ctypes.c_int),
+        "dqnx_rng_advance": ([vp, I64, vp], ctypes.c_int),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)

@@ -14,23 +14,28 @@ What changes underneath:
 * `learn()` is one stream-ordered launch sequence: sample → gather → forwards → TD → loss →
   backward → Adam.
 
-Host-visible RNG semantics are the reference's.
-* `random.sample` (uniform replay) continues Python's global MT19937 stream.
-* PER's `np.random.uniform` continues numpy's global legacy stream.
-Both are handed to the engine before the step and taken back after it, so
-`choose_actions`' ε-greedy draws interleave exactly as in the reference.
+Host-visible semantics are the reference's, synchronously from the caller's view:
+
+* RNG.  The device sampler draws the minibatch bit-exactly from the caller's global generator:
+  CPython's `random` (`random.sample`, uniform replay) or numpy's legacy global state
+  (`np.random.uniform`, PER).  learn() stages the current state for the device and advances the
+  global generator on the host by exactly the words that draw consumes before it returns
+  (dqnx_rng_sample_words: the rejection / duplicate redraws are walked on the host; PER: 2 words
+  per sample), so `choose_actions`' epsilon-greedy draws -- or any other host draw -- interleave
+  exactly as in the reference.  The state the device returns is checked against that mirror.
+* Weights.  `online_network(x)`, `.value` / `.advantages`, `.parameters()` / `named_parameters()`,
+  `state_dict()` and every replay / engine read launch a recorded step first; stream order does the
+  rest, so they read the post-step weights.
+* Errors.  learn() with fewer stored transitions than `batch_size` raises ValueError as
+  `random.sample` does (R:dqn/replay_memory.py:39); a sticky device error (PER tree hand-off, empty
+  SumTree) comes back with the control block after each step and is raised at the agent's next
+  synchronisation point (`choose_actions`, `log`, `save_model`, `flush`).
 
 The train.py loop without host round trips (R:train.py:88-108: choose_actions ->
 store_transitions -> learn -> update_target_network -> log -> save_model): `learn()` records the
-step and returns; the step is launched by the next agent call -- by `update_target_network()`
-as ONE launch sequence with the soft update fused into the Adam pass (what
-`update_target_network` would do next anyway), otherwise as a plain learn step.  The RNG state
-goes to the device and comes back through pinned buffers without a synchronisation; it is
-installed into Python's `random` (numpy's global state under PER) at the next agent call that
-needs it (`choose_actions`, `learn`, or `flush()`).  The results are bitwise those of the eager
-order.  The contract this adds: code that draws from `random` / `np.random` or reads the
-networks' parameters between `learn()` and the next agent method must call `agent.flush()`
-first.  DQNX_AGENT_DEFER=0 restores the synchronous learn().
+step and returns; the next agent call launches it -- `update_target_network()` as ONE launch
+sequence with the soft update fused into the Adam pass (what it would do next anyway), any other
+call as a plain learn step.  DQNX_AGENT_DEFER=0 launches and waits for the step inside learn().
 """
 from __future__ import annotations
 
@@ -44,7 +49,7 @@ import numpy as np
 import torch as T
 
 from . import _capi as C
-from .engine import LearnEngine, spec_from_body
+from .engine import LearnEngine, raise_device_error, spec_from_body
 from .network import DeepQNetwork, DuelingDeepQNetwork
 from .replay_memory import ReplayMemoryNaive, ReplayMemoryPrioritized
 
@@ -169,7 +174,8 @@ class Agent:
         self._learn_t0 = time.time()
         self._defer = os.environ.get("DQNX_AGENT_DEFER", "1") != "0"
         self._learn_pending = False    # learn() recorded, not launched yet
-        self._rng_pending = False      # the advanced sampler RNG is on its way back (pinned buffer)
+        self._rng_expect = None        # host mirror of the recorded step's post-draw RNG state
+        self._rng_check = None         # ... of the last launched step (checked against its readback)
         self.engine.launch_hook = self._launch_pending
         self.engine.settle_hook = self.flush
         self.update_target_network(force=True)
@@ -205,7 +211,7 @@ class Agent:
     def choose_actions(self, obses):
         self._launch_pending()
         actions = self.online_network.actions(obses)   # (waits for the stream: the learn step ran)
-        self.flush()                                   # the sampler's RNG back into `random` first
+        self._settle(wait=True)                        # free after that wait: errors, RNG mirror check
         for i in range(len(actions)):
             if random.random() <= self.epsilon():
                 actions[i] = random.randint(0, self.output_dim - 1)
@@ -215,23 +221,18 @@ class Agent:
     # RNG stream the sampler consumes: CPython's global `random` (uniform replay)
     _rng_which = C.DQNX_RNG_PY
 
-    def _rng_to_engine(self):
-        if self._rng_which == C.DQNX_RNG_PY:
-            st = random.getstate()
-            self._py_state_meta = st   # (version, -, gauss_next): restored around the new words
-            self.engine.set_rng_async(C.DQNX_RNG_PY, st[1])
-        else:
-            st = np.random.get_state()
-            self.engine.set_rng_async(C.DQNX_RNG_NP, np.append(np.asarray(st[1], dtype=np.uint32), np.uint32(st[2])))
+    def _check_population(self):
+        """random.sample(deque, batch_size) raises when the deque is shorter (R:dqn/replay_memory.py:39)."""
+        if self.engine.ring_size < self.batch_size:
+            raise ValueError("Sample larger than population or is negative")
 
-    def _rng_from_engine(self):
-        if self._rng_which == C.DQNX_RNG_PY:
-            v, _, g = self._py_state_meta
-            random.setstate((v, self.engine.rng_async_out_tuple(), g))
-        else:
-            a = self.engine.rng_async_out
-            st = np.random.get_state()
-            np.random.set_state((st[0], a[:624].copy(), int(a[624]), st[3], st[4]))
+    def _rng_handoff(self):
+        """Stage the global state for the device's draw and move the global generator past it now."""
+        e = self.engine
+        staged = e.stage_rng(random.getstate()[1])
+        words, after = e.sample_words(staged, e.ring_size, self.batch_size)
+        random.getrandbits(32 * words)   # exactly `words` MT19937 outputs, gauss_next untouched
+        return after
 
     def _pre_learn(self):
         """Per-algorithm host bookkeeping before the step is launched (PER: the beta step)."""
@@ -239,28 +240,47 @@ class Agent:
     def _launch_learn(self, soft_update):
         e = self.engine
         self._pre_learn()
-        self._rng_to_engine()                # async H2D from pinned memory
+        e.upload_staged_rng(self._rng_which)   # async H2D from the pinned staging block
         e.learn_step(soft_update=soft_update)
-        e.get_rng_async(self._rng_which)     # async D2H + event
+        e.ctrl_readback()                      # async D2H of the control block + event
         self._learn_pending = False
-        self._rng_pending = True
+        self._rng_check = self._rng_expect
 
     def _launch_pending(self, soft_update=False):
         if self._learn_pending:
             self._launch_learn(soft_update)
 
+    def _settle(self, wait):
+        """Look at the control block the last launched step sent back (if it has arrived, or waiting
+        for it): raise its sticky device error, and check the device sampler's advanced state against
+        the host mirror learn() installed."""
+        c = self.engine.ctrl_readback_result(wait)
+        if c is None:
+            return
+        ctrl = C.Ctrl.from_buffer_copy(c.tobytes())
+        if ctrl.error:
+            raise_device_error(ctrl.error)
+        want = self._rng_check
+        if want is not None:
+            got = np.frombuffer(c, dtype=np.uint32, count=625,
+                                offset=0 if self._rng_which == C.DQNX_RNG_PY else 2500)
+            if not np.array_equal(got, want):
+                raise RuntimeError("libdqnx: the device sampler's RNG state differs from the host mirror of "
+                                   "the reference's draw (internal error)")
+
     def flush(self):
-        """Launch a recorded learn step and install the advanced sampler RNG into Python's global
-        state (waits for the step).  Agent methods call it where they need it."""
+        """Launch a recorded learn step, wait for it and raise any device error it reported.  Not
+        needed for correctness (every read launches a recorded step first); agent methods that
+        synchronise anyway call it."""
         self._launch_pending()
-        if self._rng_pending:
-            self.engine.rng_wait()
-            self._rng_from_engine()
-            self._rng_pending = False
+        self._settle(wait=True)
 
     def learn(self):
         """One learn step on the engine (R:dqn/agent.py:166-185 / 204-226 / 245-272)."""
-        self.flush()
+        self._launch_pending()
+        self._settle(wait=False)
+        self._check_population()
+        self._rng_expect = self._rng_handoff()
         self._learn_pending = True
         self._count_learn()
         if not self._defer:
@@ -356,13 +376,23 @@ class PerDoubleAgent(Agent):
     def _make_replay(self):
         return ReplayMemoryPrioritized(self.buffer_size, self.batch_size, self.epsilon_decay, engine=self.engine)
 
+    def _check_population(self):
+        # the reference samples a partly filled tree (with repeats); an empty one has no transitions
+        if self.engine.ring_size == 0:
+            raise ValueError("PER sample from an empty replay memory")
+
+    def _rng_handoff(self):
+        """np.random.uniform once per sample (R:dqn/replay_memory.py:79-80): 2 words each."""
+        e = self.engine
+        st = np.random.get_state()
+        staged = e.stage_rng(np.append(np.asarray(st[1], dtype=np.uint32), np.uint32(st[2])))
+        np.random.random_sample(self.batch_size)   # the same 2 * batch_size legacy MT19937 words
+        return e.rng_advance(staged, 2 * self.batch_size)
+
     def learn(self):
-        self.flush()
+        self._launch_pending()                            # a step recorded earlier keeps its own step
         self._learn_step_at = self.step * self.n_env      # R:dqn/agent.py:247 (the step of THIS learn)
-        self._learn_pending = True
-        self._count_learn()
-        if not self._defer:
-            self.flush()
+        super().learn()
 
     def _pre_learn(self):
         e = self.engine

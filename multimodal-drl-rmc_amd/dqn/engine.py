@@ -273,7 +273,7 @@ class LearnEngine:
         self.agent_step = 0      # host mirror of dqnx_ctrl.agent_step (PER beta schedule)
         # set by a drop-in Agent that records learn() steps for launch at its next call: `launch_hook`
         # launches a recorded step (host reads of engine memory follow it in stream order),
-        # `settle_hook` also installs the sampler's advanced RNG into the global state (host draws)
+        # `settle_hook` also waits for it and raises a device error it reported
         self.launch_hook = None
         self.settle_hook = None
 
@@ -403,51 +403,80 @@ class LearnEngine:
                                     self.stream()), "rng_get")
         return a
 
-    # asynchronous RNG hand-off (dqnx_rng_set_async / _get_async through pinned buffers): the drop-in
-    # Agent's learn() installs Python's / numpy's state and reads the advanced one back without a
-    # host round trip; `rng_wait()` (an event after the download) before reading `rng_async_out`
-    def _rng_pinned(self):
-        if getattr(self, "_rng_pin", None) is None:
-            self._rng_pin = (torch.empty(625, dtype=torch.int32).pin_memory(),
-                             torch.empty(625, dtype=torch.int32).pin_memory())
-            self._rng_ev = torch.cuda.Event()
-            self._rng_ev_live = False
-            self._rng_pin_np = tuple(t.numpy().view(np.uint32) for t in self._rng_pin)
-        return self._rng_pin
+    # ---- the drop-in Agent's hand-off (no host round trip per learn()) ------------------
+    # Before a recorded step launches, the caller's global RNG state is staged into one of two pinned
+    # blocks (`stage_rng`) and uploaded with the step (`upload_staged_rng`, dqnx_rng_set_async); after
+    # it, the whole control block comes back into a pinned block with an event (`ctrl_readback`,
+    # dqnx_ctrl_get_async), read at the caller's next synchronisation point (`ctrl_readback_result`).
+    def _handoff_bufs(self):
+        if getattr(self, "_stage_pin", None) is None:
+            self._stage_pin = [torch.empty(625, dtype=torch.int32).pin_memory() for _ in range(2)]
+            self._stage_np = [t.numpy().view(np.uint32) for t in self._stage_pin]
+            self._stage_ev = [torch.cuda.Event(), torch.cuda.Event()]
+            self._stage_live = [False, False]
+            self._stage_i = 0
+            self._ctrl_pin = torch.empty(ctypes.sizeof(C.Ctrl), dtype=torch.uint8).pin_memory()
+            self._ctrl_np = self._ctrl_pin.numpy()
+            self._ctrl_ev = torch.cuda.Event()
+            self._ctrl_live = False
 
-    def set_rng_async(self, which: int, state625) -> None:
-        """state625: 625 words -- a numpy array, or a tuple of Python ints (random.getstate()[1],
-        packed straight into the pinned buffer: no 625-object numpy conversion)."""
-        src, _ = self._rng_pinned()
-        self.rng_wait()                    # the previous copies out of / into the pinned buffers ran
+    def stage_rng(self, state625) -> np.ndarray:
+        """Pack 625 words (a numpy array, or random.getstate()[1]'s tuple of ints, packed with struct:
+        no 625-object conversion) into the next pinned staging block and return it (uint32 view).  The
+        block's previous upload has run by then (its event is waited for, normally long passed)."""
+        self._handoff_bufs()
+        i = self._stage_i = self._stage_i ^ 1
+        if self._stage_live[i]:
+            self._stage_ev[i].synchronize()
+            self._stage_live[i] = False
+        dst = self._stage_np[i]
         if isinstance(state625, tuple):
-            struct.pack_into("625I", self._rng_pin_np[0], 0, *state625)
+            struct.pack_into("625I", dst, 0, *state625)
         else:
-            self._rng_pin_np[0][:] = state625
-        C.check(self.L.dqnx_rng_set_async(self.h, which, ctypes.c_void_p(src.data_ptr()), self.stream()),
-                "rng_set_async")
+            dst[:] = state625
+        return dst
 
-    def get_rng_async(self, which: int) -> None:
-        _, dst = self._rng_pinned()
-        C.check(self.L.dqnx_rng_get_async(self.h, which, ctypes.c_void_p(dst.data_ptr()), self.stream()),
-                "rng_get_async")
-        self._rng_ev.record(torch.cuda.current_stream(self.device))
-        self._rng_ev_live = True
+    def upload_staged_rng(self, which: int) -> None:
+        """The block of the last stage_rng() into dqnx_ctrl's `which` state, stream-ordered."""
+        i = self._stage_i
+        C.check(self.L.dqnx_rng_set_async(self.h, which, ctypes.c_void_p(self._stage_pin[i].data_ptr()),
+                                          self.stream()), "rng_set_async")
+        self._stage_ev[i].record(torch.cuda.current_stream(self.device))
+        self._stage_live[i] = True
 
-    def rng_wait(self):
-        if getattr(self, "_rng_ev_live", False):
-            self._rng_ev.synchronize()
-            self._rng_ev_live = False
+    def ctrl_readback(self) -> None:
+        """dqnx_ctrl_get_async into the pinned control block + an event after it."""
+        self._handoff_bufs()   # (a readback nobody looked at is superseded: same stream, same block)
+        C.check(self.L.dqnx_ctrl_get_async(self.h, ctypes.c_void_p(self._ctrl_pin.data_ptr()), self.stream()),
+                "ctrl_get_async")
+        self._ctrl_ev.record(torch.cuda.current_stream(self.device))
+        self._ctrl_live = True
 
-    @property
-    def rng_async_out(self) -> np.ndarray:
-        self._rng_pinned()
-        return self._rng_pin_np[1]
+    def ctrl_readback_result(self, wait: bool):
+        """The control block of the last ctrl_readback() (a numpy uint8 view of the pinned copy), or None
+        when there is none pending or (wait=False) it has not arrived yet."""
+        if not getattr(self, "_ctrl_live", False):
+            return None
+        if wait:
+            self._ctrl_ev.synchronize()
+        elif not self._ctrl_ev.query():
+            return None
+        self._ctrl_live = False
+        return self._ctrl_np
 
-    def rng_async_out_tuple(self) -> tuple:
-        """The downloaded 625 words as a tuple of Python ints (random.setstate's format)."""
-        self._rng_pinned()
-        return struct.unpack("625I", self._rng_pin_np[1].tobytes())
+    # host-side RNG mirror (dqnx_rng_sample_words / dqnx_rng_advance; host only)
+    def sample_words(self, state625: np.ndarray, n: int, k: int):
+        """(words, state after) of CPython's random.sample(population of n, k) from `state625`."""
+        out = np.empty(625, dtype=np.uint32)
+        w = C.I64()
+        C.check(self.L.dqnx_rng_sample_words(state625.ctypes.data, int(n), int(k), out.ctypes.data, ctypes.byref(w)),
+                "rng_sample_words")
+        return int(w.value), out
+
+    def rng_advance(self, state625: np.ndarray, words: int) -> np.ndarray:
+        out = np.empty(625, dtype=np.uint32)
+        C.check(self.L.dqnx_rng_advance(state625.ctypes.data, int(words), out.ctypes.data), "rng_advance")
+        return out
 
     # ---- steps -----------------------------------------------------------------------
     def set_graphs(self, on: bool):
@@ -560,12 +589,16 @@ class LearnEngine:
         return float(self.ctrl().loss)
 
     def check_device_error(self):
-        err = self.ctrl().error
-        if err == C.DEVERR_SAMPLE_TOO_LARGE:
-            raise ValueError("Sample larger than population or is negative")
-        if err == C.DEVERR_EMPTY_TREE:
-            raise RuntimeError("libdqnx: PER sample from a SumTree with total priority 0")
-        if err == C.DEVERR_PER_HANDOFF:
-            raise RuntimeError("libdqnx: PER tree update hand-off timed out inside a launch (internal error)")
-        if err:
-            raise RuntimeError(f"libdqnx device error {err}")
+        raise_device_error(self.ctrl().error)
+
+
+def raise_device_error(err: int):
+    """The exception of a sticky dqnx_ctrl.error code (0: none)."""
+    if err == C.DEVERR_SAMPLE_TOO_LARGE:
+        raise ValueError("Sample larger than population or is negative")
+    if err == C.DEVERR_EMPTY_TREE:
+        raise RuntimeError("libdqnx: PER sample from a SumTree with total priority 0")
+    if err == C.DEVERR_PER_HANDOFF:
+        raise RuntimeError("libdqnx: PER tree update hand-off timed out inside a launch (internal error)")
+    if err:
+        raise RuntimeError(f"libdqnx device error {err}")

@@ -44,6 +44,18 @@ class Network(nn.Module):
     def actions(self, obses):
         raise NotImplementedError
 
+    def _engine_sync(self):
+        """An agent's recorded learn step is launched before anything reads these parameters (stream
+        order does the rest), so every read sees the post-step weights as after the reference's
+        synchronous learn() (R:dqn/agent.py:204-226)."""
+        eng = getattr(self, "_engine", None)
+        if eng is not None:
+            eng.launch_recorded()
+
+    def named_parameters(self, *args, **kwargs):   # (parameters() goes through it)
+        self._engine_sync()
+        return super().named_parameters(*args, **kwargs)
+
     # -- engine binding -------------------------------------------------------------
     def bind_flat(self, views: dict, flat=None, spec=None, engine=None):
         """Move every parameter into `views[name]` (same shape, engine memory), keeping
@@ -72,9 +84,7 @@ class Network(nn.Module):
     def _act_gpu(self, obses):
         """Greedy actions through dqnx_act: obs staged through pinned memory, one launch, the
         actions copied back and the stream synchronised once (the caller needs a list)."""
-        spec, flat = self._native_act()
-        if self._engine is not None:
-            self._engine.launch_recorded()   # the agent's recorded learn step updates these weights first
+        spec, flat = self._native_act()   # (its parameters() read launches a recorded learn step first)
         x = T.as_tensor(obses, dtype=T.float32)
         n = x.shape[0]
         x = x.reshape(n, -1)
@@ -145,13 +155,11 @@ class Network(nn.Module):
         return step, episode_count, rew_mean, len_mean
 
     def state_dict(self, *args, **kwargs):
-        if self._engine is not None:   # an agent's recorded learn step lands first (stream order)
-            self._engine.launch_recorded()
+        self._engine_sync()
         return super().state_dict(*args, **kwargs)
 
     def load_state_dict(self, state_dict, *args, **kwargs):
-        if self._engine is not None:
-            self._engine.launch_recorded()
+        self._engine_sync()
         out = super().load_state_dict(state_dict, *args, **kwargs)
         if self._engine is not None:   # written into the engine's buffer: refresh its derived layouts
             self._engine.params_modified()
@@ -169,6 +177,7 @@ class DeepQNetwork(Network):
         self.to(self.device)
 
     def forward(self, s):
+        self._engine_sync()
         return self.fc_out(self.net(s))
 
     def actions(self, obses):
@@ -192,13 +201,16 @@ class DuelingDeepQNetwork(Network):
         self.to(self.device)
 
     def forward(self, s):
+        self._engine_sync()
         net = self.net(s)
         return self.aggregate_layer(self.fc_val(net), self.fc_adv(net))
 
     def value(self, s):
+        self._engine_sync()
         return self.fc_val(self.net(s))
 
     def advantages(self, s):
+        self._engine_sync()
         return self.fc_adv(self.net(s))
 
     def actions(self, obses):

@@ -23,6 +23,7 @@ def assert_grad_close(got, ref, what=""):
 # and tensor; conftest.py writes them to gpurun_out/parity_exemptions.json at session end so the
 # count is on record for every run.
 EXEMPTIONS = []
+COMPARISONS = [0]   # compare_state calls (weights checked against the oracle) this session
 
 
 def record_exemptions(counts, numels):

@@ -9,6 +9,7 @@ import pytest
 import torch
 
 from dqn import Agents
+from dqn import _capi as C
 from oracle import ref as O
 from refnets import agent_kwargs, hybrid_network_config, mse_network_config, rmsprop_network_config
 
@@ -81,8 +82,7 @@ def test_gpu_agent_train_loop_matches_oracle(tmp_path, algo, obs_dim, batch, buf
         agent.update_target_network()
         rec = oracle.learn()
         oracle.update_target_network()
-        agent.flush()   # the advanced sampler RNG reaches the global state at the next agent call
-        torch.cuda.synchronize()
+        # no flush: learn() leaves the global generators where the reference's draw leaves them
         assert np.array_equal(np.asarray(random.getstate()[1], dtype=np.uint32), oracle.py_state)
         assert np.array_equal(O.np_state_to_array(), oracle.np_state)
         assert abs(agent.engine.loss() - rec.loss) <= 1e-5 * max(1.0, abs(rec.loss))
@@ -222,3 +222,84 @@ def test_gpu_agent_deferred_learn_bit_identical(tmp_path, monkeypatch, algo, sof
     assert torch.equal(a0.engine.params, a1.engine.params)
     assert torch.equal(a0.engine.target_params, a1.engine.target_params)
     assert torch.equal(a0.engine.adam_m, a1.engine.adam_m)
+
+
+@pytest.mark.parametrize("algo,net", [("DuelingDoubleDQNAgent", "mlp"), ("PerDuelingDoubleDQNAgent", "mlp"),
+                                      ("DQNAgent", "mlp"), ("DuelingDoubleDQNAgent", "hybrid")])
+def test_gpu_agent_reads_after_learn_see_the_step(tmp_path, algo, net):
+    """R:dqn/agent.py:204-226 is synchronous: right after learn() (no update_target_network, no flush)
+    the online network's forward / value / advantages and parameters() read the post-step weights, and
+    the global RNG has moved past the step's draw."""
+    seed = 23
+    torch.manual_seed(seed)
+    over = {"nn_conf_func": hybrid_network_config} if net == "hybrid" else {}
+    agent = getattr(Agents, algo)(**agent_kwargs(algo, 284, 64, 1000, tmp_path, **over))
+    head = O.algo_spec_head(algo)
+    spec = O.hybrid_spec(8, head) if net == "hybrid" else O.mlp_spec(284, 8, head)
+    init = O.reference_init(spec, seed)
+    oracle = O.OracleLearner(spec, algo, 64, 1000, seed=seed, params=init, per_pow="cr")
+    obs, act, rew, done, nobs = O.synth_transitions(700, 284, 8, seed=seed)
+    rows = (obs, [int(a) for a in act], [float(r) for r in rew], [bool(d) for d in done], nobs)
+    agent.store_transitions(*rows, None)
+    oracle.store_transitions(*rows)
+    random.seed(seed)
+    np.random.seed(seed)
+    x = torch.as_tensor(obs[:16], device=agent.device)
+    for t in range(2):
+        agent.step = oracle.step = t
+        oracle.py_state = O.py_state_to_array()
+        oracle.np_state = O.np_state_to_array()
+        agent.learn()
+        oracle.learn()
+        assert np.array_equal(np.asarray(random.getstate()[1], dtype=np.uint32), oracle.py_state)
+        assert np.array_equal(O.np_state_to_array(), oracle.np_state)
+        with torch.no_grad():
+            q = agent.online_network(x).cpu()
+        q_ref = O.q_forward(spec, oracle.online, x.cpu())
+        np.testing.assert_allclose(q.numpy(), q_ref.numpy(), atol=1e-5, rtol=0)
+        if head == "dueling":
+            with torch.no_grad():
+                adv = agent.online_network.advantages(x).cpu()
+            np.testing.assert_allclose(adv.numpy(), O.advantages(spec, oracle.online, x.cpu()).numpy(), atol=1e-5)
+        agent.update_target_network()
+        oracle.update_target_network()
+    got = {k: p.detach().cpu() for k, p in agent.online_network.named_parameters()}
+    for k in init:
+        np.testing.assert_allclose(got[k].numpy(), oracle.online[k].numpy(), atol=1e-5, rtol=0, err_msg=k)
+
+
+def test_gpu_agent_learn_raises_on_short_replay(tmp_path):
+    """random.sample(deque, batch_size) raises ValueError when fewer transitions are stored
+    (R:dqn/replay_memory.py:39): learn() on a 10-row buffer with batch 32 does too, leaves the global
+    RNG untouched, and the agent keeps working once the buffer holds enough."""
+    agent = Agents.DuelingDoubleDQNAgent(**agent_kwargs("DuelingDoubleDQNAgent", 14, 32, 500, tmp_path))
+    obs, act, rew, done, nobs = O.synth_transitions(40, 14, 8, seed=3)
+    agent.store_transitions(obs[:10], [int(a) for a in act[:10]], [float(r) for r in rew[:10]],
+                            [bool(d) for d in done[:10]], nobs[:10], None)
+    s0 = random.getstate()
+    with pytest.raises(ValueError, match="Sample larger than population"):
+        agent.learn()
+    assert random.getstate() == s0
+    agent.store_transitions(obs[10:], [int(a) for a in act[10:]], [float(r) for r in rew[10:]],
+                            [bool(d) for d in done[10:]], nobs[10:], None)
+    agent.learn()
+    agent.update_target_network()
+    agent.choose_actions(obs[:1])
+
+
+def test_gpu_agent_surfaces_device_errors(tmp_path):
+    """A sticky device error (dqnx_ctrl.error, e.g. the PER tree hand-off timing out inside a launch)
+    comes back with the control block after the step and is raised at the agent's next
+    synchronisation point instead of training on silently."""
+    agent = Agents.PerDuelingDoubleDQNAgent(**agent_kwargs("PerDuelingDoubleDQNAgent", 14, 32, 500, tmp_path))
+    obs, act, rew, done, nobs = O.synth_transitions(100, 14, 8, seed=4)
+    agent.store_transitions(obs, [int(a) for a in act], [float(r) for r in rew], [bool(d) for d in done], nobs, None)
+    agent.learn()
+    agent.update_target_network()
+    agent.choose_actions(obs[:1])   # clean so far
+    err_off = C.Ctrl.error.offset
+    agent.engine.ctrl_bytes[err_off:err_off + 4].view(torch.int32).fill_(C.DEVERR_PER_HANDOFF)
+    agent.learn()
+    agent.update_target_network()
+    with pytest.raises(RuntimeError, match="hand-off"):
+        agent.choose_actions(obs[:1])
