@@ -371,7 +371,9 @@ def run_learner(args, eng, world, backend, steps, warmup, dist, device, dp=None)
     torch.cuda.synchronize()
     eng.check_device_error()
     dp_graph = False
-    if dp and backend == "nccl" and not args.no_dp_graph:
+    # PER shard steps stay eager: replayed as captured graphs they measured ~3x slower on the GPU
+    # clock than the same launches issued eagerly (tools/c5_graph_diag.py)
+    if dp and backend == "nccl" and not args.no_dp_graph and not args.algo.startswith("Per"):
         # the whole DP step (shard kernels + RCCL all-reduce + Adam) as one replayed graph: the
         # eager loop is host-bound (3 launches + a collective call per ~50 us step).  RCCL
         # collectives are capturable; gloo's are host calls and never are.
@@ -865,7 +867,7 @@ def main():
                 "parallelism": f"dp{world}", "graphs": args.graphs, "prefetch_sampling": args.prefetch and not per and (world == 1 or args.net == "mlp"),
                 "steps_per_call": args.chain if not dpmode else 1,
                 "sampling": "rank-local" if local else "global (reference-exact random.sample on every rank)",
-                "dp_step": (((f"one HIP graph per {args.dp_graph_steps} steps" if dp_graph else "eager")
+                "dp_step": (((f"one HIP graph per {args.dp_graph_steps} steps" if dp_graph else "eager launches")
                              + (", per-layer gradient buckets" if args.net != "mlp" and not args.no_buckets else ""))
                             if dpmode else None),
                 "compute": args.compute,

@@ -449,6 +449,7 @@ struct dqnx_engine {
     bool perm_dirty = true;
     FusedFwdArgs fplan;     // LDS geometry of the fused plan (valid when bwd_plan == 2)
     int fsplit = 1;         // layer-1 column parts of the split forward (1: one forward launch)
+    int fsplit_mr = 1;      // 16-row blocks per workgroup of the split forward's layer-1 launch
     bool pf_valid = false;   // a prefetched minibatch for the next step sits in slot pf_slot
     bool pf_inlaunch = false;   // ... drawn by the previous step's forward launch (fused plan)
     int n_cu = 256;             // compute units of the device (hipDeviceAttributeMultiprocessorCount)
@@ -931,8 +932,7 @@ void build_fused_steps(dqnx_engine* e, int flags, int32_t* idx, int32_t* phys, s
     // the forward's outputs from its own XCD's L2 (16-row tiles, tiles % 8 == 0).  Measured at
     // B=1024: head_bwd 7.2 -> 6.6 us, the forward unchanged; DQNX_XCD_ROWS=0 keeps xcd_remap's order
     const int ftiles = (e->Bl + 15) / 16;
-    const bool xcd_rows = route_knob("DQNX_XCD_ROWS", 1) != 0 && e->fplan.mr == 1 &&
-                          ftiles % 8 == 0 && !(e->fsplit > 1 && L >= 2);
+    const bool xcd_rows = route_knob("DQNX_XCD_ROWS", 1) != 0 && e->fplan.mr == 1 && ftiles % 8 == 0;
     // 2. forward (R:dqn/agent.py:209-214 / 172-173 streams, R:dqn/network.py:61-65, 90-96)
     {
         FusedFwdArgs fa = e->fplan;
@@ -964,6 +964,7 @@ void build_fused_steps(dqnx_engine* e, int flags, int32_t* idx, int32_t* phys, s
         }
         fa.stamps = at<int64_t>(e, e->ws_stamps);
         fa.xcd_rows = xcd_rows ? 1 : 0;
+        fa.lds_min = 1024 * tuning_knob("DQNX_FWD_LDSKB", 0);
         fa.adam_ctrl = ctrl;   // (the head kernel below gets no ctrl: the forward stores the scalars)
         if (e->ws_npc && c.algo == DQNX_ALGO_PER_DOUBLE && !(e->fsplit > 1 && L >= 2 && fa.mr == 1)) {
             fa.npc = at<uint32_t>(e, e->ws_npc);   // the next PER sample's MT blocks, twisted ahead
@@ -988,14 +989,34 @@ void build_fused_steps(dqnx_engine* e, int flags, int32_t* idx, int32_t* phys, s
         k.bytes = 4.0 * (nstreams * Bl * np.dense[0].in + Bl * np.dense[0].in + Bl * hsum + 3.0 * Bl * 16)
                   + 2.0 * (wbytes + 4.0 * np.head_params);
         if (e->fsplit > 1 && L >= 2 && fa.mr == 1) {
-            // layer 1 on csplit workgroups per row tile, then layers 2.. + head (H_1 via HBM)
+            // layer 1 on csplit workgroups per (16 * fsplit_mr)-row tile, then layers 2.. + head (H_1
+            // via HBM); the sampler workgroup (in-launch prefetch) rides in the layer-1 launch
             const double w0 = (double)np.dense[0].in * np.dense[0].out;
             FusedFwdArgs f1 = fa, f2 = fa;
             f1.phase = 1;
             f1.csplit = e->fsplit;
+            f1.xcd_rows = 0;   // (the layer-2 launch places row tile t on XCD t % 8 for the head kernel)
+            f1.lds_min = 1024 * tuning_knob("DQNX_FWD_L1_LDSKB", 0);
+            f2.lds_min = 1024 * tuning_knob("DQNX_FWD_L2_LDSKB", 0);
+            if (e->fsplit_mr > 1) {
+                FusedFwdArgs t = e->fplan;
+                fused_fwd_plan(t, c.net.obs_dim, e->fplan.bf16 != 0, e->fsplit_mr);
+                f1.mr = t.mr;
+                f1.sx = t.sx;
+                f1.sh = t.sh;
+                f1.buf0 = t.buf0;
+                f1.buf1 = t.buf1;
+                f1.tiles = (e->Bl + 16 * f1.mr - 1) / (16 * f1.mr);
+            }
+            if (sample_next) {
+                const int wgs = f1.tiles * nstreams * f1.csplit + 1;
+                f1.samp_shape = sample_next->k <= 2048 ? 1 : (wgs <= e->n_cu ? 3 : 2);
+            }
             f2.phase = 2;
+            f2.samp_shape = 0;
+            f2.adam_ctrl = nullptr;   // (the layer-1 launch stores the step's Adam scalars)
             KStep k1, k2;
-            k1.name = "mlp_fwd_l1";
+            k1.name = sample_next ? "mlp_fwd_l1+sample" : "mlp_fwd_l1";
             k1.flops = nstreams * Bl * 2.0 * w0;
             k1.bytes = 4.0 * (nstreams * Bl * (np.dense[0].in + np.dense[0].out) + Bl * np.dense[0].in)
                        + 2.0 * (e->fplan.bf16 ? 2.0 : 4.0) * w0;
@@ -1338,7 +1359,7 @@ SampleArgs uniform_sample_args(dqnx_engine* e, int32_t* idx, int32_t* phys) {
 bool inlaunch_prefetch_ok(const dqnx_engine* e, int flags) {
     if (tuning_flag("DQNX_PF_SIDE")) return false;   // measurements: the side-stream pipeline instead
     if (e->cfg.algo == DQNX_ALGO_PER_DOUBLE || (flags & DQNX_STEP_GIVEN_INDICES)) return false;
-    if (e->bwd_plan == 2) return e->Bs <= FWD_SAMPLE_MAX_K && e->fsplit <= 1;
+    if (e->bwd_plan == 2) return e->Bs <= FWD_SAMPLE_MAX_K;
     return e->bwd_plan == 0 && e->micro && e->Bs <= MICRO_SAMPLE_MAX_K;
 }
 // the fused plan's blocked weight copies need a rebuild launch before the next step
@@ -2605,6 +2626,11 @@ int dqnx_engine_create(const dqnx_config* cfg, dqnx_engine** out) {
                 const int w = route_knob("DQNX_FWD_SPLIT", 1);
                 if (w <= 1) e->fsplit = 1;
                 else if (e->np.dense[0].out % (16 * w) == 0) e->fsplit = w;
+            }
+            if (e->fsplit > 1) {   // layer 1's row tiles: 32 rows (each weight fragment feeds 2 MFMAs)
+                const int m = route_knob("DQNX_FWD_L1_MR", 2);
+                FusedFwdArgs t2 = e->fplan;
+                if (m == 2 && fused_fwd_plan(t2, c.net.obs_dim, e->fplan.bf16 != 0, 2)) e->fsplit_mr = 2;
             }
         }
     }

@@ -330,7 +330,7 @@ __global__ __launch_bounds__(FT) void k_mlp_fwd(FusedFwdArgs a) {
     const int T0 = xcd_remap(bid, a.tiles * a.nstreams * nsp);
     int part = T0 % nsp, T = T0 / nsp;   // the parts of one row tile are neighbours (one XCD)
     int z = T / a.tiles, tile = T - z * a.tiles;
-    if (PH == 0 && a.xcd_rows) {   // row tile t of every stream on XCD t % 8 (tiles % 8 == 0)
+    if (PH != 1 && a.xcd_rows) {   // row tile t of every stream on XCD t % 8 (tiles % 8 == 0)
         const int tp = a.tiles >> 3, L = bid >> 3;
         z = L / tp;
         tile = (L - z * tp) * 8 + (bid & 7);
@@ -344,7 +344,7 @@ __global__ __launch_bounds__(FT) void k_mlp_fwd(FusedFwdArgs a) {
     const bool keep = (s == 0);
     const int coff = PH == 1 ? part * (a.out[0] / nsp) : 0;   // layer-1 columns of this part
 
-    DQNX_STAMP(a.stamps, 24);
+    if (PH != 2) DQNX_STAMP(a.stamps, 24);   // (slots 24-27: the layer-1 launch of a split forward)
     // the step's Adam scalars for the update launch: a dependent ctrl -> table chain on the last
     // thread of one workgroup, hidden under that workgroup's gather
     if (PH != 2 && a.adam_ctrl && T0 == a.tiles * a.nstreams * nsp - 1 && tid == FT - 1) adam_advance(a.adam_ctrl, a.ab);
@@ -430,9 +430,9 @@ __global__ __launch_bounds__(FT) void k_mlp_fwd(FusedFwdArgs a) {
         }
     }
     }   // PH != 2
-    DQNX_STAMP(a.stamps, 25);
+    if (PH != 2) DQNX_STAMP(a.stamps, 25);
     lds_barrier();
-    DQNX_STAMP(a.stamps, 26);
+    if (PH != 2) DQNX_STAMP(a.stamps, 26);
 
     int cur = 0;
 #pragma unroll
@@ -1018,16 +1018,18 @@ static void allow_lds(K kern, size_t bytes) {
 }
 
 int launch_fused_fwd(const FusedFwdArgs& a, int act, hipStream_t s) {
-    if (a.phase != 0 && (a.L < 2 || a.mr != 1 || (a.phase == 1 && (a.csplit < 1 || a.out[0] % (16 * a.csplit)))))
-        return set_error(DQNX_EUNSUPPORTED, "split forward: L >= 2, 16-row tiles, layer 1 width / parts a multiple of 16");
-    if (a.samp_shape && (a.phase != 0 || a.samp_shape > 3 || a.samp.k > FWD_SAMPLE_MAX_K ||
+    if (a.phase != 0 && (a.L < 2 || a.mr != (a.phase == 1 ? a.mr : 1) || (a.phase == 1 && a.mr > 2) ||
+                         (a.phase == 1 && (a.csplit < 1 || a.out[0] % (16 * a.csplit)))))
+        return set_error(DQNX_EUNSUPPORTED, "split forward: L >= 2, 16-row tiles (layer 1: 16 or 32), layer 1 width / parts a multiple of 16");
+    if (a.samp_shape && (a.phase == 2 || a.samp_shape > 3 || a.samp.k > FWD_SAMPLE_MAX_K ||
                          (a.samp_shape == 1 && a.samp.k > 2048)))
-        return set_error(DQNX_EUNSUPPORTED, "forward sampler workgroup: whole forward, k <= %d", FWD_SAMPLE_MAX_K);
+        return set_error(DQNX_EUNSUPPORTED, "forward sampler workgroup: whole forward or layer-1 launch, k <= %d", FWD_SAMPLE_MAX_K);
     if (a.npc && (a.samp_shape || a.phase == 2 || a.npc_blocks > NPC_MAX_BLOCKS))
         return set_error(DQNX_EUNSUPPORTED, "forward MT-cache workgroup: not with the sampler workgroup / phase 2");
     const dim3 grid(a.tiles * a.nstreams * (a.phase == 1 ? a.csplit : 1) + ((a.samp_shape || a.npc) ? 1 : 0)), block(FT);
     size_t shm = (size_t)(a.buf0 + a.buf1) * 4;
     if (shm < (size_t)DQNX_FUSED_LDS_MIN) shm = DQNX_FUSED_LDS_MIN;
+    if (shm < (size_t)a.lds_min) shm = (size_t)a.lds_min;
     if (a.samp_shape && shm < (size_t)fwd_sample_lds_bytes(a.samp_shape)) shm = fwd_sample_lds_bytes(a.samp_shape);
     if (a.npc && shm < (size_t)(2 * 624 + 2) * 4) shm = (2 * 624 + 2) * 4;
 #define FUSED_FWD_MR(ACTV, NLV, BFV, MRV, PHV)                                                       \
@@ -1037,7 +1039,12 @@ int launch_fused_fwd(const FusedFwdArgs& a, int act, hipStream_t s) {
     } while (0)
 #define FUSED_FWD_BF(ACTV, NLV, BFV)                                                                 \
     do {                                                                                             \
-        if (a.phase == 1) { if constexpr (NLV >= 2) FUSED_FWD_MR(ACTV, NLV, BFV, 1, 1); }             \
+        if (a.phase == 1) {                                                                          \
+            if constexpr (NLV >= 2) {                                                                \
+                if (a.mr == 2) FUSED_FWD_MR(ACTV, NLV, BFV, 2, 1);                                   \
+                else FUSED_FWD_MR(ACTV, NLV, BFV, 1, 1);                                             \
+            }                                                                                        \
+        }                                                                                            \
         else if (a.phase == 2) { if constexpr (NLV >= 2) FUSED_FWD_MR(ACTV, NLV, BFV, 1, 2); }        \
         else if (a.mr == 4) FUSED_FWD_MR(ACTV, NLV, BFV, 4, 0);                                      \
         else if (a.mr == 2) FUSED_FWD_MR(ACTV, NLV, BFV, 2, 0);                                      \

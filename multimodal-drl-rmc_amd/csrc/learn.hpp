@@ -483,6 +483,7 @@ struct FusedFwdArgs {
     uint32_t* npc;
     const uint32_t* np_state;   // ctrl->np_mt (the state the cache must start from)
     int npc_blocks;
+    int lds_min;                 // dynamic LDS request floor in bytes (placement knob: > 80 KB = one workgroup per CU)
 };
 // The forward's sampler workgroup (512 threads), three LDS shapes (FusedFwdArgs::samp_shape):
 //   1: k <= 2048, passes of 3 MT blocks into a 4096-slot table (40 KB, no more than the forward's

@@ -77,6 +77,30 @@ for gs in (1, 4):
         torch.cuda.synchronize()
     out[f"graph{gs}"]["replay_sync_us"] = (time.perf_counter() - t0) / 10 * 1e6
     del g
+# bisection: graphs of the shard step's halves alone (timing only: the state they leave is meaningless)
+for part, fn in (("learn_only", lambda: eng.learn_step(grads_only=True)),
+                 ("apply_only", lambda: eng.apply_grads(soft_update=True))):
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        fn()
+    for _ in range(3):
+        g.replay()
+    torch.cuda.synchronize()
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    ev0.record()
+    for _ in range(50):
+        g.replay()
+    ev1.record()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(50):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    out[part] = {"graph_us": ev0.elapsed_time(ev1) * 1e3 / 50, "eager_us": e0.elapsed_time(e1) * 1e3 / 50}
+    del g
 eng.set_graphs(args.graphs)
 eng.check_device_error()
 print(json.dumps(out), flush=True)
