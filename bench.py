@@ -90,6 +90,10 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-buckets", action="store_true",
                    help="conv nets under DP: one gradient all-reduce instead of per-layer buckets")
+    p.add_argument("--mlp-buckets", action="store_true",
+                   help="MLP under DP: two gradient buckets (every layer but layer 1, then layer 1), bucket 0's "
+                        "all-reduce and Adam on a side stream under layer 1's dW tiles (default: one all-reduce; "
+                        "DESIGN.md section 6 has the latency model)")
     p.add_argument("--cpu-seconds", type=float, default=6.0, help="seconds per CPU-baseline leg")
     p.add_argument("--no-kernel-timing", action="store_true")
     p.add_argument("--no-extras", action="store_true",
@@ -349,17 +353,20 @@ def run_learner(args, eng, world, backend, steps, warmup, dist, device, dp=None)
     # conv nets exchange per-layer gradient buckets on a side stream, overlapped with the rest of
     # the backward (dp_learn_step_bucketed); the MLP's 428 KB gradient stays one all-reduce
     dp = world > 1 if dp is None else dp   # the data-parallel step (DQNX_BENCH_FORCE_DP: also at world 1)
-    bucketed = dp and args.net != "mlp" and not args.no_buckets
+    bucketed = dp and ((args.net != "mlp" and not args.no_buckets) or (args.net == "mlp" and args.mlp_buckets))
+    if bucketed and args.net == "mlp" and len(eng.dp_buckets()) < 2:
+        bucketed = False   # (past 2048 rows per GPU the MLP's gradient comes from the slab plan: one bucket)
 
     chain = args.chain if not dp else 1
 
     # pure learning loop, uniform replay: step t+1's minibatch is drawn inside step t's forward launch
-    prefetch = args.prefetch and not args.algo.startswith("Per") and not bucketed
+    # (bucketed conv nets sample their own minibatch; the bucketed MLP step prefetches like the plain one)
+    prefetch = args.prefetch and not args.algo.startswith("Per") and (not bucketed or args.net == "mlp")
 
     def step(count=1):
         if dp:   # shard compute, RCCL all-reduce (+ PER |delta| all-gather), replicated Adam
             if bucketed:
-                dp_learn_step_bucketed(eng, soft_update=True)
+                dp_learn_step_bucketed(eng, soft_update=True, prefetch=prefetch)
             else:
                 dp_learn_step(eng, soft_update=True, prefetch=prefetch)
         elif chain > 1:
@@ -392,7 +399,9 @@ def run_learner(args, eng, world, backend, steps, warmup, dist, device, dp=None)
         chain = gs
     el = timed_steps(step, steps, dist, device, chain)
     if prefetch and (dp or chain == 1):   # consume the minibatch drawn ahead (none pending after)
-        if dp:
+        if dp and bucketed:
+            dp_learn_step_bucketed(eng, soft_update=True)
+        elif dp:
             dp_learn_step(eng, soft_update=True)
         else:
             eng.learn_step(soft_update=True)
@@ -600,6 +609,35 @@ def head_net_extra(args, device):
     return out
 
 
+def configs0_extra(args, device):
+    """configs[0]: the reference's CPU plumbing case -- MLP Q-net, batch 32 (HYPER_PARAMS['bs'],
+    R:env/dqn_config.py:37) -- timed both ways on this box: the oracle learner (torch CPU restatement of
+    the reference learn step) on the host cores at MLP-284 and MLP-14, and the same learn step on the
+    GPU engine (uniform replay, DuelingDouble, the learning loop of the headline), where B = 32 is pure
+    launch latency."""
+    import copy
+    out = {"batch": 32, "replay_capacity": 100_000}
+    for D in (284, 14):
+        a = copy.copy(args)
+        a.obs_dim, a.batch, a.capacity = D, 32, 100_000
+        spec = make_spec(a)
+        eng = make_engine(a, spec, 32, 1, 0, device)
+        steps = max(args.steps, 200)
+        el, _ = run_learner(a, eng, 1, None, steps, max(args.warmup, 20), None, device)
+        row = {"gpu": {"value": 32 * steps / el, "unit": "transitions/s", "ms_per_step": el / steps * 1e3}}
+        del eng
+        torch.cuda.empty_cache()
+        if not args.no_cpu_baseline:
+            try:
+                a.cpu_seconds = min(args.cpu_seconds, 3.0)
+                cb = cpu_baseline(a, 32)
+                row["cpu_baseline"] = {k: cb[k] for k in ("value", "unit", "cores", "kind", "sample")}
+            except Exception as ex:   # the baseline must never hide the GPU number
+                log(f"configs0 cpu baseline failed: {ex!r}")
+        out[f"mlp{D}"] = row
+    return out
+
+
 def configs2_extra(args, device):
     """configs[2] as BASELINE.json states it: the stacked 4x84x84 occupancy-grid CNN encoder + dueling
     head (TwoStreamHybridNetwork on a (4,84,84) micro grid, R:env/dqn_config.py:97-143: the class is
@@ -683,10 +721,11 @@ def dropin_loop(args, device, batch=1024, iters=200, warmup=20):
     on the macro-lane MLP, one env row per iteration (n_env = 1):
     choose_actions -> store_transitions -> learn -> update_target_network, timed per call on the
     host clock, the stream synchronised only before the clock stops (as in train.py, where the next
-    choose_actions waits for the GPU).  `deferred` (the default Agent): learn() is recorded and
-    launched by update_target_network with the soft update fused, RNG hand-back through pinned
-    buffers; `synchronous`: DQNX_AGENT_DEFER=0 (learn() launches and reads the RNG back itself).
-    The replay is pre-filled through the engine (synthetic rows, like the headline line)."""
+    choose_actions waits for the GPU).  The default Agent: learn() stages the RNG (host mirror of the
+    draw) and launches the step at once, update_target_network() enqueues the soft update;
+    `deferred_fused`: DQNX_AGENT_DEFER=1 (learn() recorded, launched by update_target_network with the
+    soft update fused into the Adam pass).  The replay is pre-filled through the engine (synthetic
+    rows, like the headline line)."""
     import tempfile
 
     import torch.optim as optim
@@ -746,17 +785,17 @@ def dropin_loop(args, device, batch=1024, iters=200, warmup=20):
 
     saved = os.environ.get("DQNX_AGENT_DEFER")
     try:
-        sync = run(False)
+        now = run(False)
         dfr = run(True)
     finally:
         if saved is None:
             os.environ.pop("DQNX_AGENT_DEFER", None)
         else:
             os.environ["DQNX_AGENT_DEFER"] = saved
-    return dict(dfr, batch=batch, n_env=1, iterations=iters, synchronous=sync,
+    return dict(now, batch=batch, n_env=1, iterations=iters, deferred_fused=dfr,
                 note="Agents.DuelingDoubleDQNAgent through the R:train.py:88-108 call sequence on the MLP-284 "
-                     "macro-lane net; host clock per call; the top-level numbers are the default (deferred) "
-                     "agent, `synchronous` the DQNX_AGENT_DEFER=0 one")
+                     "macro-lane net; host clock per call; the top-level numbers are the default agent (learn() "
+                     "launches the step), `deferred_fused` the DQNX_AGENT_DEFER=1 one")
 
 
 def main():
@@ -825,7 +864,7 @@ def main():
         torch.cuda.empty_cache()
         if not dpmode:
             extras = single_gpu_extras(args, spec, device)
-            for name, fn in (("head_net", head_net_extra), ("configs2", configs2_extra),
+            for name, fn in (("configs0", configs0_extra), ("head_net", head_net_extra), ("configs2", configs2_extra),
                              ("configs4_projection_w8", c5_projection), ("dropin_loop", dropin_loop)):
                 try:
                     extras[name] = fn(args, device)
@@ -868,7 +907,8 @@ def main():
                 "steps_per_call": args.chain if not dpmode else 1,
                 "sampling": "rank-local" if local else "global (reference-exact random.sample on every rank)",
                 "dp_step": (((f"one HIP graph per {args.dp_graph_steps} steps" if dp_graph else "eager launches")
-                             + (", per-layer gradient buckets" if args.net != "mlp" and not args.no_buckets else ""))
+                             + (", per-layer gradient buckets" if ((args.net != "mlp" and not args.no_buckets)
+                                                                  or (args.net == "mlp" and args.mlp_buckets)) else ""))
                             if dpmode else None),
                 "compute": args.compute,
             },

@@ -205,8 +205,9 @@ int dqnx_engine_set_graphs(dqnx_engine* e, int32_t enabled);
 /* ---- replay ring: replaces ReplayMemoryNaive/Prioritized.store_transitions
  *      (R:dqn/replay_memory.py:30-36, :56-67) via Agent.store_transitions (R:dqn/agent.py:80-84).
  * Appends n transitions (evicting the oldest when full).  Pointers are host memory
- * (src_on_device = 0; copied with hipMemcpyAsync, caller keeps them alive until the
- * stream reaches the copy) or device memory (src_on_device = 1).  obs rows are
+ * (src_on_device = 0; up to 64 rows are copied into an engine-owned pinned block at once and sent
+ * with one async copy -- the caller's arrays are free on return; larger pushes are copied with
+ * hipMemcpyAsync and the call synchronises the stream) or device memory (src_on_device = 1).  obs rows are
  * obs_dim floats, contiguous.  done: 0/1 bytes.  Under PER new leaves get the current
  * max priority (1.0 when the tree is empty), exactly as the reference. */
 int dqnx_replay_push(dqnx_engine* e, const float* obs, const int32_t* act, const float* rew,
@@ -339,6 +340,31 @@ int dqnx_hard_update(dqnx_engine* e, void* stream);
 uint64_t dqnx_act_scratch_bytes(const dqnx_net_desc* net, int32_t n);
 int dqnx_act(const dqnx_net_desc* net, const float* params, const float* obs, int32_t n, int32_t* actions,
              float* values, void* scratch, uint64_t scratch_bytes, void* stream);
+
+/* ---- drop-in Agent fast path: one host call per agent method (R:train.py:88-108) ---------------
+ * dqnx_agent_stage_rng: Agent.learn()'s draw source -- snapshot `state625` (the caller's
+ *   random.getstate()[1], or numpy's legacy keys + pos under PER) into the engine's pinned staging
+ *   block for the next dqnx_agent_launch, and return in *words the MT19937 outputs the device draw will
+ *   consume (the host advances its generator by them, dqnx_rng_sample_words / dqnx_rng_advance).  The
+ *   post-draw state is remembered and checked against the device's at dqnx_agent_readback.  Uniform
+ *   replay with fewer stored transitions than the batch: DQNX_EINVAL with random.sample's ValueError
+ *   text (R:dqn/replay_memory.py:39).  Host only.
+ * dqnx_agent_launch: the staged state's upload, dqnx_learn_step(flags) (DQNX_STEP_SOFT_UPDATE allowed),
+ *   then the control block into an engine-owned pinned copy with an event; stream-ordered, no wait.
+ * dqnx_agent_readback: 1 when the last launch's control block has arrived (wait = 1 blocks until it
+ *   has), copied to `out` (may be NULL); 0 when none is pending or (wait = 0) it has not arrived yet;
+ *   DQNX_EDEVICE when it carries a sticky device error (dqnx_ctrl.error) or its RNG state differs from
+ *   the host mirror (dqnx_last_error() says which).
+ * dqnx_act_host: dqnx_act with HOST obs [n][obs_dim] and HOST actions [n]: the obs through pinned
+ *   memory into the END of `scratch` (dqnx_act_host_scratch_bytes(net, n) bytes, zero-filled before
+ *   its first use), one launch sequence, the actions back; synchronises `stream` (Network.actions,
+ *   R:dqn/network.py:67-74, 110-117). */
+int dqnx_agent_stage_rng(dqnx_engine* e, int32_t which, const uint32_t* state625, int64_t* words);
+int dqnx_agent_launch(dqnx_engine* e, int32_t flags, void* stream);
+int dqnx_agent_readback(dqnx_engine* e, int32_t wait, dqnx_ctrl* out);
+uint64_t dqnx_act_host_scratch_bytes(const dqnx_net_desc* net, int32_t n);
+int dqnx_act_host(const dqnx_net_desc* net, const float* params, const float* obs_host, int32_t n,
+                  int32_t* actions_host, void* scratch, uint64_t scratch_bytes, void* stream);
 
 /* ---- kernel-level timing (bench.py roofline) ---------------------------------------
  * A learn step is an ordered list of kernel launches (sample, linear_fwd_l1.., head_td_loss,

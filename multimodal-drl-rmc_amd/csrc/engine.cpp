@@ -432,6 +432,26 @@ struct dqnx_engine {
     std::map<int, hipGraphExec_t> graph_cache;
     hipStream_t capture_stream = nullptr;
     std::map<int, std::vector<KStep>> steps_cache;
+    std::map<int, DwAdam16Args> dw16_cache;   // the fused plan's k_dw_adam16 launch of each cached plan
+    int building_key = 0;                     // (the plan key steps_for is building)
+    // drop-in Agent fast path (dqnx_agent_*, small host pushes): engine-owned pinned blocks + events
+    uint32_t* ag_rng_pin = nullptr;           // [2][625] staged RNG states (alternating)
+    hipEvent_t ag_rng_ev[2] = {nullptr, nullptr};
+    bool ag_rng_live[2] = {false, false};
+    int ag_slot = 0, ag_which = -1;
+    uint32_t ag_expect[625];                  // host mirror of the staged draw's post-draw state
+    bool ag_expect_live = false;
+    dqnx_ctrl* ag_ctrl_pin = nullptr;         // control block read back after each agent launch
+    hipEvent_t ag_ctrl_ev = nullptr;
+    bool ag_ctrl_live = false;
+    bool ag_check_live = false;               // the pending readback is to be checked against ag_check
+    int ag_check_which = 0;
+    uint32_t ag_check[625];
+    char* push_pin = nullptr;                 // small host pushes: one pinned block, one H2D
+    hipEvent_t push_ev = nullptr;
+    bool push_live = false;
+    int bucket_key = -1;                      // the GRADS_ONLY plan of the bucketed step in flight
+    bool bucket_prefetch = false;
     std::map<std::tuple<int, int, void*, void*>, hipGraphExec_t> timed_cache;
     hipStream_t side_stream = nullptr;
     hipEvent_t fork_ev = nullptr, join_ev = nullptr;
@@ -1261,6 +1281,7 @@ void build_fused_steps(dqnx_engine* e, int flags, int32_t* idx, int32_t* phys, s
             k.bytes = 4.0 * (ops + (da.mode ? 7.0 * P + (da.soft ? 2.0 * P : 0.0) + blk : P));
             k.run = [=](hipStream_t s) { return launch_dw_adam16(da, s); };
             ks.push_back(k);
+            e->dw16_cache[e->building_key] = da;   // (the bucketed DP step launches subsets of it)
             return;
         }
         if (e->fplan.bf16) {   // bf16 operands, fp32 slabs: the same Adam pass follows
@@ -2250,6 +2271,90 @@ int enqueue_range(const std::vector<KStep>& ks, int a, int b, hipStream_t s) {
     return DQNX_OK;
 }
 
+// dqnx_apply_grads on the fused plan: k_dw_adam16 in apply mode (mode 3: Adam from `grads`, no K
+// loop) over every parameter tile, dense layers last-first then the head, writing the blocked copies
+static DwAdam16Args apply_dw16_args(dqnx_engine* e, const AdamArgs& aa) {
+    const dqnx_config& c = e->cfg;
+    DwAdam16Args da;
+    memset(&da, 0, sizeof(da));
+    const NetPlan& np = e->np;
+    const int L = (int)np.dense.size();
+    da.rows16 = 2;
+    int tiles = 0;
+    for (int q = 0; q <= L; q++) {   // dense layers last-first, then the head (any tiling: elementwise)
+        const int l = q < L ? L - 1 - q : -1;
+        DwAdam16Layer& d = da.L[da.nl++];
+        d.in = l >= 0 ? np.dense[l].in : np.F;
+        d.out = l >= 0 ? np.dense[l].out : np.NH;
+        d.poff = l >= 0 ? np.dense[l].off : np.head_off;
+        d.head_kind = l >= 0 ? -1 : c.net.head;
+        d.A = c.net.n_actions;
+        d.ti = (d.in + 15) / 16;
+        d.t0 = tiles;
+        tiles += d.ti * ((d.out + 31) / 32);
+        if (l >= 0) {
+            d.fwd_online = at<float>(e, e->ws_wblk[0][l]);
+            d.fwd_target = at<float>(e, e->ws_wblk[1][l]);
+            d.chain = l >= 1 ? at<float>(e, e->ws_wblkT[l]) : nullptr;
+            d.nch_fwd = e->fplan.kpad[l] / 16;
+            d.nch_chain = np.dense[l].out / 16;
+        }
+        d.dZ = aa.grads;   // (no K loop: never read)
+        d.X = aa.grads;
+        d.ldz = d.ldx = 1;
+    }
+    da.tiles = tiles;
+    da.Bl = 0;
+    da.mode = 3;
+    da.soft = aa.soft;
+    da.n_params = np.P;
+    da.p = aa.p;
+    da.m = aa.m;
+    da.v = aa.v;
+    da.grads = aa.grads;
+    da.target = aa.target;
+    da.ctrl = aa.ctrl;
+    da.w1 = aa.w1;
+    da.beta2 = aa.beta2;
+    da.c2 = aa.c2;
+    da.eps = aa.eps;
+    da.tau = aa.tau;
+    da.one_minus_tau = aa.one_minus_tau;
+    da.batch_global = e->Bg;
+    da.stamps = at<int64_t>(e, e->ws_stamps);
+    return da;
+}
+
+// The layers q of a k_dw_adam16 launch with bit q of `mask` set (a.L order), as a launch of their own:
+// the same per-tile arithmetic, tiles renumbered.  `first`: this launch computes the loss (tile 0 of
+// the gradient mode); `last`: it hosts the step's extra workgroups (PER, MT cache, staged minibatch).
+static DwAdam16Args dw16_subset(const DwAdam16Args& a, uint32_t mask, bool first, bool last) {
+    DwAdam16Args b = a;
+    b.nl = 0;
+    int tiles = 0;
+    for (int q = 0; q < a.nl; q++) {
+        const int nt = (q + 1 < a.nl ? a.L[q + 1].t0 : a.tiles) - a.L[q].t0;
+        if (!((mask >> q) & 1u)) continue;
+        DwAdam16Layer d = a.L[q];
+        d.t0 = tiles;
+        tiles += nt;
+        b.L[b.nl++] = d;
+    }
+    b.tiles = tiles;
+    if (!first) {
+        b.loss_partial = nullptr;
+        b.n_loss_partial = 0;
+    }
+    if (!last) {
+        b.mtc = nullptr;
+        b.mtc_blocks = 0;
+        b.pf_nidx = b.pf_nphys = 0;
+        b.pprop_wgs = 0;
+        b.ptrack = 0;
+    }
+    return b;
+}
+
 int enqueue_apply(dqnx_engine* e, int flags, hipStream_t s) {
     const bool keep_blk = (flags & 0x200) != 0;   // (a prefetched minibatch is pending: no sampler launch next)
     const dqnx_config& c = e->cfg;
@@ -2301,53 +2406,7 @@ int enqueue_apply(dqnx_engine* e, int flags, hipStream_t s) {
         // fused plan: k_dw_adam16 in apply mode -- 32 x 16 parameter tiles, the same per-element
         // update as k_adam, and each tile's blocked copies as (near-)contiguous blocks instead of
         // k_adam's per-element scattered stores (the DP shard step's last launch)
-        DwAdam16Args da;
-        memset(&da, 0, sizeof(da));
-        const NetPlan& np = e->np;
-        const int L = (int)np.dense.size();
-        da.rows16 = 2;
-        int tiles = 0;
-        for (int q = 0; q <= L; q++) {   // dense layers last-first, then the head (any tiling: elementwise)
-            const int l = q < L ? L - 1 - q : -1;
-            DwAdam16Layer& d = da.L[da.nl++];
-            d.in = l >= 0 ? np.dense[l].in : np.F;
-            d.out = l >= 0 ? np.dense[l].out : np.NH;
-            d.poff = l >= 0 ? np.dense[l].off : np.head_off;
-            d.head_kind = l >= 0 ? -1 : c.net.head;
-            d.A = c.net.n_actions;
-            d.ti = (d.in + 15) / 16;
-            d.t0 = tiles;
-            tiles += d.ti * ((d.out + 31) / 32);
-            if (l >= 0) {
-                d.fwd_online = at<float>(e, e->ws_wblk[0][l]);
-                d.fwd_target = at<float>(e, e->ws_wblk[1][l]);
-                d.chain = l >= 1 ? at<float>(e, e->ws_wblkT[l]) : nullptr;
-                d.nch_fwd = e->fplan.kpad[l] / 16;
-                d.nch_chain = np.dense[l].out / 16;
-            }
-            d.dZ = aa.grads;   // (no K loop: never read)
-            d.X = aa.grads;
-            d.ldz = d.ldx = 1;
-        }
-        da.tiles = tiles;
-        da.Bl = 0;
-        da.mode = 3;
-        da.soft = aa.soft;
-        da.n_params = np.P;
-        da.p = aa.p;
-        da.m = aa.m;
-        da.v = aa.v;
-        da.grads = aa.grads;
-        da.target = aa.target;
-        da.ctrl = aa.ctrl;
-        da.w1 = aa.w1;
-        da.beta2 = aa.beta2;
-        da.c2 = aa.c2;
-        da.eps = aa.eps;
-        da.tau = aa.tau;
-        da.one_minus_tau = aa.one_minus_tau;
-        da.batch_global = e->Bg;
-        da.stamps = at<int64_t>(e, e->ws_stamps);
+        DwAdam16Args da = apply_dw16_args(e, aa);
         if (prop_in_adam) {
             da.pprop = pua;
             da.pprop_wgs = (e->Bg + 511) / 512;
@@ -2402,11 +2461,15 @@ void drop_graphs(dqnx_engine* e) {
     for (auto& kv : e->timed_cache) (void)hipGraphExecDestroy(kv.second);
     e->timed_cache.clear();
     e->steps_cache.clear();
+    e->dw16_cache.clear();
 }
 
 const std::vector<KStep>& steps_for(dqnx_engine* e, int key) {
     auto it = e->steps_cache.find(key);
-    if (it == e->steps_cache.end()) it = e->steps_cache.emplace(key, build_learn_steps(e, key)).first;
+    if (it == e->steps_cache.end()) {
+        e->building_key = key;
+        it = e->steps_cache.emplace(key, build_learn_steps(e, key)).first;
+    }
     return it->second;
 }
 
@@ -2433,6 +2496,16 @@ int dp_buckets(dqnx_engine* e, std::vector<DpBucket>& out) {
             if (ks[k].name == nm) return k;
         return -1;
     };
+    if (direct && NC == 0 && np.dense.size() >= 2 && route_knob("DQNX_MLP_BUCKETS", 1) != 0) {
+        // fused MLP plan: bucket 0 = every gradient but layer 1's (the step up to the head kernel plus
+        // the dW tiles of layers 2.. and the head: one k_dw_adam16 launch), bucket 1 = layer 1's dW
+        // tiles (a second launch), so bucket 0's all-reduce and Adam run under them.  Layer 1's weight
+        // and bias lead the flat vector.  (k ranges: dqnx_learn_step_bucket splits the last launch.)
+        const int64_t cut = np.dense[1].off;
+        out.push_back({0, nk, cut, np.P - cut});
+        out.push_back({nk, nk, 0, cut});
+        return DQNX_OK;
+    }
     if (NC == 0 || direct) {
         if (direct && NC) return set_error(DQNX_EUNSUPPORTED, "dp buckets: fused dW plan with convs");
         out.push_back({0, nk, 0, np.P});
@@ -2728,6 +2801,19 @@ int dqnx_engine_destroy(dqnx_engine* e) {
     }
     if (e->fork_ev) (void)hipEventDestroy(e->fork_ev);
     if (e->join_ev) (void)hipEventDestroy(e->join_ev);
+    for (int i = 0; i < 2; i++)
+        if (e->ag_rng_ev[i]) (void)hipEventDestroy(e->ag_rng_ev[i]);
+    if (e->ag_ctrl_ev) {
+        (void)hipEventSynchronize(e->ag_ctrl_ev);
+        (void)hipEventDestroy(e->ag_ctrl_ev);
+    }
+    if (e->push_ev) {
+        (void)hipEventSynchronize(e->push_ev);
+        (void)hipEventDestroy(e->push_ev);
+    }
+    if (e->ag_rng_pin) (void)hipHostFree(e->ag_rng_pin);
+    if (e->ag_ctrl_pin) (void)hipHostFree(e->ag_ctrl_pin);
+    if (e->push_pin) (void)hipHostFree(e->push_pin);
     delete e;
     return DQNX_OK;
 }
@@ -2817,6 +2903,8 @@ int dqnx_engine_reset(dqnx_engine* e, void* stream) {
     return DQNX_OK;
 }
 
+constexpr int kPinnedPushRows = 64;   // host pushes up to this many rows take the pinned one-copy path
+
 int dqnx_replay_push(dqnx_engine* e, const float* obs, const int32_t* act, const float* rew, const uint8_t* done,
                      const float* next_obs, int32_t n, int32_t src_on_device, void* stream) {
     int rc = check_bound(e);
@@ -2826,6 +2914,30 @@ int dqnx_replay_push(dqnx_engine* e, const float* obs, const int32_t* act, const
     if (e->pf_valid) return set_error(DQNX_ESTATE, "replay push while a prefetched minibatch is pending");
     hipStream_t s = (hipStream_t)stream;
     const int D = e->cfg.net.obs_dim;
+    if (!src_on_device && n > 0 && n <= kPinnedPushRows && (int64_t)n <= e->cfg.capacity) {
+        // the env loop's n_env rows (Agent.store_transitions): packed into one pinned block, ONE
+        // H2D copy into the device staging area, the push kernel from there; no host wait (the block
+        // is reused once the event after its previous copy has passed)
+        const size_t fb = (size_t)n * D * 4, bytes = 2 * fb + (size_t)n * 9;
+        if (!e->push_pin) {
+            DQNX_HIP_CHECK(hipHostMalloc((void**)&e->push_pin, (size_t)kPinnedPushRows * (8 * (size_t)D + 9) + 64,
+                                         hipHostMallocDefault));
+            DQNX_HIP_CHECK(hipEventCreateWithFlags(&e->push_ev, hipEventDisableTiming));
+        }
+        if (e->push_live) DQNX_HIP_CHECK(hipEventSynchronize(e->push_ev));
+        char* h = e->push_pin;
+        memcpy(h, obs, fb);
+        memcpy(h + fb, next_obs, fb);
+        memcpy(h + 2 * fb, act, (size_t)n * 4);
+        memcpy(h + 2 * fb + 4 * (size_t)n, rew, (size_t)n * 4);
+        memcpy(h + 2 * fb + 8 * (size_t)n, done, (size_t)n);
+        char* d = e->arena + e->ws_stage;
+        DQNX_HIP_CHECK(hipMemcpyAsync(d, h, bytes, hipMemcpyHostToDevice, s));
+        DQNX_HIP_CHECK(hipEventRecord(e->push_ev, s));
+        e->push_live = true;
+        return dqnx_replay_push(e, (const float*)d, (const int32_t*)(d + 2 * fb), (const float*)(d + 2 * fb + 4 * (size_t)n),
+                                (const uint8_t*)(d + 2 * fb + 8 * (size_t)n), (const float*)(d + fb), n, 1, stream);
+    }
     int done_rows = 0;
     while (done_rows < n) {
         const bool per = e->cfg.algo == DQNX_ALGO_PER_DOUBLE;
@@ -3325,19 +3437,86 @@ int dqnx_dp_bucket_info(dqnx_engine* e, int32_t bucket, int64_t* first, int64_t*
     return DQNX_OK;
 }
 
+// the fused MLP plan's two buckets (dp_buckets): the dW tiles of every layer but layer 1 / of layer 1
+// (a.L order of the plan's k_dw_adam16 launch: dense layers last-first, then the head)
+static uint32_t mlp_bucket_mask(const dqnx_engine* e, int bucket) {
+    const uint32_t l1 = 1u << ((int)e->np.dense.size() - 1);
+    return bucket == 0 ? ~l1 : l1;
+}
+
+static int learn_step_bucket_mlp(dqnx_engine* e, int32_t flags, int32_t bucket, hipStream_t s) {
+    const int base = DQNX_STEP_GRADS_ONLY;
+    int rc = DQNX_OK;
+    if (bucket == 1) {   // layer 1's dW tiles (+ the step's extra workgroups: the staged-minibatch copy)
+        auto it = e->dw16_cache.find(e->bucket_key);
+        if (e->bucket_key < 0 || it == e->dw16_cache.end())
+            return set_error(DQNX_ESTATE, "dp bucket 1 before bucket 0 of the same step");
+        rc = launch_dw_adam16(dw16_subset(it->second, mlp_bucket_mask(e, 1), false, true), s);
+        if (rc) return rc;
+        const bool pf_path = (e->bucket_key & KEY_SAMPLE_NEXT) || e->pf_valid;
+        if (pf_path) {   // learn_step_inlaunch's bookkeeping
+            if (!blk_kept(e, base)) e->wblk_dirty = true;
+            if (!e->bucket_prefetch) {
+                e->pf_valid = false;
+                e->pf_inlaunch = false;
+            } else {
+                e->pf_stream = s;
+            }
+        }
+        e->bucket_key = -1;
+        return DQNX_OK;
+    }
+    const bool prefetch = (flags & DQNX_STEP_PREFETCH) != 0;
+    const bool inl = inlaunch_prefetch_ok(e, base);
+    if ((prefetch || e->pf_valid) && !(inl && (!e->pf_valid || e->pf_inlaunch)))
+        return set_error(DQNX_EUNSUPPORTED, "bucketed step: the in-launch prefetch does not apply here");
+    int key, k0;
+    if (prefetch || e->pf_valid) {   // the in-launch pipeline (learn_step_inlaunch)
+        if (e->pf_valid && s != e->pf_stream) DQNX_HIP_CHECK(hipStreamSynchronize(e->pf_stream));
+        if (!e->pf_valid) {
+            rc = inlaunch_prologue(e, base, s);
+            if (rc) return rc;
+        } else if (relayout_due(e)) {
+            rc = enqueue_relayout(e, s);
+            if (rc) return rc;
+            e->wblk_dirty = false;
+        }
+        key = base | (prefetch ? KEY_SAMPLE_NEXT : 0);
+        k0 = prefetch ? 0 : 1;
+    } else {
+        key = base | ((e->wblk_dirty || !blk_kept(e, base)) ? KEY_RELAYOUT : 0);
+        k0 = 0;
+    }
+    const std::vector<KStep>& ks = steps_for(e, key);
+    auto it = e->dw16_cache.find(key);
+    if (ks.empty() || ks.back().name != "dw16_grads" || it == e->dw16_cache.end())
+        return set_error(DQNX_ESTATE, "dp buckets: plan mismatch");
+    rc = enqueue_range(ks, k0, (int)ks.size() - 1, s);
+    if (rc) return rc;
+    rc = launch_dw_adam16(dw16_subset(it->second, mlp_bucket_mask(e, 0), true, false), s);
+    if (rc) return rc;
+    if (!(prefetch || e->pf_valid)) e->wblk_dirty = false;   // (the sampler launch rebuilt the copies)
+    e->bucket_key = key;
+    e->bucket_prefetch = prefetch;
+    return DQNX_OK;
+}
+
 int dqnx_learn_step_bucket(dqnx_engine* e, int32_t flags, int32_t bucket, void* stream) {
     int rc = check_bound(e);
     if (rc) return rc;
     hipStream_t s = (hipStream_t)stream;
-    if (flags & (DQNX_STEP_PREFETCH | DQNX_STEP_GIVEN_INDICES))
-        return set_error(DQNX_EUNSUPPORTED, "bucketed steps sample their own minibatch, without prefetch");
-    if (e->pf_valid) return set_error(DQNX_ESTATE, "a prefetched minibatch is pending");
+    if (flags & DQNX_STEP_GIVEN_INDICES) return set_error(DQNX_EUNSUPPORTED, "bucketed steps sample their own minibatch");
     std::vector<DpBucket> b;
     rc = dp_buckets(e, b);
     if (rc) return rc;
     if (bucket < 0 || bucket >= (int32_t)b.size()) return set_error(DQNX_EINVAL, "bucket %d out of range", bucket);
-    if (bucket == 0 && e->ring_size < e->Bs)
+    if (bucket == 0 && e->ring_size < e->Bs && !e->pf_valid)
         return set_error(DQNX_EINVAL, "Sample larger than population: %lld < %d", (long long)e->ring_size, e->Bs);
+    const bool mlp2 = b.size() == 2 && e->np.conv.empty();
+    if (mlp2) return learn_step_bucket_mlp(e, flags, bucket, s);
+    if (flags & DQNX_STEP_PREFETCH)
+        return set_error(DQNX_EUNSUPPORTED, "bucketed conv-net steps sample their own minibatch, without prefetch");
+    if (e->pf_valid) return set_error(DQNX_ESTATE, "a prefetched minibatch is pending");
     // the plan of a plain GRADS_ONLY step (blocked-weight rebuild as that step decides)
     const int key = DQNX_STEP_GRADS_ONLY | ((e->bwd_plan == 2 && (e->wblk_dirty || !blk_kept(e, DQNX_STEP_GRADS_ONLY))) ? KEY_RELAYOUT : 0);
     const std::vector<KStep>& ks = steps_for(e, key);
@@ -3373,6 +3552,20 @@ int dqnx_apply_grads_bucket(dqnx_engine* e, int32_t flags, int32_t bucket, void*
         if (rc) return rc;
     }
     e->perm_dirty = true;
+    const bool mlp2 = b.size() == 2 && e->np.conv.empty();
+    if (mlp2 && e->bwd_plan == 2 && e->pf_valid && e->pf_inlaunch && dw_adam16_on(e, DQNX_STEP_GRADS_ONLY) &&
+        route_knob("DQNX_APPLY_TILES", 1) != 0) {
+        // as dqnx_apply_grads with a draw pending: k_dw_adam16 apply tiles writing the blocked copies
+        // (the next step has no sampler launch to rebuild them), this bucket's layers only
+        AdamArgs aa;
+        adam_kstep(e, DQNX_STEP_GRADS_ONLY, &aa);
+        aa.mode = 2;
+        aa.soft = (flags & DQNX_STEP_SOFT_UPDATE) ? 1 : 0;
+        rc = launch_dw_adam16(dw16_subset(apply_dw16_args(e, aa), mlp_bucket_mask(e, bucket), true, true), s);
+        if (rc) return rc;
+        if (bucket == (int32_t)b.size() - 1) e->wblk_dirty = false;   // every blocked copy rewritten
+        return DQNX_OK;
+    }
     if (!adam_keeps_blk(e)) e->wblk_dirty = true;
     AdamArgs aa;
     adam_kstep(e, DQNX_STEP_GRADS_ONLY, &aa);
@@ -3517,6 +3710,133 @@ int dqnx_act(const dqnx_net_desc* net, const float* params, const float* obs, in
     a.scratch = (float*)sc;
     a.tickets = (uint32_t*)(sc + scratch_bytes) - 1;   // ticket g = tickets[-g]
     return launch_act(a, s);
+}
+
+// ---- drop-in Agent fast path ------------------------------------------------------------
+int dqnx_rng_sample_words(const uint32_t* state625, int64_t n, int32_t k, uint32_t* out625, int64_t* words);
+int dqnx_rng_advance(const uint32_t* state625, int64_t words, uint32_t* out625);
+
+int dqnx_agent_stage_rng(dqnx_engine* e, int32_t which, const uint32_t* state625, int64_t* words) {
+    int rc = check_bound(e);
+    if (rc) return rc;
+    if (!state625 || !words || (which != DQNX_RNG_PY && which != DQNX_RNG_NP)) return set_error(DQNX_EINVAL, "bad argument");
+    if (state625[624] > 624) return set_error(DQNX_EINVAL, "MT index must be <= 624");
+    if (e->pf_valid) return set_error(DQNX_ESTATE, "agent stage while a prefetched minibatch is pending");
+    if (which == DQNX_RNG_PY) {   // random.sample(deque, batch_size): refused like CPython (k > n)
+        rc = dqnx_rng_sample_words(state625, e->ring_size, e->Bs, e->ag_expect, words);
+    } else {                      // np.random.uniform once per sample: 2 words each
+        *words = 2 * (int64_t)e->Bg;
+        rc = dqnx_rng_advance(state625, *words, e->ag_expect);
+    }
+    if (rc) return rc;
+    if (!e->ag_rng_pin) {
+        DQNX_HIP_CHECK(hipHostMalloc((void**)&e->ag_rng_pin, 2 * 625 * 4, hipHostMallocDefault));
+        for (int i = 0; i < 2; i++) DQNX_HIP_CHECK(hipEventCreateWithFlags(&e->ag_rng_ev[i], hipEventDisableTiming));
+    }
+    const int i = e->ag_slot ^= 1;
+    if (e->ag_rng_live[i]) {   // that block's previous upload has run (two launches ago: long passed)
+        DQNX_HIP_CHECK(hipEventSynchronize(e->ag_rng_ev[i]));
+        e->ag_rng_live[i] = false;
+    }
+    memcpy(e->ag_rng_pin + 625 * i, state625, 625 * 4);
+    e->ag_which = which;
+    e->ag_expect_live = true;
+    return DQNX_OK;
+}
+
+int dqnx_agent_launch(dqnx_engine* e, int32_t flags, void* stream) {
+    int rc = check_bound(e);
+    if (rc) return rc;
+    if (e->ag_which < 0) return set_error(DQNX_ESTATE, "dqnx_agent_launch without a staged RNG state");
+    hipStream_t s = (hipStream_t)stream;
+    const int i = e->ag_slot;
+    uint32_t* dst = e->ag_which == DQNX_RNG_PY ? ctrl_of(e)->py_mt : ctrl_of(e)->np_mt;
+    DQNX_HIP_CHECK(hipMemcpyAsync(dst, e->ag_rng_pin + 625 * i, 625 * 4, hipMemcpyHostToDevice, s));
+    DQNX_HIP_CHECK(hipEventRecord(e->ag_rng_ev[i], s));
+    e->ag_rng_live[i] = true;
+    rc = dqnx_learn_step(e, flags & (DQNX_STEP_SOFT_UPDATE | DQNX_STEP_GRADS_ONLY), stream);
+    if (rc) return rc;
+    if (!e->ag_ctrl_pin) {
+        DQNX_HIP_CHECK(hipHostMalloc((void**)&e->ag_ctrl_pin, sizeof(dqnx_ctrl), hipHostMallocDefault));
+        DQNX_HIP_CHECK(hipEventCreateWithFlags(&e->ag_ctrl_ev, hipEventDisableTiming));
+    }
+    if (e->ag_ctrl_live) DQNX_HIP_CHECK(hipEventSynchronize(e->ag_ctrl_ev));   // (superseded, unread)
+    DQNX_HIP_CHECK(hipMemcpyAsync(e->ag_ctrl_pin, ctrl_of(e), sizeof(dqnx_ctrl), hipMemcpyDeviceToHost, s));
+    DQNX_HIP_CHECK(hipEventRecord(e->ag_ctrl_ev, s));
+    e->ag_ctrl_live = true;
+    e->ag_check_live = e->ag_expect_live;
+    e->ag_check_which = e->ag_which;
+    memcpy(e->ag_check, e->ag_expect, sizeof(e->ag_check));
+    e->ag_expect_live = false;
+    e->ag_which = -1;
+    return DQNX_OK;
+}
+
+int dqnx_agent_readback(dqnx_engine* e, int32_t wait, dqnx_ctrl* out) {
+    if (!e) return set_error(DQNX_EINVAL, "null engine");
+    if (!e->ag_ctrl_live) return 0;
+    if (wait) {
+        DQNX_HIP_CHECK(hipEventSynchronize(e->ag_ctrl_ev));
+    } else {
+        const hipError_t q = hipEventQuery(e->ag_ctrl_ev);
+        if (q == hipErrorNotReady) return 0;
+        if (q != hipSuccess) return set_hip_error(q, "hipEventQuery", __FILE__, __LINE__);
+    }
+    e->ag_ctrl_live = false;
+    const dqnx_ctrl* c = e->ag_ctrl_pin;
+    if (out) memcpy(out, c, sizeof(dqnx_ctrl));
+    if (c->error) return set_error(DQNX_EDEVICE, "device error %d", c->error);
+    if (e->ag_check_live) {
+        e->ag_check_live = false;
+        const uint32_t* got = e->ag_check_which == DQNX_RNG_PY ? c->py_mt : c->np_mt;
+        if (memcmp(got, e->ag_check, sizeof(e->ag_check)))
+            return set_error(DQNX_EDEVICE, "the device sampler's RNG state differs from the host mirror of the draw");
+    }
+    return 1;
+}
+
+uint64_t dqnx_act_host_scratch_bytes(const dqnx_net_desc* net, int32_t n) {
+    const uint64_t a = dqnx_act_scratch_bytes(net, n);
+    if (!a || !net || n < 0) return 0;
+    return a + ((uint64_t)n * net->obs_dim * 4 + 255) / 256 * 256 + ((uint64_t)n * 4 + 255) / 256 * 256;
+}
+
+int dqnx_act_host(const dqnx_net_desc* net, const float* params, const float* obs_host, int32_t n,
+                  int32_t* actions_host, void* scratch, uint64_t scratch_bytes, void* stream) {
+    if (!net || (n > 0 && (!params || !obs_host || !actions_host || !scratch))) return set_error(DQNX_EINVAL, "bad argument");
+    if (n <= 0) return n == 0 ? DQNX_OK : set_error(DQNX_EINVAL, "n < 0");
+    const uint64_t need = dqnx_act_host_scratch_bytes(net, n);
+    if (!need) return set_error(DQNX_EUNSUPPORTED, "dqnx_act_host: network not supported by the acting kernel");
+    if (scratch_bytes < need) return set_error(DQNX_EINVAL, "dqnx_act_host: scratch too small (%llu < %llu)",
+                                                (unsigned long long)scratch_bytes, (unsigned long long)need);
+    const uint64_t ob = ((uint64_t)n * net->obs_dim * 4 + 255) / 256 * 256, ab = ((uint64_t)n * 4 + 255) / 256 * 256;
+    char* sc = (char*)scratch;
+    float* d_obs = (float*)(sc + (scratch_bytes - ob - ab));   // obs and actions at the END: the acting
+    int32_t* d_act = (int32_t*)(sc + (scratch_bytes - ab));    // scratch keeps its tickets just below them
+    // pinned staging, per thread, grown as needed
+    static thread_local char* pin = nullptr;
+    static thread_local size_t pin_bytes = 0;
+    const size_t want = (size_t)n * net->obs_dim * 4 + (size_t)n * 4;
+    hipStream_t s = (hipStream_t)stream;
+    if (pin_bytes < want) {
+        if (pin) {
+            DQNX_HIP_CHECK(hipStreamSynchronize(s));
+            (void)hipHostFree(pin);
+            pin = nullptr;
+            pin_bytes = 0;
+        }
+        DQNX_HIP_CHECK(hipHostMalloc((void**)&pin, want, hipHostMallocDefault));
+        pin_bytes = want;
+    }
+    memcpy(pin, obs_host, (size_t)n * net->obs_dim * 4);
+    DQNX_HIP_CHECK(hipMemcpyAsync(d_obs, pin, (size_t)n * net->obs_dim * 4, hipMemcpyHostToDevice, s));
+    int rc = dqnx_act(net, params, d_obs, n, d_act, nullptr, scratch, scratch_bytes - ob - ab, stream);
+    if (rc) return rc;
+    int32_t* pa = (int32_t*)(pin + (size_t)n * net->obs_dim * 4);
+    DQNX_HIP_CHECK(hipMemcpyAsync(pa, d_act, (size_t)n * 4, hipMemcpyDeviceToHost, s));
+    DQNX_HIP_CHECK(hipStreamSynchronize(s));
+    memcpy(actions_host, pa, (size_t)n * 4);
+    return DQNX_OK;
 }
 
 int dqnx_debug_stamps(dqnx_engine* e, int64_t* out64, void* stream) {

@@ -87,6 +87,8 @@ EXPORTS = [
     "dqnx_per_sample", "dqnx_per_update_priorities", "dqnx_set_agent_step", "dqnx_act", "dqnx_act_scratch_bytes",
     "dqnx_params_modified", "dqnx_dp_bucket_count", "dqnx_dp_bucket_info", "dqnx_learn_step_bucket",
     "dqnx_apply_grads_bucket", "dqnx_ctrl_get_async", "dqnx_rng_sample_words", "dqnx_rng_advance",
+    "dqnx_agent_stage_rng", "dqnx_agent_launch", "dqnx_agent_readback", "dqnx_act_host_scratch_bytes",
+    "dqnx_act_host",
 ]
 
 _lib = None
@@ -157,6 +159,11 @@ def lib():
         "dqnx_ctrl_get_async": ([vp, vp, vp], ctypes.c_int),
         "dqnx_rng_sample_words": ([vp, I64, I32, vp, P(I64)], ctypes.c_int),
         "dqnx_rng_advance": ([vp, I64, vp], ctypes.c_int),
+        "dqnx_agent_stage_rng": ([vp, I32, vp, P(I64)], ctypes.c_int),
+        "dqnx_agent_launch": ([vp, I32, vp], ctypes.c_int),
+        "dqnx_agent_readback": ([vp, I32, vp], ctypes.c_int),
+        "dqnx_act_host_scratch_bytes": ([P(NetDesc), I32], ctypes.c_uint64),
+        "dqnx_act_host": ([P(NetDesc), vp, vp, I32, vp, vp, ctypes.c_uint64, vp], ctypes.c_int),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)

@@ -31,14 +31,18 @@ Host-visible semantics are the reference's, synchronously from the caller's view
   SumTree) comes back with the control block after each step and is raised at the agent's next
   synchronisation point (`choose_actions`, `log`, `save_model`, `flush`).
 
-The train.py loop without host round trips (R:train.py:88-108: choose_actions ->
-store_transitions -> learn -> update_target_network -> log -> save_model): `learn()` records the
-step and returns; the next agent call launches it -- `update_target_network()` as ONE launch
-sequence with the soft update fused into the Adam pass (what it would do next anyway), any other
-call as a plain learn step.  DQNX_AGENT_DEFER=0 launches and waits for the step inside learn().
+The train.py loop (R:train.py:88-108: choose_actions -> store_transitions -> learn ->
+update_target_network -> log -> save_model) costs one library call per agent method: learn() stages
+the RNG state and launches the step at once (dqnx_agent_stage_rng / dqnx_agent_launch: upload, learn
+step, control block back, no host wait), so the GPU runs it under update_target_network's and the
+next choose_actions' host work; update_target_network() enqueues the soft update; choose_actions runs
+the acting launch with host obs / actions (dqnx_act_host) and checks the control block the step sent
+back.  DQNX_AGENT_DEFER=1 instead records learn() and has update_target_network() launch it with the
+soft update fused into the Adam pass.
 """
 from __future__ import annotations
 
+import array
 import os
 import random
 import time
@@ -49,7 +53,7 @@ import numpy as np
 import torch as T
 
 from . import _capi as C
-from .engine import LearnEngine, raise_device_error, spec_from_body
+from .engine import LearnEngine, spec_from_body
 from .network import DeepQNetwork, DuelingDeepQNetwork
 from .replay_memory import ReplayMemoryNaive, ReplayMemoryPrioritized
 
@@ -172,10 +176,8 @@ class Agent:
         self.replay_memory_buffer = self._make_replay()
         self._learn_steps = 0          # learn() calls since the last log (throughput metric)
         self._learn_t0 = time.time()
-        self._defer = os.environ.get("DQNX_AGENT_DEFER", "1") != "0"
-        self._learn_pending = False    # learn() recorded, not launched yet
-        self._rng_expect = None        # host mirror of the recorded step's post-draw RNG state
-        self._rng_check = None         # ... of the last launched step (checked against its readback)
+        self._defer = os.environ.get("DQNX_AGENT_DEFER", "0") != "0"
+        self._learn_pending = False    # learn() recorded, not launched yet (DQNX_AGENT_DEFER=1)
         self.engine.launch_hook = self._launch_pending
         self.engine.settle_hook = self.flush
         self.update_target_network(force=True)
@@ -218,33 +220,24 @@ class Agent:
         return actions
 
     # -- learning ----------------------------------------------------------------------
-    # RNG stream the sampler consumes: CPython's global `random` (uniform replay)
-    _rng_which = C.DQNX_RNG_PY
-
     def _check_population(self):
         """random.sample(deque, batch_size) raises when the deque is shorter (R:dqn/replay_memory.py:39)."""
         if self.engine.ring_size < self.batch_size:
             raise ValueError("Sample larger than population or is negative")
 
     def _rng_handoff(self):
-        """Stage the global state for the device's draw and move the global generator past it now."""
-        e = self.engine
-        staged = e.stage_rng(random.getstate()[1])
-        words, after = e.sample_words(staged, e.ring_size, self.batch_size)
+        """Stage the global state for the device's draw and move the global generator past it now
+        (dqnx_agent_stage_rng: the words random.sample consumes, walked on the host)."""
+        words = self.engine.agent_stage_rng(C.DQNX_RNG_PY, array.array("I", random.getstate()[1]))
         random.getrandbits(32 * words)   # exactly `words` MT19937 outputs, gauss_next untouched
-        return after
 
     def _pre_learn(self):
         """Per-algorithm host bookkeeping before the step is launched (PER: the beta step)."""
 
     def _launch_learn(self, soft_update):
-        e = self.engine
         self._pre_learn()
-        e.upload_staged_rng(self._rng_which)   # async H2D from the pinned staging block
-        e.learn_step(soft_update=soft_update)
-        e.ctrl_readback()                      # async D2H of the control block + event
+        self.engine.agent_launch(soft_update=soft_update)   # RNG upload, learn step, control block back
         self._learn_pending = False
-        self._rng_check = self._rng_expect
 
     def _launch_pending(self, soft_update=False):
         if self._learn_pending:
@@ -252,21 +245,9 @@ class Agent:
 
     def _settle(self, wait):
         """Look at the control block the last launched step sent back (if it has arrived, or waiting
-        for it): raise its sticky device error, and check the device sampler's advanced state against
-        the host mirror learn() installed."""
-        c = self.engine.ctrl_readback_result(wait)
-        if c is None:
-            return
-        ctrl = C.Ctrl.from_buffer_copy(c.tobytes())
-        if ctrl.error:
-            raise_device_error(ctrl.error)
-        want = self._rng_check
-        if want is not None:
-            got = np.frombuffer(c, dtype=np.uint32, count=625,
-                                offset=0 if self._rng_which == C.DQNX_RNG_PY else 2500)
-            if not np.array_equal(got, want):
-                raise RuntimeError("libdqnx: the device sampler's RNG state differs from the host mirror of "
-                                   "the reference's draw (internal error)")
+        for it): raises its sticky device error, and a difference between the device sampler's
+        advanced state and the host mirror learn() installed."""
+        self.engine.agent_readback(wait)
 
     def flush(self):
         """Launch a recorded learn step, wait for it and raise any device error it reported.  Not
@@ -276,15 +257,18 @@ class Agent:
         self._settle(wait=True)
 
     def learn(self):
-        """One learn step on the engine (R:dqn/agent.py:166-185 / 204-226 / 245-272)."""
+        """One learn step on the engine (R:dqn/agent.py:166-185 / 204-226 / 245-272): launched at once
+        (DQNX_AGENT_DEFER=1: recorded and launched by the next agent call, update_target_network()
+        fusing its soft update into the step's Adam pass)."""
         self._launch_pending()
         self._settle(wait=False)
         self._check_population()
-        self._rng_expect = self._rng_handoff()
-        self._learn_pending = True
+        self._rng_handoff()
         self._count_learn()
-        if not self._defer:
-            self.flush()
+        if self._defer:
+            self._learn_pending = True
+        else:
+            self._launch_learn(soft_update=False)
 
     def _count_learn(self):
         self._learn_steps += 1
@@ -371,8 +355,6 @@ class PerDoubleAgent(Agent):
 
     _reduction = "none"
 
-    _rng_which = C.DQNX_RNG_NP   # np.random.uniform (R:dqn/replay_memory.py:76-80)
-
     def _make_replay(self):
         return ReplayMemoryPrioritized(self.buffer_size, self.batch_size, self.epsilon_decay, engine=self.engine)
 
@@ -383,11 +365,12 @@ class PerDoubleAgent(Agent):
 
     def _rng_handoff(self):
         """np.random.uniform once per sample (R:dqn/replay_memory.py:79-80): 2 words each."""
-        e = self.engine
         st = np.random.get_state()
-        staged = e.stage_rng(np.append(np.asarray(st[1], dtype=np.uint32), np.uint32(st[2])))
+        buf = np.empty(625, dtype=np.uint32)
+        buf[:624] = st[1]
+        buf[624] = st[2]
+        self.engine.agent_stage_rng(C.DQNX_RNG_NP, buf)
         np.random.random_sample(self.batch_size)   # the same 2 * batch_size legacy MT19937 words
-        return e.rng_advance(staged, 2 * self.batch_size)
 
     def learn(self):
         self._launch_pending()                            # a step recorded earlier keeps its own step

@@ -47,14 +47,18 @@ def exchange(engine, group=None):
         _gather_abs_td(engine, group)
 
 
-def dp_learn_step_bucketed(engine, soft_update: bool = True, group=None, comm_stream=None):
-    """The data-parallel step with per-layer gradient buckets (conv nets).  The engine's backward
-    completes the gradient in buckets (engine.dp_buckets(): dense layers + head + loss first, then
-    each conv, last conv first); bucket b's all-reduce and its Adam run on `comm_stream` while the
-    engine computes bucket b+1's backward on the current stream.  No parameter the remaining
-    backward reads is updated early: a conv's data gradient reads the permuted weight copy made at
-    the start of the step, and dF was computed before bucket 0 closed.  Equal, bit for bit, to
-    dp_learn_step: the same kernels, the same sums, the same per-element all-reduce.
+def dp_learn_step_bucketed(engine, soft_update: bool = True, group=None, comm_stream=None, prefetch: bool = False):
+    """The data-parallel step with per-layer gradient buckets.  The engine's backward completes the
+    gradient in buckets (engine.dp_buckets()): conv nets -- dense layers + head + loss first, then
+    each conv, last conv first; the fused MLP plan -- every gradient but layer 1's (one launch of
+    dW tiles), then layer 1's.  Bucket b's all-reduce and its Adam run on `comm_stream` while the
+    engine computes bucket b+1's backward on the current stream.  No parameter the remaining backward
+    reads is updated early: a conv's data gradient reads the permuted weight copy made at the start
+    of the step, dF was computed before bucket 0 closed, and the MLP's layer-1 dW tiles read only dZ_1
+    and the gathered rows.  The kernels' per-element sums are dp_learn_step's; the all-reduce of a
+    bucket sums each element in the order its ring chunking gives it, so at world > 2 an element may
+    round differently than in the one-buffer all-reduce (an ulp; world 2 is bit-identical), while every
+    rank still receives the same sum.  prefetch (MLP, uniform replay): as dp_learn_step's.
 
     On CPU tensors (gloo rehearsals) the buckets run in the same order on one thread."""
     buckets = engine.dp_buckets()
@@ -62,7 +66,10 @@ def dp_learn_step_bucketed(engine, soft_update: bool = True, group=None, comm_st
     main = torch.cuda.current_stream(engine.grads.device) if cuda else None
     comm = (comm_stream or torch.cuda.Stream(engine.grads.device)) if cuda else None
     for b, (first, count) in enumerate(buckets):
-        engine.learn_step_bucket(b)                   # on the main stream
+        if prefetch and b == 0:
+            engine.learn_step_bucket(b, prefetch=True)   # on the main stream
+        else:
+            engine.learn_step_bucket(b)
         if cuda:
             comm.wait_stream(main)
             ctx = torch.cuda.stream(comm)
@@ -123,19 +130,20 @@ class GraphedDPStep:
         engine.set_graphs(False)
         self.graph = torch.cuda.CUDAGraph()
         self.comm = torch.cuda.Stream(engine.grads.device) if bucketed else None
-        if prefetch and not bucketed:
+        if prefetch:
             engine.prefetch_prologue()
         torch.cuda.synchronize()
         with torch.cuda.graph(self.graph):
             for _ in range(self.steps):
                 if bucketed:   # the side stream forks and joins inside the capture
-                    dp_learn_step_bucketed(engine, soft_update=soft_update, group=group, comm_stream=self.comm)
+                    dp_learn_step_bucketed(engine, soft_update=soft_update, group=group, comm_stream=self.comm,
+                                           prefetch=prefetch)
                 else:
                     dp_learn_step(engine, soft_update=soft_update, group=group, prefetch=prefetch)
         torch.cuda.synchronize()
         # the captured steps recorded torch's capture stream as the pending draw's stream; replays
         # run on the caller's current stream, which dqnx_rng_get must synchronise instead
-        self._prefetch = prefetch and not bucketed
+        self._prefetch = prefetch
 
     def __call__(self):
         self.graph.replay()

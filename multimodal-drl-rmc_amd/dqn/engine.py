@@ -347,48 +347,16 @@ class LearnEngine:
             obs = np.ascontiguousarray(obs, dtype=np.float32).reshape(-1, self.spec.obs_dim)
             next_obs = np.ascontiguousarray(next_obs, dtype=np.float32).reshape(-1, self.spec.obs_dim)
             n = obs.shape[0]
-            if n <= self.PINNED_PUSH_ROWS:   # the env loop's n_env rows: one pinned H2D, no host wait
-                self._push_pinned(obs, act, rew, done, next_obs)
-            else:
-                act = np.ascontiguousarray(act, dtype=np.int32).reshape(-1)
-                rew = np.ascontiguousarray(rew, dtype=np.float32).reshape(-1)
-                done = np.ascontiguousarray(np.asarray(done).astype(bool), dtype=np.uint8).reshape(-1)
-                C.check(self.L.dqnx_replay_push(self.h, obs.ctypes.data, act.ctypes.data, rew.ctypes.data,
-                                                done.ctypes.data, next_obs.ctypes.data, n, 0, self.stream()),
-                        "replay_push")
+            act = np.ascontiguousarray(act, dtype=np.int32).reshape(-1)
+            rew = np.ascontiguousarray(rew, dtype=np.float32).reshape(-1)
+            done = np.ascontiguousarray(np.asarray(done).astype(bool), dtype=np.uint8).reshape(-1)
+            # (up to 64 rows -- the env loop's n_env -- the library packs them into its pinned block and
+            # sends one async copy; larger pushes copy array by array and wait for the stream)
+            C.check(self.L.dqnx_replay_push(self.h, obs.ctypes.data, act.ctypes.data, rew.ctypes.data,
+                                            done.ctypes.data, next_obs.ctypes.data, n, 0, self.stream()),
+                    "replay_push")
         self.ring_wptr = (self.ring_wptr + n) % self.capacity
         self.ring_size = min(self.ring_size + n, self.capacity)
-
-    PINNED_PUSH_ROWS = 256
-
-    def _push_pinned(self, obs, act, rew, done, next_obs):
-        """Small host pushes (Agent.store_transitions): obs | next_obs | act | rew | done packed into
-        one pinned block, one async H2D into a device staging block, then dqnx_replay_push from device
-        memory (stream-ordered: no host synchronisation; the pinned block is reused once the event
-        after its previous copy has passed)."""
-        n, D = obs.shape
-        nb = ((8 * n * D + 8 * n + n) + 15) // 16 * 16
-        if getattr(self, "_push_pin", None) is None or self._push_pin.numel() < nb:
-            cap = max(nb, ((8 * 16 * D + 8 * 16 + 16) + 15) // 16 * 16)
-            self._push_pin = torch.empty(cap, dtype=torch.uint8).pin_memory()
-            self._push_dev = torch.empty(cap, dtype=torch.uint8, device=self.device)
-            self._push_ev = torch.cuda.Event()
-            self._push_ev_live = False
-        if self._push_ev_live:
-            self._push_ev.synchronize()
-        h = self._push_pin.numpy()
-        o1, o2, o3, o4 = 4 * n * D, 8 * n * D, 8 * n * D + 4 * n, 8 * n * D + 8 * n
-        h[:o1].view(np.float32)[:] = obs.reshape(-1)
-        h[o1:o2].view(np.float32)[:] = next_obs.reshape(-1)
-        h[o2:o3].view(np.int32)[:] = np.asarray(act).reshape(-1)
-        h[o3:o4].view(np.float32)[:] = np.asarray(rew, dtype=np.float32).reshape(-1)
-        h[o4:o4 + n] = np.asarray(done).reshape(-1).astype(bool)
-        self._push_dev[:nb].copy_(self._push_pin[:nb], non_blocking=True)
-        self._push_ev.record(torch.cuda.current_stream(self.device))
-        self._push_ev_live = True
-        b = self._push_dev.data_ptr()
-        C.check(self.L.dqnx_replay_push(self.h, b, b + o2, b + o3, b + o4, b + o1, n, 1, self.stream()),
-                "replay_push")
 
     # ---- RNG -------------------------------------------------------------------------
     def set_rng(self, which: int, state625: np.ndarray):
@@ -403,66 +371,41 @@ class LearnEngine:
                                     self.stream()), "rng_get")
         return a
 
-    # ---- the drop-in Agent's hand-off (no host round trip per learn()) ------------------
-    # Before a recorded step launches, the caller's global RNG state is staged into one of two pinned
-    # blocks (`stage_rng`) and uploaded with the step (`upload_staged_rng`, dqnx_rng_set_async); after
-    # it, the whole control block comes back into a pinned block with an event (`ctrl_readback`,
-    # dqnx_ctrl_get_async), read at the caller's next synchronisation point (`ctrl_readback_result`).
-    def _handoff_bufs(self):
-        if getattr(self, "_stage_pin", None) is None:
-            self._stage_pin = [torch.empty(625, dtype=torch.int32).pin_memory() for _ in range(2)]
-            self._stage_np = [t.numpy().view(np.uint32) for t in self._stage_pin]
-            self._stage_ev = [torch.cuda.Event(), torch.cuda.Event()]
-            self._stage_live = [False, False]
-            self._stage_i = 0
-            self._ctrl_pin = torch.empty(ctypes.sizeof(C.Ctrl), dtype=torch.uint8).pin_memory()
-            self._ctrl_np = self._ctrl_pin.numpy()
-            self._ctrl_ev = torch.cuda.Event()
-            self._ctrl_live = False
-
-    def stage_rng(self, state625) -> np.ndarray:
-        """Pack 625 words (a numpy array, or random.getstate()[1]'s tuple of ints, packed with struct:
-        no 625-object conversion) into the next pinned staging block and return it (uint32 view).  The
-        block's previous upload has run by then (its event is waited for, normally long passed)."""
-        self._handoff_bufs()
-        i = self._stage_i = self._stage_i ^ 1
-        if self._stage_live[i]:
-            self._stage_ev[i].synchronize()
-            self._stage_live[i] = False
-        dst = self._stage_np[i]
-        if isinstance(state625, tuple):
-            struct.pack_into("625I", dst, 0, *state625)
+    # ---- the drop-in Agent's fast path (dqnx_agent_*: one library call per agent method) ----------
+    def agent_stage_rng(self, which: int, state625) -> int:
+        """Snapshot the caller's global RNG state for the next agent_launch; returns the MT19937 words
+        the device draw will consume (the caller advances its generator by them).  state625: any buffer
+        of 625 uint32 (an array.array('I') or a numpy array)."""
+        if isinstance(state625, np.ndarray):
+            ptr = state625.ctypes.data
         else:
-            dst[:] = state625
-        return dst
+            ptr = state625.buffer_info()[0]
+        w = C.I64()
+        C.check(self.L.dqnx_agent_stage_rng(self.h, which, ctypes.c_void_p(ptr), ctypes.byref(w)), "agent_stage_rng")
+        return int(w.value)
 
-    def upload_staged_rng(self, which: int) -> None:
-        """The block of the last stage_rng() into dqnx_ctrl's `which` state, stream-ordered."""
-        i = self._stage_i
-        C.check(self.L.dqnx_rng_set_async(self.h, which, ctypes.c_void_p(self._stage_pin[i].data_ptr()),
-                                          self.stream()), "rng_set_async")
-        self._stage_ev[i].record(torch.cuda.current_stream(self.device))
-        self._stage_live[i] = True
+    def agent_launch(self, soft_update: bool = False) -> None:
+        C.check(self.L.dqnx_agent_launch(self.h, C.STEP_SOFT_UPDATE if soft_update else 0, self.stream()),
+                "agent_launch")
+        if self.cfg.algo == C.DQNX_ALGO_PER_DOUBLE:   # every PER learn step samples: step += n_env
+            self.agent_step += self.cfg.n_env
 
-    def ctrl_readback(self) -> None:
-        """dqnx_ctrl_get_async into the pinned control block + an event after it."""
-        self._handoff_bufs()   # (a readback nobody looked at is superseded: same stream, same block)
-        C.check(self.L.dqnx_ctrl_get_async(self.h, ctypes.c_void_p(self._ctrl_pin.data_ptr()), self.stream()),
-                "ctrl_get_async")
-        self._ctrl_ev.record(torch.cuda.current_stream(self.device))
-        self._ctrl_live = True
-
-    def ctrl_readback_result(self, wait: bool):
-        """The control block of the last ctrl_readback() (a numpy uint8 view of the pinned copy), or None
-        when there is none pending or (wait=False) it has not arrived yet."""
-        if not getattr(self, "_ctrl_live", False):
+    def agent_readback(self, wait: bool):
+        """The control block of the last agent_launch once it has arrived (None: none pending / not
+        yet); raises its sticky device error, or a mismatch between the device sampler's RNG state and
+        the host mirror of the draw."""
+        out = getattr(self, "_ag_ctrl", None)
+        if out is None:
+            out = self._ag_ctrl = C.Ctrl()
+        rc = self.L.dqnx_agent_readback(self.h, 1 if wait else 0, ctypes.byref(out))
+        if rc == 0:
             return None
-        if wait:
-            self._ctrl_ev.synchronize()
-        elif not self._ctrl_ev.query():
-            return None
-        self._ctrl_live = False
-        return self._ctrl_np
+        if rc == C.DQNX_EDEVICE:
+            if out.error:
+                raise_device_error(out.error)
+            raise RuntimeError("libdqnx: " + self.L.dqnx_last_error().decode(errors="replace"))
+        C.check(rc if rc < 0 else 0, "agent_readback")
+        return out
 
     # host-side RNG mirror (dqnx_rng_sample_words / dqnx_rng_advance; host only)
     def sample_words(self, state625: np.ndarray, n: int, k: int):
@@ -524,9 +467,11 @@ class LearnEngine:
             out.append((f.value, c.value))
         return out
 
-    def learn_step_bucket(self, bucket: int):
-        """The part of a GRADS_ONLY learn step that completes `bucket`'s gradient."""
-        C.check(self.L.dqnx_learn_step_bucket(self.h, 0, int(bucket), self.stream()), "learn_step_bucket")
+    def learn_step_bucket(self, bucket: int, prefetch: bool = False):
+        """The part of a GRADS_ONLY learn step that completes `bucket`'s gradient.  prefetch (fused MLP
+        plan, bucket 0): the forward launch also draws the next step's minibatch (DQNX_STEP_PREFETCH)."""
+        C.check(self.L.dqnx_learn_step_bucket(self.h, C.STEP_PREFETCH if prefetch else 0, int(bucket), self.stream()),
+                "learn_step_bucket")
         if bucket == 0 and self.cfg.algo == C.DQNX_ALGO_PER_DOUBLE:   # bucket 0 samples: step += n_env
             self.agent_step += self.cfg.n_env
 

@@ -13,9 +13,13 @@ trains, with no copies.  The engine (not `.optimizer`) holds the Adam moments; s
 """
 from __future__ import annotations
 
+import ctypes
+
+import numpy as np
 import torch as T
 import torch.nn as nn
 
+from . import _capi as C
 from .engine import act as _act_native
 from .engine import act_scratch, act_supported
 from .engine import spec_from_body
@@ -35,7 +39,7 @@ class Network(nn.Module):
         self._act_flat = None       # flat fp32 parameter buffer the acting kernel reads
         self._act_ptrs = None       # data_ptr of every parameter when _act_flat was bound
         self._act_engine = False    # _act_flat belongs to a learn engine
-        self._act_bufs = None       # (rows, desc, scratch, device obs/actions, pinned obs/actions)
+        self._act_bufs = None       # (rows, spec, desc, scratch, scratch bytes, host actions)
         self._engine = None         # the learn engine whose buffer holds these parameters
 
     def forward(self, s):
@@ -82,30 +86,27 @@ class Network(nn.Module):
         return head.out_features
 
     def _act_gpu(self, obses):
-        """Greedy actions through dqnx_act: obs staged through pinned memory, one launch, the
-        actions copied back and the stream synchronised once (the caller needs a list)."""
+        """Greedy actions through the acting kernel: host obs -> dqnx_act_host (obs through pinned memory,
+        one launch sequence, actions back, one synchronisation); device obs -> dqnx_act."""
         spec, flat = self._native_act()   # (its parameters() read launches a recorded learn step first)
-        x = T.as_tensor(obses, dtype=T.float32)
+        if isinstance(obses, T.Tensor) and obses.is_cuda:
+            x = obses.reshape(obses.shape[0], -1)
+            out = _act_native(spec, flat, x, scratch=act_scratch(spec, x.shape[0], flat.device))
+            return out.cpu().tolist()
+        x = np.ascontiguousarray(obses, dtype=np.float32)
         n = x.shape[0]
         x = x.reshape(n, -1)
         if self._act_bufs is None or self._act_bufs[0] < n or self._act_bufs[1] is not spec:
-            dev = flat.device
-            self._act_bufs = (n, spec, spec.to_c(), act_scratch(spec, n, dev),
-                              T.empty(n, spec.obs_dim, dtype=T.float32, device=dev),
-                              T.empty(n, dtype=T.int32, device=dev),
-                              T.empty(n, spec.obs_dim, dtype=T.float32).pin_memory(),
-                              T.empty(n, dtype=T.int32).pin_memory())
-        _, _, desc, scratch, d_obs, d_act, h_obs, h_act = self._act_bufs
-        if x.is_cuda:
-            d_in = x
-        else:
-            h_obs[:n].copy_(x)
-            d_obs[:n].copy_(h_obs[:n], non_blocking=True)
-            d_in = d_obs[:n]
-        _act_native(spec, flat, d_in, scratch=scratch, out=d_act, desc=desc)
-        h_act[:n].copy_(d_act[:n], non_blocking=True)
-        T.cuda.current_stream(flat.device).synchronize()
-        return h_act[:n].tolist()
+            L = C.lib()
+            desc = spec.to_c()
+            nb = int(L.dqnx_act_host_scratch_bytes(ctypes.byref(desc), n))
+            scratch = T.zeros((nb + 15) // 16 * 4, dtype=T.float32, device=flat.device)
+            self._act_bufs = (n, spec, desc, scratch, scratch.numel() * 4, np.empty(n, dtype=np.int32))
+        _, _, desc, scratch, nbytes, out = self._act_bufs
+        stream = ctypes.c_void_p(T.cuda.current_stream(flat.device).cuda_stream)
+        C.check(C.lib().dqnx_act_host(ctypes.byref(desc), flat.data_ptr(), x.ctypes.data, n, out.ctypes.data,
+                                      scratch.data_ptr(), nbytes, stream), "act_host")
+        return out[:n].tolist()
 
     def _body_obs_dim(self):
         if isinstance(self.net, nn.Sequential):

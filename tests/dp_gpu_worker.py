@@ -38,12 +38,14 @@ def make_spec(case, head):
 
 def main():
     """argv: rank world algo out_dir [sampling=global|local] [case=small|c3|hyb|hyb84] [compute=fp32|bf16]
-    [mode=plain|bucketed]"""
+    [mode=plain|bucketed|plain_pf|bucketed_pf]"""
     rank, world, algo, out = int(sys.argv[1]), int(sys.argv[2]), sys.argv[3], sys.argv[4]
     local = len(sys.argv) > 5 and sys.argv[5] == "local"
     case = sys.argv[6] if len(sys.argv) > 6 else "small"
     compute = sys.argv[7] if len(sys.argv) > 7 else "fp32"
-    bucketed = len(sys.argv) > 8 and sys.argv[8] == "bucketed"
+    mode = sys.argv[8] if len(sys.argv) > 8 else "plain"
+    bucketed = mode.startswith("bucketed")
+    prefetch = mode.endswith("_pf")   # (MLP) every step but the last draws the next minibatch in its forward
     backend = os.environ.get("DQNX_TEST_BACKEND", "gloo")
     torch.cuda.set_device(0)
     dist.init_process_group(backend, rank=rank, world_size=world)
@@ -56,8 +58,8 @@ def main():
     eng.set_rng(0, O.py_state_to_array(__import__("random").Random(seed + (rank if local else 0)).getstate()))
     eng.set_rng(1, O.np_state_to_array(np.random.RandomState(seed).get_state()))
     losses, pos, trees, absd, maxmin = [], [], [], [], []
-    for _ in range(3):
-        (dp_learn_step_bucketed if bucketed else dp_learn_step)(eng, soft_update=True)
+    for t in range(3):
+        (dp_learn_step_bucketed if bucketed else dp_learn_step)(eng, soft_update=True, prefetch=prefetch and t < 2)
         torch.cuda.synchronize()
         eng.check_device_error()
         losses.append(float(eng.grads[-1].item()))

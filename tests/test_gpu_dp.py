@@ -248,7 +248,40 @@ def test_gpu_dp_bucketed_equals_unbucketed(tmp_path, case, algo):
     np.testing.assert_allclose(zb[0]["losses"], [x.loss for x in recs], rtol=1e-5, atol=1e-6)
 
 
-@pytest.mark.parametrize("net", ["hybrid", "hybrid84"])
+@pytest.mark.parametrize("case,algo,world,mode", [("small", "DuelingDoubleDQNAgent", 2, "bucketed"),
+                                                   ("small", "PerDuelingDoubleDQNAgent", 2, "bucketed"),
+                                                   ("c3", "DuelingDoubleDQNAgent", 2, "bucketed_pf"),
+                                                   ("c3", "DQNAgent", 8, "bucketed_pf")])
+def test_gpu_dp_mlp_buckets_equal_one_allreduce(tmp_path, case, algo, world, mode):
+    """The fused MLP plan's two gradient buckets (every layer but layer 1 in one k_dw_adam16 launch, then
+    layer 1's tiles; bucket 0's all-reduce and Adam on a side stream under them), with and without the
+    in-launch prefetch.  World 2: bit-identical to the one-all-reduce step (losses, sampled positions,
+    weights, target, tree: a sum of two shard gradients does not depend on the order).  World 8: a ring
+    all-reduce sums each element in an order set by where the element falls in the buffer's chunking,
+    which the buckets change, so a few weights move by an ulp (bound 1e-7); every rank still holds
+    bitwise the same replica, and losses and positions are equal."""
+    (tmp_path / "plain").mkdir()
+    (tmp_path / "bucketed").mkdir()
+    # (a prefetching step leaves the NEXT minibatch in the compute slot: the recorded positions are
+    # compared with the prefetching one-all-reduce step's)
+    zp = run_ranks(tmp_path / "plain", world, algo, case=case, timeout=400, mode=mode.replace("bucketed", "plain"))
+    zb = run_ranks(tmp_path / "bucketed", world, algo, case=case, mode=mode, timeout=400)
+    exact = ("losses", "positions", "params", "target", "tree") if world == 2 else ("losses", "positions", "tree")
+    for r in range(world):
+        for k in exact:
+            assert np.array_equal(zp[r][k], zb[r][k]), (r, k)
+        for k in ("params", "target"):
+            np.testing.assert_allclose(zb[r][k], zp[r][k], atol=1e-7, rtol=0, err_msg=k)
+            assert np.array_equal(zb[r][k], zb[0][k]), (r, k)   # the replicas stay identical
+    if mode.endswith("_pf"):   # and the prefetching steps are the sequential ones
+        (tmp_path / "seq").mkdir()
+        zs = run_ranks(tmp_path / "seq", world, algo, case=case, timeout=400, mode="bucketed")
+        for r in range(world):
+            for k in ("losses", "params", "target"):
+                assert np.array_equal(zs[r][k], zb[r][k]), (r, k)
+
+
+@pytest.mark.parametrize("net", ["hybrid", "hybrid84", "mlp"])
 def test_gpu_graphed_bucketed_dp_step(net):
     """GraphedDPStep(bucketed=True): the bucketed step with its side-stream collectives and Adam
     captured into one HIP graph (world 1 over RCCL) equals eager bucketed and unbucketed steps and

@@ -1,4 +1,4 @@
-"""GPU box, world_size 1 over RCCL, a two-stream conv net: the bucketed data-parallel step
+"""GPU box, world_size 1 over RCCL, a two-stream conv net or the MLP: the bucketed data-parallel step
 (dqn.data_parallel.dp_learn_step_bucketed: per-layer gradient buckets all-reduced and applied on
 a side stream while the backward continues) eager and graph-captured, against the unbucketed DP
 step and the single-GPU learn step -- identical weights -- with the time per step of each."""
@@ -18,15 +18,20 @@ import torch.distributed as dist  # noqa: E402
 import bench  # noqa: E402
 from dqn import _capi as C  # noqa: E402
 from dqn.data_parallel import GraphedDPStep, dp_learn_step, dp_learn_step_bucketed  # noqa: E402
-from dqn.engine import LearnEngine, hybrid_spec  # noqa: E402
+from dqn.engine import LearnEngine, hybrid_spec, mlp_spec  # noqa: E402
 
 net = sys.argv[1] if len(sys.argv) > 1 else "hybrid"
 algo = "DuelingDoubleDQNAgent"
-chw, B, cap = ((2, 27, 5), 256, 20_000) if net == "hybrid" else ((4, 84, 84), 64, 2_000)
 torch.cuda.set_device(0)
 dev = torch.device("cuda", 0)
 dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
-spec = hybrid_spec(8, "dueling", micro_chw=chw)
+if net == "mlp":   # the fused plan's two buckets, graphed with the in-launch prefetch
+    B, cap = 1024, 20_000
+    spec = mlp_spec(284, 8, "dueling")
+else:
+    chw, B, cap = ((2, 27, 5), 256, 20_000) if net == "hybrid" else ((4, 84, 84), 64, 2_000)
+    spec = hybrid_spec(8, "dueling", micro_chw=chw)
+PF = net == "mlp"
 
 
 def make():
@@ -64,17 +69,23 @@ buck_ms = timed(lambda: dp_learn_step_bucketed(b))
 c = make()
 for _ in range(3):
     dp_learn_step_bucketed(c)
-g = GraphedDPStep(c, bucketed=True)
+g = GraphedDPStep(c, bucketed=True, prefetch=PF)
 graph_ms = timed(g)
 d = make()
 for _ in range(3):
     dp_learn_step(d)
-gp = GraphedDPStep(d)
+gp = GraphedDPStep(d, prefetch=PF)
 graph_plain_ms = timed(gp)
 s = make()
 for _ in range(3):
     s.learn_step(soft_update=True)
 single_ms = timed(lambda: s.learn_step(soft_update=True))
+# one more step each (the prefetching graphs' last draw is consumed here)
+dp_learn_step(a)
+dp_learn_step_bucketed(b)
+dp_learn_step_bucketed(c)
+dp_learn_step(d)
+s.learn_step(soft_update=True)
 torch.cuda.synchronize()
 eq = lambda x, y: torch.equal(x.params, y.params) and torch.equal(x.target_params, y.target_params)  # noqa: E731
 pairs = {"plain==bucketed": eq(a, b), "plain==graphed_bucketed": eq(a, c), "plain==graphed_plain": eq(a, d),

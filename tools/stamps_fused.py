@@ -17,8 +17,9 @@ from dqn import _capi as C  # noqa: E402
 from dqn.engine import LearnEngine, mlp_spec  # noqa: E402
 
 B = int(sys.argv[1]) if len(sys.argv) > 1 else 1024
+compute = sys.argv[2] if len(sys.argv) > 2 else "fp32"   # bf16: the configs[4] forward (uniform replay here)
 spec = mlp_spec(284, 8, "dueling")
-eng = LearnEngine(spec, "DuelingDoubleDQNAgent", B, 1_000_000, graphs=False)
+eng = LearnEngine(spec, "DuelingDoubleDQNAgent", B, 1_000_000, graphs=False, compute_dtype=compute)
 eng.load_params(bench.init_params(spec))
 bench.fill_ring(eng, 1_000_000, 284, 8, eng.device)
 random.seed(1234)
