@@ -739,8 +739,10 @@ def dropin_loop(args, device, batch=1024, iters=200, warmup=20):
         return (nn.Sequential(nn.Linear(space.shape[0], 256), act, nn.Linear(256, 128), act), 128, optim.Adam,
                 nn.SmoothL1Loss)
 
-    def run(defer):
+    def run(defer, graphs=False, inplace=True):
         os.environ["DQNX_AGENT_DEFER"] = "1" if defer else "0"
+        os.environ["DQNX_AGENT_GRAPHS"] = "1" if graphs else "0"
+        os.environ["DQNX_AGENT_MT_INPLACE"] = "1" if inplace else "0"
         tmp = tempfile.mkdtemp(prefix="dqnx_dropin_")
         agent = Agents.DuelingDoubleDQNAgent(
             n_env=1, lr=1e-4, gamma=0.99, epsilon_start=1.0, epsilon_min=0.05, epsilon_decay=2e6,
@@ -783,19 +785,27 @@ def dropin_loop(args, device, batch=1024, iters=200, warmup=20):
         return {"us_per_iteration": t_all / iters * 1e6, "learn_tr_per_s": batch * iters / t_all,
                 "phases_us": {k: v / iters * 1e6 for k, v in phases.items()}}
 
-    saved = os.environ.get("DQNX_AGENT_DEFER")
+    keys = ("DQNX_AGENT_DEFER", "DQNX_AGENT_GRAPHS", "DQNX_AGENT_MT_INPLACE")
+    saved = {k: os.environ.get(k) for k in keys}
     try:
         now = run(False)
         dfr = run(True)
+        grf = run(False, graphs=True)
+        port = run(False, inplace=False)
     finally:
-        if saved is None:
-            os.environ.pop("DQNX_AGENT_DEFER", None)
-        else:
-            os.environ["DQNX_AGENT_DEFER"] = saved
-    return dict(now, batch=batch, n_env=1, iterations=iters, deferred_fused=dfr,
+        for k, v in saved.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+    return dict(now, batch=batch, n_env=1, iterations=iters, deferred_fused=dfr, graphed_step=grf,
+                portable_rng=port,
                 note="Agents.DuelingDoubleDQNAgent through the R:train.py:88-108 call sequence on the MLP-284 "
                      "macro-lane net; host clock per call; the top-level numbers are the default agent (learn() "
-                     "launches the step), `deferred_fused` the DQNX_AGENT_DEFER=1 one")
+                     "stages random._inst in place and launches the step in one library call), `deferred_fused` "
+                     "DQNX_AGENT_DEFER=1, `graphed_step` the learn step as one HIP graph launch "
+                     "(DQNX_AGENT_GRAPHS=1), `portable_rng` the getstate / getrandbits hand-off "
+                     "(DQNX_AGENT_MT_INPLACE=0)")
 
 
 def main():

@@ -361,6 +361,16 @@ int dqnx_act(const dqnx_net_desc* net, const float* params, const float* obs, in
  *   R:dqn/network.py:67-74, 110-117). */
 int dqnx_agent_stage_rng(dqnx_engine* e, int32_t which, const uint32_t* state625, int64_t* words);
 int dqnx_agent_launch(dqnx_engine* e, int32_t flags, void* stream);
+/* dqnx_agent_learn_mt: Agent.learn() on the caller's LIVE generator, uniform replay: `mt` = its 624
+ *   MT19937 state words and `*pos` its output position (CPython's RandomObject holds them as
+ *   `int index; uint32_t state[624]`: the drop-in passes the addresses inside random._inst after
+ *   checking the layout against random.getstate()).  Staged as dqnx_agent_stage_rng(DQNX_RNG_PY)
+ *   stages mt + pos, then advanced IN PLACE past the words the draw consumes (*words), i.e. the
+ *   generator is left where random.sample(deque, batch_size) leaves it (R:dqn/replay_memory.py:39);
+ *   with DQNX_AGENT_LAUNCH in flags, dqnx_agent_launch(flags without it) follows in the same call.
+ *   One library call per learn() instead of getstate + stage + getrandbits + launch. */
+#define DQNX_AGENT_LAUNCH 0x100
+int dqnx_agent_learn_mt(dqnx_engine* e, uint32_t* mt, int32_t* pos, int32_t flags, void* stream, int64_t* words);
 int dqnx_agent_readback(dqnx_engine* e, int32_t wait, dqnx_ctrl* out);
 uint64_t dqnx_act_host_scratch_bytes(const dqnx_net_desc* net, int32_t n);
 int dqnx_act_host(const dqnx_net_desc* net, const float* params, const float* obs_host, int32_t n,

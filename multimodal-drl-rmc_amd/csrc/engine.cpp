@@ -2694,7 +2694,7 @@ int dqnx_engine_create(const dqnx_config* cfg, dqnx_engine** out) {
         // per row tile.  Measured slower (B=1024: layer 1 alone 12.1 us on 384 workgroups vs
         // 15.7 us for the whole one-launch forward; step 47.7 vs 45.2 us): the weight bytes
         // streamed from L2 stay the same in total, so more workgroups do not help
-        if (e->fplan.mr == 1 && e->np.dense.size() >= 2) {
+        if (e->fplan.mr == 1 && e->fplan.gw == 0 && e->np.dense.size() >= 2) {
             if (route_flag("DQNX_FWD_SPLIT")) {
                 const int w = route_knob("DQNX_FWD_SPLIT", 1);
                 if (w <= 1) e->fsplit = 1;
@@ -3741,6 +3741,21 @@ int dqnx_agent_stage_rng(dqnx_engine* e, int32_t which, const uint32_t* state625
     memcpy(e->ag_rng_pin + 625 * i, state625, 625 * 4);
     e->ag_which = which;
     e->ag_expect_live = true;
+    return DQNX_OK;
+}
+
+int dqnx_agent_learn_mt(dqnx_engine* e, uint32_t* mt, int32_t* pos, int32_t flags, void* stream, int64_t* words) {
+    if (!mt || !pos || !words) return set_error(DQNX_EINVAL, "bad argument");
+    if (*pos < 0 || *pos > 624) return set_error(DQNX_EINVAL, "MT position must be in [0, 624]");
+    uint32_t s625[625];
+    memcpy(s625, mt, 624 * 4);
+    s625[624] = (uint32_t)*pos;
+    int rc = dqnx_agent_stage_rng(e, DQNX_RNG_PY, s625, words);
+    if (rc) return rc;
+    // the caller's generator moves past the draw now (what random.sample would have consumed)
+    memcpy(mt, e->ag_expect, 624 * 4);
+    *pos = (int32_t)e->ag_expect[624];
+    if (flags & DQNX_AGENT_LAUNCH) return dqnx_agent_launch(e, flags & ~DQNX_AGENT_LAUNCH, stream);
     return DQNX_OK;
 }
 

@@ -45,6 +45,15 @@ constexpr int FT = 64 * FW;
 constexpr int FPF = DQNX_FPF;   // 16-deep chunks per group
 constexpr int FNB = DQNX_FNB;   // register sets: FNB-1 groups of W in flight ahead of the MFMAs
 constexpr int FGQ = 6;
+// Gather registers sized to the row width: a gather slot holds one float4 of the 16 * MR-row input
+// tile, so rows of <= 288 multiplied columns (MLP-284 both ways, MLP-14) need ceil(16 MR 72 / FT)
+// slots -- 3 / 5 / 9 at MR 1 / 2 / 4 -- instead of the FGQ * MR the widest rows need (whose
+// clamped dead loads also held 96 VGPRs at MR = 4 and kept the bf16 forward at 2 waves / SIMD).
+constexpr int FWD_NARROW_Q4 = 72;
+template <int MR, int GW>
+__host__ __device__ constexpr int fwd_gather_slots() {
+    return GW == 0 ? (16 * MR * FWD_NARROW_Q4 + FT - 1) / FT : FGQ * MR;
+}
 // The PER tracking workgroup hosted by k_dw_bf16 must not raise the tiles' register budget: 4 items
 // per thread without the carried leaves stays within the 80 VGPRs of 6 waves / SIMD (8 items with
 // them took 96-101 VGPRs, 4 waves / SIMD, and dw_all 23 -> 27.5 us at B=8192)
@@ -292,10 +301,10 @@ __device__ __forceinline__ void wave_mma_rows(const void* As, int sa, int ngroup
 // PH (phase): 0 the whole forward; 1 only layer 1, its columns split over a.csplit
 // workgroups per row tile, writing H_1 of every stream to HBM; 2 layers 2.. + head, reading
 // H_1 back (the split-layer pair: twice or four times the workgroups on the widest GEMM).
-template <int ACT, int NL, bool BF, int MR, int PH>
+template <int ACT, int NL, bool BF, int MR, int PH, int GW>
 __global__ __launch_bounds__(FT) void k_mlp_fwd(FusedFwdArgs a) {
     constexpr int RW = 16 * MR;          // rows per workgroup
-    constexpr int GQ = FGQ * MR;         // float4 gather slots per thread
+    constexpr int GQ = fwd_gather_slots<MR, GW>();   // float4 gather slots per thread
     constexpr int LB = PH == 2 ? 1 : 0, LE = PH == 1 ? 1 : NL;   // layers of this launch
     extern __shared__ __attribute__((aligned(16))) float lds[];
     // LDS tile b: pointer arithmetic on `lds` keeps the LDS address space visible to the
@@ -975,13 +984,18 @@ bool fused_fwd_plan(FusedFwdArgs& a, int obs_dim, bool bf16, int mr) {
     a.bf16 = bf16 ? 1 : 0;
     const int kz = bf16 ? fwd_nch<true>(obs_dim) * 32 : fwd_nch<false>(obs_dim) * 16;
     if (16 * (kz / 4) > FGQ * FT) return false;   // gather slots (per 16 rows)
+    a.gw = kz / 4 <= FWD_NARROW_Q4 ? 0 : 1;
+    if (a.gw && mr != 1) return false;   // wide rows: 16-row tiles only
     const int rw = 16 * mr;
     a.mr = mr;
     int wmax = 0;
     for (int l = 0; l < a.L; l++) wmax = a.out[l] > wmax ? a.out[l] : wmax;
     int t0, t1;   // tile sizes in floats
-    if (bf16) {   // rows cover every chunk of the last group; stride = 32 bytes mod 256
-        a.sx = fwd_groups<true>(obs_dim) * FPF * 32 + 16;
+    if (bf16) {   // stride = an odd multiple of 32 bytes mod 256 (conflict-free b128 fragment reads)
+        // 16-row tiles read the A fragments of a whole group before skipping the chunks past nch, so
+        // their rows cover the last group; MR > 1 stops at nch (bf16 MLP-284 at MR = 4: 86 -> 74 KB
+        // of LDS, two workgroups per CU)
+        a.sx = (mr == 1 ? fwd_groups<true>(obs_dim) * FPF : fwd_nch<true>(obs_dim)) * 32 + 16;
         a.sh = ((wmax + 127) & ~127) + 16;
         t0 = rw * a.sx / 2;
         t1 = rw * a.sh / 2;
@@ -1021,6 +1035,8 @@ int launch_fused_fwd(const FusedFwdArgs& a, int act, hipStream_t s) {
     if (a.phase != 0 && (a.L < 2 || a.mr != (a.phase == 1 ? a.mr : 1) || (a.phase == 1 && a.mr > 2) ||
                          (a.phase == 1 && (a.csplit < 1 || a.out[0] % (16 * a.csplit)))))
         return set_error(DQNX_EUNSUPPORTED, "split forward: L >= 2, 16-row tiles (layer 1: 16 or 32), layer 1 width / parts a multiple of 16");
+    if (a.gw && (a.phase != 0 || a.mr != 1))
+        return set_error(DQNX_EUNSUPPORTED, "fused forward: rows wider than %d columns take the one-launch 16-row plan", 4 * FWD_NARROW_Q4);
     if (a.samp_shape && (a.phase == 2 || a.samp_shape > 3 || a.samp.k > FWD_SAMPLE_MAX_K ||
                          (a.samp_shape == 1 && a.samp.k > 2048)))
         return set_error(DQNX_EUNSUPPORTED, "forward sampler workgroup: whole forward or layer-1 launch, k <= %d", FWD_SAMPLE_MAX_K);
@@ -1032,10 +1048,17 @@ int launch_fused_fwd(const FusedFwdArgs& a, int act, hipStream_t s) {
     if (shm < (size_t)a.lds_min) shm = (size_t)a.lds_min;
     if (a.samp_shape && shm < (size_t)fwd_sample_lds_bytes(a.samp_shape)) shm = fwd_sample_lds_bytes(a.samp_shape);
     if (a.npc && shm < (size_t)(2 * 624 + 2) * 4) shm = (2 * 624 + 2) * 4;
+#define FUSED_FWD_GW(ACTV, NLV, BFV, MRV, PHV, GWV)                                                  \
+    do {                                                                                             \
+        if (shm > 64 * 1024) allow_lds(k_mlp_fwd<ACTV, NLV, BFV, MRV, PHV, GWV>, 160 * 1024);        \
+        hipLaunchKernelGGL((k_mlp_fwd<ACTV, NLV, BFV, MRV, PHV, GWV>), grid, block, shm, s, a);      \
+    } while (0)
 #define FUSED_FWD_MR(ACTV, NLV, BFV, MRV, PHV)                                                       \
     do {                                                                                             \
-        if (shm > 64 * 1024) allow_lds(k_mlp_fwd<ACTV, NLV, BFV, MRV, PHV>, 160 * 1024);             \
-        hipLaunchKernelGGL((k_mlp_fwd<ACTV, NLV, BFV, MRV, PHV>), grid, block, shm, s, a);           \
+        if constexpr (MRV == 1 && PHV == 0) {                                                        \
+            if (a.gw) { FUSED_FWD_GW(ACTV, NLV, BFV, 1, 0, 1); break; }                             \
+        }                                                                                            \
+        FUSED_FWD_GW(ACTV, NLV, BFV, MRV, PHV, 0);                                                   \
     } while (0)
 #define FUSED_FWD_BF(ACTV, NLV, BFV)                                                                 \
     do {                                                                                             \

@@ -462,6 +462,8 @@ struct FusedFwdArgs {
     const float* done;
     int bf16;                    // DQNX_COMPUTE_BF16: bf16 LDS tiles, bf16 blocked weights, bf16 MFMA
     int mr;                      // 16-row tiles per workgroup (1, 2 or 4; `tiles` counts 16*mr-row tiles)
+    int gw;                      // gather width class: 0 rows of <= 288 multiplied columns (FWD_NARROW_Q4
+                                 // float4), 1 wider (whole forward, 16-row tiles only)
     int phase;                   // 0 whole forward; 1 layer 1 split over csplit parts; 2 layers 2.. + head
     int csplit;
     int sx, sh;                  // LDS row strides (elements: floats, or bf16 under bf16) of the input / hidden tiles

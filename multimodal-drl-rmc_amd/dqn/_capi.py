@@ -31,6 +31,7 @@ STEP_SOFT_UPDATE = 0x1
 STEP_GIVEN_INDICES = 0x2
 STEP_GRADS_ONLY = 0x4
 STEP_PREFETCH = 0x8
+AGENT_LAUNCH = 0x100   # dqnx_agent_learn_mt: launch in the same call
 DEVERR_SAMPLE_TOO_LARGE = 1
 DEVERR_EMPTY_TREE = 2
 DEVERR_PER_HANDOFF = 3
@@ -88,7 +89,7 @@ EXPORTS = [
     "dqnx_params_modified", "dqnx_dp_bucket_count", "dqnx_dp_bucket_info", "dqnx_learn_step_bucket",
     "dqnx_apply_grads_bucket", "dqnx_ctrl_get_async", "dqnx_rng_sample_words", "dqnx_rng_advance",
     "dqnx_agent_stage_rng", "dqnx_agent_launch", "dqnx_agent_readback", "dqnx_act_host_scratch_bytes",
-    "dqnx_act_host",
+    "dqnx_act_host", "dqnx_agent_learn_mt",
 ]
 
 _lib = None
@@ -161,6 +162,7 @@ def lib():
         "dqnx_rng_advance": ([vp, I64, vp], ctypes.c_int),
         "dqnx_agent_stage_rng": ([vp, I32, vp, P(I64)], ctypes.c_int),
         "dqnx_agent_launch": ([vp, I32, vp], ctypes.c_int),
+        "dqnx_agent_learn_mt": ([vp, vp, vp, I32, vp, P(I64)], ctypes.c_int),
         "dqnx_agent_readback": ([vp, I32, vp], ctypes.c_int),
         "dqnx_act_host_scratch_bytes": ([P(NetDesc), I32], ctypes.c_uint64),
         "dqnx_act_host": ([P(NetDesc), vp, vp, I32, vp, vp, ctypes.c_uint64, vp], ctypes.c_int),

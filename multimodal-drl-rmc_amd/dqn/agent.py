@@ -72,6 +72,36 @@ def _summary_writer(log_dir):
         return _Null()
 
 
+def _cpython_mt_addresses():
+    """(state address, position address) of the global generator's MT19937 inside CPython's
+    RandomObject (`PyObject_HEAD; int index; uint32_t state[624]`, Modules/_randommodule.c), or None
+    when that layout cannot be confirmed against random.getstate() (then learn() takes getstate() +
+    dqnx_agent_stage_rng + getrandbits instead: the same draw, ~25 us more host time).  The
+    generator object is never moved or freed (random._inst lives as long as the module)."""
+    if os.environ.get("DQNX_AGENT_MT_INPLACE", "1") == "0":
+        return None
+    try:
+        import ctypes
+        import sys
+
+        import _random
+        inst = random._inst
+        if sys.implementation.name != "cpython" or not isinstance(inst, _random.Random):
+            return None
+        head = object.__basicsize__
+        if _random.Random.__basicsize__ < head + 4 + 624 * 4:
+            return None
+        base = id(inst)
+        pos = ctypes.c_int32.from_address(base + head)
+        mt = (ctypes.c_uint32 * 624).from_address(base + head + 4)
+        ref = inst.getstate()[1]
+        if pos.value != ref[624] or tuple(mt) != ref[:624]:
+            return None
+        return base + head + 4, base + head
+    except Exception:   # any doubt: the portable path
+        return None
+
+
 def _obs_dim(input_dim) -> int:
     shape = getattr(input_dim, "shape", None)
     if shape is not None:
@@ -177,7 +207,10 @@ class Agent:
         self._learn_steps = 0          # learn() calls since the last log (throughput metric)
         self._learn_t0 = time.time()
         self._defer = os.environ.get("DQNX_AGENT_DEFER", "0") != "0"
+        self._mt = self._live_mt()     # learn() stages and advances the live generator in one call
         self._learn_pending = False    # learn() recorded, not launched yet (DQNX_AGENT_DEFER=1)
+        if os.environ.get("DQNX_AGENT_GRAPHS", "0") == "1":   # each learn step as one graph launch
+            self.engine.set_graphs(True)
         self.engine.launch_hook = self._launch_pending
         self.engine.settle_hook = self.flush
         self.update_target_network(force=True)
@@ -225,6 +258,9 @@ class Agent:
         if self.engine.ring_size < self.batch_size:
             raise ValueError("Sample larger than population or is negative")
 
+    def _live_mt(self):
+        return _cpython_mt_addresses()
+
     def _rng_handoff(self):
         """Stage the global state for the device's draw and move the global generator past it now
         (dqnx_agent_stage_rng: the words random.sample consumes, walked on the host)."""
@@ -263,8 +299,12 @@ class Agent:
         self._launch_pending()
         self._settle(wait=False)
         self._check_population()
-        self._rng_handoff()
         self._count_learn()
+        if self._mt is not None:   # one call: stage + advance random._inst in place (+ launch)
+            self.engine.agent_learn_mt(self._mt[0], self._mt[1], launch=not self._defer)
+            self._learn_pending = self._defer
+            return
+        self._rng_handoff()
         if self._defer:
             self._learn_pending = True
         else:
@@ -362,6 +402,9 @@ class PerDoubleAgent(Agent):
         # the reference samples a partly filled tree (with repeats); an empty one has no transitions
         if self.engine.ring_size == 0:
             raise ValueError("PER sample from an empty replay memory")
+
+    def _live_mt(self):
+        return None   # numpy's generator feeds the PER draw (and _pre_learn runs at the launch)
 
     def _rng_handoff(self):
         """np.random.uniform once per sample (R:dqn/replay_memory.py:79-80): 2 words each."""

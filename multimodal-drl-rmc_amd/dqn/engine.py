@@ -332,6 +332,34 @@ class LearnEngine:
         C.check(self.L.dqnx_params_modified(self.h), "params_modified")
 
     # ---- replay ----------------------------------------------------------------------
+    STAGE_ROWS = 64   # the library's pinned one-copy push block (dqnx_replay_push, <= 64 host rows)
+
+    def push_host(self, obs, act, rew, done, next_obs, n: int):
+        """The env loop's push (Agent.store_transitions, n_env rows of host data: numpy arrays or lists):
+        the rows are written into preallocated host staging arrays whose addresses are cached, and one
+        dqnx_replay_push call copies them on (one pinned block, one async copy).  numpy's per-array
+        conversions and `.ctypes` lookups cost ~20 us per call on the old path; larger pushes take it."""
+        if n > self.STAGE_ROWS:
+            self.push(np.asarray(obs, dtype=np.float32).reshape(n, -1), np.asarray(act).reshape(n),
+                      np.asarray(rew, dtype=np.float32).reshape(n), np.asarray(done).reshape(n),
+                      np.asarray(next_obs, dtype=np.float32).reshape(n, -1))
+            return
+        st = getattr(self, "_stage", None)
+        if st is None:
+            D, R = self.spec.obs_dim, self.STAGE_ROWS
+            arrs = (np.zeros((R, D), np.float32), np.zeros(R, np.int32), np.zeros(R, np.float32), np.zeros(R, np.uint8),
+                    np.zeros((R, D), np.float32))
+            st = self._stage = (arrs, tuple(a.__array_interface__["data"][0] for a in arrs))
+        (o, a, r, d, no), (po, pa, pr, pd, pn) = st
+        o[:n] = np.asarray(obs).reshape(n, -1)
+        no[:n] = np.asarray(next_obs).reshape(n, -1)
+        a[:n] = act
+        r[:n] = rew
+        d[:n] = done
+        C.check(self.L.dqnx_replay_push(self.h, po, pa, pr, pd, pn, n, 0, self.stream()), "replay_push")
+        self.ring_wptr = (self.ring_wptr + n) % self.capacity
+        self.ring_size = min(self.ring_size + n, self.capacity)
+
     def push(self, obs, act, rew, done, next_obs):
         """Append transitions (numpy arrays or CUDA tensors)."""
         if isinstance(obs, torch.Tensor) and obs.is_cuda:
@@ -389,6 +417,16 @@ class LearnEngine:
                 "agent_launch")
         if self.cfg.algo == C.DQNX_ALGO_PER_DOUBLE:   # every PER learn step samples: step += n_env
             self.agent_step += self.cfg.n_env
+
+    def agent_learn_mt(self, mt_addr: int, pos_addr: int, launch: bool, soft_update: bool = False) -> int:
+        """dqnx_agent_learn_mt (uniform replay): stage the live MT19937 at mt_addr / pos_addr for the
+        device draw, advance it in place past the words the draw consumes, and (launch) launch the step
+        as agent_launch does.  Returns the words consumed."""
+        w = C.I64()
+        flags = (C.AGENT_LAUNCH if launch else 0) | (C.STEP_SOFT_UPDATE if soft_update else 0)
+        C.check(self.L.dqnx_agent_learn_mt(self.h, mt_addr, pos_addr, flags, self.stream(), ctypes.byref(w)),
+                "agent_learn_mt")
+        return int(w.value)
 
     def agent_readback(self, wait: bool):
         """The control block of the last agent_launch once it has arrived (None: none pending / not

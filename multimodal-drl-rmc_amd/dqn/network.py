@@ -37,9 +37,10 @@ class Network(nn.Module):
         self.device = device
         self._act_spec = None       # NetSpec of the acting kernel (None: not yet planned)
         self._act_flat = None       # flat fp32 parameter buffer the acting kernel reads
-        self._act_ptrs = None       # data_ptr of every parameter when _act_flat was bound
+        self._act_params = None     # the Parameter objects bound to _act_flat
+        self._act_ptrs = None       # their data_ptr when _act_flat was bound
         self._act_engine = False    # _act_flat belongs to a learn engine
-        self._act_bufs = None       # (rows, spec, desc, scratch, scratch bytes, host actions)
+        self._act_fast = None       # dqnx_act_host's arguments (scratch, staging, addresses), built once
         self._engine = None         # the learn engine whose buffer holds these parameters
 
     def forward(self, s):
@@ -78,7 +79,15 @@ class Network(nn.Module):
             engine.params_modified()
         if flat is not None:
             self._act_flat, self._act_spec, self._act_engine = flat, spec, True
-            self._act_ptrs = [p.data_ptr() for p in self.parameters()]
+            self._act_remember_params()
+
+    def _act_remember_params(self):
+        """The Parameter objects and their storage addresses the acting kernels were bound to: each act
+        checks the addresses against these objects (a few data_ptr() calls; walking the module tree
+        through parameters() cost ~12 us per call)."""
+        self._act_params = [p for _, p in super().named_parameters()]
+        self._act_ptrs = [p.data_ptr() for p in self._act_params]
+        self._act_fast = None
 
     # -- acting path: one dqnx_act launch for MLP bodies on a GPU -----------------------
     def _act_head_dim(self):
@@ -88,24 +97,31 @@ class Network(nn.Module):
     def _act_gpu(self, obses):
         """Greedy actions through the acting kernel: host obs -> dqnx_act_host (obs through pinned memory,
         one launch sequence, actions back, one synchronisation); device obs -> dqnx_act."""
-        spec, flat = self._native_act()   # (its parameters() read launches a recorded learn step first)
+        self._engine_sync()   # a recorded learn step first (stream order does the rest)
+        spec, flat = self._native_act()
         if isinstance(obses, T.Tensor) and obses.is_cuda:
             x = obses.reshape(obses.shape[0], -1)
             out = _act_native(spec, flat, x, scratch=act_scratch(spec, x.shape[0], flat.device))
             return out.cpu().tolist()
-        x = np.ascontiguousarray(obses, dtype=np.float32)
+        x = obses if isinstance(obses, np.ndarray) else np.asarray(obses, dtype=np.float32)
         n = x.shape[0]
-        x = x.reshape(n, -1)
-        if self._act_bufs is None or self._act_bufs[0] < n or self._act_bufs[1] is not spec:
+        f = self._act_fast
+        if f is None or f[0] < n or f[1] is not spec or f[2] is not flat:
             L = C.lib()
             desc = spec.to_c()
-            nb = int(L.dqnx_act_host_scratch_bytes(ctypes.byref(desc), n))
+            cap = max(n, 64)
+            nb = int(L.dqnx_act_host_scratch_bytes(ctypes.byref(desc), cap))
             scratch = T.zeros((nb + 15) // 16 * 4, dtype=T.float32, device=flat.device)
-            self._act_bufs = (n, spec, desc, scratch, scratch.numel() * 4, np.empty(n, dtype=np.int32))
-        _, _, desc, scratch, nbytes, out = self._act_bufs
-        stream = ctypes.c_void_p(T.cuda.current_stream(flat.device).cuda_stream)
-        C.check(C.lib().dqnx_act_host(ctypes.byref(desc), flat.data_ptr(), x.ctypes.data, n, out.ctypes.data,
-                                      scratch.data_ptr(), nbytes, stream), "act_host")
+            xs = np.zeros((cap, spec.obs_dim), dtype=np.float32)
+            out = np.zeros(cap, dtype=np.int32)
+            # (the acting launch's arguments, addresses resolved once)
+            f = self._act_fast = (cap, spec, flat, desc, ctypes.byref(desc), flat.data_ptr(), scratch,
+                                  scratch.data_ptr(), scratch.numel() * 4, xs, xs.__array_interface__["data"][0],
+                                  out, out.__array_interface__["data"][0])
+        _, _, _, _, dref, fptr, _, sptr, nbytes, xs, xaddr, out, oaddr = f
+        xs[:n] = x.reshape(n, -1)
+        stream = T.cuda.current_stream(flat.device).cuda_stream
+        C.check(C.lib().dqnx_act_host(dref, fptr, xaddr, n, oaddr, sptr, nbytes, stream), "act_host")
         return out[:n].tolist()
 
     def _body_obs_dim(self):
@@ -123,7 +139,7 @@ class Network(nn.Module):
         if self._act_flat is not None:
             if not act_supported(self._act_spec):
                 return None
-            if [p.data_ptr() for p in self.parameters()] == self._act_ptrs:
+            if all(p.data_ptr() == q for p, q in zip(self._act_params, self._act_ptrs)):
                 return self._act_spec, self._act_flat
             if self._act_engine:
                 raise RuntimeError("network parameters were moved out of the learn engine's buffer")
@@ -142,7 +158,7 @@ class Network(nn.Module):
         views = {name: flat[off:off + int(T.Size(shape).numel())].view(*shape) for name, off, shape in layout}
         self.bind_flat(views)
         self._act_spec, self._act_flat, self._act_engine = spec, flat, False
-        self._act_ptrs = [p.data_ptr() for p in self.parameters()]
+        self._act_remember_params()
         return spec, flat
 
     # -- checkpoints (R:dqn/network.py:27-47; format: dqn.utils.pack) -----------------

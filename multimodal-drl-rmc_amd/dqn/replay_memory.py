@@ -125,9 +125,7 @@ class ReplayMemory:
         n = len(actions)
         self.engine.launch_recorded()   # a recorded learn step samples the ring as it was at learn()
         if n:
-            self.engine.push(np.asarray(obses, dtype=np.float32).reshape(n, -1),
-                             np.asarray(actions).reshape(n), np.asarray(rews, dtype=np.float32).reshape(n),
-                             np.asarray(dones).reshape(n), np.asarray(new_obses, dtype=np.float32).reshape(n, -1))
+            self.engine.push_host(obses, actions, rews, dones, new_obses, n)
         for e, done in enumerate(dones):
             if done:
                 yield e

@@ -191,10 +191,13 @@ def test_gpu_agent_deferred_learn_bit_identical(tmp_path, monkeypatch, algo, sof
     """learn() records the step and the next agent call launches it (update_target_network with the
     soft update fused into the Adam pass; RNG hand-back through pinned buffers, installed lazily):
     bitwise the synchronous learn() (DQNX_AGENT_DEFER=0) over a train.py loop, hard target updates
-    (every 3 steps) included, the global RNG states after every iteration and the logged loss."""
+    (every 3 steps) included, the global RNG states after every iteration and the logged loss; and the
+    in-place staging of random._inst (dqnx_agent_learn_mt) bitwise the portable getstate / getrandbits
+    hand-off (DQNX_AGENT_MT_INPLACE=0)."""
     runs = []
-    for defer in ("0", "1"):
+    for defer, inplace in (("0", "1"), ("1", "1"), ("0", "0")):   # (+ the portable getstate/getrandbits path)
         monkeypatch.setenv("DQNX_AGENT_DEFER", defer)
+        monkeypatch.setenv("DQNX_AGENT_MT_INPLACE", inplace)
         torch.manual_seed(5)
         agent = getattr(Agents, algo)(**agent_kwargs(algo, 284, 64, 1000, tmp_path, target_soft_update=soft,
                                                      update_target_frequency=3))
@@ -212,16 +215,17 @@ def test_gpu_agent_deferred_learn_bit_identical(tmp_path, monkeypatch, algo, sof
             agent.store_transitions(obs[700 + t:701 + t], a, [float(rew[700 + t])], [False], nobs[700 + t:701 + t], None)
             agent.learn()
             agent.update_target_network()
-            states.append((a, random.getstate() if defer == "0" else None))
+            states.append((a, random.getstate()))
         agent.flush()
         torch.cuda.synchronize()
         runs.append((agent, states, random.getstate(), np.random.get_state()[1].copy(), agent.engine.loss()))
-    (a0, s0, r0, n0, l0), (a1, s1, r1, n1, l1) = runs
-    assert [x[0] for x in s0] == [x[0] for x in s1]
-    assert r0 == r1 and np.array_equal(n0, n1) and l0 == l1
-    assert torch.equal(a0.engine.params, a1.engine.params)
-    assert torch.equal(a0.engine.target_params, a1.engine.target_params)
-    assert torch.equal(a0.engine.adam_m, a1.engine.adam_m)
+    a0, s0, r0, n0, l0 = runs[0]
+    for a1, s1, r1, n1, l1 in runs[1:]:
+        assert s0 == s1   # actions and the global state after every iteration
+        assert r0 == r1 and np.array_equal(n0, n1) and l0 == l1
+        assert torch.equal(a0.engine.params, a1.engine.params)
+        assert torch.equal(a0.engine.target_params, a1.engine.target_params)
+        assert torch.equal(a0.engine.adam_m, a1.engine.adam_m)
 
 
 @pytest.mark.parametrize("algo,net", [("DuelingDoubleDQNAgent", "mlp"), ("PerDuelingDoubleDQNAgent", "mlp"),

@@ -65,3 +65,30 @@ def test_rng_advance_matches_numpy_legacy_uniform(k):
         np.random.uniform(i, i + 1)
     st = np.random.get_state()
     assert np.array_equal(after, np.append(np.asarray(st[1], dtype=np.uint32), np.uint32(st[2])))
+
+
+def test_cpython_generator_layout_and_in_place_advance():
+    """The drop-in's dqnx_agent_learn_mt works on random._inst's own MT19937 words (checked against
+    random.getstate() by dqn.agent._cpython_mt_addresses).  Writing the mirrored post-draw state there
+    leaves the generator exactly where random.sample(range(n), k) leaves it."""
+    import ctypes
+
+    from dqn.agent import _cpython_mt_addresses
+    addr = _cpython_mt_addresses()
+    assert addr is not None, "CPython RandomObject layout not recognised (the agent falls back to getstate)"
+    mt = (ctypes.c_uint32 * 624).from_address(addr[0])
+    pos = ctypes.c_int32.from_address(addr[1])
+    for n, k in ((1000, 32), (1_000_000, 1024), (5000, 4096)):
+        random.seed(n + k)
+        random.random()
+        s0 = random.getstate()
+        s625 = np.append(np.frombuffer(mt, dtype=np.uint32), np.uint32(pos.value))
+        assert np.array_equal(s625, np.asarray(s0[1], dtype=np.uint32))
+        _, after = M.sample_words(s625, n, k)
+        ctypes.memmove(mt, after.ctypes.data, 624 * 4)   # what dqnx_agent_learn_mt writes back
+        pos.value = int(after[624])
+        moved = random.getstate()
+        random.setstate(s0)
+        random.sample(range(n), k)
+        assert moved == random.getstate(), (n, k)
+        assert moved[2] == s0[2]   # gauss_next untouched
