@@ -311,7 +311,9 @@ int dqnx_apply_grads(dqnx_engine* e, int32_t flags, void* stream);
  * can all-reduce a finished bucket (on a side stream) while the engine runs the rest of the
  * backward, and apply Adam to it before the last bucket arrives.  Bucket 0 = dense layers +
  * Q head + the loss slot (done after the dense backward), then one bucket per conv, last conv
- * first; an MLP has one bucket.  Each bucket is a contiguous range of DQNX_BUF_GRADS /
+ * first.  The fused MLP plan (up to 2048 rows per GPU): bucket 0 = every layer but layer 1 + the
+ * head + the loss slot, bucket 1 = layer 1 (its weight-gradient tiles as a launch of their own); the
+ * slab plan's MLP has one bucket.  Each bucket is a contiguous range of DQNX_BUF_GRADS /
  * DQNX_BUF_PARAMS.  Enqueue dqnx_learn_step_bucket for b = 0, 1, ... in order on one stream;
  * dqnx_apply_grads_bucket(b) after bucket b's all-reduce (bucket 0's also applies the PER tree
  * update).  Together they equal dqnx_learn_step(GRADS_ONLY) + dqnx_apply_grads, bit for bit.

@@ -20,3 +20,14 @@ import json; d=json.loads(open('gpurun_out/r04j/c4_mr$mr.json').read().strip().s
 print('mr=$mr', d['value'], d['ms_per_step'], d['roofline']['achieved'], d['roofline']['frac'], json.dumps(d.get('kernels_us', d.get('roofline',{}).get('kernels','')))[:600])
 "
 done
+for v in base fnb3 fnb4fpf2 fnb3fpf2 fpf8; do
+  lib=multimodal-drl-rmc_amd/dqn/_lib/var/libdqnx_$v.so; [ $v = base ] && lib=multimodal-drl-rmc_amd/dqn/_lib/libdqnx.so
+  DQNX_LIB=$PWD/$lib timeout -k 10 200 python bench.py --steps 300 --warmup 30 --no-extras --no-cpu-baseline > gpurun_out/r04j/var_$v.json 2> gpurun_out/r04j/var_$v.err || { tail -3 gpurun_out/r04j/var_$v.err; exit 1; }
+  DQNX_LIB=$PWD/$lib timeout -k 10 200 python bench.py --algo PerDuelingDoubleDQNAgent --compute bf16 --batch 8192 --steps 30 --warmup 5 --no-extras --no-cpu-baseline > gpurun_out/r04j/var_c4_$v.json 2> gpurun_out/r04j/var_c4_$v.err || { tail -3 gpurun_out/r04j/var_c4_$v.err; exit 1; }
+  python -c "
+import json
+for f in ('var_$v','var_c4_$v'):
+    d=json.loads(open('gpurun_out/r04j/'+f+'.json').read().strip().splitlines()[-1])
+    print(f, round(d['ms_per_step']*1e3,2), [(k['kernel'],round(k['avg_us'],2)) for k in d.get('kernels',[])])
+"
+done
