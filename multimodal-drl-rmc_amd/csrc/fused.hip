@@ -115,20 +115,42 @@ struct WStream {
     __amdgpu_buffer_rsrc_t rs;
     uint32_t off[2];
     int nch;
+    int ng, rot;   // groups of FPF chunks; the group the stream starts at (DQNX_FWD_ROT)
 };
 
+// DQNX_FWD_ROT (measurement variant): a workgroup walks its stream's groups starting at group
+// `rot` (its row tile mod the group count), so the CUs of an XCD request different weight blocks
+// at any moment instead of all the same ones.  Changes the K accumulation order per row tile.
+#ifndef DQNX_FWD_ROT
+#define DQNX_FWD_ROT 0
+#endif
+// chunk s of the walk -> chunk of the stream (nch = past the end: an out-of-range fetch)
+__device__ __forceinline__ int wchunk(const WStream& w, int s) {
+#if DQNX_FWD_ROT
+    const int g = s / FPF;
+    if (g >= w.ng) return w.nch;
+    const int gr = g + w.rot < w.ng ? g + w.rot : g + w.rot - w.ng;
+    return gr * FPF + (s - g * FPF);
+#else
+    return s;
+#endif
+}
+
 template <int TN>
-__device__ __forceinline__ void bfetch(const WStream& w, int ch, float4 (&d)[2]) {
+__device__ __forceinline__ void bfetch(const WStream& w, int s, float4 (&d)[2]) {
+    const int ch = wchunk(w, s);
 #pragma unroll
     for (int t = 0; t < TN; t++) d[t] = bld4(w.rs, ch < w.nch ? w.off[t] + 1024u * ch : kOOB);
 }
 
 // Open the stream over the wave's tiles (column tile offset c0t) and issue groups 0..FNB-2.
 __device__ __forceinline__ void stream_open(const float* blk, int ntiles, int nch, int c0t, const WaveCols& c,
-                                            WStream& w, float4 (&wb)[FNB][FPF][2]) {
+                                            WStream& w, float4 (&wb)[FNB][FPF][2], int seed = 0) {
     const uint32_t lane = threadIdx.x & 63;
     w.rs = wave_rsrc(blk, (uint32_t)ntiles * nch * 1024u);
     w.nch = nch;
+    w.ng = (nch + FPF - 1) / FPF;
+    w.rot = DQNX_FWD_ROT ? seed % w.ng : 0;
     w.off[0] = ((uint32_t)(c0t + (c.tn >= 1 ? c.n0[0] >> 4 : 0)) * nch * 64u + lane) * 16u;
     w.off[1] = ((uint32_t)(c0t + (c.tn >= 2 ? c.n0[1] >> 4 : 0)) * nch * 64u + lane) * 16u;
     if (c.tn == 2) {
@@ -203,7 +225,7 @@ __device__ __forceinline__ void wave_mma_t(const void* As, int sa, int ngroups, 
             // pin the refill ahead of this group's MFMAs: left alone, the scheduler sinks the
             // loads below them and the prefetch distance collapses to ~0
             __builtin_amdgcn_sched_barrier(0);
-            if (grp + u < ngroups) mma_group<TN, BF>(ap, ch, w.nch, wb[u], acc);
+            if (grp + u < ngroups) mma_group<TN, BF>(ap, wchunk(w, ch), w.nch, wb[u], acc);
         }
     }
 }
@@ -274,7 +296,7 @@ __device__ __forceinline__ void wave_mma_mr_t(const void* As, int sa, int ngroup
 #pragma unroll
             for (int p = 0; p < FPF; p++) bfetch<TN>(w, ch + (FNB - 1) * FPF + p, wb[(u + FNB - 1) % FNB][p]);
             __builtin_amdgcn_sched_barrier(0);
-            if (grp + u < ngroups) mma_group_mr<TN, BF, MR>(ap, 16 * sa, ch, w.nch, wb[u], acc);
+            if (grp + u < ngroups) mma_group_mr<TN, BF, MR>(ap, 16 * sa, wchunk(w, ch), w.nch, wb[u], acc);
         }
     }
 }
@@ -362,7 +384,7 @@ __global__ __launch_bounds__(FT) void k_mlp_fwd(FusedFwdArgs a) {
     WaveCols c = wave_cols(PH == 1 ? a.out[0] / nsp : a.out[LB]);
     if constexpr (PH == 2) {
         // H_1 rows of this stream, written by the split layer-1 launch -> LDS (zero past the batch)
-        stream_open(a.wblk[tgt][1], a.out[1] >> 4, fwd_nch<BF>(a.in[1]), 0, c, ws, wb);
+        stream_open(a.wblk[tgt][1], a.out[1] >> 4, fwd_nch<BF>(a.in[1]), 0, c, ws, wb, tile);
         const int N0 = a.out[0], q4 = N0 >> 2;
         const float* h1 = a.H[0] + (int64_t)s * a.Bl * N0;
         float4 hv[2 * MR];
@@ -396,7 +418,7 @@ __global__ __launch_bounds__(FT) void k_mlp_fwd(FusedFwdArgs a) {
         const int q4 = kz >> 2, rs4 = a.ring_stride >> 2;
         // branch-free: every slot loads (clamped row / column) and selects zero afterwards,
         // so the loads issue back to back (one phys round trip, then one ring round trip)
-        if (DQNX_FUSED_ORDER == 1) stream_open(a.wblk[tgt][0], a.out[0] >> 4, fwd_nch<BF>(a.in[0]), coff >> 4, c, ws, wb);
+        if (DQNX_FUSED_ORDER == 1) stream_open(a.wblk[tgt][0], a.out[0] >> 4, fwd_nch<BF>(a.in[0]), coff >> 4, c, ws, wb, tile);
         int32_t slot[GQ];
 #pragma unroll
         for (int j = 0; j < GQ; j++) {
@@ -408,7 +430,7 @@ __global__ __launch_bounds__(FT) void k_mlp_fwd(FusedFwdArgs a) {
         int32_t tslot = 0;
         const bool keep0 = keep && part == 0;   // one part writes the stream-0 copies
         if (keep0 && tid < nb) tslot = a.phys[b0 + tid];
-        if (DQNX_FUSED_ORDER == 0) stream_open(a.wblk[tgt][0], a.out[0] >> 4, fwd_nch<BF>(a.in[0]), coff >> 4, c, ws, wb);
+        if (DQNX_FUSED_ORDER == 0) stream_open(a.wblk[tgt][0], a.out[0] >> 4, fwd_nch<BF>(a.in[0]), coff >> 4, c, ws, wb, tile);
         float4 xv[GQ];
 #pragma unroll
         for (int j = 0; j < GQ; j++) {
@@ -419,7 +441,7 @@ __global__ __launch_bounds__(FT) void k_mlp_fwd(FusedFwdArgs a) {
             if (!ok) x = make_float4(0.f, 0.f, 0.f, 0.f);
             xv[j] = x;
         }
-        if (DQNX_FUSED_ORDER == 2) stream_open(a.wblk[tgt][0], a.out[0] >> 4, fwd_nch<BF>(a.in[0]), coff >> 4, c, ws, wb);
+        if (DQNX_FUSED_ORDER == 2) stream_open(a.wblk[tgt][0], a.out[0] >> 4, fwd_nch<BF>(a.in[0]), coff >> 4, c, ws, wb, tile);
         // after the row loads are in flight: the transition scalars' own round trip overlaps them
         if (keep0 && tid < nb)
             a.trans[b0 + tid] = make_float4(__int_as_float(a.act[tslot]), a.rew[tslot], a.done[tslot], 0.f);
@@ -458,7 +480,7 @@ __global__ __launch_bounds__(FT) void k_mlp_fwd(FusedFwdArgs a) {
         // next layer's weight stream in flight during the epilogue + barrier
         if (l + 1 < LE) {
             c = wave_cols(a.out[l + 1]);
-            stream_open(a.wblk[tgt][l + 1], a.out[l + 1] >> 4, fwd_nch<BF>(a.in[l + 1]), 0, c, ws, wb);
+            stream_open(a.wblk[tgt][l + 1], a.out[l + 1] >> 4, fwd_nch<BF>(a.in[l + 1]), 0, c, ws, wb, tile);
         }
         float* Hs = FBUF(cur ^ 1);
         // H to HBM: stream 0 (the backward's operands); the split layer 1 writes every stream's
@@ -784,6 +806,9 @@ __global__ __launch_bounds__(FT) void k_head_bwd(HeadBwdArgs a) {
 #ifndef DQNX_DWB_KT64
 #define DQNX_DWB_KT64 32
 #endif
+#ifndef DQNX_DWB_PIPE
+#define DQNX_DWB_PIPE 1   // two passes in flight, two LDS buffers (0: one pass ahead, one buffer)
+#endif
 #ifndef DQNX_DWB_KT32
 #define DQNX_DWB_KT32 128
 #endif
@@ -798,9 +823,13 @@ struct DwbShape {
 // rows [k0, k0 + KT) x cols [c0, c0 + BT) of a [K][ld] operand; pair index q = (column group of
 // 4) * KP + k pair, q = tid + 256 u.  Column j reads 0 past `ncols`, or 1.0 at j == aug.
 template <int BT, int KT>
+struct DwbStage {
+    static constexpr int KP = KT / 2, NQ = KP * (BT / 4), NU = NQ / 256 > 0 ? NQ / 256 : 1;
+};
+template <int BT, int KT>
 __device__ __forceinline__ void dwb_stage(const float* base, int ld, int ncols, int aug, int c0, int k0, int kend,
-                                          float4 (&v)[(KT / 2) * (BT / 4) / 256 > 0 ? (KT / 2) * (BT / 4) / 256 : 1][2]) {
-    constexpr int KP = DwbShape<KT>::KP, NQ = KP * (BT / 4), NU = NQ / 256 > 0 ? NQ / 256 : 1;
+                                          float4 (&v)[DwbStage<BT, KT>::NU][2]) {
+    constexpr int KP = DwbStage<BT, KT>::KP, NQ = DwbStage<BT, KT>::NQ, NU = DwbStage<BT, KT>::NU;
 #pragma unroll
     for (int u = 0; u < NU; u++) {
         const int q = threadIdx.x + 256 * u;
@@ -826,9 +855,9 @@ __device__ __forceinline__ void dwb_stage(const float* base, int ld, int ncols, 
     }
 }
 template <int BT, int KT>
-__device__ __forceinline__ void dwb_store(uint32_t* dst,
-                                          const float4 (&v)[(KT / 2) * (BT / 4) / 256 > 0 ? (KT / 2) * (BT / 4) / 256 : 1][2]) {
-    constexpr int KP = DwbShape<KT>::KP, SD = DwbShape<KT>::SD, NQ = KP * (BT / 4), NU = NQ / 256 > 0 ? NQ / 256 : 1;
+__device__ __forceinline__ void dwb_store(uint32_t* dst, const float4 (&v)[DwbStage<BT, KT>::NU][2]) {
+    constexpr int KP = DwbStage<BT, KT>::KP, SD = DwbShape<KT>::SD, NQ = DwbStage<BT, KT>::NQ,
+                  NU = DwbStage<BT, KT>::NU;
 #pragma unroll
     for (int u = 0; u < NU; u++) {
         const int q = threadIdx.x + 256 * u;
@@ -842,17 +871,25 @@ __device__ __forceinline__ void dwb_store(uint32_t* dst,
     }
 }
 
-// BT x BT output tile (32 or 64), 4 waves of (BT/32) x (BT/32) 16x16 tiles, KT samples per pass.
-template <int BT, int KT>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DQNX_DWB_WAVES))) void k_dw_bf16(BwdArgs a) {
-    static_assert(BT == 32 || BT == 64, "tile");
+// BM x BN output tile (rows = dZ columns, cols = X columns + the ones column), 4 waves in a 2 x 2
+// grid of (BM/2) x (BN/2) wave tiles of 16x16 MFMA tiles, KT samples per pass.  Larger tiles read
+// fewer operand bytes per MFMA: 64 x 64 moves 16 KiB of fp32 rows per 4 MFMAs a wave, 128 x 128
+// 32 KiB per 16 (configs[4]: 8192 samples, 32 split-K slices).
+template <int BM, int BN>
+constexpr int dwb_waves() {
+    return BM * BN >= 128 * 128 ? 2 : BM * BN >= 128 * 64 ? 3 : (DQNX_DWB_PIPE ? 4 : DQNX_DWB_WAVES);
+}
+template <int BM, int BN, int KT>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(dwb_waves<BM, BN>()))) void k_dw_bf16(BwdArgs a) {
+    static_assert((BM == 32 || BM == 64 || BM == 128) && (BN == 32 || BN == 64 || BN == 128), "tile");
     static_assert(KT % 32 == 0, "whole MFMA chunks");
-    constexpr int T = BT / 32, SD = DwbShape<KT>::SD;
-    constexpr int NU = (KT / 2) * (BT / 4) / 256 > 0 ? (KT / 2) * (BT / 4) / 256 : 1;
-    static_assert((KT / 2) * (BT / 4) <= 256 * NU, "pairs per thread");
-    __shared__ __attribute__((aligned(16))) uint32_t lds[2 * BT * SD];
+    constexpr int TM = BM / 32, TN = BN / 32, SD = DwbShape<KT>::SD;
+    constexpr int NUA = DwbStage<BM, KT>::NU, NUB = DwbStage<BN, KT>::NU;
+    static_assert((KT / 2) * (BM / 4) <= 256 * NUA && (KT / 2) * (BN / 4) <= 256 * NUB, "pairs per thread");
+    constexpr int NB = DQNX_DWB_PIPE ? 2 : 1;   // LDS pass buffers
+    __shared__ __attribute__((aligned(16))) uint32_t lds[NB * (BM + BN) * SD];
     uint32_t* la = lds;            // dZ columns (rows m of the gradient tile)
-    uint32_t* lb = lds + BT * SD;  // X columns (+ ones)
+    uint32_t* lb = lds + BM * SD;  // X columns (+ ones)
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int i = lane & 15, g = lane >> 4;
     const int wm = wid >> 1, wn = wid & 1;
@@ -884,52 +921,89 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DQNX_DWB_WA
     const int bx = b % d.grid_x;
     const int t2 = b / d.grid_x;
     const int by = t2 % d.grid_y, bz = t2 / d.grid_y;
-    const int m0 = by * BT, n0 = bx * BT;
+    const int m0 = by * BM, n0 = bx * BN;
     const int kb = bz * a.kslice;
     const int ke = min(a.Bl, kb + a.kslice);
-    floatx4 acc[T][T];
+    floatx4 acc[TM][TN];
 #pragma unroll
-    for (int tm = 0; tm < T; tm++)
+    for (int tm = 0; tm < TM; tm++)
 #pragma unroll
-        for (int tn = 0; tn < T; tn++) acc[tm][tn] = floatx4{0.f, 0.f, 0.f, 0.f};
+        for (int tn = 0; tn < TN; tn++) acc[tm][tn] = floatx4{0.f, 0.f, 0.f, 0.f};
     const int ncz = d.out < d.ldz ? d.out : d.ldz;   // dZ columns that exist (head: ldz 16 >= NH)
-    float4 va[NU][2], vb[NU][2];
-    dwb_stage<BT, KT>(d.dZ, d.ldz, ncz, -1, m0, kb, ke, va);
-    dwb_stage<BT, KT>(d.X, d.ldx, d.in, d.in, n0, kb, ke, vb);
-    for (int k0 = kb; k0 < ke; k0 += KT) {
-        __syncthreads();   // previous pass's fragments read
-        dwb_store<BT, KT>(la, va);
-        dwb_store<BT, KT>(lb, vb);
-        __syncthreads();
-        if (k0 + KT < ke) {   // next pass in flight during this one's MFMAs
-            dwb_stage<BT, KT>(d.dZ, d.ldz, ncz, -1, m0, k0 + KT, ke, va);
-            dwb_stage<BT, KT>(d.X, d.ldx, d.in, d.in, n0, k0 + KT, ke, vb);
-        }
+    auto mma_pass = [&](const uint32_t* pa, const uint32_t* pb) {
 #pragma unroll
         for (int ch = 0; ch < KT / 32; ch++) {
-            u32x4 fa[T], fb[T];
+            u32x4 fa[TM], fb[TN];
 #pragma unroll
-            for (int t = 0; t < T; t++) {
-                fa[t] = *reinterpret_cast<const u32x4*>(la + (wm * 16 * T + t * 16 + i) * SD + 16 * ch + 4 * g);
-                fb[t] = *reinterpret_cast<const u32x4*>(lb + (wn * 16 * T + t * 16 + i) * SD + 16 * ch + 4 * g);
+            for (int t = 0; t < TM; t++)
+                fa[t] = *reinterpret_cast<const u32x4*>(pa + (wm * 16 * TM + t * 16 + i) * SD + 16 * ch + 4 * g);
+#pragma unroll
+            for (int t = 0; t < TN; t++)
+                fb[t] = *reinterpret_cast<const u32x4*>(pb + (wn * 16 * TN + t * 16 + i) * SD + 16 * ch + 4 * g);
+#pragma unroll
+            for (int tm = 0; tm < TM; tm++)
+#pragma unroll
+                for (int tn = 0; tn < TN; tn++) acc[tm][tn] = mfma16x16x32bf16(fa[tm], fb[tn], acc[tm][tn]);
+        }
+    };
+    float4 va[NUA][2], vb[NUB][2];
+    dwb_stage<BM, KT>(d.dZ, d.ldz, ncz, -1, m0, kb, ke, va);
+    dwb_stage<BN, KT>(d.X, d.ldx, d.in, d.in, n0, kb, ke, vb);
+    if constexpr (DQNX_DWB_PIPE) {
+        // two passes in flight in registers, two LDS buffers, one barrier per pass: while pass p's
+        // fragments are multiplied out of buffer p & 1, pass p+1 goes into the other buffer and
+        // pass p+2's rows are loading
+        uint32_t* la1 = lds + (BM + BN) * SD;
+        uint32_t* lb1 = la1 + BM * SD;
+        float4 wa[NUA][2], wb2[NUB][2];
+        dwb_stage<BM, KT>(d.dZ, d.ldz, ncz, -1, m0, kb + KT, ke, wa);
+        dwb_stage<BN, KT>(d.X, d.ldx, d.in, d.in, n0, kb + KT, ke, wb2);
+        dwb_store<BM, KT>(la, va);
+        dwb_store<BN, KT>(lb, vb);
+        dwb_stage<BM, KT>(d.dZ, d.ldz, ncz, -1, m0, kb + 2 * KT, ke, va);
+        dwb_stage<BN, KT>(d.X, d.ldx, d.in, d.in, n0, kb + 2 * KT, ke, vb);
+        __syncthreads();
+        for (int k0 = kb; k0 < ke; k0 += 2 * KT) {
+            mma_pass(la, lb);                                // pass k0 (buffer 0)
+            if (k0 + KT >= ke) break;
+            dwb_store<BM, KT>(la1, wa);                      // pass k0 + KT -> buffer 1
+            dwb_store<BN, KT>(lb1, wb2);
+            dwb_stage<BM, KT>(d.dZ, d.ldz, ncz, -1, m0, k0 + 3 * KT, ke, wa);
+            dwb_stage<BN, KT>(d.X, d.ldx, d.in, d.in, n0, k0 + 3 * KT, ke, wb2);
+            __syncthreads();
+            mma_pass(la1, lb1);                              // pass k0 + KT (buffer 1)
+            if (k0 + 2 * KT >= ke) break;
+            // buffer 0's readers (pass k0) all passed the barrier above
+            dwb_store<BM, KT>(la, va);                       // pass k0 + 2 KT -> buffer 0
+            dwb_store<BN, KT>(lb, vb);
+            dwb_stage<BM, KT>(d.dZ, d.ldz, ncz, -1, m0, k0 + 4 * KT, ke, va);
+            dwb_stage<BN, KT>(d.X, d.ldx, d.in, d.in, n0, k0 + 4 * KT, ke, vb);
+            __syncthreads();
+        }
+    } else {
+        for (int k0 = kb; k0 < ke; k0 += KT) {
+            __syncthreads();   // previous pass's fragments read
+            dwb_store<BM, KT>(la, va);
+            dwb_store<BN, KT>(lb, vb);
+            __syncthreads();
+            if (k0 + KT < ke) {   // next pass in flight during this one's MFMAs
+                dwb_stage<BM, KT>(d.dZ, d.ldz, ncz, -1, m0, k0 + KT, ke, va);
+                dwb_stage<BN, KT>(d.X, d.ldx, d.in, d.in, n0, k0 + KT, ke, vb);
             }
-#pragma unroll
-            for (int tm = 0; tm < T; tm++)
-#pragma unroll
-                for (int tn = 0; tn < T; tn++) acc[tm][tn] = mfma16x16x32bf16(fa[tm], fb[tn], acc[tm][tn]);
+            mma_pass(la, lb);
         }
     }
     // rows beyond `out` / columns beyond `in` (+1) of the tile are not stored
     float* part = d.partial + (int64_t)bz * d.pstride;
 #pragma unroll
-    for (int tn = 0; tn < T; tn++) {
-        const int col = n0 + wn * 16 * T + tn * 16 + i;
+    for (int tn = 0; tn < TN; tn++) {
+        const int col = n0 + wn * 16 * TN + tn * 16 + i;
         if (col > d.in) continue;
 #pragma unroll
-        for (int tm = 0; tm < T; tm++)
+        for (int tm = 0; tm < TM; tm++)
 #pragma unroll
             for (int r = 0; r < 4; r++) {
-                const int row = m0 + wm * 16 * T + tm * 16 + 4 * g + r;
+                const int row = m0 + wm * 16 * TM + tm * 16 + 4 * g + r;
                 if (row >= d.out) continue;
                 int64_t o;
                 if (d.head_kind < 0) o = (col < d.in) ? (int64_t)row * d.in + col : (int64_t)d.out * d.in + row;
@@ -939,21 +1013,28 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DQNX_DWB_WA
     }
 }
 
-// Tile size: 64 x 64 when that still gives >= 512 workgroups (large batches: fewer operand
-// re-reads), else 32 x 32 (B=1024: 132 workgroups of 64 x 64 left the chip idle).
-static int dw_bf16_tile(const BwdArgs& a) {
+// Tile shape (BM x BN): 64 x 64 when that still gives >= 512 workgroups (large batches: fewer operand
+// re-reads), else 32 x 32 (B=1024: 132 workgroups of 64 x 64 left the chip idle).  DQNX_DWB_SHAPE
+// (tuning builds): 1 = 32 x 32, 2 = 64 x 64, 3 = 128 x 128, 4 = 128 x 64.
+struct DwbTile { int bm, bn; };
+static DwbTile dw_bf16_tile(const BwdArgs& a) {
+    static const int shape = tuning_knob("DQNX_DWB_SHAPE", 0);
+    if (shape == 1) return {32, 32};
+    if (shape == 2) return {64, 64};
+    if (shape == 3) return {128, 128};
+    if (shape == 4) return {128, 64};
     int n64 = 0;
     for (int p = 0; p < a.ndw; p++)
         n64 += ((a.dw[p].in + 1 + 63) / 64) * ((a.dw[p].out + 63) / 64) * a.dw_slices;
-    return n64 >= 512 ? 64 : 32;
+    return n64 >= 512 ? DwbTile{64, 64} : DwbTile{32, 32};
 }
 
 void dw_bf16_grid(BwdArgs& a) {
-    const int bt = dw_bf16_tile(a);
+    const DwbTile t = dw_bf16_tile(a);
     for (int p = 0; p < a.ndw; p++) {
         DwProblem& d = a.dw[p];
-        d.grid_x = (d.in + 1 + bt - 1) / bt;
-        d.grid_y = (d.out + bt - 1) / bt;
+        d.grid_x = (d.in + 1 + t.bn - 1) / t.bn;
+        d.grid_y = (d.out + t.bm - 1) / t.bm;
         d.blocks = d.grid_x * d.grid_y * a.dw_slices;
     }
 }
@@ -968,8 +1049,11 @@ int launch_dw_bf16(const BwdArgs& a, hipStream_t s) {
             return set_error(DQNX_EUNSUPPORTED, "bf16 weight gradients need row strides that are multiples of 4");
     // measured: 64 x 64 tiles best with 32-sample passes (64: +1.7 us, 128: +6 us at B=8192);
     // 32 x 32 tiles with 128-sample passes (the fp32 kernel's depth)
-    if (dw_bf16_tile(a) == 64) hipLaunchKernelGGL((k_dw_bf16<64, DQNX_DWB_KT64>), dim3(blocks), dim3(256), 0, s, a);
-    else hipLaunchKernelGGL((k_dw_bf16<32, DQNX_DWB_KT32>), dim3(blocks), dim3(256), 0, s, a);
+    const DwbTile t = dw_bf16_tile(a);
+    if (t.bm == 128 && t.bn == 128) hipLaunchKernelGGL((k_dw_bf16<128, 128, 32>), dim3(blocks), dim3(256), 0, s, a);
+    else if (t.bm == 128) hipLaunchKernelGGL((k_dw_bf16<128, 64, 32>), dim3(blocks), dim3(256), 0, s, a);
+    else if (t.bm == 64) hipLaunchKernelGGL((k_dw_bf16<64, 64, DQNX_DWB_KT64>), dim3(blocks), dim3(256), 0, s, a);
+    else hipLaunchKernelGGL((k_dw_bf16<32, 32, DQNX_DWB_KT32>), dim3(blocks), dim3(256), 0, s, a);
     DQNX_HIP_CHECK(hipGetLastError());
     return DQNX_OK;
 }
