@@ -2711,7 +2711,9 @@ int dqnx_engine_create(const dqnx_config* cfg, dqnx_engine** out) {
     const int L = (int)e->np.dense.size();
     e->slices.assign(L, 1);
     e->kslice.assign(L, e->Bl);
-    int dw_rows = 256;   // minibatch rows per split-K slice of the weight gradients
+    // minibatch rows per split-K slice of the weight gradients.  bf16 (configs[4], B=8192): 512 rows
+    // = 16 slabs, the Adam pass sums half the partials (step 94-96 -> 92 us, profiles/r04/dw_bf16_shapes.json)
+    int dw_rows = (e->bwd_plan == 2 && e->fplan.bf16) ? 512 : 256;
     dw_rows = std::max(16, tuning_knob("DQNX_DW_ROWS", dw_rows));
     for (int l = 0; l < L; l++) {
         int S = e->Bl / dw_rows;

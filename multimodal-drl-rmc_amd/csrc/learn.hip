@@ -909,7 +909,22 @@ __global__ __launch_bounds__(256) void k_adam4(AdamArgs a) {
         const int64_t ps = sg.pstride;
         float4 g = z4;
         const int cnt = live && j < sg.S ? (sg.S - j + ADAM_WIDE - 1) / ADAM_WIDE : 0;   // slabs j, j + W, ...
-        for (int u0 = 0; u0 < cnt; u0 += 16) {
+        if (cnt > 0 && cnt <= 4) {   // (up to 32 slabs: one round trip of 4 loads instead of 16, 12 of
+                                     // them clamped; cnt = 0: slab j may not exist, nothing is loaded)
+            float4 pv[4];
+#pragma unroll
+            for (int q = 0; q < 4; q++) pv[q] = ld4(q4 + (int64_t)(j + (q < cnt ? q : 0) * ADAM_WIDE) * ps);
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                if (q >= cnt) break;
+                if (q == 0) {
+                    g = pv[q];
+                } else {
+                    g.x += pv[q].x; g.y += pv[q].y; g.z += pv[q].z; g.w += pv[q].w;
+                }
+            }
+        }
+        for (int u0 = 0; cnt > 4 && u0 < cnt; u0 += 16) {
             float4 pv[16];
 #pragma unroll
             for (int q = 0; q < 16; q++) {   // addresses clamped to slab j: the loads stay unconditional
