@@ -378,9 +378,9 @@ def run_learner(args, eng, world, backend, steps, warmup, dist, device, dp=None)
     torch.cuda.synchronize()
     eng.check_device_error()
     dp_graph = False
-    # PER shard steps stay eager: replayed as captured graphs they measured ~3x slower on the GPU
-    # clock than the same launches issued eagerly (tools/c5_graph_diag.py)
-    if dp and backend == "nccl" and not args.no_dp_graph and not args.algo.startswith("Per"):
+    # (PER shard steps too: the ~3x slower graphed PER steps of round 3 were the one-GPU projection's
+    # stale |delta| shards, not the graphs -- tools/c5_graph_diag.py)
+    if dp and backend == "nccl" and not args.no_dp_graph:
         # the whole DP step (shard kernels + RCCL all-reduce + Adam) as one replayed graph: the
         # eager loop is host-bound (3 launches + a collective call per ~50 us step).  RCCL
         # collectives are capturable; gloo's are host calls and never are.
@@ -493,9 +493,24 @@ def roofline_of(args, kern, batch_tag):
 ALLREDUCE_EST_US = 20.0   # assumed RCCL all-reduce of the 428 KB MLP-284 gradient over 8 xGMI-linked GPUs
 
 
+def shard_td_exchange(eng):
+    """Stand-in, on one GPU, for the |delta| all-gather of a PER shard step: the other ranks' shards of
+    `per_abs_td` get this rank's |delta| (one small copy kernel).  Without it the ordered priority update
+    of the projection writes stale |delta| for 7/8 of the minibatch, and the degenerate priorities it
+    leaves (most sampled leaves at the minimum) make the SumTree max / min rescans run nearly every step
+    after a few hundred steps (profiles/r04/c5_dynamics.json): the projection would time a state no
+    real world-8 run reaches."""
+    W = eng.world_size
+    if W > 1 and eng.per_abs_td.numel():
+        n = eng.batch // W
+        td = eng.per_abs_td
+        td[n:].view(W - 1, n).copy_(td[:n].unsqueeze(0).expand(W - 1, n))
+
+
 def graphed_shard_steps(eng, args, steps, device, prefetch=None):
     """`steps` GRADS_ONLY shard steps (+ apply_grads) replayed --dp-graph-steps per captured graph, as
-    GraphedDPStep runs them under torchrun (the collective left out).  Returns (seconds, steps per graph)."""
+    GraphedDPStep runs them under torchrun (the collective left out; PER: shard_td_exchange in its place).
+    Returns (seconds, steps per graph)."""
     prefetch = args.prefetch if prefetch is None else prefetch
     gs = max(1, args.dp_graph_steps)
     eng.set_graphs(False)
@@ -506,6 +521,7 @@ def graphed_shard_steps(eng, args, steps, device, prefetch=None):
     with torch.cuda.graph(g):
         for _ in range(gs):
             eng.learn_step(grads_only=True, prefetch=prefetch)
+            shard_td_exchange(eng)
             eng.apply_grads(soft_update=True)
     for _ in range(max(2, args.warmup // gs)):
         g.replay()
@@ -689,6 +705,7 @@ def c5_projection(args, device):
 
     def shard_step():
         eng.learn_step(grads_only=True)
+        shard_td_exchange(eng)              # (the |delta| all-gather's output)
         eng.apply_grads(soft_update=True)   # Adam + the PER tree update of all 8192 |delta|
     for _ in range(args.warmup):
         shard_step()
@@ -697,9 +714,9 @@ def c5_projection(args, device):
     ks = kernel_times(eng, C.STEP_GRADS_ONLY, count=30, reps=3)
     del eng
     torch.cuda.empty_cache()
-    # (replayed graphs of the PER shard step measure ~3x slower than eager launches on ROCm 7.2, while
-    # a kernel trace of the same replays shows the kernels back to back at the eager rate: the faster
-    # of the two is the projection, both are reported)
+    # (round 3 measured these graphed PER shard steps at ~3x the eager time: an artefact of the
+    # projection, which wrote stale |delta| for 7/8 of the minibatch until shard_td_exchange; the
+    # faster of the two is the projection, both are reported)
     t1, shard_g, shard_e = el1 / steps * 1e6, el / steps * 1e6, el_eager / steps * 1e6
     shard = min(shard_g, shard_e)
     return {"one_gpu_step_us": t1, "one_gpu_value": Bg * steps / el1, "rows_per_rank": Bg // W,
@@ -712,8 +729,9 @@ def c5_projection(args, device):
                                  "allreduce_estimate_us": ALLREDUCE_EST_US},
             "note": "rank 0 of world_size 8 on one GPU: the 1024-row shard's GRADS_ONLY step (every rank draws the "
                     "same global 8192 PER sample) + apply_grads (Adam, soft update, the ordered priority update "
-                    "of all 8192 |delta| on every tree replica); add the |delta| all-gather (32 KB) and the "
-                    "428 KB gradient all-reduce for the 8-GPU step"}
+                    "of all 8192 |delta| on every tree replica), the other ranks' |delta| shards filled from "
+                    "rank 0's by one copy kernel in place of the all-gather; add the |delta| all-gather (32 KB) "
+                    "and the 428 KB gradient all-reduce for the 8-GPU step"}
 
 
 def dropin_loop(args, device, batch=1024, iters=200, warmup=20):

@@ -3718,6 +3718,22 @@ int dqnx_act(const dqnx_net_desc* net, const float* params, const float* obs, in
 int dqnx_rng_sample_words(const uint32_t* state625, int64_t n, int32_t k, uint32_t* out625, int64_t* words);
 int dqnx_rng_advance(const uint32_t* state625, int64_t words, uint32_t* out625);
 
+// the caller's state into the engine's pinned staging slot for the next dqnx_agent_launch
+static int agent_pin_state(dqnx_engine* e, int32_t which, const uint32_t* state625) {
+    if (!e->ag_rng_pin) {
+        DQNX_HIP_CHECK(hipHostMalloc((void**)&e->ag_rng_pin, 2 * 625 * 4, hipHostMallocDefault));
+        for (int i = 0; i < 2; i++) DQNX_HIP_CHECK(hipEventCreateWithFlags(&e->ag_rng_ev[i], hipEventDisableTiming));
+    }
+    const int i = e->ag_slot ^= 1;
+    if (e->ag_rng_live[i]) {   // that block's previous upload has run (two launches ago: long passed)
+        DQNX_HIP_CHECK(hipEventSynchronize(e->ag_rng_ev[i]));
+        e->ag_rng_live[i] = false;
+    }
+    memcpy(e->ag_rng_pin + 625 * i, state625, 625 * 4);
+    e->ag_which = which;
+    return DQNX_OK;
+}
+
 int dqnx_agent_stage_rng(dqnx_engine* e, int32_t which, const uint32_t* state625, int64_t* words) {
     int rc = check_bound(e);
     if (rc) return rc;
@@ -3731,17 +3747,8 @@ int dqnx_agent_stage_rng(dqnx_engine* e, int32_t which, const uint32_t* state625
         rc = dqnx_rng_advance(state625, *words, e->ag_expect);
     }
     if (rc) return rc;
-    if (!e->ag_rng_pin) {
-        DQNX_HIP_CHECK(hipHostMalloc((void**)&e->ag_rng_pin, 2 * 625 * 4, hipHostMallocDefault));
-        for (int i = 0; i < 2; i++) DQNX_HIP_CHECK(hipEventCreateWithFlags(&e->ag_rng_ev[i], hipEventDisableTiming));
-    }
-    const int i = e->ag_slot ^= 1;
-    if (e->ag_rng_live[i]) {   // that block's previous upload has run (two launches ago: long passed)
-        DQNX_HIP_CHECK(hipEventSynchronize(e->ag_rng_ev[i]));
-        e->ag_rng_live[i] = false;
-    }
-    memcpy(e->ag_rng_pin + 625 * i, state625, 625 * 4);
-    e->ag_which = which;
+    rc = agent_pin_state(e, which, state625);
+    if (rc) return rc;
     e->ag_expect_live = true;
     return DQNX_OK;
 }
@@ -3752,12 +3759,32 @@ int dqnx_agent_learn_mt(dqnx_engine* e, uint32_t* mt, int32_t* pos, int32_t flag
     uint32_t s625[625];
     memcpy(s625, mt, 624 * 4);
     s625[624] = (uint32_t)*pos;
-    int rc = dqnx_agent_stage_rng(e, DQNX_RNG_PY, s625, words);
+    int rc;
+    if (flags & DQNX_AGENT_LAUNCH) {
+        // the device only needs the state BEFORE the draw: stage it and launch first, then walk the draw
+        // on the host while the GPU runs the step (the walk of a 1024-row draw is ~7 us)
+        rc = check_bound(e);
+        if (rc) return rc;
+        if (e->pf_valid) return set_error(DQNX_ESTATE, "agent stage while a prefetched minibatch is pending");
+        if ((int64_t)e->Bs > e->ring_size) return set_error(DQNX_EINVAL, "Sample larger than population or is negative");
+        rc = agent_pin_state(e, DQNX_RNG_PY, s625);
+        if (rc) return rc;
+        e->ag_expect_live = false;   // (the check below is armed after the walk)
+        rc = dqnx_agent_launch(e, flags & ~DQNX_AGENT_LAUNCH, stream);
+        if (rc) return rc;
+        rc = dqnx_rng_sample_words(s625, e->ring_size, e->Bs, e->ag_check, words);
+        if (rc) return rc;
+        e->ag_check_live = true;
+        e->ag_check_which = DQNX_RNG_PY;
+        memcpy(mt, e->ag_check, 624 * 4);   // the caller's generator moves past the draw
+        *pos = (int32_t)e->ag_check[624];
+        return DQNX_OK;
+    }
+    rc = dqnx_agent_stage_rng(e, DQNX_RNG_PY, s625, words);
     if (rc) return rc;
     // the caller's generator moves past the draw now (what random.sample would have consumed)
     memcpy(mt, e->ag_expect, 624 * 4);
     *pos = (int32_t)e->ag_expect[624];
-    if (flags & DQNX_AGENT_LAUNCH) return dqnx_agent_launch(e, flags & ~DQNX_AGENT_LAUNCH, stream);
     return DQNX_OK;
 }
 

@@ -94,11 +94,11 @@ class Network(nn.Module):
         head = self.fc_adv if hasattr(self, "fc_adv") else self.fc_out
         return head.out_features
 
-    def _act_gpu(self, obses):
+    def _act_gpu(self, obses, na=None):
         """Greedy actions through the acting kernel: host obs -> dqnx_act_host (obs through pinned memory,
         one launch sequence, actions back, one synchronisation); device obs -> dqnx_act."""
         self._engine_sync()   # a recorded learn step first (stream order does the rest)
-        spec, flat = self._native_act()
+        spec, flat = na if na is not None else self._native_act()
         if isinstance(obses, T.Tensor) and obses.is_cuda:
             x = obses.reshape(obses.shape[0], -1)
             out = _act_native(spec, flat, x, scratch=act_scratch(spec, x.shape[0], flat.device))
@@ -198,8 +198,9 @@ class DeepQNetwork(Network):
         return self.fc_out(self.net(s))
 
     def actions(self, obses):
-        if self._native_act() is not None:
-            return self._act_gpu(obses)
+        na = self._native_act()
+        if na is not None:
+            return self._act_gpu(obses, na)
         obses_t = T.as_tensor(obses, dtype=T.float32).to(self.device)
         q_values = self(obses_t)
         return T.argmax(q_values, dim=1).detach().tolist()
@@ -231,8 +232,9 @@ class DuelingDeepQNetwork(Network):
         return self.fc_adv(self.net(s))
 
     def actions(self, obses):
-        if self._native_act() is not None:
-            return self._act_gpu(obses)
+        na = self._native_act()
+        if na is not None:
+            return self._act_gpu(obses, na)
         obses_t = T.as_tensor(obses, dtype=T.float32).to(self.device)
         adv_q_values = self.advantages(obses_t)
         return T.argmax(adv_q_values, dim=1).detach().tolist()

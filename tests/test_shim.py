@@ -98,3 +98,19 @@ def test_act_scratch_layout_is_monotone():
     sizes = [C.lib().dqnx_act_scratch_bytes(ctypes.byref(d), n) for n in range(1, 70)]
     assert all(b >= a for a, b in zip(sizes, sizes[1:]))
     assert sizes[0] == 256 * 4 + 4
+
+
+def test_epsilon_interp_matches_numpy():
+    """Agent.epsilon (R:dqn/agent.py:86-90) uses a scalar restatement of np.interp over the two points
+    [0, epsilon_decay]; it must give numpy's bits at every step, the end points included."""
+    import random as _r
+
+    from dqn.agent import _interp2
+    rng = _r.Random(7)
+    for _ in range(20000):
+        d = rng.choice([0.0, 1.0, 12345.0, 1e5, 2e6])
+        a, b = rng.uniform(0, 1), rng.uniform(0, 1)
+        x = rng.choice([0, 1, int(d), int(d) + 1, -3, rng.randrange(0, int(3 * d) + 2)])
+        assert _interp2(x, d, a, b) == float(np.interp(x, [0, d], [a, b])), (x, d, a, b)
+        la, lb = np.log(a + 1e-3), np.log(b + 1e-3)
+        assert np.exp(_interp2(x, d, la, lb)) == np.exp(np.interp(x, [0, d], [la, lb]))

@@ -31,6 +31,8 @@ out = {"algo": algo, "global_batch": Bg}
 
 def shard_step():
     eng.learn_step(grads_only=True)
+    if os.environ.get("C5_TD_EXCHANGE", "1") != "0":
+        bench.shard_td_exchange(eng)   # (the |delta| all-gather's output: without it the state degenerates)
     eng.apply_grads(soft_update=True)
 
 
@@ -77,6 +79,12 @@ for gs in (1, 4):
         torch.cuda.synchronize()
     out[f"graph{gs}"]["replay_sync_us"] = (time.perf_counter() - t0) / 10 * 1e6
     del g
+# eager again after the graphs: a slowdown that comes with the state the steps reach (e.g. the
+# SumTree max / min rescans of the priority tracking) shows here too; one from the graphs does not
+torch.cuda.synchronize()
+for w in range(3):
+    el = bench.timed_steps(shard_step, 100, None, dev)
+    out.setdefault("eager_after_us", []).append(el / 100 * 1e6)
 # bisection: graphs of the shard step's halves alone (timing only: the state they leave is meaningless)
 for part, fn in (("learn_only", lambda: eng.learn_step(grads_only=True)),
                  ("apply_only", lambda: eng.apply_grads(soft_update=True))):
