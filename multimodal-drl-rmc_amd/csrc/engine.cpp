@@ -2917,13 +2917,13 @@ int dqnx_replay_push(dqnx_engine* e, const float* obs, const int32_t* act, const
     hipStream_t s = (hipStream_t)stream;
     const int D = e->cfg.net.obs_dim;
     if (!src_on_device && n > 0 && n <= kPinnedPushRows && (int64_t)n <= e->cfg.capacity) {
-        // the env loop's n_env rows (Agent.store_transitions): packed into one pinned block, ONE
-        // H2D copy into the device staging area, the push kernel from there; no host wait (the block
-        // is reused once the event after its previous copy has passed)
-        const size_t fb = (size_t)n * D * 4, bytes = 2 * fb + (size_t)n * 9;
+        // the env loop's n_env rows (Agent.store_transitions): packed into one pinned, fine-grained
+        // (host-coherent) block that the push kernel reads in place over the fabric: no copy call, no
+        // host wait (the block is reused once the event after its previous push kernel has passed)
+        const size_t fb = (size_t)n * D * 4;
         if (!e->push_pin) {
             DQNX_HIP_CHECK(hipHostMalloc((void**)&e->push_pin, (size_t)kPinnedPushRows * (8 * (size_t)D + 9) + 64,
-                                         hipHostMallocDefault));
+                                         hipHostMallocCoherent));
             DQNX_HIP_CHECK(hipEventCreateWithFlags(&e->push_ev, hipEventDisableTiming));
         }
         if (e->push_live) DQNX_HIP_CHECK(hipEventSynchronize(e->push_ev));
@@ -2933,12 +2933,12 @@ int dqnx_replay_push(dqnx_engine* e, const float* obs, const int32_t* act, const
         memcpy(h + 2 * fb, act, (size_t)n * 4);
         memcpy(h + 2 * fb + 4 * (size_t)n, rew, (size_t)n * 4);
         memcpy(h + 2 * fb + 8 * (size_t)n, done, (size_t)n);
-        char* d = e->arena + e->ws_stage;
-        DQNX_HIP_CHECK(hipMemcpyAsync(d, h, bytes, hipMemcpyHostToDevice, s));
+        rc = dqnx_replay_push(e, (const float*)h, (const int32_t*)(h + 2 * fb), (const float*)(h + 2 * fb + 4 * (size_t)n),
+                              (const uint8_t*)(h + 2 * fb + 8 * (size_t)n), (const float*)(h + fb), n, 1, stream);
+        if (rc) return rc;
         DQNX_HIP_CHECK(hipEventRecord(e->push_ev, s));
         e->push_live = true;
-        return dqnx_replay_push(e, (const float*)d, (const int32_t*)(d + 2 * fb), (const float*)(d + 2 * fb + 4 * (size_t)n),
-                                (const uint8_t*)(d + 2 * fb + 8 * (size_t)n), (const float*)(d + fb), n, 1, stream);
+        return DQNX_OK;
     }
     int done_rows = 0;
     while (done_rows < n) {
@@ -3869,8 +3869,19 @@ int dqnx_act_host(const dqnx_net_desc* net, const float* params, const float* ob
             pin = nullptr;
             pin_bytes = 0;
         }
-        DQNX_HIP_CHECK(hipHostMalloc((void**)&pin, want, hipHostMallocDefault));
+        DQNX_HIP_CHECK(hipHostMalloc((void**)&pin, want, hipHostMallocCoherent));
         pin_bytes = want;
+    }
+    if (net->kind == DQNX_NET_MLP) {
+        // one launch: the acting kernel reads the obs from and writes the actions to the pinned,
+        // fine-grained block in place (no copy calls), then one synchronisation
+        memcpy(pin, obs_host, (size_t)n * net->obs_dim * 4);
+        int32_t* pa = (int32_t*)(pin + (size_t)n * net->obs_dim * 4);
+        int rc = dqnx_act(net, params, (const float*)pin, n, pa, nullptr, scratch, scratch_bytes - ob - ab, stream);
+        if (rc) return rc;
+        DQNX_HIP_CHECK(hipStreamSynchronize(s));
+        memcpy(actions_host, pa, (size_t)n * 4);
+        return DQNX_OK;
     }
     memcpy(pin, obs_host, (size_t)n * net->obs_dim * 4);
     DQNX_HIP_CHECK(hipMemcpyAsync(d_obs, pin, (size_t)n * net->obs_dim * 4, hipMemcpyHostToDevice, s));
