@@ -436,6 +436,9 @@ struct dqnx_engine {
     int building_key = 0;                     // (the plan key steps_for is building)
     // drop-in Agent fast path (dqnx_agent_*, small host pushes): engine-owned pinned blocks + events
     uint32_t* ag_rng_pin = nullptr;           // [2][625] staged RNG states (alternating)
+    uint32_t* ag_rng_zc = nullptr;            // [625] fine-grained pinned block the sampler reads in place
+    bool ag_zc_launch = false;                // (set around the learn step of an agent launch)
+    bool ag_zc_used = false;                  // the block is read by an agent launch not yet known done
     hipEvent_t ag_rng_ev[2] = {nullptr, nullptr};
     bool ag_rng_live[2] = {false, false};
     int ag_slot = 0, ag_which = -1;
@@ -1347,6 +1350,9 @@ constexpr int KEY_RELAYOUT = 0x40;
 // 0 holds the minibatch the previous step drew); one more workgroup of the forward launch draws the
 // next step's minibatch into the staging slot 1, and the last launch copies it over slot 0
 constexpr int KEY_SAMPLE_NEXT = 0x80;
+// KEY_AGENT_RNG: the sampler launch draws from the drop-in Agent's pinned state block in place
+// (dqnx_agent_launch, uniform replay) instead of the control block an upload copy filled
+constexpr int KEY_AGENT_RNG = 0x4000;
 
 SampleArgs uniform_sample_args(dqnx_engine* e, int32_t* idx, int32_t* phys) {
     dqnx_ctrl* ctrl = ctrl_of(e);
@@ -1432,6 +1438,7 @@ std::vector<KStep> build_learn_steps(dqnx_engine* e, int key) {
         SampleArgs sa = uniform_sample_args(e, idx, phys);
         sa.rl = rl;
         sa.rl_blocks = rl_blocks;
+        if (key & KEY_AGENT_RNG) sa.state_in = e->ag_rng_zc;
         KStep k;
         k.name = "sample_uniform";
         k.bytes = 2.0 * 625 * 4 + 4.0 * e->Bs + 4.0 * Bl;
@@ -2814,6 +2821,7 @@ int dqnx_engine_destroy(dqnx_engine* e) {
         (void)hipEventDestroy(e->push_ev);
     }
     if (e->ag_rng_pin) (void)hipHostFree(e->ag_rng_pin);
+    if (e->ag_rng_zc) (void)hipHostFree(e->ag_rng_zc);
     if (e->ag_ctrl_pin) (void)hipHostFree(e->ag_ctrl_pin);
     if (e->push_pin) (void)hipHostFree(e->push_pin);
     delete e;
@@ -3177,7 +3185,8 @@ int dqnx_learn_step(dqnx_engine* e, int32_t flags, void* stream) {
     if (prefetch && inl) return learn_step_inlaunch(e, base, true, s);
     if (!prefetch && !e->pf_valid) {
         // the weights changed outside the Adam pass: this step's sampler launch rebuilds the copies
-        const int key = base | ((e->bwd_plan == 2 && (e->wblk_dirty || !blk_kept(e, base))) ? KEY_RELAYOUT : 0);
+        const int key = base | ((e->bwd_plan == 2 && (e->wblk_dirty || !blk_kept(e, base))) ? KEY_RELAYOUT : 0) |
+                        (e->ag_zc_launch ? KEY_AGENT_RNG : 0);
         const std::vector<KStep>& ks = steps_for(e, key);
         rc = run_graphed(e, key, s, [&](hipStream_t cs) { return enqueue_range(ks, 0, (int)ks.size(), cs); });
         if (!rc) e->wblk_dirty = !blk_kept(e, base);   // stale again after an update that does not keep them
@@ -3794,12 +3803,27 @@ int dqnx_agent_launch(dqnx_engine* e, int32_t flags, void* stream) {
     if (e->ag_which < 0) return set_error(DQNX_ESTATE, "dqnx_agent_launch without a staged RNG state");
     hipStream_t s = (hipStream_t)stream;
     const int i = e->ag_slot;
-    uint32_t* dst = e->ag_which == DQNX_RNG_PY ? ctrl_of(e)->py_mt : ctrl_of(e)->np_mt;
-    DQNX_HIP_CHECK(hipMemcpyAsync(dst, e->ag_rng_pin + 625 * i, 625 * 4, hipMemcpyHostToDevice, s));
-    DQNX_HIP_CHECK(hipEventRecord(e->ag_rng_ev[i], s));
-    e->ag_rng_live[i] = true;
-    rc = dqnx_learn_step(e, flags & (DQNX_STEP_SOFT_UPDATE | DQNX_STEP_GRADS_ONLY), stream);
-    if (rc) return rc;
+    // uniform replay, no draw pending: the sampler launch reads the staged state in place from a
+    // fine-grained pinned block (no upload copy call); other configurations upload it into ctrl
+    const bool zc = e->ag_which == DQNX_RNG_PY && !e->pf_valid && e->cfg.algo != DQNX_ALGO_PER_DOUBLE &&
+                    route_knob("DQNX_AGENT_ZC", 1) != 0;
+    if (zc) {
+        if (!e->ag_rng_zc) DQNX_HIP_CHECK(hipHostMalloc((void**)&e->ag_rng_zc, 625 * 4, hipHostMallocCoherent));
+        if (e->ag_zc_used) DQNX_HIP_CHECK(hipEventSynchronize(e->ag_ctrl_ev));   // its last reader has run
+        memcpy(e->ag_rng_zc, e->ag_rng_pin + 625 * i, 625 * 4);
+        e->ag_zc_launch = true;
+        rc = dqnx_learn_step(e, flags & (DQNX_STEP_SOFT_UPDATE | DQNX_STEP_GRADS_ONLY), stream);
+        e->ag_zc_launch = false;
+        if (rc) return rc;
+        e->ag_zc_used = true;
+    } else {
+        uint32_t* dst = e->ag_which == DQNX_RNG_PY ? ctrl_of(e)->py_mt : ctrl_of(e)->np_mt;
+        DQNX_HIP_CHECK(hipMemcpyAsync(dst, e->ag_rng_pin + 625 * i, 625 * 4, hipMemcpyHostToDevice, s));
+        DQNX_HIP_CHECK(hipEventRecord(e->ag_rng_ev[i], s));
+        e->ag_rng_live[i] = true;
+        rc = dqnx_learn_step(e, flags & (DQNX_STEP_SOFT_UPDATE | DQNX_STEP_GRADS_ONLY), stream);
+        if (rc) return rc;
+    }
     if (!e->ag_ctrl_pin) {
         DQNX_HIP_CHECK(hipHostMalloc((void**)&e->ag_ctrl_pin, sizeof(dqnx_ctrl), hipHostMallocDefault));
         DQNX_HIP_CHECK(hipEventCreateWithFlags(&e->ag_ctrl_ev, hipEventDisableTiming));

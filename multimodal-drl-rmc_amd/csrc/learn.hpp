@@ -281,7 +281,9 @@ struct PushArgs {
 };
 
 struct SampleArgs {
-    uint32_t* state;          // [625]
+    uint32_t* state;          // [625] the advanced state is written here
+    const uint32_t* state_in; // [625] the state drawn from, when not `state` (null: `state`): the drop-in
+                              // Agent's pinned fine-grained host block, read in place (no upload copy)
     const int64_t* n_dev;     // population size from device (ring size) or null
     int64_t n_val;
     int32_t k;

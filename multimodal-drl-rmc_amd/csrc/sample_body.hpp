@@ -71,8 +71,9 @@ __device__ __forceinline__ void sample_uniform_body(const SampleArgs& a, SampleL
         phys_base = wptr - n;
         if (phys_base < 0) phys_base += a.capacity;
     }
-    for (int j = tid; j < 624; j += NT) blk[0][j] = a.state[j];
-    uint32_t pos = a.state[624];
+    const uint32_t* src = a.state_in ? a.state_in : a.state;
+    for (int j = tid; j < 624; j += NT) blk[0][j] = src[j];
+    uint32_t pos = src[624];
 
     if (n <= a.setsize) {
         // ---- pool branch: one lane, CPython order (only while the buffer is tiny) ----
@@ -224,7 +225,7 @@ __device__ __forceinline__ void sample_uniform_body(const SampleArgs& a, SampleL
             const int wf = s_final;
             const int bf = (wf < avail) ? 0 : 1 + (wf - avail) / 624;
             const uint32_t nx = (uint32_t)((wf < avail) ? (int)pos + wf + 1 : (wf - avail) % 624 + 1);
-            if (bf > 0)
+            if (bf > 0 || a.state_in)   // (drawn from state_in: `state` does not hold block 0 yet)
                 for (int j = tid; j < 624; j += NT) a.state[j] = blk[bf][j];
             if (tid == 0) a.state[624] = nx;
             break;

@@ -96,8 +96,9 @@ __device__ __forceinline__ bool sample_fast_path(const SampleArgs& a, SampleFast
     // feeds to a scalar gets waited for right there, serialising the round trips
     const int64_t n = gld(a.n_dev);
     const int64_t wptr = gld(a.wptr_dev);
-    const uint32_t st_j = gld(a.state + (tid < 624 ? tid : 624));
-    const int pos = (int)gld(a.state + 624);
+    const uint32_t* src = a.state_in ? a.state_in : a.state;
+    const uint32_t st_j = gld(src + (tid < 624 ? tid : 624));
+    const int pos = (int)gld(src + 624);
     const int k = a.k;
     // the MT block cache (learn.hpp), fetched speculatively with the state: word f = tid + 1024 i
     // of the cached blocks (block f / 624, offset f % 624); block 0 must equal the state block
@@ -304,7 +305,7 @@ __device__ __forceinline__ bool sample_fast_path(const SampleArgs& a, SampleFast
     if (gfinal >= 0) {   // this wave: the state after the k-th draw (its block, index just past it)
         const int bf = (gfinal < avail) ? 0 : 1 + (gfinal - avail) / 624;
         const uint32_t nx = (uint32_t)((gfinal < avail) ? pos + gfinal + 1 : (gfinal - avail) - 624 * (bf - 1) + 1);
-        if (bf > 0)
+        if (bf > 0 || a.state_in)   // (drawn from state_in: `state` does not hold block 0 yet)
             for (int j = lane; j < 624; j += 64) a.state[j] = S.blk[bf][j];
         if (lane == 0) a.state[624] = nx;
         if (a.mtc_blocks > 0) {   // the cache for the next call: the new state block and the successors twisted here

@@ -195,9 +195,12 @@ def test_gpu_agent_deferred_learn_bit_identical(tmp_path, monkeypatch, algo, sof
     in-place staging of random._inst (dqnx_agent_learn_mt) bitwise the portable getstate / getrandbits
     hand-off (DQNX_AGENT_MT_INPLACE=0)."""
     runs = []
-    for defer, inplace in (("0", "1"), ("1", "1"), ("0", "0")):   # (+ the portable getstate/getrandbits path)
+    # (+ the portable getstate / getrandbits hand-off, and the RNG upload copy instead of the sampler
+    #  reading the pinned block in place)
+    for defer, inplace, zc in (("0", "1", "1"), ("1", "1", "1"), ("0", "0", "1"), ("0", "1", "0")):
         monkeypatch.setenv("DQNX_AGENT_DEFER", defer)
         monkeypatch.setenv("DQNX_AGENT_MT_INPLACE", inplace)
+        monkeypatch.setenv("DQNX_AGENT_ZC", zc)
         torch.manual_seed(5)
         agent = getattr(Agents, algo)(**agent_kwargs(algo, 284, 64, 1000, tmp_path, target_soft_update=soft,
                                                      update_target_frequency=3))
