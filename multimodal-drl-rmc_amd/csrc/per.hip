@@ -34,7 +34,10 @@ constexpr int PER_NT = 1024;   // threads of the one-workgroup tracking kernel (
 // ---------------------------------------------------------------------------------------
 constexpr int PER_SNT = 256;     // samples (threads) per sampling workgroup: the descents' scattered
                                  // loads are texture-path bound, so spread them over more CUs
-constexpr int PER_STOP = 8191;   // nodes of depth <= 12 (64 KiB of float64) cached per workgroup
+#ifndef DQNX_PER_STOP
+#define DQNX_PER_STOP 8191
+#endif
+constexpr int PER_STOP = DQNX_PER_STOP;   // nodes of depth <= 12 (64 KiB of float64) cached per workgroup
 constexpr int PER_LA = 4;        // tree levels fetched per dependent global round trip
 
 // the chosen subtree's half of the first N nodes of a level fetched ahead:
