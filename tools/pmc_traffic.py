@@ -28,6 +28,7 @@ NAMES = [   # (substring of the HIP kernel name, bench step name); the first mat
     ("k_head<", "head_td_loss"),
     ("k_bwd_level<", "dw_all"),
     ("k_dw_adam16", "dw_adam16"),
+    ("k_dw_bf16", "dw_all"),
     ("k_adam", "adam_fused"),
     ("k_per_sample", "per_sample"),
     ("k_per_update", "per_update"),
