@@ -1001,7 +1001,11 @@ void build_fused_steps(dqnx_engine* e, int flags, int32_t* idx, int32_t* phys, s
             const int wgs = fa.tiles * nstreams + 1;
             fa.samp_shape = sample_next->k <= 2048 ? 1 : (wgs <= e->n_cu ? 3 : 2);
             fa.samp = *sample_next;
+#ifdef DQNX_STAMPS
+            fa.samp.stamps = at<int64_t>(e, e->ws_stamps);   // (diagnostic builds: the sampler's slots 0-15)
+#else
             fa.samp.stamps = nullptr;
+#endif
         }
         KStep k;
         k.name = sample_next ? "mlp_fwd+sample" : "mlp_fwd";
@@ -1261,8 +1265,8 @@ void build_fused_steps(dqnx_engine* e, int flags, int32_t* idx, int32_t* phys, s
                 da.pf_phys_src = sample_next->phys_out;
                 da.pf_phys_dst = phys;
                 da.pf_nphys = e->Bl;
-                da.mtc = nullptr;   // the forward's sampler body draws from the MT state itself
-                da.mtc_blocks = 0;
+                // (da.mtc kept: the extension workgroup twists the next draw's MT blocks ahead for the
+                // forward's sampler body, which reads them from the cache instead of twisting)
             }
             if (per_fused) {
                 da.pprop = pua;
@@ -1318,8 +1322,7 @@ void build_fused_steps(dqnx_engine* e, int flags, int32_t* idx, int32_t* phys, s
             aa.pf_phys_src = sample_next->phys_out;
             aa.pf_phys_dst = phys;
             aa.pf_nphys = e->Bl;
-            aa.mtc = nullptr;   // the forward's sampler body draws from the MT state itself
-            aa.mtc_blocks = 0;
+            // (aa.mtc kept: the forward's sampler body reads the blocks its extension twists ahead)
             fill_blk_layers(e, aa, true);   // ... and the next step has no sampler launch to rebuild them
             if (per_track) {
                 aa.pprop = pua;
@@ -2417,6 +2420,10 @@ int enqueue_apply(dqnx_engine* e, int flags, hipStream_t s) {
         if (prop_in_adam) {
             da.pprop = pua;
             da.pprop_wgs = (e->Bg + 511) / 512;
+        }
+        if (e->mtc_blocks > 0 && !prop_in_adam) {   // the next step's in-forward draw reads its MT blocks from the cache
+            da.mtc = at<uint32_t>(e, e->ws_mtc);
+            da.mtc_blocks = e->mtc_blocks;
         }
         return launch_dw_adam16(da, s);
     }

@@ -117,6 +117,25 @@ __device__ __forceinline__ void sample_uniform_body(const SampleArgs& a, SampleL
     int accepted = 0;
     uint32_t spos0 = 0;      // stream position (since the call began) of blk[0][pos]
     int iter = 0;
+    // The MT block cache (a.mtc, sample_pipe.hpp's layout: [0] blocks held, [64 + 624 b + o] block b,
+    // block 0 = a state block): successors twisted ahead by an earlier launch (the update launch's
+    // extension workgroup, or the previous call's own blocks).  Used only when its block 0 is this
+    // call's state block; then the passes copy cached blocks instead of twisting them.
+    int cache_next = 1, cache_left = 0;
+    if (a.mtc && a.mtc_blocks > 0) {
+        const int cnt = (int)a.mtc[0];
+        bool mis = cnt < 2 || cnt > MTC_MAX_BLOCKS;   // (one block alone saves no twist: skip the compare)
+        for (int j = tid; j < 624 && !mis; j += NT) mis = a.mtc[64 + j] != blk[0][j];   // (this thread's own words)
+        // block-wide OR through the wave totals (no __syncthreads_or: it takes static LDS, which the
+        // forward launch's 150 KB dynamic request leaves no room for)
+        const unsigned long long wb = __ballot(mis);
+        if (lane == 0) wave_tot[wid] = wb ? 1 : 0;
+        __syncthreads();
+        int any = 0;
+#pragma unroll
+        for (int w = 0; w < NW; w++) any |= wave_tot[w];
+        cache_left = any ? 0 : cnt - 1;
+    }
     __syncthreads();
     while (true) {
         // ---- plan the pass: the rest of blk[0], then nb freshly twisted blocks ----
@@ -129,7 +148,29 @@ __device__ __forceinline__ void sample_uniform_body(const SampleArgs& a, SampleL
         nb = nb > room ? room : nb;
         nb = nb > AHEAD ? AHEAD : nb;
         nb = nb < (avail == 0 ? 1 : 0) ? 1 : nb;
-        for (int j = 1; j <= nb; j++) mt_twist_into(blk[j - 1], blk[j]);
+        {
+            // cached blocks first: every load of them in flight at once (one round trip), then the stores
+            const int nc = nb < cache_left ? nb : cache_left;
+            if (nc > 0) {
+                constexpr int CW = (AHEAD * 624 + NT - 1) / NT;   // cached words per thread, at most
+                uint32_t cv[CW];
+                const uint32_t* src = a.mtc + 64 + 624 * cache_next;
+#pragma unroll
+                for (int u = 0; u < CW; u++) {
+                    const int f = tid + u * NT;
+                    cv[u] = f < nc * 624 ? src[f] : 0u;
+                }
+#pragma unroll
+                for (int u = 0; u < CW; u++) {
+                    const int f = tid + u * NT;
+                    if (f < nc * 624) blk[1 + f / 624][f % 624] = cv[u];
+                }
+                cache_next += nc;
+                cache_left -= nc;
+                __syncthreads();
+            }
+            for (int j = nc + 1; j <= nb; j++) mt_twist_into(blk[j - 1], blk[j]);   // each ends with a barrier
+        }
         if (iter == 0) DQNX_STAMP(a.stamps, 2);
         const int nwords = avail + 624 * nb;
         // ---- insert: thread t owns the contiguous words [t*m, t*m + m) of the pass ----
@@ -228,6 +269,11 @@ __device__ __forceinline__ void sample_uniform_body(const SampleArgs& a, SampleL
             if (bf > 0 || a.state_in)   // (drawn from state_in: `state` does not hold block 0 yet)
                 for (int j = tid; j < 624; j += NT) a.state[j] = blk[bf][j];
             if (tid == 0) a.state[624] = nx;
+            if (a.mtc && a.mtc_blocks > 0) {   // the cache for the next call: the new state block + its successors here
+                const int keep = min(nb - bf + 1, a.mtc_blocks);
+                for (int f = tid; f < keep * 624; f += NT) a.mtc[64 + f] = blk[bf + f / 624][f % 624];
+                if (tid == 0) a.mtc[0] = (uint32_t)keep;
+            }
             break;
         }
         // the whole pass was consumed: continue from the last block's end
