@@ -1377,6 +1377,7 @@ SampleArgs uniform_sample_args(dqnx_engine* e, int32_t* idx, int32_t* phys) {
     sa.gtab = sample_table_bytes(e->Bs) ? at<unsigned long long>(e, e->ws_gtab) : nullptr;
     sa.mtc = at<uint32_t>(e, e->ws_mtc);
     sa.mtc_blocks = e->mtc_blocks;
+    sa.bm_cap = route_knob("DQNX_SAMPLER_BM_CAP", 0);
     return sa;
 }
 

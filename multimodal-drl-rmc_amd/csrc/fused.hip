@@ -344,7 +344,7 @@ __global__ __launch_bounds__(FT) void k_mlp_fwd(FusedFwdArgs a) {
         do {                                                                                         \
             constexpr int AH = fwd_sample_ahead(SH);                                                 \
             static_assert(sizeof(SampleLdsBase<FT, AH>) <= (size_t)fwd_sample_tab_off(SH), "layout"); \
-            sample_uniform_body<FT, fwd_sample_hs(SH), AH>(                                          \
+            sample_uniform_body<FT, fwd_sample_hs(SH), AH, fwd_sample_bmx(SH)>(                                          \
                 a.samp, *reinterpret_cast<SampleLdsBase<FT, AH>*>(lds),                               \
                 reinterpret_cast<unsigned long long*>(reinterpret_cast<char*>(lds) + fwd_sample_tab_off(SH))); \
         } while (0)

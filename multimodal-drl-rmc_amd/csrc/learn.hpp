@@ -303,6 +303,9 @@ struct SampleArgs {
     int test_flags;           // tests only (DQNX_SAMPLER_FORCE_FALLBACK): 1 = take the fast path's fallback
     uint32_t* mtc;            // MT block cache (mt_cache_words), or null: [0] = blocks held, [64 + 624 b + o]
     int mtc_blocks;           // blocks the cache is kept at (the state's block + its successors)
+    int bm_cap;               // bitmap first pass (hosts with a repeat table): repeated words it takes
+                              // before falling back to the hash table; 0 = half the table, < 0 = off
+                              // (tests: DQNX_SAMPLER_BM_CAP)
 };
 // Fused plan (fp32): every weight gradient over the FULL minibatch on 16 x 16 parameter tiles,
 // then Adam, the soft update and the fragment-blocked weight copies of the tile, in one launch
@@ -495,7 +498,9 @@ struct FusedFwdArgs {
 //   2: k <= FWD_SAMPLE_MAX_K, passes of 3 blocks into 8192 slots (72 KB: two forward workgroups per
 //      CU still fit, for grids larger than the chip);
 //   3: k <= FWD_SAMPLE_MAX_K, ONE pass of 9 blocks into 16384 slots (150 KB: one workgroup per CU,
-//      only when the forward's grid leaves a CU idle), so k = 4096 takes one pass instead of three
+//      only when the forward's grid leaves a CU idle), so k = 4096 takes one pass instead of three;
+//      the same 128 KB serve as an exact 2^20-bit "seen" bitmap for a first pass with n <= 2^20
+//      (+ a 512-slot table for the repeated values, sample_body.hpp)
 constexpr int FWD_SAMPLE_MAX_K = 4608;
 constexpr int MICRO_SAMPLE_MAX_K = 2048;   // k_micro_fwd's sampler workgroup (256 threads, 4096 slots)
 __host__ __device__ constexpr int fwd_sample_ahead(int shape) { return shape == 3 ? 8 : 2; }
@@ -504,7 +509,10 @@ __host__ __device__ constexpr int fwd_sample_hs(int shape) { return shape == 1 ?
 __host__ __device__ constexpr int fwd_sample_tab_off(int shape) {
     return (((fwd_sample_ahead(shape) + 1) * 624 + 16) * 4 + 63) / 64 * 64;
 }
-__host__ __device__ constexpr int fwd_sample_lds_bytes(int shape) { return fwd_sample_tab_off(shape) + 8 * fwd_sample_hs(shape); }
+__host__ __device__ constexpr int fwd_sample_bmx(int shape) { return shape == 3 ? 512 : 0; }   // repeat-table slots
+__host__ __device__ constexpr int fwd_sample_lds_bytes(int shape) {
+    return fwd_sample_tab_off(shape) + 8 * fwd_sample_hs(shape) + (fwd_sample_bmx(shape) ? 8 * fwd_sample_bmx(shape) + 64 : 0);
+}
 struct HeadBwdArgs {
     int L, Bl, A, NH, F, head_kind, algo;
     int nsplit;                  // workgroups per 16-sample tile (split the last dZ's columns)

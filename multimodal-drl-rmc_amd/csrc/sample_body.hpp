@@ -48,7 +48,8 @@ struct SampleLds : SampleLdsBase<NT> {
 };
 
 // `tab`: HS slots in LDS, or (k too large for LDS) in global memory, used by this one workgroup
-template <int NT, int HS, int AH = sample_default_ahead<NT>()>
+// BMX > 0: `tab` is followed by a BMX-slot repeat table and a counter (the bitmap first pass)
+template <int NT, int HS, int AH = sample_default_ahead<NT>(), int BMX = 0>
 __device__ __forceinline__ void sample_uniform_body(const SampleArgs& a, SampleLdsBase<NT, AH>& S,
                                                     unsigned long long* tab) {
     constexpr int NW = NT / 64, AHEAD = SampleShape<NT, AH>::AHEAD, WPT = SampleShape<NT, AH>::WPT;
@@ -111,6 +112,16 @@ __device__ __forceinline__ void sample_uniform_body(const SampleArgs& a, SampleL
         for (int i = 0; i < HS / NT; i++) tab[tid + i * NT] = ~0ull;
         __threadfence_block();
     }
+    if constexpr (BMX > 0) {
+        for (int i = tid; i < BMX; i += NT) tab[HS + i] = ~0ull;
+        if (tid == 0) *reinterpret_cast<int*>(tab + HS + BMX) = 0;
+    }
+    // the bitmap first pass: values fit the table's bits, and few repeats expected (~nwords^2 / 2n
+    // pairs: n >= 32 k keeps them well under the repeat table's half)
+    const bool bm_ok = BMX > 0 && a.bm_cap >= 0 && n <= (int64_t)HS * 64 && n >= 32ll * k;
+    const int bm_cap = (a.bm_cap > 0 && a.bm_cap < BMX / 2) ? a.bm_cap : BMX / 2;
+    (void)bm_ok;
+    (void)bm_cap;
     const int bits = bit_length64((uint64_t)n);
     const uint32_t shift = 32u - (uint32_t)bits;
     const float inv_accept = (float)((double)(1ull << bits) / (double)n);   // words per valid draw
@@ -176,25 +187,109 @@ __device__ __forceinline__ void sample_uniform_body(const SampleArgs& a, SampleL
         // ---- insert: thread t owns the contiguous words [t*m, t*m + m) of the pass ----
         const int m = (nwords + NT - 1) / NT;
         uint32_t cv[WPT], hv[WPT];
-        bool val[WPT];
-        unsigned long long prev[WPT];
+        bool val[WPT], first[WPT];
 #pragma unroll
-        for (int u = 0; u < WPT; u++) {   // first probe of every word, issued back to back
+        for (int u = 0; u < WPT; u++) {   // the candidates (tempered, scaled, range-checked)
             const int w = tid * m + u;
             val[u] = false;
             cv[u] = 0;
             hv[u] = 0;
-            prev[u] = ~0ull;
             if (u < m && w < nwords) {
                 const int bw = (w < avail) ? 0 : 1 + (w - avail) / 624;
                 const int ow = (w < avail) ? (int)pos + w : (w - avail) % 624;
                 const uint32_t c = mt_temper(blk[bw][ow]) >> shift;
-                if ((int64_t)c < n) {   // insert (value, stream position); earliest position wins
-                    val[u] = true;
-                    cv[u] = c;
-                    hv[u] = hash_u32(c) & (HS - 1);
-                    prev[u] = atomicCAS(&tab[hv[u]], ~0ull, ((unsigned long long)c << 32) | (spos0 + (uint32_t)w));
+                val[u] = (int64_t)c < n;
+                cv[u] = c;
+            }
+        }
+        bool hashed = true;
+        if constexpr (BMX > 0) {
+            if (bm_ok && iter == 0) {
+                // Bitmap first pass: bit c of the cleared table (all ones) is cleared by the first
+                // word of value c to arrive; a word that finds it cleared repeats a value, and only
+                // such words (then the words whose value they repeat) meet in the exact repeat table,
+                // where the earliest stream position wins.  32-bit LDS atomics on ~k words instead
+                // of 64-bit compare-and-swaps.
+                uint32_t* bm = reinterpret_cast<uint32_t*>(tab);
+                unsigned long long* xt = tab + HS;
+                int* xn = reinterpret_cast<int*>(tab + HS + BMX);
+                bool xc[WPT];
+                uint32_t old[WPT];
+                DQNX_STAMP(a.stamps, 7);
+#pragma unroll
+                for (int u = 0; u < WPT; u++) {   // branch-free, so every atomic is in flight at once
+                    const uint32_t bit = 1u << (cv[u] & 31u);   // (no word: an all-ones AND of a pad word)
+                    uint32_t* p = val[u] ? &bm[cv[u] >> 5] : reinterpret_cast<uint32_t*>(xn + 1);
+                    old[u] = atomicAnd(p, val[u] ? ~bit : ~0u);
                 }
+#pragma unroll
+                for (int u = 0; u < WPT; u++) xc[u] = val[u] && (old[u] & (1u << (cv[u] & 31u))) == 0u;
+                DQNX_STAMP(a.stamps, 8);
+#pragma unroll
+                for (int u = 0; u < WPT; u++) {
+                    if (!xc[u] || atomicAdd(xn, 1) >= bm_cap) continue;
+                    const unsigned long long key = ((unsigned long long)cv[u] << 32) | (spos0 + (uint32_t)(tid * m + u));
+                    uint32_t h = hash_u32(cv[u]) & (BMX - 1);
+                    while (true) {   // (at most bm_cap <= BMX / 2 values: an empty slot exists)
+                        const unsigned long long pv = atomicCAS(&xt[h], ~0ull, key);
+                        if (pv == ~0ull) break;
+                        if ((uint32_t)(pv >> 32) == cv[u]) { atomicMin(&xt[h], key); break; }
+                        h = (h + 1) & (BMX - 1);
+                    }
+                    hv[u] = h;
+                }
+                DQNX_STAMP(a.stamps, 9);
+                __syncthreads();
+                const int nx = *xn;
+                DQNX_STAMP(a.stamps, 10);
+                if (nx <= bm_cap) {
+                    hashed = false;
+                    if (nx > 0) {
+                        unsigned long long t[WPT];
+                        uint32_t hp[WPT];
+#pragma unroll
+                        for (int u = 0; u < WPT; u++) {   // every first probe in flight at once
+                            hp[u] = hash_u32(cv[u]) & (BMX - 1);
+                            t[u] = xt[hp[u]];
+                        }
+#pragma unroll
+                        for (int u = 0; u < WPT; u++) {   // the first-arrived words of the repeated values
+                            if (!val[u] || xc[u]) continue;
+                            uint32_t h = hp[u];
+                            while (t[u] != ~0ull && (uint32_t)(t[u] >> 32) != cv[u]) {
+                                h = (h + 1) & (BMX - 1);
+                                t[u] = xt[h];
+                            }
+                            if (t[u] == ~0ull) continue;
+                            xc[u] = true;
+                            hv[u] = h;
+                            atomicMin(&xt[h], ((unsigned long long)cv[u] << 32) | (spos0 + (uint32_t)(tid * m + u)));
+                        }
+                    }
+                    DQNX_STAMP(a.stamps, 11);
+#ifdef DQNX_STAMPS
+                    if (a.stamps && tid == 0) a.stamps[13] = 1000 + nx;   // (diagnostic: the bitmap pass ran, nx repeats)
+#endif
+                    if (tid == 0) s_final = -1;
+                    __syncthreads();
+                    if (iter == 0) DQNX_STAMP(a.stamps, 3);
+#pragma unroll
+                    for (int u = 0; u < WPT; u++)
+                        first[u] = val[u] && (!xc[u] || (uint32_t)(xt[hv[u]] & 0xffffffffull) == spos0 + (uint32_t)(tid * m + u));
+                } else {   // more repeats than the table takes: this pass on the hash table
+                    for (int i = tid; i < HS; i += NT) tab[i] = ~0ull;
+                    __syncthreads();
+                }
+            }
+        }
+        if (hashed) {
+        unsigned long long prev[WPT];
+#pragma unroll
+        for (int u = 0; u < WPT; u++) {   // first probe of every word, issued back to back
+            prev[u] = ~0ull;
+            if (val[u]) {   // insert (value, stream position); earliest position wins
+                hv[u] = hash_u32(cv[u]) & (HS - 1);
+                prev[u] = atomicCAS(&tab[hv[u]], ~0ull, ((unsigned long long)cv[u] << 32) | (spos0 + (uint32_t)(tid * m + u)));
             }
         }
 #pragma unroll
@@ -215,16 +310,17 @@ __device__ __forceinline__ void sample_uniform_body(const SampleArgs& a, SampleL
         __syncthreads();
         if (iter == 0) DQNX_STAMP(a.stamps, 3);
         // ---- first occurrences, exclusive scan in stream (= thread, then u) order ----
-        int cnt = 0;
-        bool first[WPT];
 #pragma unroll
         for (int u = 0; u < WPT; u++) {
             // (an agent-scope load: a global table's lines must come from L2, where the atomics ran)
             const unsigned long long tv =
                 val[u] ? __hip_atomic_load(&tab[hv[u]], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
             first[u] = val[u] && (uint32_t)(tv & 0xffffffffull) == spos0 + (uint32_t)(tid * m + u);
-            cnt += first[u] ? 1 : 0;
         }
+        }
+        int cnt = 0;
+#pragma unroll
+        for (int u = 0; u < WPT; u++) cnt += first[u] ? 1 : 0;
         int incl = cnt;   // wave inclusive scan
 #pragma unroll
         for (int o = 1; o < 64; o <<= 1) {
@@ -277,6 +373,18 @@ __device__ __forceinline__ void sample_uniform_body(const SampleArgs& a, SampleL
             break;
         }
         // the whole pass was consumed: continue from the last block's end
+        if (!hashed) {   // the next passes dedup on the hash table, seeded with this pass's first words
+            for (int i = tid; i < HS; i += NT) tab[i] = ~0ull;
+            __syncthreads();
+#pragma unroll
+            for (int u = 0; u < WPT; u++) {
+                if (!first[u]) continue;
+                const unsigned long long key = ((unsigned long long)cv[u] << 32) | (spos0 + (uint32_t)(tid * m + u));
+                uint32_t h = hash_u32(cv[u]) & (HS - 1);
+                while (atomicCAS(&tab[h], ~0ull, key) != ~0ull) h = (h + 1) & (HS - 1);
+            }
+            __syncthreads();
+        }
         spos0 += (uint32_t)nwords;
         if (nb > 0) {
             for (int j = tid; j < 624; j += NT) blk[0][j] = blk[nb][j];

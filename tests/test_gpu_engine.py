@@ -503,6 +503,44 @@ def test_gpu_prefetch_dp_shard_step_bit_identical(world, k):
     assert np.array_equal(e1.get_rng(0), e2.get_rng(0))
 
 
+@pytest.mark.parametrize("world,n,cap", [(8, 260000, None), (4, 260000, None), (8, 150000, None),
+                                         (8, 260000, "2"), (8, 260000, "-1")])
+def test_gpu_prefetch_bitmap_first_pass_bit_identical(monkeypatch, world, n, cap):
+    """The in-forward draw's bitmap first pass (one-pass shape, n <= 2^20 and n >= 32 k): exact
+    "seen" bits plus the repeat table give the same positions and RNG state as the sampler launch,
+    bitwise.  n = 260000: one pass; n = 150000: 1.75 words per draw, so the draw continues on the
+    hash table seeded from the first pass; DQNX_SAMPLER_BM_CAP=2: more repeats than the cap, the
+    pass redone on the hash table; -1: the bitmap pass off."""
+    if cap is not None:
+        monkeypatch.setenv("DQNX_SAMPLER_BM_CAP", cap)
+    E = _engine_mod()
+    k = 4096
+    ospec = O.mlp_spec(32, 8, "dueling")
+    init = O.reference_init(ospec, 43)
+    data = O.synth_transitions(n, 32, 8, seed=143)
+    engines = []
+    for _ in range(2):
+        eng = E.LearnEngine(E.mlp_spec(32, 8, "dueling"), "DuelingDoubleDQNAgent", k, n,
+                            world_size=world, rank=0)
+        eng.load_params(init)
+        eng.push(*data)
+        random.seed(49)
+        eng.set_rng(0, O.py_state_to_array())
+        engines.append(eng)
+    e1, e2 = engines
+    for i in range(4):
+        e1.learn_step(grads_only=True)
+        e1.apply_grads(soft_update=True)
+        e2.learn_step(grads_only=True, prefetch=i < 3)
+        e2.apply_grads(soft_update=True)
+    torch.cuda.synchronize()
+    e1.check_device_error()
+    e2.check_device_error()
+    assert torch.equal(e1.grads, e2.grads)
+    assert torch.equal(e1.params, e2.params) and torch.equal(e1.target_params, e2.target_params)
+    assert np.array_equal(e1.get_rng(0), e2.get_rng(0))
+
+
 @pytest.mark.parametrize("algo,batch", [("DuelingDoubleDQNAgent", 1024), ("DQNAgent", 200),
                                         ("PerDuelingDoubleDQNAgent", 512)])
 def test_gpu_dw16_row_pair_tiles_bit_identical(monkeypatch, algo, batch):

@@ -27,7 +27,10 @@ for step in range(8):
     s = list(out)
     body = ["state+clear", "twists", "insert", "scan", "out+pass"]
     print(f"step {step}: in-forward sampler total {s[15] - s[0]} cyc: "
-          + ", ".join(f"{body[j]} {s[j + 1] - s[j]}" for j in range(5)) + f", rest {s[15] - s[5]}")
+          + ", ".join(f"{body[j]} {s[j + 1] - s[j]}" for j in range(5)) + f", rest {s[15] - s[5]}"
+          + (f" [bitmap pass, {s[13] - 1000} repeats: temper {s[7] - s[2]}, atomics {s[8] - s[7]}, "
+             f"repeat inserts {s[9] - s[8]}, barrier {s[10] - s[9]}, probes {s[11] - s[10]}, barrier {s[3] - s[11]}]"
+             if 1000 <= s[13] < 2000 else ""))
 eng.learn_step(grads_only=True)
 eng.apply_grads(soft_update=True)
 torch.cuda.synchronize()
