@@ -1378,6 +1378,7 @@ SampleArgs uniform_sample_args(dqnx_engine* e, int32_t* idx, int32_t* phys) {
     sa.mtc = at<uint32_t>(e, e->ws_mtc);
     sa.mtc_blocks = e->mtc_blocks;
     sa.bm_cap = route_knob("DQNX_SAMPLER_BM_CAP", 0);
+    sa.bm_rolled = route_knob("DQNX_SAMPLER_ROLLED", 0);
     return sa;
 }
 

@@ -306,6 +306,7 @@ struct SampleArgs {
     int bm_cap;               // bitmap first pass (hosts with a repeat table): repeated words it takes
                               // before falling back to the hash table; 0 = half the table, < 0 = off
                               // (tests: DQNX_SAMPLER_BM_CAP)
+    int bm_rolled;            // the bitmap pass in rolled loops (DQNX_SAMPLER_ROLLED, 0/1)
 };
 // Fused plan (fp32): every weight gradient over the FULL minibatch on 16 x 16 parameter tiles,
 // then Adam, the soft update and the fragment-blocked weight copies of the tile, in one launch

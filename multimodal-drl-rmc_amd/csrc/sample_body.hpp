@@ -53,6 +53,7 @@ template <int NT, int HS, int AH = sample_default_ahead<NT>(), int BMX = 0>
 __device__ __forceinline__ void sample_uniform_body(const SampleArgs& a, SampleLdsBase<NT, AH>& S,
                                                     unsigned long long* tab) {
     constexpr int NW = NT / 64, AHEAD = SampleShape<NT, AH>::AHEAD, WPT = SampleShape<NT, AH>::WPT;
+    static_assert(BMX == 0 || WPT <= 32, "the rolled bitmap pass keeps a thread's words in 32-bit masks");
     auto& blk = S.blk;
     int* wave_tot = S.wave_tot;
     int& s_final = S.s_final;
@@ -186,25 +187,106 @@ __device__ __forceinline__ void sample_uniform_body(const SampleArgs& a, SampleL
         const int nwords = avail + 624 * nb;
         // ---- insert: thread t owns the contiguous words [t*m, t*m + m) of the pass ----
         const int m = (nwords + NT - 1) / NT;
+        auto word_of = [&](int u, uint32_t& c) -> bool {   // word u of this thread: a valid candidate?
+            const int w = tid * m + u;
+            if (u >= m || w >= nwords) return false;
+            const int bw = (w < avail) ? 0 : 1 + (w - avail) / 624;
+            const int ow = (w < avail) ? (int)pos + w : (w - avail) % 624;
+            c = mt_temper(blk[bw][ow]) >> shift;
+            return (int64_t)c < n;
+        };
         uint32_t cv[WPT], hv[WPT];
         bool val[WPT], first[WPT];
+        bool hashed = true;
+        // Rolled bitmap pass (a.bm_rolled): the same algorithm as the unrolled one below, with the
+        // per-word flags in bit masks and the values recomputed from the LDS blocks, so the code the
+        // workgroup runs once per launch stays a few hundred bytes (every instruction of this
+        // workgroup is fetched cold: the forward's other workgroups run other code).
+        bool rolled = false;
+        uint32_t fmask = 0;
+        if constexpr (BMX > 0) {
+            if (bm_ok && iter == 0 && a.bm_rolled) {
+                uint32_t* bm = reinterpret_cast<uint32_t*>(tab);
+                unsigned long long* xt = tab + HS;
+                int* xn = reinterpret_cast<int*>(tab + HS + BMX);
+                uint32_t vmask = 0, cmask = 0;
+#pragma unroll 1
+                for (int u = 0; u < m; u++) {
+                    uint32_t c;
+                    if (!word_of(u, c)) continue;
+                    vmask |= 1u << u;
+                    const uint32_t bit = 1u << (c & 31u);
+                    if ((atomicAnd(&bm[c >> 5], ~bit) & bit) != 0u) continue;
+                    cmask |= 1u << u;
+                    if (atomicAdd(xn, 1) >= bm_cap) continue;
+                    const unsigned long long key = ((unsigned long long)c << 32) | (spos0 + (uint32_t)(tid * m + u));
+                    uint32_t h = hash_u32(c) & (BMX - 1);
+                    while (true) {
+                        const unsigned long long pv = atomicCAS(&xt[h], ~0ull, key);
+                        if (pv == ~0ull) break;
+                        if ((uint32_t)(pv >> 32) == c) { atomicMin(&xt[h], key); break; }
+                        h = (h + 1) & (BMX - 1);
+                    }
+                }
+                __syncthreads();
+                const int nx = *xn;
+                if (nx <= bm_cap) {
+                    rolled = true;
+                    hashed = false;
+                    auto find = [&](uint32_t c) -> uint32_t {   // the slot of value c (or an empty one)
+                        uint32_t h = hash_u32(c) & (BMX - 1);
+                        unsigned long long t = xt[h];
+                        while (t != ~0ull && (uint32_t)(t >> 32) != c) {
+                            h = (h + 1) & (BMX - 1);
+                            t = xt[h];
+                        }
+                        return h;
+                    };
+                    if (nx > 0) {
+#pragma unroll 1
+                        for (int u = 0; u < m; u++) {
+                            uint32_t c;
+                            if (!((vmask >> u) & 1u) || ((cmask >> u) & 1u) || !word_of(u, c)) continue;
+                            const uint32_t h = find(c);
+                            if (xt[h] == ~0ull) continue;
+                            cmask |= 1u << u;
+                            atomicMin(&xt[h], ((unsigned long long)c << 32) | (spos0 + (uint32_t)(tid * m + u)));
+                        }
+                    }
+#ifdef DQNX_STAMPS
+                    if (a.stamps && tid == 0) a.stamps[13] = 2000 + nx;   // (diagnostic: the rolled pass ran)
+#endif
+                    if (tid == 0) s_final = -1;
+                    __syncthreads();
+                    if (iter == 0) DQNX_STAMP(a.stamps, 3);
+                    fmask = vmask & ~cmask;
+                    if (cmask) {
+#pragma unroll 1
+                        for (int u = 0; u < m; u++) {
+                            uint32_t c;
+                            if (!((cmask >> u) & 1u) || !word_of(u, c)) continue;
+                            if ((uint32_t)(xt[find(c)] & 0xffffffffull) == spos0 + (uint32_t)(tid * m + u)) fmask |= 1u << u;
+                        }
+                    }
+                } else {   // more repeats than the table takes: this pass on the hash table
+                    for (int i = tid; i < HS; i += NT) tab[i] = ~0ull;
+                    __syncthreads();
+                }
+            }
+        }
+        if (!rolled) {
 #pragma unroll
         for (int u = 0; u < WPT; u++) {   // the candidates (tempered, scaled, range-checked)
-            const int w = tid * m + u;
             val[u] = false;
             cv[u] = 0;
             hv[u] = 0;
-            if (u < m && w < nwords) {
-                const int bw = (w < avail) ? 0 : 1 + (w - avail) / 624;
-                const int ow = (w < avail) ? (int)pos + w : (w - avail) % 624;
-                const uint32_t c = mt_temper(blk[bw][ow]) >> shift;
-                val[u] = (int64_t)c < n;
-                cv[u] = c;
-            }
+            uint32_t c = 0;
+            if (word_of(u, c)) val[u] = true;
+            cv[u] = c;
         }
-        bool hashed = true;
+        }
         if constexpr (BMX > 0) {
-            if (bm_ok && iter == 0) {
+            if (bm_ok && iter == 0 && !a.bm_rolled) {
                 // Bitmap first pass: bit c of the cleared table (all ones) is cleared by the first
                 // word of value c to arrive; a word that finds it cleared repeats a value, and only
                 // such words (then the words whose value they repeat) meet in the exact repeat table,
@@ -282,7 +364,7 @@ __device__ __forceinline__ void sample_uniform_body(const SampleArgs& a, SampleL
                 }
             }
         }
-        if (hashed) {
+        if (hashed) {   // (never with `rolled`)
         unsigned long long prev[WPT];
 #pragma unroll
         for (int u = 0; u < WPT; u++) {   // first probe of every word, issued back to back
@@ -319,8 +401,12 @@ __device__ __forceinline__ void sample_uniform_body(const SampleArgs& a, SampleL
         }
         }
         int cnt = 0;
+        if (rolled) {
+            cnt = __popc(fmask);
+        } else {
 #pragma unroll
-        for (int u = 0; u < WPT; u++) cnt += first[u] ? 1 : 0;
+            for (int u = 0; u < WPT; u++) cnt += first[u] ? 1 : 0;
+        }
         int incl = cnt;   // wave inclusive scan
 #pragma unroll
         for (int o = 1; o < 64; o <<= 1) {
@@ -338,11 +424,9 @@ __device__ __forceinline__ void sample_uniform_body(const SampleArgs& a, SampleL
             total += tw;
         }
         int r = accepted + before;
-#pragma unroll
-        for (int u = 0; u < WPT; u++) {
-            if (!first[u]) continue;
+        auto emit = [&](int u, uint32_t cu) {   // the r-th acceptance: word u of this thread, value cu
             if (r < k) {
-                const int32_t c = (int32_t)cv[u];
+                const int32_t c = (int32_t)cu;
                 a.out[r] = c;
                 if (a.phys_out && r >= a.shard_begin && r < a.shard_begin + a.shard_len) {
                     int64_t ps = phys_base + (int64_t)c;
@@ -352,6 +436,17 @@ __device__ __forceinline__ void sample_uniform_body(const SampleArgs& a, SampleL
                 if (r == k - 1) s_final = tid * m + u;   // word index of the k-th acceptance
             }
             r++;
+        };
+        if (rolled) {
+#pragma unroll 1
+            for (int u = 0; u < m; u++) {
+                uint32_t c;
+                if (((fmask >> u) & 1u) && word_of(u, c)) emit(u, c);
+            }
+        } else {
+#pragma unroll
+            for (int u = 0; u < WPT; u++)
+                if (first[u]) emit(u, cv[u]);
         }
         __syncthreads();
         DQNX_STAMP(a.stamps, 5 + (iter < 9 ? iter : 9));
@@ -376,12 +471,21 @@ __device__ __forceinline__ void sample_uniform_body(const SampleArgs& a, SampleL
         if (!hashed) {   // the next passes dedup on the hash table, seeded with this pass's first words
             for (int i = tid; i < HS; i += NT) tab[i] = ~0ull;
             __syncthreads();
-#pragma unroll
-            for (int u = 0; u < WPT; u++) {
-                if (!first[u]) continue;
-                const unsigned long long key = ((unsigned long long)cv[u] << 32) | (spos0 + (uint32_t)(tid * m + u));
-                uint32_t h = hash_u32(cv[u]) & (HS - 1);
+            auto seed = [&](int u, uint32_t c) {
+                const unsigned long long key = ((unsigned long long)c << 32) | (spos0 + (uint32_t)(tid * m + u));
+                uint32_t h = hash_u32(c) & (HS - 1);
                 while (atomicCAS(&tab[h], ~0ull, key) != ~0ull) h = (h + 1) & (HS - 1);
+            };
+            if (rolled) {
+#pragma unroll 1
+                for (int u = 0; u < m; u++) {
+                    uint32_t c;
+                    if (((fmask >> u) & 1u) && word_of(u, c)) seed(u, c);
+                }
+            } else {
+#pragma unroll
+                for (int u = 0; u < WPT; u++)
+                    if (first[u]) seed(u, cv[u]);
             }
             __syncthreads();
         }

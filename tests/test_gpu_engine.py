@@ -503,14 +503,18 @@ def test_gpu_prefetch_dp_shard_step_bit_identical(world, k):
     assert np.array_equal(e1.get_rng(0), e2.get_rng(0))
 
 
-@pytest.mark.parametrize("world,n,cap", [(8, 260000, None), (4, 260000, None), (8, 150000, None),
-                                         (8, 260000, "2"), (8, 260000, "-1")])
-def test_gpu_prefetch_bitmap_first_pass_bit_identical(monkeypatch, world, n, cap):
+@pytest.mark.parametrize("world,n,cap,rolled", [(8, 260000, None, "0"), (4, 260000, None, "0"),
+                                                (8, 150000, None, "0"), (8, 260000, "2", "0"),
+                                                (8, 260000, "-1", "0"), (8, 260000, None, "1"),
+                                                (4, 150000, None, "1"), (8, 260000, "2", "1")])
+def test_gpu_prefetch_bitmap_first_pass_bit_identical(monkeypatch, world, n, cap, rolled):
     """The in-forward draw's bitmap first pass (one-pass shape, n <= 2^20 and n >= 32 k): exact
     "seen" bits plus the repeat table give the same positions and RNG state as the sampler launch,
     bitwise.  n = 260000: one pass; n = 150000: 1.75 words per draw, so the draw continues on the
     hash table seeded from the first pass; DQNX_SAMPLER_BM_CAP=2: more repeats than the cap, the
-    pass redone on the hash table; -1: the bitmap pass off."""
+    pass redone on the hash table; -1: the bitmap pass off.  DQNX_SAMPLER_ROLLED: either form of the
+    bitmap pass (unrolled register arrays / rolled loops over bit masks)."""
+    monkeypatch.setenv("DQNX_SAMPLER_ROLLED", rolled)
     if cap is not None:
         monkeypatch.setenv("DQNX_SAMPLER_BM_CAP", cap)
     E = _engine_mod()
