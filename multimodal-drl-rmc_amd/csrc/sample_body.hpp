@@ -73,6 +73,7 @@ __device__ __forceinline__ void sample_uniform_body(const SampleArgs& a, SampleL
         phys_base = wptr - n;
         if (phys_base < 0) phys_base += a.capacity;
     }
+    const uint32_t pb32 = (uint32_t)phys_base, cap32 = (uint32_t)a.capacity;
     const uint32_t* src = a.state_in ? a.state_in : a.state;
     for (int j = tid; j < 624; j += NT) blk[0][j] = src[j];
     uint32_t pos = src[624];
@@ -123,6 +124,7 @@ __device__ __forceinline__ void sample_uniform_body(const SampleArgs& a, SampleL
     const int bm_cap = (a.bm_cap > 0 && a.bm_cap < BMX / 2) ? a.bm_cap : BMX / 2;
     (void)bm_ok;
     (void)bm_cap;
+    const uint32_t n32 = (uint32_t)n;   // (n < 2^31: the engine's rings and the test hook refuse more)
     const int bits = bit_length64((uint64_t)n);
     const uint32_t shift = 32u - (uint32_t)bits;
     const float inv_accept = (float)((double)(1ull << bits) / (double)n);   // words per valid draw
@@ -187,13 +189,13 @@ __device__ __forceinline__ void sample_uniform_body(const SampleArgs& a, SampleL
         const int nwords = avail + 624 * nb;
         // ---- insert: thread t owns the contiguous words [t*m, t*m + m) of the pass ----
         const int m = (nwords + NT - 1) / NT;
+        // word w of the pass is blk[0][pos + w] read flat (blk[0][pos..624) then blocks 1..nb: avail = 624 - pos)
+        const uint32_t* wflat = &blk[0][0] + pos;
         auto word_of = [&](int u, uint32_t& c) -> bool {   // word u of this thread: a valid candidate?
             const int w = tid * m + u;
             if (u >= m || w >= nwords) return false;
-            const int bw = (w < avail) ? 0 : 1 + (w - avail) / 624;
-            const int ow = (w < avail) ? (int)pos + w : (w - avail) % 624;
-            c = mt_temper(blk[bw][ow]) >> shift;
-            return (int64_t)c < n;
+            c = mt_temper(wflat[w]) >> shift;
+            return c < n32;
         };
         uint32_t cv[WPT], hv[WPT];
         bool val[WPT], first[WPT];
@@ -220,7 +222,7 @@ __device__ __forceinline__ void sample_uniform_body(const SampleArgs& a, SampleL
                     cmask |= 1u << u;
                     if (atomicAdd(xn, 1) >= bm_cap) continue;
                     const unsigned long long key = ((unsigned long long)c << 32) | (spos0 + (uint32_t)(tid * m + u));
-                    uint32_t h = hash_u32(c) & (BMX - 1);
+                    uint32_t h = c & (BMX - 1);
                     while (true) {
                         const unsigned long long pv = atomicCAS(&xt[h], ~0ull, key);
                         if (pv == ~0ull) break;
@@ -234,7 +236,7 @@ __device__ __forceinline__ void sample_uniform_body(const SampleArgs& a, SampleL
                     rolled = true;
                     hashed = false;
                     auto find = [&](uint32_t c) -> uint32_t {   // the slot of value c (or an empty one)
-                        uint32_t h = hash_u32(c) & (BMX - 1);
+                        uint32_t h = c & (BMX - 1);
                         unsigned long long t = xt[h];
                         while (t != ~0ull && (uint32_t)(t >> 32) != c) {
                             h = (h + 1) & (BMX - 1);
@@ -291,7 +293,8 @@ __device__ __forceinline__ void sample_uniform_body(const SampleArgs& a, SampleL
                 // word of value c to arrive; a word that finds it cleared repeats a value, and only
                 // such words (then the words whose value they repeat) meet in the exact repeat table,
                 // where the earliest stream position wins.  32-bit LDS atomics on ~k words instead
-                // of 64-bit compare-and-swaps.
+                // of 64-bit compare-and-swaps.  The repeat table is indexed by the value's low bits
+                // (uniform: n >= 32 k); the pass is VALU-bound (8 waves on 4 SIMDs), so no hash.
                 uint32_t* bm = reinterpret_cast<uint32_t*>(tab);
                 unsigned long long* xt = tab + HS;
                 int* xn = reinterpret_cast<int*>(tab + HS + BMX);
@@ -311,7 +314,7 @@ __device__ __forceinline__ void sample_uniform_body(const SampleArgs& a, SampleL
                 for (int u = 0; u < WPT; u++) {
                     if (!xc[u] || atomicAdd(xn, 1) >= bm_cap) continue;
                     const unsigned long long key = ((unsigned long long)cv[u] << 32) | (spos0 + (uint32_t)(tid * m + u));
-                    uint32_t h = hash_u32(cv[u]) & (BMX - 1);
+                    uint32_t h = cv[u] & (BMX - 1);
                     while (true) {   // (at most bm_cap <= BMX / 2 values: an empty slot exists)
                         const unsigned long long pv = atomicCAS(&xt[h], ~0ull, key);
                         if (pv == ~0ull) break;
@@ -331,7 +334,7 @@ __device__ __forceinline__ void sample_uniform_body(const SampleArgs& a, SampleL
                         uint32_t hp[WPT];
 #pragma unroll
                         for (int u = 0; u < WPT; u++) {   // every first probe in flight at once
-                            hp[u] = hash_u32(cv[u]) & (BMX - 1);
+                            hp[u] = cv[u] & (BMX - 1);
                             t[u] = xt[hp[u]];
                         }
 #pragma unroll
@@ -429,8 +432,8 @@ __device__ __forceinline__ void sample_uniform_body(const SampleArgs& a, SampleL
                 const int32_t c = (int32_t)cu;
                 a.out[r] = c;
                 if (a.phys_out && r >= a.shard_begin && r < a.shard_begin + a.shard_len) {
-                    int64_t ps = phys_base + (int64_t)c;
-                    if (ps >= a.capacity) ps -= a.capacity;
+                    uint32_t ps = pb32 + (uint32_t)c;   // (< 2^32: both terms < capacity < 2^31)
+                    if (ps >= cap32) ps -= cap32;
                     a.phys_out[r - a.shard_begin] = (int32_t)ps;
                 }
                 if (r == k - 1) s_final = tid * m + u;   // word index of the k-th acceptance

@@ -85,7 +85,7 @@ def test_gpu_sampler_k_larger_than_n_sets_error():
     before = d_state.clone()
     out = torch.zeros(8, dtype=torch.int32, device="cuda")
     err = torch.zeros(1, dtype=torch.int32, device="cuda")
-    scratch = torch.zeros(1024, dtype=torch.uint8, device="cuda")
+    scratch = torch.zeros(int(L.dqnx_sample_scratch_bytes(5, 8)) + 16, dtype=torch.uint8, device="cuda")
     C.check(L.dqnx_sample_uniform(d_state.data_ptr(), 5, 8, out.data_ptr(), scratch.data_ptr(), err.data_ptr(),
                                   torch.cuda.current_stream().cuda_stream), "sample")
     torch.cuda.synchronize()
