@@ -14,6 +14,14 @@ pytestmark = pytest.mark.gpu
 HERE = os.path.dirname(os.path.abspath(__file__))
 
 
+
+def _error_lines(text, limit=20):
+    """The lines of a child's stderr that name the error (a watchdog's stack trace hides them from
+    the tail)."""
+    keys = ("error", "Error", "what()", "fault", "Fault", "illegal", "dqnx")
+    hits = [ln for ln in text.splitlines() if any(k in ln for k in keys) and "frame #" not in ln]
+    return "\n".join(hits[:limit]) + "\n"
+
 def run_ranks(tmp_path, world, algo, sampling="global", case="small", compute="fp32", timeout=300, mode="plain"):
     env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(free_port()))
     procs = [subprocess.Popen([sys.executable, os.path.join(HERE, "dp_gpu_worker.py"), str(r), str(world), algo,
@@ -129,7 +137,7 @@ def test_gpu_graphed_dp_step_matches_eager(algo):
     env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(free_port()))
     r = subprocess.run([sys.executable, os.path.join(os.path.dirname(HERE), "tools", "dp_graph_check.py"), algo, "256"],
                        env=env, capture_output=True, text=True, timeout=240)
-    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    assert r.returncode == 0, r.stdout[-2000:] + _error_lines(r.stderr) + r.stderr[-2000:]
     assert "graphed == eager: True; dp == single: True; prefetch == eager: True" in r.stdout, r.stdout[-2000:]
 
 
@@ -289,5 +297,5 @@ def test_gpu_graphed_bucketed_dp_step(net):
     env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(free_port()))
     r = subprocess.run([sys.executable, os.path.join(os.path.dirname(HERE), "tools", "dp_bucket_check.py"), net],
                        env=env, capture_output=True, text=True, timeout=280)
-    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    assert r.returncode == 0, r.stdout[-2000:] + _error_lines(r.stderr) + r.stderr[-2000:]
     assert "all equal: True" in r.stdout, r.stdout[-2000:]
