@@ -40,6 +40,7 @@ sys.path.insert(0, os.path.join(REPO, "multimodal-drl-rmc_amd"))
 
 from dqn import _capi as C  # noqa: E402
 from dqn.data_parallel import GraphedDPStep, dp_learn_step, dp_learn_step_bucketed  # noqa: E402
+from dqn.data_parallel import capture as dp_capture  # noqa: E402
 from dqn.engine import LearnEngine, hybrid_spec, mlp_spec  # noqa: E402
 
 PEAK_FP32_MFMA_TFLOPS = 157.3   # MI355X_MICROARCH.md: F32 matrix, dense
@@ -518,7 +519,7 @@ def graphed_shard_steps(eng, args, steps, device, prefetch=None):
         eng.prefetch_prologue()
     torch.cuda.synchronize()
     g = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(g):
+    with dp_capture(g):
         for _ in range(gs):
             eng.learn_step(grads_only=True, prefetch=prefetch)
             shard_td_exchange(eng)

@@ -3771,6 +3771,8 @@ int dqnx_agent_stage_rng(dqnx_engine* e, int32_t which, const uint32_t* state625
     return DQNX_OK;
 }
 
+static int agent_launch_impl(dqnx_engine* e, int32_t flags, void* stream, int* prev_rc);
+
 int dqnx_agent_learn_mt(dqnx_engine* e, uint32_t* mt, int32_t* pos, int32_t flags, void* stream, int64_t* words) {
     if (!mt || !pos || !words) return set_error(DQNX_EINVAL, "bad argument");
     if (*pos < 0 || *pos > 624) return set_error(DQNX_EINVAL, "MT position must be in [0, 624]");
@@ -3788,7 +3790,8 @@ int dqnx_agent_learn_mt(dqnx_engine* e, uint32_t* mt, int32_t* pos, int32_t flag
         rc = agent_pin_state(e, DQNX_RNG_PY, s625);
         if (rc) return rc;
         e->ag_expect_live = false;   // (the check below is armed after the walk)
-        rc = dqnx_agent_launch(e, flags & ~DQNX_AGENT_LAUNCH, stream);
+        int prev_rc;
+        rc = agent_launch_impl(e, flags & ~DQNX_AGENT_LAUNCH, stream, &prev_rc);
         if (rc) return rc;
         rc = dqnx_rng_sample_words(s625, e->ring_size, e->Bs, e->ag_check, words);
         if (rc) return rc;
@@ -3796,7 +3799,7 @@ int dqnx_agent_learn_mt(dqnx_engine* e, uint32_t* mt, int32_t* pos, int32_t flag
         e->ag_check_which = DQNX_RNG_PY;
         memcpy(mt, e->ag_check, 624 * 4);   // the caller's generator moves past the draw
         *pos = (int32_t)e->ag_check[624];
-        return DQNX_OK;
+        return prev_rc;   // the launched step's draw is mirrored; the previous step's checks raise
     }
     rc = dqnx_agent_stage_rng(e, DQNX_RNG_PY, s625, words);
     if (rc) return rc;
@@ -3806,7 +3809,25 @@ int dqnx_agent_learn_mt(dqnx_engine* e, uint32_t* mt, int32_t* pos, int32_t flag
     return DQNX_OK;
 }
 
-int dqnx_agent_launch(dqnx_engine* e, int32_t flags, void* stream) {
+// the checks of a completed control-block readback: sticky device error, then the device sampler's
+// RNG state against the host mirror of the draw
+static int agent_check_ctrl(dqnx_engine* e, dqnx_ctrl* out) {
+    const dqnx_ctrl* c = e->ag_ctrl_pin;
+    if (out) memcpy(out, c, sizeof(dqnx_ctrl));
+    const bool check = e->ag_check_live;
+    e->ag_check_live = false;
+    if (c->error) return set_error(DQNX_EDEVICE, "device error %d", c->error);
+    if (check) {
+        const uint32_t* got = e->ag_check_which == DQNX_RNG_PY ? c->py_mt : c->np_mt;
+        if (memcmp(got, e->ag_check, sizeof(e->ag_check)))
+            return set_error(DQNX_EDEVICE, "the device sampler's RNG state differs from the host mirror of the draw");
+    }
+    return DQNX_OK;
+}
+
+// *prev_rc: the checks of the previous step's unread readback (this step is launched either way)
+static int agent_launch_impl(dqnx_engine* e, int32_t flags, void* stream, int* prev_rc) {
+    *prev_rc = DQNX_OK;
     int rc = check_bound(e);
     if (rc) return rc;
     if (e->ag_which < 0) return set_error(DQNX_ESTATE, "dqnx_agent_launch without a staged RNG state");
@@ -3837,7 +3858,11 @@ int dqnx_agent_launch(dqnx_engine* e, int32_t flags, void* stream) {
         DQNX_HIP_CHECK(hipHostMalloc((void**)&e->ag_ctrl_pin, sizeof(dqnx_ctrl), hipHostMallocDefault));
         DQNX_HIP_CHECK(hipEventCreateWithFlags(&e->ag_ctrl_ev, hipEventDisableTiming));
     }
-    if (e->ag_ctrl_live) DQNX_HIP_CHECK(hipEventSynchronize(e->ag_ctrl_ev));   // (superseded, unread)
+    if (e->ag_ctrl_live) {   // the previous step's readback was never read: check it before it is overwritten
+        DQNX_HIP_CHECK(hipEventSynchronize(e->ag_ctrl_ev));
+        e->ag_ctrl_live = false;
+        *prev_rc = agent_check_ctrl(e, nullptr);
+    }
     DQNX_HIP_CHECK(hipMemcpyAsync(e->ag_ctrl_pin, ctrl_of(e), sizeof(dqnx_ctrl), hipMemcpyDeviceToHost, s));
     DQNX_HIP_CHECK(hipEventRecord(e->ag_ctrl_ev, s));
     e->ag_ctrl_live = true;
@@ -3847,6 +3872,12 @@ int dqnx_agent_launch(dqnx_engine* e, int32_t flags, void* stream) {
     e->ag_expect_live = false;
     e->ag_which = -1;
     return DQNX_OK;
+}
+
+int dqnx_agent_launch(dqnx_engine* e, int32_t flags, void* stream) {
+    int prev_rc;
+    const int rc = agent_launch_impl(e, flags, stream, &prev_rc);
+    return rc ? rc : prev_rc;
 }
 
 int dqnx_agent_readback(dqnx_engine* e, int32_t wait, dqnx_ctrl* out) {
@@ -3860,16 +3891,8 @@ int dqnx_agent_readback(dqnx_engine* e, int32_t wait, dqnx_ctrl* out) {
         if (q != hipSuccess) return set_hip_error(q, "hipEventQuery", __FILE__, __LINE__);
     }
     e->ag_ctrl_live = false;
-    const dqnx_ctrl* c = e->ag_ctrl_pin;
-    if (out) memcpy(out, c, sizeof(dqnx_ctrl));
-    if (c->error) return set_error(DQNX_EDEVICE, "device error %d", c->error);
-    if (e->ag_check_live) {
-        e->ag_check_live = false;
-        const uint32_t* got = e->ag_check_which == DQNX_RNG_PY ? c->py_mt : c->np_mt;
-        if (memcmp(got, e->ag_check, sizeof(e->ag_check)))
-            return set_error(DQNX_EDEVICE, "the device sampler's RNG state differs from the host mirror of the draw");
-    }
-    return 1;
+    const int rc = agent_check_ctrl(e, out);
+    return rc ? rc : 1;
 }
 
 uint64_t dqnx_act_host_scratch_bytes(const dqnx_net_desc* net, int32_t n) {
@@ -3887,9 +3910,14 @@ int dqnx_act_host(const dqnx_net_desc* net, const float* params, const float* ob
     if (scratch_bytes < need) return set_error(DQNX_EINVAL, "dqnx_act_host: scratch too small (%llu < %llu)",
                                                 (unsigned long long)scratch_bytes, (unsigned long long)need);
     const uint64_t ob = ((uint64_t)n * net->obs_dim * 4 + 255) / 256 * 256, ab = ((uint64_t)n * 4 + 255) / 256 * 256;
+    // obs and actions at the START, the acting scratch after them: dqnx_act keeps its arrival tickets at
+    // the END of the scratch it is given, which is then the end of the caller's buffer for every n (a
+    // call's obs never lands on the tickets another n's call uses; tests/test_gpu_act.py)
     char* sc = (char*)scratch;
-    float* d_obs = (float*)(sc + (scratch_bytes - ob - ab));   // obs and actions at the END: the acting
-    int32_t* d_act = (int32_t*)(sc + (scratch_bytes - ab));    // scratch keeps its tickets just below them
+    float* d_obs = (float*)sc;
+    int32_t* d_act = (int32_t*)(sc + ob);
+    void* act_sc = sc + ob + ab;
+    const uint64_t act_bytes = scratch_bytes - ob - ab;
     // pinned staging, per thread, grown as needed
     static thread_local char* pin = nullptr;
     static thread_local size_t pin_bytes = 0;
@@ -3910,7 +3938,7 @@ int dqnx_act_host(const dqnx_net_desc* net, const float* params, const float* ob
         // fine-grained block in place (no copy calls), then one synchronisation
         memcpy(pin, obs_host, (size_t)n * net->obs_dim * 4);
         int32_t* pa = (int32_t*)(pin + (size_t)n * net->obs_dim * 4);
-        int rc = dqnx_act(net, params, (const float*)pin, n, pa, nullptr, scratch, scratch_bytes - ob - ab, stream);
+        int rc = dqnx_act(net, params, (const float*)pin, n, pa, nullptr, act_sc, act_bytes, stream);
         if (rc) return rc;
         DQNX_HIP_CHECK(hipStreamSynchronize(s));
         memcpy(actions_host, pa, (size_t)n * 4);
@@ -3918,7 +3946,7 @@ int dqnx_act_host(const dqnx_net_desc* net, const float* params, const float* ob
     }
     memcpy(pin, obs_host, (size_t)n * net->obs_dim * 4);
     DQNX_HIP_CHECK(hipMemcpyAsync(d_obs, pin, (size_t)n * net->obs_dim * 4, hipMemcpyHostToDevice, s));
-    int rc = dqnx_act(net, params, d_obs, n, d_act, nullptr, scratch, scratch_bytes - ob - ab, stream);
+    int rc = dqnx_act(net, params, d_obs, n, d_act, nullptr, act_sc, act_bytes, stream);
     if (rc) return rc;
     int32_t* pa = (int32_t*)(pin + (size_t)n * net->obs_dim * 4);
     DQNX_HIP_CHECK(hipMemcpyAsync(pa, d_act, (size_t)n * 4, hipMemcpyDeviceToHost, s));

@@ -92,6 +92,8 @@ EXPORTS = [
     "dqnx_act_host", "dqnx_agent_learn_mt",
 ]
 
+GIL_HELD = ("dqnx_agent_learn_mt",)   # entry points called with the GIL held (see lib())
+
 _lib = None
 
 
@@ -167,10 +169,16 @@ def lib():
         "dqnx_act_host_scratch_bytes": ([P(NetDesc), I32], ctypes.c_uint64),
         "dqnx_act_host": ([P(NetDesc), vp, vp, I32, vp, vp, ctypes.c_uint64, vp], ctypes.c_int),
     }
+    # dqnx_agent_learn_mt reads and writes random._inst's MT words in place: call it through a PyDLL
+    # handle, which keeps the GIL for the call (a CDLL call releases it, and another thread's `random`
+    # use could then see a torn generator state; the reference's random.sample holds the GIL throughout)
+    L_gil = ctypes.PyDLL(LIB_PATH)
     for name, (args, res) in sig.items():
-        f = getattr(L, name)
+        f = getattr(L_gil if name in GIL_HELD else L, name)
         f.argtypes = args
         f.restype = res
+        if name in GIL_HELD:
+            setattr(L, name, f)
     _lib = L
     return L
 

@@ -100,6 +100,25 @@ def _gather_abs_td(engine, group):
     dist.all_gather(parts, mine, group=group)
 
 
+CAPTURE_MODE = "thread_local"
+
+
+def capture(graph):
+    """torch.cuda.graph(graph) in "thread_local" capture mode -- the mode every capture of this package
+    uses.
+
+    torch's default, "global", makes HIP refuse capture-unsafe calls from EVERY thread while the capture
+    is open, and ProcessGroupNCCL's watchdog thread polls the events of the eager collectives still in its
+    list (hipEventQuery, every ~100 ms).  A poll that landed inside a DP-step capture returned a capture
+    error, the watchdog rethrew it as a HIP error and the process aborted (SIGABRT from
+    WorkNCCL::finishedGPUExecutionInternal: test_gpu_graphed_bucketed_dp_step, round 4, twice in ~20
+    runs, on the conv nets whose captures take longest).  "thread_local" keeps the check for the capturing
+    thread (a sync or allocation there would still be an error) and lets other threads query events.
+    tests/test_gpu_dp.py::test_gpu_capture_tolerates_watchdog_polls holds a collective's work pending in the
+    watchdog across a capture (tools/capture_watchdog_check.py)."""
+    return torch.cuda.graph(graph, capture_error_mode=CAPTURE_MODE)
+
+
 class GraphedDPStep:
     """The whole data-parallel step -- the shard's learn kernels, the RCCL all-reduce (+ the
     PER |delta| all-gather), Adam + soft update -- captured once into one HIP graph
@@ -133,7 +152,7 @@ class GraphedDPStep:
         if prefetch:
             engine.prefetch_prologue()
         torch.cuda.synchronize()
-        with torch.cuda.graph(self.graph):
+        with capture(self.graph):
             for _ in range(self.steps):
                 if bucketed:   # the side stream forks and joins inside the capture
                     dp_learn_step_bucketed(engine, soft_update=soft_update, group=group, comm_stream=self.comm,

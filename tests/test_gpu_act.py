@@ -146,3 +146,38 @@ def test_gpu_standalone_network_actions(cls):
     with torch.no_grad():
         ref2 = (other.advantages(xt) if cls is DuelingDeepQNetwork else other(xt)).argmax(1).tolist()
     assert net.actions(x) == ref2
+
+
+@pytest.mark.parametrize("net", ["mlp", "two_stream"])
+def test_gpu_act_host_shared_scratch_across_row_counts(net):
+    """dqnx_act_host with one scratch buffer and n = 64 then smaller n: the acting kernel's
+    arrival tickets must sit at the same address for every n.  They used to follow the end of the
+    n-dependent acting region, and on the two-stream path a 64-row call's obs filled the words an
+    8-row call then took for its tickets: its last-arriver test never fired and stale actions came
+    back without an error.  Every call's actions and values are compared with dqnx_act's."""
+    import ctypes
+
+    from dqn import _capi as C
+    if net == "mlp":
+        ospec, espec = O.mlp_spec(284, 8, "dueling"), E.mlp_spec(284, 8, "dueling")
+    else:
+        ospec, espec = O.hybrid_spec(8, "dueling"), E.hybrid_spec(8, "dueling")
+    params = O.reference_init(ospec, 8)
+    flat = _flat(espec, params)
+    desc = espec.to_c()
+    L = C.lib()
+    nb = int(L.dqnx_act_host_scratch_bytes(ctypes.byref(desc), 64))
+    scratch = torch.zeros((nb + 15) // 16 * 4, dtype=torch.float32, device="cuda")
+    stream = torch.cuda.current_stream().cuda_stream
+    for n in (64, 8, 1, 64, 3, 8):
+        x = O.synth_transitions(n, ospec.obs_dim, 8, seed=100 + n)[0]
+        x = np.ascontiguousarray(x, dtype=np.float32) + np.float32(0.25)   # obs words far from 0
+        out = np.full(n, -1, dtype=np.int32)
+        C.check(L.dqnx_act_host(ctypes.byref(desc), flat.data_ptr(), x.ctypes.data, n, out.ctypes.data,
+                                scratch.data_ptr(), scratch.numel() * 4, stream), "act_host")
+        vals = torch.empty(n, 8, dtype=torch.float32, device="cuda")
+        acts = E.act(espec, flat, torch.from_numpy(x).cuda(), vals).cpu().numpy()
+        assert np.array_equal(out, acts), (n, out, acts)
+        with torch.no_grad():
+            ref = O.advantages(ospec, params, torch.from_numpy(x)).numpy()
+        _check(vals.cpu().numpy(), ref, out)

@@ -299,3 +299,18 @@ def test_gpu_graphed_bucketed_dp_step(net):
                        env=env, capture_output=True, text=True, timeout=280)
     assert r.returncode == 0, r.stdout[-2000:] + _error_lines(r.stderr) + r.stderr[-2000:]
     assert "all equal: True" in r.stdout, r.stdout[-2000:]
+
+
+def test_gpu_capture_tolerates_watchdog_polls():
+    """The round-4 abort of test_gpu_graphed_bucketed_dp_step, forced deterministically: an all-reduce's
+    work is held incomplete (behind a spin kernel) in ProcessGroupNCCL's watchdog list while a graph
+    capture stays open for 0.6 s, so the watchdog's ~100 ms event poll lands inside the capture.  Under
+    torch's default "global" capture mode HIP refuses that poll and the watchdog aborts the process;
+    the package captures in dqn.data_parallel.CAPTURE_MODE ("thread_local").  The same run then captures
+    the HEAD net's bucketed DP step with the capture stretched past the poll interval and checks its
+    replays against eager steps (tools/capture_watchdog_check.py)."""
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(free_port()))
+    r = subprocess.run([sys.executable, os.path.join(os.path.dirname(HERE), "tools", "capture_watchdog_check.py"),
+                        "package"], env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stdout[-2000:] + _error_lines(r.stderr) + r.stderr[-2000:]
+    assert "capture ok (package)" in r.stdout and "5 replays == eager" in r.stdout, r.stdout[-2000:]

@@ -46,7 +46,7 @@ eng.set_graphs(False)
 for gs in (1, 4):
     torch.cuda.synchronize()
     g = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(g):
+    with torch.cuda.graph(g, capture_error_mode="thread_local"):
         for _ in range(gs):
             shard_step()
     for _ in range(3):
@@ -90,7 +90,7 @@ for part, fn in (("learn_only", lambda: eng.learn_step(grads_only=True)),
                  ("apply_only", lambda: eng.apply_grads(soft_update=True))):
     torch.cuda.synchronize()
     g = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(g):
+    with torch.cuda.graph(g, capture_error_mode="thread_local"):
         fn()
     for _ in range(3):
         g.replay()

@@ -28,7 +28,7 @@ for W in Ws:
     eng.prefetch_prologue()
     torch.cuda.synchronize()
     g = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(g):
+    with torch.cuda.graph(g, capture_error_mode="thread_local"):
         for _ in range(per_graph):
             eng.learn_step(grads_only=True, prefetch=True)
             eng.apply_grads(soft_update=True)
