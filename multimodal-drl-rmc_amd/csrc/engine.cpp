@@ -409,6 +409,10 @@ struct dqnx_engine {
     // fused plan: fragment-blocked weight copies [online fwd | target fwd | online chain] per layer
     uint64_t ws_wblk[2][FUSED_MAX_L] = {{0}}, ws_wblkT[FUSED_MAX_L] = {0};
     std::vector<uint64_t> ws_H, ws_dZ, ws_part;
+    // bf16 weight gradients from T16 copies (k_dw_bf16t): stream 0's rows / H_l and dZ_l / dHead in bf16
+    bool dwt = false;
+    uint64_t ws_xT16 = 0, ws_dheadT16 = 0;
+    std::vector<uint64_t> ws_HT16, ws_dZT16;
     // two-stream CNN: per conv layer im2col [3][M][Kstride], activations [3][M][Co],
     // dZ [M][Co], split-K partial slabs; dense input F [3][Bl][strideF] and its gradient
     std::vector<uint64_t> ws_col, ws_Hc, ws_dZc, ws_cpart;
@@ -548,6 +552,16 @@ int layout(dqnx_engine* e) {
     }
     e->ws_head_part = sub((uint64_t)e->slices[L - 1] * head_pstride(np) * 4);
     e->ws_dhead = sub((uint64_t)e->Bl * 16 * 4);
+    e->ws_HT16.assign(L, 0);
+    e->ws_dZT16.assign(L, 0);
+    if (e->dwt) {
+        e->ws_xT16 = sub((uint64_t)e->Bl * np.dense[0].in * 2);
+        for (int l = 0; l < L; l++) {
+            e->ws_HT16[l] = sub((uint64_t)e->Bl * np.dense[l].out * 2);
+            e->ws_dZT16[l] = sub((uint64_t)e->Bl * np.dense[l].out * 2);
+        }
+        e->ws_dheadT16 = sub((uint64_t)e->Bl * 16 * 2);
+    }
     e->ws_raw = sub((uint64_t)3 * e->Bl * 16 * 4);
     e->ws_trans = sub((uint64_t)e->Bl * 16);
     if (e->bwd_plan == 2) {
@@ -976,6 +990,10 @@ void build_fused_steps(dqnx_engine* e, int flags, int32_t* idx, int32_t* phys, s
         fa.phys = phys;
         fa.xcopy = at<float>(e, e->ws_xobs);
         for (int l = 0; l < L; l++) fa.H[l] = at<float>(e, e->ws_H[l]);   // stream-0 third of [3][Bl][w]
+        if (e->dwt) {   // + the T16 copies k_dw_bf16t reads
+            fa.xT16 = at<uint16_t>(e, e->ws_xT16);
+            for (int l = 0; l < L; l++) fa.HT16[l] = at<uint16_t>(e, e->ws_HT16[l]);
+        }
         fa.raw = at<float>(e, e->ws_raw);
         fa.trans = at<float4>(e, e->ws_trans);
         fa.act = at<int32_t>(e, e->off[DQNX_BUF_RING_ACT]);
@@ -1105,6 +1123,10 @@ void build_fused_steps(dqnx_engine* e, int flags, int32_t* idx, int32_t* phys, s
         ha.Q = at<float>(e, e->off[DQNX_BUF_Q]);
         ha.td = at<float>(e, e->off[DQNX_BUF_TD]);
         ha.dhead = at<float>(e, e->ws_dhead);
+        if (e->dwt) {
+            for (int l = 0; l < L; l++) ha.dZT16[l] = at<uint16_t>(e, e->ws_dZT16[l]);
+            ha.dheadT16 = at<uint16_t>(e, e->ws_dheadT16);
+        }
         ha.loss_partial = at<float>(e, e->ws_loss_part);
         ha.ctrl = nullptr;   // the forward launch stores the step's Adam scalars
         ha.xcd_rows = xcd_rows ? 1 : 0;
@@ -1180,6 +1202,12 @@ void build_fused_steps(dqnx_engine* e, int flags, int32_t* idx, int32_t* phys, s
             d.partial = at<float>(e, e->ws_part[l]);
             d.pstride = (int64_t)lp.out * lp.in + lp.out;
             d.head_kind = -1;
+            if (e->dwt) {
+                d.dZT = at<uint16_t>(e, e->ws_dZT16[l]);
+                d.cz = lp.out;
+                d.XT = at<uint16_t>(e, l > 0 ? e->ws_HT16[l - 1] : e->ws_xT16);
+                d.cx = lp.in;
+            }
             flops += 2.0 * Bl * lp.out * (lp.in + 1.0);
             bytes += 4.0 * (Bl * (lp.out + lp.in) + ba.dw_slices * (lp.out * (lp.in + 1.0)));
         }
@@ -1187,6 +1215,12 @@ void build_fused_steps(dqnx_engine* e, int flags, int32_t* idx, int32_t* phys, s
             DwProblem& h = ba.dw[ba.ndw++];
             h.dZ = at<float>(e, e->ws_dhead);
             h.ldz = 16;
+            if (e->dwt) {
+                h.dZT = at<uint16_t>(e, e->ws_dheadT16);
+                h.cz = 16;
+                h.XT = at<uint16_t>(e, e->ws_HT16[L - 1]);
+                h.cx = np.F;
+            }
             h.X = at<float>(e, e->ws_H[L - 1]);
             h.ldx = np.F;
             h.in = np.F;
@@ -1293,6 +1327,7 @@ void build_fused_steps(dqnx_engine* e, int flags, int32_t* idx, int32_t* phys, s
         }
         if (e->fplan.bf16) {   // bf16 operands, fp32 slabs: the same Adam pass follows
             dw_bf16_grid(ba);
+            ba.t16 = e->dwt && dw_bf16t_supported(ba) ? 1 : 0;
             if (per_fused) {   // tracking in this launch, prop in the Adam launch; or prop here
                 ba.pprop = pua;
                 ba.ptrack = per_track ? 1 : 0;
@@ -2719,7 +2754,7 @@ int dqnx_engine_create(const dqnx_config* cfg, dqnx_engine** out) {
             if (e->fsplit > 1) {   // layer 1's row tiles: 32 rows (each weight fragment feeds 2 MFMAs)
                 const int m = route_knob("DQNX_FWD_L1_MR", 2);
                 FusedFwdArgs t2 = e->fplan;
-                if (m == 2 && fused_fwd_plan(t2, c.net.obs_dim, e->fplan.bf16 != 0, 2)) e->fsplit_mr = 2;
+                if ((m == 2 || m == 4) && fused_fwd_plan(t2, c.net.obs_dim, e->fplan.bf16 != 0, m)) e->fsplit_mr = m;
             }
         }
     }
@@ -2740,6 +2775,10 @@ int dqnx_engine_create(const dqnx_config* cfg, dqnx_engine** out) {
         e->slices[l] = S;
         e->kslice[l] = ks;
     }
+    // bf16 weight gradients from T16 copies written by the forward (the one-launch plan) and the head
+    // kernel (k_dw_bf16t; DQNX_DWB_T=0 keeps k_dw_bf16's fp32-row staging): whole 32-sample chunks
+    e->dwt = e->bwd_plan == 2 && e->fplan.bf16 && !(e->fsplit > 1 && e->fplan.mr == 1) && e->Bl % 32 == 0 &&
+             e->kslice[0] % 32 == 0 && e->kslice[0] <= 512 && route_knob("DQNX_DWB_T", 1) != 0;
     const int NC = (int)e->np.conv.size();
     e->cslices.assign(NC, 1);
     e->ckslice.assign(NC, 1);

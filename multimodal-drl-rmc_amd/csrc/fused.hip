@@ -83,6 +83,11 @@ __host__ __device__ __forceinline__ int fwd_groups(int K) { return (fwd_nch<BF>(
 // to HBM and for the weight prefetch in flight across the barrier.
 __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
+template <class K>
+static void allow_lds(K kern, size_t bytes) {
+    if (bytes > 64 * 1024) (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+}
+
 // ---- weight streams -------------------------------------------------------------------
 // Buffer loads through a wave-uniform descriptor: they stay VMEM ops counted by vmcnt alone
 // (a generic pointer that lost its address space becomes a flat load, and the compiler then
@@ -485,22 +490,47 @@ __global__ __launch_bounds__(FT) void k_mlp_fwd(FusedFwdArgs a) {
         float* Hs = FBUF(cur ^ 1);
         // H to HBM: stream 0 (the backward's operands); the split layer 1 writes every stream's
         float* Hg = (PH == 1) ? a.H[0] + (int64_t)s * a.Bl * N : (keep ? a.H[l] : nullptr);
+        // bf16 + k_dw_bf16t: stream 0's H_l also as a T16 copy (4 consecutive samples per lane: 8 bytes)
+        uint16_t* Ht = (BF && PH == 0 && keep) ? a.HT16[l] : nullptr;
 #pragma unroll
         for (int t = 0; t < 2; t++) {
             if (t >= cl.tn) continue;
             const int col = cl.n0[t] + i;
 #pragma unroll
-            for (int m = 0; m < MR; m++)
+            for (int m = 0; m < MR; m++) {
+                float vv[4];
 #pragma unroll
                 for (int r = 0; r < 4; r++) {
                     const int rr = 16 * m + 4 * g + r;
                     const float v = act_fwd<ACT>(acc[m][t][r] + bias[t]);
+                    vv[r] = v;
                     if constexpr (PH != 1) {
                         if constexpr (BF) reinterpret_cast<uint16_t*>(Hs)[rr * a.sh + col] = bf16_bits(v);
                         else Hs[rr * a.sh + col] = v;
                     }
                     if (Hg && rr < nb) Hg[(int64_t)(b0 + rr) * N + coff + col] = v;
                 }
+                if (Ht && 16 * m + 4 * g < nb)   // (T16 runs need whole 32-row blocks: nb % 32 == 0)
+                    *reinterpret_cast<uint2*>(Ht + t16_index(b0 + 16 * m + 4 * g, col, N)) =
+                        make_uint2(bf16_pack2(vv[0], vv[1]), bf16_pack2(vv[2], vv[3]));
+            }
+        }
+        if constexpr (BF && PH == 0) {
+            // stream 0's input rows as a T16 copy, from the bf16 input tile (still in buffer 0 until
+            // layer 2's epilogue), while layer 2's weight stream is in flight: 8 rows of a column per piece
+            if (l == 0 && keep && a.xT16) {
+                const int C = a.in[0];
+                const uint16_t* xs = reinterpret_cast<const uint16_t*>(FBUF(0));
+                for (int q = tid; q < 2 * MR * C; q += FT) {
+                    const int ph = q / C, cc = q - ph * C;
+                    if (8 * ph >= nb) continue;
+                    const uint16_t* col = xs + 8 * ph * a.sx + cc;
+                    uint32_t w[4];
+#pragma unroll
+                    for (int j = 0; j < 4; j++) w[j] = (uint32_t)col[(2 * j) * a.sx] | ((uint32_t)col[(2 * j + 1) * a.sx] << 16);
+                    *reinterpret_cast<uint4*>(a.xT16 + t16_index(b0 + 8 * ph, cc, C)) = make_uint4(w[0], w[1], w[2], w[3]);
+                }
+            }
         }
         if constexpr (PH == 1) return;
         lds_barrier();
@@ -720,6 +750,7 @@ __global__ __launch_bounds__(FT) void k_head_bwd(HeadBwdArgs a) {
                 a.Q[(int64_t)2 * a.Bl * A + qrow] = q2;
             }
             a.dhead[(int64_t)(b0 + hb) * 16 + hj] = d;
+            if (a.dheadT16) a.dheadT16[t16_index(b0 + hb, hj, 16)] = bf16_bits(d);
             if (hj == 0) {
                 const int gb = b0 + hb;
                 a.td[gb] = y;
@@ -751,14 +782,19 @@ __global__ __launch_bounds__(FT) void k_head_bwd(HeadBwdArgs a) {
 #pragma unroll
             for (int jj = 0; jj < 4; jj++) acc = mfma16x16x4(dh[i][4 * g + jj], whv[t][jj], acc);
             const int col = cF.n0[t] + i;
+            float vv[4];
 #pragma unroll
             for (int r = 0; r < 4; r++) {
                 const int rr = 4 * g + r;
                 const float v = act_bwd<ACT>(acc[r], hmask[t][r]);
+                vv[r] = v;
                 if constexpr (BF) reinterpret_cast<uint16_t*>(dz)[rr * HB_SDH + col] = bf16_bits(v);
                 else dz[rr * HB_SD + col] = v;
                 if (lead && rr < nb) dzg[(int64_t)(b0 + rr) * F + col] = v;
             }
+            if (lead && a.dZT16[L - 1] && 4 * g < nb)   // T16 copy for k_dw_bf16t
+                *reinterpret_cast<uint2*>(a.dZT16[L - 1] + t16_index(b0 + 4 * g, col, F)) =
+                    make_uint2(bf16_pack2(vv[0], vv[1]), bf16_pack2(vv[2], vv[3]));
         }
     }
 
@@ -779,16 +815,21 @@ __global__ __launch_bounds__(FT) void k_head_bwd(HeadBwdArgs a) {
         for (int t = 0; t < 2; t++) {
             if (t >= cw.tn) continue;
             const int col = cw.n0[t] + i;
+            float vv[4];
 #pragma unroll
             for (int r = 0; r < 4; r++) {
                 const int rr = 4 * g + r;
                 const float v = act_bwd<ACT>(acc[t][r], hm[t][r]);
+                vv[r] = v;
                 if (l > 1) {   // the last level's tile feeds nothing
                     if constexpr (BF) reinterpret_cast<uint16_t*>(dz)[rr * HB_SDH + col] = bf16_bits(v);
                     else dz[rr * HB_SD + col] = v;
                 }
                 if (store && rr < nb) dzg[(int64_t)(b0 + rr) * ldn + coff + col] = v;
             }
+            if (store && a.dZT16[l - 1] && 4 * g < nb)
+                *reinterpret_cast<uint2*>(a.dZT16[l - 1] + t16_index(b0 + 4 * g, coff + col, ldn)) =
+                    make_uint2(bf16_pack2(vv[0], vv[1]), bf16_pack2(vv[2], vv[3]));
         }
         cur ^= 1;
     }
@@ -1013,6 +1054,118 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(dwb_waves<B
     }
 }
 
+// The same weight gradients from the T16 bf16 copies the forward (stream 0's rows and activations)
+// and the head kernel (dZ_l, dHead) write beside their fp32 outputs (BwdArgs::t16).  Every operand
+// row of the tile's split-K slice -- BM dZ columns and BN X columns, kslice samples each -- is staged
+// into LDS by LDS-DMA (global_load_lds_dwordx4: a lane moves 8 consecutive samples of its column, a
+// wave-instruction 512 samples of one column) all at once, one wait, one barrier, then every MFMA of
+// the slice out of LDS.  No register staging, no per-pass barriers: k_dw_bf16's 16 dependent
+// load -> LDS -> barrier passes per slice were its bound (2.5 % of the bf16 peak, 18 % of HBM).
+// LDS rows are kslice bf16 + 16 bytes (1040 B at 512 samples: 4 dwords mod 64 per row, so the
+// ds_read_b128 fragment reads of 16 consecutive rows hit distinct banks).  The MFMA inputs, their
+// k order and the output slabs are k_dw_bf16's (bitwise equal: test_gpu_bf16_t16_dw_bit_identical).
+// Rows with no operand (dZ columns >= out, X columns > in) are zero; X column `in` is the ones column.
+template <int BM, int BN>
+__global__ __launch_bounds__(256) void k_dw_bf16t(BwdArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t dlds[];
+    constexpr int TM = BM / 32, TN = BN / 32;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int i = lane & 15, g = lane >> 4;
+    const int wm = wid >> 1, wn = wid & 1;
+    if (a.ptrack && blockIdx.x == 0) {   // k_per_update's tracking (as k_dw_bf16)
+        auto& tl = *reinterpret_cast<PerTrackLds<256>*>(dlds);
+        per_track_block<256, DQNX_BF16_TRACK_IPT, DQNX_BF16_TRACK_CARRY>(a.pprop, tl);
+        return;
+    }
+    int b = (int)blockIdx.x - a.ptrack;
+    {
+        int tiles = 0;
+        for (int p = 0; p < a.ndw; p++) tiles += a.dw[p].blocks;
+        if (b >= tiles) {
+            per_prop_block(a.pprop, (b - tiles) * 256, reinterpret_cast<double*>(dlds));
+            return;
+        }
+    }
+    int p = 0;
+    while (p + 1 < a.ndw && b >= a.dw[p].blocks) { b -= a.dw[p].blocks; p++; }
+    const DwProblem& d = a.dw[p];
+    b = xcd_remap(b, d.blocks);
+    const int bx = b % d.grid_x;
+    const int t2 = b / d.grid_x;
+    const int by = t2 % d.grid_y, bz = t2 / d.grid_y;
+    const int m0 = by * BM, n0 = bx * BN;
+    const int kb = bz * a.kslice;
+    const int ke = min(a.Bl, kb + a.kslice);
+    const int RB = a.kslice * 2 + 16;                 // LDS bytes per operand row
+    const int nk8 = (ke - kb) >> 3;                   // 8-sample pieces of this slice
+    const int ncz = d.out < d.cz ? d.out : d.cz;      // dZ columns that exist
+    char* lb = reinterpret_cast<char*>(dlds);
+    // (1) every row of both operands in flight at once: row q < BM is dZ column m0 + q, else X column
+    //     n0 + q - BM; the wave-instruction for (row, 512-sample segment) writes RB-aligned LDS bytes
+    for (int q = wid; q < BM + BN; q += 4) {
+        const bool isA = q < BM;
+        const int c = isA ? m0 + q : n0 + (q - BM);
+        char* row = lb + q * RB;
+        const bool have = isA ? c < ncz : c < d.in;
+        if (have) {
+            const uint16_t* src = isA ? d.dZT : d.XT;
+            const int C = isA ? d.cz : d.cx;
+            for (int s0 = 0; s0 < nk8; s0 += 64) {
+                const int k8 = s0 + lane;
+                if (k8 < nk8) {
+                    const int64_t bb = (int64_t)kb + 8 * k8;
+                    __builtin_amdgcn_global_load_lds(src + t16_index(bb, c, C),
+                                                     (__attribute__((address_space(3))) void*)(row + 16 * s0),
+                                                     16, 0, 0);
+                }
+            }
+        } else {   // zeros, or the ones column (bias)
+            const uint32_t v = (!isA && c == d.in) ? 0x3F803F80u : 0u;
+            for (int k8 = lane; k8 < nk8; k8 += 64)
+                *reinterpret_cast<uint4*>(row + 16 * k8) = make_uint4(v, v, v, v);
+        }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    // (2) the slice's MFMAs, chunk order as k_dw_bf16 (32 samples per 16x16x32 MFMA)
+    floatx4 acc[TM][TN];
+#pragma unroll
+    for (int tm = 0; tm < TM; tm++)
+#pragma unroll
+        for (int tn = 0; tn < TN; tn++) acc[tm][tn] = floatx4{0.f, 0.f, 0.f, 0.f};
+    const int nch = (ke - kb) >> 5;
+    const char* pa = lb + (wm * 16 * TM + i) * RB + 16 * g;
+    const char* pb = lb + (BM + wn * 16 * TN + i) * RB + 16 * g;
+    for (int ch = 0; ch < nch; ch++) {
+        u32x4 fa[TM], fb[TN];
+#pragma unroll
+        for (int t = 0; t < TM; t++) fa[t] = *reinterpret_cast<const u32x4*>(pa + t * 16 * RB + 64 * ch);
+#pragma unroll
+        for (int t = 0; t < TN; t++) fb[t] = *reinterpret_cast<const u32x4*>(pb + t * 16 * RB + 64 * ch);
+#pragma unroll
+        for (int tm = 0; tm < TM; tm++)
+#pragma unroll
+            for (int tn = 0; tn < TN; tn++) acc[tm][tn] = mfma16x16x32bf16(fa[tm], fb[tn], acc[tm][tn]);
+    }
+    float* part = d.partial + (int64_t)bz * d.pstride;
+#pragma unroll
+    for (int tn = 0; tn < TN; tn++) {
+        const int col = n0 + wn * 16 * TN + tn * 16 + i;
+        if (col > d.in) continue;
+#pragma unroll
+        for (int tm = 0; tm < TM; tm++)
+#pragma unroll
+            for (int r = 0; r < 4; r++) {
+                const int row = m0 + wm * 16 * TM + tm * 16 + 4 * g + r;
+                if (row >= d.out) continue;
+                int64_t o;
+                if (d.head_kind < 0) o = (col < d.in) ? (int64_t)row * d.in + col : (int64_t)d.out * d.in + row;
+                else o = (col < d.in) ? head_w_off(d.head_kind, row, d.in) + col : head_b_off(d.head_kind, row, d.in, d.A);
+                part[o] = acc[tm][tn][r];
+            }
+    }
+}
+
 // Tile shape (BM x BN): 64 x 64 when that still gives >= 512 workgroups (large batches: fewer operand
 // re-reads), else 32 x 32 (B=1024: 132 workgroups of 64 x 64 left the chip idle).  DQNX_DWB_SHAPE
 // (tuning builds): 1 = 32 x 32, 2 = 64 x 64, 3 = 128 x 128, 4 = 128 x 64.
@@ -1039,11 +1192,41 @@ void dw_bf16_grid(BwdArgs& a) {
     }
 }
 
+// k_dw_bf16t's LDS: every operand row of a tile's slice (kslice bf16 + 16 bytes each)
+static size_t dw_bf16t_lds_bytes(int bm, int bn, int kslice) { return (size_t)(bm + bn) * (kslice * 2 + 16); }
+
+bool dw_bf16t_supported(const BwdArgs& a) {
+    const DwbTile t = dw_bf16_tile(a);
+    return a.kslice % 32 == 0 && a.Bl % 32 == 0 && ((t.bm == 64 && t.bn == 64) || (t.bm == 32 && t.bn == 32)) &&
+           dw_bf16t_lds_bytes(t.bm, t.bn, a.kslice) <= 160 * 1024;
+}
+
 int launch_dw_bf16(const BwdArgs& a, hipStream_t s) {
     int blocks = a.pprop_wgs + a.ptrack;   // (+ k_per_prop's workgroups: 256 updates each, after the
                                             // tiles; + the tracking workgroup, block 0)
     if (a.ptrack && a.pprop.n > PER_CHUNK) return set_error(DQNX_EINVAL, "dw_bf16: PER tracking chunk %d", a.pprop.n);
     for (int p = 0; p < a.ndw; p++) blocks += a.dw[p].blocks;
+    if (a.t16) {
+        const DwbTile t = dw_bf16_tile(a);
+        size_t shm = dw_bf16t_lds_bytes(t.bm, t.bn, a.kslice);
+        if (a.kslice % 32 || a.Bl % 32 || shm > 160 * 1024)
+            return set_error(DQNX_EUNSUPPORTED, "dw_bf16t: slices / batch a multiple of 32 samples, LDS <= 160 KB");
+        for (int p = 0; p < a.ndw; p++)
+            if (!a.dw[p].dZT || !a.dw[p].XT) return set_error(DQNX_EINVAL, "dw_bf16t: T16 operand missing");
+        if (shm < sizeof(PerTrackLds<256>)) shm = sizeof(PerTrackLds<256>);
+        if (shm < PER_TOP * sizeof(double)) shm = PER_TOP * sizeof(double);
+        if (t.bm == 64 && t.bn == 64) {
+            allow_lds(k_dw_bf16t<64, 64>, 160 * 1024);
+            hipLaunchKernelGGL((k_dw_bf16t<64, 64>), dim3(blocks), dim3(256), shm, s, a);
+        } else if (t.bm == 32 && t.bn == 32) {
+            allow_lds(k_dw_bf16t<32, 32>, 160 * 1024);
+            hipLaunchKernelGGL((k_dw_bf16t<32, 32>), dim3(blocks), dim3(256), shm, s, a);
+        } else {
+            return set_error(DQNX_EUNSUPPORTED, "dw_bf16t: %dx%d tiles", t.bm, t.bn);
+        }
+        DQNX_HIP_CHECK(hipGetLastError());
+        return DQNX_OK;
+    }
     for (int p = 0; p < a.ndw; p++)   // 16-byte row loads
         if (a.dw[p].ldx % 4 || a.dw[p].ldz % 4)
             return set_error(DQNX_EUNSUPPORTED, "bf16 weight gradients need row strides that are multiples of 4");
@@ -1110,15 +1293,11 @@ int fused_wblk_bytes(bool bf16, int rows, int kpad) { return rows * kpad * (bf16
 #ifndef DQNX_HEAD_LDS_PAD
 #define DQNX_HEAD_LDS_PAD 0
 #endif
-template <class K>
-static void allow_lds(K kern, size_t bytes) {
-    if (bytes > 64 * 1024) (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
-}
 
 int launch_fused_fwd(const FusedFwdArgs& a, int act, hipStream_t s) {
-    if (a.phase != 0 && (a.L < 2 || a.mr != (a.phase == 1 ? a.mr : 1) || (a.phase == 1 && a.mr > 2) ||
+    if (a.phase != 0 && (a.L < 2 || a.mr != (a.phase == 1 ? a.mr : 1) ||
                          (a.phase == 1 && (a.csplit < 1 || a.out[0] % (16 * a.csplit)))))
-        return set_error(DQNX_EUNSUPPORTED, "split forward: L >= 2, 16-row tiles (layer 1: 16 or 32), layer 1 width / parts a multiple of 16");
+        return set_error(DQNX_EUNSUPPORTED, "split forward: L >= 2, 16-row tiles (layer 1: 16, 32 or 64), layer 1 width / parts a multiple of 16");
     if (a.gw && (a.phase != 0 || a.mr != 1))
         return set_error(DQNX_EUNSUPPORTED, "fused forward: rows wider than %d columns take the one-launch 16-row plan", 4 * FWD_NARROW_Q4);
     if (a.samp_shape && (a.phase == 2 || a.samp_shape > 3 || a.samp.k > FWD_SAMPLE_MAX_K ||
@@ -1148,7 +1327,8 @@ int launch_fused_fwd(const FusedFwdArgs& a, int act, hipStream_t s) {
     do {                                                                                             \
         if (a.phase == 1) {                                                                          \
             if constexpr (NLV >= 2) {                                                                \
-                if (a.mr == 2) FUSED_FWD_MR(ACTV, NLV, BFV, 2, 1);                                   \
+                if (a.mr == 4) FUSED_FWD_MR(ACTV, NLV, BFV, 4, 1);                                   \
+                else if (a.mr == 2) FUSED_FWD_MR(ACTV, NLV, BFV, 2, 1);                              \
                 else FUSED_FWD_MR(ACTV, NLV, BFV, 1, 1);                                             \
             }                                                                                        \
         }                                                                                            \

@@ -111,7 +111,19 @@ struct DwProblem {
     int head_kind;         // -1 plain Linear layout, else dqnx_head_kind
     int A;                 // actions (head layout)
     int grid_x, grid_y, blocks;   // filled by bwd_level_grid
+    // k_dw_bf16t (BwdArgs::t16): the same operands as bf16 copies in the T16 layout (t16_index):
+    // dZ with cz columns, X with cx columns; X's column `in` is the ones column (the bias), not stored
+    const uint16_t* dZT;
+    const uint16_t* XT;
+    int cz, cx;
 };
+// T16 layout of a bf16 operand with C columns over the minibatch: element (sample b, column c) at
+// ((b >> 4) * C + c) * 16 + (b & 15) -- 16 consecutive samples of one column contiguous (32 bytes),
+// so the bf16 weight-gradient kernel fetches 8 consecutive samples of a column as one 16-byte piece
+// and its producers (the forward's stream 0, the head kernel) write whole 16-row tiles contiguously.
+__host__ __device__ __forceinline__ int64_t t16_index(int64_t b, int c, int C) {
+    return ((b >> 4) * C + c) * 16 + (b & 15);
+}
 struct BwdArgs {
     // dx role (skipped when dZprev == null): dZprev = (dZ W) (.) act'(Hprev)
     const float* dZ;       // [Bl][out]
@@ -125,6 +137,7 @@ struct BwdArgs {
     int ndw;
     int Bl, kslice, dw_slices;
     int dx_blocks, dx_grid_x;
+    int t16;               // bf16 weight gradients from the T16 copies (k_dw_bf16t) instead of fp32 rows
     int pprop_wgs;         // k_dw_bf16: + workgroups running k_per_prop's body (single-GPU PER step)
     int ptrack;            // k_dw_bf16: + block 0 running k_per_update's tracking (its prop in the Adam launch)
     PerUpdateArgs pprop;
@@ -461,6 +474,8 @@ struct FusedFwdArgs {
     const int32_t* phys;         // [Bl] physical ring slots
     float* xcopy;                // [Bl][ring_stride] stream-0 gathered rows (layer-1 dW operand)
     float* H[FUSED_MAX_L];       // stream-0 activations [Bl][out_l]
+    uint16_t* xT16;              // bf16 + k_dw_bf16t: stream 0's rows / activations as T16 copies (or null)
+    uint16_t* HT16[FUSED_MAX_L];
     float* raw;                  // [3][Bl][16] head outputs per logical stream
     float4* trans;               // [Bl] stream 0: {act (int bits), rew, done, 0} of each sampled slot
     const int32_t* act;          // replay ring columns (gathered for `trans`)
@@ -537,6 +552,8 @@ struct HeadBwdArgs {
     const float* H[FUSED_MAX_L]; // stream-0 activations
     float* dZ[FUSED_MAX_L];      // [Bl][out_l]
     float* dhead;                // [Bl][16]
+    uint16_t* dZT16[FUSED_MAX_L];   // bf16 + k_dw_bf16t: T16 copies of dZ_l / dHead (or null)
+    uint16_t* dheadT16;
     float* loss_partial;         // [tiles]
     dqnx_ctrl* ctrl;
     const float* wblkT[FUSED_MAX_L];     // chain-blocked online W_l, l >= 1 (relayout.hpp)
@@ -551,6 +568,7 @@ int launch_fused_fwd(const FusedFwdArgs& a, int act, hipStream_t s);
 int launch_head_bwd(const HeadBwdArgs& a, int act, hipStream_t s);
 void dw_bf16_grid(BwdArgs& a);                               // 64x64 tiles of k_dw_bf16
 int launch_dw_bf16(const BwdArgs& a, hipStream_t s);          // bf16 split-K weight gradients
+bool dw_bf16t_supported(const BwdArgs& a);                   // k_dw_bf16t fits (after dw_bf16_grid)
 
 // ---- implicit-GEMM convolutions (conv_ig.hip): the (4,84,84) variant's convs without
 //      materialised column matrices ----

@@ -219,3 +219,30 @@ def test_gpu_bf16_prefetch_bit_identical(batch):
     torch.cuda.synchronize()
     assert torch.equal(e1.params, e2.params) and torch.equal(e1.target_params, e2.target_params)
     assert np.array_equal(e1.get_rng(0), e2.get_rng(0))
+
+
+@pytest.mark.parametrize("algo,batch,per,mr", [
+    ("DuelingDoubleDQNAgent", 1024, False, "1"),      # 32 x 32 tiles, 2 slabs, 16-row forward
+    ("DuelingDoubleDQNAgent", 8192, False, None),     # 64 x 64 tiles, 16 slabs of 512 samples
+    ("DQNAgent", 4096, False, "2"),                   # linear head, 32-row forward tiles
+    ("PerDuelingDoubleDQNAgent", 8192, True, None),   # configs[4]: + the tracking / prop workgroups
+])
+def test_gpu_bf16_t16_dw_bit_identical(monkeypatch, algo, batch, per, mr):
+    """k_dw_bf16t (operands from the T16 bf16 copies the forward and the head kernel write, staged by
+    LDS-DMA) against k_dw_bf16 (fp32 rows rounded and transposed through registers): the same bf16
+    operands, the same 32-sample MFMA chunks, the same slabs -- weights, Adam state and (PER) tree
+    bitwise equal after three steps."""
+    if mr is not None:
+        monkeypatch.setenv("DQNX_FWD_MR", mr)
+    outs = []
+    for t16 in ("0", "1"):
+        monkeypatch.setenv("DQNX_DWB_T", t16)
+        _, _, eng = make_bf16_pair(algo, 284, batch, 3 * batch, 3 * batch, 71, per=per, graphs=False)
+        for _ in range(3):
+            eng.learn_step(soft_update=True)
+        torch.cuda.synchronize()
+        eng.check_device_error()
+        outs.append([eng.params.clone(), eng.target_params.clone(), eng.adam_m.clone(), eng.adam_v.clone(),
+                     eng.grads.clone()] + ([eng.sumtree.clone()] if per else []))
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)

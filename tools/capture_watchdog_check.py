@@ -41,15 +41,22 @@ dist.all_reduce(x)   # communicator warm-up
 torch.cuda.synchronize()
 
 # 1-2: an incomplete collective in the watchdog's list across a held-open capture
+g2 = dist.new_group([0]) if mode == "nccl_group2" else None
+if g2 is not None:
+    dist.all_reduce(x, group=g2)   # (its communicator warm-up)
+    torch.cuda.synchronize()
 torch.cuda._sleep(int(2.0e9))   # ~1 s of spinning at the loaded clock
 dist.all_reduce(x)
 side = torch.cuda.Stream(dev)
 y = torch.zeros(1 << 16, device=dev)
 g = torch.cuda.CUDAGraph()
 t0 = time.perf_counter()
+cmode = CAPTURE_MODE if mode == "package" else ("global" if mode.startswith("nccl") else mode)
 with torch.cuda.stream(side):   # (torch.cuda.graph would synchronise first and let the work complete)
-    g.capture_begin(capture_error_mode=CAPTURE_MODE if mode == "package" else mode)
+    g.capture_begin(capture_error_mode=cmode)
     y.add_(1.0)
+    if mode.startswith("nccl"):   # a captured collective: the PG's NCCL stream joins the capture
+        dist.all_reduce(y, group=g2)
     time.sleep(0.6)
     g.capture_end()
 held = time.perf_counter() - t0
