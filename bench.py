@@ -812,10 +812,22 @@ def dropin_loop(args, device, batch=1024, iters=200, warmup=20):
         agent.flush()
         torch.cuda.synchronize(device)
         t_all = time.perf_counter() - t_start
+        # choose_actions with no learn step in flight (R:train.py's loop with a real env: env.step -- 40
+        # TraCI simulation steps, R:env/custom_env/rl_controller.py:211-250 -- runs between learn() and
+        # the next choose_actions, so the step has finished): host obs in, action list out
+        idle = []
+        for t in range(100):
+            torch.cuda.synchronize(device)
+            t0 = time.perf_counter()
+            agent.choose_actions(obs[t:t + 1])
+            idle.append(time.perf_counter() - t0)
+        idle.sort()
         del agent
         torch.cuda.empty_cache()
         return {"us_per_iteration": t_all / iters * 1e6, "learn_tr_per_s": batch * iters / t_all,
-                "phases_us": {k: v / iters * 1e6 for k, v in phases.items()}}
+                "phases_us": {k: v / iters * 1e6 for k, v in phases.items()},
+                "choose_actions_idle_us": {"median": idle[len(idle) // 2] * 1e6, "p10": idle[len(idle) // 10] * 1e6,
+                                           "p90": idle[(9 * len(idle)) // 10] * 1e6}}
 
     keys = ("DQNX_AGENT_DEFER", "DQNX_AGENT_GRAPHS", "DQNX_AGENT_MT_INPLACE")
     saved = {k: os.environ.get(k) for k in keys}
@@ -837,7 +849,9 @@ def dropin_loop(args, device, batch=1024, iters=200, warmup=20):
                      "stages random._inst in place and launches the step in one library call), `deferred_fused` "
                      "DQNX_AGENT_DEFER=1, `graphed_step` the learn step as one HIP graph launch "
                      "(DQNX_AGENT_GRAPHS=1), `portable_rng` the getstate / getrandbits hand-off "
-                     "(DQNX_AGENT_MT_INPLACE=0)")
+                     "(DQNX_AGENT_MT_INPLACE=0); phases_us.choose_actions includes waiting for the learn step "
+                     "launched in the previous iteration (no env.step in this loop), choose_actions_idle_us is "
+                     "the call with the GPU idle, as after a real env.step")
 
 
 def main():

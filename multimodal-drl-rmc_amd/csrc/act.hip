@@ -15,6 +15,8 @@
 //     per pass with all of a pass's loads in flight before the first FMA;
 //   * the argmax (first maximal index, like torch.argmax) is one thread per row.
 // Rows are processed R = 1, 2 or 4 at a time per workgroup column (grid.y = row groups).
+#include <algorithm>
+
 #include "common.hpp"
 #include "learn.hpp"
 
@@ -237,12 +239,162 @@ __global__ __launch_bounds__(kActThreads) void k_act_mlp(ActArgs a) {
             if (v > bv || (v != v && bv == bv)) { bv = v; best = j; }   // first max; NaN wins like torch
         }
         a.actions[row0 + r] = best;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (r == 0 && grp == 0 && gridDim.y == 1 && a.done_flag)
+            __hip_atomic_store(a.done_flag, a.done_seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     }
+}
+
+// The completion word for dqnx_act_host: system-scope release after the actions' stores, so the
+// host sees the actions once it sees done_seq (fine-grained pinned memory)
+__device__ __forceinline__ void act_signal(const ActArgs& a) {
+    if (a.done_flag) __hip_atomic_store(a.done_flag, a.done_seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// Two hidden layers (the reference's MLP bodies): layer 2 is summed in parts where layer 1 is made.
+// Workgroup w owns layer-1 neurons [16 w, 16 w + 16) (one per wave, as k_act_mlp) and also forms
+// their share of every layer-2 pre-activation, p_w[r][o] = sum_{k < 16} W2[o][16 w + k] h1[r][16 w + k];
+// the last workgroup to arrive sums the G shares in w order (+ b2, activation), then runs the head
+// (advantage stream for dueling nets) and the first-max argmax.  Against k_act_mlp the tail after the
+// hand-off no longer waits on a weight load of its own: layer 2's weights and the head's are fetched
+// at the top of the kernel, beside layer 1's, and the hand-off moves G floats per layer-2 neuron.
+// The shares go out as write-through (sc1) stores, so the producers need no release fence (the
+// last arriver's acquire stays: cdna_hip_programming.md Guideline 16, the sc1 form of the recipe).
+template <int R, int ACT>
+__global__ __launch_bounds__(kActThreads) void k_act_mlp2(ActArgs a) {
+    extern __shared__ float lds[];
+    __shared__ int s_last;
+    float* x = lds;                      // [R][ld] obs, later h2
+    float* h1 = lds + R * a.ld;          // [R][16] this workgroup's layer-1 outputs, later Q [R][16]
+    float* hw = h1 + R * 16;             // [A][F] head weights (last arriver)
+    const int grp = blockIdx.y;
+    const int row0 = grp * R;
+    const int nr = min(R, a.n - row0);
+    const int tid = threadIdx.x;
+    const int G = gridDim.x;
+    const int h0 = a.out[0], o1 = a.out[1], F = a.F, A = a.A;
+    const int k0 = blockIdx.x * kActWaves;
+    const int nk = min(kActWaves, h0 - k0);
+    // (0) loads that do not depend on the observation, first: this thread's layer-2 weights (row
+    //     o = tid, the workgroup's 16 columns) and bias, and a float4 of the head's weights
+    const float* W2 = a.params + a.off[1];
+    float w2[kActWaves];
+#pragma unroll
+    for (int k = 0; k < kActWaves; k++) w2[k] = (tid < o1 && k < nk) ? W2[(int64_t)tid * h0 + k0 + k] : 0.f;
+    const float b2 = tid < o1 ? W2[(int64_t)o1 * h0 + tid] : 0.f;
+    const float* Hh = a.params + a.head_off;
+    const float* Wh = a.dueling ? Hh + F + 1 : Hh;   // advantage stream (R:dqn/network.py:110-117)
+    const int nh4 = (A * F) >> 2;                     // (A * F % 4 == 0 and 16-byte rows: act2_ok)
+    const float4 hwv = tid < nh4 ? ld4(Wh + 4 * tid) : make_float4(0.f, 0.f, 0.f, 0.f);
+    const float hb = tid < A ? Wh[(int64_t)A * F + tid] : 0.f;
+    for (int i = tid; i < R * a.D; i += kActThreads) {
+        const int r = i / a.D, k = i - r * a.D;
+        x[r * a.ld + k] = r < nr ? a.obs[(int64_t)(row0 + r) * a.D + k] : 0.f;
+    }
+    __syncthreads();
+    // (1) layer 1: neuron k0 + wave of every row into LDS
+    {
+        const int j = k0 + tid / kWave;
+        const float* W = a.params + a.off[0];
+        if (j < h0) {
+            if ((a.D & 3) == 0 && (a.off[0] & 3) == 0 && (a.ld & 3) == 0)
+                act_layer1_neuron<R, ACT, true>(W, W + (int64_t)h0 * a.D, a.D, j, x, a.ld, h1 - k0, 16);
+            else
+                act_layer1_neuron<R, ACT, false>(W, W + (int64_t)h0 * a.D, a.D, j, x, a.ld, h1 - k0, 16);
+        }
+    }
+    __syncthreads();
+    // (2) this workgroup's share of layer 2, written through (sc1) to memory
+    float* part = a.scratch + (int64_t)grp * G * R * o1;   // [G][R][o1] of this row group
+    if (tid < o1) {
+#pragma unroll
+        for (int r = 0; r < R; r++) {
+            float acc = 0.f;
+#pragma unroll
+            for (int k = 0; k < kActWaves; k++) acc = fmaf(w2[k], h1[r * 16 + k], acc);
+            __hip_atomic_store(part + ((int64_t)blockIdx.x * R + r) * o1 + tid, acc, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (G > 1) {
+        if (tid == 0) {
+            const uint32_t t = __hip_atomic_fetch_add(a.tickets - grp, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const int last = t == (uint32_t)G - 1;
+            if (last) {
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                *(a.tickets - grp) = 0;   // ready for the next launch
+            }
+            s_last = last;
+        }
+        __syncthreads();
+        if (!s_last) return;
+    }
+    // (3) last arriver: h2 = act(sum of the shares in workgroup order + b2), the head, argmax
+    if (tid < nh4) *reinterpret_cast<float4*>(hw + 4 * tid) = hwv;
+    if (tid < o1) {
+#pragma unroll
+        for (int r = 0; r < R; r++) {
+            float z = 0.f;
+            for (int w = 0; w < G; w++)
+                z += __hip_atomic_load(part + ((int64_t)w * R + r) * o1 + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            x[r * a.ld + tid] = act_fwd<ACT>(z + b2);
+        }
+    }
+    const float hbj = __shfl(hb, tid & 15, kWave);   // (bias of head output tid % 16, from lane tid % 16)
+    __syncthreads();
+    float* q = h1;
+    if (tid < R * 16) {
+        const int r = tid >> 4, j = tid & 15;
+        if (j < A) {
+            const float* xr = x + r * a.ld;
+            const float* wr = hw + j * F;
+            float acc = 0.f;
+            for (int k = 0; k < F; k++) acc = fmaf(wr[k], xr[k], acc);
+            q[r * 16 + j] = acc + hbj;
+        }
+    }
+    __syncthreads();
+    if (tid < nr) {
+        const int r = tid;
+        const float* qr = q + r * 16;
+        int best = 0;
+        float bv = qr[0];
+        for (int j = 0; j < A; j++) {
+            const float v = qr[j];
+            if (a.values) a.values[(int64_t)(row0 + r) * A + j] = v;
+            if (v > bv || (v != v && bv == bv)) { bv = v; best = j; }   // first max; NaN wins like torch
+        }
+        a.actions[row0 + r] = best;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (r == 0 && grp == 0 && gridDim.y == 1) act_signal(a);   // (one row group: n <= R)
+    }
+}
+
+// k_act_mlp2 applies: two hidden layers, layer 2 on one thread per neuron, the head's advantage / Q
+// rows as float4s of one pass (A * F % 4 == 0, 16-byte aligned, <= 4096 floats), A <= 16; with a
+// completion word, one row group (act_signal stores it from row group 0)
+static bool act2_ok(const ActArgs& a, int R) {
+    const int64_t hoff = a.head_off + (a.dueling ? a.F + 1 : 0);
+    return a.L == 2 && a.out[1] <= kActThreads && a.A <= 16 && (a.A * a.F) % 4 == 0 &&
+           a.A * a.F <= 4 * kActThreads && (hoff & 3) == 0 && (a.done_flag == nullptr || a.n <= R) &&
+           route_knob("DQNX_ACT2", 1) != 0;
 }
 
 template <int R>
 int launch_act_r(const ActArgs& a, hipStream_t s) {
     const dim3 grid((a.out[0] + kActWaves - 1) / kActWaves, (a.n + R - 1) / R);
+    if (act2_ok(a, R)) {
+        const size_t lds2 = ((size_t)R * a.ld + R * 16 + (size_t)a.A * a.F) * sizeof(float);
+        if (a.act == DQNX_ACT_RELU)
+            hipLaunchKernelGGL((k_act_mlp2<R, DQNX_ACT_RELU>), grid, dim3(kActThreads), lds2, s, a);
+        else
+            hipLaunchKernelGGL((k_act_mlp2<R, DQNX_ACT_ELU>), grid, dim3(kActThreads), lds2, s, a);
+        DQNX_HIP_CHECK(hipGetLastError());
+        return DQNX_OK;
+    }
     const size_t lds = (size_t)2 * R * a.ld * sizeof(float);
     if (a.act == DQNX_ACT_RELU)
         hipLaunchKernelGGL((k_act_mlp<R, DQNX_ACT_RELU>), grid, dim3(kActThreads), lds, s, a);
@@ -260,11 +412,14 @@ int act_rows_per_block(int n, int ld) {
     return (size_t)2 * R * ld * sizeof(float) > kActMaxLds ? 0 : R;
 }
 
-uint64_t act_scratch_bytes(int n, int h0, int ld) {
+uint64_t act_scratch_bytes(int n, int h0, int ld, int L, int out1) {
     const int R = act_rows_per_block(n, ld);
     if (R == 0 || n <= 0) return 0;
     const int64_t groups = (n + R - 1) / R;
-    return (uint64_t)groups * R * h0 * sizeof(float) + (uint64_t)groups * 4;
+    // per row group: k_act_mlp's [R][h0] layer-1 outputs, or k_act_mlp2's [G][R][out1] layer-2 shares
+    const int64_t G = (h0 + kActWaves - 1) / kActWaves;
+    const int64_t per = std::max<int64_t>((int64_t)R * h0, L >= 2 ? G * R * out1 : 0);
+    return (uint64_t)groups * per * sizeof(float) + (uint64_t)groups * 4;
 }
 
 int launch_act(const ActArgs& a, hipStream_t s) {

@@ -7,6 +7,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <chrono>
 #include <cmath>
 #include <functional>
 #include <map>
@@ -3700,13 +3701,24 @@ uint64_t dqnx_act_scratch_bytes(const dqnx_net_desc* net, int32_t n) {
     NetPlan np;
     ActArgs a;
     if (act_plan(net, np, a)) return 0;
-    const uint64_t mlp = act_scratch_bytes(n, a.out[0], a.ld);
+    const uint64_t mlp = act_scratch_bytes(n, a.out[0], a.ld, a.L, a.L >= 2 ? a.out[1] : 0);
     if (!mlp) return 0;
     return (net->kind == DQNX_NET_MLP ? 0 : act_conv_scratch_bytes(np, n, a.D)) + mlp;
 }
 
+// done_flag: the MLP acting kernel stores done_seq there (system scope) after the actions (dqnx_act_host)
+static int act_impl(const dqnx_net_desc* net, const float* params, const float* obs, int32_t n, int32_t* actions,
+                    float* values, void* scratch, uint64_t scratch_bytes, void* stream, uint32_t* done_flag,
+                    uint32_t done_seq);
+
 int dqnx_act(const dqnx_net_desc* net, const float* params, const float* obs, int32_t n, int32_t* actions,
              float* values, void* scratch, uint64_t scratch_bytes, void* stream) {
+    return act_impl(net, params, obs, n, actions, values, scratch, scratch_bytes, stream, nullptr, 0);
+}
+
+static int act_impl(const dqnx_net_desc* net, const float* params, const float* obs, int32_t n, int32_t* actions,
+                    float* values, void* scratch, uint64_t scratch_bytes, void* stream, uint32_t* done_flag,
+                    uint32_t done_seq) {
     NetPlan np;
     ActArgs a;
     int rc = act_plan(net, np, a);
@@ -3716,6 +3728,8 @@ int dqnx_act(const dqnx_net_desc* net, const float* params, const float* obs, in
     if (n > 0 && act_rows_per_block(n, a.ld) == 0)
         return set_error(DQNX_EUNSUPPORTED, "dqnx_act: layer width %d does not fit LDS", a.ld);
     a.params = params; a.obs = obs; a.actions = actions; a.values = values; a.n = n;
+    a.done_flag = net->kind == DQNX_NET_MLP ? done_flag : nullptr;
+    a.done_seq = done_seq;
     if (n == 0) return DQNX_OK;
     const uint64_t need = dqnx_act_scratch_bytes(net, n);
     if (scratch_bytes < need || (scratch_bytes & 3) || ((uintptr_t)scratch & 15))
@@ -3957,10 +3971,12 @@ int dqnx_act_host(const dqnx_net_desc* net, const float* params, const float* ob
     int32_t* d_act = (int32_t*)(sc + ob);
     void* act_sc = sc + ob + ab;
     const uint64_t act_bytes = scratch_bytes - ob - ab;
-    // pinned staging, per thread, grown as needed
+    // pinned staging, per thread, grown as needed: [obs n x D][actions n][completion word]
     static thread_local char* pin = nullptr;
     static thread_local size_t pin_bytes = 0;
-    const size_t want = (size_t)n * net->obs_dim * 4 + (size_t)n * 4;
+    static thread_local uint32_t seq = 0;
+    const size_t flag_at = ((size_t)n * net->obs_dim * 4 + (size_t)n * 4 + 63) / 64 * 64;
+    const size_t want = flag_at + 64;
     hipStream_t s = (hipStream_t)stream;
     if (pin_bytes < want) {
         if (pin) {
@@ -3974,18 +3990,34 @@ int dqnx_act_host(const dqnx_net_desc* net, const float* params, const float* ob
     }
     if (net->kind == DQNX_NET_MLP) {
         // one launch: the acting kernel reads the obs from and writes the actions to the pinned,
-        // fine-grained block in place (no copy calls), then one synchronisation
+        // fine-grained block in place (no copy calls) and then a completion word, which the host
+        // polls instead of synchronising the stream (the wake-up of a stream synchronisation costs
+        // more than the kernel); a kernel that never signals ends the poll after ~0.5 s, and the
+        // stream synchronisation then reports its error
         memcpy(pin, obs_host, (size_t)n * net->obs_dim * 4);
         int32_t* pa = (int32_t*)(pin + (size_t)n * net->obs_dim * 4);
-        int rc = dqnx_act(net, params, (const float*)pin, n, pa, nullptr, act_sc, act_bytes, stream);
+        volatile uint32_t* flag = (volatile uint32_t*)(pin + flag_at);
+        const uint32_t want_seq = ++seq ? seq : ++seq;   // (never 0)
+        int rc = act_impl(net, params, (const float*)pin, n, pa, nullptr, act_sc, act_bytes, stream,
+                          (uint32_t*)(pin + flag_at), want_seq);
         if (rc) return rc;
-        DQNX_HIP_CHECK(hipStreamSynchronize(s));
+        const bool polled = n <= 4 && route_knob("DQNX_ACT_POLL", 1) != 0;   // (one row group signals)
+        bool seen = false;
+        if (polled) {
+            const auto t0 = std::chrono::steady_clock::now();
+            for (uint64_t it = 0;; it++) {
+                if (__atomic_load_n(flag, __ATOMIC_ACQUIRE) == want_seq) { seen = true; break; }
+                if ((it & 1023) == 1023 && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(500)) break;
+                __builtin_ia32_pause();
+            }
+        }
+        if (!seen) DQNX_HIP_CHECK(hipStreamSynchronize(s));
         memcpy(actions_host, pa, (size_t)n * 4);
         return DQNX_OK;
     }
     memcpy(pin, obs_host, (size_t)n * net->obs_dim * 4);
     DQNX_HIP_CHECK(hipMemcpyAsync(d_obs, pin, (size_t)n * net->obs_dim * 4, hipMemcpyHostToDevice, s));
-    int rc = dqnx_act(net, params, d_obs, n, d_act, nullptr, act_sc, act_bytes, stream);
+    int rc = act_impl(net, params, d_obs, n, d_act, nullptr, act_sc, act_bytes, stream, nullptr, 0);
     if (rc) return rc;
     int32_t* pa = (int32_t*)(pin + (size_t)n * net->obs_dim * 4);
     DQNX_HIP_CHECK(hipMemcpyAsync(pa, d_act, (size_t)n * 4, hipMemcpyDeviceToHost, s));

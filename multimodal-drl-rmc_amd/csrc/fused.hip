@@ -1215,11 +1215,15 @@ int launch_dw_bf16(const BwdArgs& a, hipStream_t s) {
             if (!a.dw[p].dZT || !a.dw[p].XT) return set_error(DQNX_EINVAL, "dw_bf16t: T16 operand missing");
         if (shm < sizeof(PerTrackLds<256>)) shm = sizeof(PerTrackLds<256>);
         if (shm < PER_TOP * sizeof(double)) shm = PER_TOP * sizeof(double);
+        // (the attribute only past 64 KB, and exactly the bytes requested: a failed hipFuncSetAttribute
+        // -- static LDS + a 160 KB maximum -- would be the launch's hipGetLastError)
         if (t.bm == 64 && t.bn == 64) {
-            allow_lds(k_dw_bf16t<64, 64>, 160 * 1024);
+            if (shm > 64 * 1024)
+                DQNX_HIP_CHECK(hipFuncSetAttribute((const void*)k_dw_bf16t<64, 64>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm));
             hipLaunchKernelGGL((k_dw_bf16t<64, 64>), dim3(blocks), dim3(256), shm, s, a);
         } else if (t.bm == 32 && t.bn == 32) {
-            allow_lds(k_dw_bf16t<32, 32>, 160 * 1024);
+            if (shm > 64 * 1024)
+                DQNX_HIP_CHECK(hipFuncSetAttribute((const void*)k_dw_bf16t<32, 32>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm));
             hipLaunchKernelGGL((k_dw_bf16t<32, 32>), dim3(blocks), dim3(256), shm, s, a);
         } else {
             return set_error(DQNX_EUNSUPPORTED, "dw_bf16t: %dx%d tiles", t.bm, t.bn);

@@ -773,6 +773,10 @@ struct ActArgs {
     int in[kActMaxDense], out[kActMaxDense];
     int64_t off[kActMaxDense];
     int64_t head_off;
+    // dqnx_act_host: the last arriver stores done_seq here (system scope, after the actions) and the
+    // host polls it instead of synchronising the stream (null: no flag)
+    uint32_t* done_flag;
+    uint32_t done_seq;
 };
 // two-stream acting: one conv layer over n rows (act_hybrid.hip); images CHW, rows strided
 struct ActConvArgs {
@@ -785,7 +789,7 @@ struct ActConvArgs {
 size_t act_conv_lds_bytes(const ActConvArgs& a);
 int launch_act_conv(const ActConvArgs& a, hipStream_t s);
 int act_rows_per_block(int n, int ld);
-uint64_t act_scratch_bytes(int n, int h0, int ld);
+uint64_t act_scratch_bytes(int n, int h0, int ld, int L, int out1);
 int launch_act(const ActArgs& a, hipStream_t s);
 int launch_soft_update(float* target, const float* p, int64_t n, float tau, float omt, hipStream_t s);
 int launch_replay_push(const PushArgs& a, hipStream_t s);

@@ -149,6 +149,8 @@ def test_act_argument_checks_without_gpu():
     assert L.dqnx_act(ctypes.byref(mlp), None, None, 4, None, None, None, 0, None) == C.DQNX_EINVAL
     assert L.dqnx_act(ctypes.byref(mlp), None, None, 0, None, None, None, 0, None) == C.DQNX_OK
     need = L.dqnx_act_scratch_bytes(ctypes.byref(mlp), 3)
-    assert need == 4 * 256 * 4 + 4    # one group of R = 4 rows of layer-1 activations + its ticket
+    # one group of R = 4 rows: the larger of k_act_mlp's layer-1 activations [4][256] and k_act_mlp2's
+    # layer-2 shares [16 workgroups][4][128], + its ticket
+    assert need == max(4 * 256, 16 * 4 * 128) * 4 + 4
     # too small a scratch is refused before any launch
     assert L.dqnx_act(ctypes.byref(mlp), 16, 16, 3, 16, None, 16, need - 4, None) == C.DQNX_EINVAL

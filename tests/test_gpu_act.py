@@ -181,3 +181,26 @@ def test_gpu_act_host_shared_scratch_across_row_counts(net):
         with torch.no_grad():
             ref = O.advantages(ospec, params, torch.from_numpy(x)).numpy()
         _check(vals.cpu().numpy(), ref, out)
+
+
+@pytest.mark.parametrize("kernel", ["0", "1"])
+@pytest.mark.parametrize("head", ["dueling", "linear"])
+@pytest.mark.parametrize("n", [1, 2, 5, 64])
+def test_gpu_act_two_hidden_layer_kernels(monkeypatch, kernel, head, n):
+    """Both acting kernels of a two-hidden-layer MLP against the oracle: k_act_mlp (DQNX_ACT2=0: the last
+    workgroup runs layer 2 on the gathered h1) and k_act_mlp2 (the default: layer 2 summed from the
+    layer-1 workgroups' shares, its weights and the head's fetched at the top of the kernel)."""
+    monkeypatch.setenv("DQNX_ACT2", kernel)
+    ospec = O.mlp_spec(284, 8, head)
+    params = O.reference_init(ospec, 9)
+    espec = E.mlp_spec(284, 8, head)
+    flat = _flat(espec, params)
+    x = torch.from_numpy(np.random.default_rng(100 + n).random((n, 284), dtype=np.float32))
+    scratch = E.act_scratch(espec, 64, "cuda")
+    for _ in range(3):   # the same scratch (tickets) across calls
+        vals = torch.empty(n, 8, dtype=torch.float32, device="cuda")
+        acts = E.act(espec, flat, x.cuda(), vals, scratch=scratch)
+        torch.cuda.synchronize()
+        with torch.no_grad():
+            ref = (O.advantages(ospec, params, x) if head == "dueling" else O.q_forward(ospec, params, x)).numpy()
+        _check(vals.cpu().numpy(), ref, acts.cpu().numpy())

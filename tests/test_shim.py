@@ -97,7 +97,7 @@ def test_act_scratch_layout_is_monotone():
     d = E.mlp_spec(284, 8, "dueling").to_c()
     sizes = [C.lib().dqnx_act_scratch_bytes(ctypes.byref(d), n) for n in range(1, 70)]
     assert all(b >= a for a, b in zip(sizes, sizes[1:]))
-    assert sizes[0] == 256 * 4 + 4
+    assert sizes[0] == 16 * 128 * 4 + 4   # n = 1: k_act_mlp2's 16 workgroups' layer-2 shares + the ticket
 
 
 def test_epsilon_interp_matches_numpy():
