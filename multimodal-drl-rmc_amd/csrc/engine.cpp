@@ -556,12 +556,13 @@ int layout(dqnx_engine* e) {
     e->ws_HT16.assign(L, 0);
     e->ws_dZT16.assign(L, 0);
     if (e->dwt) {
-        e->ws_xT16 = sub((uint64_t)e->Bl * np.dense[0].in * 2);
+        const uint64_t rows = (uint64_t)e->slices[0] * e->kslice[0];   // whole slices (tcopy_index)
+        e->ws_xT16 = sub(rows * np.dense[0].in * 2);
         for (int l = 0; l < L; l++) {
-            e->ws_HT16[l] = sub((uint64_t)e->Bl * np.dense[l].out * 2);
-            e->ws_dZT16[l] = sub((uint64_t)e->Bl * np.dense[l].out * 2);
+            e->ws_HT16[l] = sub(rows * np.dense[l].out * 2);
+            e->ws_dZT16[l] = sub(rows * np.dense[l].out * 2);
         }
-        e->ws_dheadT16 = sub((uint64_t)e->Bl * 16 * 2);
+        e->ws_dheadT16 = sub(rows * 16 * 2);
     }
     e->ws_raw = sub((uint64_t)3 * e->Bl * 16 * 4);
     e->ws_trans = sub((uint64_t)e->Bl * 16);
@@ -970,7 +971,11 @@ void build_fused_steps(dqnx_engine* e, int flags, int32_t* idx, int32_t* phys, s
     // the forward's outputs from its own XCD's L2 (16-row tiles, tiles % 8 == 0).  Measured at
     // B=1024: head_bwd 7.2 -> 6.6 us, the forward unchanged; DQNX_XCD_ROWS=0 keeps xcd_remap's order
     const int ftiles = (e->Bl + 15) / 16;
-    const bool xcd_rows = route_knob("DQNX_XCD_ROWS", 1) != 0 && e->fplan.mr == 1 && ftiles % 8 == 0;
+    // (row tiles of 16 * mr rows: the head kernel's 16-sample tiles follow their row tile's XCD)
+    const int frows = 16 * e->fplan.mr;
+    const bool xcd_rows = route_knob("DQNX_XCD_ROWS", 1) != 0 && ftiles % 8 == 0 &&
+                          (e->fplan.mr == 1 || (route_knob("DQNX_XCD_ROWS_MR", 1) != 0 && e->Bl % frows == 0 &&
+                                                (e->Bl / frows) % 8 == 0));
     // 2. forward (R:dqn/agent.py:209-214 / 172-173 streams, R:dqn/network.py:61-65, 90-96)
     {
         FusedFwdArgs fa = e->fplan;
@@ -993,6 +998,7 @@ void build_fused_steps(dqnx_engine* e, int flags, int32_t* idx, int32_t* phys, s
         for (int l = 0; l < L; l++) fa.H[l] = at<float>(e, e->ws_H[l]);   // stream-0 third of [3][Bl][w]
         if (e->dwt) {   // + the T16 copies k_dw_bf16t reads
             fa.xT16 = at<uint16_t>(e, e->ws_xT16);
+            fa.tkb = e->kslice[0];
             for (int l = 0; l < L; l++) fa.HT16[l] = at<uint16_t>(e, e->ws_HT16[l]);
         }
         fa.raw = at<float>(e, e->ws_raw);
@@ -1127,10 +1133,12 @@ void build_fused_steps(dqnx_engine* e, int flags, int32_t* idx, int32_t* phys, s
         if (e->dwt) {
             for (int l = 0; l < L; l++) ha.dZT16[l] = at<uint16_t>(e, e->ws_dZT16[l]);
             ha.dheadT16 = at<uint16_t>(e, e->ws_dheadT16);
+            ha.tkb = e->kslice[0];
         }
         ha.loss_partial = at<float>(e, e->ws_loss_part);
         ha.ctrl = nullptr;   // the forward launch stores the step's Adam scalars
         ha.xcd_rows = xcd_rows ? 1 : 0;
+        ha.xcd_mr = e->fplan.mr;
         ha.xcd_shift = (sample_next || (e->ws_npc && c.algo == DQNX_ALGO_PER_DOUBLE)) ? 1 : 0;   // forward's block 0
         for (int l = 1; l < L; l++) ha.wblkT[l] = at<float>(e, e->ws_wblkT[l]);
         ha.ab = adam_bias_args(e);

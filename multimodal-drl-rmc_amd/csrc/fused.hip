@@ -490,7 +490,7 @@ __global__ __launch_bounds__(FT) void k_mlp_fwd(FusedFwdArgs a) {
         float* Hs = FBUF(cur ^ 1);
         // H to HBM: stream 0 (the backward's operands); the split layer 1 writes every stream's
         float* Hg = (PH == 1) ? a.H[0] + (int64_t)s * a.Bl * N : (keep ? a.H[l] : nullptr);
-        // bf16 + k_dw_bf16t: stream 0's H_l also as a T16 copy (4 consecutive samples per lane: 8 bytes)
+        // bf16 + k_dw_bf16t: stream 0's H_l also as a slab-transposed copy (4 consecutive samples per lane: 8 bytes)
         uint16_t* Ht = (BF && PH == 0 && keep) ? a.HT16[l] : nullptr;
 #pragma unroll
         for (int t = 0; t < 2; t++) {
@@ -510,13 +510,13 @@ __global__ __launch_bounds__(FT) void k_mlp_fwd(FusedFwdArgs a) {
                     }
                     if (Hg && rr < nb) Hg[(int64_t)(b0 + rr) * N + coff + col] = v;
                 }
-                if (Ht && 16 * m + 4 * g < nb)   // (T16 runs need whole 32-row blocks: nb % 32 == 0)
-                    *reinterpret_cast<uint2*>(Ht + t16_index(b0 + 16 * m + 4 * g, col, N)) =
+                if (Ht && 16 * m + 4 * g < nb)   // (copies need whole 32-row blocks: nb % 32 == 0)
+                    *reinterpret_cast<uint2*>(Ht + tcopy_index(b0 + 16 * m + 4 * g, col, N, a.tkb)) =
                         make_uint2(bf16_pack2(vv[0], vv[1]), bf16_pack2(vv[2], vv[3]));
             }
         }
         if constexpr (BF && PH == 0) {
-            // stream 0's input rows as a T16 copy, from the bf16 input tile (still in buffer 0 until
+            // stream 0's input rows as a slab-transposed copy, from the bf16 input tile (still in buffer 0 until
             // layer 2's epilogue), while layer 2's weight stream is in flight: 8 rows of a column per piece
             if (l == 0 && keep && a.xT16) {
                 const int C = a.in[0];
@@ -528,7 +528,7 @@ __global__ __launch_bounds__(FT) void k_mlp_fwd(FusedFwdArgs a) {
                     uint32_t w[4];
 #pragma unroll
                     for (int j = 0; j < 4; j++) w[j] = (uint32_t)col[(2 * j) * a.sx] | ((uint32_t)col[(2 * j + 1) * a.sx] << 16);
-                    *reinterpret_cast<uint4*>(a.xT16 + t16_index(b0 + 8 * ph, cc, C)) = make_uint4(w[0], w[1], w[2], w[3]);
+                    *reinterpret_cast<uint4*>(a.xT16 + tcopy_index(b0 + 8 * ph, cc, C, a.tkb)) = make_uint4(w[0], w[1], w[2], w[3]);
                 }
             }
         }
@@ -613,10 +613,11 @@ __global__ __launch_bounds__(FT) void k_head_bwd(HeadBwdArgs a) {
     // nsplit workgroups per 16-sample tile: each recomputes the (cheap) head part and takes
     // 1/nsplit of the columns of the LAST dZ of the chain (dZ_1, the widest)
     int tile = blockIdx.x / a.nsplit, part = blockIdx.x - tile * a.nsplit;
-    if (a.xcd_rows) {   // tile t on the XCD whose L2 holds the forward's outputs of row tile t
+    if (a.xcd_rows) {   // tile t on the XCD whose L2 holds the forward's outputs of its row tile t / xcd_mr
         const int xh = blockIdx.x & 7, k = blockIdx.x >> 3;
-        tile = (k / a.nsplit) * 8 + ((xh - a.xcd_shift) & 7);
-        part = k - (k / a.nsplit) * a.nsplit;
+        const int kt = k / a.nsplit, mr = a.xcd_mr;
+        tile = ((kt / mr) * 8 + ((xh - a.xcd_shift) & 7)) * mr + (kt - (kt / mr) * mr);
+        part = k - kt * a.nsplit;
     }
     const bool lead = part == 0;
     const int b0 = tile * 16, nb = min(16, a.Bl - b0);
@@ -750,7 +751,7 @@ __global__ __launch_bounds__(FT) void k_head_bwd(HeadBwdArgs a) {
                 a.Q[(int64_t)2 * a.Bl * A + qrow] = q2;
             }
             a.dhead[(int64_t)(b0 + hb) * 16 + hj] = d;
-            if (a.dheadT16) a.dheadT16[t16_index(b0 + hb, hj, 16)] = bf16_bits(d);
+            if (a.dheadT16) a.dheadT16[tcopy_index(b0 + hb, hj, 16, a.tkb)] = bf16_bits(d);
             if (hj == 0) {
                 const int gb = b0 + hb;
                 a.td[gb] = y;
@@ -792,8 +793,8 @@ __global__ __launch_bounds__(FT) void k_head_bwd(HeadBwdArgs a) {
                 else dz[rr * HB_SD + col] = v;
                 if (lead && rr < nb) dzg[(int64_t)(b0 + rr) * F + col] = v;
             }
-            if (lead && a.dZT16[L - 1] && 4 * g < nb)   // T16 copy for k_dw_bf16t
-                *reinterpret_cast<uint2*>(a.dZT16[L - 1] + t16_index(b0 + 4 * g, col, F)) =
+            if (lead && a.dZT16[L - 1] && 4 * g < nb)   // slab-transposed copy for k_dw_bf16t
+                *reinterpret_cast<uint2*>(a.dZT16[L - 1] + tcopy_index(b0 + 4 * g, col, F, a.tkb)) =
                     make_uint2(bf16_pack2(vv[0], vv[1]), bf16_pack2(vv[2], vv[3]));
         }
     }
@@ -828,7 +829,7 @@ __global__ __launch_bounds__(FT) void k_head_bwd(HeadBwdArgs a) {
                 if (store && rr < nb) dzg[(int64_t)(b0 + rr) * ldn + coff + col] = v;
             }
             if (store && a.dZT16[l - 1] && 4 * g < nb)
-                *reinterpret_cast<uint2*>(a.dZT16[l - 1] + t16_index(b0 + 4 * g, coff + col, ldn)) =
+                *reinterpret_cast<uint2*>(a.dZT16[l - 1] + tcopy_index(b0 + 4 * g, coff + col, ldn, a.tkb)) =
                     make_uint2(bf16_pack2(vv[0], vv[1]), bf16_pack2(vv[2], vv[3]));
         }
         cur ^= 1;
@@ -1054,8 +1055,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(dwb_waves<B
     }
 }
 
-// The same weight gradients from the T16 bf16 copies the forward (stream 0's rows and activations)
-// and the head kernel (dZ_l, dHead) write beside their fp32 outputs (BwdArgs::t16).  Every operand
+// The same weight gradients from the slab-transposed bf16 copies the forward (stream 0's rows and
+// activations) and the head kernel (dZ_l, dHead) write beside their fp32 outputs (BwdArgs::t16).  Every operand
 // row of the tile's split-K slice -- BM dZ columns and BN X columns, kslice samples each -- is staged
 // into LDS by LDS-DMA (global_load_lds_dwordx4: a lane moves 8 consecutive samples of its column, a
 // wave-instruction 512 samples of one column) all at once, one wait, one barrier, then every MFMA of
@@ -1114,7 +1115,7 @@ __global__ __launch_bounds__(256) void k_dw_bf16t(BwdArgs a) {
                 const int k8 = s0 + lane;
                 if (k8 < nk8) {
                     const int64_t bb = (int64_t)kb + 8 * k8;
-                    __builtin_amdgcn_global_load_lds(src + t16_index(bb, c, C),
+                    __builtin_amdgcn_global_load_lds(src + tcopy_index(bb, c, C, a.kslice),
                                                      (__attribute__((address_space(3))) void*)(row + 16 * s0),
                                                      16, 0, 0);
                 }

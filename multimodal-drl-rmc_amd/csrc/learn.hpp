@@ -111,18 +111,20 @@ struct DwProblem {
     int head_kind;         // -1 plain Linear layout, else dqnx_head_kind
     int A;                 // actions (head layout)
     int grid_x, grid_y, blocks;   // filled by bwd_level_grid
-    // k_dw_bf16t (BwdArgs::t16): the same operands as bf16 copies in the T16 layout (t16_index):
+    // k_dw_bf16t (BwdArgs::t16): the same operands as bf16 copies in the slab-transposed layout (tcopy_index):
     // dZ with cz columns, X with cx columns; X's column `in` is the ones column (the bias), not stored
     const uint16_t* dZT;
     const uint16_t* XT;
     int cz, cx;
 };
-// T16 layout of a bf16 operand with C columns over the minibatch: element (sample b, column c) at
-// ((b >> 4) * C + c) * 16 + (b & 15) -- 16 consecutive samples of one column contiguous (32 bytes),
-// so the bf16 weight-gradient kernel fetches 8 consecutive samples of a column as one 16-byte piece
-// and its producers (the forward's stream 0, the head kernel) write whole 16-row tiles contiguously.
-__host__ __device__ __forceinline__ int64_t t16_index(int64_t b, int c, int C) {
-    return ((b >> 4) * C + c) * 16 + (b & 15);
+// Slab-transposed layout of a bf16 operand with C columns over the minibatch, KB = the weight
+// gradients' split-K slice (kslice): element (sample b, column c) at ((b / KB) * C + c) * KB + b % KB --
+// one column's samples of one slice contiguous, so k_dw_bf16t stages an operand row of its slice
+// with one LDS-DMA wave-instruction per 512 samples reading whole cache lines.  (A first layout kept
+// 16-sample blocks, [b/16][C][16]: each wave-instruction then touched 32 lines for 32 bytes each and
+// the kernel ran 45 us against k_dw_bf16's 29 at configs[4].)
+__host__ __device__ __forceinline__ int64_t tcopy_index(int64_t b, int c, int C, int KB) {
+    return ((b / KB) * C + c) * KB + b % KB;
 }
 struct BwdArgs {
     // dx role (skipped when dZprev == null): dZprev = (dZ W) (.) act'(Hprev)
@@ -474,8 +476,9 @@ struct FusedFwdArgs {
     const int32_t* phys;         // [Bl] physical ring slots
     float* xcopy;                // [Bl][ring_stride] stream-0 gathered rows (layer-1 dW operand)
     float* H[FUSED_MAX_L];       // stream-0 activations [Bl][out_l]
-    uint16_t* xT16;              // bf16 + k_dw_bf16t: stream 0's rows / activations as T16 copies (or null)
-    uint16_t* HT16[FUSED_MAX_L];
+    uint16_t* xT16;              // bf16 + k_dw_bf16t: stream 0's rows / activations as slab-transposed
+    uint16_t* HT16[FUSED_MAX_L]; // copies (tcopy_index, slice length tkb), or null
+    int tkb;
     float* raw;                  // [3][Bl][16] head outputs per logical stream
     float4* trans;               // [Bl] stream 0: {act (int bits), rew, done, 0} of each sampled slot
     const int32_t* act;          // replay ring columns (gathered for `trans`)
@@ -534,6 +537,7 @@ struct HeadBwdArgs {
     int nsplit;                  // workgroups per 16-sample tile (split the last dZ's columns)
     int xcd_rows;                // tile t's workgroups on the XCD the forward ran row tile t on
     int xcd_shift;               // ... whose workgroups the forward's extra block 0 shifted by one
+    int xcd_mr;                  // ... of 16 * xcd_mr rows (the forward's row-tile height)
     int bf16;                    // DQNX_COMPUTE_BF16: dZ chain on bf16 operands (LDS tiles + wblkT)
     int in[FUSED_MAX_L], out[FUSED_MAX_L];
     int64_t woff[FUSED_MAX_L], head_off;
@@ -552,8 +556,9 @@ struct HeadBwdArgs {
     const float* H[FUSED_MAX_L]; // stream-0 activations
     float* dZ[FUSED_MAX_L];      // [Bl][out_l]
     float* dhead;                // [Bl][16]
-    uint16_t* dZT16[FUSED_MAX_L];   // bf16 + k_dw_bf16t: T16 copies of dZ_l / dHead (or null)
+    uint16_t* dZT16[FUSED_MAX_L];   // bf16 + k_dw_bf16t: slab-transposed copies of dZ_l / dHead (or null)
     uint16_t* dheadT16;
+    int tkb;                     // their slice length (tcopy_index)
     float* loss_partial;         // [tiles]
     dqnx_ctrl* ctrl;
     const float* wblkT[FUSED_MAX_L];     // chain-blocked online W_l, l >= 1 (relayout.hpp)

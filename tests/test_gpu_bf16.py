@@ -246,3 +246,22 @@ def test_gpu_bf16_t16_dw_bit_identical(monkeypatch, algo, batch, per, mr):
                      eng.grads.clone()] + ([eng.sumtree.clone()] if per else []))
     for a, b in zip(*outs):
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("algo,batch,per", [("DuelingDoubleDQNAgent", 8192, False), ("PerDuelingDoubleDQNAgent", 8192, True)])
+def test_gpu_bf16_xcd_rows_multirow_bit_identical(monkeypatch, algo, batch, per):
+    """bf16 at configs[4]'s batch runs 64-row forward tiles; with the XCD row mapping the head kernel's
+    16-sample tile t follows its row tile t / 4 onto one XCD (DQNX_XCD_ROWS_MR=0: xcd_remap's order).
+    Workgroups only move: weights, Adam moments and the tree are bitwise equal."""
+    outs = []
+    for on in ("0", "1"):
+        monkeypatch.setenv("DQNX_XCD_ROWS_MR", on)
+        _, _, eng = make_bf16_pair(algo, 284, batch, 3 * batch, 3 * batch, 73, per=per, graphs=False)
+        for _ in range(3):
+            eng.learn_step(soft_update=True)
+        torch.cuda.synchronize()
+        eng.check_device_error()
+        outs.append([eng.params.clone(), eng.target_params.clone(), eng.adam_v.clone(), eng.q.clone()] +
+                    ([eng.sumtree.clone()] if per else []))
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
