@@ -1167,6 +1167,124 @@ __global__ __launch_bounds__(256) void k_dw_bf16t(BwdArgs a) {
     }
 }
 
+// The same product with the MFMA fragments loaded straight from the slab-transposed copies into
+// registers (no LDS, no barrier): lane (i, g) of a wave fetches samples 32 ch + 8 g .. + 7 of its tile
+// row / column i as one 16-byte load, DWT_STAGES chunks ahead of the MFMAs that use them.  The
+// fragments, their k order and the slabs are k_dw_bf16's (bitwise equal).
+#ifndef DQNX_DWT_STAGES
+#define DQNX_DWT_STAGES 4
+#endif
+template <int BM, int BN>
+__global__ __launch_bounds__(256) void k_dw_bf16d(BwdArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t dlds[];   // (PER tracking / prop scratch only)
+    constexpr int TM = BM / 32, TN = BN / 32, NS = DQNX_DWT_STAGES;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int i = lane & 15, g = lane >> 4;
+    const int wm = wid >> 1, wn = wid & 1;
+    if (a.ptrack && blockIdx.x == 0) {
+        auto& tl = *reinterpret_cast<PerTrackLds<256>*>(dlds);
+        per_track_block<256, DQNX_BF16_TRACK_IPT, DQNX_BF16_TRACK_CARRY>(a.pprop, tl);
+        return;
+    }
+    int b = (int)blockIdx.x - a.ptrack;
+    {
+        int tiles = 0;
+        for (int p = 0; p < a.ndw; p++) tiles += a.dw[p].blocks;
+        if (b >= tiles) {
+            per_prop_block(a.pprop, (b - tiles) * 256, reinterpret_cast<double*>(dlds));
+            return;
+        }
+    }
+    int p = 0;
+    while (p + 1 < a.ndw && b >= a.dw[p].blocks) { b -= a.dw[p].blocks; p++; }
+    const DwProblem& d = a.dw[p];
+    b = xcd_remap(b, d.blocks);
+    const int bx = b % d.grid_x;
+    const int t2 = b / d.grid_x;
+    const int by = t2 % d.grid_y, bz = t2 / d.grid_y;
+    const int m0 = by * BM, n0 = bx * BN;
+    const int kb = bz * a.kslice;
+    const int ke = min(a.Bl, kb + a.kslice);
+    const int KB = a.kslice;
+    const int ncz = d.out < d.cz ? d.out : d.cz;
+    // this lane's TM dZ columns and TN X columns; missing ones read a valid address and are replaced
+    const uint16_t* ap[TM];
+    const uint16_t* bp[TN];
+    uint32_t afill[TM], bfill[TN];   // 0: load; else the constant bf16 pair to use (zero: 1, ones: 0x3F803F80)
+#pragma unroll
+    for (int t = 0; t < TM; t++) {
+        const int c = m0 + wm * 16 * TM + t * 16 + i;
+        const bool have = c < ncz;
+        ap[t] = d.dZT + tcopy_index(kb, have ? c : 0, d.cz, KB) + 8 * g;
+        afill[t] = have ? 0u : 1u;
+    }
+#pragma unroll
+    for (int t = 0; t < TN; t++) {
+        const int c = n0 + wn * 16 * TN + t * 16 + i;
+        const bool have = c < d.in;
+        bp[t] = d.XT + tcopy_index(kb, have ? c : 0, d.cx, KB) + 8 * g;
+        bfill[t] = have ? 0u : (c == d.in ? 0x3F803F80u : 1u);
+    }
+    floatx4 acc[TM][TN];
+#pragma unroll
+    for (int tm = 0; tm < TM; tm++)
+#pragma unroll
+        for (int tn = 0; tn < TN; tn++) acc[tm][tn] = floatx4{0.f, 0.f, 0.f, 0.f};
+    const int nch = (ke - kb) >> 5;
+    u32x4 fa[NS][TM], fb[NS][TN];
+    auto fetch = [&](int ch, u32x4 (&xa)[TM], u32x4 (&xb)[TN]) {
+        const int cc = ch < nch ? ch : nch - 1;   // (clamped: past the last chunk a valid, unused load)
+#pragma unroll
+        for (int t = 0; t < TM; t++) xa[t] = *reinterpret_cast<const u32x4*>(ap[t] + 32 * cc);
+#pragma unroll
+        for (int t = 0; t < TN; t++) xb[t] = *reinterpret_cast<const u32x4*>(bp[t] + 32 * cc);
+    };
+#pragma unroll
+    for (int st = 0; st < NS - 1; st++) fetch(st, fa[st], fb[st]);
+    for (int c0 = 0; c0 < nch; c0 += NS) {
+#pragma unroll
+        for (int st = 0; st < NS; st++) {
+            const int ch = c0 + st;
+            fetch(ch + NS - 1, fa[(st + NS - 1) % NS], fb[(st + NS - 1) % NS]);
+            __builtin_amdgcn_sched_barrier(0);
+            if (ch < nch) {
+                u32x4 xa[TM], xb[TN];
+#pragma unroll
+                for (int t = 0; t < TM; t++) {
+                    const uint32_t f = afill[t] == 1u ? 0u : afill[t];
+                    xa[t] = afill[t] ? u32x4{f, f, f, f} : fa[st][t];
+                }
+#pragma unroll
+                for (int t = 0; t < TN; t++) {
+                    const uint32_t f = bfill[t] == 1u ? 0u : bfill[t];
+                    xb[t] = bfill[t] ? u32x4{f, f, f, f} : fb[st][t];
+                }
+#pragma unroll
+                for (int tm = 0; tm < TM; tm++)
+#pragma unroll
+                    for (int tn = 0; tn < TN; tn++) acc[tm][tn] = mfma16x16x32bf16(xa[tm], xb[tn], acc[tm][tn]);
+            }
+        }
+    }
+    float* part = d.partial + (int64_t)bz * d.pstride;
+#pragma unroll
+    for (int tn = 0; tn < TN; tn++) {
+        const int col = n0 + wn * 16 * TN + tn * 16 + i;
+        if (col > d.in) continue;
+#pragma unroll
+        for (int tm = 0; tm < TM; tm++)
+#pragma unroll
+            for (int r = 0; r < 4; r++) {
+                const int row = m0 + wm * 16 * TM + tm * 16 + 4 * g + r;
+                if (row >= d.out) continue;
+                int64_t o;
+                if (d.head_kind < 0) o = (col < d.in) ? (int64_t)row * d.in + col : (int64_t)d.out * d.in + row;
+                else o = (col < d.in) ? head_w_off(d.head_kind, row, d.in) + col : head_b_off(d.head_kind, row, d.in, d.A);
+                part[o] = acc[tm][tn][r];
+            }
+    }
+}
+
 // Tile shape (BM x BN): 64 x 64 when that still gives >= 512 workgroups (large batches: fewer operand
 // re-reads), else 32 x 32 (B=1024: 132 workgroups of 64 x 64 left the chip idle).  DQNX_DWB_SHAPE
 // (tuning builds): 1 = 32 x 32, 2 = 64 x 64, 3 = 128 x 128, 4 = 128 x 64.
@@ -1218,6 +1336,14 @@ int launch_dw_bf16(const BwdArgs& a, hipStream_t s) {
         if (shm < PER_TOP * sizeof(double)) shm = PER_TOP * sizeof(double);
         // (the attribute only past 64 KB, and exactly the bytes requested: a failed hipFuncSetAttribute
         // -- static LDS + a 160 KB maximum -- would be the launch's hipGetLastError)
+        if (route_knob("DQNX_DWB_T", 1) != 2) {   // fragments straight into registers (default)
+            size_t shd = sizeof(PerTrackLds<256>) > PER_TOP * sizeof(double) ? sizeof(PerTrackLds<256>) : PER_TOP * sizeof(double);
+            if (t.bm == 64 && t.bn == 64) hipLaunchKernelGGL((k_dw_bf16d<64, 64>), dim3(blocks), dim3(256), shd, s, a);
+            else if (t.bm == 32 && t.bn == 32) hipLaunchKernelGGL((k_dw_bf16d<32, 32>), dim3(blocks), dim3(256), shd, s, a);
+            else return set_error(DQNX_EUNSUPPORTED, "dw_bf16d: %dx%d tiles", t.bm, t.bn);
+            DQNX_HIP_CHECK(hipGetLastError());
+            return DQNX_OK;
+        }
         if (t.bm == 64 && t.bn == 64) {
             if (shm > 64 * 1024)
                 DQNX_HIP_CHECK(hipFuncSetAttribute((const void*)k_dw_bf16t<64, 64>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm));
