@@ -1337,6 +1337,7 @@ void build_fused_steps(dqnx_engine* e, int flags, int32_t* idx, int32_t* phys, s
         if (e->fplan.bf16) {   // bf16 operands, fp32 slabs: the same Adam pass follows
             dw_bf16_grid(ba);
             ba.t16 = e->dwt && dw_bf16t_supported(ba) ? 1 : 0;
+            ba.stamps = at<int64_t>(e, e->ws_stamps);
             if (per_fused) {   // tracking in this launch, prop in the Adam launch; or prop here
                 ba.pprop = pua;
                 ba.ptrack = per_track ? 1 : 0;
@@ -2784,10 +2785,11 @@ int dqnx_engine_create(const dqnx_config* cfg, dqnx_engine** out) {
         e->slices[l] = S;
         e->kslice[l] = ks;
     }
-    // bf16 weight gradients from T16 copies written by the forward (the one-launch plan) and the head
-    // kernel (k_dw_bf16t; DQNX_DWB_T=0 keeps k_dw_bf16's fp32-row staging): whole 32-sample chunks
+    // opt-in (DQNX_DWB_T=1): bf16 weight gradients from slab-transposed copies written by the forward
+    // (the one-launch plan) and the head kernel (k_dw_bf16d; measured slower at configs[4], fused.hip);
+    // whole 32-sample chunks
     e->dwt = e->bwd_plan == 2 && e->fplan.bf16 && !(e->fsplit > 1 && e->fplan.mr == 1) && e->Bl % 32 == 0 &&
-             e->kslice[0] % 32 == 0 && e->kslice[0] <= 512 && route_knob("DQNX_DWB_T", 1) != 0;
+             e->kslice[0] % 32 == 0 && e->kslice[0] <= 512 && route_knob("DQNX_DWB_T", 0) != 0;
     const int NC = (int)e->np.conv.size();
     e->cslices.assign(NC, 1);
     e->ckslice.assign(NC, 1);

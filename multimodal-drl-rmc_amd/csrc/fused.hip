@@ -490,7 +490,7 @@ __global__ __launch_bounds__(FT) void k_mlp_fwd(FusedFwdArgs a) {
         float* Hs = FBUF(cur ^ 1);
         // H to HBM: stream 0 (the backward's operands); the split layer 1 writes every stream's
         float* Hg = (PH == 1) ? a.H[0] + (int64_t)s * a.Bl * N : (keep ? a.H[l] : nullptr);
-        // bf16 + k_dw_bf16t: stream 0's H_l also as a slab-transposed copy (4 consecutive samples per lane: 8 bytes)
+        // bf16 + DQNX_DWB_T=1 (k_dw_bf16d): stream 0's H_l also as a slab-transposed copy (4 consecutive samples per lane: 8 bytes)
         uint16_t* Ht = (BF && PH == 0 && keep) ? a.HT16[l] : nullptr;
 #pragma unroll
         for (int t = 0; t < 2; t++) {
@@ -793,7 +793,7 @@ __global__ __launch_bounds__(FT) void k_head_bwd(HeadBwdArgs a) {
                 else dz[rr * HB_SD + col] = v;
                 if (lead && rr < nb) dzg[(int64_t)(b0 + rr) * F + col] = v;
             }
-            if (lead && a.dZT16[L - 1] && 4 * g < nb)   // slab-transposed copy for k_dw_bf16t
+            if (lead && a.dZT16[L - 1] && 4 * g < nb)   // slab-transposed copy for k_dw_bf16d
                 *reinterpret_cast<uint2*>(a.dZT16[L - 1] + tcopy_index(b0 + 4 * g, col, F, a.tkb)) =
                     make_uint2(bf16_pack2(vv[0], vv[1]), bf16_pack2(vv[2], vv[3]));
         }
@@ -1055,122 +1055,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(dwb_waves<B
     }
 }
 
-// The same weight gradients from the slab-transposed bf16 copies the forward (stream 0's rows and
-// activations) and the head kernel (dZ_l, dHead) write beside their fp32 outputs (BwdArgs::t16).  Every operand
-// row of the tile's split-K slice -- BM dZ columns and BN X columns, kslice samples each -- is staged
-// into LDS by LDS-DMA (global_load_lds_dwordx4: a lane moves 8 consecutive samples of its column, a
-// wave-instruction 512 samples of one column) all at once, one wait, one barrier, then every MFMA of
-// the slice out of LDS.  No register staging, no per-pass barriers: k_dw_bf16's 16 dependent
-// load -> LDS -> barrier passes per slice were its bound (2.5 % of the bf16 peak, 18 % of HBM).
-// LDS rows are kslice bf16 + 16 bytes (1040 B at 512 samples: 4 dwords mod 64 per row, so the
-// ds_read_b128 fragment reads of 16 consecutive rows hit distinct banks).  The MFMA inputs, their
-// k order and the output slabs are k_dw_bf16's (bitwise equal: test_gpu_bf16_t16_dw_bit_identical).
-// Rows with no operand (dZ columns >= out, X columns > in) are zero; X column `in` is the ones column.
-template <int BM, int BN>
-__global__ __launch_bounds__(256) void k_dw_bf16t(BwdArgs a) {
-    extern __shared__ __attribute__((aligned(16))) uint32_t dlds[];
-    constexpr int TM = BM / 32, TN = BN / 32;
-    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    const int i = lane & 15, g = lane >> 4;
-    const int wm = wid >> 1, wn = wid & 1;
-    if (a.ptrack && blockIdx.x == 0) {   // k_per_update's tracking (as k_dw_bf16)
-        auto& tl = *reinterpret_cast<PerTrackLds<256>*>(dlds);
-        per_track_block<256, DQNX_BF16_TRACK_IPT, DQNX_BF16_TRACK_CARRY>(a.pprop, tl);
-        return;
-    }
-    int b = (int)blockIdx.x - a.ptrack;
-    {
-        int tiles = 0;
-        for (int p = 0; p < a.ndw; p++) tiles += a.dw[p].blocks;
-        if (b >= tiles) {
-            per_prop_block(a.pprop, (b - tiles) * 256, reinterpret_cast<double*>(dlds));
-            return;
-        }
-    }
-    int p = 0;
-    while (p + 1 < a.ndw && b >= a.dw[p].blocks) { b -= a.dw[p].blocks; p++; }
-    const DwProblem& d = a.dw[p];
-    b = xcd_remap(b, d.blocks);
-    const int bx = b % d.grid_x;
-    const int t2 = b / d.grid_x;
-    const int by = t2 % d.grid_y, bz = t2 / d.grid_y;
-    const int m0 = by * BM, n0 = bx * BN;
-    const int kb = bz * a.kslice;
-    const int ke = min(a.Bl, kb + a.kslice);
-    const int RB = a.kslice * 2 + 16;                 // LDS bytes per operand row
-    const int nk8 = (ke - kb) >> 3;                   // 8-sample pieces of this slice
-    const int ncz = d.out < d.cz ? d.out : d.cz;      // dZ columns that exist
-    char* lb = reinterpret_cast<char*>(dlds);
-    // (1) every row of both operands in flight at once: row q < BM is dZ column m0 + q, else X column
-    //     n0 + q - BM; the wave-instruction for (row, 512-sample segment) writes RB-aligned LDS bytes
-    for (int q = wid; q < BM + BN; q += 4) {
-        const bool isA = q < BM;
-        const int c = isA ? m0 + q : n0 + (q - BM);
-        char* row = lb + q * RB;
-        const bool have = isA ? c < ncz : c < d.in;
-        if (have) {
-            const uint16_t* src = isA ? d.dZT : d.XT;
-            const int C = isA ? d.cz : d.cx;
-            for (int s0 = 0; s0 < nk8; s0 += 64) {
-                const int k8 = s0 + lane;
-                if (k8 < nk8) {
-                    const int64_t bb = (int64_t)kb + 8 * k8;
-                    __builtin_amdgcn_global_load_lds(src + tcopy_index(bb, c, C, a.kslice),
-                                                     (__attribute__((address_space(3))) void*)(row + 16 * s0),
-                                                     16, 0, 0);
-                }
-            }
-        } else {   // zeros, or the ones column (bias)
-            const uint32_t v = (!isA && c == d.in) ? 0x3F803F80u : 0u;
-            for (int k8 = lane; k8 < nk8; k8 += 64)
-                *reinterpret_cast<uint4*>(row + 16 * k8) = make_uint4(v, v, v, v);
-        }
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    // (2) the slice's MFMAs, chunk order as k_dw_bf16 (32 samples per 16x16x32 MFMA)
-    floatx4 acc[TM][TN];
-#pragma unroll
-    for (int tm = 0; tm < TM; tm++)
-#pragma unroll
-        for (int tn = 0; tn < TN; tn++) acc[tm][tn] = floatx4{0.f, 0.f, 0.f, 0.f};
-    const int nch = (ke - kb) >> 5;
-    const char* pa = lb + (wm * 16 * TM + i) * RB + 16 * g;
-    const char* pb = lb + (BM + wn * 16 * TN + i) * RB + 16 * g;
-    for (int ch = 0; ch < nch; ch++) {
-        u32x4 fa[TM], fb[TN];
-#pragma unroll
-        for (int t = 0; t < TM; t++) fa[t] = *reinterpret_cast<const u32x4*>(pa + t * 16 * RB + 64 * ch);
-#pragma unroll
-        for (int t = 0; t < TN; t++) fb[t] = *reinterpret_cast<const u32x4*>(pb + t * 16 * RB + 64 * ch);
-#pragma unroll
-        for (int tm = 0; tm < TM; tm++)
-#pragma unroll
-            for (int tn = 0; tn < TN; tn++) acc[tm][tn] = mfma16x16x32bf16(fa[tm], fb[tn], acc[tm][tn]);
-    }
-    float* part = d.partial + (int64_t)bz * d.pstride;
-#pragma unroll
-    for (int tn = 0; tn < TN; tn++) {
-        const int col = n0 + wn * 16 * TN + tn * 16 + i;
-        if (col > d.in) continue;
-#pragma unroll
-        for (int tm = 0; tm < TM; tm++)
-#pragma unroll
-            for (int r = 0; r < 4; r++) {
-                const int row = m0 + wm * 16 * TM + tm * 16 + 4 * g + r;
-                if (row >= d.out) continue;
-                int64_t o;
-                if (d.head_kind < 0) o = (col < d.in) ? (int64_t)row * d.in + col : (int64_t)d.out * d.in + row;
-                else o = (col < d.in) ? head_w_off(d.head_kind, row, d.in) + col : head_b_off(d.head_kind, row, d.in, d.A);
-                part[o] = acc[tm][tn][r];
-            }
-    }
-}
-
-// The same product with the MFMA fragments loaded straight from the slab-transposed copies into
-// registers (no LDS, no barrier): lane (i, g) of a wave fetches samples 32 ch + 8 g .. + 7 of its tile
-// row / column i as one 16-byte load, DWT_STAGES chunks ahead of the MFMAs that use them.  The
-// fragments, their k order and the slabs are k_dw_bf16's (bitwise equal).
+// Opt-in (DQNX_DWB_T=1): the same weight gradients from slab-transposed bf16 copies that the forward
+// (stream 0's rows and activations) and the head kernel (dZ_l, dHead) write beside their fp32 outputs,
+// the MFMA fragments loaded straight into registers (no LDS, no barrier): lane (i, g) of a wave fetches
+// samples 32 ch + 8 g .. + 7 of its tile row / column i as one 16-byte load, DWT_STAGES chunks ahead of
+// the MFMAs that use them.  The fragments, their k order and the slabs are k_dw_bf16's (bitwise equal,
+// test_gpu_bf16_t16_dw_bit_identical).  Measured at configs[4] (rocprofv3, profiles/r05/): 30.2 us
+// against k_dw_bf16's 28.1, and the copies cost the forward 3.3 us and the head 1.8; an LDS-DMA variant
+// (every operand row of a slice staged by global_load_lds at once) took 45-48 us.  Block 0's stamps
+// (tools/stamps_dw.py): ~7.5 K cycles per 4 chunks of 16-byte loads, i.e. ~3 us per round trip while
+// all 528 tiles load at once -- the launch is bound by the memory system's queueing, not by how a tile
+// stages its operands, so k_dw_bf16 stays the default.
 #ifndef DQNX_DWT_STAGES
 #define DQNX_DWT_STAGES 4
 #endif
@@ -1198,6 +1093,7 @@ __global__ __launch_bounds__(256) void k_dw_bf16d(BwdArgs a) {
     int p = 0;
     while (p + 1 < a.ndw && b >= a.dw[p].blocks) { b -= a.dw[p].blocks; p++; }
     const DwProblem& d = a.dw[p];
+    DQNX_STAMP(a.stamps, 57);
     b = xcd_remap(b, d.blocks);
     const int bx = b % d.grid_x;
     const int t2 = b / d.grid_x;
@@ -1265,7 +1161,9 @@ __global__ __launch_bounds__(256) void k_dw_bf16d(BwdArgs a) {
                     for (int tn = 0; tn < TN; tn++) acc[tm][tn] = mfma16x16x32bf16(xa[tm], xb[tn], acc[tm][tn]);
             }
         }
+        if (c0 == 0) DQNX_STAMP(a.stamps, 58);
     }
+    DQNX_STAMP(a.stamps, 59);
     float* part = d.partial + (int64_t)bz * d.pstride;
 #pragma unroll
     for (int tn = 0; tn < TN; tn++) {
@@ -1283,6 +1181,13 @@ __global__ __launch_bounds__(256) void k_dw_bf16d(BwdArgs a) {
                 part[o] = acc[tm][tn][r];
             }
     }
+#ifdef DQNX_STAMPS
+    DQNX_STAMP(a.stamps, 60);
+    if (a.stamps && threadIdx.x == 0) {   // the last workgroup's end, and how many workgroups ran
+        atomicMax(reinterpret_cast<unsigned long long*>(a.stamps + 61), (unsigned long long)__builtin_amdgcn_s_memtime());
+        atomicAdd(reinterpret_cast<unsigned long long*>(a.stamps + 62), 1ull);
+    }
+#endif
 }
 
 // Tile shape (BM x BN): 64 x 64 when that still gives >= 512 workgroups (large batches: fewer operand
@@ -1311,13 +1216,9 @@ void dw_bf16_grid(BwdArgs& a) {
     }
 }
 
-// k_dw_bf16t's LDS: every operand row of a tile's slice (kslice bf16 + 16 bytes each)
-static size_t dw_bf16t_lds_bytes(int bm, int bn, int kslice) { return (size_t)(bm + bn) * (kslice * 2 + 16); }
-
 bool dw_bf16t_supported(const BwdArgs& a) {
     const DwbTile t = dw_bf16_tile(a);
-    return a.kslice % 32 == 0 && a.Bl % 32 == 0 && ((t.bm == 64 && t.bn == 64) || (t.bm == 32 && t.bn == 32)) &&
-           dw_bf16t_lds_bytes(t.bm, t.bn, a.kslice) <= 160 * 1024;
+    return a.kslice % 32 == 0 && a.Bl % 32 == 0 && ((t.bm == 64 && t.bn == 64) || (t.bm == 32 && t.bn == 32));
 }
 
 int launch_dw_bf16(const BwdArgs& a, hipStream_t s) {
@@ -1327,34 +1228,16 @@ int launch_dw_bf16(const BwdArgs& a, hipStream_t s) {
     for (int p = 0; p < a.ndw; p++) blocks += a.dw[p].blocks;
     if (a.t16) {
         const DwbTile t = dw_bf16_tile(a);
-        size_t shm = dw_bf16t_lds_bytes(t.bm, t.bn, a.kslice);
-        if (a.kslice % 32 || a.Bl % 32 || shm > 160 * 1024)
-            return set_error(DQNX_EUNSUPPORTED, "dw_bf16t: slices / batch a multiple of 32 samples, LDS <= 160 KB");
+        if (a.kslice % 32 || a.Bl % 32)
+            return set_error(DQNX_EUNSUPPORTED, "dw_bf16d: slices / batch a multiple of 32 samples");
         for (int p = 0; p < a.ndw; p++)
-            if (!a.dw[p].dZT || !a.dw[p].XT) return set_error(DQNX_EINVAL, "dw_bf16t: T16 operand missing");
-        if (shm < sizeof(PerTrackLds<256>)) shm = sizeof(PerTrackLds<256>);
-        if (shm < PER_TOP * sizeof(double)) shm = PER_TOP * sizeof(double);
+            if (!a.dw[p].dZT || !a.dw[p].XT) return set_error(DQNX_EINVAL, "dw_bf16d: copy operand missing");
         // (the attribute only past 64 KB, and exactly the bytes requested: a failed hipFuncSetAttribute
         // -- static LDS + a 160 KB maximum -- would be the launch's hipGetLastError)
-        if (route_knob("DQNX_DWB_T", 1) != 2) {   // fragments straight into registers (default)
-            size_t shd = sizeof(PerTrackLds<256>) > PER_TOP * sizeof(double) ? sizeof(PerTrackLds<256>) : PER_TOP * sizeof(double);
-            if (t.bm == 64 && t.bn == 64) hipLaunchKernelGGL((k_dw_bf16d<64, 64>), dim3(blocks), dim3(256), shd, s, a);
-            else if (t.bm == 32 && t.bn == 32) hipLaunchKernelGGL((k_dw_bf16d<32, 32>), dim3(blocks), dim3(256), shd, s, a);
-            else return set_error(DQNX_EUNSUPPORTED, "dw_bf16d: %dx%d tiles", t.bm, t.bn);
-            DQNX_HIP_CHECK(hipGetLastError());
-            return DQNX_OK;
-        }
-        if (t.bm == 64 && t.bn == 64) {
-            if (shm > 64 * 1024)
-                DQNX_HIP_CHECK(hipFuncSetAttribute((const void*)k_dw_bf16t<64, 64>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm));
-            hipLaunchKernelGGL((k_dw_bf16t<64, 64>), dim3(blocks), dim3(256), shm, s, a);
-        } else if (t.bm == 32 && t.bn == 32) {
-            if (shm > 64 * 1024)
-                DQNX_HIP_CHECK(hipFuncSetAttribute((const void*)k_dw_bf16t<32, 32>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm));
-            hipLaunchKernelGGL((k_dw_bf16t<32, 32>), dim3(blocks), dim3(256), shm, s, a);
-        } else {
-            return set_error(DQNX_EUNSUPPORTED, "dw_bf16t: %dx%d tiles", t.bm, t.bn);
-        }
+        const size_t shd = sizeof(PerTrackLds<256>) > PER_TOP * sizeof(double) ? sizeof(PerTrackLds<256>) : PER_TOP * sizeof(double);
+        if (t.bm == 64 && t.bn == 64) hipLaunchKernelGGL((k_dw_bf16d<64, 64>), dim3(blocks), dim3(256), shd, s, a);
+        else if (t.bm == 32 && t.bn == 32) hipLaunchKernelGGL((k_dw_bf16d<32, 32>), dim3(blocks), dim3(256), shd, s, a);
+        else return set_error(DQNX_EUNSUPPORTED, "dw_bf16d: %dx%d tiles", t.bm, t.bn);
         DQNX_HIP_CHECK(hipGetLastError());
         return DQNX_OK;
     }

@@ -111,7 +111,7 @@ struct DwProblem {
     int head_kind;         // -1 plain Linear layout, else dqnx_head_kind
     int A;                 // actions (head layout)
     int grid_x, grid_y, blocks;   // filled by bwd_level_grid
-    // k_dw_bf16t (BwdArgs::t16): the same operands as bf16 copies in the slab-transposed layout (tcopy_index):
+    // k_dw_bf16d (BwdArgs::t16, opt-in DQNX_DWB_T=1): the same operands as bf16 copies in the slab-transposed layout (tcopy_index):
     // dZ with cz columns, X with cx columns; X's column `in` is the ones column (the bias), not stored
     const uint16_t* dZT;
     const uint16_t* XT;
@@ -119,10 +119,8 @@ struct DwProblem {
 };
 // Slab-transposed layout of a bf16 operand with C columns over the minibatch, KB = the weight
 // gradients' split-K slice (kslice): element (sample b, column c) at ((b / KB) * C + c) * KB + b % KB --
-// one column's samples of one slice contiguous, so k_dw_bf16t stages an operand row of its slice
-// with one LDS-DMA wave-instruction per 512 samples reading whole cache lines.  (A first layout kept
-// 16-sample blocks, [b/16][C][16]: each wave-instruction then touched 32 lines for 32 bytes each and
-// the kernel ran 45 us against k_dw_bf16's 29 at configs[4].)
+// one column's samples of one slice contiguous (whole cache lines for k_dw_bf16d's 16-byte fragment
+// loads; a first layout of 16-sample blocks, [b/16][C][16], left 32 bytes used per line touched).
 __host__ __device__ __forceinline__ int64_t tcopy_index(int64_t b, int c, int C, int KB) {
     return ((b / KB) * C + c) * KB + b % KB;
 }
@@ -139,7 +137,8 @@ struct BwdArgs {
     int ndw;
     int Bl, kslice, dw_slices;
     int dx_blocks, dx_grid_x;
-    int t16;               // bf16 weight gradients from the T16 copies (k_dw_bf16t) instead of fp32 rows
+    int t16;               // bf16 weight gradients from the slab-transposed copies (k_dw_bf16d) instead of fp32 rows
+    int64_t* stamps;       // diagnostic builds (-DDQNX_STAMPS): k_dw_bf16d's slots 57..62
     int pprop_wgs;         // k_dw_bf16: + workgroups running k_per_prop's body (single-GPU PER step)
     int ptrack;            // k_dw_bf16: + block 0 running k_per_update's tracking (its prop in the Adam launch)
     PerUpdateArgs pprop;
@@ -476,7 +475,7 @@ struct FusedFwdArgs {
     const int32_t* phys;         // [Bl] physical ring slots
     float* xcopy;                // [Bl][ring_stride] stream-0 gathered rows (layer-1 dW operand)
     float* H[FUSED_MAX_L];       // stream-0 activations [Bl][out_l]
-    uint16_t* xT16;              // bf16 + k_dw_bf16t: stream 0's rows / activations as slab-transposed
+    uint16_t* xT16;              // bf16 + DQNX_DWB_T=1: stream 0's rows / activations as slab-transposed
     uint16_t* HT16[FUSED_MAX_L]; // copies (tcopy_index, slice length tkb), or null
     int tkb;
     float* raw;                  // [3][Bl][16] head outputs per logical stream
@@ -556,7 +555,7 @@ struct HeadBwdArgs {
     const float* H[FUSED_MAX_L]; // stream-0 activations
     float* dZ[FUSED_MAX_L];      // [Bl][out_l]
     float* dhead;                // [Bl][16]
-    uint16_t* dZT16[FUSED_MAX_L];   // bf16 + k_dw_bf16t: slab-transposed copies of dZ_l / dHead (or null)
+    uint16_t* dZT16[FUSED_MAX_L];   // bf16 + DQNX_DWB_T=1: slab-transposed copies of dZ_l / dHead (or null)
     uint16_t* dheadT16;
     int tkb;                     // their slice length (tcopy_index)
     float* loss_partial;         // [tiles]
@@ -573,7 +572,7 @@ int launch_fused_fwd(const FusedFwdArgs& a, int act, hipStream_t s);
 int launch_head_bwd(const HeadBwdArgs& a, int act, hipStream_t s);
 void dw_bf16_grid(BwdArgs& a);                               // 64x64 tiles of k_dw_bf16
 int launch_dw_bf16(const BwdArgs& a, hipStream_t s);          // bf16 split-K weight gradients
-bool dw_bf16t_supported(const BwdArgs& a);                   // k_dw_bf16t fits (after dw_bf16_grid)
+bool dw_bf16t_supported(const BwdArgs& a);                   // k_dw_bf16d fits (after dw_bf16_grid)
 
 // ---- implicit-GEMM convolutions (conv_ig.hip): the (4,84,84) variant's convs without
 //      materialised column matrices ----

@@ -228,10 +228,10 @@ def test_gpu_bf16_prefetch_bit_identical(batch):
     ("PerDuelingDoubleDQNAgent", 8192, True, None),   # configs[4]: + the tracking / prop workgroups
 ])
 def test_gpu_bf16_t16_dw_bit_identical(monkeypatch, algo, batch, per, mr):
-    """k_dw_bf16t (operands from the T16 bf16 copies the forward and the head kernel write, staged by
-    LDS-DMA) against k_dw_bf16 (fp32 rows rounded and transposed through registers): the same bf16
-    operands, the same 32-sample MFMA chunks, the same slabs -- weights, Adam state and (PER) tree
-    bitwise equal after three steps."""
+    """k_dw_bf16d (DQNX_DWB_T=1: operands from the slab-transposed bf16 copies the forward and the head
+    kernel write, loaded straight into the MFMA fragments) against k_dw_bf16 (the default: fp32 rows
+    rounded and transposed through LDS): the same bf16 operands, the same 32-sample MFMA chunks, the same
+    slabs -- weights, Adam state and (PER) tree bitwise equal after three steps."""
     if mr is not None:
         monkeypatch.setenv("DQNX_FWD_MR", mr)
     outs = []
