@@ -150,13 +150,29 @@ static void run_case(const Case& k) {
     }
     int32_t nb = 0;
     if (dqnx_dp_bucket_count(e, &nb) == DQNX_OK) {
-        int64_t last = -1;
+        // the buckets tile [0, P) exactly (bucket 0 carries the loss slot at P), every range starts on a
+        // float4 (the bucket Adam passes run the float4 kernel from `first`), none is empty
+        int64_t P = 0;
+        CHECK(dqnx_net_param_count(&k.net, &P, nullptr) == DQNX_OK, "param_count");
+        std::vector<std::pair<int64_t, int64_t>> rg;
         for (int b = 0; b < nb; b++) {
             int64_t first = -1, count = -1;
             CHECK(dqnx_dp_bucket_info(e, b, &first, &count) == DQNX_OK && first >= 0 && count > 0, "bucket %d", b);
-            CHECK(first != last, "bucket %d repeats a range", b);
-            last = first;
+            if (b == 0) {
+                CHECK(first + count == P + 1, "bucket 0 must end with the loss slot (%lld + %lld vs P %lld)",
+                      (long long)first, (long long)count, (long long)P);
+                count -= 1;
+            }
+            CHECK(first % 4 == 0, "bucket %d starts at %lld, not a float4", b, (long long)first);
+            rg.push_back({first, first + count});
         }
+        std::sort(rg.begin(), rg.end());
+        int64_t at = 0;
+        for (const auto& r : rg) {
+            CHECK(r.first == at && r.second > r.first, "buckets leave a gap or overlap at %lld", (long long)at);
+            at = r.second;
+        }
+        CHECK(at == P, "buckets end at %lld, not at P %lld", (long long)at, (long long)P);
         CHECK(dqnx_dp_bucket_info(e, nb, nullptr, nullptr) == DQNX_EINVAL, "bucket past the end");
     }
     CHECK(dqnx_params_modified(e) == DQNX_OK, "params_modified");
@@ -198,6 +214,12 @@ int main() {
                 cases.push_back({nets[6], a, 256, W, r, 0, DQNX_COMPUTE_FP32, 100000});
                 cases.push_back({nets[8], a, 256, W, r, 0, DQNX_COMPUTE_FP32, 1000});
             }
+    // world 1 (the bucketed DP tests' engines) for both conv nets, every algorithm, and the small
+    // batches those tests use
+    for (int n : {6, 7, 8})
+        for (int a : algos)
+            for (int B : {64, 256})
+                cases.push_back({nets[n], a, B, 1, 0, 0, DQNX_COMPUTE_FP32, n == 8 ? 2000 : 20000});
     for (int n = 6; n < 9; n++)
         for (int a : algos)
             for (int B : {32, 48, 256})

@@ -17,9 +17,18 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 
 def _error_lines(text, limit=20):
     """The lines of a child's stderr that name the error (a watchdog's stack trace hides them from
-    the tail)."""
-    keys = ("error", "Error", "what()", "fault", "Fault", "illegal", "dqnx")
+    the tail).  The whole stderr also goes to gpurun_out/dp_child_<n>.log (merged back from the GPU
+    box), so a failure that happens once keeps its first lines."""
+    keys = ("error", "Error", "what()", "fault", "Fault", "illegal", "dqnx", "HIP", "hip")
     hits = [ln for ln in text.splitlines() if any(k in ln for k in keys) and "frame #" not in ln]
+    try:
+        out = os.path.join(os.path.dirname(HERE), "gpurun_out")
+        os.makedirs(out, exist_ok=True)
+        n = len([f for f in os.listdir(out) if f.startswith("dp_child_")])
+        with open(os.path.join(out, f"dp_child_{n}.log"), "w") as f:
+            f.write(text)
+    except OSError:
+        pass
     return "\n".join(hits[:limit]) + "\n"
 
 def run_ranks(tmp_path, world, algo, sampling="global", case="small", compute="fp32", timeout=300, mode="plain"):
