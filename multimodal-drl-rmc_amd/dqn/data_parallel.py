@@ -105,17 +105,16 @@ CAPTURE_MODE = "thread_local"
 
 def capture(graph):
     """torch.cuda.graph(graph) in "thread_local" capture mode -- the mode every capture of this package
-    uses.
+    uses: the capture restricts only the capturing thread, not ProcessGroupNCCL's watchdog thread, which
+    polls the events of eager collectives (hipEventQuery) every ~100 ms.
 
-    torch's default, "global", makes HIP refuse capture-unsafe calls from EVERY thread while the capture
-    is open, and ProcessGroupNCCL's watchdog thread polls the events of the eager collectives still in its
-    list (hipEventQuery, every ~100 ms).  A poll that landed inside a DP-step capture returned a capture
-    error, the watchdog rethrew it as a HIP error and the process aborted (SIGABRT from
-    WorkNCCL::finishedGPUExecutionInternal: test_gpu_graphed_bucketed_dp_step, round 4, twice in ~20
-    runs, on the conv nets whose captures take longest).  "thread_local" keeps the check for the capturing
-    thread (a sync or allocation there would still be an error) and lets other threads query events.
-    tests/test_gpu_dp.py::test_gpu_capture_tolerates_watchdog_polls holds a collective's work pending in the
-    watchdog across a capture (tools/capture_watchdog_check.py)."""
+    Round 5 tested whether such a poll inside a capture explains round 4's two aborts of
+    test_gpu_graphed_bucketed_dp_step (SIGABRT from WorkNCCL::finishedGPUExecutionInternal, a HIP error
+    returned to the watchdog's event query).  tools/capture_watchdog_check.py holds an eager all-reduce's
+    work incomplete in the watchdog's list across a capture held open for 0.6 s: in "global" and
+    "thread_local" mode, with and without a captured collective on the same process group's stream, the
+    process survives (gpurun_out r05a / r05k, DESIGN.md §6).  So the watchdog poll is not that cause;
+    tests/test_gpu_dp.py::test_gpu_capture_tolerates_watchdog_polls keeps the condition covered."""
     return torch.cuda.graph(graph, capture_error_mode=CAPTURE_MODE)
 
 

@@ -311,13 +311,12 @@ def test_gpu_graphed_bucketed_dp_step(net):
 
 
 def test_gpu_capture_tolerates_watchdog_polls():
-    """The round-4 abort of test_gpu_graphed_bucketed_dp_step, forced deterministically: an all-reduce's
-    work is held incomplete (behind a spin kernel) in ProcessGroupNCCL's watchdog list while a graph
-    capture stays open for 0.6 s, so the watchdog's ~100 ms event poll lands inside the capture.  Under
-    torch's default "global" capture mode HIP refuses that poll and the watchdog aborts the process;
-    the package captures in dqn.data_parallel.CAPTURE_MODE ("thread_local").  The same run then captures
-    the HEAD net's bucketed DP step with the capture stretched past the poll interval and checks its
-    replays against eager steps (tools/capture_watchdog_check.py)."""
+    """A graph capture while ProcessGroupNCCL's watchdog polls an eager collective's pending work: the
+    work is held incomplete (behind a spin kernel) in the watchdog's list while a capture in the
+    package's mode (dqn.data_parallel.CAPTURE_MODE) stays open for 0.6 s, so the ~100 ms event poll
+    lands inside it; then the HEAD net's bucketed DP step is captured with the capture stretched past
+    the poll interval and its replays are checked against eager steps (tools/capture_watchdog_check.py).
+    A round-5 hypothesis for round 4's watchdog aborts, ruled out by this condition passing."""
     env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(free_port()))
     r = subprocess.run([sys.executable, os.path.join(os.path.dirname(HERE), "tools", "capture_watchdog_check.py"),
                         "package"], env=env, capture_output=True, text=True, timeout=240)

@@ -1,7 +1,8 @@
 """GPU box, world_size 1 over RCCL: a graph capture while ProcessGroupNCCL's watchdog thread still holds
-an eager collective's work (the round-4 abort of test_gpu_graphed_bucketed_dp_step).
+an eager collective's work (a hypothesis for round 4's aborts of test_gpu_graphed_bucketed_dp_step,
+DESIGN.md §6 -- ruled out: every mode below survives on MI355X / ROCm 7.0 HIP in torch 2.10).
 
-    python tools/capture_watchdog_check.py [package|global|thread_local]
+    python tools/capture_watchdog_check.py [package|global|thread_local|nccl_same|nccl_group2]
 
 1. A spin kernel (torch.cuda._sleep) and then an all-reduce are enqueued on the current stream, so the
    all-reduce's work stays incomplete -- and in the watchdog's list, which it polls every ~100 ms with
@@ -10,9 +11,9 @@ an eager collective's work (the round-4 abort of test_gpu_graphed_bucketed_dp_st
    watchdog polls the pending work during the capture (deterministically: the work cannot complete
    before the spin kernel ends).
    * "package" (default): dqn.data_parallel.CAPTURE_MODE, the mode of every capture of the package;
-   * "global" / "thread_local": torch.cuda.CUDAGraph.capture_begin(capture_error_mode=...).
-   Under "global" the watchdog's poll is a capture-unsafe call from another thread: HIP refuses it, the
-   watchdog rethrows and the process aborts.
+   * "global" / "thread_local": torch.cuda.CUDAGraph.capture_begin(capture_error_mode=...);
+   * "nccl_same" / "nccl_group2": global mode with a collective captured as well, on the pending work's
+     process group (its NCCL stream joins the capture) / on a second group.
 3. "package" then also captures the bucketed DP step of the HEAD net (GraphedDPStep(bucketed=True)) with
    its capture stretched by 0.3 s per bucket, right after eager bucketed steps, and checks that replays
    equal eager steps bit for bit.
