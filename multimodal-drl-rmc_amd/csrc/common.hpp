@@ -90,9 +90,24 @@ __device__ __forceinline__ int xcd_remap(int L, int total) {
     do {                                                                             \
         if ((ptr) && threadIdx.x == 0) (ptr)[i] = (int64_t)__builtin_amdgcn_s_memtime(); \
     } while (0)
+// block `blk`, thread 0
+#define DQNX_STAMP_BLK(ptr, i, blk)                                                   \
+    do {                                                                             \
+        if ((ptr) && blockIdx.x == (unsigned)(blk) && threadIdx.x == 0) (ptr)[i] = (int64_t)__builtin_amdgcn_s_memtime(); \
+    } while (0)
+// ... after this wave's loads and stores have completed (s_waitcnt vmcnt(0))
+#define DQNX_STAMP_BLK_W(ptr, i, blk)                                                 \
+    do {                                                                             \
+        if ((ptr) && blockIdx.x == (unsigned)(blk)) {                                \
+            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");              \
+            if (threadIdx.x == 0) (ptr)[i] = (int64_t)__builtin_amdgcn_s_memtime();  \
+        }                                                                            \
+    } while (0)
 #else
 #define DQNX_STAMP(ptr, i) do { } while (0)
 #define DQNX_STAMP_WG(ptr, i) do { } while (0)
+#define DQNX_STAMP_BLK(ptr, i, blk) do { } while (0)
+#define DQNX_STAMP_BLK_W(ptr, i, blk) do { } while (0)
 #endif
 
 }  // namespace dqnx

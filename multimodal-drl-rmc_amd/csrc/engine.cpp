@@ -1663,6 +1663,9 @@ std::vector<KStep> build_learn_steps(dqnx_engine* e, int key) {
                                           at<int32_t>(e, e->ws_phys) + (size_t)e->Bl);
             ma.samp.stamps = nullptr;
         }
+#ifdef DQNX_STAMPS
+        ma.stamps = at<int64_t>(e, e->ws_stamps);
+#endif
         double flops = 0, bytes = 0;
         for (int l = 0; l < NC; l++) {
             const ConvPlan& cp = np.conv[l];
@@ -2060,6 +2063,9 @@ std::vector<KStep> build_learn_steps(dqnx_engine* e, int key) {
         micro_dx_layout(mconv, NC, xa.S, xa.lds_d, &xa.zero);
         micro_dx_waves(xa);
         xa.lds_floats = e->micro_dx_lds;
+#ifdef DQNX_STAMPS
+        xa.stamps = at<int64_t>(e, e->ws_stamps);
+#endif
         double xf = 0, xb = 0;
         for (int l = 1; l < NC; l++) {
             const ConvPlan& cp = np.conv[l];

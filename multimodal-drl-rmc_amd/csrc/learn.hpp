@@ -689,6 +689,7 @@ struct MicroFwdArgs {
     // staging slot with the 256-thread sampler body (k <= 2048: 3-block passes into 4096 LDS slots)
     int samp_on;
     SampleArgs samp;
+    int64_t* stamps;           // diagnostic builds: slots 40..46 (first compute workgroup's phases, launch span)
 };
 struct MicroDxArgs {           // data gradients, last conv down to conv 2's input (stream 0)
     MicroConv c[MICRO_MAX_CONV];
@@ -698,7 +699,9 @@ struct MicroDxArgs {           // data gradients, last conv down to conv 2's inp
     int lds_d[MICRO_MAX_CONV]; // LDS float offset of each conv's dZ images [S][Ho*Wo][c.cs]
     int zero;
     int lds_floats;
-    int wasg[MICRO_MAX_CONV][4];   // per level, per wave: sub-pixel phase | first tile << 4 | tiles << 12
+    int nw;                    // waves per workgroup (4 or 8)
+    int wasg[MICRO_MAX_CONV][8];   // per level, per wave: phase | first tile << 4 | tiles << 12 | first row tile << 16 | row tiles << 20
+    int64_t* stamps;           // diagnostic builds: slots 47..52
 };
 struct MicroDwLayer {
     int Ci, Hi, Wi, Co, Ho, Wo, sh, sw;

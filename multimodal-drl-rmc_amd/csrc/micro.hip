@@ -121,12 +121,16 @@ static int dx_lds_floats(const MicroConv* c, int nc, int S, int* lds_d, int* zer
     *zero = cur;
     return cur + MICRO_ZERO;
 }
-// data gradients: a wave owns (sub-pixel phase, a contiguous run of that phase's pixel tiles) and
-// every ci row tile of it (MT = Ci/16 accumulator rows): the phase's taps' weights are read by that
-// phase's waves only, and a wave carries MT x NTW independent accumulators.  Waves are dealt to
-// phases to minimise the busiest wave's tiles x taps.
+// data gradients: a wave owns (sub-pixel phase, a contiguous run of that phase's pixel tiles, a
+// contiguous run of its ci row tiles): the phase's taps' weights are read by that phase's waves
+// only, and a wave carries (row tiles) x (pixel tiles) independent accumulators.  Each phase's
+// tiles x rows are split over its waves, the phases' splits chosen to minimise the busiest SIMD's
+// MFMAs (wave w on SIMD w % 4), then the busiest wave's.  8 waves per workgroup (the default at
+// one sample per workgroup: one workgroup per CU at B = 256, so 2 waves per SIMD hide each other's
+// LDS / weight latency); DQNX_MDX_WAVES=4 keeps 4.
 constexpr int MNT_DX = 4;      // pixel tiles per wave and level in the data-gradient kernel ...
 constexpr int MACC_DX = 8;     // ... and row x pixel accumulator tiles (5 tiles spill)
+constexpr int MWD_MAX = 8;     // waves per data-gradient workgroup (max)
 static int dx_phase_tiles(const MicroConv& L, int ph, int S, int* taps) {
     const int pa = ph / L.sw, pc = ph - pa * L.sw;
     const int Hq = (L.Hi - pa + L.sh - 1) / L.sh, Wq = (L.Wi - pc + L.sw - 1) / L.sw;
@@ -134,48 +138,87 @@ static int dx_phase_tiles(const MicroConv& L, int ph, int S, int* taps) {
     *taps = ((2 - i0) / L.sh + 1) * ((2 - j0) / L.sw + 1);
     return (S * Hq * Wq + 15) / 16;
 }
-static bool dx_assign(const MicroConv& L, int S, int* asg) {   // asg[MW]: phase | t0 << 4 | nt << 12
-    const int nph = L.sh * L.sw;
-    if (nph > MW) return false;
+static bool dx_assign(const MicroConv& L, int S, int nw, int* asg) {   // asg[nw]; nt = 0: idle wave
+    const int nph = L.sh * L.sw, MT = L.Ci / 16;
+    if (nph > nw || nph > 4) return false;
     int tiles[4], taps[4];
     for (int p = 0; p < nph; p++) tiles[p] = dx_phase_tiles(L, p, S, &taps[p]);
-    int best = 1 << 30, bk[4] = {0, 0, 0, 0};
-    int k[4];
-    // every composition of MW waves into nph phases (each phase at least one wave)
-    for (k[0] = 1; k[0] <= MW; k[0]++)
-        for (k[1] = nph > 1 ? 1 : 0; k[1] <= (nph > 1 ? MW : 0); k[1]++)
-            for (k[2] = nph > 2 ? 1 : 0; k[2] <= (nph > 2 ? MW : 0); k[2]++)
-                for (k[3] = nph > 3 ? 1 : 0; k[3] <= (nph > 3 ? MW : 0); k[3]++) {
-                    if (k[0] + k[1] + k[2] + k[3] != MW) continue;
-                    int cost = 0;
-                    bool ok = true;
-                    for (int p = 0; p < nph; p++) {
-                        const int nt = (tiles[p] + k[p] - 1) / k[p];
-                        ok = ok && nt <= MNT_DX && nt * (L.Ci / 16) <= MACC_DX;
-                        cost = std::max(cost, nt * taps[p]);
-                    }
-                    if (ok && cost < best) {
-                        best = cost;
-                        for (int p = 0; p < 4; p++) bk[p] = k[p];
+    // per phase: (tile split ts, row split rs) options
+    struct Opt { int ts, rs; };
+    std::vector<Opt> opts[4];
+    for (int p = 0; p < nph; p++)
+        for (int rs = 1; rs <= MT; rs *= 2) {
+            if (MT % rs) continue;
+            for (int ts = 1; ts <= std::min(tiles[p], nw); ts++) {
+                const int nt = (tiles[p] + ts - 1) / ts;
+                if (ts * rs <= nw && nt <= MNT_DX && nt * (MT / rs) <= MACC_DX) opts[p].push_back({ts, rs});
+            }
+        }
+    for (int p = 0; p < nph; p++)
+        if (opts[p].empty()) return false;
+    long best = -1;
+    int bw[MWD_MAX * 2], nbw = 0;
+    int idx[4] = {0, 0, 0, 0};
+    while (true) {
+        int waves = 0;
+        for (int p = 0; p < nph; p++) waves += opts[p][idx[p]].ts * opts[p][idx[p]].rs;
+        if (waves <= nw) {
+            // the waves (encoded) and their costs (MFMA k-steps: tiles x taps x rows)
+            int enc[MWD_MAX], cost[MWD_MAX], n = 0;
+            for (int p = 0; p < nph; p++) {
+                const Opt o = opts[p][idx[p]];
+                for (int j = 0; j < o.ts; j++) {
+                    const int t0 = tiles[p] * j / o.ts, t1 = tiles[p] * (j + 1) / o.ts;
+                    for (int r = 0; r < o.rs; r++) {
+                        const int mw = MT / o.rs;
+                        enc[n] = p | (t0 << 4) | ((t1 - t0) << 12) | ((r * mw) << 16) | (mw << 20);
+                        cost[n++] = (t1 - t0) * taps[p] * mw;
                     }
                 }
-    if (best == 1 << 30) return false;
-    int w = 0;
-    for (int p = 0; p < nph; p++)
-        for (int j = 0; j < bk[p]; j++) {   // tiles split as evenly as possible, in order
-            const int t0 = tiles[p] * j / bk[p], t1 = tiles[p] * (j + 1) / bk[p];
-            asg[w++] = p | (t0 << 4) | ((t1 - t0) << 12);
+            }
+            // heaviest first, each onto the least loaded SIMD with a free slot
+            int order[MWD_MAX];
+            for (int i = 0; i < n; i++) order[i] = i;
+            std::sort(order, order + n, [&](int x, int y) { return cost[x] > cost[y] || (cost[x] == cost[y] && x < y); });
+            int load[4] = {0, 0, 0, 0}, used[4] = {0, 0, 0, 0}, slot[MWD_MAX];
+            const int per = nw / 4;
+            for (int i = 0; i < n; i++) {
+                int sbest = -1;
+                for (int sd = 0; sd < 4; sd++)
+                    if (used[sd] < per && (sbest < 0 || load[sd] < load[sbest])) sbest = sd;
+                slot[order[i]] = sbest + 4 * used[sbest];
+                used[sbest]++;
+                load[sbest] += cost[order[i]];
+            }
+            int mx = 0, mwv = 0;
+            for (int sd = 0; sd < 4; sd++) mx = std::max(mx, load[sd]);
+            for (int i = 0; i < n; i++) mwv = std::max(mwv, cost[i]);
+            const long key = (long)mx * 4096 + mwv;
+            if (best < 0 || key < best) {
+                best = key;
+                nbw = nw;
+                for (int w = 0; w < nw; w++) bw[w] = 0;   // idle: nt = 0
+                for (int i = 0; i < n; i++) bw[slot[i]] = enc[i];
+            }
         }
+        int p = 0;
+        while (p < nph && ++idx[p] == (int)opts[p].size()) idx[p++] = 0;
+        if (p == nph) break;
+    }
+    if (best < 0) return false;
+    for (int w = 0; w < nbw; w++) asg[w] = bw[w];
     return true;
 }
+static int dx_waves_knob() { return route_knob("DQNX_MDX_WAVES", 8) == 4 ? 4 : 8; }
 bool micro_dx_plan(const MicroConv* convs, int nc, int Bl, int* S_out, int* lds_d, int* lds_floats) {
     if (!micro_geom_ok(convs, nc)) return false;
     (void)Bl;
+    const int nw = dx_waves_knob();
     for (int S = 1; S <= 3; S++) {   // S = 1: one workgroup per sample (B = 256: one per CU)
-        int zero, asg[MW];
+        int zero, asg[MWD_MAX];
         const int lf = dx_lds_floats(convs, nc, S, lds_d, &zero);
         bool ok = (size_t)lf * 4 <= 160 * 1024;
-        for (int l = 1; l < nc && ok; l++) ok = dx_assign(convs[l], S, asg) && convs[l].Ci / 16 <= 4;
+        for (int l = 1; l < nc && ok; l++) ok = dx_assign(convs[l], S, nw, asg) && convs[l].Ci / 16 <= 4;
         if (ok) {
             *S_out = S;
             *lds_floats = lf;
@@ -185,7 +228,8 @@ bool micro_dx_plan(const MicroConv* convs, int nc, int Bl, int* S_out, int* lds_
     return false;
 }
 void micro_dx_waves(MicroDxArgs& a) {
-    for (int l = 1; l < a.nc; l++) dx_assign(a.c[l], a.S, a.wasg[l]);
+    a.nw = dx_waves_knob();
+    for (int l = 1; l < a.nc; l++) dx_assign(a.c[l], a.S, a.nw, a.wasg[l]);
 }
 
 // weight gradients.  convs 2..: a workgroup = (ci tile, slice of samples), wave w owns co tile w
@@ -448,14 +492,28 @@ __device__ __forceinline__ float4 bias_elu(const floatx4& a, const float4& b) {
 }
 
 // conv 1: K = Ci*9 <= 64 in torch order k = (ci, i, j); A = W straight from the parameters, B
-// gathered per k-step from the CHW images (scalar LDS reads, zero outside the grid)
+// gathered per k-step from the CHW images (scalar LDS reads, zero outside the grid).  The lane's
+// weights (k = 4 st + g, zero past K0) and bias are loaded with the input images (conv1_weights).
+constexpr int MICRO_C1_KS = 16;   // k-steps of conv 1: Ci*9 <= 64
+__device__ __forceinline__ void conv1_weights(const MicroConv& L, const float* P, int mt, float (&wv)[MICRO_C1_KS],
+                                              float4& bv4) {
+    const int lane = threadIdx.x & 63, i16 = lane & 15, g = lane >> 4, K0 = L.Ci * 9;
+    const float* W = P + L.woff + (int64_t)(mt * 16 + i16) * K0;
+#pragma unroll
+    for (int st = 0; st < MICRO_C1_KS; st++) {
+        const int k = 4 * st + g;
+        const float w = W[k < K0 ? k : K0 - 1];   // unconditional (vmcnt)
+        wv[st] = k < K0 ? w : 0.f;
+    }
+    const float* bias = P + L.woff + (int64_t)L.Co * K0 + mt * 16 + 4 * g;
+    bv4 = make_float4(bias[0], bias[1], bias[2], bias[3]);
+}
 template <int NTW>
-__device__ __forceinline__ void micro_conv1(const MicroFwdArgs& a, const MicroConv& L, float* lds, const float* P,
-                                            bool keep, int b0, int ns, int mt, int n0, int nst) {
+__device__ __forceinline__ void micro_conv1(const MicroFwdArgs& a, const MicroConv& L, float* lds, const float (&wv)[MICRO_C1_KS],
+                                            float4 bv4, bool keep, int b0, int ns, int mt, int n0, int nst) {
     const int lane = threadIdx.x & 63, i16 = lane & 15, g = lane >> 4;
     const int Pq = L.Ho * L.Wo, img = L.Ci * L.Hi * L.Wi, HW = L.Hi * L.Wi, K0 = L.Ci * 9, ks = (K0 + 3) >> 2;
     const int npx = a.S * Pq;
-    const float* W = P + L.woff + (int64_t)(mt * 16 + i16) * K0;
     int r0[NTW], c0[NTW], xb[NTW];
 #pragma unroll
     for (int t = 0; t < NTW; t++) {
@@ -470,24 +528,24 @@ __device__ __forceinline__ void micro_conv1(const MicroFwdArgs& a, const MicroCo
     floatx4 acc[NTW];
 #pragma unroll
     for (int t = 0; t < NTW; t++) acc[t] = floatx4{0.f, 0.f, 0.f, 0.f};
-    for (int st = 0; st < ks; st++) {
-        const int k = 4 * st + g;
-        const float w = W[k < K0 ? k : K0 - 1];
-        const float av = k < K0 ? w : 0.f;
-        const int ci = k / 9, tap = k - 9 * ci, ti = tap / 3, tj = tap - 3 * ti;
-        float bv[NTW];
 #pragma unroll
-        for (int t = 0; t < NTW; t++) {
-            const int r = r0[t] + ti, c = c0[t] + tj;
-            const bool ok = k < K0 && (unsigned)r < (unsigned)L.Hi && (unsigned)c < (unsigned)L.Wi;
-            bv[t] = lds[ok ? xb[t] + ci * HW + r * L.Wi + c : a.zero];
+    for (int st = 0; st < MICRO_C1_KS; st++) {
+        if (st < ks) {
+            const int k = 4 * st + g;
+            const float av = wv[st];
+            const int ci = k / 9, tap = k - 9 * ci, ti = tap / 3, tj = tap - 3 * ti;
+            float bv[NTW];
+#pragma unroll
+            for (int t = 0; t < NTW; t++) {
+                const int r = r0[t] + ti, c = c0[t] + tj;
+                const bool ok = k < K0 && (unsigned)r < (unsigned)L.Hi && (unsigned)c < (unsigned)L.Wi;
+                bv[t] = lds[ok ? xb[t] + ci * HW + r * L.Wi + c : a.zero];
+            }
+#pragma unroll
+            for (int t = 0; t < NTW; t++) acc[t] = mfma16x16x4(av, bv[t], acc[t]);
         }
-#pragma unroll
-        for (int t = 0; t < NTW; t++) acc[t] = mfma16x16x4(av, bv[t], acc[t]);
     }
     const int co0 = mt * 16 + 4 * g;
-    const float* bias = P + L.woff + (int64_t)L.Co * K0 + co0;
-    const float4 bv4 = make_float4(bias[0], bias[1], bias[2], bias[3]);
 #pragma unroll
     for (int t = 0; t < NTW; t++) {
         const int p = (n0 + t * nst) * 16 + i16;
@@ -572,7 +630,12 @@ __global__ __launch_bounds__(MTH, 3) void k_micro_fwd(MicroFwdArgs a) {   // 3 w
         return;
     }
     const int bid = (int)blockIdx.x - (a.samp_on ? 1 : 0);
+    const int sblk = a.samp_on ? 1 : 0;   // diagnostic stamps: the first compute workgroup
+    DQNX_STAMP_BLK(a.stamps, 40, sblk);
     const int tid = threadIdx.x, wid = tid >> 6;
+#ifdef DQNX_STAMPS
+    if (a.stamps && blockIdx.x == (unsigned)sblk && (tid & 63) == 0) a.stamps[56 + wid] = (int64_t)__builtin_amdgcn_s_memtime();
+#endif
     const int z = bid / a.groups, grp = bid - z * a.groups;
     const int s = a.stream_of[z];
     const int tgt = s == 2 ? 1 : 0;
@@ -583,34 +646,73 @@ __global__ __launch_bounds__(MTH, 3) void k_micro_fwd(MicroFwdArgs a) {   // 3 w
     const int b0 = grp * a.S, ns = min(a.S, a.Bl - b0);
 
     // (0) the micro grids of the S gathered rows -> LDS (CHW, zero past the batch); the F row tail
-    //     = the macro features + zero padding (R:env/dqn_config.py:138: cat([cnn_out, macro]))
+    //     = the macro features + zero padding (R:env/dqn_config.py:138: cat([cnn_out, macro])).
+    //     One round of loads: the rows' offsets (uniform), then every grid / tail element of this
+    //     thread's first batch and conv 1's weights are in flight together before any store.
+    const MicroConv& C0 = a.c[0];
+    const int c1_mt = wid % (C0.Co >> 4);
+    float c1w[MICRO_C1_KS];
+    float4 c1b;
     {
-        const MicroConv& C0 = a.c[0];
-        const int img = C0.Ci * C0.Hi * C0.Wi;
-        for (int e = tid; e < a.S * img; e += MTH) {
-            const int sb = e / img, k = e - sb * img;
-            float v = 0.f;
-            if (sb < ns) v = ring[(int64_t)a.phys[b0 + sb] * a.ring_stride + a.macro_len + k];
-            lds[a.x0 + e] = v;
+        const int img = C0.Ci * C0.Hi * C0.Wi, tot = a.S * img, tail = a.strideF - a.flat_cols, ttot = ns * tail;
+        int64_t ro[3];
+#pragma unroll
+        for (int sb = 0; sb < 3; sb++) ro[sb] = (int64_t)a.phys[b0 + min(sb, ns - 1)] * a.ring_stride;
+        auto row = [&](int sb) { return sb == 0 ? ro[0] : (sb == 1 ? ro[1] : ro[2]); };
+        constexpr int GE = 4;   // grid elements per thread and batch
+        auto gload = [&](int base, float (&v)[GE]) {
+#pragma unroll
+            for (int j = 0; j < GE; j++) {
+                const int e = min(base + tid + j * MTH, tot - 1), sb = e / img;
+                const float x = ring[row(sb) + a.macro_len + (e - sb * img)];   // unconditional (vmcnt)
+                v[j] = sb < ns ? x : 0.f;
+            }
+        };
+        auto gstore = [&](int base, const float (&v)[GE]) {
+#pragma unroll
+            for (int j = 0; j < GE; j++)
+                if (base + tid + j * MTH < tot) lds[a.x0 + base + tid + j * MTH] = v[j];
+        };
+        auto tload = [&](int e) {
+            if (tail == 0 || a.macro_len == 0) return 0.f;
+            const int ec = min(e, max(ttot - 1, 0)), sb = ec / tail, m = ec - sb * tail;
+            const float x = ring[row(sb) + min(m, a.macro_len - 1)];
+            return m < a.macro_len ? x : 0.f;
+        };
+        auto tstore = [&](int e, float v) {
+            if (e < ttot) {
+                const int sb = e / tail, m = e - sb * tail;
+                F[(int64_t)(b0 + sb) * a.strideF + a.flat_cols + m] = v;
+            }
+        };
+        float v[GE];
+        DQNX_STAMP_BLK_W(a.stamps, 53, sblk);
+        gload(0, v);
+        const float tv = tload(tid);
+        conv1_weights(C0, P, c1_mt, c1w, c1b);
+        DQNX_STAMP_BLK_W(a.stamps, 54, sblk);
+        gstore(0, v);
+        tstore(tid, tv);
+        DQNX_STAMP_BLK_W(a.stamps, 55, sblk);
+        for (int base = GE * MTH; base < tot; base += GE * MTH) {   // grids past one batch (larger S)
+            gload(base, v);
+            gstore(base, v);
         }
+        for (int e = tid + MTH; e < ttot; e += MTH) tstore(e, tload(e));
         if (tid < MICRO_ZERO) lds[a.zero + tid] = 0.f;
-        const int tail = a.strideF - a.flat_cols;
-        for (int e = tid; e < ns * tail; e += MTH) {
-            const int sb = e / tail, m = e - sb * tail;
-            const float v = m < a.macro_len ? ring[(int64_t)a.phys[b0 + sb] * a.ring_stride + m] : 0.f;
-            F[(int64_t)(b0 + sb) * a.strideF + a.flat_cols + m] = v;
-        }
     }
     micro_barrier();
+    DQNX_STAMP_BLK(a.stamps, 41, sblk);
     {   // (1) conv 1
         const MicroConv& L = a.c[0];
         const int Mt = L.Co >> 4, nst = MW / Mt, n0 = wid / Mt, mt = wid - n0 * Mt;
         const int ntw = wave_tiles((a.S * L.Ho * L.Wo + 15) >> 4, n0, nst);
-#define C1(N) micro_conv1<N>(a, L, lds, P, keep, b0, ns, mt, n0, nst)
+#define C1(N) micro_conv1<N>(a, L, lds, c1w, c1b, keep, b0, ns, mt, n0, nst)
         MICRO_DISPATCH6(ntw, C1)
 #undef C1
     }
     micro_barrier();
+    DQNX_STAMP_BLK(a.stamps, 42, sblk);
     // (2) convs 2 .. NC, each from the previous conv's LDS image (constant layer indices)
     auto conv = [&](const MicroConv& L, const MicroConv& Lp, bool last) {
         const int Mt = L.Co >> 4, nst = MW / Mt, n0 = wid / Mt, mt = wid - n0 * Mt;
@@ -630,8 +732,10 @@ __global__ __launch_bounds__(MTH, 3) void k_micro_fwd(MicroFwdArgs a) {   // 3 w
         conv(a.c[1], a.c[0], true);
     } else {
         conv(a.c[1], a.c[0], false);
+        DQNX_STAMP_BLK(a.stamps, 43, sblk);
         conv(a.c[2], a.c[1], true);
     }
+    DQNX_STAMP_BLK(a.stamps, 44, sblk);
 }
 
 int launch_micro_fwd(const MicroFwdArgs& a, hipStream_t s) {
@@ -656,7 +760,7 @@ int launch_micro_fwd(const MicroFwdArgs& a, hipStream_t s) {
 // K = its taps x co (B = dZ_l image from LDS, float4 over co).
 template <int MT, int NTW>
 __device__ __forceinline__ void micro_dx_phase(const MicroDxArgs& a, const MicroConv& L, const MicroConv& Lp, float* lds,
-                                               int l, int b0, int ns, int pa, int pc, int t0) {
+                                               int l, int b0, int ns, int pa, int pc, int t0, int m0) {
     const int lane = threadIdx.x & 63, i16 = lane & 15, g = lane >> 4;
     const int Pq = L.Ho * L.Wo, Pin = L.Hi * L.Wi;
     const int Hq = (L.Hi - pa + L.sh - 1) / L.sh, Wq = (L.Wi - pc + L.sw - 1) / L.sw, HWq = Hq * Wq;
@@ -675,7 +779,7 @@ __device__ __forceinline__ void micro_dx_phase(const MicroDxArgs& a, const Micro
         xb[t] = xq + (pc + 1 - j0) / L.sw;
         ob[t] = sb * Pq;
     }
-    const float* wrow = L.wT + (int64_t)i16 * 9 * L.Co + 4 * g;   // row tile m: + m * 16 * 9 * Co
+    const float* wrow = L.wT + (int64_t)(m0 * 16 + i16) * 9 * L.Co + 4 * g;   // row tile m: + m * 16 * 9 * Co
     const int ldz = a.lds_d[l];
     floatx4 acc[MT][NTW];
 #pragma unroll
@@ -692,56 +796,79 @@ __device__ __forceinline__ void micro_dx_phase(const MicroDxArgs& a, const Micro
         const int tu = ch >> lcpt, u = tu / nj, v = tu - u * nj;
         return ((i0 + L.sh * u) * 3 + j0 + L.sw * v) * L.Co + (ch & (cpt - 1)) * 16;
     };
+    // conv l-1's outputs for the epilogue's ELU', loaded ahead of the GEMM (unconditional: pixels
+    // outside re-read the tile's first valid one)
+    int pixo[NTW], hrow[NTW];
+    float4 hv[MT][NTW];
+#pragma unroll
+    for (int t = 0; t < NTW; t++) {
+        const int p = (t0 + t) * 16 + i16;
+        const bool v = p < npx && p / HWq < ns;
+        const int pc_ = v ? p : 0;
+        const int sb = pc_ / HWq, mm = pc_ - sb * HWq;
+        const int yq = mm / Wq, xq = mm - yq * Wq;
+        pixo[t] = v ? sb * Pin + (pa + L.sh * yq) * L.Wi + pc + L.sw * xq : -1;
+        hrow[t] = b0 * Pin + sb * Pin + (pa + L.sh * yq) * L.Wi + pc + L.sw * xq;
+#pragma unroll
+        for (int m = 0; m < MT; m++) hv[m][t] = ld4(Lp.hc + (int64_t)hrow[t] * L.Ci + (m0 + m) * 16 + 4 * g);
+    }
     igemm_chunks_m<MT, NTW>(lds, wrow, 16 * 9 * L.Co, ni * nj * cpt, lcpt, base_of, woff, acc);
     // epilogue: ELU' of conv l-1's output (torch elu_backward on the result)
 #pragma unroll
     for (int t = 0; t < NTW; t++) {
-        const int p = (t0 + t) * 16 + i16;
-        if (p >= npx) continue;
-        const int sb = p / HWq, mm = p - sb * HWq;
-        if (sb >= ns) continue;
-        const int yq = mm / Wq, xq = mm - yq * Wq;
-        const int pix = (pa + L.sh * yq) * L.Wi + pc + L.sw * xq;
+        if (pixo[t] < 0) continue;
 #pragma unroll
         for (int m = 0; m < MT; m++) {
-            const int ci0 = m * 16 + 4 * g;
-            const int64_t go = ((int64_t)(b0 + sb) * Pin + pix) * L.Ci + ci0;
-            const float4 h = ld4(Lp.hc + go);
+            const int ci0 = (m0 + m) * 16 + 4 * g;
+            const int64_t go = (int64_t)hrow[t] * L.Ci + ci0;
+            const float4 h = hv[m][t];
             const float4 d = make_float4(act_bwd<DQNX_ACT_ELU>(acc[m][t][0], h.x), act_bwd<DQNX_ACT_ELU>(acc[m][t][1], h.y),
                                          act_bwd<DQNX_ACT_ELU>(acc[m][t][2], h.z), act_bwd<DQNX_ACT_ELU>(acc[m][t][3], h.w));
             *reinterpret_cast<float4*>(Lp.dz + go) = d;
-            if (l - 1 >= 1) *reinterpret_cast<float4*>(lds + a.lds_d[l - 1] + (sb * Pin + pix) * Lp.cs + ci0) = d;
+            if (l - 1 >= 1) *reinterpret_cast<float4*>(lds + a.lds_d[l - 1] + pixo[t] * Lp.cs + ci0) = d;
         }
     }
 }
 
-template <int NC>
-__global__ __launch_bounds__(MTH) void k_micro_dx(MicroDxArgs a) {
+template <int NC, int NW>
+__global__ __launch_bounds__(64 * NW) void k_micro_dx(MicroDxArgs a) {
+    constexpr int MTH = 64 * NW;
     extern __shared__ __attribute__((aligned(16))) float lds[];
+    DQNX_STAMP(a.stamps, 47);
     const int tid = threadIdx.x, wid = tid >> 6;
     const int b0 = blockIdx.x * a.S, ns = min(a.S, a.Bl - b0);
     // (0) dZ of the last conv: the dF rows (flatten_CHW order) -> LDS (NHWC) and the HBM copy
-    {
+    {   // batches of DE elements per thread, every load of a batch in flight before its stores
         const MicroConv& L = a.c[NC - 1];
-        const int Pq = L.Ho * L.Wo, per = L.Co * Pq;
-        for (int e = tid; e < a.S * per; e += MTH) {
-            const int sb = e / per, rem = e - sb * per, co = rem / Pq, q = rem - co * Pq;
-            float v = 0.f;
-            if (sb < ns) {
-                v = a.dF[(int64_t)(b0 + sb) * a.ldf + rem];
-                L.dz[((int64_t)(b0 + sb) * Pq + q) * L.Co + co] = v;
+        const int Pq = L.Ho * L.Wo, per = L.Co * Pq, tot = a.S * per;
+        constexpr int DE = 8;
+        for (int base = 0; base < tot; base += DE * MTH) {
+            float v[DE];
+#pragma unroll
+            for (int j = 0; j < DE; j++) {
+                const int e = min(base + tid + j * MTH, tot - 1), sb = e / per;
+                const float x = a.dF[(int64_t)(b0 + min(sb, ns - 1)) * a.ldf + (e - sb * per)];   // unconditional (vmcnt)
+                v[j] = sb < ns ? x : 0.f;
             }
-            lds[a.lds_d[NC - 1] + (sb * Pq + q) * L.cs + co] = v;
+#pragma unroll
+            for (int j = 0; j < DE; j++) {
+                const int e = base + tid + j * MTH;
+                if (e >= tot) break;
+                const int sb = e / per, rem = e - sb * per, co = rem / Pq, q = rem - co * Pq;
+                if (sb < ns) L.dz[((int64_t)(b0 + sb) * Pq + q) * L.Co + co] = v[j];
+                lds[a.lds_d[NC - 1] + (sb * Pq + q) * L.cs + co] = v[j];
+            }
         }
         if (tid < MICRO_ZERO) lds[a.zero + tid] = 0.f;
     }
     micro_barrier();
+    DQNX_STAMP(a.stamps, 48);
     // levels NC-1 .. 1 (constant layer indices); this wave's (phase, tile run) from the host plan
     auto level = [&](const MicroConv& L, const MicroConv& Lp, int l) {
-        const int w = a.wasg[l][wid], ph = w & 15, t0 = (w >> 4) & 255, nt = w >> 12;
+        const int w = a.wasg[l][wid], ph = w & 15, t0 = (w >> 4) & 255, nt = (w >> 12) & 15;
+        const int m0 = (w >> 16) & 15, mt = (w >> 20) & 15;
         const int pa = ph / L.sw, pc = ph - pa * L.sw;
-        const int mt = L.Ci >> 4;
-#define DX(M, N) micro_dx_phase<M, N>(a, L, Lp, lds, l, b0, ns, pa, pc, t0)
+#define DX(M, N) micro_dx_phase<M, N>(a, L, Lp, lds, l, b0, ns, pa, pc, t0, m0)
 #define DXN(M)                      \
     switch (nt) {                   \
         case 1: DX(M, 1); break;    \
@@ -767,15 +894,22 @@ __global__ __launch_bounds__(MTH) void k_micro_dx(MicroDxArgs a) {
     if constexpr (NC == 3) {
         level(a.c[2], a.c[1], 2);
         micro_barrier();
+        DQNX_STAMP(a.stamps, 49);
     }
     level(a.c[1], a.c[0], 1);
+    DQNX_STAMP(a.stamps, 50);
 }
 
 int launch_micro_dx(const MicroDxArgs& a, hipStream_t s) {
     const dim3 grid(a.groups);
     const size_t lds = (size_t)a.lds_floats * 4;
-    if (a.nc == 3) hipLaunchKernelGGL(k_micro_dx<3>, grid, dim3(MTH), lds, s, a);
-    else hipLaunchKernelGGL(k_micro_dx<2>, grid, dim3(MTH), lds, s, a);
+    if (a.nw == 8) {
+        if (a.nc == 3) hipLaunchKernelGGL((k_micro_dx<3, 8>), grid, dim3(512), lds, s, a);
+        else hipLaunchKernelGGL((k_micro_dx<2, 8>), grid, dim3(512), lds, s, a);
+    } else {
+        if (a.nc == 3) hipLaunchKernelGGL((k_micro_dx<3, 4>), grid, dim3(256), lds, s, a);
+        else hipLaunchKernelGGL((k_micro_dx<2, 4>), grid, dim3(256), lds, s, a);
+    }
     DQNX_HIP_CHECK(hipGetLastError());
     return DQNX_OK;
 }

@@ -248,3 +248,30 @@ def test_gpu_hybrid_adam_written_conv_copies_bit_identical(algo):
     e2.check_device_error()
     assert torch.equal(e1.q, e2.q) and torch.equal(e1.grads, e2.grads)
     assert torch.equal(e1.params, e2.params) and torch.equal(e1.target_params, e2.target_params)
+
+
+def _run_hybrid_steps(algo, batch, steps, seed):
+    _, eng = make_hybrid_pair(algo, batch, 2000, 1500, seed)
+    for _ in range(steps):
+        eng.learn_step(soft_update=True)
+    torch.cuda.synchronize()
+    eng.check_device_error()
+    out = [eng.params.cpu().clone(), eng.target_params.cpu().clone(), eng.q.cpu().clone()]
+    del eng
+    return out
+
+
+@pytest.mark.parametrize("knob,a,b", [
+    ("DQNX_MDX_WAVES", "8", "4"),    # micro data gradients: 8 vs 4 waves per workgroup
+])
+@pytest.mark.parametrize("algo,batch", [("DuelingDoubleDQNAgent", 256), ("PerDuelingDoubleDQNAgent", 100)])
+def test_gpu_hybrid_head_variants_bit_identical(monkeypatch, knob, a, b, algo, batch):
+    """The HEAD net's launch variants change only where partial sums are combined or which wave
+    computes an output, never the order of any sum: parameters, targets and Q-values stay bitwise
+    equal over 4 steps."""
+    monkeypatch.setenv(knob, a)
+    ra = _run_hybrid_steps(algo, batch, 4, 41)
+    monkeypatch.setenv(knob, b)
+    rb = _run_hybrid_steps(algo, batch, 4, 41)
+    for x, y, name in zip(ra, rb, ("params", "target", "q")):
+        assert torch.equal(x, y), f"{knob}={a} vs {b}: {name} differ"

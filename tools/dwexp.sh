@@ -1,7 +1,7 @@
 # per-conv timing of k_micro_dw (tuning build: DQNX_MDW_SKIP masks convs out, DQNX_MDW_SPW<l> overrides)
 set -u
 mkdir -p gpurun_out/dwexp
-export DQNX_LIB=multimodal-drl-rmc_amd/dqn/_lib/libdqnx_tuning.so
+export DQNX_LIB=${DQNX_LIB:-multimodal-drl-rmc_amd/dqn/_lib/libdqnx_stamps.so}
 run() { # tag envs...
   tag=$1; shift
   env "$@" timeout -k 10 120 python bench.py --net hybrid --batch 256 --no-cpu-baseline --no-extras --steps 50 --warmup 5 > gpurun_out/dwexp/$tag.json 2> gpurun_out/dwexp/$tag.err || return 1

@@ -1,5 +1,9 @@
-"""Diagnostic: s_memtime phase stamps of conv 1's first k_micro_dw workgroup (block 0, wave 0;
-libdqnx_stamps.so) on the HEAD net (Hybrid-284) learn step."""
+"""Diagnostic (libdqnx_stamps.so): s_memtime phase stamps of the micro-CNN kernels on the HEAD net
+(Hybrid-284 (2,27,5), DuelingDouble, uniform replay, B = argv[1] (256)).
+
+k_micro_fwd, first compute workgroup: input staged (41), conv 1 (42), conv 2 (43), conv 3 + F (44);
+over all waves: earliest start (45) / latest end (46).  k_micro_dx, workgroup 0: dF staged (48),
+level 2 (49), level 1 (50); all waves: 51 / 52.  k_micro_dw conv 1 workgroup 0: slots 24..39."""
 import ctypes
 import os
 import random
@@ -17,27 +21,25 @@ from dqn import _capi as C  # noqa: E402
 from dqn.engine import LearnEngine, hybrid_spec  # noqa: E402
 
 B = int(sys.argv[1]) if len(sys.argv) > 1 else 256
-CAP = 100_000
+CAP = int(sys.argv[2]) if len(sys.argv) > 2 else 100_000
 spec = hybrid_spec(8, "dueling", micro_chw=(2, 27, 5))
-eng = LearnEngine(spec, "PerDuelingDoubleDQNAgent", B, CAP, graphs=False)
+eng = LearnEngine(spec, "DuelingDoubleDQNAgent", B, CAP, graphs=False)
 eng.load_params(bench.init_params(spec))
 bench.fill_ring(eng, CAP, spec.obs_dim, 8, eng.device)
 random.seed(1234)
 eng.set_rng(0, np.array(random.getstate()[1], dtype=np.uint32))
 out = (ctypes.c_int64 * 64)()
-names = {25: "maps+borders", 26: "first loads issued", 27: "first store+barriers", 36: "stages 2..", 39: "reduce+write"}
-for s_ in range(2):
-    for k, nm in enumerate(("next loads issued", "mfma loop", "db", "store+barriers")):
-        names[28 + 4 * s_ + k] = f"stage {s_} {nm}"
-for step in range(5):
+M = 1 << 62
+for step in range(6):
     eng.learn_step(soft_update=True)
     torch.cuda.synchronize()
     C.check(C.lib().dqnx_debug_stamps(eng.h, out, eng.stream()), "stamps")
     s = list(out)
-    d = s[24:40]
-    seq, prev = [], d[0]
-    for j in range(1, 16):
-        if d[j] and d[j] >= prev:
-            seq.append(f"{names.get(24 + j, 24 + j)} {d[j] - prev}")
-            prev = d[j]
-    print(f"step {step}: micro_dw conv1 wg0 total {prev - d[0]} cyc: " + ", ".join(seq))
+    f0 = s[40]
+    print(f"step {step}: fwd wg: staged {s[41] - f0} conv1 {s[42] - s[41]} conv2 {s[43] - s[42]} conv3 {s[44] - s[43]} "
+          f"(total {s[44] - f0})", flush=True)
+
+    print(f"        fwd staging: rows {s[53] - f0} loads {s[54] - s[53]} stores {s[55] - s[54]} barrier {s[41] - s[55]}; "
+          f"wave starts {[s[56 + w] - f0 for w in range(4)]}", flush=True)
+    d0 = s[47]
+    print(f"        dx wg0: staged {s[48] - d0} level2 {s[49] - s[48]} level1 {s[50] - s[49]} (total {s[50] - d0})", flush=True)
