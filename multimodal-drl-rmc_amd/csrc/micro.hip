@@ -288,10 +288,11 @@ int micro_dw_plan(MicroDwArgs& a, int n_cu) {
         return l == 0 ? (L.nct * (L.Co / 16) + MW - 1) / MW : L.nct;
     };
     // (constants fitted to the per-conv timings of tools/dwexp.sh on the HEAD net: ~14K cycles of
-    // start, conv 1 ~3.3K cycles per sample, MFMA issue ~1.5x the two-wave pipe time)
+    // start, MFMA issue ~1.5x the two-wave pipe time; conv 1 ~4.8K cycles per sample, refitted in
+    // round 5 (tools/variants/mdw_spw3.txt: 11 samples per slice 30.7 us, 6-8 samples 26.5 us))
     auto cost = [&](int l, int spw) {
         const MicroDwLayer& L = a.L[l];
-        if (l == 0) return 14000.0 + 3250.0 * spw;
+        if (l == 0) return 14000.0 + 4800.0 * spw;
         return 14000.0 + 2500.0 * ((spw + L.G - 1) / L.G) + 1.5 * 64.0 * dw_mfma_per_sample_wave(L, false) * spw;
     };
     auto spw_for = [&](int l, double T) {   // the most samples per workgroup within makespan T (0: none)
@@ -325,7 +326,7 @@ int micro_dw_plan(MicroDwArgs& a, int n_cu) {
         MicroDwLayer& L = a.L[l];
         const bool first = l == 0;
         int spw = std::max(1, spw_for(l, Thi));
-        spw = std::max(1, std::min(tuning_knob(l == 0 ? "DQNX_MDW_SPW0" : l == 1 ? "DQNX_MDW_SPW1" : "DQNX_MDW_SPW2", spw), a.Bl));
+        spw = std::max(1, std::min(route_knob(l == 0 ? "DQNX_MDW_SPW0" : l == 1 ? "DQNX_MDW_SPW1" : "DQNX_MDW_SPW2", spw), a.Bl));
         L.skip = (tuning_knob("DQNX_MDW_SKIP", 0) >> l) & 1;
         L.spw = spw;
         L.slices = (a.Bl + spw - 1) / spw;
