@@ -1815,6 +1815,9 @@ std::vector<KStep> build_learn_steps(dqnx_engine* e, int key) {
             fa.ksplit = e->f1_ksplit;
             fa.kchunk = e->f1_kchunk;
             fa.partial = at<float>(e, e->ws_fpart);
+#ifdef DQNX_STAMPS
+            fa.stamps = at<int64_t>(e, e->ws_stamps);
+#endif
             k.run = [=](hipStream_t s) { return launch_linear_fwd_split(fa, np_, act, vecb, s); };
             ks.push_back(k);
             KStep kr;

@@ -4,7 +4,12 @@
 
 namespace dqnx {
 
-enum { L_ROWS_K = 0, L_K_ROWS = 1 };
+// L_ROWS_KU / L_ROWS_K2 (L_K_ROWSU / L_K_ROWS2): the ROWS_K (K_ROWS) image loaded with
+// unconditional loads (an element outside the operand reads a valid address and is zeroed by a
+// select, so the compiler's vmcnt waits stay exact and no load sits under a branch), as float4
+// (the VEC layouts' conditions) or as float2 pairs (ld and K / the column count even: rows
+// 8-byte aligned, e.g. the HEAD net's 1358-wide dense-1 weight rows); ROWS_K*: no copy, no gather
+enum { L_ROWS_K = 0, L_K_ROWS = 1, L_ROWS_KU = 2, L_ROWS_K2 = 3, L_K_ROWSU = 4, L_K_ROWS2 = 5 };
 
 // One GEMM operand in global memory.
 //   ROWS_K: element (r, k) = base[rowidx(r)*ld + k], rowidx(r) = gather ? gather[r] : r;

@@ -123,12 +123,101 @@ struct StageKRows {
     }
 };
 
+// ROWS_K image, unconditional loads (L_ROWS_KU: float4, L_ROWS_K2: float2 pairs)
+template <int R, int KT, bool PAIR>
+struct StageRowsKU : StageRowsK<R, KT, true> {
+    using Base = StageRowsK<R, KT, true>;
+    using Base::NQ;
+    using Base::Q4;
+    __device__ __forceinline__ void load(const Operand& o, int r0, int kb) {
+        const int tid = threadIdx.x;
+#pragma unroll
+        for (int j = 0; j < NQ; j++) {
+            const int q = tid + 256 * j, qc = q < R * Q4 ? q : 0;
+            const int r = qc / Q4, k = kb + 4 * (qc - r * Q4), gr = r0 + r;
+            const int grc = min(gr, o.nrows - 1);
+            const float* row = o.base + (int64_t)grc * o.ld;
+            const bool v = q < R * Q4 && gr < o.nrows;
+            float4 x;
+            // an element outside the operand reads offset 0 of the row instead (any valid address)
+            if (PAIR) {   // pairs (k, k+1), (k+2, k+3); K even: a pair is wholly in or out
+                const bool vl = v && k < o.K, vh = v && k + 2 < o.K;
+                const float2 lo = *reinterpret_cast<const float2*>(row + (vl ? k : 0));
+                const float2 hi = *reinterpret_cast<const float2*>(row + (vh ? k + 2 : 0));
+                x = make_float4(vl ? lo.x : 0.f, vl ? lo.y : 0.f, vh ? hi.x : 0.f, vh ? hi.y : 0.f);
+            } else {
+                const bool vk = v && k < o.K;
+                const float4 y = ld4(row + (vk ? k : 0));
+                x = vk ? y : make_float4(0.f, 0.f, 0.f, 0.f);
+            }
+            this->v[j] = x;
+        }
+    }
+};
+
+// K_ROWS image, unconditional loads (L_K_ROWSU: float4 as StageKRows<VEC = true>, L_K_ROWS2:
+// float2 pairs, ld and the column count even)
+template <int C, int KT, bool PAIR>
+struct StageKRowsU : StageKRows<C, KT, true> {
+    using Base = StageKRows<C, KT, true>;
+    using Base::NQ;
+    using Base::C4;
+    __device__ __forceinline__ void load(const Operand& o, int c0, int kb) {
+        const int tid = threadIdx.x;
+#pragma unroll
+        for (int j = 0; j < NQ; j++) {
+            const int q = tid + 256 * j, qc = q < KT * C4 ? q : 0;
+            const int kr = qc / C4, c = c0 + 4 * (qc - kr * C4), k = kb + kr;
+            const bool v = q < KT * C4 && k < o.K;
+            const float* row = o.base + (int64_t)(v ? k : 0) * o.ld;
+            float4 x;
+            if (PAIR) {
+                const bool vl = v && c < o.nrows, vh = v && c + 2 < o.nrows;
+                const float2 lo = *reinterpret_cast<const float2*>(row + (vl ? c : 0));
+                const float2 hi = *reinterpret_cast<const float2*>(row + (vh ? c + 2 : 0));
+                x = make_float4(vl ? lo.x : 0.f, vl ? lo.y : 0.f, vh ? hi.x : 0.f, vh ? hi.y : 0.f);
+            } else {
+                const bool vc = v && c < o.nrows;
+                const float4 y = ld4(row + (vc ? c : 0));
+                x = vc ? y : make_float4(0.f, 0.f, 0.f, 0.f);
+            }
+            this->v[j] = x;
+        }
+    }
+};
+
 template <int LAYOUT, int R, int KT, bool VEC>
 struct Stage;
 template <int R, int KT, bool VEC>
 struct Stage<L_ROWS_K, R, KT, VEC> : StageRowsK<R, KT, VEC> {
     __device__ __forceinline__ void fragx(const float* lds, int rw, int kk, float (&f)[4], int, int) const {
         this->frag(lds, rw, kk, f);
+    }
+};
+template <int R, int KT, bool VEC>
+struct Stage<L_ROWS_KU, R, KT, VEC> : StageRowsKU<R, KT, false> {
+    __device__ __forceinline__ void fragx(const float* lds, int rw, int kk, float (&f)[4], int, int) const {
+        this->frag(lds, rw, kk, f);
+    }
+};
+template <int R, int KT, bool VEC>
+struct Stage<L_ROWS_K2, R, KT, VEC> : StageRowsKU<R, KT, true> {
+    __device__ __forceinline__ void fragx(const float* lds, int rw, int kk, float (&f)[4], int, int) const {
+        this->frag(lds, rw, kk, f);
+    }
+};
+template <int R, int KT, bool VEC>
+struct Stage<L_K_ROWSU, R, KT, VEC> : StageKRowsU<R, KT, false> {
+    __device__ __forceinline__ void fragx(const float* lds, int rw, int kk, float (&f)[4], int col_abs,
+                                          int aug) const {
+        this->frag(lds, rw, kk, f, col_abs, aug);
+    }
+};
+template <int R, int KT, bool VEC>
+struct Stage<L_K_ROWS2, R, KT, VEC> : StageKRowsU<R, KT, true> {
+    __device__ __forceinline__ void fragx(const float* lds, int rw, int kk, float (&f)[4], int col_abs,
+                                          int aug) const {
+        this->frag(lds, rw, kk, f, col_abs, aug);
     }
 };
 template <int R, int KT, bool VEC>
@@ -202,6 +291,79 @@ struct TileGemm {
             sb.store(lb, B, n0, kn);
             __syncthreads();
             kb = kn;
+        }
+    }
+
+    // run() with two passes in flight: pass k+2's loads are issued before pass k is multiplied and
+    // stored to LDS only after pass k+1 (two register sets under fixed names, the loop unrolled by
+    // two).  Same LDS image per pass and same MFMA order: bit-identical to run().
+    __device__ __forceinline__ static void mma_pass(const float* la, const float* lb, const SA& sa, const SB& sb,
+                                                    const Operand& B, int n0, int klen, floatx4 (&acc)[TM][TN]) {
+        const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+        const int wm = wid / WN, wn = wid % WN;
+        for (int kk = 0; kk < klen; kk += 16) {
+            float a[TM][4], b[TN][4];
+#pragma unroll
+            for (int tm = 0; tm < TM; tm++) sa.fragx(la, (wm * TM + tm) * 16, kk, a[tm], -1, -2);
+#pragma unroll
+            for (int tn = 0; tn < TN; tn++) {
+                const int cw = (wn * TN + tn) * 16;
+                sb.fragx(lb, cw, kk, b[tn], n0 + cw + (lane & 15), B.aug);
+            }
+#pragma unroll
+            for (int jj = 0; jj < 4; jj++)
+#pragma unroll
+                for (int tm = 0; tm < TM; tm++)
+#pragma unroll
+                    for (int tn = 0; tn < TN; tn++) acc[tm][tn] = mfma16x16x4(a[tm][jj], b[tn][jj], acc[tm][tn]);
+        }
+    }
+    __device__ __forceinline__ static void run2(float* lds, const Operand& A, const Operand& B, int m0, int n0,
+                                                int kbeg, int kend, floatx4 (&acc)[TM][TN]) {
+        float* la = lds;
+        float* lb = lds + SA::LDS_FLOATS;
+#pragma unroll
+        for (int tm = 0; tm < TM; tm++)
+#pragma unroll
+            for (int tn = 0; tn < TN; tn++) acc[tm][tn] = floatx4{0.f, 0.f, 0.f, 0.f};
+        SA a0, a1;
+        SB b0, b1;
+        int kb = kbeg;
+        if (kb >= kend) return;
+        a0.load(A, m0, kb);
+        b0.load(B, n0, kb);
+        if (kb + KT < kend) {
+            a1.load(A, m0, kb + KT);
+            b1.load(B, n0, kb + KT);
+        }
+        a0.store(la, A, m0, kb);
+        b0.store(lb, B, n0, kb);
+        __syncthreads();
+        while (true) {
+            // LDS: pass kb; set 1: pass kb + KT (if any); set 0 <- pass kb + 2 KT
+            if (kb + 2 * KT < kend) {
+                a0.load(A, m0, kb + 2 * KT);
+                b0.load(B, n0, kb + 2 * KT);
+            }
+            mma_pass(la, lb, a1, b1, B, n0, min(KT, kend - kb), acc);
+            if (kb + KT >= kend) break;
+            __syncthreads();
+            a1.store(la, A, m0, kb + KT);
+            b1.store(lb, B, n0, kb + KT);
+            __syncthreads();
+            kb += KT;
+            // LDS: pass kb; set 0: pass kb + KT (if any); set 1 <- pass kb + 2 KT
+            if (kb + 2 * KT < kend) {
+                a1.load(A, m0, kb + 2 * KT);
+                b1.load(B, n0, kb + 2 * KT);
+            }
+            mma_pass(la, lb, a0, b0, B, n0, min(KT, kend - kb), acc);
+            if (kb + KT >= kend) break;
+            __syncthreads();
+            a0.store(la, A, m0, kb + KT);
+            b0.store(lb, B, n0, kb + KT);
+            __syncthreads();
+            kb += KT;
         }
     }
 };

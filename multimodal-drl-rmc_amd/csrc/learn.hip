@@ -84,9 +84,11 @@ struct Engine {
 // =====================================================================================
 // GATHER: first layer (operand rows gathered from the replay ring through the sampled
 // physical rows); hidden layers read the previous activation rows in order.
-template <int ACT, bool VECB, bool GATHER>
+// ULOAD (dense rows, no gather, K % 4 == 0): unconditional operand loads (gemm_common.hpp)
+template <int ACT, bool VECB, bool GATHER, bool ULOAD = false>
 __global__ __launch_bounds__(256) void k_linear_fwd(FwdArgs args) {
-    using E = Engine<FWD_BM, FWD_BN, DQNX_FWD_KT, DQNX_FWD_WM, L_ROWS_K, L_ROWS_K, true, VECB>;
+    constexpr int LAY = ULOAD ? L_ROWS_KU : L_ROWS_K;
+    using E = Engine<FWD_BM, FWD_BN, DQNX_FWD_KT, DQNX_FWD_WM, LAY, LAY, true, VECB>;
     constexpr int TM = E::TM, TN = E::TN;
     __shared__ __attribute__((aligned(16))) float lds[E::LDS_FLOATS];
     // tiles ordered (stream, m-tile, n-tile) with n fastest; each XCD gets a contiguous
@@ -132,10 +134,11 @@ __global__ __launch_bounds__(256) void k_linear_fwd(FwdArgs args) {
 // into C.  A 128-row tile loads each weight K-slab once per 128 rows instead of once per 16.
 // The per-element accumulation order (K ascending, 16-deep MFMA chunks) is the one of the
 // 16x64 kernel, so both give bit-identical outputs.
-template <int ACT, bool VECB, int BM, int BN, int WM, int KT = FWD_BIG_KT>
+template <int ACT, bool VECB, int BM, int BN, int WM, int KT = FWD_BIG_KT, int LAYA = L_ROWS_K, int LAYB = L_ROWS_K,
+          int PF = 1>
 __global__ __launch_bounds__(256) void k_linear_fwd_big(FwdArgs args) {
     constexpr int WN = 4 / WM;
-    using G = TileGemm<BM, BN, KT, WM, WN, L_ROWS_K, L_ROWS_K, true, VECB>;
+    using G = TileGemm<BM, BN, KT, WM, WN, LAYA, LAYB, true, VECB>;
     constexpr int TM = G::TM, TN = G::TN;
     __shared__ __attribute__((aligned(16))) float lds[G::LDS_FLOATS];
     const int M = args.M, N = args.N, K = args.K;
@@ -155,7 +158,10 @@ __global__ __launch_bounds__(256) void k_linear_fwd_big(FwdArgs args) {
     Operand A{P.A, P.lda, nullptr, M, Kpad, -1, nullptr, P.lda};
     Operand B{P.W, K, nullptr, N, K, -1, nullptr, 0};
     floatx4 acc[TM][TN];
-    G::run(lds, A, B, m0, n0, kb, ke, acc);
+    DQNX_STAMP(args.stamps, 53);
+    if constexpr (PF == 2) G::run2(lds, A, B, m0, n0, kb, ke, acc);
+    else G::run(lds, A, B, m0, n0, kb, ke, acc);
+    DQNX_STAMP(args.stamps, 54);
     const int ro = (wid / WN) * TM * 16, co = (wid % WN) * TN * 16;
     if (args.ksplit == 1) {
 #pragma unroll
@@ -186,6 +192,7 @@ __global__ __launch_bounds__(256) void k_linear_fwd_big(FwdArgs args) {
                 if (row < M) part[(int64_t)row * N + col] = acc[tm][tn][r];
             }
     }
+    DQNX_STAMP(args.stamps, 55);
 }
 
 template <int ACT>
@@ -300,10 +307,13 @@ int launch_conv_dx_big(const BwdArgs& a, hipStream_t s) {
 // =====================================================================================
 // VECW: the dx role's weight rows (length `in`) allow float4 loads (in % 4 == 0).
 // Hprev == null: no activation mask (conv dX columns before col2im).
-template <int ACT, bool VECW>
+// U: unconditional operand loads (gemm_common.hpp); the dx role's weight rows as float4 (VECW) or
+// float2 pairs
+template <int ACT, bool VECW, bool U = false>
 __global__ __launch_bounds__(256) void k_bwd_level(BwdArgs a) {
-    using EX = Engine<BWD_BM, BWD_BN, DQNX_BWD_KT, DQNX_BWD_WM, L_ROWS_K, L_K_ROWS, true, VECW>;
-    using EW = Engine<BWD_BM, BWD_BN, DQNX_BWD_KT, DQNX_BWD_WM, L_K_ROWS, L_K_ROWS, true, true>;
+    using EX = Engine<BWD_BM, BWD_BN, DQNX_BWD_KT, DQNX_BWD_WM, U ? L_ROWS_KU : L_ROWS_K,
+                      U ? (VECW ? L_K_ROWSU : L_K_ROWS2) : L_K_ROWS, true, VECW>;
+    using EW = Engine<BWD_BM, BWD_BN, DQNX_BWD_KT, DQNX_BWD_WM, U ? L_K_ROWSU : L_K_ROWS, U ? L_K_ROWSU : L_K_ROWS, true, true>;
     constexpr int TM = EX::TM, TN = EX::TN;
     constexpr int LF = EX::LDS_FLOATS > EW::LDS_FLOATS ? EX::LDS_FLOATS : EW::LDS_FLOATS;
     __shared__ __attribute__((aligned(16))) float lds[LF];
@@ -1340,9 +1350,15 @@ __global__ void k_replay_push(PushArgs a) {
 // =====================================================================================
 // host-side launchers
 // =====================================================================================
+// DQNX_FWD_ULOAD=1: the unconditional loader for dense rows (bit-identical; measured no faster on
+// the HEAD net's dense 2 in round 5: opt-in)
 template <int ACT, bool VECB>
 static void launch_fwd_gather(const FwdArgs& a, dim3 grid, hipStream_t s) {
+    bool u = VECB && !a.p[0].phys && a.K % 4 == 0 && route_knob("DQNX_FWD_ULOAD", 0) != 0;
+    for (int z = 0; z < a.nprob; z++)
+        u = u && a.p[z].lda % 4 == 0 && ((uintptr_t)a.p[z].A & 15) == 0 && ((uintptr_t)a.p[z].W & 15) == 0;
     if (a.p[0].phys) hipLaunchKernelGGL((k_linear_fwd<ACT, VECB, true>), grid, dim3(256), 0, s, a);
+    else if (u) hipLaunchKernelGGL((k_linear_fwd<ACT, true, false, true>), grid, dim3(256), 0, s, a);
     else hipLaunchKernelGGL((k_linear_fwd<ACT, VECB, false>), grid, dim3(256), 0, s, a);
 }
 
@@ -1412,19 +1428,34 @@ int fwd_split_ksplit(int M, int N, int K, int nprob, int n_cu, int* kchunk) {
     return S;
 }
 
+template <int ACT>
+static void launch_fwd_split_t(const FwdArgs& a2, bool vecb, dim3 grid, hipStream_t s) {
+    constexpr int T = FWD_SPLIT_T, KT = FWD_SPLIT_KT;
+    // unconditional operand loads (exact vmcnt waits): A = the dense input rows (float4), B = the
+    // weight rows as float4, or as float2 pairs where the rows are only 8-byte aligned (the HEAD
+    // net's K = 1358); odd strides keep the scalar loader
+    bool a4 = route_knob("DQNX_F1_ULOAD", 1) != 0, b2 = a4 && !vecb && a2.K % 2 == 0;
+    for (int z = 0; z < a2.nprob; z++) {
+        a4 = a4 && a2.p[z].lda % 4 == 0 && ((uintptr_t)a2.p[z].A & 15) == 0;
+        b2 = b2 && ((uintptr_t)a2.p[z].W & 7) == 0;
+    }
+    // ... optionally with two passes in flight (DQNX_F1_PF=2)
+    const bool pf2 = route_knob("DQNX_F1_PF", 1) == 2;   // (measured 1 us slower at the HEAD net: opt-in)
+    if (a4 && vecb && pf2) hipLaunchKernelGGL((k_linear_fwd_big<ACT, true, T, T, 2, KT, L_ROWS_KU, L_ROWS_KU, 2>), grid, dim3(256), 0, s, a2);
+    else if (a4 && b2 && pf2) hipLaunchKernelGGL((k_linear_fwd_big<ACT, false, T, T, 2, KT, L_ROWS_KU, L_ROWS_K2, 2>), grid, dim3(256), 0, s, a2);
+    else if (a4 && vecb) hipLaunchKernelGGL((k_linear_fwd_big<ACT, true, T, T, 2, KT, L_ROWS_KU, L_ROWS_KU>), grid, dim3(256), 0, s, a2);
+    else if (a4 && b2) hipLaunchKernelGGL((k_linear_fwd_big<ACT, false, T, T, 2, KT, L_ROWS_KU, L_ROWS_K2>), grid, dim3(256), 0, s, a2);
+    else if (vecb) hipLaunchKernelGGL((k_linear_fwd_big<ACT, true, T, T, 2, KT>), grid, dim3(256), 0, s, a2);
+    else hipLaunchKernelGGL((k_linear_fwd_big<ACT, false, T, T, 2, KT>), grid, dim3(256), 0, s, a2);
+}
 int launch_linear_fwd_split(const FwdArgs& args, int nprob, int act, bool vecb, hipStream_t s) {
     FwdArgs a2 = args;
     a2.nprob = nprob;
-    constexpr int T = FWD_SPLIT_T, KT = FWD_SPLIT_KT;
+    constexpr int T = FWD_SPLIT_T;
     const int tiles = ((a2.N + T - 1) / T) * ((a2.M + T - 1) / T) * nprob;
     const dim3 grid(tiles * a2.ksplit);
-    if (act == DQNX_ACT_RELU) {
-        if (vecb) hipLaunchKernelGGL((k_linear_fwd_big<DQNX_ACT_RELU, true, T, T, 2, KT>), grid, dim3(256), 0, s, a2);
-        else hipLaunchKernelGGL((k_linear_fwd_big<DQNX_ACT_RELU, false, T, T, 2, KT>), grid, dim3(256), 0, s, a2);
-    } else {
-        if (vecb) hipLaunchKernelGGL((k_linear_fwd_big<DQNX_ACT_ELU, true, T, T, 2, KT>), grid, dim3(256), 0, s, a2);
-        else hipLaunchKernelGGL((k_linear_fwd_big<DQNX_ACT_ELU, false, T, T, 2, KT>), grid, dim3(256), 0, s, a2);
-    }
+    if (act == DQNX_ACT_RELU) launch_fwd_split_t<DQNX_ACT_RELU>(a2, vecb, grid, s);
+    else launch_fwd_split_t<DQNX_ACT_ELU>(a2, vecb, grid, s);
     DQNX_HIP_CHECK(hipGetLastError());
     return DQNX_OK;
 }
@@ -1457,17 +1488,26 @@ void bwd_level_grid(BwdArgs& a) {
     }
 }
 
+template <int ACT>
+static void launch_bwd_level_t(const BwdArgs& a, int blocks, hipStream_t s) {
+    const bool vw = (a.in % 4) == 0;
+    // unconditional loads where every operand meets its loader's alignment: dZ / X rows as float4
+    // (row strides multiples of 4, 16-byte bases), the dx role's weight rows as float4 or pairs
+    bool u = route_knob("DQNX_BWD_ULOAD", 1) != 0 && (vw || (a.in % 2 == 0 && ((uintptr_t)a.W & 7) == 0));
+    if (a.dx_blocks) u = u && a.out % 4 == 0 && ((uintptr_t)a.dZ & 15) == 0 && (!vw || ((uintptr_t)a.W & 15) == 0);
+    for (int p = 0; p < a.ndw; p++)
+        u = u && a.dw[p].ldz % 4 == 0 && a.dw[p].ldx % 4 == 0 && ((uintptr_t)a.dw[p].dZ & 15) == 0 &&
+            ((uintptr_t)a.dw[p].X & 15) == 0;
+    if (u && vw) hipLaunchKernelGGL((k_bwd_level<ACT, true, true>), dim3(blocks), dim3(256), 0, s, a);
+    else if (u) hipLaunchKernelGGL((k_bwd_level<ACT, false, true>), dim3(blocks), dim3(256), 0, s, a);
+    else if (vw) hipLaunchKernelGGL((k_bwd_level<ACT, true>), dim3(blocks), dim3(256), 0, s, a);
+    else hipLaunchKernelGGL((k_bwd_level<ACT, false>), dim3(blocks), dim3(256), 0, s, a);
+}
 int launch_bwd_level(const BwdArgs& a, int act, hipStream_t s) {
     int blocks = a.dx_blocks;
     for (int p = 0; p < a.ndw; p++) blocks += a.dw[p].blocks;
-    const bool vw = (a.in % 4) == 0;
-    if (act == DQNX_ACT_RELU) {
-        if (vw) hipLaunchKernelGGL((k_bwd_level<DQNX_ACT_RELU, true>), dim3(blocks), dim3(256), 0, s, a);
-        else hipLaunchKernelGGL((k_bwd_level<DQNX_ACT_RELU, false>), dim3(blocks), dim3(256), 0, s, a);
-    } else {
-        if (vw) hipLaunchKernelGGL((k_bwd_level<DQNX_ACT_ELU, true>), dim3(blocks), dim3(256), 0, s, a);
-        else hipLaunchKernelGGL((k_bwd_level<DQNX_ACT_ELU, false>), dim3(blocks), dim3(256), 0, s, a);
-    }
+    if (act == DQNX_ACT_RELU) launch_bwd_level_t<DQNX_ACT_RELU>(a, blocks, s);
+    else launch_bwd_level_t<DQNX_ACT_ELU>(a, blocks, s);
     DQNX_HIP_CHECK(hipGetLastError());
     return DQNX_OK;
 }

@@ -94,6 +94,7 @@ struct FwdArgs {
     // them in chunk order (deterministic), then bias and activation
     int ksplit, kchunk;
     float* partial;
+    int64_t* stamps;           // diagnostic builds: launch_linear_fwd_split's workgroup 0 (slots 53..55)
 };
 
 // One split-K weight-gradient GEMM: partial[s] = dZ^T [X | 1] over the samples of slice s.

@@ -687,14 +687,11 @@ __global__ __launch_bounds__(MTH, 3) void k_micro_fwd(MicroFwdArgs a) {   // 3 w
             }
         };
         float v[GE];
-        DQNX_STAMP_BLK_W(a.stamps, 53, sblk);
         gload(0, v);
         const float tv = tload(tid);
         conv1_weights(C0, P, c1_mt, c1w, c1b);
-        DQNX_STAMP_BLK_W(a.stamps, 54, sblk);
         gstore(0, v);
         tstore(tid, tv);
-        DQNX_STAMP_BLK_W(a.stamps, 55, sblk);
         for (int base = GE * MTH; base < tot; base += GE * MTH) {   // grids past one batch (larger S)
             gload(base, v);
             gstore(base, v);

@@ -263,6 +263,10 @@ def _run_hybrid_steps(algo, batch, steps, seed):
 
 @pytest.mark.parametrize("knob,a,b", [
     ("DQNX_MDX_WAVES", "8", "4"),    # micro data gradients: 8 vs 4 waves per workgroup
+    ("DQNX_F1_ULOAD", "1", "0"),     # dense 1: unconditional float4 / float2-pair loads vs the guarded loader
+    ("DQNX_F1_PF", "2", "1"),        # dense 1: two K passes in flight vs one
+    ("DQNX_FWD_ULOAD", "1", "0"),    # dense 2: unconditional float4 loads vs the guarded loader
+    ("DQNX_BWD_ULOAD", "1", "0"),    # dense backward: unconditional float4 / pair loads vs the guarded loader
 ])
 @pytest.mark.parametrize("algo,batch", [("DuelingDoubleDQNAgent", 256), ("PerDuelingDoubleDQNAgent", 100)])
 def test_gpu_hybrid_head_variants_bit_identical(monkeypatch, knob, a, b, algo, batch):

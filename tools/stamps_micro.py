@@ -39,7 +39,7 @@ for step in range(6):
     print(f"step {step}: fwd wg: staged {s[41] - f0} conv1 {s[42] - s[41]} conv2 {s[43] - s[42]} conv3 {s[44] - s[43]} "
           f"(total {s[44] - f0})", flush=True)
 
-    print(f"        fwd staging: rows {s[53] - f0} loads {s[54] - s[53]} stores {s[55] - s[54]} barrier {s[41] - s[55]}; "
-          f"wave starts {[s[56 + w] - f0 for w in range(4)]}", flush=True)
+    print(f"        fwd wave starts {[s[56 + w] - f0 for w in range(4)]}", flush=True)
+    print(f"        dense-1 split wg0: GEMM {s[54] - s[53]} slab store {s[55] - s[54]}", flush=True)
     d0 = s[47]
     print(f"        dx wg0: staged {s[48] - d0} level2 {s[49] - s[48]} level1 {s[50] - s[49]} (total {s[50] - d0})", flush=True)
