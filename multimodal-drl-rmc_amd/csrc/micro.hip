@@ -334,6 +334,7 @@ int micro_dw_plan(MicroDwArgs& a, int n_cu) {
         wg += L.slices * wg_per_slice(l);
         L.pstride = (int64_t)L.Co * L.Ci * 9 + L.Co;
         lf = std::max(lf, dw_lds_floats(L, first, first ? L.spw : L.G));
+        if (!first) lf = std::max(lf, MW * 16 * 144);   // the slab store's transpose rows
     }
     a.wgs = wg;
     a.lds_floats = lf;
@@ -942,6 +943,9 @@ __device__ __forceinline__ void micro_dw_body_ci(const MicroDwArgs& a, const Mic
     const int dsz = G * dper;
     const int bufsz = (dsz + G * xper + 3) & ~3, zero = 2 * bufsz;
     const int ks = (Pq + 3) >> 2;
+    const int sblk = L.wg0;   // diagnostic stamps: this conv's first workgroup (conv 2: slots 53..58, conv 3: 0..5)
+    const int sb_ = &L == &a.L[1] ? 53 : 0;
+    DQNX_STAMP_BLK(a.stamps, sb_, sblk);
     for (int bb = 0; bb < 2; bb++)   // zero borders of both buffers
         for (int e = tid; e < G * xper; e += MTH) lds[bb * bufsz + dsz + e] = 0.f;
     if (tid < MICRO_ZERO) lds[zero + tid] = 0.f;
@@ -989,10 +993,12 @@ __device__ __forceinline__ void micro_dw_body_ci(const MicroDwArgs& a, const Mic
 #pragma unroll
     for (int t = 0; t < NT; t++) acc[t] = floatx4{0.f, 0.f, 0.f, 0.f};
     float dbias = 0.f;
+    DQNX_STAMP_BLK(a.stamps, sb_ + 1, sblk);
     gload(s0);
     micro_barrier();   // borders / zeros before the first store
     sstore(0);
     micro_barrier();
+    DQNX_STAMP_BLK(a.stamps, sb_ + 2, sblk);
     int cur = 0;
     for (int sb0 = s0; sb0 < s1; sb0 += G) {
         const int cb = cur * bufsz, nG = min(G, s1 - sb0), T = nG * ks;
@@ -1033,19 +1039,32 @@ __device__ __forceinline__ void micro_dw_body_ci(const MicroDwArgs& a, const Mic
                     for (int q = g; q < Pq; q += 4) dbias += lds[cb + gg * dper + q * csD + mt * 16 + i16];
         }
         micro_barrier();   // every read of the other buffer's previous stage is done
+        if (sb0 == s0) DQNX_STAMP_BLK(a.stamps, sb_ + 3, sblk);
         if (sb0 + G < s1) {
             sstore(cur ^ 1);
             micro_barrier();
         }
         cur ^= 1;
     }
+    DQNX_STAMP_BLK(a.stamps, sb_ + 4, sblk);
     if (!active) return;
     float* part = L.partial + (int64_t)slice * L.pstride;
-    const int co = mt * 16 + 4 * g, ci = ct * 16 + i16;
+    // the wave's 16 co x (16 ci x 9 taps) outputs are 16 runs of 144 contiguous floats of the slab
+    // ([co][ci][i][j]): transposed through the wave's own LDS rows (the stages' buffers are free
+    // after the loop's last barrier), then written as whole float4s
+    {
+        float* w = lds + wid * 16 * 144;
 #pragma unroll
-    for (int t = 0; t < NT; t++)
+        for (int t = 0; t < NT; t++)
 #pragma unroll
-        for (int r = 0; r < 4; r++) part[((int64_t)(co + r) * L.Ci + ci) * 9 + t] = acc[t][r];
+            for (int r = 0; r < 4; r++) w[(4 * g + r) * 144 + i16 * 9 + t] = acc[t][r];
+        float* dst = part + ((int64_t)(mt * 16) * L.Ci + ct * 16) * 9;
+#pragma unroll
+        for (int j = 0; j < 9; j++) {   // 16 rows x 36 float4 = 576 = 9 per lane
+            const int q = lane + 64 * j, row = q / 36, c4 = q - row * 36;
+            *reinterpret_cast<float4*>(dst + (int64_t)row * L.Ci * 9 + 4 * c4) = *reinterpret_cast<const float4*>(w + row * 144 + 4 * c4);
+        }
+    }
     if (ct == 0) {   // the 4 lane groups' partial column sums, in group order
         float sb = __shfl(dbias, i16, 64);
         sb += __shfl(dbias, 16 + i16, 64);
@@ -1053,6 +1072,7 @@ __device__ __forceinline__ void micro_dw_body_ci(const MicroDwArgs& a, const Mic
         sb += __shfl(dbias, 48 + i16, 64);
         if (g == 0) part[(int64_t)L.Co * L.Ci * 9 + mt * 16 + i16] = sb;
     }
+    DQNX_STAMP_BLK(a.stamps, sb_ + 5, sblk);
 }
 
 // conv 1: workgroup = (group of up to MW (co tile, im2col column tile) pairs, slice of samples);

@@ -41,5 +41,8 @@ for step in range(6):
 
     print(f"        fwd wave starts {[s[56 + w] - f0 for w in range(4)]}", flush=True)
     print(f"        dense-1 split wg0: GEMM {s[54] - s[53]} slab store {s[55] - s[54]}", flush=True)
+    for nm, b in (("conv2", 53), ("conv3", 0)):
+        print(f"        dw {nm} wg: maps {s[b + 1] - s[b]} first stage {s[b + 2] - s[b + 1]} stage 0 {s[b + 3] - s[b + 2]} "
+              f"rest {s[b + 4] - s[b + 3]} store {s[b + 5] - s[b + 4]} (total {s[b + 5] - s[b]})", flush=True)
     d0 = s[47]
     print(f"        dx wg0: staged {s[48] - d0} level2 {s[49] - s[48]} level1 {s[50] - s[49]} (total {s[50] - d0})", flush=True)
