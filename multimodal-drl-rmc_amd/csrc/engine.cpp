@@ -1948,6 +1948,12 @@ std::vector<KStep> build_learn_steps(dqnx_engine* e, int key) {
         double flops = 2.0 * Bl * lp.out * (lp.in + 1.0) + (dx ? 2.0 * Bl * lp.out * lp.in : 0.0);
         double bytes = 4.0 * (Bl * lp.out + Bl * lp.in + ba.dw_slices * (lp.out * (lp.in + 1.0))
                               + (dx ? lp.out * (double)lp.in + 2.0 * Bl * lp.in : 0.0));
+        // very large levels (the (4,84,84) variant's 56,462 -> 512 dense 1): 64 x 64 tiles, a quarter of
+        // the 32 x 32 workgroups with four times the MFMAs per operand pass: its backward level 434 ->
+        // 351 us; the HEAD net's 1358 -> 512 keeps 32 x 32 (16.1 us; 25.9 with 64 x 64: ~1 workgroup per
+        // CU, latency-bound).  DQNX_BWD_TS=32 / 64 forces the edge
+        const int bts = route_knob("DQNX_BWD_TS", 0);
+        if (bts == 64 || (bts == 0 && (int64_t)(lp.in + 1) * lp.out >= ((int64_t)4 << 20) && e->Bl >= 64)) ba.ts = 64;
         if (l == L - 1) {   // head weight gradient: dHead^T [H_L | 1]
             DwProblem& h = ba.dw[ba.ndw++];
             h.dZ = at<float>(e, e->ws_dhead);

@@ -309,11 +309,13 @@ int launch_conv_dx_big(const BwdArgs& a, hipStream_t s) {
 // Hprev == null: no activation mask (conv dX columns before col2im).
 // U: unconditional operand loads (gemm_common.hpp); the dx role's weight rows as float4 (VECW) or
 // float2 pairs
-template <int ACT, bool VECW, bool U = false>
+template <int ACT, bool VECW, bool U = false, int TS = BWD_BM>
 __global__ __launch_bounds__(256) void k_bwd_level(BwdArgs a) {
-    using EX = Engine<BWD_BM, BWD_BN, DQNX_BWD_KT, DQNX_BWD_WM, U ? L_ROWS_KU : L_ROWS_K,
+    constexpr int BWD_BM = TS, BWD_BN = TS;   // (shadows the default tile edge)
+    constexpr int KT = TS == 64 ? 64 : DQNX_BWD_KT;   // 64 x 64 tiles: 64-deep passes (36 KB of LDS)
+    using EX = Engine<BWD_BM, BWD_BN, KT, DQNX_BWD_WM, U ? L_ROWS_KU : L_ROWS_K,
                       U ? (VECW ? L_K_ROWSU : L_K_ROWS2) : L_K_ROWS, true, VECW>;
-    using EW = Engine<BWD_BM, BWD_BN, DQNX_BWD_KT, DQNX_BWD_WM, U ? L_K_ROWSU : L_K_ROWS, U ? L_K_ROWSU : L_K_ROWS, true, true>;
+    using EW = Engine<BWD_BM, BWD_BN, KT, DQNX_BWD_WM, U ? L_K_ROWSU : L_K_ROWS, U ? L_K_ROWSU : L_K_ROWS, true, true>;
     constexpr int TM = EX::TM, TN = EX::TN;
     constexpr int LF = EX::LDS_FLOATS > EW::LDS_FLOATS ? EX::LDS_FLOATS : EW::LDS_FLOATS;
     __shared__ __attribute__((aligned(16))) float lds[LF];
@@ -1472,7 +1474,7 @@ int launch_linear_fwd_reduce(const FwdArgs& args, int nprob, int act, hipStream_
 }
 
 void bwd_level_grid(BwdArgs& a) {
-    constexpr int BM = BWD_BM, BN = BWD_BN;
+    const int BM = a.ts ? a.ts : BWD_BM, BN = a.ts ? a.ts : BWD_BN;
     if (a.dZprev) {
         a.dx_grid_x = (a.in + BN - 1) / BN;
         a.dx_blocks = a.dx_grid_x * ((a.Bl + BM - 1) / BM);
@@ -1498,7 +1500,11 @@ static void launch_bwd_level_t(const BwdArgs& a, int blocks, hipStream_t s) {
     for (int p = 0; p < a.ndw; p++)
         u = u && a.dw[p].ldz % 4 == 0 && a.dw[p].ldx % 4 == 0 && ((uintptr_t)a.dw[p].dZ & 15) == 0 &&
             ((uintptr_t)a.dw[p].X & 15) == 0;
-    if (u && vw) hipLaunchKernelGGL((k_bwd_level<ACT, true, true>), dim3(blocks), dim3(256), 0, s, a);
+    if (a.ts == 64 && u && vw) hipLaunchKernelGGL((k_bwd_level<ACT, true, true, 64>), dim3(blocks), dim3(256), 0, s, a);
+    else if (a.ts == 64 && u) hipLaunchKernelGGL((k_bwd_level<ACT, false, true, 64>), dim3(blocks), dim3(256), 0, s, a);
+    else if (a.ts == 64 && vw) hipLaunchKernelGGL((k_bwd_level<ACT, true, false, 64>), dim3(blocks), dim3(256), 0, s, a);
+    else if (a.ts == 64) hipLaunchKernelGGL((k_bwd_level<ACT, false, false, 64>), dim3(blocks), dim3(256), 0, s, a);
+    else if (u && vw) hipLaunchKernelGGL((k_bwd_level<ACT, true, true>), dim3(blocks), dim3(256), 0, s, a);
     else if (u) hipLaunchKernelGGL((k_bwd_level<ACT, false, true>), dim3(blocks), dim3(256), 0, s, a);
     else if (vw) hipLaunchKernelGGL((k_bwd_level<ACT, true>), dim3(blocks), dim3(256), 0, s, a);
     else hipLaunchKernelGGL((k_bwd_level<ACT, false>), dim3(blocks), dim3(256), 0, s, a);

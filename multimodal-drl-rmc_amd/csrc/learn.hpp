@@ -138,6 +138,8 @@ struct BwdArgs {
     int ndw;
     int Bl, kslice, dw_slices;
     int dx_blocks, dx_grid_x;
+    int ts;                // k_bwd_level tile edge: 0 = DQNX_BWD_BM (32), or 64 (large layers: a quarter of the
+                           // workgroups, four times the MFMAs per operand pass; set before bwd_level_grid)
     int t16;               // bf16 weight gradients from the slab-transposed copies (k_dw_bf16d) instead of fp32 rows
     int64_t* stamps;       // diagnostic builds (-DDQNX_STAMPS): k_dw_bf16d's slots 57..62
     int pprop_wgs;         // k_dw_bf16: + workgroups running k_per_prop's body (single-GPU PER step)
