@@ -467,21 +467,92 @@ def kernel_times(eng, flags, count=50, reps=5, only=None):
     return out
 
 
-def roofline_of(args, kern, batch_tag):
-    """roofline object for the dominant kernel: achieved algorithmic FLOP/s (or B/s) against the
-    MI355X peak of the compute dtype, plus both fractions; `traffic` = HBM bytes per launch
-    from the committed rocprofv3 PMC passes of the same workload (profiles/pmc_traffic_*.json)."""
-    nm, us, fl, by = kern
-    peak_mfma = PEAK_BF16_MFMA_TFLOPS if args.compute == "bf16" else PEAK_FP32_MFMA_TFLOPS
-    traffic = None
+def kernel_event_us(eng, flags, name, count=100):
+    """Average launch duration of kernel `name` of the learn step, measured live with a HIP event pair
+    recorded on the engine's stream immediately before and after that one launch (dqnx_learn_step_timed:
+    every other kernel of the step is enqueued eagerly around it, so the pair brackets the kernel alone),
+    over `count` steps; the host enqueues all of them before reading the events.  This is the quantity
+    rocprofv3's kernel trace reports (dispatch begin to end), unlike kernel_times' with / without
+    difference.  Returns (mean_us, median_us)."""
+    L = C.lib()
+    infos = kernel_infos(eng, flags)
+    idx = next(i for i, k in enumerate(infos) if k[0] == name)
+    stream = eng.stream()
+    ev = (ctypes.c_void_p * (2 * count))()
+    C.check(L.dqnx_events_create(2 * count, ev), "events_create")
+    try:
+        for _ in range(5):   # warm: the same launches as the timed ones
+            C.check(L.dqnx_learn_step_timed(eng.h, flags, idx, ev[0], ev[1], stream), "timed step")
+        torch.cuda.synchronize()
+        for j in range(count):
+            C.check(L.dqnx_learn_step_timed(eng.h, flags, idx, ev[2 * j], ev[2 * j + 1], stream), "timed step")
+        us = []
+        for j in range(count):
+            ms = ctypes.c_float()
+            C.check(L.dqnx_event_elapsed(ev[2 * j], ev[2 * j + 1], ctypes.byref(ms)), "event_elapsed")
+            us.append(ms.value * 1e3)
+    finally:
+        torch.cuda.synchronize()
+        L.dqnx_events_destroy(2 * count, ev)
+    us.sort()
+    return sum(us) / len(us), us[len(us) // 2]
+
+
+ROCPROF_ROUND = "r06"
+
+
+def rocprof_avg_us(stats_name, kernel):
+    """The committed rocprofv3 --kernel-trace --stats summary of this same bench command
+    (profiles/<round>/kernel_stats_<workload>.csv): average duration (us) of the kernel whose name
+    contains k_<kernel> (the engine's kernel names are k_<timing name>), or None."""
+    path = os.path.join(REPO, "profiles", ROCPROF_ROUND, f"kernel_stats_{stats_name}.csv")
+    if not os.path.exists(path):
+        return None, None
+    import csv
+    base = "k_" + kernel.split("+")[0]
+    # the implicit-GEMM convs (configs[2]) share one kernel template, one instantiation per conv: the
+    # dominant conv_fwd_c2 is the k_conv_ig instantiation with the largest total time
+    key = "TotalDurationNs" if kernel.startswith("conv_fwd_c") else "Calls"
+    if kernel.startswith("conv_fwd_c"):
+        base = "k_conv_ig"
+    best = None
+    with open(path) as f:
+        for row in csv.DictReader(f):
+            nm = row.get("Name", "")
+            short = nm.split("(")[0].split("<")[0].split("::")[-1].strip()
+            if short == base and (best is None or float(row[key]) > float(best[key])):
+                best = row
+    if best is None:
+        return None, path
+    return float(best["AverageNs"]) / 1e3, os.path.relpath(path, REPO)
+
+
+def pmc_traffic(args, batch_tag):
+    """The committed rocprofv3 PMC traffic passes of this workload (profiles/pmc_traffic_*.json):
+    {kernel: hbm bytes per launch} (2 x FETCH_SIZE + WRITE_SIZE, the gfx950 correction), or {}."""
     tag = "" if args.compute == "fp32" else f"_{args.compute}"
     pmc_path = os.path.join(REPO, "profiles", f"pmc_traffic_{args.net}_b{batch_tag}{tag}.json")
-    if os.path.exists(pmc_path):
-        try:
-            pmc = json.load(open(pmc_path))   # keyed by kernel ("mlp_fwd+sample" is the k_mlp_fwd launch)
-            traffic = pmc.get(nm, pmc.get(nm.split("+")[0], {})).get("hbm_bytes_per_launch")
-        except Exception:
-            traffic = None
+    if not os.path.exists(pmc_path):
+        return {}
+    try:
+        pmc = json.load(open(pmc_path))
+        return {k: v["hbm_bytes_per_launch"] for k, v in pmc.items() if isinstance(v, dict) and "hbm_bytes_per_launch" in v}
+    except Exception:
+        return {}
+
+
+def roofline_of(args, kern, batch_tag, incontext_us=None, stats_name=None, step_kernels=None):
+    """roofline object for the dominant kernel: achieved algorithmic FLOP/s (or B/s) against the
+    MI355X peak of the compute dtype, plus both fractions.  kern = (name, avg_us, flops, bytes) with
+    avg_us the kernel's average launch duration measured live by HIP events around the launch
+    (kernel_event_us).  `traffic` = HBM bytes per launch from the committed rocprofv3 PMC passes of the
+    same workload; `traffic_ratio` = traffic / algorithmic bytes (per launch and, over every kernel of
+    the step the passes cover, per step).  `rocprof` = the committed kernel-trace average of the same
+    kernel (profiles/<round>/kernel_stats_<stats_name>.csv) and the fraction it gives."""
+    nm, us, fl, by = kern
+    peak_mfma = PEAK_BF16_MFMA_TFLOPS if args.compute == "bf16" else PEAK_FP32_MFMA_TFLOPS
+    pmc = pmc_traffic(args, batch_tag)
+    traffic = pmc.get(nm, pmc.get(nm.split("+")[0]))
     sec = us * 1e-6
     mfma_ach = fl / sec / 1e12 if fl else 0.0
     hbm_ach = by / sec / 1e9
@@ -494,14 +565,52 @@ def roofline_of(args, kern, batch_tag):
     # roof is the MFMA peak of the compute dtype, whatever bounds it below that (LDS, L2->VGPR, latency:
     # DESIGN.md section 3), and `frac` says how far below it runs
     hbm_measured_frac = ((traffic or by) / sec / 1e9) / PEAK_HBM_GBS
-    common = {"traffic": traffic, "kernel": nm, "avg_us": us, "algorithmic_flops": fl, "algorithmic_bytes": by,
+    mfma_bound = fl > 0 and hbm_measured_frac < 0.5
+    common = {"traffic": traffic, "kernel": nm, "avg_us": us, "avg_us_source": "HIP events around the launch",
+              "algorithmic_flops": fl, "algorithmic_bytes": by,
+              "traffic_ratio": (traffic / by) if (traffic and by) else None,
               "mfma_frac": mfma_frac, "hbm_frac": hbm_frac, "hbm_measured_frac": hbm_measured_frac,
               "intensity_flop_per_byte": intensity, "ridge_flop_per_byte": ridge}
-    if fl > 0 and hbm_measured_frac < 0.5:
+    if incontext_us is not None:   # the step-time difference with / without the kernel (kernel_times)
+        common["avg_us_incontext_omit"] = incontext_us
+    if step_kernels:
+        covered = [(k[0], k[3]) for k in step_kernels if pmc.get(k[0], pmc.get(k[0].split("+")[0])) is not None]
+        if covered:
+            t = sum(pmc.get(n, pmc.get(n.split("+")[0])) for n, _ in covered)
+            b = sum(b for _, b in covered)
+            common["traffic_step"] = t
+            common["algorithmic_bytes_step"] = b
+            common["traffic_ratio_step"] = t / b if b else None
+            common["traffic_step_kernels"] = [n for n, _ in covered]
+    if stats_name:
+        rp_us, rp_path = rocprof_avg_us(stats_name, nm)
+        if rp_us:
+            rp_frac = (fl / (rp_us * 1e-6) / 1e12 / peak_mfma) if mfma_bound else (by / (rp_us * 1e-6) / 1e9 / PEAK_HBM_GBS)
+            common["rocprof"] = {"avg_us": rp_us, "frac": rp_frac, "file": rp_path,
+                                 "live_over_rocprof": us / rp_us}
+    if mfma_bound:
         return dict({"bound": "mfma", "achieved": mfma_ach, "peak": peak_mfma, "unit": "TFLOP/s",
                      "frac": mfma_frac}, **common)
     return dict({"bound": "hbm", "achieved": hbm_ach, "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": hbm_frac},
                 **common)
+
+
+def dominant_roofline(args, eng, flags, batch_tag, stats_name, count=50, reps=5, ev_count=200):
+    """Every kernel's in-context time (kernel_times), the dominant one picked by it, then that kernel's
+    average launch duration from HIP event pairs (kernel_event_us) for the roofline.
+    Returns (kernels list, roofline)."""
+    ks = kernel_times(eng, flags, count=count, reps=reps)
+    dom = max(ks, key=lambda k: k[1])
+    mean_us, med_us = kernel_event_us(eng, flags, dom[0], count=ev_count)
+    kernels = [{"kernel": k[0], "avg_us_incontext_omit": k[1], "flops": k[2], "bytes": k[3]} for k in ks]
+    for k in kernels:
+        if k["kernel"] == dom[0]:
+            k["avg_us_events"] = mean_us
+            k["median_us_events"] = med_us
+    roof = roofline_of(args, (dom[0], mean_us, dom[2], dom[3]), batch_tag, incontext_us=dom[1],
+                       stats_name=stats_name, step_kernels=ks)
+    roof["median_us_events"] = med_us
+    return kernels, roof
 
 
 ALLREDUCE_EST_US = 20.0   # assumed RCCL all-reduce of the 428 KB MLP-284 gradient over 8 xGMI-linked GPUs
@@ -612,7 +721,71 @@ def single_gpu_extras(args, spec, device):
         "allreduce_estimate_us": ALLREDUCE_EST_US, "one_gpu_step_us": t1}
     del eng
     torch.cuda.empty_cache()
+    out["projection_w8_weak"] = weak_projection(args, spec, device, t1)
     return out
+
+
+def sampler_route(k):
+    """Which random.sample kernel the engine launches for k draws (csrc/sample.hip launch_sample_uniform)."""
+    if 2048 <= k <= 4608:
+        return "k_sample_fast (one-round draw, bitmap dedup, MT block cache; csrc/sample_pipe.hpp)"
+    need = 4 * (k + 624)
+    hs = 2048
+    while hs < need and hs < 16384:
+        hs <<= 1
+    if need <= 3 * hs:
+        return f"k_sample_uniform<{hs}> (one 1024-thread workgroup, LDS hash table of {hs} slots)"
+    hs = 32768
+    while hs < need:
+        hs <<= 1
+    return (f"k_sample_uniform_g<{hs}> (one 1024-thread workgroup, multi-pass body, a {hs}-slot (value, position) "
+            "hash table in global memory)")
+
+
+def weak_projection(args, spec, device, t1_us, W=8, rows=4096):
+    """Weak scaling (4096 rows per rank, global minibatch 32768 at world 8), rank 0 of a world_size = 8
+    engine on one GPU: every rank draws the SAME global 32768-sample random.sample (bit-exact with one
+    GPU, R:dqn/replay_memory.py:38-39) and computes its 4096-row shard, then Adam + soft update.  The
+    efficiency bound is the one-GPU 4096-row step (configs3_n1) over the shard step (+ the all-reduce
+    estimate); the sampler's route and cost at k = 32768 are measured as its own launch."""
+    Bg = rows * W
+    eng = make_engine(args, spec, Bg, W, 0, device)
+    steps = max(args.steps // 2, 50)
+
+    def shard_step(prefetch=args.prefetch):
+        eng.learn_step(grads_only=True, prefetch=prefetch)
+        eng.apply_grads(soft_update=True)
+    for _ in range(args.warmup):
+        shard_step()
+    el_pf = timed_steps(shard_step, steps, None, device)
+    shard_step(prefetch=False)   # consume the pending draw
+    for _ in range(max(2, args.warmup // 2)):
+        shard_step(prefetch=False)
+    el_seq = timed_steps(lambda: shard_step(prefetch=False), steps, None, device)
+    ks = kernel_times(eng, C.STEP_GRADS_ONLY, count=30, reps=3)
+    samp = next((k for k in ks if k[0].startswith("sample")), None)
+    samp_ev = kernel_event_us(eng, C.STEP_GRADS_ONLY, samp[0], count=50) if samp else None
+    kpf = kernel_times(eng, C.STEP_GRADS_ONLY | C.STEP_PREFETCH, count=30, reps=3) if args.prefetch else []
+    del eng
+    torch.cuda.empty_cache()
+    shard_pf, shard_seq = el_pf / steps * 1e6, el_seq / steps * 1e6
+    shard = min(shard_pf, shard_seq)
+    return {"rows_per_rank": rows, "global_batch": Bg, "world": W,
+            "shard_step_us": shard, "shard_step_us_prefetch": shard_pf, "shard_step_us_sampler_launch": shard_seq,
+            "one_gpu_step_us_4096": t1_us,
+            "sampler": {"kernel": samp[0] if samp else None, "k": Bg,
+                        "route": sampler_route(Bg),
+                        "avg_us_events": samp_ev[0] if samp_ev else None,
+                        "avg_us_incontext_omit": samp[1] if samp else None},
+            "kernels": [{"kernel": k[0], "avg_us": k[1]} for k in ks],
+            "kernels_prefetch": [{"kernel": k[0], "avg_us": k[1]} for k in kpf],
+            "efficiency_bound": {"without_allreduce": t1_us / shard,
+                                 "with_allreduce": t1_us / (shard + ALLREDUCE_EST_US),
+                                 "allreduce_estimate_us": ALLREDUCE_EST_US},
+            "note": "weak scaling: per-GPU work fixed at 4096 rows; efficiency = one-GPU 4096-row step time / "
+                    "world-8 shard step time (each rank still draws the global 32768-sample random.sample, the "
+                    "replicated O(B_global) term); the all-reduce term is an estimate, the driver's 8-GPU node "
+                    "measures it"}
 
 
 def head_net_extra(args, device):
@@ -627,13 +800,9 @@ def head_net_extra(args, device):
     steps = max(args.steps, 100)
     el, _ = run_learner(a, eng, 1, None, steps, args.warmup, None, device)
     flags = C.STEP_SOFT_UPDATE | (C.STEP_PREFETCH if a.prefetch else 0)
-    ks = kernel_times(eng, flags, count=50, reps=3)
-    dom = max(ks, key=lambda k: k[1])
-    dom = kernel_times(eng, flags, count=100, reps=5, only={dom[0]})[0]
+    kernels, roof = dominant_roofline(a, eng, flags, 256, "hybrid_b256", count=50, reps=3, ev_count=200)
     out = {"value": 256 * steps / el, "unit": "transitions/s", "ms_per_step": el / steps * 1e3, "batch": 256,
-           "net": net_name(a), "algo": a.algo, "dtype": "fp32",
-           "kernels": [{"kernel": k[0], "avg_us": (dom[1] if k[0] == dom[0] else k[1])} for k in ks],
-           "roofline": roofline_of(a, dom, 256)}
+           "net": net_name(a), "algo": a.algo, "dtype": "fp32", "kernels": kernels, "roofline": roof}
     del eng
     torch.cuda.empty_cache()
     return out
@@ -683,14 +852,10 @@ def configs2_extra(args, device):
     steps = max(args.steps, 20)
     el, _ = run_learner(a, eng, 1, None, steps, max(2, min(args.warmup, 5)), None, device)
     flags = C.STEP_SOFT_UPDATE | (C.STEP_PREFETCH if a.prefetch else 0)
-    ks = kernel_times(eng, flags, count=6, reps=3)
-    dom = max(ks, key=lambda k: k[1])
-    dom = kernel_times(eng, flags, count=20, reps=5, only={dom[0]})[0]
+    kernels, roof = dominant_roofline(a, eng, flags, 256, "hybrid84_b256", count=6, reps=3, ev_count=20)
     out = {"value": 256 * steps / el, "unit": "transitions/s", "ms_per_step": el / steps * 1e3, "steps": steps,
            "batch": 256, "replay_capacity": a.capacity, "net": net_name(a), "algo": a.algo, "dtype": "fp32",
-           "workload": workload_name(a, 1),
-           "kernels": [{"kernel": k[0], "avg_us": (dom[1] if k[0] == dom[0] else k[1])} for k in ks],
-           "roofline": roofline_of(a, dom, 256)}
+           "workload": workload_name(a, 1), "kernels": kernels, "roofline": roof}
     del eng
     torch.cuda.empty_cache()
     if not args.no_cpu_baseline:
@@ -713,6 +878,8 @@ def c5_projection(args, device):
     steps = max(args.steps // 2, 50)
     eng = make_engine(a, spec, Bg, 1, 0, device)
     el1, _ = run_learner(a, eng, 1, None, steps, args.warmup, None, device)
+    kernels1, roof1 = dominant_roofline(a, eng, C.STEP_SOFT_UPDATE, Bg, "mlp_b8192_bf16", count=30, reps=3,
+                                        ev_count=100)
     del eng
     torch.cuda.empty_cache()
     eng = make_engine(a, spec, Bg, W, 0, device)
@@ -733,7 +900,8 @@ def c5_projection(args, device):
     # faster of the two is the projection, both are reported)
     t1, shard_g, shard_e = el1 / steps * 1e6, el / steps * 1e6, el_eager / steps * 1e6
     shard = min(shard_g, shard_e)
-    return {"one_gpu_step_us": t1, "one_gpu_value": Bg * steps / el1, "rows_per_rank": Bg // W,
+    return {"one_gpu_step_us": t1, "one_gpu_value": Bg * steps / el1, "one_gpu_kernels": kernels1,
+            "one_gpu_roofline": roof1, "rows_per_rank": Bg // W,
             "shard_step_us": shard, "shard_step_us_eager": shard_e, "shard_step_us_graph": shard_g,
             "steps_per_graph": gs,
             "tr_per_s_without_collectives": Bg / (shard * 1e-6),
@@ -906,13 +1074,8 @@ def main():
         flags = C.STEP_GRADS_ONLY if dpmode else C.STEP_SOFT_UPDATE
         if args.prefetch and not per:   # the plan the timed loop ran (steady state: no sampler launch)
             flags |= C.STEP_PREFETCH
-        ks = kernel_times(eng, flags, count=50, reps=5)
-        dom = max(ks, key=lambda k: k[1])
-        # re-time the dominant kernel with more steps per sample
-        dom = kernel_times(eng, flags, count=max(args.steps, 100), reps=7, only={dom[0]})[0]
-        kernels = [{"kernel": k[0], "avg_us": (dom[1] if k[0] == dom[0] else k[1]), "flops": k[2], "bytes": k[3]}
-                   for k in ks]
-        roofline = roofline_of(args, dom, Bl)
+        tag = "" if args.compute == "fp32" else f"_{args.compute}"
+        kernels, roofline = dominant_roofline(args, eng, flags, Bl, f"{args.net}_b{Bl}{tag}")
 
     extras = {}
     if not args.no_extras and args.net == "mlp" and not per and args.compute == "fp32":

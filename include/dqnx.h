@@ -374,6 +374,11 @@ int dqnx_agent_launch(dqnx_engine* e, int32_t flags, void* stream);
 #define DQNX_AGENT_LAUNCH 0x100
 int dqnx_agent_learn_mt(dqnx_engine* e, uint32_t* mt, int32_t* pos, int32_t flags, void* stream, int64_t* words);
 int dqnx_agent_readback(dqnx_engine* e, int32_t wait, dqnx_ctrl* out);
+/* dqnx_agent_quiesce: waits for what dqnx_agent_launch / dqnx_agent_learn_mt would wait on before
+ *   launching (the previous step's unread control-block readback); no state changes.  The drop-in
+ *   calls it, with the GIL released, before a dqnx_agent_learn_mt (GIL held) whose previous readback
+ *   is still unread, so no other Python thread is blocked for the length of a GPU wait. */
+int dqnx_agent_quiesce(dqnx_engine* e);
 uint64_t dqnx_act_host_scratch_bytes(const dqnx_net_desc* net, int32_t n);
 int dqnx_act_host(const dqnx_net_desc* net, const float* params, const float* obs_host, int32_t n,
                   int32_t* actions_host, void* scratch, uint64_t scratch_bytes, void* stream);

@@ -260,6 +260,13 @@ __device__ __forceinline__ void act_signal(const ActArgs& a) {
 // at the top of the kernel, beside layer 1's, and the hand-off moves G floats per layer-2 neuron.
 // The shares go out as write-through (sc1) stores, so the producers need no release fence (the
 // last arriver's acquire stays: cdna_hip_programming.md Guideline 16, the sc1 form of the recipe).
+// This rests on gfx950 ISA behaviour, not on the HIP/C++ memory model: a relaxed agent-scope store
+// lowers to `global_store ... sc1` (write-through to memory), every storing wave drains vmcnt before
+// the workgroup barrier, and ONE lane then takes the relaxed agent-scope ticket; the workgroup whose
+// ticket comes back last is the consumer -- row 1 of MI355X_MICROARCH.md's measured hand-off table
+// ("ONE lane of each storing workgroup, for ALL that workgroup's stores ... an agent-scope atomic
+// add").  A release RMW on the ticket would be the portable form; it lowers to buffer_wbl2 (an L2
+// write-back per workgroup) on this chip, which the sc1 stores make redundant.
 template <int R, int ACT>
 __global__ __launch_bounds__(kActThreads) void k_act_mlp2(ActArgs a) {
     extern __shared__ float lds[];
@@ -389,17 +396,17 @@ int launch_act_r(const ActArgs& a, hipStream_t s) {
     if (act2_ok(a, R)) {
         const size_t lds2 = ((size_t)R * a.ld + R * 16 + (size_t)a.A * a.F) * sizeof(float);
         if (a.act == DQNX_ACT_RELU)
-            hipLaunchKernelGGL((k_act_mlp2<R, DQNX_ACT_RELU>), grid, dim3(kActThreads), lds2, s, a);
+            DQNX_LAUNCH((k_act_mlp2<R, DQNX_ACT_RELU>), grid, dim3(kActThreads), lds2, s, a);
         else
-            hipLaunchKernelGGL((k_act_mlp2<R, DQNX_ACT_ELU>), grid, dim3(kActThreads), lds2, s, a);
+            DQNX_LAUNCH((k_act_mlp2<R, DQNX_ACT_ELU>), grid, dim3(kActThreads), lds2, s, a);
         DQNX_HIP_CHECK(hipGetLastError());
         return DQNX_OK;
     }
     const size_t lds = (size_t)2 * R * a.ld * sizeof(float);
     if (a.act == DQNX_ACT_RELU)
-        hipLaunchKernelGGL((k_act_mlp<R, DQNX_ACT_RELU>), grid, dim3(kActThreads), lds, s, a);
+        DQNX_LAUNCH((k_act_mlp<R, DQNX_ACT_RELU>), grid, dim3(kActThreads), lds, s, a);
     else
-        hipLaunchKernelGGL((k_act_mlp<R, DQNX_ACT_ELU>), grid, dim3(kActThreads), lds, s, a);
+        DQNX_LAUNCH((k_act_mlp<R, DQNX_ACT_ELU>), grid, dim3(kActThreads), lds, s, a);
     DQNX_HIP_CHECK(hipGetLastError());
     return DQNX_OK;
 }

@@ -78,7 +78,7 @@ int launch_act_conv(const ActConvArgs& a, hipStream_t s) {
     const size_t lds = act_conv_lds_bytes(a);
     if (lds > 64 * 1024 || a.Ho * a.Wo > kConvThreads * 64)
         return set_error(DQNX_EUNSUPPORTED, "dqnx_act: conv layer too large for the acting kernel (%zu B LDS)", lds);
-    hipLaunchKernelGGL(k_act_conv, dim3(a.Co, a.n), dim3(kConvThreads), lds, s, a);
+    DQNX_LAUNCH(k_act_conv, dim3(a.Co, a.n), dim3(kConvThreads), lds, s, a);
     DQNX_HIP_CHECK(hipGetLastError());
     return DQNX_OK;
 }

@@ -113,7 +113,7 @@ void dw_adam_grid(DwAdamArgs& a) {
 int launch_dw_adam(const DwAdamArgs& a, hipStream_t s) {
     int blocks = 0;
     for (int p = 0; p < a.npr; p++) blocks += a.pr[p].blocks;
-    hipLaunchKernelGGL(k_dw_adam, dim3(blocks), dim3(64 * DW_NWV), 0, s, a);
+    DQNX_LAUNCH(k_dw_adam, dim3(blocks), dim3(64 * DW_NWV), 0, s, a);
     DQNX_HIP_CHECK(hipGetLastError());
     return DQNX_OK;
 }

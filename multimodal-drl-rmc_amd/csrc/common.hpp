@@ -112,6 +112,30 @@ __device__ __forceinline__ int xcd_remap(int L, int total) {
 
 }  // namespace dqnx
 
+// Kernel-duration timing (dqnx_learn_step_timed, bench.py's roofline): while a pair of events is
+// armed on this host thread, the NEXT kernel launched through DQNX_LAUNCH goes out through
+// hipExtLaunchKernelGGL with the pair bound to its dispatch, so the events carry that dispatch's own
+// begin / end timestamps (the packet's profiling signal, the source rocprofv3's kernel trace reads),
+// not the time of marker packets around it.  Disarmed by that launch.
+#include <hip/hip_ext.h>
+namespace dqnx {
+struct KernelTimer {
+    hipEvent_t start = nullptr, stop = nullptr;
+};
+KernelTimer& kernel_timer();   // thread-local (engine.cpp)
+}  // namespace dqnx
+#define DQNX_LAUNCH(K, G, B, SH, S, ...)                                                         \
+    do {                                                                                         \
+        dqnx::KernelTimer& _kt = dqnx::kernel_timer();                                           \
+        if (_kt.start) {                                                                         \
+            const hipEvent_t _e0 = _kt.start, _e1 = _kt.stop;                                    \
+            _kt.start = _kt.stop = nullptr;                                                      \
+            hipExtLaunchKernelGGL(K, dim3(G), dim3(B), (std::uint32_t)(SH), S, _e0, _e1, 0u, __VA_ARGS__); \
+        } else {                                                                                 \
+            hipLaunchKernelGGL(K, G, B, SH, S, __VA_ARGS__);                                     \
+        }                                                                                        \
+    } while (0)
+
 #define DQNX_HIP_CHECK(expr)                                                    \
     do {                                                                        \
         hipError_t _e = (expr);                                                 \

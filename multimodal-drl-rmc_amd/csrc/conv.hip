@@ -299,8 +299,8 @@ __global__ __launch_bounds__(256) void k_col2im_3x3(Col2imArgs a, int ci_shift) 
 
 template <int SH, int SW>
 static void launch_col2im_3x3(const Col2imArgs& a, int act, int shift, dim3 g, hipStream_t s) {
-    if (act == DQNX_ACT_RELU) hipLaunchKernelGGL((k_col2im_3x3<DQNX_ACT_RELU, SH, SW>), g, dim3(256), 0, s, a, shift);
-    else hipLaunchKernelGGL((k_col2im_3x3<DQNX_ACT_ELU, SH, SW>), g, dim3(256), 0, s, a, shift);
+    if (act == DQNX_ACT_RELU) DQNX_LAUNCH((k_col2im_3x3<DQNX_ACT_RELU, SH, SW>), g, dim3(256), 0, s, a, shift);
+    else DQNX_LAUNCH((k_col2im_3x3<DQNX_ACT_ELU, SH, SW>), g, dim3(256), 0, s, a, shift);
 }
 
 static dim3 grid_for(int64_t total) {
@@ -329,20 +329,20 @@ int launch_im2col(const Im2colArgs& a, hipStream_t s) {
     if (im2col_mode() == 1 && band <= 64 * 1024 && a.M % (a.Ho * a.Wo) == 0 && a.Wo * a.Kstride >= 2048 &&
         a.kw < 256 && (size_t)a.kh * a.Ci * a.Wi < (1u << 23)) {
         const int64_t g = (int64_t)a.nstreams * (a.M / (a.Ho * a.Wo)) * a.Ho * G;
-        hipLaunchKernelGGL(k_im2col_lds, dim3((unsigned)g), dim3(256), band, s, a, G);
+        DQNX_LAUNCH(k_im2col_lds, dim3((unsigned)g), dim3(256), band, s, a, G);
         DQNX_HIP_CHECK(hipGetLastError());
         return DQNX_OK;
     }
     if (a.Kstride < 64) {   // measured: conv 1 (K 18 / 36) 30 -> 15 us / 1.40 -> 0.82 ms; K >= 288 slower
         int64_t g = ((int64_t)a.M * a.nstreams * a.Kstride + 255) / 256;
         if (g > 16384) g = 16384;
-        hipLaunchKernelGGL(k_im2col_flat, dim3((unsigned)g), dim3(256), 0, s, a);
+        DQNX_LAUNCH(k_im2col_flat, dim3((unsigned)g), dim3(256), 0, s, a);
         DQNX_HIP_CHECK(hipGetLastError());
         return DQNX_OK;
     }
     int64_t g = ((int64_t)a.M * a.nstreams + 3) / 4;   // 4 rows (waves) per block
     if (g > 8192) g = 8192;
-    hipLaunchKernelGGL(k_im2col_rows, dim3((unsigned)g), dim3(256), 0, s, a);
+    DQNX_LAUNCH(k_im2col_rows, dim3((unsigned)g), dim3(256), 0, s, a);
     DQNX_HIP_CHECK(hipGetLastError());
     return DQNX_OK;
 }
@@ -351,17 +351,17 @@ int launch_flatten_concat(const FlattenArgs& a, hipStream_t s) {
     // (4,84,84) B=256: 395 -> 67 us; the (2,27,5) net's 21-pixel maps keep the element-wise form
     if (im2col_mode() == 1 && a.C <= 128 && a.Ho * a.Wo >= 256) {
         const int64_t g = (int64_t)a.nstreams * a.Bl * ((a.Ho * a.Wo + 63) / 64 + 1);
-        hipLaunchKernelGGL(k_flatten_concat_tiled, dim3((unsigned)g), dim3(256), 0, s, a);
+        DQNX_LAUNCH(k_flatten_concat_tiled, dim3((unsigned)g), dim3(256), 0, s, a);
         DQNX_HIP_CHECK(hipGetLastError());
         return DQNX_OK;
     }
-    hipLaunchKernelGGL(k_flatten_concat, grid_for((int64_t)a.Bl * a.strideF * a.nstreams), dim3(256), 0, s, a);
+    DQNX_LAUNCH(k_flatten_concat, grid_for((int64_t)a.Bl * a.strideF * a.nstreams), dim3(256), 0, s, a);
     DQNX_HIP_CHECK(hipGetLastError());
     return DQNX_OK;
 }
 
 int launch_unflatten(const UnflattenArgs& a, hipStream_t s) {
-    hipLaunchKernelGGL(k_unflatten, grid_for((int64_t)a.Bl * a.Ho * a.Wo * a.C), dim3(256), 0, s, a);
+    DQNX_LAUNCH(k_unflatten, grid_for((int64_t)a.Bl * a.Ho * a.Wo * a.C), dim3(256), 0, s, a);
     DQNX_HIP_CHECK(hipGetLastError());
     return DQNX_OK;
 }
@@ -379,8 +379,8 @@ int launch_col2im(const Col2imArgs& a, int act, hipStream_t s) {
         DQNX_HIP_CHECK(hipGetLastError());
         return DQNX_OK;
     }
-    if (act == DQNX_ACT_RELU) hipLaunchKernelGGL(k_col2im<DQNX_ACT_RELU>, g, dim3(256), 0, s, a);
-    else hipLaunchKernelGGL(k_col2im<DQNX_ACT_ELU>, g, dim3(256), 0, s, a);
+    if (act == DQNX_ACT_RELU) DQNX_LAUNCH(k_col2im<DQNX_ACT_RELU>, g, dim3(256), 0, s, a);
+    else DQNX_LAUNCH(k_col2im<DQNX_ACT_ELU>, g, dim3(256), 0, s, a);
     DQNX_HIP_CHECK(hipGetLastError());
     return DQNX_OK;
 }

@@ -567,7 +567,7 @@ template <class KernelT>
 int launch_persistent(KernelT fn, const ConvIgArgs& a, size_t lds, hipStream_t s) {
     const int64_t tiles = (int64_t)a.nstreams * a.nclass * a.Bl * a.maxtiles;
     const int grid = persistent_grid(reinterpret_cast<const void*>(fn), lds, tiles);
-    hipLaunchKernelGGL(fn, dim3(grid), dim3(256), lds, s, a);
+    DQNX_LAUNCH(fn, dim3(grid), dim3(256), lds, s, a);
     DQNX_HIP_CHECK(hipGetLastError());
     return DQNX_OK;
 }
@@ -623,10 +623,10 @@ int launch_conv_dw_ig(const ConvDwIgArgs& a, hipStream_t s) {
     if (lds > 160 * 1024) return set_error(DQNX_EUNSUPPORTED, "conv_dw_ig: band of %zu B exceeds LDS", lds);
     const dim3 grid((unsigned)((int64_t)a.slices * (a.C / a.CB)));
     const bool vec = a.X.cstride == 1;
-    if (a.Co == 64 && a.TN == 9 && vec) hipLaunchKernelGGL((k_conv_dw_ig<9, 4, true>), grid, dim3(256), lds, s, a);
-    else if (a.Co == 32 && a.TN == 9 && vec) hipLaunchKernelGGL((k_conv_dw_ig<9, 2, true>), grid, dim3(256), lds, s, a);
-    else if (a.Co == 64 && a.TN == 3 && !vec) hipLaunchKernelGGL((k_conv_dw_ig<3, 4, false>), grid, dim3(256), lds, s, a);
-    else if (a.Co == 32 && a.TN == 3 && !vec) hipLaunchKernelGGL((k_conv_dw_ig<3, 2, false>), grid, dim3(256), lds, s, a);
+    if (a.Co == 64 && a.TN == 9 && vec) DQNX_LAUNCH((k_conv_dw_ig<9, 4, true>), grid, dim3(256), lds, s, a);
+    else if (a.Co == 32 && a.TN == 9 && vec) DQNX_LAUNCH((k_conv_dw_ig<9, 2, true>), grid, dim3(256), lds, s, a);
+    else if (a.Co == 64 && a.TN == 3 && !vec) DQNX_LAUNCH((k_conv_dw_ig<3, 4, false>), grid, dim3(256), lds, s, a);
+    else if (a.Co == 32 && a.TN == 3 && !vec) DQNX_LAUNCH((k_conv_dw_ig<3, 2, false>), grid, dim3(256), lds, s, a);
     else return set_error(DQNX_EUNSUPPORTED, "conv_dw_ig: Co %d TN %d", a.Co, a.TN);
     DQNX_HIP_CHECK(hipGetLastError());
     return DQNX_OK;
@@ -634,14 +634,14 @@ int launch_conv_dw_ig(const ConvDwIgArgs& a, hipStream_t s) {
 
 int launch_unflatten_tiled(const UnflattenArgs& a, hipStream_t s) {
     const int nt = (a.Ho * a.Wo + 63) / 64;
-    hipLaunchKernelGGL(k_unflatten_tiled, dim3((unsigned)((int64_t)a.Bl * nt)), dim3(256), 0, s, a);
+    DQNX_LAUNCH(k_unflatten_tiled, dim3((unsigned)((int64_t)a.Bl * nt)), dim3(256), 0, s, a);
     DQNX_HIP_CHECK(hipGetLastError());
     return DQNX_OK;
 }
 
 int launch_conv_perm(const ConvPermArgs& a, hipStream_t s) {
     if (a.njobs <= 0) return DQNX_OK;
-    hipLaunchKernelGGL(k_conv_perm, dim3(64, a.njobs), dim3(256), 0, s, a);
+    DQNX_LAUNCH(k_conv_perm, dim3(64, a.njobs), dim3(256), 0, s, a);
     DQNX_HIP_CHECK(hipGetLastError());
     return DQNX_OK;
 }

@@ -19,6 +19,11 @@
 
 namespace dqnx {
 
+KernelTimer& kernel_timer() {   // (DQNX_LAUNCH, common.hpp)
+    static thread_local KernelTimer t;
+    return t;
+}
+
 static thread_local char g_err[512] = "";
 
 int set_error(int code, const char* fmt, ...) {
@@ -3388,20 +3393,28 @@ int dqnx_learn_step_timed(dqnx_engine* e, int32_t flags, int32_t kernel_index, v
     if (e->pf_valid) return set_error(DQNX_ESTATE, "timed step with a prefetched minibatch pending");
     if (e->ring_size < e->Bs && !(flags & DQNX_STEP_GIVEN_INDICES))
         return set_error(DQNX_EINVAL, "Sample larger than population: %lld < %d", (long long)e->ring_size, e->Bs);
-    const int key = flags & 7;
+    // the plan kernel_count / kernel_info / step_omit describe (with DQNX_STEP_PREFETCH: the
+    // steady-state step of a prefetching loop; the draw it makes is left stale, as step_omit's)
+    const int key = timing_key(e, flags);
     const std::vector<KStep>& ks = steps_for(e, key);
     const int n = (int)ks.size();
     if (kernel_index < 0 || kernel_index >= n) return set_error(DQNX_EINVAL, "kernel index out of range");
     hipStream_t s = (hipStream_t)stream;
-    // eager launches (HIP cannot time events recorded inside a graph); the caller enqueues
-    // many steps before reading the events, so the host runs ahead of the GPU and the event
-    // pair brackets the kernel alone
+    // eager launches (HIP cannot time events recorded inside a graph).  The event pair is bound to
+    // the timed kernel's own dispatch (DQNX_LAUNCH through hipExtLaunchKernelGGL, common.hpp): the
+    // events carry that dispatch's begin / end timestamps, as rocprofv3's kernel trace does, with no
+    // marker packets between the kernels of the step
     rc = enqueue_range(ks, 0, kernel_index, s);
     if (rc) return rc;
-    DQNX_HIP_CHECK(hipEventRecord((hipEvent_t)ev_start, s));
+    KernelTimer& kt = kernel_timer();
+    kt.start = (hipEvent_t)ev_start;
+    kt.stop = (hipEvent_t)ev_stop;
     rc = enqueue_range(ks, kernel_index, kernel_index + 1, s);
+    const bool unused = kt.start != nullptr;
+    kt.start = kt.stop = nullptr;
     if (rc) return rc;
-    DQNX_HIP_CHECK(hipEventRecord((hipEvent_t)ev_stop, s));
+    if (unused) return set_error(DQNX_EUNSUPPORTED, "kernel %d (%s) launches nothing through DQNX_LAUNCH", kernel_index,
+                                 ks[kernel_index].name.c_str());
     return enqueue_range(ks, kernel_index + 1, n, s);
 }
 
@@ -3734,7 +3747,7 @@ uint64_t dqnx_act_scratch_bytes(const dqnx_net_desc* net, int32_t n) {
 // done_flag: the MLP acting kernel stores done_seq there (system scope) after the actions (dqnx_act_host)
 static int act_impl(const dqnx_net_desc* net, const float* params, const float* obs, int32_t n, int32_t* actions,
                     float* values, void* scratch, uint64_t scratch_bytes, void* stream, uint32_t* done_flag,
-                    uint32_t done_seq);
+                    uint32_t done_seq, bool* signals = nullptr);
 
 int dqnx_act(const dqnx_net_desc* net, const float* params, const float* obs, int32_t n, int32_t* actions,
              float* values, void* scratch, uint64_t scratch_bytes, void* stream) {
@@ -3743,17 +3756,21 @@ int dqnx_act(const dqnx_net_desc* net, const float* params, const float* obs, in
 
 static int act_impl(const dqnx_net_desc* net, const float* params, const float* obs, int32_t n, int32_t* actions,
                     float* values, void* scratch, uint64_t scratch_bytes, void* stream, uint32_t* done_flag,
-                    uint32_t done_seq) {
+                    uint32_t done_seq, bool* signals) {
     NetPlan np;
     ActArgs a;
+    if (signals) *signals = false;
     int rc = act_plan(net, np, a);
     if (rc) return rc;
     if (n < 0 || (n > 0 && (!params || !obs || !actions || !scratch)))
         return set_error(DQNX_EINVAL, "dqnx_act: bad argument");
-    if (n > 0 && act_rows_per_block(n, a.ld) == 0)
-        return set_error(DQNX_EUNSUPPORTED, "dqnx_act: layer width %d does not fit LDS", a.ld);
+    const int R = n > 0 ? act_rows_per_block(n, a.ld) : 1;
+    if (R == 0) return set_error(DQNX_EUNSUPPORTED, "dqnx_act: layer width %d does not fit LDS", a.ld);
     a.params = params; a.obs = obs; a.actions = actions; a.values = values; a.n = n;
-    a.done_flag = net->kind == DQNX_NET_MLP ? done_flag : nullptr;
+    // the acting kernels store the completion word from row group 0 only when the launch has ONE row
+    // group (n <= R rows per workgroup: R halves for inputs wider than 2048 / 4096 floats)
+    a.done_flag = (net->kind == DQNX_NET_MLP && n <= R) ? done_flag : nullptr;
+    if (signals) *signals = a.done_flag != nullptr && n > 0;
     a.done_seq = done_seq;
     if (n == 0) return DQNX_OK;
     const uint64_t need = dqnx_act_scratch_bytes(net, n);
@@ -3958,6 +3975,15 @@ int dqnx_agent_launch(dqnx_engine* e, int32_t flags, void* stream) {
     return rc ? rc : prev_rc;
 }
 
+int dqnx_agent_quiesce(dqnx_engine* e) {
+    if (!e) return set_error(DQNX_EINVAL, "null engine");
+    // the waits agent_launch_impl would make (the previous step's unread control-block readback, the
+    // last reader of the zero-copy RNG block), made here instead: callers reach this through a binding
+    // that releases the GIL, so dqnx_agent_learn_mt (GIL held) finds them complete
+    if (e->ag_ctrl_ev && (e->ag_ctrl_live || e->ag_zc_used)) DQNX_HIP_CHECK(hipEventSynchronize(e->ag_ctrl_ev));
+    return DQNX_OK;
+}
+
 int dqnx_agent_readback(dqnx_engine* e, int32_t wait, dqnx_ctrl* out) {
     if (!e) return set_error(DQNX_EINVAL, "null engine");
     if (!e->ag_ctrl_live) return 0;
@@ -4023,10 +4049,13 @@ int dqnx_act_host(const dqnx_net_desc* net, const float* params, const float* ob
         int32_t* pa = (int32_t*)(pin + (size_t)n * net->obs_dim * 4);
         volatile uint32_t* flag = (volatile uint32_t*)(pin + flag_at);
         const uint32_t want_seq = ++seq ? seq : ++seq;   // (never 0)
+        *flag = 0;   // (a grown or reused block never holds a stale word, whatever its sequence)
+        bool signals = false;
         int rc = act_impl(net, params, (const float*)pin, n, pa, nullptr, act_sc, act_bytes, stream,
-                          (uint32_t*)(pin + flag_at), want_seq);
+                          (uint32_t*)(pin + flag_at), want_seq, &signals);
         if (rc) return rc;
-        const bool polled = n <= 4 && route_knob("DQNX_ACT_POLL", 1) != 0;   // (one row group signals)
+        // poll only a launch that stores the word (one row group); any other waits on the stream
+        const bool polled = signals && route_knob("DQNX_ACT_POLL", 1) != 0;
         bool seen = false;
         if (polled) {
             const auto t0 = std::chrono::steady_clock::now();

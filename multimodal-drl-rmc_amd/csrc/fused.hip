@@ -1235,8 +1235,8 @@ int launch_dw_bf16(const BwdArgs& a, hipStream_t s) {
         // (the attribute only past 64 KB, and exactly the bytes requested: a failed hipFuncSetAttribute
         // -- static LDS + a 160 KB maximum -- would be the launch's hipGetLastError)
         const size_t shd = sizeof(PerTrackLds<256>) > PER_TOP * sizeof(double) ? sizeof(PerTrackLds<256>) : PER_TOP * sizeof(double);
-        if (t.bm == 64 && t.bn == 64) hipLaunchKernelGGL((k_dw_bf16d<64, 64>), dim3(blocks), dim3(256), shd, s, a);
-        else if (t.bm == 32 && t.bn == 32) hipLaunchKernelGGL((k_dw_bf16d<32, 32>), dim3(blocks), dim3(256), shd, s, a);
+        if (t.bm == 64 && t.bn == 64) DQNX_LAUNCH((k_dw_bf16d<64, 64>), dim3(blocks), dim3(256), shd, s, a);
+        else if (t.bm == 32 && t.bn == 32) DQNX_LAUNCH((k_dw_bf16d<32, 32>), dim3(blocks), dim3(256), shd, s, a);
         else return set_error(DQNX_EUNSUPPORTED, "dw_bf16d: %dx%d tiles", t.bm, t.bn);
         DQNX_HIP_CHECK(hipGetLastError());
         return DQNX_OK;
@@ -1247,10 +1247,10 @@ int launch_dw_bf16(const BwdArgs& a, hipStream_t s) {
     // measured: 64 x 64 tiles best with 32-sample passes (64: +1.7 us, 128: +6 us at B=8192);
     // 32 x 32 tiles with 128-sample passes (the fp32 kernel's depth)
     const DwbTile t = dw_bf16_tile(a);
-    if (t.bm == 128 && t.bn == 128) hipLaunchKernelGGL((k_dw_bf16<128, 128, 32>), dim3(blocks), dim3(256), 0, s, a);
-    else if (t.bm == 128) hipLaunchKernelGGL((k_dw_bf16<128, 64, 32>), dim3(blocks), dim3(256), 0, s, a);
-    else if (t.bm == 64) hipLaunchKernelGGL((k_dw_bf16<64, 64, DQNX_DWB_KT64>), dim3(blocks), dim3(256), 0, s, a);
-    else hipLaunchKernelGGL((k_dw_bf16<32, 32, DQNX_DWB_KT32>), dim3(blocks), dim3(256), 0, s, a);
+    if (t.bm == 128 && t.bn == 128) DQNX_LAUNCH((k_dw_bf16<128, 128, 32>), dim3(blocks), dim3(256), 0, s, a);
+    else if (t.bm == 128) DQNX_LAUNCH((k_dw_bf16<128, 64, 32>), dim3(blocks), dim3(256), 0, s, a);
+    else if (t.bm == 64) DQNX_LAUNCH((k_dw_bf16<64, 64, DQNX_DWB_KT64>), dim3(blocks), dim3(256), 0, s, a);
+    else DQNX_LAUNCH((k_dw_bf16<32, 32, DQNX_DWB_KT32>), dim3(blocks), dim3(256), 0, s, a);
     DQNX_HIP_CHECK(hipGetLastError());
     return DQNX_OK;
 }
@@ -1328,7 +1328,7 @@ int launch_fused_fwd(const FusedFwdArgs& a, int act, hipStream_t s) {
 #define FUSED_FWD_GW(ACTV, NLV, BFV, MRV, PHV, GWV)                                                  \
     do {                                                                                             \
         if (shm > 64 * 1024) allow_lds(k_mlp_fwd<ACTV, NLV, BFV, MRV, PHV, GWV>, 160 * 1024);        \
-        hipLaunchKernelGGL((k_mlp_fwd<ACTV, NLV, BFV, MRV, PHV, GWV>), grid, block, shm, s, a);      \
+        DQNX_LAUNCH((k_mlp_fwd<ACTV, NLV, BFV, MRV, PHV, GWV>), grid, block, shm, s, a);      \
     } while (0)
 #define FUSED_FWD_MR(ACTV, NLV, BFV, MRV, PHV)                                                       \
     do {                                                                                             \
@@ -1377,10 +1377,10 @@ int launch_head_bwd(const HeadBwdArgs& a, int act, hipStream_t s) {
     do {                                                                                             \
         if (a.bf16) {                                                                                \
             if (pad > 64 * 1024) allow_lds(k_head_bwd<ACTV, NLV, true>, 120 * 1024);                 \
-            hipLaunchKernelGGL((k_head_bwd<ACTV, NLV, true>), grid, block, pad, s, a);               \
+            DQNX_LAUNCH((k_head_bwd<ACTV, NLV, true>), grid, block, pad, s, a);               \
         } else {                                                                                     \
             if (pad > 64 * 1024) allow_lds(k_head_bwd<ACTV, NLV, false>, 120 * 1024);                \
-            hipLaunchKernelGGL((k_head_bwd<ACTV, NLV, false>), grid, block, pad, s, a);              \
+            DQNX_LAUNCH((k_head_bwd<ACTV, NLV, false>), grid, block, pad, s, a);              \
         }                                                                                            \
     } while (0)
     const bool relu = act == DQNX_ACT_RELU;

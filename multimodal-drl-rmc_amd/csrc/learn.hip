@@ -285,7 +285,7 @@ int conv_dw_big_tiles(int in, int out) { return ((in + 1 + 127) / 128) * ((out +
 
 int launch_conv_dw_big(const BwdArgs& a, hipStream_t s) {
     const dim3 grid(conv_dw_big_tiles(a.dw[0].in, a.dw[0].out) * a.dw_slices);
-    hipLaunchKernelGGL(k_conv_dw_big, grid, dim3(256), 0, s, a);
+    DQNX_LAUNCH(k_conv_dw_big, grid, dim3(256), 0, s, a);
     DQNX_HIP_CHECK(hipGetLastError());
     return DQNX_OK;
 }
@@ -294,8 +294,8 @@ int conv_dx_big_tiles(int Bl, int in) { return ((in + 63) / 64) * ((Bl + 127) / 
 
 int launch_conv_dx_big(const BwdArgs& a, hipStream_t s) {
     const dim3 grid(conv_dx_big_tiles(a.Bl, a.in));
-    if (a.in % 4 == 0) hipLaunchKernelGGL((k_conv_dx_big<true>), grid, dim3(256), 0, s, a);
-    else hipLaunchKernelGGL((k_conv_dx_big<false>), grid, dim3(256), 0, s, a);
+    if (a.in % 4 == 0) DQNX_LAUNCH((k_conv_dx_big<true>), grid, dim3(256), 0, s, a);
+    else DQNX_LAUNCH((k_conv_dx_big<false>), grid, dim3(256), 0, s, a);
     DQNX_HIP_CHECK(hipGetLastError());
     return DQNX_OK;
 }
@@ -1296,22 +1296,22 @@ int launch_dw_adam16(const DwAdam16Args& a, hipStream_t s) {
     const dim3 grid(a.tiles + a.ptrack + (a.mtc ? 1 : 0) + (a.pf_nidx > 0 ? 1 : 0) + a.pprop_wgs);
     if (a.rows16 == 2) {
         switch (var) {   // measurement variants (waves per tile, k-steps per register set)
-            case 7: hipLaunchKernelGGL((k_dw_adam16<16, 4, 2>), grid, dim3(1024), 0, s, a); break;
-            case 8: hipLaunchKernelGGL((k_dw_adam16<8, 4, 2>), grid, dim3(512), 0, s, a); break;
-            default: hipLaunchKernelGGL((k_dw_adam16<8, 8, 2>), grid, dim3(512), 0, s, a); break;
+            case 7: DQNX_LAUNCH((k_dw_adam16<16, 4, 2>), grid, dim3(1024), 0, s, a); break;
+            case 8: DQNX_LAUNCH((k_dw_adam16<8, 4, 2>), grid, dim3(512), 0, s, a); break;
+            default: DQNX_LAUNCH((k_dw_adam16<8, 8, 2>), grid, dim3(512), 0, s, a); break;
         }
         DQNX_HIP_CHECK(hipGetLastError());
         return DQNX_OK;
     }
     if (a.rows16 != 1) return set_error(DQNX_EINVAL, "dw_adam16: %d row blocks per tile", a.rows16);
     switch (var) {   // measurement variants (waves per tile, k-steps per register set)
-        case 1: hipLaunchKernelGGL((k_dw_adam16<4, 8, 1>), grid, dim3(256), 0, s, a); break;
-        case 2: hipLaunchKernelGGL((k_dw_adam16<16, 4, 1>), grid, dim3(1024), 0, s, a); break;
-        case 3: hipLaunchKernelGGL((k_dw_adam16<8, 4, 1>), grid, dim3(512), 0, s, a); break;
-        case 4: hipLaunchKernelGGL((k_dw_adam16<4, 16, 1>), grid, dim3(256), 0, s, a); break;
-        case 5: hipLaunchKernelGGL((k_dw_adam16<8, 16, 1>), grid, dim3(512), 0, s, a); break;
-        case 6: hipLaunchKernelGGL((k_dw_adam16<16, 8, 1>), grid, dim3(1024), 0, s, a); break;
-        default: hipLaunchKernelGGL((k_dw_adam16<8, 8, 1>), grid, dim3(512), 0, s, a); break;
+        case 1: DQNX_LAUNCH((k_dw_adam16<4, 8, 1>), grid, dim3(256), 0, s, a); break;
+        case 2: DQNX_LAUNCH((k_dw_adam16<16, 4, 1>), grid, dim3(1024), 0, s, a); break;
+        case 3: DQNX_LAUNCH((k_dw_adam16<8, 4, 1>), grid, dim3(512), 0, s, a); break;
+        case 4: DQNX_LAUNCH((k_dw_adam16<4, 16, 1>), grid, dim3(256), 0, s, a); break;
+        case 5: DQNX_LAUNCH((k_dw_adam16<8, 16, 1>), grid, dim3(512), 0, s, a); break;
+        case 6: DQNX_LAUNCH((k_dw_adam16<16, 8, 1>), grid, dim3(1024), 0, s, a); break;
+        default: DQNX_LAUNCH((k_dw_adam16<8, 8, 1>), grid, dim3(512), 0, s, a); break;
     }
     DQNX_HIP_CHECK(hipGetLastError());
     return DQNX_OK;
@@ -1359,9 +1359,9 @@ static void launch_fwd_gather(const FwdArgs& a, dim3 grid, hipStream_t s) {
     bool u = VECB && !a.p[0].phys && a.K % 4 == 0 && route_knob("DQNX_FWD_ULOAD", 0) != 0;
     for (int z = 0; z < a.nprob; z++)
         u = u && a.p[z].lda % 4 == 0 && ((uintptr_t)a.p[z].A & 15) == 0 && ((uintptr_t)a.p[z].W & 15) == 0;
-    if (a.p[0].phys) hipLaunchKernelGGL((k_linear_fwd<ACT, VECB, true>), grid, dim3(256), 0, s, a);
-    else if (u) hipLaunchKernelGGL((k_linear_fwd<ACT, true, false, true>), grid, dim3(256), 0, s, a);
-    else hipLaunchKernelGGL((k_linear_fwd<ACT, VECB, false>), grid, dim3(256), 0, s, a);
+    if (a.p[0].phys) DQNX_LAUNCH((k_linear_fwd<ACT, VECB, true>), grid, dim3(256), 0, s, a);
+    else if (u) DQNX_LAUNCH((k_linear_fwd<ACT, true, false, true>), grid, dim3(256), 0, s, a);
+    else DQNX_LAUNCH((k_linear_fwd<ACT, VECB, false>), grid, dim3(256), 0, s, a);
 }
 
 int launch_linear_fwd(const FwdArgs& args, int nprob, int act, bool vecb, hipStream_t s) {
@@ -1396,11 +1396,11 @@ static void launch_fwd_big_t(const FwdArgs& a, int act, bool vecb, hipStream_t s
     const int tiles = ((a.N + BN - 1) / BN) * ((a.M + BM - 1) / BM) * a.nprob;
     const dim3 grid(tiles * a.ksplit);
     if (act == DQNX_ACT_RELU) {
-        if (vecb) hipLaunchKernelGGL((k_linear_fwd_big<DQNX_ACT_RELU, true, BM, BN, WM>), grid, dim3(256), 0, s, a);
-        else hipLaunchKernelGGL((k_linear_fwd_big<DQNX_ACT_RELU, false, BM, BN, WM>), grid, dim3(256), 0, s, a);
+        if (vecb) DQNX_LAUNCH((k_linear_fwd_big<DQNX_ACT_RELU, true, BM, BN, WM>), grid, dim3(256), 0, s, a);
+        else DQNX_LAUNCH((k_linear_fwd_big<DQNX_ACT_RELU, false, BM, BN, WM>), grid, dim3(256), 0, s, a);
     } else {
-        if (vecb) hipLaunchKernelGGL((k_linear_fwd_big<DQNX_ACT_ELU, true, BM, BN, WM>), grid, dim3(256), 0, s, a);
-        else hipLaunchKernelGGL((k_linear_fwd_big<DQNX_ACT_ELU, false, BM, BN, WM>), grid, dim3(256), 0, s, a);
+        if (vecb) DQNX_LAUNCH((k_linear_fwd_big<DQNX_ACT_ELU, true, BM, BN, WM>), grid, dim3(256), 0, s, a);
+        else DQNX_LAUNCH((k_linear_fwd_big<DQNX_ACT_ELU, false, BM, BN, WM>), grid, dim3(256), 0, s, a);
     }
 }
 
@@ -1443,12 +1443,12 @@ static void launch_fwd_split_t(const FwdArgs& a2, bool vecb, dim3 grid, hipStrea
     }
     // ... optionally with two passes in flight (DQNX_F1_PF=2)
     const bool pf2 = route_knob("DQNX_F1_PF", 1) == 2;   // (measured 1 us slower at the HEAD net: opt-in)
-    if (a4 && vecb && pf2) hipLaunchKernelGGL((k_linear_fwd_big<ACT, true, T, T, 2, KT, L_ROWS_KU, L_ROWS_KU, 2>), grid, dim3(256), 0, s, a2);
-    else if (a4 && b2 && pf2) hipLaunchKernelGGL((k_linear_fwd_big<ACT, false, T, T, 2, KT, L_ROWS_KU, L_ROWS_K2, 2>), grid, dim3(256), 0, s, a2);
-    else if (a4 && vecb) hipLaunchKernelGGL((k_linear_fwd_big<ACT, true, T, T, 2, KT, L_ROWS_KU, L_ROWS_KU>), grid, dim3(256), 0, s, a2);
-    else if (a4 && b2) hipLaunchKernelGGL((k_linear_fwd_big<ACT, false, T, T, 2, KT, L_ROWS_KU, L_ROWS_K2>), grid, dim3(256), 0, s, a2);
-    else if (vecb) hipLaunchKernelGGL((k_linear_fwd_big<ACT, true, T, T, 2, KT>), grid, dim3(256), 0, s, a2);
-    else hipLaunchKernelGGL((k_linear_fwd_big<ACT, false, T, T, 2, KT>), grid, dim3(256), 0, s, a2);
+    if (a4 && vecb && pf2) DQNX_LAUNCH((k_linear_fwd_big<ACT, true, T, T, 2, KT, L_ROWS_KU, L_ROWS_KU, 2>), grid, dim3(256), 0, s, a2);
+    else if (a4 && b2 && pf2) DQNX_LAUNCH((k_linear_fwd_big<ACT, false, T, T, 2, KT, L_ROWS_KU, L_ROWS_K2, 2>), grid, dim3(256), 0, s, a2);
+    else if (a4 && vecb) DQNX_LAUNCH((k_linear_fwd_big<ACT, true, T, T, 2, KT, L_ROWS_KU, L_ROWS_KU>), grid, dim3(256), 0, s, a2);
+    else if (a4 && b2) DQNX_LAUNCH((k_linear_fwd_big<ACT, false, T, T, 2, KT, L_ROWS_KU, L_ROWS_K2>), grid, dim3(256), 0, s, a2);
+    else if (vecb) DQNX_LAUNCH((k_linear_fwd_big<ACT, true, T, T, 2, KT>), grid, dim3(256), 0, s, a2);
+    else DQNX_LAUNCH((k_linear_fwd_big<ACT, false, T, T, 2, KT>), grid, dim3(256), 0, s, a2);
 }
 int launch_linear_fwd_split(const FwdArgs& args, int nprob, int act, bool vecb, hipStream_t s) {
     FwdArgs a2 = args;
@@ -1467,8 +1467,8 @@ int launch_linear_fwd_reduce(const FwdArgs& args, int nprob, int act, hipStream_
     a2.nprob = nprob;
     int64_t g = ((int64_t)args.M * args.N * nprob + 255) / 256;
     if (g > 4096) g = 4096;
-    if (act == DQNX_ACT_RELU) hipLaunchKernelGGL((k_linear_fwd_reduce<DQNX_ACT_RELU>), dim3((unsigned)g), dim3(256), 0, s, a2);
-    else hipLaunchKernelGGL((k_linear_fwd_reduce<DQNX_ACT_ELU>), dim3((unsigned)g), dim3(256), 0, s, a2);
+    if (act == DQNX_ACT_RELU) DQNX_LAUNCH((k_linear_fwd_reduce<DQNX_ACT_RELU>), dim3((unsigned)g), dim3(256), 0, s, a2);
+    else DQNX_LAUNCH((k_linear_fwd_reduce<DQNX_ACT_ELU>), dim3((unsigned)g), dim3(256), 0, s, a2);
     DQNX_HIP_CHECK(hipGetLastError());
     return DQNX_OK;
 }
@@ -1500,14 +1500,14 @@ static void launch_bwd_level_t(const BwdArgs& a, int blocks, hipStream_t s) {
     for (int p = 0; p < a.ndw; p++)
         u = u && a.dw[p].ldz % 4 == 0 && a.dw[p].ldx % 4 == 0 && ((uintptr_t)a.dw[p].dZ & 15) == 0 &&
             ((uintptr_t)a.dw[p].X & 15) == 0;
-    if (a.ts == 64 && u && vw) hipLaunchKernelGGL((k_bwd_level<ACT, true, true, 64>), dim3(blocks), dim3(256), 0, s, a);
-    else if (a.ts == 64 && u) hipLaunchKernelGGL((k_bwd_level<ACT, false, true, 64>), dim3(blocks), dim3(256), 0, s, a);
-    else if (a.ts == 64 && vw) hipLaunchKernelGGL((k_bwd_level<ACT, true, false, 64>), dim3(blocks), dim3(256), 0, s, a);
-    else if (a.ts == 64) hipLaunchKernelGGL((k_bwd_level<ACT, false, false, 64>), dim3(blocks), dim3(256), 0, s, a);
-    else if (u && vw) hipLaunchKernelGGL((k_bwd_level<ACT, true, true>), dim3(blocks), dim3(256), 0, s, a);
-    else if (u) hipLaunchKernelGGL((k_bwd_level<ACT, false, true>), dim3(blocks), dim3(256), 0, s, a);
-    else if (vw) hipLaunchKernelGGL((k_bwd_level<ACT, true>), dim3(blocks), dim3(256), 0, s, a);
-    else hipLaunchKernelGGL((k_bwd_level<ACT, false>), dim3(blocks), dim3(256), 0, s, a);
+    if (a.ts == 64 && u && vw) DQNX_LAUNCH((k_bwd_level<ACT, true, true, 64>), dim3(blocks), dim3(256), 0, s, a);
+    else if (a.ts == 64 && u) DQNX_LAUNCH((k_bwd_level<ACT, false, true, 64>), dim3(blocks), dim3(256), 0, s, a);
+    else if (a.ts == 64 && vw) DQNX_LAUNCH((k_bwd_level<ACT, true, false, 64>), dim3(blocks), dim3(256), 0, s, a);
+    else if (a.ts == 64) DQNX_LAUNCH((k_bwd_level<ACT, false, false, 64>), dim3(blocks), dim3(256), 0, s, a);
+    else if (u && vw) DQNX_LAUNCH((k_bwd_level<ACT, true, true>), dim3(blocks), dim3(256), 0, s, a);
+    else if (u) DQNX_LAUNCH((k_bwd_level<ACT, false, true>), dim3(blocks), dim3(256), 0, s, a);
+    else if (vw) DQNX_LAUNCH((k_bwd_level<ACT, true>), dim3(blocks), dim3(256), 0, s, a);
+    else DQNX_LAUNCH((k_bwd_level<ACT, false>), dim3(blocks), dim3(256), 0, s, a);
 }
 int launch_bwd_level(const BwdArgs& a, int act, hipStream_t s) {
     int blocks = a.dx_blocks;
@@ -1520,8 +1520,8 @@ int launch_bwd_level(const BwdArgs& a, int act, hipStream_t s) {
 
 template <int F>
 static void launch_head_f(const HeadArgs& a, int act, int tiles, hipStream_t s) {
-    if (act == DQNX_ACT_RELU) hipLaunchKernelGGL((k_head<DQNX_ACT_RELU, F>), dim3(tiles), dim3(256), 0, s, a);
-    else hipLaunchKernelGGL((k_head<DQNX_ACT_ELU, F>), dim3(tiles), dim3(256), 0, s, a);
+    if (act == DQNX_ACT_RELU) DQNX_LAUNCH((k_head<DQNX_ACT_RELU, F>), dim3(tiles), dim3(256), 0, s, a);
+    else DQNX_LAUNCH((k_head<DQNX_ACT_ELU, F>), dim3(tiles), dim3(256), 0, s, a);
 }
 
 bool head_supported(int F) { return F == 64 || F == 128 || F == 256; }
@@ -1582,8 +1582,8 @@ int launch_adam(const AdamArgs& a_in, hipStream_t s) {
     if (a.mtc) blocks++;   // + the sampler-cache workgroup
     if (a.pf_nidx > 0) blocks++;   // + the staged-minibatch copy
     blocks += a.pprop_wgs;         // + k_per_prop's workgroups (256 updates each)
-    if (vec) hipLaunchKernelGGL(k_adam4, dim3(blocks), dim3(256), 0, s, a);
-    else hipLaunchKernelGGL(k_adam, dim3(blocks), dim3(256), 0, s, a);
+    if (vec) DQNX_LAUNCH(k_adam4, dim3(blocks), dim3(256), 0, s, a);
+    else DQNX_LAUNCH(k_adam, dim3(blocks), dim3(256), 0, s, a);
     DQNX_HIP_CHECK(hipGetLastError());
     return DQNX_OK;
 }
@@ -1591,14 +1591,14 @@ int launch_adam(const AdamArgs& a_in, hipStream_t s) {
 int launch_soft_update(float* target, const float* p, int64_t n, float tau, float omt, hipStream_t s) {
     int blocks = (int)((n + 255) / 256);
     if (blocks > 2048) blocks = 2048;
-    hipLaunchKernelGGL(k_soft_update, dim3(blocks), dim3(256), 0, s, target, p, n, tau, omt);
+    DQNX_LAUNCH(k_soft_update, dim3(blocks), dim3(256), 0, s, target, p, n, tau, omt);
     DQNX_HIP_CHECK(hipGetLastError());
     return DQNX_OK;
 }
 
 int launch_replay_push(const PushArgs& a, hipStream_t s) {
     if (a.n <= 0) return DQNX_OK;
-    hipLaunchKernelGGL(k_replay_push, dim3(a.n), dim3(128), 0, s, a);
+    DQNX_LAUNCH(k_replay_push, dim3(a.n), dim3(128), 0, s, a);
     DQNX_HIP_CHECK(hipGetLastError());
     return DQNX_OK;
 }

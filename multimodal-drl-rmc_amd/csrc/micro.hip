@@ -743,8 +743,8 @@ int launch_micro_fwd(const MicroFwdArgs& a, hipStream_t s) {
     const dim3 grid(a.nstreams * a.groups + (a.samp_on ? 1 : 0));
     size_t lds = (size_t)a.lds_floats * 4;
     if (a.samp_on && lds < (size_t)MICRO_SAMP_LDS) lds = MICRO_SAMP_LDS;
-    if (a.nc == 3) hipLaunchKernelGGL(k_micro_fwd<3>, grid, dim3(MTH), lds, s, a);
-    else hipLaunchKernelGGL(k_micro_fwd<2>, grid, dim3(MTH), lds, s, a);
+    if (a.nc == 3) DQNX_LAUNCH(k_micro_fwd<3>, grid, dim3(MTH), lds, s, a);
+    else DQNX_LAUNCH(k_micro_fwd<2>, grid, dim3(MTH), lds, s, a);
     DQNX_HIP_CHECK(hipGetLastError());
     return DQNX_OK;
 }
@@ -903,11 +903,11 @@ int launch_micro_dx(const MicroDxArgs& a, hipStream_t s) {
     const dim3 grid(a.groups);
     const size_t lds = (size_t)a.lds_floats * 4;
     if (a.nw == 8) {
-        if (a.nc == 3) hipLaunchKernelGGL((k_micro_dx<3, 8>), grid, dim3(512), lds, s, a);
-        else hipLaunchKernelGGL((k_micro_dx<2, 8>), grid, dim3(512), lds, s, a);
+        if (a.nc == 3) DQNX_LAUNCH((k_micro_dx<3, 8>), grid, dim3(512), lds, s, a);
+        else DQNX_LAUNCH((k_micro_dx<2, 8>), grid, dim3(512), lds, s, a);
     } else {
-        if (a.nc == 3) hipLaunchKernelGGL((k_micro_dx<3, 4>), grid, dim3(256), lds, s, a);
-        else hipLaunchKernelGGL((k_micro_dx<2, 4>), grid, dim3(256), lds, s, a);
+        if (a.nc == 3) DQNX_LAUNCH((k_micro_dx<3, 4>), grid, dim3(256), lds, s, a);
+        else DQNX_LAUNCH((k_micro_dx<2, 4>), grid, dim3(256), lds, s, a);
     }
     DQNX_HIP_CHECK(hipGetLastError());
     return DQNX_OK;
@@ -1212,8 +1212,8 @@ __global__ __launch_bounds__(MTH, 2) void k_micro_dw(MicroDwArgs a) {   // 2 wav
 
 int launch_micro_dw(const MicroDwArgs& a, hipStream_t s) {
     const size_t lds = (size_t)a.lds_floats * 4;
-    if (a.nc == 3) hipLaunchKernelGGL(k_micro_dw<3>, dim3(a.wgs), dim3(MTH), lds, s, a);
-    else hipLaunchKernelGGL(k_micro_dw<2>, dim3(a.wgs), dim3(MTH), lds, s, a);
+    if (a.nc == 3) DQNX_LAUNCH(k_micro_dw<3>, dim3(a.wgs), dim3(MTH), lds, s, a);
+    else DQNX_LAUNCH(k_micro_dw<2>, dim3(a.wgs), dim3(MTH), lds, s, a);
     DQNX_HIP_CHECK(hipGetLastError());
     return DQNX_OK;
 }

@@ -496,7 +496,7 @@ int launch_per_sample(const PerSampleArgs& a, hipStream_t s) {
     if (a.Bg < 1 || a.Bg > PER_MAX_B) return set_error(DQNX_EUNSUPPORTED, "PER batch %d outside [1, %d]", a.Bg, PER_MAX_B);
     if (a.spw < 1 || a.spw > PER_SNT) return set_error(DQNX_EINVAL, "PER samples per workgroup %d", a.spw);
     const int G = (a.Bg + a.spw - 1) / a.spw;
-    hipLaunchKernelGGL(k_per_sample, dim3(G + a.rl_blocks), dim3(PER_SNT), 0, s, a);
+    DQNX_LAUNCH(k_per_sample, dim3(G + a.rl_blocks), dim3(PER_SNT), 0, s, a);
     DQNX_HIP_CHECK(hipGetLastError());
     return DQNX_OK;
 }
@@ -507,18 +507,18 @@ int launch_per_update(const PerUpdateArgs& a, hipStream_t s) {
     const int g = (a.n + PER_GT - 1) / PER_GT;
     if ((a.skip & PER_SKIP_PREP) && (a.mode != 0 || a.numpy121))
         return set_error(DQNX_EINVAL, "PER update: the prep pass is hosted only for mode 0 without numpy121");
-    if (!(a.skip & PER_SKIP_PREP)) hipLaunchKernelGGL(k_per_prep, dim3(g), dim3(PER_GT), 0, s, a);
-    hipLaunchKernelGGL(k_per_update, dim3(1), dim3(PER_NT), 0, s, a);
+    if (!(a.skip & PER_SKIP_PREP)) DQNX_LAUNCH(k_per_prep, dim3(g), dim3(PER_GT), 0, s, a);
+    DQNX_LAUNCH(k_per_update, dim3(1), dim3(PER_NT), 0, s, a);
     if (a.numpy121 && a.mode == 0) {   // float32 change / ancestor sums in update order
         int N2 = 1;
         while (N2 < a.n) N2 <<= 1;
         int depths = 0;   // internal depths 0 .. (deepest leaf depth - 1)
         while (((int64_t)1 << (depths + 1)) <= 2 * a.cap - 1) depths++;
-        hipLaunchKernelGGL(k_per_chain<true>, dim3(1), dim3(PER_CHAIN_NT), (size_t)N2 * 8, s, a);
+        DQNX_LAUNCH(k_per_chain<true>, dim3(1), dim3(PER_CHAIN_NT), (size_t)N2 * 8, s, a);
         if (depths > 0)
-            hipLaunchKernelGGL(k_per_chain<false>, dim3(depths), dim3(PER_CHAIN_NT), (size_t)N2 * 8 + (size_t)a.n * 8, s, a);
+            DQNX_LAUNCH(k_per_chain<false>, dim3(depths), dim3(PER_CHAIN_NT), (size_t)N2 * 8 + (size_t)a.n * 8, s, a);
     } else if (!(a.skip & PER_SKIP_PROP)) {
-        hipLaunchKernelGGL(k_per_prop, dim3(g), dim3(PER_GT), 0, s, a);
+        DQNX_LAUNCH(k_per_prop, dim3(g), dim3(PER_GT), 0, s, a);
     }
     DQNX_HIP_CHECK(hipGetLastError());
     return DQNX_OK;

@@ -76,7 +76,7 @@ int launch_idx_to_phys(const int32_t* idx, int32_t* phys, int shard_begin, int n
     if (rl && rl_blocks > 0) r = *rl;
     else rl_blocks = 0;
     const int pb = (n + 255) / 256;
-    hipLaunchKernelGGL(k_idx_to_phys, dim3(pb + 4 * rl_blocks), dim3(256), 0, s, idx, phys, shard_begin, n, ctrl,
+    DQNX_LAUNCH(k_idx_to_phys, dim3(pb + 4 * rl_blocks), dim3(256), 0, s, idx, phys, shard_begin, n, ctrl,
                        capacity, r, pb);
     DQNX_HIP_CHECK(hipGetLastError());
     return DQNX_OK;
@@ -150,25 +150,25 @@ int launch_sample_uniform(const SampleArgs& a_in, hipStream_t s) {
     const int lhs = lds_hash_slots(a.k);
     if (a.k <= SAMPLE_FAST_MAX_K && (a.k >= fast_min_k() || route_flag("DQNX_SAMPLER_FAST") || a.test_flags) &&
         !route_flag("DQNX_SAMPLER_OLD")) {
-        hipLaunchKernelGGL(k_sample_fast, grid, dim3(SAMPLE_FAST_NT), 0, s, a);
+        DQNX_LAUNCH(k_sample_fast, grid, dim3(SAMPLE_FAST_NT), 0, s, a);
     } else if (lhs > 0) {
         switch (lhs) {
-            case 2048: hipLaunchKernelGGL(k_sample_uniform<2048>, grid, dim3(SAMPLE_NT), 0, s, a); break;
-            case 4096: hipLaunchKernelGGL(k_sample_uniform<4096>, grid, dim3(SAMPLE_NT), 0, s, a); break;
-            case 8192: hipLaunchKernelGGL(k_sample_uniform<8192>, grid, dim3(SAMPLE_NT), 0, s, a); break;
-            default: hipLaunchKernelGGL(k_sample_uniform<16384>, grid, dim3(SAMPLE_NT), 0, s, a); break;
+            case 2048: DQNX_LAUNCH(k_sample_uniform<2048>, grid, dim3(SAMPLE_NT), 0, s, a); break;
+            case 4096: DQNX_LAUNCH(k_sample_uniform<4096>, grid, dim3(SAMPLE_NT), 0, s, a); break;
+            case 8192: DQNX_LAUNCH(k_sample_uniform<8192>, grid, dim3(SAMPLE_NT), 0, s, a); break;
+            default: DQNX_LAUNCH(k_sample_uniform<16384>, grid, dim3(SAMPLE_NT), 0, s, a); break;
         }
     } else {
         const int ghs = global_hash_slots(a.k);
         if (ghs < 0) return set_error(DQNX_EUNSUPPORTED, "sample: k=%d too large", a.k);
         if (!a.gtab) return set_error(DQNX_EINVAL, "sample: k=%d needs a global table", a.k);
         switch (ghs) {
-            case 32768: hipLaunchKernelGGL(k_sample_uniform_g<32768>, grid, dim3(SAMPLE_NT), 0, s, a); break;
-            case 65536: hipLaunchKernelGGL(k_sample_uniform_g<65536>, grid, dim3(SAMPLE_NT), 0, s, a); break;
-            case 131072: hipLaunchKernelGGL(k_sample_uniform_g<131072>, grid, dim3(SAMPLE_NT), 0, s, a); break;
-            case 262144: hipLaunchKernelGGL(k_sample_uniform_g<262144>, grid, dim3(SAMPLE_NT), 0, s, a); break;
-            case 524288: hipLaunchKernelGGL(k_sample_uniform_g<524288>, grid, dim3(SAMPLE_NT), 0, s, a); break;
-            default: hipLaunchKernelGGL(k_sample_uniform_g<1048576>, grid, dim3(SAMPLE_NT), 0, s, a); break;
+            case 32768: DQNX_LAUNCH(k_sample_uniform_g<32768>, grid, dim3(SAMPLE_NT), 0, s, a); break;
+            case 65536: DQNX_LAUNCH(k_sample_uniform_g<65536>, grid, dim3(SAMPLE_NT), 0, s, a); break;
+            case 131072: DQNX_LAUNCH(k_sample_uniform_g<131072>, grid, dim3(SAMPLE_NT), 0, s, a); break;
+            case 262144: DQNX_LAUNCH(k_sample_uniform_g<262144>, grid, dim3(SAMPLE_NT), 0, s, a); break;
+            case 524288: DQNX_LAUNCH(k_sample_uniform_g<524288>, grid, dim3(SAMPLE_NT), 0, s, a); break;
+            default: DQNX_LAUNCH(k_sample_uniform_g<1048576>, grid, dim3(SAMPLE_NT), 0, s, a); break;
         }
     }
     DQNX_HIP_CHECK(hipGetLastError());

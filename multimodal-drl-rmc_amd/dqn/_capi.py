@@ -89,7 +89,7 @@ EXPORTS = [
     "dqnx_params_modified", "dqnx_dp_bucket_count", "dqnx_dp_bucket_info", "dqnx_learn_step_bucket",
     "dqnx_apply_grads_bucket", "dqnx_ctrl_get_async", "dqnx_rng_sample_words", "dqnx_rng_advance",
     "dqnx_agent_stage_rng", "dqnx_agent_launch", "dqnx_agent_readback", "dqnx_act_host_scratch_bytes",
-    "dqnx_act_host", "dqnx_agent_learn_mt",
+    "dqnx_act_host", "dqnx_agent_learn_mt", "dqnx_agent_quiesce",
 ]
 
 GIL_HELD = ("dqnx_agent_learn_mt",)   # entry points called with the GIL held (see lib())
@@ -166,6 +166,7 @@ def lib():
         "dqnx_agent_launch": ([vp, I32, vp], ctypes.c_int),
         "dqnx_agent_learn_mt": ([vp, vp, vp, I32, vp, P(I64)], ctypes.c_int),
         "dqnx_agent_readback": ([vp, I32, vp], ctypes.c_int),
+        "dqnx_agent_quiesce": ([vp], ctypes.c_int),
         "dqnx_act_host_scratch_bytes": ([P(NetDesc), I32], ctypes.c_uint64),
         "dqnx_act_host": ([P(NetDesc), vp, vp, I32, vp, vp, ctypes.c_uint64, vp], ctypes.c_int),
     }

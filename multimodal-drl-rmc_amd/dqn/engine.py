@@ -238,6 +238,7 @@ class LearnEngine:
         h = ctypes.c_void_p()
         C.check(self.L.dqnx_engine_create(ctypes.byref(cfg), ctypes.byref(h)), "dqnx_engine_create")
         self.h = h
+        self._ag_unread = False   # an agent step's control-block readback not yet consumed
         nbytes = ctypes.c_uint64()
         C.check(self.L.dqnx_engine_arena_bytes(h, ctypes.byref(nbytes)), "arena_bytes")
         self.arena = torch.zeros(int(nbytes.value), dtype=torch.uint8, device=self.device)
@@ -415,6 +416,7 @@ class LearnEngine:
     def agent_launch(self, soft_update: bool = False) -> None:
         C.check(self.L.dqnx_agent_launch(self.h, C.STEP_SOFT_UPDATE if soft_update else 0, self.stream()),
                 "agent_launch")
+        self._ag_unread = True
         if self.cfg.algo == C.DQNX_ALGO_PER_DOUBLE:   # every PER learn step samples: step += n_env
             self.agent_step += self.cfg.n_env
 
@@ -424,8 +426,13 @@ class LearnEngine:
         as agent_launch does.  Returns the words consumed."""
         w = C.I64()
         flags = (C.AGENT_LAUNCH if launch else 0) | (C.STEP_SOFT_UPDATE if soft_update else 0)
+        if launch and self._ag_unread:
+            # the previous step's control block is still unread: wait for it here, through the CDLL
+            # binding (GIL released), not inside dqnx_agent_learn_mt (GIL held for random._inst)
+            C.check(self.L.dqnx_agent_quiesce(self.h), "agent_quiesce")
         C.check(self.L.dqnx_agent_learn_mt(self.h, mt_addr, pos_addr, flags, self.stream(), ctypes.byref(w)),
                 "agent_learn_mt")
+        self._ag_unread = self._ag_unread or launch
         return int(w.value)
 
     def agent_readback(self, wait: bool):
@@ -437,7 +444,10 @@ class LearnEngine:
             out = self._ag_ctrl = C.Ctrl()
         rc = self.L.dqnx_agent_readback(self.h, 1 if wait else 0, ctypes.byref(out))
         if rc == 0:
+            if wait:   # (nothing pending)
+                self._ag_unread = False
             return None
+        self._ag_unread = False
         if rc == C.DQNX_EDEVICE:
             if out.error:
                 raise_device_error(out.error)

@@ -147,7 +147,7 @@ def make_agent(agent_mod, algo, nn_conf_func, obs_dim, batch, buffer, lr=1e-4, s
 
 
 def gen_learn(agent_mod, nn_conf_func, tag, spec_fn, obs_dim, batch, buffer, n_fill, steps, seed,
-              algos, full_weights=True, stride=1):
+              algos, full_weights=True, stride=1, full_tree=False):
     for algo in algos:
         ag = make_agent(agent_mod, algo, nn_conf_func, obs_dim, batch, buffer, seed=seed)
         spec = spec_fn(O.algo_spec_head(algo))
@@ -235,7 +235,8 @@ def gen_learn(agent_mod, nn_conf_func, tag, spec_fn, obs_dim, batch, buffer, n_f
             out["isw"] = np.stack(rec["isw"])
             out["absd"] = np.stack(rec["absd"])
             tree = ag.replay_memory_buffer.replay_buffer
-            out["tree"] = tree.tree.copy() if len(tree.tree) <= 70000 else tree.tree[::stride].copy()
+            out["tree"] = tree.tree.copy() if (full_tree or len(tree.tree) <= 70000) else tree.tree[::stride].copy()
+            out["tree_full"] = np.bool_(len(out["tree"]) == len(tree.tree))
             out["tree_max_idx"] = np.int64(tree.max_priority_index)
             out["tree_min_idx"] = np.int64(tree.min_priority_index)
         keys = list(online.keys())
@@ -293,7 +294,8 @@ def gen_sumtree(sumtree_mod):
 
 def main():
     """python make_golden.py [name ...]: regenerate every fixture, or only the named groups
-    (sampler, np_uniform, sumtree, mlp14, mlp284, hybrid284, mlp284b1024, mlp284b4096, mlp284b8192)."""
+    (sampler, np_uniform, sumtree, mlp14, mlp284, hybrid284, mlp284b1024, mlp284b4096, mlp284b8192,
+    mlp284long1024, mlp284long8192)."""
     only = set(sys.argv[1:])
 
     def want(name):
@@ -333,6 +335,17 @@ def main():
         gen_learn(agent_mod, mlp_cfg.network_config, "mlp284b8192", mlp284, 284,
                   batch=8192, buffer=40000, n_fill=40000, steps=2, seed=23,
                   algos=["PerDuelingDoubleDQNAgent"], full_weights=False, stride=5)
+    # longer prioritised runs (8 learn steps each, the full SumTree kept): every step's sampled leaves
+    # and the final tree pin the engine's float32 priority power over many dependent tree updates
+    # (the reference's np.power here is numpy's SVML path; libdqnx computes the correctly rounded powf)
+    if want("mlp284long1024"):
+        gen_learn(agent_mod, mlp_cfg.network_config, "mlp284long1024", mlp284, 284,
+                  batch=1024, buffer=20000, n_fill=20000, steps=8, seed=31,
+                  algos=["PerDuelingDoubleDQNAgent"], full_weights=False, stride=5, full_tree=True)
+    if want("mlp284long8192"):
+        gen_learn(agent_mod, mlp_cfg.network_config, "mlp284long8192", mlp284, 284,
+                  batch=8192, buffer=40000, n_fill=40000, steps=8, seed=32,
+                  algos=["PerDuelingDoubleDQNAgent"], full_weights=False, stride=5, full_tree=True)
 
 
 if __name__ == "__main__":

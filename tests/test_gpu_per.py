@@ -361,3 +361,41 @@ def test_gpu_per_fused_update_bit_identical(monkeypatch, batch, compute, cap, wo
         assert np.array_equal(t0, t1) and mx0 == mx1 and mn0 == mn1, mode
         assert torch.equal(e0.batch_idx, e1.batch_idx) and torch.equal(e0.is_weights, e1.is_weights), mode
         assert torch.equal(e0.params, e1.params) and torch.equal(e0.target_params, e1.target_params), mode
+
+
+PER_LONG = ["learn_mlp284long1024_PerDuelingDoubleDQNAgent", "learn_mlp284long8192_PerDuelingDoubleDQNAgent"]
+
+
+@pytest.mark.parametrize("golden", PER_LONG)
+def test_gpu_per_long_golden(golden):
+    """The reference's own 8-step prioritised runs (tests/golden, make_golden.py mlp284long1024 /
+    mlp284long8192: B = 1024 and configs[4]'s B = 8192, fp32, full SumTree kept): every step's sampled
+    leaves compared with ==, the numpy RNG state after the run with ==, the final tree's max / min leaf
+    indices with ==.  The tree VALUES are compared to rtol 1e-4: libdqnx's |delta| comes from its own
+    fp32 forward (summation order differs from torch CPU by ~1e-7 relative), so the float32 priorities
+    it writes may differ by an ulp from the reference's, and the IS weights fed back through the
+    training carry that on (the oracle with the correctly rounded power drifts as far from the same
+    run: tests/test_oracle.py::test_oracle_per_long_tree_and_cr_pow).  R:dqn/replay_memory.py:69-98."""
+    from dqn import engine as E
+    z = np.load(os.path.join(GOLDEN, golden + ".npz"))
+    assert bool(z["tree_full"])
+    batch, cap, seed = int(z["batch"]), int(z["buffer"]), int(z["seed"])
+    spec = O.mlp_spec(int(z["obs_dim"]), 8, "dueling")
+    eng = E.LearnEngine(E.mlp_spec(int(z["obs_dim"]), 8, "dueling"), ALGO, batch, cap)
+    eng.load_params(O.reference_init(spec, seed))
+    eng.push(*O.synth_transitions(int(z["n_fill"]), int(z["obs_dim"]), 8, seed=seed + 100))
+    eng.set_rng(0, z["py_state_in"])
+    eng.set_rng(1, z["np_state_in"])
+    moved = []
+    for s in range(int(z["steps"])):
+        eng.learn_step(soft_update=True)
+        torch.cuda.synchronize()
+        eng.check_device_error()
+        got = eng.batch_idx.cpu().numpy().astype(np.int64) + cap - 1
+        moved.append(int((got != z["pos"][s]).sum()))
+        assert abs(eng.loss() - z["loss"][s]) <= 1e-5 * max(1.0, abs(z["loss"][s])), (s, eng.loss(), z["loss"][s])
+    assert moved == [0] * int(z["steps"]), f"sampled leaves differing from the reference run, per step: {moved}"
+    assert np.array_equal(eng.get_rng(1), z["np_state_out"])
+    tree, mx, mn = tree_state(eng)
+    assert (mx, mn) == (int(z["tree_max_idx"]), int(z["tree_min_idx"]))
+    np.testing.assert_allclose(tree, z["tree"], rtol=1e-4, atol=0)

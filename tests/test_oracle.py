@@ -173,3 +173,35 @@ def test_bf16_oracle_learn_close_to_fp32():
     assert np.array_equal(a.positions, b.positions)
     qa, qb = a.q_online.numpy(), b.q_online.numpy()
     assert 0 < np.abs(qa - qb).max() <= 2e-2 * np.abs(qa).max()
+
+
+PER_LONG = sorted(glob.glob(os.path.join(GOLDEN, "learn_mlp284long*_PerDuelingDoubleDQNAgent.npz")))
+
+
+@pytest.mark.parametrize("path", PER_LONG, ids=[os.path.basename(p)[6:-4] for p in PER_LONG])
+def test_oracle_per_long_tree_and_cr_pow(path):
+    """The 8-step prioritised runs of the reference (make_golden.py mlp284long1024 / mlp284long8192,
+    full SumTree kept): the oracle with this host's numpy power (what the reference computed here)
+    reproduces the final tree bit for bit; with the correctly rounded float32 power that libdqnx
+    computes (oracle pow_mode "cr"), every step's sampled leaves still equal the reference run's and the
+    tree differs only by the rounding of the priorities it carries forward (R:dqn/replay_memory.py:94-98,
+    R:dqn/utils/sum_tree.py:15-32)."""
+    z = np.load(path)
+    assert bool(z["tree_full"])
+    L, _ = run_oracle_from_fixture(z)
+    assert np.array_equal(L.replay.replay_buffer.tree, z["tree"])
+    assert L.replay.replay_buffer.max_priority_index == int(z["tree_max_idx"])
+    assert L.replay.replay_buffer.min_priority_index == int(z["tree_min_idx"])
+    # the same run with the correctly rounded power
+    torch.set_num_threads(1)
+    spec, seed = _spec_for(z), int(z["seed"])
+    Lc = O.OracleLearner(spec, str(z["algo"]), int(z["batch"]), int(z["buffer"]), seed=seed,
+                         params=O.reference_init(spec, seed), per_pow="cr")
+    O.fill_replay(Lc, *O.synth_transitions(int(z["n_fill"]), int(z["obs_dim"]), 8, seed=seed + 100))
+    Lc.py_state, Lc.np_state = z["py_state_in"].copy(), z["np_state_in"].copy()
+    for s in range(int(z["steps"])):
+        r = Lc.train_step()
+        assert np.array_equal(r.positions, z["pos"][s]), f"cr pow moved a sampled leaf at step {s}"
+    assert np.array_equal(Lc.np_state, z["np_state_out"])
+    t = Lc.replay.replay_buffer.tree
+    np.testing.assert_allclose(t, z["tree"], rtol=1e-4, atol=0)
