@@ -549,8 +549,13 @@ def roofline_of(args, kern, batch_tag, incontext_us=None, stats_name=None, step_
     same workload; `traffic_ratio` = traffic / algorithmic bytes (per launch and, over every kernel of
     the step the passes cover, per step).  `rocprof` = the committed kernel-trace average of the same
     kernel (profiles/<round>/kernel_stats_<stats_name>.csv) and the fraction it gives."""
-    nm, us, fl, by = kern
+    nm, us_live, fl, by = kern
     peak_mfma = PEAK_BF16_MFMA_TFLOPS if args.compute == "bf16" else PEAK_FP32_MFMA_TFLOPS
+    # the duration behind achieved / frac (VERDICT r5 #1: reproducible from profiles/): the committed
+    # rocprofv3 kernel-trace average of this workload's kernel when there is one, else the live
+    # event-bound measurement; both are on the line (avg_us_events, frac_live)
+    rp_us, rp_path = rocprof_avg_us(stats_name, nm) if stats_name else (None, None)
+    us = rp_us or us_live
     pmc = pmc_traffic(args, batch_tag)
     traffic = pmc.get(nm, pmc.get(nm.split("+")[0]))
     sec = us * 1e-6
@@ -566,7 +571,10 @@ def roofline_of(args, kern, batch_tag, incontext_us=None, stats_name=None, step_
     # DESIGN.md section 3), and `frac` says how far below it runs
     hbm_measured_frac = ((traffic or by) / sec / 1e9) / PEAK_HBM_GBS
     mfma_bound = fl > 0 and hbm_measured_frac < 0.5
-    common = {"traffic": traffic, "kernel": nm, "avg_us": us, "avg_us_source": "HIP events around the launch",
+    common = {"traffic": traffic, "kernel": nm, "avg_us": us,
+              "avg_us_source": (f"rocprofv3 --kernel-trace --stats average ({rp_path})" if rp_us else
+                                "HIP events bound to the launch's dispatch (kernel_event_us)"),
+              "avg_us_events": us_live,
               "algorithmic_flops": fl, "algorithmic_bytes": by,
               "traffic_ratio": (traffic / by) if (traffic and by) else None,
               "mfma_frac": mfma_frac, "hbm_frac": hbm_frac, "hbm_measured_frac": hbm_measured_frac,
@@ -582,12 +590,10 @@ def roofline_of(args, kern, batch_tag, incontext_us=None, stats_name=None, step_
             common["algorithmic_bytes_step"] = b
             common["traffic_ratio_step"] = t / b if b else None
             common["traffic_step_kernels"] = [n for n, _ in covered]
-    if stats_name:
-        rp_us, rp_path = rocprof_avg_us(stats_name, nm)
-        if rp_us:
-            rp_frac = (fl / (rp_us * 1e-6) / 1e12 / peak_mfma) if mfma_bound else (by / (rp_us * 1e-6) / 1e9 / PEAK_HBM_GBS)
-            common["rocprof"] = {"avg_us": rp_us, "frac": rp_frac, "file": rp_path,
-                                 "live_over_rocprof": us / rp_us}
+    frac_live = (fl / (us_live * 1e-6) / 1e12 / peak_mfma) if mfma_bound else (by / (us_live * 1e-6) / 1e9 / PEAK_HBM_GBS)
+    common["frac_live"] = frac_live
+    if rp_us:
+        common["rocprof"] = {"avg_us": rp_us, "file": rp_path, "events_over_rocprof": us_live / rp_us}
     if mfma_bound:
         return dict({"bound": "mfma", "achieved": mfma_ach, "peak": peak_mfma, "unit": "TFLOP/s",
                      "frac": mfma_frac}, **common)

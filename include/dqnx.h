@@ -150,6 +150,10 @@ typedef struct dqnx_ctrl {
 #define DQNX_DEVERR_SAMPLE_TOO_LARGE 1   /* random.sample: k > n (ValueError) */
 #define DQNX_DEVERR_EMPTY_TREE 2         /* PER sample with total priority 0 */
 #define DQNX_DEVERR_PER_HANDOFF 3        /* internal: a PER update hand-off inside one launch timed out */
+/* internal: a write outside its range was skipped (bounds checks on the DP-bucket write paths) */
+#define DQNX_DEVERR_BOUNDS_ADAM_WIDE 16  /*   k_adam4 wide path: a float4 outside [e0, n_params) of the launch */
+#define DQNX_DEVERR_BOUNDS_ADAM_PERM 17  /*   k_adam4 wide path: a permuted conv-weight copy outside the range */
+#define DQNX_DEVERR_BOUNDS_MICRO_DW 18   /*   k_micro_dw: a split-K slab tile outside its conv's slabs */
 
 /* ---- engine lifetime --------------------------------------------------------------- */
 typedef struct dqnx_engine dqnx_engine;
@@ -379,6 +383,22 @@ int dqnx_agent_readback(dqnx_engine* e, int32_t wait, dqnx_ctrl* out);
  *   calls it, with the GIL released, before a dqnx_agent_learn_mt (GIL held) whose previous readback
  *   is still unread, so no other Python thread is blocked for the length of a GPU wait. */
 int dqnx_agent_quiesce(dqnx_engine* e);
+/* dqnx_agent_choose: Agent.choose_actions(obses) (R:dqn/agent.py:92-99) in ONE call, MLP nets on the
+ *   engine's online parameters: the greedy actions of the n HOST rows at obs_host (dqnx_act_host's
+ *   launch: the advantage stream for dueling nets, R:dqn/network.py:110-117), and -- while the acting
+ *   kernel runs -- for every env i in order: u = random.random() from the caller's LIVE MT19937 (mt =
+ *   its 624 words, *pos its index, advanced in place as dqnx_agent_learn_mt does: CPython's
+ *   genrand_res53, 2 words); if u <= epsilon, actions[i] = random.randint(0, n_actions - 1)
+ *   (_randbelow: getrandbits(n_actions.bit_length()) redrawn while >= n_actions).  Then the wait for
+ *   the kernel and the last agent step's control-block checks (as dqnx_agent_readback(wait = 1)).
+ *   `scratch` as dqnx_act_host's (dqnx_act_host_scratch_bytes(&cfg.net, n)); n <= DQNX_CHOOSE_MAX_ENVS.
+ *   flags & DQNX_CHOOSE_GIL_HELD: the caller holds the Python GIL (it must, for the in-place generator
+ *   update); the GIL is released around the GPU wait (PyEval_SaveThread / PyEval_RestoreThread of the
+ *   running interpreter). */
+#define DQNX_CHOOSE_MAX_ENVS 256
+#define DQNX_CHOOSE_GIL_HELD 0x1
+int dqnx_agent_choose(dqnx_engine* e, const float* obs_host, int32_t n, double epsilon, uint32_t* mt, int32_t* pos,
+                      int32_t* actions_out, void* scratch, uint64_t scratch_bytes, int32_t flags, void* stream);
 uint64_t dqnx_act_host_scratch_bytes(const dqnx_net_desc* net, int32_t n);
 int dqnx_act_host(const dqnx_net_desc* net, const float* params, const float* obs_host, int32_t n,
                   int32_t* actions_host, void* scratch, uint64_t scratch_bytes, void* stream);

@@ -8,6 +8,7 @@
 #include <string.h>
 
 #include <chrono>
+#include <dlfcn.h>
 #include <cmath>
 #include <functional>
 #include <map>
@@ -410,6 +411,8 @@ struct dqnx_engine {
     uint64_t total = 0;
     // workspace sub-regions (byte offsets from the arena base)
     uint64_t ws_phys = 0, ws_pool = 0, ws_xobs = 0, ws_head_part = 0, ws_loss_part = 0, ws_stage = 0;
+    uint64_t ws_ring16[2] = {0, 0};   // bf16 engines: [cap][stride16] bf16 copies of obs / next_obs
+    int stride16 = 0;
     uint64_t ws_npc = 0;   // numpy MT block cache (PER, fused plan)
     uint64_t ws_adam_tab = 0, ws_stamps = 0, ws_dhead = 0, ws_raw = 0, ws_trans = 0, ws_gtab = 0, ws_mtc = 0, ws_per_ticket = 0, ws_per_wl = 0, ws_per_wp = 0, ws_per_winit = 0, ws_per_last = 0, ws_per_wchg = 0;
     // fused plan: fragment-blocked weight copies [online fwd | target fwd | online chain] per layer
@@ -546,6 +549,11 @@ int layout(dqnx_engine* e) {
                         ? mt_cache_target_blocks(e->Bs, c.capacity) : 0;
     e->ws_mtc = sub((uint64_t)mt_cache_words() * 4);   // always valid for the sampler's loads
     e->ws_xobs = sub((uint64_t)e->Bl * e->stride * 4);
+    if (e->bwd_plan == 2 && e->fplan.bf16) {   // the bf16 forward gathers these (csrc/fused.hip)
+        e->stride16 = (c.net.obs_dim + 7) & ~7;
+        e->ws_ring16[0] = sub(cap * e->stride16 * 2);
+        e->ws_ring16[1] = sub(cap * e->stride16 * 2);
+    }
     e->ws_H.assign(L, 0);
     e->ws_dZ.assign(L, 0);
     e->ws_part.assign(L, 0);
@@ -998,6 +1006,9 @@ void build_fused_steps(dqnx_engine* e, int flags, int32_t* idx, int32_t* phys, s
         fa.ring_obs = at<float>(e, e->off[DQNX_BUF_RING_OBS]);
         fa.ring_next = at<float>(e, e->off[DQNX_BUF_RING_NEXT_OBS]);
         fa.ring_stride = e->stride;
+        fa.ring16_obs = e->stride16 ? at<uint16_t>(e, e->ws_ring16[0]) : nullptr;
+        fa.ring16_next = e->stride16 ? at<uint16_t>(e, e->ws_ring16[1]) : nullptr;
+        fa.stride16 = e->stride16;
         fa.phys = phys;
         fa.xcopy = at<float>(e, e->ws_xobs);
         for (int l = 0; l < L; l++) fa.H[l] = at<float>(e, e->ws_H[l]);   // stream-0 third of [3][Bl][w]
@@ -2095,6 +2106,7 @@ std::vector<KStep> build_learn_steps(dqnx_engine* e, int key) {
         MicroDwArgs da = e->micro_dw;
         da.ring_obs = ring_obs;
         da.stamps = at<int64_t>(e, e->ws_stamps);
+        da.err = &ctrl_of(e)->error;
         da.phys = phys;
         da.ring_stride = e->stride;
         da.macro_len = np.macro_len;
@@ -3073,6 +3085,9 @@ int dqnx_replay_push(dqnx_engine* e, const float* obs, const int32_t* act, const
         pa.ring_rew = at<float>(e, e->off[DQNX_BUF_RING_REW]);
         pa.ring_done = at<float>(e, e->off[DQNX_BUF_RING_DONE]);
         pa.ctrl = ctrl_of(e);
+        pa.ring16_obs = e->stride16 ? at<uint16_t>(e, e->ws_ring16[0]) : nullptr;
+        pa.ring16_next = e->stride16 ? at<uint16_t>(e, e->ws_ring16[1]) : nullptr;
+        pa.stride16 = e->stride16;
         if (m > cap) {
             // only the last `cap` rows survive; push them alone
             const int skip = (int)(m - cap);
@@ -4005,9 +4020,22 @@ uint64_t dqnx_act_host_scratch_bytes(const dqnx_net_desc* net, int32_t n) {
     return a + ((uint64_t)n * net->obs_dim * 4 + 255) / 256 * 256 + ((uint64_t)n * 4 + 255) / 256 * 256;
 }
 
-int dqnx_act_host(const dqnx_net_desc* net, const float* params, const float* obs_host, int32_t n,
-                  int32_t* actions_host, void* scratch, uint64_t scratch_bytes, void* stream) {
-    if (!net || (n > 0 && (!params || !obs_host || !actions_host || !scratch))) return set_error(DQNX_EINVAL, "bad argument");
+// dqnx_act_host in two halves: the launch (obs into the pinned block, one acting launch sequence) and
+// the wait (the completion word polled, or the stream synchronised), with the host free in between
+// (dqnx_agent_choose draws the epsilon-greedy words there)
+struct ActHostCall {
+    char* pin = nullptr;
+    int32_t* pa = nullptr;
+    volatile uint32_t* flag = nullptr;
+    uint32_t want_seq = 0;
+    bool signals = false, direct = false;
+    int32_t n = 0;
+    hipStream_t s = nullptr;
+};
+
+static int act_host_launch(const dqnx_net_desc* net, const float* params, const float* obs_host, int32_t n,
+                           void* scratch, uint64_t scratch_bytes, void* stream, ActHostCall& c) {
+    if (!net || (n > 0 && (!params || !obs_host || !scratch))) return set_error(DQNX_EINVAL, "bad argument");
     if (n <= 0) return n == 0 ? DQNX_OK : set_error(DQNX_EINVAL, "n < 0");
     const uint64_t need = dqnx_act_host_scratch_bytes(net, n);
     if (!need) return set_error(DQNX_EUNSUPPORTED, "dqnx_act_host: network not supported by the acting kernel");
@@ -4039,45 +4067,143 @@ int dqnx_act_host(const dqnx_net_desc* net, const float* params, const float* ob
         DQNX_HIP_CHECK(hipHostMalloc((void**)&pin, want, hipHostMallocCoherent));
         pin_bytes = want;
     }
+    c.pin = pin;
+    c.n = n;
+    c.s = s;
+    c.pa = (int32_t*)(pin + (size_t)n * net->obs_dim * 4);
+    memcpy(pin, obs_host, (size_t)n * net->obs_dim * 4);
     if (net->kind == DQNX_NET_MLP) {
         // one launch: the acting kernel reads the obs from and writes the actions to the pinned,
         // fine-grained block in place (no copy calls) and then a completion word, which the host
         // polls instead of synchronising the stream (the wake-up of a stream synchronisation costs
         // more than the kernel); a kernel that never signals ends the poll after ~0.5 s, and the
         // stream synchronisation then reports its error
-        memcpy(pin, obs_host, (size_t)n * net->obs_dim * 4);
-        int32_t* pa = (int32_t*)(pin + (size_t)n * net->obs_dim * 4);
-        volatile uint32_t* flag = (volatile uint32_t*)(pin + flag_at);
-        const uint32_t want_seq = ++seq ? seq : ++seq;   // (never 0)
-        *flag = 0;   // (a grown or reused block never holds a stale word, whatever its sequence)
-        bool signals = false;
-        int rc = act_impl(net, params, (const float*)pin, n, pa, nullptr, act_sc, act_bytes, stream,
-                          (uint32_t*)(pin + flag_at), want_seq, &signals);
-        if (rc) return rc;
-        // poll only a launch that stores the word (one row group); any other waits on the stream
-        const bool polled = signals && route_knob("DQNX_ACT_POLL", 1) != 0;
-        bool seen = false;
-        if (polled) {
-            const auto t0 = std::chrono::steady_clock::now();
-            for (uint64_t it = 0;; it++) {
-                if (__atomic_load_n(flag, __ATOMIC_ACQUIRE) == want_seq) { seen = true; break; }
-                if ((it & 1023) == 1023 && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(500)) break;
-                __builtin_ia32_pause();
-            }
-        }
-        if (!seen) DQNX_HIP_CHECK(hipStreamSynchronize(s));
-        memcpy(actions_host, pa, (size_t)n * 4);
-        return DQNX_OK;
+        c.direct = true;
+        c.flag = (volatile uint32_t*)(pin + flag_at);
+        c.want_seq = ++seq ? seq : ++seq;   // (never 0)
+        *c.flag = 0;   // (a grown or reused block never holds a stale word, whatever its sequence)
+        return act_impl(net, params, (const float*)pin, n, c.pa, nullptr, act_sc, act_bytes, stream,
+                        (uint32_t*)(pin + flag_at), c.want_seq, &c.signals);
     }
-    memcpy(pin, obs_host, (size_t)n * net->obs_dim * 4);
     DQNX_HIP_CHECK(hipMemcpyAsync(d_obs, pin, (size_t)n * net->obs_dim * 4, hipMemcpyHostToDevice, s));
     int rc = act_impl(net, params, d_obs, n, d_act, nullptr, act_sc, act_bytes, stream, nullptr, 0);
     if (rc) return rc;
-    int32_t* pa = (int32_t*)(pin + (size_t)n * net->obs_dim * 4);
-    DQNX_HIP_CHECK(hipMemcpyAsync(pa, d_act, (size_t)n * 4, hipMemcpyDeviceToHost, s));
-    DQNX_HIP_CHECK(hipStreamSynchronize(s));
-    memcpy(actions_host, pa, (size_t)n * 4);
+    DQNX_HIP_CHECK(hipMemcpyAsync(c.pa, d_act, (size_t)n * 4, hipMemcpyDeviceToHost, s));
     return DQNX_OK;
+}
+
+static int act_host_wait(ActHostCall& c) {
+    if (c.n <= 0) return DQNX_OK;
+    // poll only a launch that stores the word (one row group); any other waits on the stream
+    bool seen = false;
+    if (c.direct && c.signals && route_knob("DQNX_ACT_POLL", 1) != 0) {
+        const auto t0 = std::chrono::steady_clock::now();
+        for (uint64_t it = 0;; it++) {
+            if (__atomic_load_n(c.flag, __ATOMIC_ACQUIRE) == c.want_seq) { seen = true; break; }
+            if ((it & 1023) == 1023 && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(500)) break;
+            __builtin_ia32_pause();
+        }
+    }
+    if (!seen) DQNX_HIP_CHECK(hipStreamSynchronize(c.s));
+    return DQNX_OK;
+}
+
+int dqnx_act_host(const dqnx_net_desc* net, const float* params, const float* obs_host, int32_t n,
+                  int32_t* actions_host, void* scratch, uint64_t scratch_bytes, void* stream) {
+    if (n > 0 && !actions_host) return set_error(DQNX_EINVAL, "bad argument");
+    ActHostCall c;
+    int rc = act_host_launch(net, params, obs_host, n, scratch, scratch_bytes, stream, c);
+    if (rc || n <= 0) return rc;
+    rc = act_host_wait(c);
+    if (rc) return rc;
+    memcpy(actions_host, c.pa, (size_t)n * 4);
+    return DQNX_OK;
+}
+
+// The GIL, when the caller holds it (DQNX_CHOOSE_GIL_HELD): released around the GPU wait through the
+// interpreter's own PyEval_SaveThread / PyEval_RestoreThread, looked up in the process (no link-time
+// dependency on libpython; absent outside a Python process, where the flag is not passed)
+struct GilRelease {
+    void* ts = nullptr;
+    void (*restore)(void*) = nullptr;
+    explicit GilRelease(bool held) {
+        if (!held) return;
+        static void* (*save_fn)() = (void* (*)())dlsym(RTLD_DEFAULT, "PyEval_SaveThread");
+        static void (*restore_fn)(void*) = (void (*)(void*))dlsym(RTLD_DEFAULT, "PyEval_RestoreThread");
+        if (save_fn && restore_fn) {
+            restore = restore_fn;
+            ts = save_fn();
+        }
+    }
+    ~GilRelease() {
+        if (restore) restore(ts);
+    }
+};
+
+// CPython's random.random() (genrand_res53) and randint(0, m - 1) = randrange(m) = _randbelow(m)
+// (getrandbits(m.bit_length()) redrawn while >= m, Lib/random.py), on the caller's live MT19937
+static inline uint32_t py_mt_next(uint32_t* w, int32_t* pos) {
+    if (*pos >= 624) {
+        for (int i = 0; i < 624; i++) {   // CPython genrand_uint32's regeneration, in index order
+            const uint32_t y = (w[i] & 0x80000000u) | (w[(i + 1) % 624] & 0x7fffffffu);
+            w[i] = w[(i + 397) % 624] ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
+        }
+        *pos = 0;
+    }
+    uint32_t y = w[(*pos)++];
+    y ^= y >> 11;
+    y ^= (y << 7) & 0x9d2c5680u;
+    y ^= (y << 15) & 0xefc60000u;
+    return y ^ (y >> 18);
+}
+
+int dqnx_agent_choose(dqnx_engine* e, const float* obs_host, int32_t n, double epsilon, uint32_t* mt, int32_t* pos,
+                      int32_t* actions_out, void* scratch, uint64_t scratch_bytes, int32_t flags, void* stream) {
+    int rc = check_bound(e);
+    if (rc) return rc;
+    if (n < 0 || (n > 0 && (!obs_host || !actions_out)) || !mt || !pos) return set_error(DQNX_EINVAL, "bad argument");
+    if (*pos < 0 || *pos > 624) return set_error(DQNX_EINVAL, "MT position must be in [0, 624]");
+    if (n > DQNX_CHOOSE_MAX_ENVS) return set_error(DQNX_EINVAL, "n > %d environments", DQNX_CHOOSE_MAX_ENVS);
+    const float* params = at<float>(e, e->off[DQNX_BUF_PARAMS]);
+    ActHostCall c;
+    rc = act_host_launch(&e->cfg.net, params, obs_host, n, scratch, scratch_bytes, stream, c);
+    if (rc) return rc;
+    // while the acting kernel runs: R:dqn/agent.py:95-97 for every env, in env order, on the live
+    // generator (the draws do not depend on the greedy actions)
+    int32_t rnd[DQNX_CHOOSE_MAX_ENVS];
+    bool take[DQNX_CHOOSE_MAX_ENVS];
+    const uint32_t m = (uint32_t)e->cfg.net.n_actions;
+    int k = 0;
+    while (k < 32 && ((uint64_t)1 << k) <= m) k++;   // m.bit_length()
+    for (int i = 0; i < n; i++) {
+        const uint32_t a = py_mt_next(mt, pos) >> 5, b = py_mt_next(mt, pos) >> 6;
+        const double u = ((double)a * 67108864.0 + (double)b) * (1.0 / 9007199254740992.0);
+        take[i] = u <= epsilon;
+        if (take[i]) {
+            uint32_t r;
+            do {
+                r = k ? py_mt_next(mt, pos) >> (32 - k) : 0;
+            } while (r >= m && m > 0);
+            rnd[i] = (int32_t)r;
+        }
+    }
+    int prev_rc = DQNX_OK;
+    {
+        GilRelease gil((flags & DQNX_CHOOSE_GIL_HELD) != 0);
+        rc = act_host_wait(c);
+        // the last agent step's control block (its readback ran before the acting kernel on this stream)
+        if (!rc && e->ag_ctrl_live) {
+            const hipError_t q = hipEventSynchronize(e->ag_ctrl_ev);
+            if (q != hipSuccess) rc = set_hip_error(q, "hipEventSynchronize", __FILE__, __LINE__);
+        }
+    }
+    if (rc) return rc;
+    if (e->ag_ctrl_live) {
+        e->ag_ctrl_live = false;
+        prev_rc = agent_check_ctrl(e, nullptr);
+    }
+    for (int i = 0; i < n; i++) actions_out[i] = take[i] ? rnd[i] : c.pa[i];
+    return prev_rc;
 }
 
 int dqnx_debug_stamps(dqnx_engine* e, int64_t* out64, void* stream) {

@@ -54,6 +54,11 @@ template <int MR, int GW>
 __host__ __device__ constexpr int fwd_gather_slots() {
     return GW == 0 ? (16 * MR * FWD_NARROW_Q4 + FT - 1) / FT : FGQ * MR;
 }
+// bf16: slots of 8 bf16 (16 bytes) from the ring's bf16 copies, half as many
+template <int MR, int GW>
+__host__ __device__ constexpr int fwd_gather_slots16() {
+    return GW == 0 ? (16 * MR * (FWD_NARROW_Q4 / 2) + FT - 1) / FT : (FGQ * MR + 1) / 2;
+}
 // The PER tracking workgroup hosted by k_dw_bf16 must not raise the tiles' register budget: 4 items
 // per thread without the carried leaves stays within the 80 VGPRs of 6 waves / SIMD (8 items with
 // them took 96-101 VGPRs, 4 waves / SIMD, and dw_all 23 -> 27.5 us at B=8192)
@@ -331,7 +336,7 @@ __device__ __forceinline__ void wave_mma_rows(const void* As, int sa, int ngroup
 template <int ACT, int NL, bool BF, int MR, int PH, int GW>
 __global__ __launch_bounds__(FT) void k_mlp_fwd(FusedFwdArgs a) {
     constexpr int RW = 16 * MR;          // rows per workgroup
-    constexpr int GQ = fwd_gather_slots<MR, GW>();   // float4 gather slots per thread
+    constexpr int GQ = BF ? fwd_gather_slots16<MR, GW>() : fwd_gather_slots<MR, GW>();   // gather slots per thread
     constexpr int LB = PH == 2 ? 1 : 0, LE = PH == 1 ? 1 : NL;   // layers of this launch
     extern __shared__ __attribute__((aligned(16))) float lds[];
     // LDS tile b: pointer arithmetic on `lds` keeps the LDS address space visible to the
@@ -418,16 +423,23 @@ __global__ __launch_bounds__(FT) void k_mlp_fwd(FusedFwdArgs a) {
     // (0) gather the 16 ring rows -> LDS, zero beyond the batch / row; stream 0 keeps a copy.
     //     Issue order matters (vmcnt retires in order): ring slots first, then layer 1's
     //     weight stream (independent of the rows), then the dependent row loads.
+    //     bf16: the rows come from the ring's bf16 copies (the replay push rounds them as the forward
+    //     would: the same operands, half the gathered bytes, 16-byte pieces straight into the LDS tile);
+    //     stream 0's fp32 copy for the weight gradient is those values widened (k_dw_bf16 rounds them
+    //     to the same bf16 again).
     {
         const int kz = fwd_nch<BF>(a.in[0]) * (BF ? 32 : 16);   // columns multiplied
-        const int q4 = kz >> 2, rs4 = a.ring_stride >> 2;
+        constexpr int PW = BF ? 8 : 4;                            // elements per gather piece (16 bytes)
+        const int qp = kz / PW;                                   // pieces per row
+        const int rsp = BF ? (a.stride16 >> 3) : (a.ring_stride >> 2);   // pieces a ring row holds
+        const int rs4 = a.ring_stride >> 2;
         // branch-free: every slot loads (clamped row / column) and selects zero afterwards,
         // so the loads issue back to back (one phys round trip, then one ring round trip)
         if (DQNX_FUSED_ORDER == 1) stream_open(a.wblk[tgt][0], a.out[0] >> 4, fwd_nch<BF>(a.in[0]), coff >> 4, c, ws, wb, tile);
         int32_t slot[GQ];
 #pragma unroll
         for (int j = 0; j < GQ; j++) {
-            const int r = (tid + j * FT) / q4;
+            const int r = (tid + j * FT) / qp;
             slot[j] = a.phys[b0 + (r < nb ? r : nb - 1)];
         }
         // stream 0 also gathers the transition scalars for the head kernel (one contiguous
@@ -436,14 +448,19 @@ __global__ __launch_bounds__(FT) void k_mlp_fwd(FusedFwdArgs a) {
         const bool keep0 = keep && part == 0;   // one part writes the stream-0 copies
         if (keep0 && tid < nb) tslot = a.phys[b0 + tid];
         if (DQNX_FUSED_ORDER == 0) stream_open(a.wblk[tgt][0], a.out[0] >> 4, fwd_nch<BF>(a.in[0]), coff >> 4, c, ws, wb, tile);
-        float4 xv[GQ];
+        u32x4 xv[GQ];
+        const uint16_t* ring16 = BF ? ((s == 0) ? a.ring16_obs : a.ring16_next) : nullptr;
 #pragma unroll
         for (int j = 0; j < GQ; j++) {
             const int q = tid + j * FT;
-            const int r = q / q4, c4 = q - r * q4;
-            const bool ok = r < nb && c4 < rs4;
-            float4 x = ld4(ring + (int64_t)slot[j] * a.ring_stride + 4 * (ok ? c4 : 0));
-            if (!ok) x = make_float4(0.f, 0.f, 0.f, 0.f);
+            const int r = q / qp, cp = q - r * qp;
+            const bool ok = r < nb && cp < rsp;
+            u32x4 x;
+            if constexpr (BF)
+                x = *reinterpret_cast<const u32x4*>(ring16 + (int64_t)slot[j] * a.stride16 + 8 * (ok ? cp : 0));
+            else
+                x = __builtin_bit_cast(u32x4, ld4(ring + (int64_t)slot[j] * a.ring_stride + 4 * (ok ? cp : 0)));
+            if (!ok) x = u32x4{0u, 0u, 0u, 0u};
             xv[j] = x;
         }
         if (DQNX_FUSED_ORDER == 2) stream_open(a.wblk[tgt][0], a.out[0] >> 4, fwd_nch<BF>(a.in[0]), coff >> 4, c, ws, wb, tile);
@@ -453,15 +470,26 @@ __global__ __launch_bounds__(FT) void k_mlp_fwd(FusedFwdArgs a) {
 #pragma unroll
         for (int j = 0; j < GQ; j++) {
             const int q = tid + j * FT;
-            const int r = q / q4, c4 = q - r * q4;
+            const int r = q / qp, cp = q - r * qp;
             if (r < RW) {
-                if constexpr (BF)
-                    *reinterpret_cast<uint2*>(reinterpret_cast<uint16_t*>(FBUF(0)) + r * a.sx + 4 * c4) =
-                        make_uint2(bf16_pack2(xv[j].x, xv[j].y), bf16_pack2(xv[j].z, xv[j].w));
-                else
-                    *reinterpret_cast<float4*>(FBUF(0) + r * a.sx + 4 * c4) = xv[j];
-                if (keep0 && r < nb && c4 < rs4)
-                    *reinterpret_cast<float4*>(a.xcopy + (int64_t)(b0 + r) * a.ring_stride + 4 * c4) = xv[j];
+                if constexpr (BF) {
+                    *reinterpret_cast<u32x4*>(reinterpret_cast<uint16_t*>(FBUF(0)) + r * a.sx + 8 * cp) = xv[j];
+                    if (keep0 && r < nb && cp < rsp) {   // widened: bf16 -> fp32 is exact
+                        float* dst = a.xcopy + (int64_t)(b0 + r) * a.ring_stride + 8 * cp;
+                        const u32x4 w = xv[j];
+                        if (2 * cp < rs4)
+                            *reinterpret_cast<float4*>(dst) = make_float4(__uint_as_float(w.x << 16), __uint_as_float(w.x & 0xffff0000u),
+                                                                          __uint_as_float(w.y << 16), __uint_as_float(w.y & 0xffff0000u));
+                        if (2 * cp + 1 < rs4)
+                            *reinterpret_cast<float4*>(dst + 4) = make_float4(__uint_as_float(w.z << 16), __uint_as_float(w.z & 0xffff0000u),
+                                                                              __uint_as_float(w.w << 16), __uint_as_float(w.w & 0xffff0000u));
+                    }
+                } else {
+                    *reinterpret_cast<float4*>(FBUF(0) + r * a.sx + 4 * cp) = __builtin_bit_cast(float4, xv[j]);
+                    if (keep0 && r < nb && cp < rs4)
+                        *reinterpret_cast<float4*>(a.xcopy + (int64_t)(b0 + r) * a.ring_stride + 4 * cp) =
+                            __builtin_bit_cast(float4, xv[j]);
+                }
             }
         }
     }
@@ -1317,6 +1345,8 @@ int launch_fused_fwd(const FusedFwdArgs& a, int act, hipStream_t s) {
     if (a.samp_shape && (a.phase == 2 || a.samp_shape > 3 || a.samp.k > FWD_SAMPLE_MAX_K ||
                          (a.samp_shape == 1 && a.samp.k > 2048)))
         return set_error(DQNX_EUNSUPPORTED, "forward sampler workgroup: whole forward or layer-1 launch, k <= %d", FWD_SAMPLE_MAX_K);
+    if (a.bf16 && a.phase != 2 && (!a.ring16_obs || !a.ring16_next || a.stride16 % 8 || a.stride16 < a.in[0]))
+        return set_error(DQNX_EUNSUPPORTED, "bf16 forward: needs the ring's bf16 copies (16-byte rows)");
     if (a.npc && (a.samp_shape || a.phase == 2 || a.npc_blocks > NPC_MAX_BLOCKS))
         return set_error(DQNX_EUNSUPPORTED, "forward MT-cache workgroup: not with the sampler workgroup / phase 2");
     const dim3 grid(a.tiles * a.nstreams * (a.phase == 1 ? a.csplit : 1) + ((a.samp_shape || a.npc) ? 1 : 0)), block(FT);

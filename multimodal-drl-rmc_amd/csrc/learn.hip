@@ -874,6 +874,12 @@ __device__ __forceinline__ AdamSegment adam_segment_of(const AdamArgs& a, int64_
     return sg;
 }
 
+// an out-of-range write skipped: sticky ctrl.error (the first site to report wins), raised by the host
+// at its next synchronisation point (dqn.engine.raise_device_error)
+__device__ __forceinline__ void adam_bounds_error(const AdamArgs& a, int site) {
+    if (a.ctrl) __hip_atomic_store(&a.ctrl->error, (int32_t)site, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 __global__ __launch_bounds__(256) void k_adam4(AdamArgs a) {
     if (adam_extra_wg(a)) return;   // the sampler-cache / staged-minibatch workgroups
     const int eb = (int)blockIdx.x - adam_extra_count(a);   // element block
@@ -960,6 +966,14 @@ __global__ __launch_bounds__(256) void k_adam4(AdamArgs a) {
             g.z += __shfl_xor(g.z, o);
             g.w += __shfl_xor(g.w, o);
         }
+        // bounds check (the bucketed DP step): a wide float4 lies inside this launch's
+        // element range [e0, n_params) -- a DP bucket's range -- or its stores are skipped and the
+        // sticky ctrl.error names the site (a write into another bucket's range would race with that
+        // bucket's Adam on the other stream)
+        if (live && (e < a.e0 || e + 4 > a.n_params)) {
+            if (j == 0) adam_bounds_error(a, DQNX_DEVERR_BOUNDS_ADAM_WIDE);
+            return;
+        }
         if (live && !perms) {
             if (j == 0) adam4_update(a, e, 4, g, m, v, p, tg, step_size, bc2s, true);
         } else if (live) {
@@ -977,6 +991,10 @@ __global__ __launch_bounds__(256) void k_adam4(AdamArgs a) {
                     const int64_t le = e + j - L.woff;
                     if (le < 0 || le >= (int64_t)L.Co * K) continue;   // (a layer's bias is not permuted)
                     const int co = (int)le / K, r = (int)le - co * K, ci = r / 9, t = r - ci * 9;
+                    if (e + j >= a.n_params) {   // (a permuted copy of an element outside this range)
+                        adam_bounds_error(a, DQNX_DEVERR_BOUNDS_ADAM_PERM);
+                        continue;
+                    }
                     L.p0[(co * 9 + t) * L.Ci + ci] = pv;
                     L.p1[(co * 9 + t) * L.Ci + ci] = tv;
                     L.pT[(ci * 9 + t) * L.Co + co] = pv;
@@ -1336,6 +1354,14 @@ __global__ void k_replay_push(PushArgs a) {
     for (int j = threadIdx.x; j < a.obs_dim; j += blockDim.x) {
         o[j] = so[j];
         no[j] = sn[j];
+    }
+    if (a.ring16_obs) {   // bf16 engines: the rows' bf16 copies (RNE, as the forward rounds them), pad zero
+        uint16_t* o16 = a.ring16_obs + slot * a.stride16;
+        uint16_t* n16 = a.ring16_next + slot * a.stride16;
+        for (int j = threadIdx.x; j < a.stride16; j += blockDim.x) {
+            o16[j] = j < a.obs_dim ? bf16_bits(so[j]) : (uint16_t)0;
+            n16[j] = j < a.obs_dim ? bf16_bits(sn[j]) : (uint16_t)0;
+        }
     }
     if (threadIdx.x == 0) {
         a.ring_act[slot] = a.act[row];

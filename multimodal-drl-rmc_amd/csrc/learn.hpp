@@ -295,6 +295,9 @@ struct PushArgs {
     float* ring_rew;
     float* ring_done;
     dqnx_ctrl* ctrl;
+    uint16_t* ring16_obs;        // bf16 engines: the rows' bf16 copies too (null: none)
+    uint16_t* ring16_next;
+    int stride16;
 };
 
 struct SampleArgs {
@@ -475,6 +478,11 @@ struct FusedFwdArgs {
     const float* ring_obs;
     const float* ring_next;
     int ring_stride;             // floats per ring row (obs_dim rounded up to 4)
+    // bf16 compute: the rows as bf16 copies (RNE of the fp32 rows, written by the replay push), which is
+    // all the bf16 GEMMs read of them; the forward gathers these (half the bytes), bitwise the same operands
+    const uint16_t* ring16_obs;
+    const uint16_t* ring16_next;
+    int stride16;                // bf16 elements per ring16 row (obs_dim rounded up to 8: 16-byte rows)
     const int32_t* phys;         // [Bl] physical ring slots
     float* xcopy;                // [Bl][ring_stride] stream-0 gathered rows (layer-1 dW operand)
     float* H[FUSED_MAX_L];       // stream-0 activations [Bl][out_l]
@@ -726,6 +734,7 @@ struct MicroDwArgs {
     int ring_stride, macro_len;
     int lds_floats;
     int64_t* stamps;           // diagnostic builds (-DDQNX_STAMPS): slots 24..39 (conv 1 workgroup 0)
+    int32_t* err;              // &ctrl.error: a bounds check that skipped a slab store reports there
 };
 // plans (host): false if the net is outside what the micro kernels implement
 bool micro_plan(const MicroConv* convs, int nc, int Bl, int nstreams, int n_cu, int* S, int* lds_floats);

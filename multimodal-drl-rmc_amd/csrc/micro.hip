@@ -1048,6 +1048,13 @@ __device__ __forceinline__ void micro_dw_body_ci(const MicroDwArgs& a, const Mic
     }
     DQNX_STAMP_BLK(a.stamps, sb_ + 4, sblk);
     if (!active) return;
+    // bounds check: the tile's slab rows lie inside its conv's [slices][Co*Ci*9 + Co]
+    if (slice >= L.slices || mt * 16 + 16 > L.Co || ct * 16 + 16 > L.Ci ||
+        (int64_t)L.Co * L.Ci * 9 + L.Co > L.pstride) {
+        if (lane == 0 && a.err) __hip_atomic_store(a.err, (int32_t)DQNX_DEVERR_BOUNDS_MICRO_DW, __ATOMIC_RELAXED,
+                                                   __HIP_MEMORY_SCOPE_AGENT);
+        return;
+    }
     float* part = L.partial + (int64_t)slice * L.pstride;
     // the wave's 16 co x (16 ci x 9 taps) outputs are 16 runs of 144 contiguous floats of the slab
     // ([co][ci][i][j]): transposed through the wave's own LDS rows (the stages' buffers are free

@@ -32,9 +32,14 @@ STEP_GIVEN_INDICES = 0x2
 STEP_GRADS_ONLY = 0x4
 STEP_PREFETCH = 0x8
 AGENT_LAUNCH = 0x100   # dqnx_agent_learn_mt: launch in the same call
+CHOOSE_MAX_ENVS = 256
+CHOOSE_GIL_HELD = 0x1
 DEVERR_SAMPLE_TOO_LARGE = 1
 DEVERR_EMPTY_TREE = 2
 DEVERR_PER_HANDOFF = 3
+DEVERR_BOUNDS = {16: "k_adam4 wide path: a float4 outside the launch's element range",
+                 17: "k_adam4 wide path: a permuted conv-weight copy outside the launch's range",
+                 18: "k_micro_dw: a split-K slab tile outside its conv's slabs"}
 
 I32 = ctypes.c_int32
 I64 = ctypes.c_int64
@@ -89,10 +94,10 @@ EXPORTS = [
     "dqnx_params_modified", "dqnx_dp_bucket_count", "dqnx_dp_bucket_info", "dqnx_learn_step_bucket",
     "dqnx_apply_grads_bucket", "dqnx_ctrl_get_async", "dqnx_rng_sample_words", "dqnx_rng_advance",
     "dqnx_agent_stage_rng", "dqnx_agent_launch", "dqnx_agent_readback", "dqnx_act_host_scratch_bytes",
-    "dqnx_act_host", "dqnx_agent_learn_mt", "dqnx_agent_quiesce",
+    "dqnx_act_host", "dqnx_agent_learn_mt", "dqnx_agent_quiesce", "dqnx_agent_choose",
 ]
 
-GIL_HELD = ("dqnx_agent_learn_mt",)   # entry points called with the GIL held (see lib())
+GIL_HELD = ("dqnx_agent_learn_mt", "dqnx_agent_choose")   # entry points called with the GIL held (see lib())
 
 _lib = None
 
@@ -167,6 +172,7 @@ def lib():
         "dqnx_agent_learn_mt": ([vp, vp, vp, I32, vp, P(I64)], ctypes.c_int),
         "dqnx_agent_readback": ([vp, I32, vp], ctypes.c_int),
         "dqnx_agent_quiesce": ([vp], ctypes.c_int),
+        "dqnx_agent_choose": ([vp, vp, I32, ctypes.c_double, vp, vp, vp, vp, ctypes.c_uint64, I32, vp], ctypes.c_int),
         "dqnx_act_host_scratch_bytes": ([P(NetDesc), I32], ctypes.c_uint64),
         "dqnx_act_host": ([P(NetDesc), vp, vp, I32, vp, vp, ctypes.c_uint64, vp], ctypes.c_int),
     }

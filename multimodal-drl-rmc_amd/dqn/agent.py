@@ -43,6 +43,7 @@ soft update fused into the Adam pass.
 from __future__ import annotations
 
 import array
+import ctypes
 import os
 import random
 import time
@@ -53,7 +54,7 @@ import numpy as np
 import torch as T
 
 from . import _capi as C
-from .engine import LearnEngine, spec_from_body
+from .engine import LearnEngine, raise_device_error, spec_from_body
 from .network import DeepQNetwork, DuelingDeepQNetwork
 from .replay_memory import ReplayMemoryNaive, ReplayMemoryPrioritized
 
@@ -100,6 +101,12 @@ def _cpython_mt_addresses():
         return base + head + 4, base + head
     except Exception:   # any doubt: the portable path
         return None
+
+
+def _raw_stream(device_index):
+    """The current HIP stream of the device, as dqn.engine.LearnEngine.stream() takes it (torch's current
+    stream), without building a torch Stream object per call."""
+    return T._C._cuda_getCurrentRawStream(device_index)
 
 
 def _interp2(x, x1, f0, f1):
@@ -221,6 +228,7 @@ class Agent:
         self._learn_t0 = time.time()
         self._defer = os.environ.get("DQNX_AGENT_DEFER", "0") != "0"
         self._mt = self._live_mt()     # learn() stages and advances the live generator in one call
+        self._choose_cache = None      # dqnx_agent_choose's arguments, resolved once
         self._learn_pending = False    # learn() recorded, not launched yet (DQNX_AGENT_DEFER=1)
         if os.environ.get("DQNX_AGENT_GRAPHS", "0") == "1":   # each learn step as one graph launch
             self.engine.set_graphs(True)
@@ -259,12 +267,71 @@ class Agent:
 
     def choose_actions(self, obses):
         self._launch_pending()
+        fast = self._choose_one_call(obses)
+        if fast is not None:
+            return fast
         actions = self.online_network.actions(obses)   # (waits for the stream: the learn step ran)
         self._settle(wait=True)                        # free after that wait: errors, RNG mirror check
         for i in range(len(actions)):
             if random.random() <= self.epsilon():
                 actions[i] = random.randint(0, self.output_dim - 1)
         return actions
+
+    def _choose_one_call(self, obses):
+        """choose_actions as ONE library call (dqnx_agent_choose): the acting kernel on the engine's online
+        parameters, the epsilon-greedy draws of R:dqn/agent.py:95-97 on the live `random` generator in
+        place (while the kernel runs), the wait (GIL released) and the last learn step's readback checks.
+        None when that path does not apply (the generator's layout unconfirmed, a non-MLP body, device
+        observations, more than CHOOSE_MAX_ENVS rows): the method-by-method path runs instead."""
+        if self._mt is None or isinstance(obses, T.Tensor):
+            return None
+        x = obses
+        if not (isinstance(x, np.ndarray) and x.dtype == np.float32 and x.ndim == 2 and x.flags.c_contiguous):
+            x = np.ascontiguousarray(obses, dtype=np.float32)
+            if x.ndim != 2:
+                x = x.reshape(x.shape[0], -1)
+        n = x.shape[0]
+        c = self._choose_cache
+        if c is None or c[0] < n:
+            c = self._choose_cache = self._choose_setup(n)
+            if c is None:
+                return None
+        cap, f, h, mt, pos, out, oaddr, sptr, nbytes, dev = c
+        if x.shape[1] != self.engine.spec.obs_dim:
+            raise ValueError(f"observations of width {x.shape[1]}, the network takes {self.engine.spec.obs_dim}")
+        rc = f(h, x.__array_interface__["data"][0], n, float(self.epsilon()), mt, pos, oaddr, sptr, nbytes,
+               C.CHOOSE_GIL_HELD, _raw_stream(dev))
+        self.engine._ag_unread = False   # (the call consumed the last step's readback)
+        if rc != C.DQNX_OK:
+            if rc == C.DQNX_EDEVICE:   # the sticky device error (or the RNG mirror mismatch the message names)
+                err = self.engine.ctrl().error
+                if err:
+                    raise_device_error(err)
+                raise RuntimeError("libdqnx: " + C.lib().dqnx_last_error().decode(errors="replace"))
+            C.check(rc, "agent_choose")
+        return out[:n].tolist()
+
+    def _choose_setup(self, n):
+        if n > C.CHOOSE_MAX_ENVS or os.environ.get("DQNX_AGENT_CHOOSE", "1") == "0":
+            return None
+        net = self.online_network
+        na = net._native_act()
+        spec = self.engine.spec
+        if na is None or spec.kind != C.DQNX_NET_MLP or na[1] is not self.engine.params:
+            return None
+        L = C.lib()
+        desc = spec.to_c()
+        cap = min(max(n, 64), C.CHOOSE_MAX_ENVS)
+        nb = int(L.dqnx_act_host_scratch_bytes(ctypes.byref(desc), cap))
+        if not nb:
+            return None
+        self._choose_scratch = T.zeros((nb + 15) // 16 * 4, dtype=T.float32, device=self.engine.device)
+        out = np.zeros(cap, dtype=np.int32)
+        self._choose_out = out
+        dev = self.engine.device.index if self.engine.device.index is not None else T.cuda.current_device()
+        return (cap, L.dqnx_agent_choose, self.engine.h, self._mt[0], self._mt[1], out,
+                out.__array_interface__["data"][0], self._choose_scratch.data_ptr(), self._choose_scratch.numel() * 4,
+                dev)
 
     # -- learning ----------------------------------------------------------------------
     def _check_population(self):

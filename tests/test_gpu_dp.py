@@ -322,3 +322,53 @@ def test_gpu_capture_tolerates_watchdog_polls():
                         "package"], env=env, capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stdout[-2000:] + _error_lines(r.stderr) + r.stderr[-2000:]
     assert "capture ok (package)" in r.stdout and "5 replays == eager" in r.stdout, r.stdout[-2000:]
+
+
+@pytest.mark.parametrize("algo", ["DuelingDoubleDQNAgent", "PerDuelingDoubleDQNAgent"])
+@pytest.mark.parametrize("micro", [(2, 27, 5), (4, 84, 84)])
+def test_gpu_bucketed_step_bounds_checked(micro, algo):
+    """the bucketed DP step's write paths carry bounds checks (k_adam4's wide float4 and
+    permuted-copy stores against the launch's element range, k_micro_dw's slab tiles against their
+    conv's slabs) that skip an out-of-range write and name it in the sticky ctrl.error.  One process,
+    world 1 (the all-reduce of one rank is the identity): every bucket's GRADS_ONLY part, then its Adam
+    on a second stream, as dp_learn_step_bucketed runs them -- including the bucket whose range ends on
+    the last conv's bias -- with no device error, bitwise equal to the single-GPU learn step.
+    R:dqn/agent.py:204-226 / 245-272."""
+    import torch
+    from dqn import engine as E
+    batch, cap = (256, 3000) if micro == (2, 27, 5) else (64, 600)
+    head = O.algo_spec_head(algo)
+    spec_o = O.hybrid_spec(8, head, micro_chw=micro)
+    engs = []
+    for _ in range(2):
+        e = E.LearnEngine(E.hybrid_spec(8, head, micro_chw=micro), algo, batch, cap, graphs=False)
+        e.load_params(O.reference_init(spec_o, 5))
+        e.push(*O.synth_transitions(cap, spec_o.obs_dim, 8, seed=105))
+        e.set_rng(0, np.array(__import__("random").Random(7).getstate()[1], dtype=np.uint32))
+        st = np.random.RandomState(11).get_state()
+        e.set_rng(1, np.append(st[1], st[2]).astype(np.uint32))
+        engs.append(e)
+    plain, buck = engs
+    buckets = buck.dp_buckets()
+    names = list(buck.param_views(buck.params).keys())
+    views = buck.param_views(buck.params)
+    # the flat end of the last conv's bias
+    conv_biases = [k for k in names if k.startswith("net.cnn_stream") and k.endswith(".bias")]
+    last_bias = conv_biases[-1]
+    end = (views[last_bias].data_ptr() - buck.params.data_ptr()) // 4 + views[last_bias].numel()
+    assert any(f + c == end for f, c in buckets), (buckets, end)
+    comm = torch.cuda.Stream()
+    main = torch.cuda.current_stream()
+    for _ in range(3):
+        plain.learn_step(soft_update=True)
+        for b in range(len(buckets)):
+            buck.learn_step_bucket(b)
+            comm.wait_stream(main)
+            with torch.cuda.stream(comm):
+                buck.apply_grads_bucket(b, soft_update=True)
+        main.wait_stream(comm)
+    torch.cuda.synchronize()
+    plain.check_device_error()
+    buck.check_device_error()
+    assert torch.equal(plain.params, buck.params)
+    assert torch.equal(plain.target_params, buck.target_params)
