@@ -509,19 +509,26 @@ def rocprof_avg_us(stats_name, kernel):
     if not os.path.exists(path):
         return None, None
     import csv
-    base = "k_" + kernel.split("+")[0]
-    # the implicit-GEMM convs (configs[2]) share one kernel template, one instantiation per conv: the
-    # dominant conv_fwd_c2 is the k_conv_ig instantiation with the largest total time
-    key = "TotalDurationNs" if kernel.startswith("conv_fwd_c") else "Calls"
-    if kernel.startswith("conv_fwd_c"):
-        base = "k_conv_ig"
+    tname = kernel.split("+")[0]
+    # timing names whose kernel function is named otherwise; the implicit-GEMM convs (configs[2]) share
+    # one kernel template, one instantiation per conv: the dominant conv_fwd_c2 is the k_conv_ig
+    # instantiation with the largest total time
+    alias = {"dw_all": ("k_dw_bf16", "k_bwd_level"), "adam_fused": ("k_adam4", "k_adam")}
+    bases = alias.get(tname, ("k_" + tname,))
+    key = "TotalDurationNs" if tname.startswith("conv_fwd_c") else "Calls"
+    if tname.startswith("conv_fwd_c"):
+        bases = ("k_conv_ig",)
     best = None
     with open(path) as f:
-        for row in csv.DictReader(f):
+        rows = list(csv.DictReader(f))
+    for base in bases:
+        for row in rows:
             nm = row.get("Name", "")
             short = nm.split("(")[0].split("<")[0].split("::")[-1].strip()
             if short == base and (best is None or float(row[key]) > float(best[key])):
                 best = row
+        if best is not None:
+            break
     if best is None:
         return None, path
     return float(best["AverageNs"]) / 1e3, os.path.relpath(path, REPO)
@@ -731,7 +738,7 @@ def single_gpu_extras(args, spec, device):
     return out
 
 
-def sampler_route(k):
+def sampler_route(k, capacity):
     """Which random.sample kernel the engine launches for k draws (csrc/sample.hip launch_sample_uniform)."""
     if 2048 <= k <= 4608:
         return "k_sample_fast (one-round draw, bitmap dedup, MT block cache; csrc/sample_pipe.hpp)"
@@ -741,6 +748,9 @@ def sampler_route(k):
         hs <<= 1
     if need <= 3 * hs:
         return f"k_sample_uniform<{hs}> (one 1024-thread workgroup, LDS hash table of {hs} slots)"
+    if capacity <= (1 << 20):
+        return ("k_sample_bitmap (one 1024-thread workgroup: a seen-bit per value of the <= 2^20 population in LDS, "
+                "passes of up to 5 MT blocks, in-pass repeats resolved in a small LDS table; csrc/sample_body.hpp)")
     hs = 32768
     while hs < need:
         hs <<= 1
@@ -780,7 +790,7 @@ def weak_projection(args, spec, device, t1_us, W=8, rows=4096):
             "shard_step_us": shard, "shard_step_us_prefetch": shard_pf, "shard_step_us_sampler_launch": shard_seq,
             "one_gpu_step_us_4096": t1_us,
             "sampler": {"kernel": samp[0] if samp else None, "k": Bg,
-                        "route": sampler_route(Bg),
+                        "route": sampler_route(Bg, args.capacity),
                         "avg_us_events": samp_ev[0] if samp_ev else None,
                         "avg_us_incontext_omit": samp[1] if samp else None},
             "kernels": [{"kernel": k[0], "avg_us": k[1]} for k in ks],

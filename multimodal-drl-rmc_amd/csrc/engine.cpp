@@ -3184,7 +3184,17 @@ int dqnx_ctrl_get_async(dqnx_engine* e, void* dst, void* stream) {
 // The sampler is the only writer of ctrl->py_mt and the slots, so results are bit-identical
 // to sequential steps.
 static int pf_events(dqnx_engine* e) {
-    if (!e->side_stream) DQNX_HIP_CHECK(hipStreamCreateWithFlags(&e->side_stream, hipStreamNonBlocking));
+    if (!e->side_stream) {
+        // the highest priority the device offers: the side stream's sampler workgroup (one workgroup with
+        // up to 154 KiB of LDS) is placed ahead of the remaining workgroups of the step's forward instead of
+        // waiting for a CU to drain (measured round 6: the side draw otherwise started near the forward's end)
+        int lo = 0, hi = 0;
+        if (hipDeviceGetStreamPriorityRange(&lo, &hi) == hipSuccess && hi != lo) {
+            DQNX_HIP_CHECK(hipStreamCreateWithPriority(&e->side_stream, hipStreamNonBlocking, hi));
+        } else {
+            DQNX_HIP_CHECK(hipStreamCreateWithFlags(&e->side_stream, hipStreamNonBlocking));
+        }
+    }
     for (int i = 0; i < 2; i++) {
         if (!e->ev_sampled[i]) DQNX_HIP_CHECK(hipEventCreateWithFlags(&e->ev_sampled[i], hipEventDisableTiming));
         if (!e->ev_computed[i]) DQNX_HIP_CHECK(hipEventCreateWithFlags(&e->ev_computed[i], hipEventDisableTiming));
@@ -3257,6 +3267,72 @@ static int learn_step_inlaunch(dqnx_engine* e, int base, bool prefetch, hipStrea
     return DQNX_OK;
 }
 
+// Side-stream prefetch on the fused plan, where the in-launch draw does not fit (k beyond the forward's
+// sampler workgroup: configs[3] weak scaling, every rank drawing the global 32768): step t computes on
+// slot 0 on the caller's stream while the engine's side stream draws step t+1's minibatch into slot 1
+// (the sampler reads only the MT state and the ring's size / write pointer, which no kernel of a step
+// writes); once step t's kernels are done with slot 0 the side stream copies slot 1 over it, and the
+// step's last act on the caller's stream is to wait for that -- every step (and any captured sequence
+// of them) is self-contained, the draw hidden under the step's compute.  The blocked weight copies (no
+// sampler launch in the step to rebuild them) are rebuilt on the caller's stream when stale.  Bitwise
+// equal to sequential steps (test_gpu_side_prefetch_bit_identical).
+static bool side_fused_ok(const dqnx_engine* e, int base) {
+    return e->bwd_plan == 2 && e->cfg.algo != DQNX_ALGO_PER_DOUBLE && !(base & DQNX_STEP_GIVEN_INDICES) &&
+           !inlaunch_prefetch_ok(e, base) && route_knob("DQNX_PF_SIDE_FUSED", 1) != 0;
+}
+
+static int side_fused_prologue(dqnx_engine* e, int base, hipStream_t s) {
+    int rc = pf_events(e);
+    if (rc) return rc;
+    const std::vector<KStep>& ks0 = steps_for(e, base);   // (slot 0; kernel 0 = the sampler launch)
+    rc = run_graphed(e, 0x80000 | base, s, [&](hipStream_t cs) { return enqueue_range(ks0, 0, 1, cs); });
+    if (rc) return rc;
+    DQNX_HIP_CHECK(hipEventRecord(e->ev_sampled[0], s));
+    e->pf_slot = 0;
+    e->pf_valid = true;
+    e->pf_inlaunch = false;
+    return DQNX_OK;
+}
+
+static int learn_step_side_fused(dqnx_engine* e, int base, bool prefetch, hipStream_t s) {
+    int rc = DQNX_OK;
+    if (!e->pf_valid) {   // this step's minibatch, drawn on the caller's stream
+        rc = side_fused_prologue(e, base, s);
+        if (rc) return rc;
+    }
+    if (prefetch) {   // step t+1's draw into slot 1, beside this step (after everything enqueued before it)
+        DQNX_HIP_CHECK(hipEventRecord(e->fork_ev, s));
+        DQNX_HIP_CHECK(hipStreamWaitEvent(e->side_stream, e->fork_ev, 0));
+        rc = pf_sample(e, base, 1);
+        if (rc) return rc;
+    }
+    if (relayout_due(e)) {
+        rc = enqueue_relayout(e, s);
+        if (rc) return rc;
+        e->wblk_dirty = false;
+    }
+    const std::vector<KStep>& ks = steps_for(e, base);
+    rc = run_graphed(e, base | 0x20000, s, [&](hipStream_t cs) { return enqueue_range(ks, 1, (int)ks.size(), cs); });
+    if (rc) return rc;
+    if (!blk_kept(e, base)) e->wblk_dirty = true;
+    if (!prefetch) {   // consumed the pending minibatch; nothing drawn ahead
+        e->pf_valid = false;
+        return DQNX_OK;
+    }
+    // slot 1 over slot 0 once this step no longer reads it, then the draw joins the step
+    DQNX_HIP_CHECK(hipEventRecord(e->ev_computed[0], s));
+    DQNX_HIP_CHECK(hipStreamWaitEvent(e->side_stream, e->ev_computed[0], 0));
+    int32_t* idx = at<int32_t>(e, e->off[DQNX_BUF_BATCH_IDX]);
+    int32_t* phys = at<int32_t>(e, e->ws_phys);
+    DQNX_HIP_CHECK(hipMemcpyAsync(idx, idx + e->Bg, (size_t)e->Bg * 4, hipMemcpyDeviceToDevice, e->side_stream));
+    DQNX_HIP_CHECK(hipMemcpyAsync(phys, phys + e->Bl, (size_t)e->Bl * 4, hipMemcpyDeviceToDevice, e->side_stream));
+    DQNX_HIP_CHECK(hipEventRecord(e->ev_sampled[0], e->side_stream));
+    DQNX_HIP_CHECK(hipStreamWaitEvent(s, e->ev_sampled[0], 0));
+    e->pf_slot = 0;
+    e->pf_stream = s;
+    return DQNX_OK;
+}
+
 int dqnx_learn_step(dqnx_engine* e, int32_t flags, void* stream) {
     int rc = check_bound(e);
     if (rc) return rc;
@@ -3269,8 +3345,9 @@ int dqnx_learn_step(dqnx_engine* e, int32_t flags, void* stream) {
     // sampler, slab plan), nothing is drawn ahead.  Per-layer plan: a side-stream pipeline.
     const int base = flags & (DQNX_STEP_SOFT_UPDATE | DQNX_STEP_GIVEN_INDICES | DQNX_STEP_GRADS_ONLY);
     const bool inl = inlaunch_prefetch_ok(e, base);
+    const bool side = side_fused_ok(e, base);
     const bool prefetch = (flags & DQNX_STEP_PREFETCH) && !(flags & DQNX_STEP_GIVEN_INDICES) &&
-                          e->cfg.algo != DQNX_ALGO_PER_DOUBLE && (e->bwd_plan != 2 || inl);
+                          e->cfg.algo != DQNX_ALGO_PER_DOUBLE && (e->bwd_plan != 2 || inl || side);
     if (e->ring_size < e->Bs && !(flags & DQNX_STEP_GIVEN_INDICES) && !e->pf_valid)
         return set_error(DQNX_EINVAL, "Sample larger than population: %lld < %d", (long long)e->ring_size, e->Bs);
     if (e->pf_valid && (flags & DQNX_STEP_GIVEN_INDICES))
@@ -3286,6 +3363,7 @@ int dqnx_learn_step(dqnx_engine* e, int32_t flags, void* stream) {
         if (!rc) e->wblk_dirty = !blk_kept(e, base);   // stale again after an update that does not keep them
         return rc;
     }
+    if (e->bwd_plan == 2) return learn_step_side_fused(e, base, prefetch, s);
     rc = pf_events(e);
     if (rc) return rc;
     if (!e->pf_valid) {   // prologue: this step's minibatch, ordered after everything on s
@@ -3373,10 +3451,12 @@ int dqnx_prefetch_begin(dqnx_engine* e, int32_t flags, void* stream) {
     int rc = check_bound(e);
     if (rc) return rc;
     const int base = flags & (DQNX_STEP_SOFT_UPDATE | DQNX_STEP_GRADS_ONLY);
-    if (e->pf_valid || e->cfg.algo == DQNX_ALGO_PER_DOUBLE || !inlaunch_prefetch_ok(e, base))
+    const bool side = side_fused_ok(e, base);
+    if (e->pf_valid || e->cfg.algo == DQNX_ALGO_PER_DOUBLE || (!inlaunch_prefetch_ok(e, base) && !side))
         return DQNX_OK;   // a draw is pending already, or this configuration does not draw ahead
     if (e->ring_size < e->Bs)
         return set_error(DQNX_EINVAL, "Sample larger than population: %lld < %d", (long long)e->ring_size, e->Bs);
+    if (side) return side_fused_prologue(e, base, (hipStream_t)stream);
     return inlaunch_prologue(e, base, (hipStream_t)stream);
 }
 

@@ -874,7 +874,10 @@ __global__ __launch_bounds__(FT) void k_head_bwd(HeadBwdArgs a) {
 // conflict-free.
 // =====================================================================================
 #ifndef DQNX_DWB_KT64
-#define DQNX_DWB_KT64 32
+// samples per pass of the 64 x 64 tiles (configs[4]: 512-sample split-K slices).  Measured round 6,
+// B = 8192 PER bf16 (gpurun_out r06g): 32 -> dw_all 29.1 us, 64 -> 26.6, 128 -> 36.0 (2 waves / SIMD),
+// 64 with two passes in flight 28.2; the chunks still accumulate in k order (bitwise the same sums)
+#define DQNX_DWB_KT64 64
 #endif
 #ifndef DQNX_DWB_PIPE
 #define DQNX_DWB_PIPE 0   // 1: two passes in flight, two LDS buffers (measured equal: 27.7 vs 26.4 us at B=8192)

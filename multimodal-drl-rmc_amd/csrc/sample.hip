@@ -56,6 +56,17 @@ __global__ __launch_bounds__(SAMPLE_NT) void k_sample_uniform_g(SampleArgs a) {
 }
 
 
+// k beyond the LDS hash tables, population <= 2^20 (sample_bitmap_body): the dedup state in LDS
+constexpr int SAMPLE_BITMAP_AH = 4, SAMPLE_BITMAP_BMX = 2048;   // 156 KiB of LDS: passes of 4 new blocks
+__global__ __launch_bounds__(SAMPLE_NT) void k_sample_bitmap(SampleArgs a) {
+    __shared__ SampleBitmapLds<SAMPLE_NT, SAMPLE_BITMAP_AH, SAMPLE_BITMAP_BMX> S;
+    if (blockIdx.x > 0) {
+        relayout_run(a.rl, blockIdx.x - 1, gridDim.x - 1);
+        return;
+    }
+    sample_bitmap_body<SAMPLE_NT, SAMPLE_BITMAP_AH, SAMPLE_BITMAP_BMX>(a, S);
+}
+
 // Logical positions (given by the caller) -> physical ring slots of the local shard.
 __global__ void k_idx_to_phys(const int32_t* idx, int32_t* phys, int shard_begin, int n, const dqnx_ctrl* ctrl,
                               int64_t capacity, RelayoutArgs rl, int pblocks) {
@@ -158,6 +169,10 @@ int launch_sample_uniform(const SampleArgs& a_in, hipStream_t s) {
             case 8192: DQNX_LAUNCH(k_sample_uniform<8192>, grid, dim3(SAMPLE_NT), 0, s, a); break;
             default: DQNX_LAUNCH(k_sample_uniform<16384>, grid, dim3(SAMPLE_NT), 0, s, a); break;
         }
+    } else if (a.capacity > 0 && a.capacity <= SAMPLE_BITMAP_MAX_N && !route_flag("DQNX_SAMPLER_GLOBAL")) {
+        // k beyond the LDS tables over a replay of <= 2^20 slots: the LDS bitmap body (configs[3] weak
+        // scaling at world 8: k = 32768, n = 10^6); DQNX_SAMPLER_GLOBAL keeps the global-table body
+        DQNX_LAUNCH(k_sample_bitmap, grid, dim3(SAMPLE_NT), 0, s, a);
     } else {
         const int ghs = global_hash_slots(a.k);
         if (ghs < 0) return set_error(DQNX_EUNSUPPORTED, "sample: k=%d too large", a.k);
@@ -208,6 +223,7 @@ extern "C" int dqnx_sample_uniform(uint32_t* mt625, int64_t n, int32_t k, int32_
     }
     a.n_dev = (const int64_t*)sc;
     a.n_val = n;
+    a.capacity = n;   // (the population bound the routes check; no physical slots are written)
     a.wptr_dev = (const int64_t*)sc + 1;
     a.mtc = (uint32_t*)(sc + 256);
     a.mtc_blocks = 0;

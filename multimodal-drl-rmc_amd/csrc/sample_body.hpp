@@ -503,4 +503,231 @@ __device__ __forceinline__ void sample_uniform_body(const SampleArgs& a, SampleL
     DQNX_STAMP(a.stamps, 15);
 }
 
+// ---------------------------------------------------------------------------------------------
+// Large minibatches over a population of at most 2^20 (the replay capacity): k beyond every LDS hash
+// table (configs[3]'s weak-scaling global draw: k = 32,768 = 4096 rows x 8 ranks, n = 10^6), where
+// the multi-pass body's (value, position) table would live in global memory (~205 us per draw on
+// MI355X, one global atomicCAS per word).  The same first-occurrence semantics of random.sample's set
+// branch (R:dqn/replay_memory.py:38-39), with the dedup state in LDS:
+//   * a "seen" bit per value (2^20 bits = 128 KiB), set by every accepted draw and kept for the call;
+//   * a pass = the rest of the current MT block + up to AH twisted blocks; a word whose bit was set by
+//     an EARLIER pass repeats an accepted value and is dropped (read before any atomic of this pass);
+//   * inside a pass, the word that finds its bit already set (atomicOr) repeats a value of the same
+//     pass: such values go to a small (value, earliest position) table, every other word of the pass
+//     probes it, and the earliest position wins.  A pass of W words repeats at most W / 2 distinct
+//     values, and the table holds more than that: no overflow, no fallback;
+//   * first occurrences are ranked in stream order by a block scan, as in sample_uniform_body.
+template <int NT, int AH, int BMX>
+struct SampleBitmapLds {
+    SampleLdsBase<NT, AH> b;
+    uint32_t bm[1 << 15];            // "seen" bit of every value < 2^20
+    unsigned long long xt[BMX];      // (value << 32 | stream position): values repeated inside a pass
+    int xn;                          // nonzero: the pass has a repeated value
+};
+constexpr int64_t SAMPLE_BITMAP_MAX_N = (int64_t)1 << 20;
+
+// LDS-only workgroup barrier: the sampler's cross-thread data is all in LDS, so no wave waits here for
+// its global stores (the minibatch it writes) to complete -- __syncthreads() would, once per pass
+__device__ __forceinline__ void bm_lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+// mt_twist_into without its closing barrier (the caller ends it)
+__device__ __forceinline__ void mt_twist_into_nowait(const uint32_t* old, uint32_t* nw) {
+    const int t = threadIdx.x;
+    if (t < 227) {
+        const uint32_t a0 = old[t + 397] ^ mt_mix(old[t], old[t + 1]);
+        const uint32_t a1 = a0 ^ mt_mix(old[t + 227], old[t + 228]);
+        nw[t] = a0;
+        nw[t + 227] = a1;
+        if (t < 169) nw[t + 454] = a1 ^ mt_mix(old[t + 454], old[t + 455]);
+        if (t == 169) nw[623] = a1 ^ mt_mix(old[623], old[397] ^ mt_mix(old[0], old[1]));
+    }
+}
+
+template <int NT, int AH, int BMX>
+__device__ __forceinline__ void sample_bitmap_body(const SampleArgs& a, SampleBitmapLds<NT, AH, BMX>& S) {
+    static_assert(BMX > 624 * (AH + 1) / 2 && (BMX & (BMX - 1)) == 0, "a pass's repeated values fit the table");
+    static_assert(NT >= 624, "one state word per thread");
+    constexpr int NW = NT / 64, WPT = (624 * (AH + 1) + NT - 1) / NT;
+    auto& blk = S.b.blk;
+    int* wave_tot = S.b.wave_tot;
+    int& s_final = S.b.s_final;
+    const int tid = threadIdx.x;
+    const int lane = tid & 63, wid = tid >> 6;
+    // every global load of the call issued at once, unconditionally (a load whose value a branch needs
+    // is waited for right there: three serialised round trips otherwise)
+    const int64_t n = a.n_dev ? gld(a.n_dev) : a.n_val;
+    const int64_t wptr0 = a.phys_out ? gld(a.wptr_dev) : 0;
+    const uint32_t* src = a.state_in ? a.state_in : a.state;
+    const uint32_t st_j = gld(src + (tid < 624 ? tid : 624));
+    const uint32_t pos0 = gld(src + 624);
+    const int k = a.k;
+    if (k < 0 || (int64_t)k > n || n <= a.setsize || n > SAMPLE_BITMAP_MAX_N) {
+        // errors and the pool branch (a replay still smaller than random.sample's setsize): the general
+        // body (its set branch is never reached from here: n > 2^20 exceeds every routed capacity)
+        sample_uniform_body<NT, 1024, AH, 0>(a, S.b, reinterpret_cast<unsigned long long*>(S.bm));
+        return;
+    }
+    if (k == 0) return;
+    DQNX_STAMP(a.stamps, 0);
+    int64_t phys_base = 0;
+    if (a.phys_out) {
+        phys_base = wptr0 - n;
+        if (phys_base < 0) phys_base += a.capacity;
+    }
+    const uint32_t pb32 = (uint32_t)phys_base, cap32 = (uint32_t)a.capacity;
+    if (tid < 624) blk[0][tid] = st_j;
+    uint32_t pos = pos0;
+    {
+        uint4* bm4 = reinterpret_cast<uint4*>(S.bm);
+#pragma unroll
+        for (int i = 0; i < (1 << 13) / NT; i++) bm4[tid + i * NT] = make_uint4(0u, 0u, 0u, 0u);
+        for (int i = tid; i < BMX; i += NT) S.xt[i] = ~0ull;
+        if (tid == 0) S.xn = 0;
+    }
+    bm_lds_sync();
+    const uint32_t n32 = (uint32_t)n;
+    const int bits = bit_length64((uint64_t)n);
+    const uint32_t shift = 32u - (uint32_t)bits;
+    const float inv_accept = (float)((double)(1ull << bits) / (double)n);   // words per valid draw
+    int accepted = 0;
+    uint32_t spos0 = 0;   // stream position (since the call began) of blk[0][pos]
+    int pass = 0;
+    DQNX_STAMP(a.stamps, 1);
+    while (true) {
+        const int avail = 624 - (int)pos;
+        const int need = k - accepted;
+        const float est = need * inv_accept * (1.f + (float)(accepted + need) / (2.f * (float)n)) + 32.f + need / 16.f;
+        int nb = (int)ceilf((est - (float)avail) / 624.f);
+        nb = nb > AH ? AH : nb;
+        nb = nb < (avail == 0 ? 1 : 0) ? 1 : nb;
+        for (int j = 1; j <= nb; j++) {   // block-parallel twists, each ended by an LDS-only barrier
+            mt_twist_into_nowait(blk[j - 1], blk[j]);
+            bm_lds_sync();
+        }
+        if (pass == 1) DQNX_STAMP(a.stamps, 2);
+        const int nwords = avail + 624 * nb;
+        const int m = (nwords + NT - 1) / NT;   // thread t owns the words [t m, t m + m) of the pass
+        const uint32_t* wflat = &blk[0][0] + pos;
+        uint32_t cv[WPT], hv[WPT];
+        bool val[WPT], xc[WPT];
+#pragma unroll
+        for (int u = 0; u < WPT; u++) {   // the candidates; then drop repeats of earlier passes
+            const int w = tid * m + u;
+            const bool live = u < m && w < nwords;
+            const uint32_t c = live ? mt_temper(wflat[w]) >> shift : 0u;
+            cv[u] = c;
+            val[u] = live && c < n32 && ((S.bm[c >> 5] >> (c & 31u)) & 1u) == 0u;
+            hv[u] = 0;
+        }
+        bm_lds_sync();   // every earlier-pass read before this pass's first atomic
+        if (pass == 1) DQNX_STAMP(a.stamps, 3);
+#pragma unroll
+        for (int u = 0; u < WPT; u++) {
+            const uint32_t bit = 1u << (cv[u] & 31u);
+            xc[u] = val[u] && (atomicOr(&S.bm[cv[u] >> 5], bit) & bit) != 0u;
+        }
+#pragma unroll
+        for (int u = 0; u < WPT; u++) {   // values repeated inside the pass: (value, earliest position)
+            if (!xc[u]) continue;
+            const unsigned long long key = ((unsigned long long)cv[u] << 32) | (spos0 + (uint32_t)(tid * m + u));
+            uint32_t h = cv[u] & (BMX - 1);
+            while (true) {
+                const unsigned long long pv = atomicCAS(&S.xt[h], ~0ull, key);
+                if (pv == ~0ull) break;
+                if ((uint32_t)(pv >> 32) == cv[u]) { atomicMin(&S.xt[h], key); break; }
+                h = (h + 1) & (BMX - 1);
+            }
+            hv[u] = h;
+            S.xn = 1;
+        }
+        if (tid == 0) s_final = -1;
+        bm_lds_sync();
+        if (pass == 1) DQNX_STAMP(a.stamps, 4);
+        const int nx = S.xn;
+        if (nx) {   // the other words of a repeated value (the one that set its bit first among them)
+#pragma unroll
+            for (int u = 0; u < WPT; u++) {
+                if (!val[u] || xc[u]) continue;
+                uint32_t h = cv[u] & (BMX - 1);
+                unsigned long long t = S.xt[h];
+                while (t != ~0ull && (uint32_t)(t >> 32) != cv[u]) {
+                    h = (h + 1) & (BMX - 1);
+                    t = S.xt[h];
+                }
+                if (t == ~0ull) continue;
+                xc[u] = true;
+                hv[u] = h;
+                atomicMin(&S.xt[h], ((unsigned long long)cv[u] << 32) | (spos0 + (uint32_t)(tid * m + u)));
+            }
+            bm_lds_sync();
+        }
+        if (pass == 1) DQNX_STAMP(a.stamps, 5);
+        bool first[WPT];
+        int cnt = 0;
+#pragma unroll
+        for (int u = 0; u < WPT; u++) {
+            first[u] = val[u] && (!xc[u] || (uint32_t)(S.xt[hv[u]] & 0xffffffffull) == spos0 + (uint32_t)(tid * m + u));
+            cnt += first[u] ? 1 : 0;
+        }
+        int incl = cnt;   // wave inclusive scan
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int y = __shfl_up(incl, o);
+            if (lane >= o) incl += y;
+        }
+        if (lane == 63) wave_tot[wid] = incl;
+        bm_lds_sync();
+        int before = incl - cnt, total = 0;
+#pragma unroll
+        for (int w = 0; w < NW; w++) {
+            const int tw = wave_tot[w];
+            before += (w < wid) ? tw : 0;
+            total += tw;
+        }
+        int r = accepted + before;
+        if (pass == 1) DQNX_STAMP(a.stamps, 6);
+#pragma unroll
+        for (int u = 0; u < WPT; u++) {
+            if (!first[u]) continue;
+            if (r < k) {
+                const int32_t c = (int32_t)cv[u];
+                a.out[r] = c;
+                if (a.phys_out && r >= a.shard_begin && r < a.shard_begin + a.shard_len) {
+                    uint32_t ps = pb32 + (uint32_t)c;   // (< 2^32: both terms < capacity <= 2^20)
+                    if (ps >= cap32) ps -= cap32;
+                    a.phys_out[r - a.shard_begin] = (int32_t)ps;
+                }
+                if (r == k - 1) s_final = tid * m + u;   // word index of the k-th acceptance
+            }
+            r++;
+        }
+        bm_lds_sync();
+        if (pass == 1) DQNX_STAMP(a.stamps, 7);
+        pass++;
+        accepted += total;
+        if (accepted >= k) {   // state after the k-th draw: the block holding that word, index just past it
+            const int wf = s_final;
+            const int bf = (wf < avail) ? 0 : 1 + (wf - avail) / 624;
+            const uint32_t nxp = (uint32_t)((wf < avail) ? (int)pos + wf + 1 : (wf - avail) % 624 + 1);
+            if (bf > 0 || a.state_in)
+                for (int j = tid; j < 624; j += NT) a.state[j] = blk[bf][j];
+            if (tid == 0) a.state[624] = nxp;
+            DQNX_STAMP(a.stamps, 15);
+#ifdef DQNX_STAMPS
+            if (a.stamps && blockIdx.x == 0 && tid == 0) a.stamps[14] = pass;
+#endif
+            break;
+        }
+        // the whole pass was consumed: clear the repeat table, continue from the last block's end
+        if (nx) {
+            for (int i = tid; i < BMX; i += NT) S.xt[i] = ~0ull;
+            if (tid == 0) S.xn = 0;
+        }
+        spos0 += (uint32_t)nwords;
+        if (nb > 0)
+            for (int j = tid; j < 624; j += NT) blk[0][j] = blk[nb][j];
+        bm_lds_sync();
+        pos = 624;
+    }
+}
+
 }  // namespace dqnx

@@ -29,8 +29,11 @@ def test_gpu_sampler_matches_oracle():
              (3000, 0), (999, 999),
              # pipelined sampler (k <= 5984): acceptance ~1/2 (two rounds), its largest k, small k
              (524289, 4096), (524289, 5984), (1000000, 5984), (5000, 100), (2049, 600),
-             # k beyond the LDS tables: the global-memory hash table
-             (100000, 12000), (1000000, 16384)]
+             # k beyond the LDS tables: the LDS-bitmap body (population <= 2^20; DQNX_SAMPLER_GLOBAL:
+             # the global-memory hash table), incl. configs[3]'s weak-scaling draw (k = 32768 = 8 x 4096),
+             # the bitmap's largest population and the pool branch at setsize(32768) = 262165
+             (100000, 12000), (1000000, 16384), (1000000, 32768), (1048576, 32768), (300000, 32768),
+             (262165, 32768), (1000000, 100000)]
     for j, (n, k) in enumerate(cases):
         random.seed(1000 + j)
         st = O.py_state_to_array()
@@ -52,7 +55,8 @@ def test_gpu_sampler_matches_oracle():
             st = want_state
 
 
-@pytest.mark.parametrize("mode", ["DQNX_SAMPLER_FORCE_FALLBACK", "DQNX_SAMPLER_OLD", "DQNX_SAMPLER_FAST"])
+@pytest.mark.parametrize("mode", ["DQNX_SAMPLER_FORCE_FALLBACK", "DQNX_SAMPLER_OLD", "DQNX_SAMPLER_FAST",
+                                  "DQNX_SAMPLER_GLOBAL"])
 def test_gpu_sampler_other_paths_match_oracle(monkeypatch, mode):
     """The fast sampler's exact fallback (taken when a draw needs more words than the 8-sigma
     margin provides), the multi-pass kernel alone, and the fast path below its default k range,
@@ -655,3 +659,62 @@ def test_gpu_apply_grads_tiles_bit_identical(monkeypatch, world, k):
     assert torch.equal(e1.adam_m, e2.adam_m) and torch.equal(e1.adam_v, e2.adam_v)
     assert e1.loss() == e2.loss()
 
+
+
+@pytest.mark.parametrize("batch,world,cap,graph_steps", [(8192, 1, 30000, 0), (32768, 8, 300000, 0),
+                                                          (32768, 8, 300000, 3)])
+def test_gpu_side_prefetch_bit_identical(batch, world, cap, graph_steps):
+    """The fused plan's side-stream prefetch (k beyond the forward's sampler workgroup: step t+1's
+    random.sample drawn on the engine's side stream beside step t, then copied over the compute slot):
+    bitwise the same weights, target, RNG state and minibatch as sequential steps -- one GPU at B = 8192,
+    and rank 0 of world 8 at configs[3]'s weak-scaling global 32768 (the LDS-bitmap sampler), eager and
+    as a captured graph of an odd number of steps.  R:dqn/replay_memory.py:38-39, R:dqn/agent.py:204-226."""
+    from dqn import data_parallel as DP
+    E = _engine_mod()
+    spec = E.mlp_spec(284, 8, "dueling")
+    data = O.synth_transitions(cap, 284, 8, seed=3)
+    init = O.reference_init(O.mlp_spec(284, 8, "dueling"), 4)
+
+    def make():
+        e = E.LearnEngine(spec, "DuelingDoubleDQNAgent", batch, cap, world_size=world, rank=0)
+        e.load_params(init)
+        e.push(*data)
+        random.seed(77)
+        e.set_rng(0, np.array(random.getstate()[1], dtype=np.uint32))
+        return e
+
+    def step(e, pf):
+        if world > 1:
+            e.learn_step(grads_only=True, prefetch=pf)
+            e.apply_grads(soft_update=True)
+        else:
+            e.learn_step(soft_update=True, prefetch=pf)
+
+    a = make()
+    for _ in range(7):
+        step(a, False)
+    torch.cuda.synchronize()
+    a.check_device_error()
+    b = make()
+    if graph_steps:
+        b.set_graphs(False)
+        b.prefetch_prologue(grads_only=world > 1)
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with DP.capture(g):
+            for _ in range(graph_steps):
+                step(b, True)
+        for _ in range(6 // graph_steps):
+            g.replay()
+        C_ = __import__("dqn._capi", fromlist=["lib"])
+        C_.check(C_.lib().dqnx_prefetch_stream(b.h, b.stream()), "prefetch_stream")
+    else:
+        for _ in range(6):
+            step(b, True)
+    step(b, False)   # consumes the pending draw
+    torch.cuda.synchronize()
+    b.check_device_error()
+    assert torch.equal(a.batch_idx, b.batch_idx)
+    assert np.array_equal(a.get_rng(0), b.get_rng(0))
+    assert torch.equal(a.params, b.params)
+    assert torch.equal(a.target_params, b.target_params)
