@@ -380,6 +380,154 @@ __global__ __launch_bounds__(kActThreads) void k_act_mlp2(ActArgs a) {
     }
 }
 
+// ONE workgroup for the whole forward of n <= 2 rows (the agent's n_env): every weight of the net
+// (MLP-284: 428 KB) is requested by the 1024 threads at once, straight into registers -- one CU's
+// L2 / Infinity-Cache stream -- so the launch makes ONE dependent memory round trip plus the
+// actions' store, where k_act_mlp2 makes three (layer 1 across 16 workgroups, the share hand-off,
+// the head): no ticket, no acquire, no cross-workgroup hand-off.
+//   layer 1: TPN1 = 1024 / h0 threads per neuron, thread (j, q) holds float4 q, q + TPN1, ... of row
+//            j (consecutive lanes read consecutive 16 bytes), partial dot products per row summed
+//            over the TPN1 lanes by xor shuffles;
+//   layer 2: TPN2 = 1024 / h1 threads per neuron, float4 q, q + TPN2, ... of row o (loaded with
+//            layer 1's weights);
+//   head:    A rows (advantages for dueling nets, R:dqn/network.py:110-117) x F, one float4 per
+//            thread, summed over the F / 4 lanes of a row.
+// Compile-time register budget: W1S float4 of layer 1 and W2S of layer 2 per thread (act1_ok).
+constexpr int kAct1Threads = 512;   // 2 waves per SIMD: 256 registers a lane for the weight slices
+template <int TPN>
+__device__ __forceinline__ float group_sum(float v) {   // over TPN consecutive lanes (power of two)
+#pragma unroll
+    for (int o = TPN / 2; o >= 1; o >>= 1) v += __shfl_xor(v, o, kWave);
+    return v;
+}
+template <int R, int ACT, int TPN1, int TPN2, int W1S, int W2S>
+__global__ __launch_bounds__(kAct1Threads) void k_act_mlp1(ActArgs a) {
+    extern __shared__ float lds[];
+    const int tid = threadIdx.x;
+    const int D = a.D, h0 = a.out[0], h1 = a.out[1], F = a.F, A = a.A;
+    const int n = a.n;
+    const int d4 = D >> 2, h04 = h0 >> 2;
+    float4* x4 = reinterpret_cast<float4*>(lds);          // [R][d4] obs
+    float* y1 = lds + R * D;                               // [R][h0]
+    float* y2 = y1 + R * h0;                               // [R][h1]
+    float* q = y2 + R * h1;                                // [R][16]
+    const float* P = a.params;
+    // (0) every load at once: layer 1's row slices, layer 2's, the head's float4, the biases, the obs
+    const int j = tid / TPN1, q1 = tid % TPN1;
+    const float4* W1 = reinterpret_cast<const float4*>(P + a.off[0]) + (int64_t)(j < h0 ? j : 0) * d4;
+    float4 w1[W1S];
+#pragma unroll
+    for (int i = 0; i < W1S; i++) {
+        const int c = q1 + TPN1 * i;
+        w1[i] = (c < d4 && j < h0) ? W1[c] : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    const int o = tid / TPN2, q2 = tid % TPN2;
+    const float4* W2 = reinterpret_cast<const float4*>(P + a.off[1]) + (int64_t)(o < h1 ? o : 0) * h04;
+    float4 w2[W2S];
+#pragma unroll
+    for (int i = 0; i < W2S; i++) {
+        const int c = q2 + TPN2 * i;
+        w2[i] = (c < h04 && o < h1) ? W2[c] : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    const float* Hh = P + a.head_off;
+    const float* Wh = a.dueling ? Hh + F + 1 : Hh;   // advantage stream (R:dqn/network.py:110-117)
+    // (the advantage rows start F + 1 floats into the head block: 4-byte aligned only -> scalar loads,
+    // two consecutive elements of one row per thread, F / 2 lanes per row)
+    const int hr = tid / (F / 2), hc = 2 * (tid % (F / 2));
+    const float wh0 = hr < A ? Wh[(int64_t)hr * F + hc] : 0.f;
+    const float wh1 = hr < A ? Wh[(int64_t)hr * F + hc + 1] : 0.f;
+    const float b1 = j < h0 ? P[a.off[0] + (int64_t)h0 * D + j] : 0.f;
+    const float b2 = o < h1 ? P[a.off[1] + (int64_t)h1 * h0 + o] : 0.f;
+    const float bh = hr < A ? Wh[(int64_t)A * F + hr] : 0.f;
+    for (int e = tid; e < R * d4; e += kAct1Threads) {
+        const int r = e / d4, c = e - r * d4;
+        x4[e] = r < n ? reinterpret_cast<const float4*>(a.obs + (int64_t)r * D)[c] : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    __syncthreads();
+    // (1) layer 1
+#pragma unroll
+    for (int r = 0; r < R; r++) {
+        float acc = 0.f;
+#pragma unroll
+        for (int i = 0; i < W1S; i++) {
+            const int c = q1 + TPN1 * i;
+            if (c < d4) {
+                const float4 xv = x4[r * d4 + c];
+                acc = fmaf(w1[i].x, xv.x, acc);
+                acc = fmaf(w1[i].y, xv.y, acc);
+                acc = fmaf(w1[i].z, xv.z, acc);
+                acc = fmaf(w1[i].w, xv.w, acc);
+            }
+        }
+        acc = group_sum<TPN1>(acc);
+        if (q1 == 0 && j < h0) y1[r * h0 + j] = act_fwd<ACT>(acc + b1);
+    }
+    __syncthreads();
+    // (2) layer 2
+    const float4* y14 = reinterpret_cast<const float4*>(y1);
+#pragma unroll
+    for (int r = 0; r < R; r++) {
+        float acc = 0.f;
+#pragma unroll
+        for (int i = 0; i < W2S; i++) {
+            const int c = q2 + TPN2 * i;
+            if (c < h04) {
+                const float4 xv = y14[r * h04 + c];
+                acc = fmaf(w2[i].x, xv.x, acc);
+                acc = fmaf(w2[i].y, xv.y, acc);
+                acc = fmaf(w2[i].z, xv.z, acc);
+                acc = fmaf(w2[i].w, xv.w, acc);
+            }
+        }
+        acc = group_sum<TPN2>(acc);
+        if (q2 == 0 && o < h1) y2[r * h1 + o] = act_fwd<ACT>(acc + b2);
+    }
+    __syncthreads();
+    // (3) the head: F / 2 lanes per output row (a power of two, <= 64: act1_ok)
+#pragma unroll
+    for (int r = 0; r < R; r++) {
+        float acc = 0.f;
+        if (hr < A) {
+            acc = fmaf(wh0, y2[r * h1 + hc], acc);
+            acc = fmaf(wh1, y2[r * h1 + hc + 1], acc);
+        }
+        for (int off = F / 4; off >= 1; off >>= 1) acc += __shfl_xor(acc, off, kWave);
+        if (hc == 0 && hr < A) q[r * 16 + hr] = acc + bh;
+    }
+    __syncthreads();
+    if (tid < n) {
+        const int r = tid;
+        const float* qr = q + r * 16;
+        int best = 0;
+        float bv = qr[0];
+        for (int jj = 0; jj < A; jj++) {
+            const float v = qr[jj];
+            if (a.values) a.values[(int64_t)r * A + jj] = v;
+            if (v > bv || (v != v && bv == bv)) { bv = v; best = jj; }   // first max; NaN wins like torch
+        }
+        a.actions[r] = best;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (r == 0) act_signal(a);
+    }
+}
+
+// k_act_mlp1 applies: n <= 2 rows, two hidden layers, widths dividing the 1024 threads into powers of
+// two per neuron, every weight row a whole number of 16-byte pieces within the register budget, a
+// head whose F / 4 lanes per row fit one wave.  (DQNX_ACT1=0: the multi-workgroup kernels.)
+static bool act1_ok(const ActArgs& a, int* tpn1, int* tpn2) {
+    if (a.L != 2 || a.n > 4 || a.A > 16 || route_knob("DQNX_ACT1", 1) == 0) return false;
+    const int D = a.D, h0 = a.out[0], h1 = a.out[1], F = a.F;
+    if (D % 4 || h0 % 4 || F % 4 || (a.off[0] & 3) || (a.off[1] & 3) || F != h1) return false;
+    auto pow2 = [](int v) { return v > 0 && (v & (v - 1)) == 0; };
+    if (!pow2(h0) || !pow2(h1) || h0 > kAct1Threads || h1 > kAct1Threads) return false;
+    const int t1 = kAct1Threads / h0, t2 = kAct1Threads / h1;
+    const int lpr = F / 2;   // head lanes per row
+    if (!pow2(lpr) || lpr > kWave || a.A * lpr > kAct1Threads) return false;
+    *tpn1 = t1;
+    *tpn2 = t2;
+    return true;
+}
+
 // k_act_mlp2 applies: two hidden layers, layer 2 on one thread per neuron, the head's advantage / Q
 // rows as float4s of one pass (A * F % 4 == 0, 16-byte aligned, <= 4096 floats), A <= 16; with a
 // completion word, one row group (act_signal stores it from row group 0)
@@ -390,8 +538,36 @@ static bool act2_ok(const ActArgs& a, int R) {
            route_knob("DQNX_ACT2", 1) != 0;
 }
 
+template <int R, int ACT>
+static int launch_act1(const ActArgs& a, int t1, int t2, hipStream_t s) {
+    const size_t lds = ((size_t)R * (a.D + a.out[0] + a.out[1] + 16)) * sizeof(float);
+    const int s1 = (a.D / 4 + t1 - 1) / t1, s2 = (a.out[0] / 4 + t2 - 1) / t2;   // float4 slots per thread
+#define ACT1(T1, T2, S1, S2) DQNX_LAUNCH((k_act_mlp1<R, ACT, T1, T2, S1, S2>), dim3(1), dim3(kAct1Threads), lds, s, a)
+    // the reference's MLP (R:env/custom_env/macro with lane/dqn_config.py:76-84): D -> 256 -> 128
+    if (t1 == 2 && t2 == 4 && s2 <= 16) {
+        if (s1 <= 8) ACT1(2, 4, 8, 16);
+        else if (s1 <= 16) ACT1(2, 4, 16, 16);
+        else if (s1 <= 24) ACT1(2, 4, 24, 16);
+        else if (s1 <= 36) ACT1(2, 4, 36, 16);   // MLP-284: 71 float4 per row over 2 lanes
+        else return -1;
+    } else {
+        return -1;
+    }
+#undef ACT1
+    DQNX_HIP_CHECK(hipGetLastError());
+    return DQNX_OK;
+}
+
 template <int R>
 int launch_act_r(const ActArgs& a, hipStream_t s) {
+    if constexpr (R <= 2) {   // (4 rows of MLP-284's slices would spill the 256 registers)
+        int t1 = 0, t2 = 0;
+        if (a.n <= R && ((uintptr_t)a.obs & 15) == 0 && act1_ok(a, &t1, &t2)) {
+            const int rc = a.act == DQNX_ACT_RELU ? launch_act1<R, DQNX_ACT_RELU>(a, t1, t2, s)
+                                                   : launch_act1<R, DQNX_ACT_ELU>(a, t1, t2, s);
+            if (rc != -1) return rc;
+        }
+    }
     const dim3 grid((a.out[0] + kActWaves - 1) / kActWaves, (a.n + R - 1) / R);
     if (act2_ok(a, R)) {
         const size_t lds2 = ((size_t)R * a.ld + R * 16 + (size_t)a.A * a.F) * sizeof(float);

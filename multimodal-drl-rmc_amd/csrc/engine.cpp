@@ -3795,7 +3795,47 @@ int dqnx_hard_update(dqnx_engine* e, void* stream) {
 
 // acting kernel geometry of a network (host only).  A two-stream net acts as its convs (one
 // launch each, act_hybrid.hip) followed by the MLP acting kernel on F = cat(flatten(conv), macro).
-static int act_plan(const dqnx_net_desc* net, NetPlan& np, ActArgs& a) {
+static int act_plan_build(const dqnx_net_desc* net, NetPlan& np, ActArgs& a);
+
+// act_plan for the acting path's every call (choose_actions: one per env step): the plans of the last
+// few network descriptions this thread acted with, keyed by the description's bytes (planning a net --
+// param layout, names -- costs ~3.4 us of host time, and dqnx_act_host / dqnx_agent_choose need it
+// three times per call).  *npp points into the cache: valid until this thread plans 4 other nets.
+static int act_plan(const dqnx_net_desc* net, const NetPlan** npp, ActArgs& a) {
+    struct Entry {
+        bool used = false;
+        dqnx_net_desc desc;
+        NetPlan np;
+        ActArgs a;
+        int rc = 0;
+    };
+    static thread_local Entry cache[4];
+    static thread_local int next = 0;
+    if (!net) return set_error(DQNX_EINVAL, "null net");
+    for (Entry& en : cache) {
+        if (en.used && !memcmp(&en.desc, net, sizeof(dqnx_net_desc))) {
+            if (en.rc) {   // (re-raise its error message)
+                NetPlan tmp;
+                return act_plan_build(net, tmp, a);
+            }
+            *npp = &en.np;
+            a = en.a;
+            return DQNX_OK;
+        }
+    }
+    Entry& en = cache[next];
+    next = (next + 1) & 3;
+    en.used = true;
+    memcpy(&en.desc, net, sizeof(dqnx_net_desc));
+    en.np = NetPlan();
+    en.rc = act_plan_build(net, en.np, en.a);
+    if (en.rc) return en.rc;
+    *npp = &en.np;
+    a = en.a;
+    return DQNX_OK;
+}
+
+static int act_plan_build(const dqnx_net_desc* net, NetPlan& np, ActArgs& a) {
     int rc = plan_net(net, np);
     if (rc) return rc;
     memset(&a, 0, sizeof(a));
@@ -3831,9 +3871,10 @@ static uint64_t act_conv_scratch_bytes(const NetPlan& np, int n, int D) {
 }
 
 uint64_t dqnx_act_scratch_bytes(const dqnx_net_desc* net, int32_t n) {
-    NetPlan np;
+    const NetPlan* npp = nullptr;
     ActArgs a;
-    if (act_plan(net, np, a)) return 0;
+    if (act_plan(net, &npp, a)) return 0;
+    const NetPlan& np = *npp;
     const uint64_t mlp = act_scratch_bytes(n, a.out[0], a.ld, a.L, a.L >= 2 ? a.out[1] : 0);
     if (!mlp) return 0;
     return (net->kind == DQNX_NET_MLP ? 0 : act_conv_scratch_bytes(np, n, a.D)) + mlp;
@@ -3852,11 +3893,12 @@ int dqnx_act(const dqnx_net_desc* net, const float* params, const float* obs, in
 static int act_impl(const dqnx_net_desc* net, const float* params, const float* obs, int32_t n, int32_t* actions,
                     float* values, void* scratch, uint64_t scratch_bytes, void* stream, uint32_t* done_flag,
                     uint32_t done_seq, bool* signals) {
-    NetPlan np;
+    const NetPlan* npp = nullptr;
     ActArgs a;
     if (signals) *signals = false;
-    int rc = act_plan(net, np, a);
+    int rc = act_plan(net, &npp, a);
     if (rc) return rc;
+    const NetPlan& np = *npp;
     if (n < 0 || (n > 0 && (!params || !obs || !actions || !scratch)))
         return set_error(DQNX_EINVAL, "dqnx_act: bad argument");
     const int R = n > 0 ? act_rows_per_block(n, a.ld) : 1;

@@ -229,6 +229,7 @@ class Agent:
         self._defer = os.environ.get("DQNX_AGENT_DEFER", "0") != "0"
         self._mt = self._live_mt()     # learn() stages and advances the live generator in one call
         self._choose_cache = None      # dqnx_agent_choose's arguments, resolved once
+        self._eps_logs = None          # (epsilon_start, epsilon_min), np.log of each
         self._learn_pending = False    # learn() recorded, not launched yet (DQNX_AGENT_DEFER=1)
         if os.environ.get("DQNX_AGENT_GRAPHS", "0") == "1":   # each learn step as one graph launch
             self.engine.set_graphs(True)
@@ -261,8 +262,11 @@ class Agent:
     def epsilon(self):
         """R:dqn/agent.py:86-90 (called once per env by choose_actions)."""
         if self.epsilon_exp_decay:
-            return np.exp(_interp2(self.step * self.n_env, self.epsilon_decay,
-                                   np.log(self.epsilon_start), np.log(self.epsilon_min)))
+            lg = getattr(self, "_eps_logs", None)
+            if lg is None or lg[0] != (self.epsilon_start, self.epsilon_min):   # (np.log once per setting)
+                lg = self._eps_logs = ((self.epsilon_start, self.epsilon_min), np.log(self.epsilon_start),
+                                       np.log(self.epsilon_min))
+            return np.exp(_interp2(self.step * self.n_env, self.epsilon_decay, lg[1], lg[2]))
         return _interp2(self.step * self.n_env, self.epsilon_decay, self.epsilon_start, self.epsilon_min)
 
     def choose_actions(self, obses):
