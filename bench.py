@@ -523,7 +523,7 @@ def rocprof_avg_us(stats_name, kernel):
         rows = list(csv.DictReader(f))
     for base in bases:
         for row in rows:
-            nm = row.get("Name", "")
+            nm = row.get("Name", "").replace("(anonymous namespace)::", "")
             short = nm.split("(")[0].split("<")[0].split("::")[-1].strip()
             if short == base and (best is None or float(row[key]) > float(best[key])):
                 best = row
