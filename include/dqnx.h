@@ -150,6 +150,7 @@ typedef struct dqnx_ctrl {
 #define DQNX_DEVERR_SAMPLE_TOO_LARGE 1   /* random.sample: k > n (ValueError) */
 #define DQNX_DEVERR_EMPTY_TREE 2         /* PER sample with total priority 0 */
 #define DQNX_DEVERR_PER_HANDOFF 3        /* internal: a PER update hand-off inside one launch timed out */
+#define DQNX_DEVERR_FWD_PAIR_HANDOFF 4   /* internal: the paired-column forward's H_1 hand-off timed out */
 /* internal: a write outside its range was skipped (bounds checks on the DP-bucket write paths) */
 #define DQNX_DEVERR_BOUNDS_ADAM_WIDE 16  /*   k_adam4 wide path: a float4 outside [e0, n_params) of the launch */
 #define DQNX_DEVERR_BOUNDS_ADAM_PERM 17  /*   k_adam4 wide path: a permuted conv-weight copy outside the range */

@@ -414,6 +414,7 @@ struct dqnx_engine {
     uint64_t ws_ring16[2] = {0, 0};   // bf16 engines: [cap][stride16] bf16 copies of obs / next_obs
     int stride16 = 0;
     uint64_t ws_npc = 0;   // numpy MT block cache (PER, fused plan)
+    uint64_t ws_pairflag = 0;   // paired forward: [3][tiles] H_1 hand-off words
     uint64_t ws_adam_tab = 0, ws_stamps = 0, ws_dhead = 0, ws_raw = 0, ws_trans = 0, ws_gtab = 0, ws_mtc = 0, ws_per_ticket = 0, ws_per_wl = 0, ws_per_wp = 0, ws_per_winit = 0, ws_per_last = 0, ws_per_wchg = 0;
     // fused plan: fragment-blocked weight copies [online fwd | target fwd | online chain] per layer
     uint64_t ws_wblk[2][FUSED_MAX_L] = {{0}}, ws_wblkT[FUSED_MAX_L] = {0};
@@ -486,6 +487,7 @@ struct dqnx_engine {
     FusedFwdArgs fplan;     // LDS geometry of the fused plan (valid when bwd_plan == 2)
     int fsplit = 1;         // layer-1 column parts of the split forward (1: one forward launch)
     int fsplit_mr = 1;      // 16-row blocks per workgroup of the split forward's layer-1 launch
+    int fpair = 0;          // DQNX_FWD_PAIR=1: one forward launch, layer 1's columns over 2 partner workgroups
     bool pf_valid = false;   // a prefetched minibatch for the next step sits in slot pf_slot
     bool pf_inlaunch = false;   // ... drawn by the previous step's forward launch (fused plan)
     int n_cu = 256;             // compute units of the device (hipDeviceAttributeMultiprocessorCount)
@@ -590,6 +592,7 @@ int layout(dqnx_engine* e) {
     }
     e->ws_adam_tab = sub((uint64_t)kAdamTable * 2 * 4);
     e->ws_stamps = sub(64 * 8);
+    if (e->fpair) e->ws_pairflag = sub((uint64_t)3 * ((e->Bl + 15) / 16) * 4);
     e->ws_per_ticket = sub(128);   // k_per_sample arrival counter (zero between launches); [16]: PER chunk
                                    // epoch; [20]: the in-launch tracking -> prop hand-off word
     // numpy MT block cache: only where the fused forward launch keeps it extended
@@ -1036,10 +1039,16 @@ void build_fused_steps(dqnx_engine* e, int flags, int32_t* idx, int32_t* phys, s
             fa.npc_blocks = np_cache_blocks(e->Bg);
         }
         fa.ab = adam_bias_args(e);
+        if (e->fpair && e->ws_pairflag && xcd_rows && L >= 2 && fa.mr == 1 && !fa.bf16 && fa.gw == 0) {
+            fa.phase = 3;   // (the row tiles keep their XCDs: the head kernel's mapping is unchanged)
+            fa.csplit = 2;
+            fa.pair_flags = at<uint32_t>(e, e->ws_pairflag);
+            fa.err = &ctrl->error;
+        }
         if (sample_next) {   // + the next step's minibatch into the staging slot (in-launch prefetch)
             // the one-pass shape only when the row tiles leave a CU idle (its LDS allows one
             // workgroup per CU); else the 3-block passes, whose LDS keeps two per CU
-            const int wgs = fa.tiles * nstreams + 1;
+            const int wgs = fa.tiles * nstreams * (fa.phase == 3 ? 2 : 1) + 1;
             fa.samp_shape = sample_next->k <= 2048 ? 1 : (wgs <= e->n_cu ? 3 : 2);
             fa.samp = *sample_next;
 #ifdef DQNX_STAMPS
@@ -2793,6 +2802,11 @@ int dqnx_engine_create(const dqnx_config* cfg, dqnx_engine** out) {
                 if (w <= 1) e->fsplit = 1;
                 else if (e->np.dense[0].out % (16 * w) == 0) e->fsplit = w;
             }
+            // opt-in (DQNX_FWD_PAIR=1, fp32): the one-launch forward with layer 1's columns over two
+            // partner workgroups of one XCD and an in-launch sc1 hand-off of the H_1 halves (fused.hip)
+            bool pair_ok = e->np.dense[0].out % 32 == 0 && e->np.dense[0].out <= 32 * FUSED_WAVES;
+            for (size_t l = 1; l < e->np.dense.size(); l++) pair_ok = pair_ok && e->np.dense[l].out <= 16 * FUSED_WAVES;
+            if (e->fsplit <= 1 && !e->fplan.bf16 && route_knob("DQNX_FWD_PAIR", 0) != 0 && pair_ok) e->fpair = 1;
             if (e->fsplit > 1) {   // layer 1's row tiles: 32 rows (each weight fragment feeds 2 MFMAs)
                 const int m = route_knob("DQNX_FWD_L1_MR", 2);
                 FusedFwdArgs t2 = e->fplan;

@@ -99,6 +99,9 @@ static void allow_lds(K kern, size_t bytes) {
 // drains vmcnt AND lgkmcnt at every use), and an out-of-range offset reads zeros without
 // touching memory (the prefetch overrun past the last chunk needs no branch).
 constexpr uint32_t kOOB = 0x80000000u;
+// buffer op cache-policy operand: sc1 (write-through stores, L1-bypassing loads on gfx950)
+constexpr int kCacheSC1 = 16;
+constexpr int kPairSpinLimit = 1 << 20;   // paired forward: hand-off polls (s_sleep 1 each) before the error
 
 __device__ __forceinline__ float4 bld4(__amdgpu_buffer_rsrc_t r, uint32_t off) {
     const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
@@ -154,6 +157,8 @@ __device__ __forceinline__ void bfetch(const WStream& w, int s, float4 (&d)[2]) 
 }
 
 // Open the stream over the wave's tiles (column tile offset c0t) and issue groups 0..FNB-2.
+// MAXTN: the most column tiles a wave of this kernel owns (1: the second register half is never used)
+template <int MAXTN = 2>
 __device__ __forceinline__ void stream_open(const float* blk, int ntiles, int nch, int c0t, const WaveCols& c,
                                             WStream& w, float4 (&wb)[FNB][FPF][2], int seed = 0) {
     const uint32_t lane = threadIdx.x & 63;
@@ -163,7 +168,7 @@ __device__ __forceinline__ void stream_open(const float* blk, int ntiles, int nc
     w.rot = DQNX_FWD_ROT ? seed % w.ng : 0;
     w.off[0] = ((uint32_t)(c0t + (c.tn >= 1 ? c.n0[0] >> 4 : 0)) * nch * 64u + lane) * 16u;
     w.off[1] = ((uint32_t)(c0t + (c.tn >= 2 ? c.n0[1] >> 4 : 0)) * nch * 64u + lane) * 16u;
-    if (c.tn == 2) {
+    if (MAXTN >= 2 && c.tn == 2) {
 #pragma unroll
         for (int u = 0; u + 1 < FNB; u++)
 #pragma unroll
@@ -239,10 +244,10 @@ __device__ __forceinline__ void wave_mma_t(const void* As, int sa, int ngroups, 
         }
     }
 }
-template <bool BF>
+template <bool BF, int MAXTN = 2>
 __device__ __forceinline__ void wave_mma(const void* As, int sa, int ngroups, const WaveCols& c, const WStream& w,
                                          float4 (&wb)[FNB][FPF][2], floatx4 (&acc)[2]) {
-    if (c.tn == 2) wave_mma_t<2, BF>(As, sa, ngroups, w, wb, acc);
+    if (MAXTN >= 2 && c.tn == 2) wave_mma_t<2, BF>(As, sa, ngroups, w, wb, acc);
     else if (c.tn == 1) wave_mma_t<1, BF>(As, sa, ngroups, w, wb, acc);
 }
 
@@ -310,11 +315,11 @@ __device__ __forceinline__ void wave_mma_mr_t(const void* As, int sa, int ngroup
         }
     }
 }
-template <bool BF, int MR>
+template <bool BF, int MR, int MAXTN = 2>
 __device__ __forceinline__ void wave_mma_rows(const void* As, int sa, int ngroups, const WaveCols& c, const WStream& w,
                                               float4 (&wb)[FNB][FPF][2], floatx4 (&acc)[MR][2]) {
     if constexpr (MR == 1) {
-        wave_mma<BF>(As, sa, ngroups, c, w, wb, acc[0]);
+        wave_mma<BF, MAXTN>(As, sa, ngroups, c, w, wb, acc[0]);
     } else {
         if (c.tn == 2) wave_mma_mr_t<2, BF, MR>(As, sa, ngroups, w, wb, acc);
         else if (c.tn == 1) wave_mma_mr_t<1, BF, MR>(As, sa, ngroups, w, wb, acc);
@@ -333,11 +338,16 @@ __device__ __forceinline__ void wave_mma_rows(const void* As, int sa, int ngroup
 // PH (phase): 0 the whole forward; 1 only layer 1, its columns split over a.csplit
 // workgroups per row tile, writing H_1 of every stream to HBM; 2 layers 2.. + head, reading
 // H_1 back (the split-layer pair: twice or four times the workgroups on the widest GEMM).
+// the paired forward (PH 3) needs two workgroups per CU resident (its 2 * tiles * streams grid exceeds
+// the chip at B = 1024): 4 waves per SIMD, i.e. <= 128 VGPRs
+template <int PH>
+constexpr int fwd_waves() { return PH == 3 ? 4 : 1; }
 template <int ACT, int NL, bool BF, int MR, int PH, int GW>
-__global__ __launch_bounds__(FT) void k_mlp_fwd(FusedFwdArgs a) {
+__global__ __launch_bounds__(FT) __attribute__((amdgpu_waves_per_eu(fwd_waves<PH>()))) void k_mlp_fwd(FusedFwdArgs a) {
     constexpr int RW = 16 * MR;          // rows per workgroup
     constexpr int GQ = BF ? fwd_gather_slots16<MR, GW>() : fwd_gather_slots<MR, GW>();   // gather slots per thread
     constexpr int LB = PH == 2 ? 1 : 0, LE = PH == 1 ? 1 : NL;   // layers of this launch
+    constexpr int MTN = PH == 3 ? 1 : 2;   // column tiles per wave (paired forward: <= 128 columns a layer)
     extern __shared__ __attribute__((aligned(16))) float lds[];
     // LDS tile b: pointer arithmetic on `lds` keeps the LDS address space visible to the
     // compiler (ds_read, not flat loads that share the vmcnt counter with the W stream)
@@ -366,12 +376,17 @@ __global__ __launch_bounds__(FT) void k_mlp_fwd(FusedFwdArgs a) {
     }
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int i = lane & 15, g = lane >> 4;
-    const int nsp = PH == 1 ? a.csplit : 1;
+    const int nsp = PH == 1 ? a.csplit : (PH == 3 ? 2 : 1);
     const int bid = (int)blockIdx.x - ((a.samp_shape || a.npc) ? 1 : 0);
     const int T0 = xcd_remap(bid, a.tiles * a.nstreams * nsp);
     int part = T0 % nsp, T = T0 / nsp;   // the parts of one row tile are neighbours (one XCD)
     int z = T / a.tiles, tile = T - z * a.tiles;
-    if (PH != 1 && a.xcd_rows) {   // row tile t of every stream on XCD t % 8 (tiles % 8 == 0)
+    if constexpr (PH == 3) {   // the two parts of a row tile: blocks bid and bid ^ 8 (one XCD, tiles % 8 == 0)
+        const int tp = a.tiles >> 3, L = bid >> 3, L2 = L >> 1;
+        part = L & 1;
+        z = L2 / tp;
+        tile = (L2 - z * tp) * 8 + (bid & 7);
+    } else if (PH != 1 && a.xcd_rows) {   // row tile t of every stream on XCD t % 8 (tiles % 8 == 0)
         const int tp = a.tiles >> 3, L = bid >> 3;
         z = L / tp;
         tile = (L - z * tp) * 8 + (bid & 7);
@@ -383,7 +398,7 @@ __global__ __launch_bounds__(FT) void k_mlp_fwd(FusedFwdArgs a) {
     const float* P = tgt ? a.tparams : a.params;
     const float* ring = (s == 0) ? a.ring_obs : a.ring_next;
     const bool keep = (s == 0);
-    const int coff = PH == 1 ? part * (a.out[0] / nsp) : 0;   // layer-1 columns of this part
+    const int coff = (PH == 1 || PH == 3) ? part * (a.out[0] / nsp) : 0;   // layer-1 columns of this part
 
     if (PH != 2) DQNX_STAMP(a.stamps, 24);   // (slots 24-27: the layer-1 launch of a split forward)
     // the step's Adam scalars for the update launch: a dependent ctrl -> table chain on the last
@@ -391,10 +406,10 @@ __global__ __launch_bounds__(FT) void k_mlp_fwd(FusedFwdArgs a) {
     if (PH != 2 && a.adam_ctrl && T0 == a.tiles * a.nstreams * nsp - 1 && tid == FT - 1) adam_advance(a.adam_ctrl, a.ab);
     float4 wb[FNB][FPF][2];
     WStream ws;
-    WaveCols c = wave_cols(PH == 1 ? a.out[0] / nsp : a.out[LB]);
+    WaveCols c = wave_cols((PH == 1 || PH == 3) ? a.out[0] / nsp : a.out[LB]);
     if constexpr (PH == 2) {
         // H_1 rows of this stream, written by the split layer-1 launch -> LDS (zero past the batch)
-        stream_open(a.wblk[tgt][1], a.out[1] >> 4, fwd_nch<BF>(a.in[1]), 0, c, ws, wb, tile);
+        stream_open<MTN>(a.wblk[tgt][1], a.out[1] >> 4, fwd_nch<BF>(a.in[1]), 0, c, ws, wb, tile);
         const int N0 = a.out[0], q4 = N0 >> 2;
         const float* h1 = a.H[0] + (int64_t)s * a.Bl * N0;
         float4 hv[2 * MR];
@@ -435,7 +450,7 @@ __global__ __launch_bounds__(FT) void k_mlp_fwd(FusedFwdArgs a) {
         const int rs4 = a.ring_stride >> 2;
         // branch-free: every slot loads (clamped row / column) and selects zero afterwards,
         // so the loads issue back to back (one phys round trip, then one ring round trip)
-        if (DQNX_FUSED_ORDER == 1) stream_open(a.wblk[tgt][0], a.out[0] >> 4, fwd_nch<BF>(a.in[0]), coff >> 4, c, ws, wb, tile);
+        if (DQNX_FUSED_ORDER == 1) stream_open<MTN>(a.wblk[tgt][0], a.out[0] >> 4, fwd_nch<BF>(a.in[0]), coff >> 4, c, ws, wb, tile);
         int32_t slot[GQ];
 #pragma unroll
         for (int j = 0; j < GQ; j++) {
@@ -447,7 +462,7 @@ __global__ __launch_bounds__(FT) void k_mlp_fwd(FusedFwdArgs a) {
         int32_t tslot = 0;
         const bool keep0 = keep && part == 0;   // one part writes the stream-0 copies
         if (keep0 && tid < nb) tslot = a.phys[b0 + tid];
-        if (DQNX_FUSED_ORDER == 0) stream_open(a.wblk[tgt][0], a.out[0] >> 4, fwd_nch<BF>(a.in[0]), coff >> 4, c, ws, wb, tile);
+        if (DQNX_FUSED_ORDER == 0) stream_open<MTN>(a.wblk[tgt][0], a.out[0] >> 4, fwd_nch<BF>(a.in[0]), coff >> 4, c, ws, wb, tile);
         u32x4 xv[GQ];
         const uint16_t* ring16 = BF ? ((s == 0) ? a.ring16_obs : a.ring16_next) : nullptr;
 #pragma unroll
@@ -463,7 +478,7 @@ __global__ __launch_bounds__(FT) void k_mlp_fwd(FusedFwdArgs a) {
             if (!ok) x = u32x4{0u, 0u, 0u, 0u};
             xv[j] = x;
         }
-        if (DQNX_FUSED_ORDER == 2) stream_open(a.wblk[tgt][0], a.out[0] >> 4, fwd_nch<BF>(a.in[0]), coff >> 4, c, ws, wb, tile);
+        if (DQNX_FUSED_ORDER == 2) stream_open<MTN>(a.wblk[tgt][0], a.out[0] >> 4, fwd_nch<BF>(a.in[0]), coff >> 4, c, ws, wb, tile);
         // after the row loads are in flight: the transition scalars' own round trip overlaps them
         if (keep0 && tid < nb)
             a.trans[b0 + tid] = make_float4(__int_as_float(a.act[tslot]), a.rew[tslot], a.done[tslot], 0.f);
@@ -507,21 +522,24 @@ __global__ __launch_bounds__(FT) void k_mlp_fwd(FusedFwdArgs a) {
 #pragma unroll
         for (int t = 0; t < 2; t++) bias[t] = bias_p[(t < c.tn ? c.n0[t] : 0) + i];   // branch-free
         floatx4 acc[MR][2];
-        wave_mma_rows<BF, MR>(FBUF(cur), l == 0 ? a.sx : a.sh, fwd_groups<BF>(K), c, ws, wb, acc);
+        wave_mma_rows<BF, MR, MTN>(FBUF(cur), l == 0 ? a.sx : a.sh, fwd_groups<BF>(K), c, ws, wb, acc);
         DQNX_STAMP(a.stamps, 27 + 2 * l);
         const WaveCols cl = c;
+        // the paired forward's part 1 ends after layer 1: it publishes its H_1 half (below)
+        const bool pub = PH == 3 && l == 0 && part == 1;
         // next layer's weight stream in flight during the epilogue + barrier
-        if (l + 1 < LE) {
+        if (l + 1 < LE && !pub) {
             c = wave_cols(a.out[l + 1]);
-            stream_open(a.wblk[tgt][l + 1], a.out[l + 1] >> 4, fwd_nch<BF>(a.in[l + 1]), 0, c, ws, wb, tile);
+            stream_open<MTN>(a.wblk[tgt][l + 1], a.out[l + 1] >> 4, fwd_nch<BF>(a.in[l + 1]), 0, c, ws, wb, tile);
         }
         float* Hs = FBUF(cur ^ 1);
-        // H to HBM: stream 0 (the backward's operands); the split layer 1 writes every stream's
-        float* Hg = (PH == 1) ? a.H[0] + (int64_t)s * a.Bl * N : (keep ? a.H[l] : nullptr);
+        // H to HBM: stream 0 (the backward's operands); the split layer 1 writes every stream's; the
+        // paired forward's part 1 writes its half from the LDS tile, 16 bytes a lane (below)
+        float* Hg = (PH == 1) ? a.H[0] + (int64_t)s * a.Bl * N : ((keep && !pub) ? a.H[l] : nullptr);
         // bf16 + DQNX_DWB_T=1 (k_dw_bf16d): stream 0's H_l also as a slab-transposed copy (4 consecutive samples per lane: 8 bytes)
         uint16_t* Ht = (BF && PH == 0 && keep) ? a.HT16[l] : nullptr;
 #pragma unroll
-        for (int t = 0; t < 2; t++) {
+        for (int t = 0; t < MTN; t++) {
             if (t >= cl.tn) continue;
             const int col = cl.n0[t] + i;
 #pragma unroll
@@ -561,6 +579,49 @@ __global__ __launch_bounds__(FT) void k_mlp_fwd(FusedFwdArgs a) {
             }
         }
         if constexpr (PH == 1) return;
+        if constexpr (PH == 3 && !BF) {
+            if (l == 0) {
+                // H_1 halves of the row tile: part 1 publishes (write-through sc1 16-byte stores of its LDS
+                // half, every storing wave drained, then ONE lane's sc1 flag store behind a workgroup
+                // barrier); part 0's polling lane matches the flag with sc1 loads, and after a barrier every
+                // wave loads the half with sc1 loads into its tile (MI355X_MICROARCH.md, the measured
+                // hand-off table's first row).  Stream 0's half is also the backward's H_1.
+                uint32_t* flag = a.pair_flags + (z * a.tiles + tile);
+                const int hw = N >> 1, q4 = hw >> 2;
+                float* Hx = a.H[0] + (int64_t)s * a.Bl * N + (int64_t)b0 * N;   // [nb][N] of this stream
+                const __amdgpu_buffer_rsrc_t xr = wave_rsrc(Hx, (uint32_t)nb * N * 4u);   // rows past nb: dropped / 0
+                lds_barrier();
+                if (pub) {
+                    for (int q = tid; q < 16 * q4; q += FT) {
+                        const int r = q / q4, c4 = q - r * q4;
+                        const u32x4 v = *reinterpret_cast<const u32x4*>(Hs + r * a.sh + 4 * c4);
+                        __builtin_amdgcn_raw_buffer_store_b128(v, xr, (uint32_t)(r * N + hw + 4 * c4) * 4u, 0, kCacheSC1);
+                    }
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                    lds_barrier();
+                    if (tid == 0) __hip_atomic_store(flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    return;
+                }
+                if (tid == 0) {
+                    int spins = 0;
+                    while (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) {
+                        if (++spins > kPairSpinLimit) {   // (never expected: the partner is dispatched right behind)
+                            if (a.err) __hip_atomic_store(a.err, (int32_t)DQNX_DEVERR_FWD_PAIR_HANDOFF, __ATOMIC_RELAXED,
+                                                          __HIP_MEMORY_SCOPE_AGENT);
+                            break;
+                        }
+                        __builtin_amdgcn_s_sleep(1);
+                    }
+                    __hip_atomic_store(flag, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // zero for the next launch
+                }
+                lds_barrier();
+                for (int q = tid; q < 16 * q4; q += FT) {
+                    const int r = q / q4, c4 = q - r * q4;
+                    const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(xr, (uint32_t)(r * N + hw + 4 * c4) * 4u, 0, kCacheSC1);
+                    *reinterpret_cast<u32x4*>(Hs + r * a.sh + hw + 4 * c4) = v;
+                }
+            }
+        }
         lds_barrier();
         DQNX_STAMP(a.stamps, 28 + 2 * l);
         cur ^= 1;
@@ -1343,6 +1404,12 @@ int launch_fused_fwd(const FusedFwdArgs& a, int act, hipStream_t s) {
     if (a.phase != 0 && (a.L < 2 || a.mr != (a.phase == 1 ? a.mr : 1) ||
                          (a.phase == 1 && (a.csplit < 1 || a.out[0] % (16 * a.csplit)))))
         return set_error(DQNX_EUNSUPPORTED, "split forward: L >= 2, 16-row tiles (layer 1: 16, 32 or 64), layer 1 width / parts a multiple of 16");
+    bool pair_ok = a.L >= 2 && a.mr == 1 && !a.bf16 && !a.gw && a.xcd_rows && a.tiles % 8 == 0 && a.out[0] % 32 == 0 &&
+                   a.out[0] <= 32 * FW && a.pair_flags;
+    for (int l = 1; l < a.L; l++) pair_ok = pair_ok && a.out[l] <= 16 * FW;   // one column tile per wave
+    if (a.phase == 3 && !pair_ok)
+        return set_error(DQNX_EUNSUPPORTED, "paired forward: fp32, L >= 2, 16-row tiles, tiles %% 8 == 0, layer 1 width a "
+                                            "multiple of 32 and <= %d, later layers <= %d wide", 32 * FW, 16 * FW);
     if (a.gw && (a.phase != 0 || a.mr != 1))
         return set_error(DQNX_EUNSUPPORTED, "fused forward: rows wider than %d columns take the one-launch 16-row plan", 4 * FWD_NARROW_Q4);
     if (a.samp_shape && (a.phase == 2 || a.samp_shape > 3 || a.samp.k > FWD_SAMPLE_MAX_K ||
@@ -1352,7 +1419,8 @@ int launch_fused_fwd(const FusedFwdArgs& a, int act, hipStream_t s) {
         return set_error(DQNX_EUNSUPPORTED, "bf16 forward: needs the ring's bf16 copies (16-byte rows)");
     if (a.npc && (a.samp_shape || a.phase == 2 || a.npc_blocks > NPC_MAX_BLOCKS))
         return set_error(DQNX_EUNSUPPORTED, "forward MT-cache workgroup: not with the sampler workgroup / phase 2");
-    const dim3 grid(a.tiles * a.nstreams * (a.phase == 1 ? a.csplit : 1) + ((a.samp_shape || a.npc) ? 1 : 0)), block(FT);
+    const dim3 grid(a.tiles * a.nstreams * (a.phase == 1 ? a.csplit : (a.phase == 3 ? 2 : 1)) +
+                    ((a.samp_shape || a.npc) ? 1 : 0)), block(FT);
     size_t shm = (size_t)(a.buf0 + a.buf1) * 4;
     if (shm < (size_t)DQNX_FUSED_LDS_MIN) shm = DQNX_FUSED_LDS_MIN;
     if (shm < (size_t)a.lds_min) shm = (size_t)a.lds_min;
@@ -1380,6 +1448,7 @@ int launch_fused_fwd(const FusedFwdArgs& a, int act, hipStream_t s) {
             }                                                                                        \
         }                                                                                            \
         else if (a.phase == 2) { if constexpr (NLV >= 2) FUSED_FWD_MR(ACTV, NLV, BFV, 1, 2); }        \
+        else if (a.phase == 3) { if constexpr (NLV >= 2 && !BFV) FUSED_FWD_GW(ACTV, NLV, BFV, 1, 3, 0); } \
         else if (a.mr == 4) FUSED_FWD_MR(ACTV, NLV, BFV, 4, 0);                                      \
         else if (a.mr == 2) FUSED_FWD_MR(ACTV, NLV, BFV, 2, 0);                                      \
         else FUSED_FWD_MR(ACTV, NLV, BFV, 1, 0);                                                     \

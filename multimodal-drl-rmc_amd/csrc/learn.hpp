@@ -498,8 +498,12 @@ struct FusedFwdArgs {
     int mr;                      // 16-row tiles per workgroup (1, 2 or 4; `tiles` counts 16*mr-row tiles)
     int gw;                      // gather width class: 0 rows of <= 288 multiplied columns (FWD_NARROW_Q4
                                  // float4), 1 wider (whole forward, 16-row tiles only)
-    int phase;                   // 0 whole forward; 1 layer 1 split over csplit parts; 2 layers 2.. + head
+    int phase;                   // 0 whole forward; 1 layer 1 split over csplit parts; 2 layers 2.. + head;
+                                 // 3 whole forward, layer 1's columns over 2 partner workgroups of one XCD
+                                 // (in-launch H_1 hand-off, DQNX_FWD_PAIR)
     int csplit;
+    uint32_t* pair_flags;        // phase 3: [nstreams * tiles] hand-off words (zero between launches)
+    int32_t* err;                // phase 3: dqnx_ctrl.error (hand-off timeout)
     int sx, sh;                  // LDS row strides (elements: floats, or bf16 under bf16) of the input / hidden tiles
     int buf0, buf1;              // LDS buffer sizes (floats)
     int kpad[FUSED_MAX_L];       // layer inputs zero padded to kpad (blocked copies): fp32 a multiple of 64, bf16 of 32

@@ -37,6 +37,7 @@ CHOOSE_GIL_HELD = 0x1
 DEVERR_SAMPLE_TOO_LARGE = 1
 DEVERR_EMPTY_TREE = 2
 DEVERR_PER_HANDOFF = 3
+DEVERR_FWD_PAIR_HANDOFF = 4
 DEVERR_BOUNDS = {16: "k_adam4 wide path: a float4 outside the launch's element range",
                  17: "k_adam4 wide path: a permuted conv-weight copy outside the launch's range",
                  18: "k_micro_dw: a split-K slab tile outside its conv's slabs"}

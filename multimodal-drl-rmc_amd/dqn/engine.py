@@ -593,6 +593,8 @@ def raise_device_error(err: int):
         raise RuntimeError("libdqnx: PER sample from a SumTree with total priority 0")
     if err == C.DEVERR_PER_HANDOFF:
         raise RuntimeError("libdqnx: PER tree update hand-off timed out inside a launch (internal error)")
+    if err == C.DEVERR_FWD_PAIR_HANDOFF:
+        raise RuntimeError("libdqnx: paired-column forward hand-off timed out inside a launch (internal error)")
     if err in C.DEVERR_BOUNDS:
         raise RuntimeError(f"libdqnx: out-of-range write skipped (internal error): {C.DEVERR_BOUNDS[err]}")
     if err:

@@ -183,6 +183,39 @@ def test_gpu_act_host_shared_scratch_across_row_counts(net):
         _check(vals.cpu().numpy(), ref, out)
 
 
+@pytest.mark.parametrize("obs_dim,n", [(3000, 3), (3000, 2), (5000, 2), (5000, 1)])
+def test_gpu_act_host_wide_inputs_several_row_groups(obs_dim, n):
+    """dqnx_act_host on inputs wider than 2048 / 4096 floats, where a workgroup takes 2 / 1 rows:
+    a launch with several row groups stores no completion word, so the call must not poll for one (it
+    used to spin 0.5 s per call before falling back to a stream synchronize).  Actions equal dqnx_act's,
+    and 20 calls finish well inside one poll timeout."""
+    import ctypes
+    import time
+
+    from dqn import _capi as C
+    ospec, espec = O.mlp_spec(obs_dim, 8, "dueling"), E.mlp_spec(obs_dim, 8, "dueling")
+    params = O.reference_init(ospec, 8)
+    flat = _flat(espec, params)
+    desc = espec.to_c()
+    L = C.lib()
+    nb = int(L.dqnx_act_host_scratch_bytes(ctypes.byref(desc), n))
+    scratch = torch.zeros((nb + 15) // 16 * 4, dtype=torch.float32, device="cuda")
+    stream = torch.cuda.current_stream().cuda_stream
+    x = np.ascontiguousarray(np.random.default_rng(obs_dim + n).random((n, obs_dim), dtype=np.float32))
+    out = np.full(n, -1, dtype=np.int32)
+    C.check(L.dqnx_act_host(ctypes.byref(desc), flat.data_ptr(), x.ctypes.data, n, out.ctypes.data,
+                            scratch.data_ptr(), scratch.numel() * 4, stream), "act_host")
+    vals = torch.empty(n, 8, dtype=torch.float32, device="cuda")
+    acts = E.act(espec, flat, torch.from_numpy(x).cuda(), vals).cpu().numpy()
+    assert np.array_equal(out, acts), (out, acts)
+    t0 = time.perf_counter()
+    for _ in range(20):
+        C.check(L.dqnx_act_host(ctypes.byref(desc), flat.data_ptr(), x.ctypes.data, n, out.ctypes.data,
+                                scratch.data_ptr(), scratch.numel() * 4, stream), "act_host")
+    assert time.perf_counter() - t0 < 0.4, "act_host waited for a completion word its launch never stores"
+    assert np.array_equal(out, acts)
+
+
 @pytest.mark.parametrize("kernel", ["0", "1"])
 @pytest.mark.parametrize("head", ["dueling", "linear"])
 @pytest.mark.parametrize("n", [1, 2, 5, 64])

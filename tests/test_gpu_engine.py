@@ -242,6 +242,25 @@ def test_gpu_split_forward_identical(monkeypatch, split, compute):
     assert torch.equal(outs[0][1], outs[1][1])
 
 
+@pytest.mark.parametrize("algo,batch", [("DuelingDoubleDQNAgent", 1024), ("DuelingDoubleDQNAgent", 1020),
+                                        ("DQNAgent", 1024), ("DoubleDQNAgent", 4096)])
+def test_gpu_pair_forward_identical(monkeypatch, algo, batch):
+    """DQNX_FWD_PAIR=1: the one-launch forward with layer 1's columns over two partner workgroups
+    and the in-launch hand-off of the H_1 halves gives bitwise the same steps as the default
+    forward, over enough steps that every hand-off word is reused; ragged last tile at 1020."""
+    outs = []
+    for pair in ("1", "0"):
+        monkeypatch.setenv("DQNX_FWD_PAIR", pair)
+        o, e = make_pair(algo, 284, batch, 20000, 20000, 45)
+        for _ in range(8):
+            e.learn_step(soft_update=True)
+        torch.cuda.synchronize()
+        e.check_device_error()
+        outs.append((e.params.clone(), e.target_params.clone(), e.q.clone()))
+    for x, y in zip(outs[0], outs[1]):
+        assert torch.equal(x, y)
+
+
 @pytest.mark.parametrize("split", ["2", "4"])
 def test_gpu_fused_head_split_identical(monkeypatch, split):
     """The fused plan's head/dZ-chain kernel with the last dZ split over 2 or 4 workgroups per
