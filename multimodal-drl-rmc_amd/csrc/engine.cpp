@@ -383,7 +383,9 @@ static bool micro_geom(const NetPlan& np, MicroConv* c) {
         m.Ci = cp.Ci; m.Hi = cp.Hi; m.Wi = cp.Wi; m.Co = cp.Co; m.Ho = cp.Ho; m.Wo = cp.Wo;
         m.sh = cp.sh; m.sw = cp.sw;
         m.woff = cp.off;
-        m.cs = cp.Co + 8;
+        // LDS floats per pixel: Co + 8 (b128 reads conflict-free); DQNX_MICRO_PIXPAD=4: Co + 4 (also
+        // conflict-free for the stride-2 taps; measured equal, kept for the LDS counter comparison)
+        m.cs = cp.Co + (route_knob("DQNX_MICRO_PIXPAD", 8) == 4 ? 4 : 8);
     }
     return true;
 }

@@ -680,7 +680,7 @@ struct MicroConv {
     int64_t woff;              // flat offset of W [Co][Ci][3][3] (the bias follows)
     const float* wp[2];        // l >= 1: [Co][9][Ci] copies of the online / target W (k_conv_perm mode 0)
     const float* wT;           // l >= 1: [Ci][9][Co] copy of the online W (mode 1, data gradient)
-    int cs;                    // LDS floats per pixel of this conv's output image (Co + 8: b128 reads conflict-free)
+    int cs;                    // LDS floats per pixel of this conv's output image (Co + 8: b128 reads conflict-free; Co + 4 knob)
     int lds;                   // LDS float offset of this conv's output images [S][Ho*Wo][cs]
     float* hc;                 // l < nc - 1: stream-0 output (ELU applied), NHWC [Bl][Ho*Wo][Co]
     float* dz;                 // stream-0 dZ of this conv's output (ELU' applied), NHWC [Bl][Ho*Wo][Co]

@@ -72,7 +72,7 @@ static int fwd_lds_floats(const MicroConv* c, int nc, int S, int* x0, int* zero,
     int cur = 0;
     for (int l = 0; l + 1 < nc; l++) {
         offs[l] = cur;
-        cur += S * c[l].Ho * c[l].Wo * (c[l].Co + 8);
+        cur += S * c[l].Ho * c[l].Wo * c[l].cs;
     }
     *x0 = cur;
     cur += (S * c[0].Ci * c[0].Hi * c[0].Wi + 3) & ~3;
@@ -116,7 +116,7 @@ static int dx_lds_floats(const MicroConv* c, int nc, int S, int* lds_d, int* zer
     for (int l = 0; l < nc; l++) lds_d[l] = -1;
     for (int l = 1; l < nc; l++) {   // dZ of conv l (conv 1's dZ goes to HBM only)
         lds_d[l] = cur;
-        cur += S * c[l].Ho * c[l].Wo * (c[l].Co + 8);
+        cur += S * c[l].Ho * c[l].Wo * c[l].cs;
     }
     *zero = cur;
     return cur + MICRO_ZERO;

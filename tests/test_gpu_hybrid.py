@@ -268,6 +268,7 @@ def _run_hybrid_steps(algo, batch, steps, seed):
     ("DQNX_FWD_ULOAD", "1", "0"),    # dense 2: unconditional float4 loads vs the guarded loader
     ("DQNX_BWD_ULOAD", "1", "0"),    # dense backward: unconditional float4 / pair loads vs the guarded loader
     ("DQNX_BWD_TS", "64", "32"),     # dense-1 backward: 64 x 64 vs 32 x 32 tiles
+    ("DQNX_MICRO_PIXPAD", "4", "8"), # micro forward / data gradients: LDS pixel stride Co + 4 vs Co + 8
 ])
 @pytest.mark.parametrize("algo,batch", [("DuelingDoubleDQNAgent", 256), ("PerDuelingDoubleDQNAgent", 100)])
 def test_gpu_hybrid_head_variants_bit_identical(monkeypatch, knob, a, b, algo, batch):
