@@ -57,7 +57,7 @@ __global__ __launch_bounds__(SAMPLE_NT) void k_sample_uniform_g(SampleArgs a) {
 
 
 // k beyond the LDS hash tables, population <= 2^20 (sample_bitmap_body): the dedup state in LDS
-constexpr int SAMPLE_BITMAP_AH = 4, SAMPLE_BITMAP_BMX = 2048;   // 156 KiB of LDS: passes of 4 new blocks
+constexpr int SAMPLE_BITMAP_AH = 5, SAMPLE_BITMAP_BMX = 2048;   // 158.7 KiB of LDS: passes of 5 new blocks (4: 14 passes at k = 32768)
 __global__ __launch_bounds__(SAMPLE_NT) void k_sample_bitmap(SampleArgs a) {
     __shared__ SampleBitmapLds<SAMPLE_NT, SAMPLE_BITMAP_AH, SAMPLE_BITMAP_BMX> S;
     if (blockIdx.x > 0) {
