@@ -400,34 +400,42 @@ __device__ __forceinline__ float group_sum(float v) {   // over TPN consecutive 
     for (int o = TPN / 2; o >= 1; o >>= 1) v += __shfl_xor(v, o, kWave);
     return v;
 }
-template <int R, int ACT, int TPN1, int TPN2, int W1S, int W2S>
+// G > 1 (DQNX_ACT1_G): the same over G workgroups on G CUs, workgroup g owning layer-1 neurons
+// [g h0/G, (g+1) h0/G) and its share of every layer-2 pre-activation (k_act_mlp2's split, G-fold wider
+// slices): each CU streams 1/G of the weights.  The shares go out write-through (sc1), every storing
+// wave drains vmcnt, a barrier, ONE lane's agent-scope ticket; the workgroup whose ticket comes back last
+// sums the shares in workgroup order with sc1 loads and runs bias + activation, the head and the argmax
+// (MI355X_MICROARCH.md's measured hand-off table, first row).
+template <int R, int ACT, int G, int TPN1, int TPN2, int W1S, int W2S>
 __global__ __launch_bounds__(kAct1Threads) void k_act_mlp1(ActArgs a) {
     extern __shared__ float lds[];
+    __shared__ int s_last;
     const int tid = threadIdx.x;
     const int D = a.D, h0 = a.out[0], h1 = a.out[1], F = a.F, A = a.A;
     const int n = a.n;
-    const int d4 = D >> 2, h04 = h0 >> 2;
+    const int h0g = h0 / G, g0 = (G > 1 ? (int)blockIdx.x : 0) * h0g;   // this workgroup's layer-1 neurons
+    const int d4 = D >> 2, h04 = h0 >> 2, h0g4 = h0g >> 2;
     float4* x4 = reinterpret_cast<float4*>(lds);          // [R][d4] obs
-    float* y1 = lds + R * D;                               // [R][h0]
-    float* y2 = y1 + R * h0;                               // [R][h1]
+    float* y1 = lds + R * D;                               // [R][h0g]
+    float* y2 = y1 + R * h0g;                              // [R][h1]
     float* q = y2 + R * h1;                                // [R][16]
     const float* P = a.params;
     // (0) every load at once: layer 1's row slices, layer 2's, the head's float4, the biases, the obs
-    const int j = tid / TPN1, q1 = tid % TPN1;
-    const float4* W1 = reinterpret_cast<const float4*>(P + a.off[0]) + (int64_t)(j < h0 ? j : 0) * d4;
+    const int jl = tid / TPN1, q1 = tid % TPN1, j = g0 + jl;
+    const float4* W1 = reinterpret_cast<const float4*>(P + a.off[0]) + (int64_t)(jl < h0g ? j : 0) * d4;
     float4 w1[W1S];
 #pragma unroll
     for (int i = 0; i < W1S; i++) {
         const int c = q1 + TPN1 * i;
-        w1[i] = (c < d4 && j < h0) ? W1[c] : make_float4(0.f, 0.f, 0.f, 0.f);
+        w1[i] = (c < d4 && jl < h0g) ? W1[c] : make_float4(0.f, 0.f, 0.f, 0.f);
     }
     const int o = tid / TPN2, q2 = tid % TPN2;
-    const float4* W2 = reinterpret_cast<const float4*>(P + a.off[1]) + (int64_t)(o < h1 ? o : 0) * h04;
+    const float4* W2 = reinterpret_cast<const float4*>(P + a.off[1]) + (int64_t)(o < h1 ? o : 0) * h04 + (g0 >> 2);
     float4 w2[W2S];
 #pragma unroll
     for (int i = 0; i < W2S; i++) {
         const int c = q2 + TPN2 * i;
-        w2[i] = (c < h04 && o < h1) ? W2[c] : make_float4(0.f, 0.f, 0.f, 0.f);
+        w2[i] = (c < h0g4 && o < h1) ? W2[c] : make_float4(0.f, 0.f, 0.f, 0.f);
     }
     const float* Hh = P + a.head_off;
     const float* Wh = a.dueling ? Hh + F + 1 : Hh;   // advantage stream (R:dqn/network.py:110-117)
@@ -436,7 +444,7 @@ __global__ __launch_bounds__(kAct1Threads) void k_act_mlp1(ActArgs a) {
     const int hr = tid / (F / 2), hc = 2 * (tid % (F / 2));
     const float wh0 = hr < A ? Wh[(int64_t)hr * F + hc] : 0.f;
     const float wh1 = hr < A ? Wh[(int64_t)hr * F + hc + 1] : 0.f;
-    const float b1 = j < h0 ? P[a.off[0] + (int64_t)h0 * D + j] : 0.f;
+    const float b1 = jl < h0g ? P[a.off[0] + (int64_t)h0 * D + j] : 0.f;
     const float b2 = o < h1 ? P[a.off[1] + (int64_t)h1 * h0 + o] : 0.f;
     const float bh = hr < A ? Wh[(int64_t)A * F + hr] : 0.f;
     for (int e = tid; e < R * d4; e += kAct1Threads) {
@@ -444,7 +452,7 @@ __global__ __launch_bounds__(kAct1Threads) void k_act_mlp1(ActArgs a) {
         x4[e] = r < n ? reinterpret_cast<const float4*>(a.obs + (int64_t)r * D)[c] : make_float4(0.f, 0.f, 0.f, 0.f);
     }
     __syncthreads();
-    // (1) layer 1
+    // (1) layer 1 (this workgroup's neurons)
 #pragma unroll
     for (int r = 0; r < R; r++) {
         float acc = 0.f;
@@ -460,28 +468,60 @@ __global__ __launch_bounds__(kAct1Threads) void k_act_mlp1(ActArgs a) {
             }
         }
         acc = group_sum<TPN1>(acc);
-        if (q1 == 0 && j < h0) y1[r * h0 + j] = act_fwd<ACT>(acc + b1);
+        if (q1 == 0 && jl < h0g) y1[r * h0g + jl] = act_fwd<ACT>(acc + b1);
     }
     __syncthreads();
-    // (2) layer 2
+    // (2) layer 2: the pre-activations (G == 1), or this workgroup's share of them
     const float4* y14 = reinterpret_cast<const float4*>(y1);
+    float z[R];
 #pragma unroll
     for (int r = 0; r < R; r++) {
         float acc = 0.f;
 #pragma unroll
         for (int i = 0; i < W2S; i++) {
             const int c = q2 + TPN2 * i;
-            if (c < h04) {
-                const float4 xv = y14[r * h04 + c];
+            if (c < h0g4) {
+                const float4 xv = y14[r * h0g4 + c];
                 acc = fmaf(w2[i].x, xv.x, acc);
                 acc = fmaf(w2[i].y, xv.y, acc);
                 acc = fmaf(w2[i].z, xv.z, acc);
                 acc = fmaf(w2[i].w, xv.w, acc);
             }
         }
-        acc = group_sum<TPN2>(acc);
-        if (q2 == 0 && o < h1) y2[r * h1 + o] = act_fwd<ACT>(acc + b2);
+        z[r] = group_sum<TPN2>(acc);
     }
+    if constexpr (G > 1) {
+        float* part = a.scratch;   // [G][R][h1] (one row group)
+        if (q2 == 0 && o < h1) {
+#pragma unroll
+            for (int r = 0; r < R; r++)
+                __hip_atomic_store(part + ((int64_t)blockIdx.x * R + r) * h1 + o, z[r], __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (tid == 0) {
+            const uint32_t t = __hip_atomic_fetch_add(a.tickets, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const int last = t == (uint32_t)G - 1;
+            if (last) __hip_atomic_store(a.tickets, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // next launch
+            s_last = last;
+        }
+        __syncthreads();
+        if (!s_last) return;
+        if (q2 == 0 && o < h1) {
+#pragma unroll
+            for (int r = 0; r < R; r++) {
+                float sum = 0.f;
+#pragma unroll
+                for (int w = 0; w < G; w++)
+                    sum += __hip_atomic_load(part + ((int64_t)w * R + r) * h1 + o, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                z[r] = sum;
+            }
+        }
+    }
+#pragma unroll
+    for (int r = 0; r < R; r++)
+        if (q2 == 0 && o < h1) y2[r * h1 + o] = act_fwd<ACT>(z[r] + b2);
     __syncthreads();
     // (3) the head: F / 2 lanes per output row (a power of two, <= 64: act1_ok)
 #pragma unroll
@@ -514,13 +554,15 @@ __global__ __launch_bounds__(kAct1Threads) void k_act_mlp1(ActArgs a) {
 // k_act_mlp1 applies: n <= 2 rows, two hidden layers, widths dividing the 1024 threads into powers of
 // two per neuron, every weight row a whole number of 16-byte pieces within the register budget, a
 // head whose F / 4 lanes per row fit one wave.  (DQNX_ACT1=0: the multi-workgroup kernels.)
-static bool act1_ok(const ActArgs& a, int* tpn1, int* tpn2) {
+static bool act1_ok(const ActArgs& a, int G, int* tpn1, int* tpn2) {
     if (a.L != 2 || a.n > 4 || a.A > 16 || route_knob("DQNX_ACT1", 1) == 0) return false;
     const int D = a.D, h0 = a.out[0], h1 = a.out[1], F = a.F;
-    if (D % 4 || h0 % 4 || F % 4 || (a.off[0] & 3) || (a.off[1] & 3) || F != h1) return false;
+    if (D % 4 || h0 % (4 * G) || F % 4 || (a.off[0] & 3) || (a.off[1] & 3) || F != h1) return false;
+    if (G > 1 && (!a.scratch || !a.tickets)) return false;
     auto pow2 = [](int v) { return v > 0 && (v & (v - 1)) == 0; };
-    if (!pow2(h0) || !pow2(h1) || h0 > kAct1Threads || h1 > kAct1Threads) return false;
-    const int t1 = kAct1Threads / h0, t2 = kAct1Threads / h1;
+    const int h0g = h0 / G;
+    if (!pow2(h0g) || !pow2(h1) || h0g > kAct1Threads || h1 > kAct1Threads) return false;
+    const int t1 = kAct1Threads / h0g, t2 = kAct1Threads / h1;
     const int lpr = F / 2;   // head lanes per row
     if (!pow2(lpr) || lpr > kWave || a.A * lpr > kAct1Threads) return false;
     *tpn1 = t1;
@@ -539,16 +581,28 @@ static bool act2_ok(const ActArgs& a, int R) {
 }
 
 template <int R, int ACT>
-static int launch_act1(const ActArgs& a, int t1, int t2, hipStream_t s) {
-    const size_t lds = ((size_t)R * (a.D + a.out[0] + a.out[1] + 16)) * sizeof(float);
-    const int s1 = (a.D / 4 + t1 - 1) / t1, s2 = (a.out[0] / 4 + t2 - 1) / t2;   // float4 slots per thread
-#define ACT1(T1, T2, S1, S2) DQNX_LAUNCH((k_act_mlp1<R, ACT, T1, T2, S1, S2>), dim3(1), dim3(kAct1Threads), lds, s, a)
+static int launch_act1(const ActArgs& a, int G, int t1, int t2, hipStream_t s) {
+    const size_t lds = ((size_t)R * (a.D + a.out[0] / G + a.out[1] + 16)) * sizeof(float);
+    const int s1 = (a.D / 4 + t1 - 1) / t1, s2 = (a.out[0] / G / 4 + t2 - 1) / t2;   // float4 slots per thread
+#define ACT1(GG, T1, T2, S1, S2) DQNX_LAUNCH((k_act_mlp1<R, ACT, GG, T1, T2, S1, S2>), dim3(GG), dim3(kAct1Threads), lds, s, a)
     // the reference's MLP (R:env/custom_env/macro with lane/dqn_config.py:76-84): D -> 256 -> 128
-    if (t1 == 2 && t2 == 4 && s2 <= 16) {
-        if (s1 <= 8) ACT1(2, 4, 8, 16);
-        else if (s1 <= 16) ACT1(2, 4, 16, 16);
-        else if (s1 <= 24) ACT1(2, 4, 24, 16);
-        else if (s1 <= 36) ACT1(2, 4, 36, 16);   // MLP-284: 71 float4 per row over 2 lanes
+    if (G == 1 && t1 == 2 && t2 == 4 && s2 <= 16) {
+        if (s1 <= 8) ACT1(1, 2, 4, 8, 16);
+        else if (s1 <= 16) ACT1(1, 2, 4, 16, 16);
+        else if (s1 <= 24) ACT1(1, 2, 4, 24, 16);
+        else if (s1 <= 36) ACT1(1, 2, 4, 36, 16);   // MLP-284: 71 float4 per row over 2 lanes
+        else return -1;
+    } else if (G == 4 && t1 == 8 && t2 == 4 && s2 <= 4) {   // 64 layer-1 neurons a workgroup
+        if (s1 <= 4) ACT1(4, 8, 4, 4, 4);
+        else if (s1 <= 8) ACT1(4, 8, 4, 8, 4);
+        else if (s1 <= 12) ACT1(4, 8, 4, 12, 4);   // MLP-284: 71 float4 per row over 8 lanes
+        else return -1;
+    } else if (G == 8 && t1 == 16 && t2 == 4 && s2 <= 2) {   // 32 a workgroup
+        if (s1 <= 8) ACT1(8, 16, 4, 8, 2);   // MLP-284: 71 float4 per row over 16 lanes
+        else return -1;
+    } else if (G == 2 && t1 == 4 && t2 == 4 && s2 <= 8) {   // 128 a workgroup
+        if (s1 <= 8) ACT1(2, 4, 4, 8, 8);
+        else if (s1 <= 18) ACT1(2, 4, 4, 18, 8);   // MLP-284: 71 float4 per row over 4 lanes
         else return -1;
     } else {
         return -1;
@@ -562,10 +616,14 @@ template <int R>
 int launch_act_r(const ActArgs& a, hipStream_t s) {
     if constexpr (R <= 2) {   // (4 rows of MLP-284's slices would spill the 256 registers)
         int t1 = 0, t2 = 0;
-        if (a.n <= R && ((uintptr_t)a.obs & 15) == 0 && act1_ok(a, &t1, &t2)) {
-            const int rc = a.act == DQNX_ACT_RELU ? launch_act1<R, DQNX_ACT_RELU>(a, t1, t2, s)
-                                                   : launch_act1<R, DQNX_ACT_ELU>(a, t1, t2, s);
-            if (rc != -1) return rc;
+        // DQNX_ACT1_G: workgroups (CUs) the one-round-trip kernel spreads the weights over (1, 2 or 4)
+        const int kg = route_knob("DQNX_ACT1_G", 4);
+        for (int G : {kg == 1 || kg == 2 || kg == 4 || kg == 8 ? kg : 4, 1}) {
+            if (a.n <= R && ((uintptr_t)a.obs & 15) == 0 && act1_ok(a, G, &t1, &t2)) {
+                const int rc = a.act == DQNX_ACT_RELU ? launch_act1<R, DQNX_ACT_RELU>(a, G, t1, t2, s)
+                                                       : launch_act1<R, DQNX_ACT_ELU>(a, G, t1, t2, s);
+                if (rc != -1) return rc;
+            }
         }
     }
     const dim3 grid((a.out[0] + kActWaves - 1) / kActWaves, (a.n + R - 1) / R);

@@ -183,6 +183,39 @@ def test_gpu_act_host_shared_scratch_across_row_counts(net):
         _check(vals.cpu().numpy(), ref, out)
 
 
+@pytest.mark.parametrize("G", ["1", "2", "4", "8"])
+@pytest.mark.parametrize("head", ["dueling", "linear"])
+@pytest.mark.parametrize("n", [1, 2])
+def test_gpu_act_one_round_trip_kernel_workgroups(monkeypatch, G, head, n):
+    """k_act_mlp1 with its layer-1 neurons over G workgroups (DQNX_ACT1_G; layer-2 shares summed by the
+    last arriving workgroup after a write-through hand-off) against the oracle, through dqnx_act_host
+    (the agent's path, completion word polled) and dqnx_act; repeated calls reuse the arrival ticket."""
+    import ctypes
+
+    from dqn import _capi as C
+    monkeypatch.setenv("DQNX_ACT1_G", G)
+    ospec, espec = O.mlp_spec(284, 8, head), E.mlp_spec(284, 8, head)
+    params = O.reference_init(ospec, 21)
+    flat = _flat(espec, params)
+    desc = espec.to_c()
+    L = C.lib()
+    nb = int(L.dqnx_act_host_scratch_bytes(ctypes.byref(desc), n))
+    scratch = torch.zeros((nb + 15) // 16 * 4, dtype=torch.float32, device="cuda")
+    stream = torch.cuda.current_stream().cuda_stream
+    for rep in range(6):
+        x = np.ascontiguousarray(np.random.default_rng(100 * rep + n).random((n, 284), dtype=np.float32))
+        out = np.full(n, -1, dtype=np.int32)
+        C.check(L.dqnx_act_host(ctypes.byref(desc), flat.data_ptr(), x.ctypes.data, n, out.ctypes.data,
+                                scratch.data_ptr(), scratch.numel() * 4, stream), "act_host")
+        vals = torch.empty(n, 8, dtype=torch.float32, device="cuda")
+        acts = E.act(espec, flat, torch.from_numpy(x).cuda(), vals).cpu().numpy()
+        assert np.array_equal(out, acts), (rep, out, acts)
+        with torch.no_grad():
+            xt = torch.from_numpy(x)
+            ref = (O.advantages(ospec, params, xt) if head == "dueling" else O.q_forward(ospec, params, xt)).numpy()
+        _check(vals.cpu().numpy(), ref, out)
+
+
 @pytest.mark.parametrize("obs_dim,n", [(3000, 3), (3000, 2), (5000, 2), (5000, 1)])
 def test_gpu_act_host_wide_inputs_several_row_groups(obs_dim, n):
     """dqnx_act_host on inputs wider than 2048 / 4096 floats, where a workgroup takes 2 / 1 rows:
