@@ -3297,16 +3297,24 @@ static bool side_fused_ok(const dqnx_engine* e, int base) {
            !inlaunch_prefetch_ok(e, base) && route_knob("DQNX_PF_SIDE_FUSED", 1) != 0;
 }
 
+// Side-stream prefetch (fused plan, k past the forward's sampler workgroup): the pending minibatch
+// always sits in slot 1.  A step first copies slot 1 over the compute slot 0 on the caller's stream
+// (one small launch), then forks the side stream there and draws step t+1 into slot 1 beside its own
+// compute, so the caller's stream never waits on the side stream after the compute: only the next
+// step's copy waits for that draw, which has had the whole step to finish.  (A first version copied at
+// the END of the step on the side stream: two cross-queue hops and two copy launches between the
+// compute and the DP apply launch, ~39 us per step at configs[3]'s weak shard.)
 static int side_fused_prologue(dqnx_engine* e, int base, hipStream_t s) {
     int rc = pf_events(e);
     if (rc) return rc;
-    const std::vector<KStep>& ks0 = steps_for(e, base);   // (slot 0; kernel 0 = the sampler launch)
-    rc = run_graphed(e, 0x80000 | base, s, [&](hipStream_t cs) { return enqueue_range(ks0, 0, 1, cs); });
+    const std::vector<KStep>& ks1 = steps_for(e, base | (1 << 8));   // (kernel 0 = the sampler launch, slot 1)
+    rc = run_graphed(e, 0x80000 | base | (1 << 8), s, [&](hipStream_t cs) { return enqueue_range(ks1, 0, 1, cs); });
     if (rc) return rc;
-    DQNX_HIP_CHECK(hipEventRecord(e->ev_sampled[0], s));
-    e->pf_slot = 0;
+    DQNX_HIP_CHECK(hipEventRecord(e->ev_sampled[1], s));
+    e->pf_slot = 1;
     e->pf_valid = true;
     e->pf_inlaunch = false;
+    e->pf_stream = s;
     return DQNX_OK;
 }
 
@@ -3316,11 +3324,18 @@ static int learn_step_side_fused(dqnx_engine* e, int base, bool prefetch, hipStr
         rc = side_fused_prologue(e, base, s);
         if (rc) return rc;
     }
+    // the pending minibatch (slot 1) over the compute slot, once its draw is done
+    DQNX_HIP_CHECK(hipStreamWaitEvent(s, e->ev_sampled[1], 0));
+    int32_t* idx = at<int32_t>(e, e->off[DQNX_BUF_BATCH_IDX]);
+    int32_t* phys = at<int32_t>(e, e->ws_phys);
+    rc = launch_copy_i32x2(idx, idx + e->Bg, e->Bg, phys, phys + e->Bl, e->Bl, s);
+    if (rc) return rc;
     if (prefetch) {   // step t+1's draw into slot 1, beside this step (after everything enqueued before it)
         DQNX_HIP_CHECK(hipEventRecord(e->fork_ev, s));
         DQNX_HIP_CHECK(hipStreamWaitEvent(e->side_stream, e->fork_ev, 0));
         rc = pf_sample(e, base, 1);
         if (rc) return rc;
+        DQNX_HIP_CHECK(hipEventRecord(e->ev_sampled[1], e->side_stream));
     }
     if (relayout_due(e)) {
         rc = enqueue_relayout(e, s);
@@ -3335,16 +3350,12 @@ static int learn_step_side_fused(dqnx_engine* e, int base, bool prefetch, hipStr
         e->pf_valid = false;
         return DQNX_OK;
     }
-    // slot 1 over slot 0 once this step no longer reads it, then the draw joins the step
-    DQNX_HIP_CHECK(hipEventRecord(e->ev_computed[0], s));
-    DQNX_HIP_CHECK(hipStreamWaitEvent(e->side_stream, e->ev_computed[0], 0));
-    int32_t* idx = at<int32_t>(e, e->off[DQNX_BUF_BATCH_IDX]);
-    int32_t* phys = at<int32_t>(e, e->ws_phys);
-    DQNX_HIP_CHECK(hipMemcpyAsync(idx, idx + e->Bg, (size_t)e->Bg * 4, hipMemcpyDeviceToDevice, e->side_stream));
-    DQNX_HIP_CHECK(hipMemcpyAsync(phys, phys + e->Bl, (size_t)e->Bl * 4, hipMemcpyDeviceToDevice, e->side_stream));
-    DQNX_HIP_CHECK(hipEventRecord(e->ev_sampled[0], e->side_stream));
-    DQNX_HIP_CHECK(hipStreamWaitEvent(s, e->ev_sampled[0], 0));
-    e->pf_slot = 0;
+    // a captured graph may not end with the side draw unjoined: join it at the step's end there
+    // (eager steps leave it running into the next step's copy)
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    DQNX_HIP_CHECK(hipStreamIsCapturing(s, &cs));
+    if (cs == hipStreamCaptureStatusActive) DQNX_HIP_CHECK(hipStreamWaitEvent(s, e->ev_sampled[1], 0));
+    e->pf_slot = 1;
     e->pf_stream = s;
     return DQNX_OK;
 }

@@ -1335,6 +1335,24 @@ int launch_dw_adam16(const DwAdam16Args& a, hipStream_t s) {
     return DQNX_OK;
 }
 
+// two int32 arrays copied in one launch (the side-stream prefetch's staged minibatch over the compute
+// slot: the sampled positions and their ring slots)
+__global__ __launch_bounds__(256) void k_copy_i32x2(int32_t* __restrict__ d0, const int32_t* __restrict__ s0, int n0,
+                                                    int32_t* __restrict__ d1, const int32_t* __restrict__ s1, int n1) {
+    for (int i = blockIdx.x * 256 + threadIdx.x; i < n0 + n1; i += gridDim.x * 256) {
+        if (i < n0) d0[i] = s0[i];
+        else d1[i - n0] = s1[i - n0];
+    }
+}
+int launch_copy_i32x2(int32_t* d0, const int32_t* s0, int n0, int32_t* d1, const int32_t* s1, int n1, hipStream_t s) {
+    const int n = n0 + n1;
+    if (n <= 0) return DQNX_OK;
+    const int blocks = std::min((n + 255) / 256, 256);
+    DQNX_LAUNCH(k_copy_i32x2, dim3(blocks), dim3(256), 0, s, d0, s0, n0, d1, s1, n1);
+    DQNX_HIP_CHECK(hipGetLastError());
+    return DQNX_OK;
+}
+
 __global__ void k_soft_update(float* __restrict__ target, const float* __restrict__ p, int64_t n, float tau,
                               float omt) {
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;

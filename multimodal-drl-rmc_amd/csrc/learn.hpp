@@ -815,6 +815,7 @@ int act_rows_per_block(int n, int ld);
 uint64_t act_scratch_bytes(int n, int h0, int ld, int L, int out1);
 int launch_act(const ActArgs& a, hipStream_t s);
 int launch_soft_update(float* target, const float* p, int64_t n, float tau, float omt, hipStream_t s);
+int launch_copy_i32x2(int32_t* d0, const int32_t* s0, int n0, int32_t* d1, const int32_t* s1, int n1, hipStream_t s);
 int launch_replay_push(const PushArgs& a, hipStream_t s);
 
 int launch_sample_uniform(const SampleArgs& a, hipStream_t s);
