@@ -778,16 +778,18 @@ def weak_projection(args, spec, device, t1_us, W=8, rows=4096):
     for _ in range(max(2, args.warmup // 2)):
         shard_step(prefetch=False)
     el_seq = timed_steps(lambda: shard_step(prefetch=False), steps, None, device)
+    el_g, gs = graphed_shard_steps(eng, args, steps, device)   # as GraphedDPStep replays it under torchrun
     ks = kernel_times(eng, C.STEP_GRADS_ONLY, count=30, reps=3)
     samp = next((k for k in ks if k[0].startswith("sample")), None)
     samp_ev = kernel_event_us(eng, C.STEP_GRADS_ONLY, samp[0], count=50) if samp else None
     kpf = kernel_times(eng, C.STEP_GRADS_ONLY | C.STEP_PREFETCH, count=30, reps=3) if args.prefetch else []
     del eng
     torch.cuda.empty_cache()
-    shard_pf, shard_seq = el_pf / steps * 1e6, el_seq / steps * 1e6
-    shard = min(shard_pf, shard_seq)
+    shard_pf, shard_seq, shard_g = el_pf / steps * 1e6, el_seq / steps * 1e6, el_g / steps * 1e6
+    shard = min(shard_pf, shard_seq, shard_g)
     return {"rows_per_rank": rows, "global_batch": Bg, "world": W,
             "shard_step_us": shard, "shard_step_us_prefetch": shard_pf, "shard_step_us_sampler_launch": shard_seq,
+            "shard_step_us_graphed": shard_g, "graph_steps": gs,
             "one_gpu_step_us_4096": t1_us,
             "sampler": {"kernel": samp[0] if samp else None, "k": Bg,
                         "route": sampler_route(Bg, args.capacity),

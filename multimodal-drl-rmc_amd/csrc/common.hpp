@@ -127,7 +127,7 @@ KernelTimer& kernel_timer();   // thread-local (engine.cpp)
 #define DQNX_LAUNCH(K, G, B, SH, S, ...)                                                         \
     do {                                                                                         \
         dqnx::KernelTimer& _kt = dqnx::kernel_timer();                                           \
-        if (_kt.start) {                                                                         \
+        if (_kt.start || _kt.stop) {                                                             \
             const hipEvent_t _e0 = _kt.start, _e1 = _kt.stop;                                    \
             _kt.start = _kt.stop = nullptr;                                                      \
             hipExtLaunchKernelGGL(K, dim3(G), dim3(B), (std::uint32_t)(SH), S, _e0, _e1, 0u, __VA_ARGS__); \

@@ -2511,7 +2511,7 @@ int enqueue_apply(dqnx_engine* e, int flags, hipStream_t s) {
             da.pprop = pua;
             da.pprop_wgs = (e->Bg + 511) / 512;
         }
-        if (e->mtc_blocks > 0 && !prop_in_adam) {   // the next step's in-forward draw reads its MT blocks from the cache
+        if (e->mtc_blocks > 0 && !prop_in_adam && (flags & 0x400)) {   // the next step's in-forward draw reads its MT blocks from the cache
             da.mtc = at<uint32_t>(e, e->ws_mtc);
             da.mtc_blocks = e->mtc_blocks;
         }
@@ -3328,22 +3328,51 @@ static int learn_step_side_fused(dqnx_engine* e, int base, bool prefetch, hipStr
     DQNX_HIP_CHECK(hipStreamWaitEvent(s, e->ev_sampled[1], 0));
     int32_t* idx = at<int32_t>(e, e->off[DQNX_BUF_BATCH_IDX]);
     int32_t* phys = at<int32_t>(e, e->ws_phys);
-    rc = launch_copy_i32x2(idx, idx + e->Bg, e->Bg, phys, phys + e->Bl, e->Bl, s);
-    if (rc) return rc;
-    if (prefetch) {   // step t+1's draw into slot 1, beside this step (after everything enqueued before it)
+    if (relayout_due(e)) {   // (an apply with a draw pending rewrites the blocked copies itself)
+        rc = enqueue_relayout(e, s);
+        if (rc) return rc;
+        e->wblk_dirty = false;
+    }
+    // the copy and this step's compute launches as one graph (a separate copy launch ahead of the
+    // graph measured a ~7 us hop between them); step t+1's draw forks once the copy has read slot 1
+    const std::vector<KStep>& ks = steps_for(e, base);
+    const int key = base | 0x20000 | 0x10000000;
+    auto copy = [&](hipStream_t cs) { return launch_copy_i32x2(idx, idx + e->Bg, e->Bg, phys, phys + e->Bl, e->Bl, cs); };
+    hipStreamCaptureStatus cst = hipStreamCaptureStatusNone;
+    DQNX_HIP_CHECK(hipStreamIsCapturing(s, &cst));
+    if (prefetch && cst == hipStreamCaptureStatusNone && route_knob("DQNX_SIDE_EXTEV", 1) != 0) {
+        // eager: the fork and the draw's completion recorded by the copy's and the sampler's own
+        // dispatches (hipExtLaunchKernelGGL's stop event) -- no marker packet of their own
+        KernelTimer& kt = kernel_timer();
+        kt.start = nullptr;
+        kt.stop = e->fork_ev;
+        rc = copy(s);
+        kt.stop = nullptr;
+        if (rc) return rc;
+        DQNX_HIP_CHECK(hipStreamWaitEvent(e->side_stream, e->fork_ev, 0));
+        kt.stop = e->ev_sampled[1];
+        rc = enqueue_range(steps_for(e, base | (1 << 8)), 0, 1, e->side_stream);
+        kt.stop = nullptr;
+        if (rc) return rc;
+        rc = run_graphed(e, key, s, [&](hipStream_t cs) { return enqueue_range(ks, 1, (int)ks.size(), cs); });
+    } else if (prefetch) {
+        rc = run_graphed(e, key | 0x8000000, s, copy);
+        if (rc) return rc;
         DQNX_HIP_CHECK(hipEventRecord(e->fork_ev, s));
         DQNX_HIP_CHECK(hipStreamWaitEvent(e->side_stream, e->fork_ev, 0));
         rc = pf_sample(e, base, 1);
         if (rc) return rc;
         DQNX_HIP_CHECK(hipEventRecord(e->ev_sampled[1], e->side_stream));
+        if (route_knob("DQNX_SIDE_GRAPH", 1) != 0)
+            rc = run_graphed(e, key, s, [&](hipStream_t cs) { return enqueue_range(ks, 1, (int)ks.size(), cs); });
+        else
+            rc = enqueue_range(ks, 1, (int)ks.size(), s);
+    } else {
+        rc = run_graphed(e, key | 0x4000000, s, [&](hipStream_t cs) {
+            int r = copy(cs);
+            return r ? r : enqueue_range(ks, 1, (int)ks.size(), cs);
+        });
     }
-    if (relayout_due(e)) {
-        rc = enqueue_relayout(e, s);
-        if (rc) return rc;
-        e->wblk_dirty = false;
-    }
-    const std::vector<KStep>& ks = steps_for(e, base);
-    rc = run_graphed(e, base | 0x20000, s, [&](hipStream_t cs) { return enqueue_range(ks, 1, (int)ks.size(), cs); });
     if (rc) return rc;
     if (!blk_kept(e, base)) e->wblk_dirty = true;
     if (!prefetch) {   // consumed the pending minibatch; nothing drawn ahead
@@ -3624,8 +3653,9 @@ int dqnx_apply_grads(dqnx_engine* e, int32_t flags, void* stream) {
     // with an in-launch prefetch pending the next step has no sampler launch: this pass writes the
     // fused plan's blocked copies itself (measured 2.4-2.6 us per DP shard step faster than a
     // relayout launch); otherwise the next sampler launch rebuilds them for free
-    const bool keep = e->bwd_plan == 2 && e->pf_valid && e->pf_inlaunch;
-    const int key = 0x100 | (flags & DQNX_STEP_SOFT_UPDATE) | (keep ? 0x200 : 0);
+    // (the side-stream pipeline too: its next step has no sampler launch on the compute stream)
+    const bool keep = e->bwd_plan == 2 && e->pf_valid && (e->pf_inlaunch || route_knob("DQNX_SIDE_APPLY_KEEP", 1) != 0);
+    const int key = 0x100 | (flags & DQNX_STEP_SOFT_UPDATE) | (keep ? 0x200 : 0) | (keep && e->pf_inlaunch ? 0x400 : 0);
     const int rc2 = run_graphed(e, key, (hipStream_t)stream, [&](hipStream_t s) { return enqueue_apply(e, key, s); });
     if (rc2) return rc2;
     e->perm_dirty = true;   // (mode 2: the conv weights change without their permuted copies)
