@@ -3307,9 +3307,12 @@ static bool side_fused_ok(const dqnx_engine* e, int base) {
 static int side_fused_prologue(dqnx_engine* e, int base, hipStream_t s) {
     int rc = pf_events(e);
     if (rc) return rc;
-    const std::vector<KStep>& ks1 = steps_for(e, base | (1 << 8));   // (kernel 0 = the sampler launch, slot 1)
-    rc = run_graphed(e, 0x80000 | base | (1 << 8), s, [&](hipStream_t cs) { return enqueue_range(ks1, 0, 1, cs); });
+    // (kernel 0 = the sampler launch, slot 1; its spare workgroups rebuild stale blocked copies)
+    const int key1 = base | (1 << 8) | (relayout_due(e) ? KEY_RELAYOUT : 0);
+    const std::vector<KStep>& ks1 = steps_for(e, key1);
+    rc = run_graphed(e, 0x80000 | key1, s, [&](hipStream_t cs) { return enqueue_range(ks1, 0, 1, cs); });
     if (rc) return rc;
+    if (key1 & KEY_RELAYOUT) e->wblk_dirty = false;
     DQNX_HIP_CHECK(hipEventRecord(e->ev_sampled[1], s));
     e->pf_slot = 1;
     e->pf_valid = true;
@@ -3379,11 +3382,11 @@ static int learn_step_side_fused(dqnx_engine* e, int base, bool prefetch, hipStr
         e->pf_valid = false;
         return DQNX_OK;
     }
-    // a captured graph may not end with the side draw unjoined: join it at the step's end there
-    // (eager steps leave it running into the next step's copy)
-    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-    DQNX_HIP_CHECK(hipStreamIsCapturing(s, &cs));
-    if (cs == hipStreamCaptureStatusActive) DQNX_HIP_CHECK(hipStreamWaitEvent(s, e->ev_sampled[1], 0));
+    // a captured graph may not end with the side draw unjoined: join it at the step's end there, after
+    // the Adam pass (GRADS_ONLY: at the end of dqnx_apply_grads) -- the same graph edges as leaving it
+    // to the next step's copy, whose wait the join then duplicates; eager steps leave it running
+    if (cst == hipStreamCaptureStatusActive && !(base & DQNX_STEP_GRADS_ONLY))
+        DQNX_HIP_CHECK(hipStreamWaitEvent(s, e->ev_sampled[1], 0));
     e->pf_slot = 1;
     e->pf_stream = s;
     return DQNX_OK;
@@ -3658,6 +3661,11 @@ int dqnx_apply_grads(dqnx_engine* e, int32_t flags, void* stream) {
     const int key = 0x100 | (flags & DQNX_STEP_SOFT_UPDATE) | (keep ? 0x200 : 0) | (keep && e->pf_inlaunch ? 0x400 : 0);
     const int rc2 = run_graphed(e, key, (hipStream_t)stream, [&](hipStream_t s) { return enqueue_apply(e, key, s); });
     if (rc2) return rc2;
+    if (e->bwd_plan == 2 && e->pf_valid && !e->pf_inlaunch && e->side_stream) {   // (learn_step_side_fused: the captured join)
+        hipStreamCaptureStatus cst = hipStreamCaptureStatusNone;
+        DQNX_HIP_CHECK(hipStreamIsCapturing((hipStream_t)stream, &cst));
+        if (cst == hipStreamCaptureStatusActive) DQNX_HIP_CHECK(hipStreamWaitEvent((hipStream_t)stream, e->ev_sampled[1], 0));
+    }
     e->perm_dirty = true;   // (mode 2: the conv weights change without their permuted copies)
     if (keep) e->wblk_dirty = false;                          // every blocked copy rewritten from the new weights
     else if (!adam_keeps_blk(e)) e->wblk_dirty = true;        // this Adam pass leaves the blocked copies behind
