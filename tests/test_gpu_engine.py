@@ -680,15 +680,21 @@ def test_gpu_apply_grads_tiles_bit_identical(monkeypatch, world, k):
 
 
 
-@pytest.mark.parametrize("batch,world,cap,graph_steps", [(8192, 1, 30000, 0), (32768, 8, 300000, 0),
-                                                          (32768, 8, 300000, 3)])
-def test_gpu_side_prefetch_bit_identical(batch, world, cap, graph_steps):
+@pytest.mark.parametrize("batch,world,cap,graph_steps,knobs", [
+    (8192, 1, 30000, 0, ""), (32768, 8, 300000, 0, ""), (32768, 8, 300000, 3, ""),
+    # the side pipeline's alternative routes: fork / draw-done as marker packets (+ the compute
+    # launches eager), and the apply leaving the blocked copies to a relayout launch
+    (32768, 8, 300000, 0, "DQNX_SIDE_EXTEV=0"), (32768, 8, 300000, 0, "DQNX_SIDE_EXTEV=0,DQNX_SIDE_GRAPH=0"),
+    (32768, 8, 300000, 0, "DQNX_SIDE_APPLY_KEEP=0"), (8192, 1, 30000, 0, "DQNX_SIDE_APPLY_KEEP=0")])
+def test_gpu_side_prefetch_bit_identical(batch, world, cap, graph_steps, knobs, monkeypatch):
     """The fused plan's side-stream prefetch (k beyond the forward's sampler workgroup: step t+1's
     random.sample drawn on the engine's side stream beside step t, then copied over the compute slot):
     bitwise the same weights, target, RNG state and minibatch as sequential steps -- one GPU at B = 8192,
     and rank 0 of world 8 at configs[3]'s weak-scaling global 32768 (the LDS-bitmap sampler), eager and
     as a captured graph of an odd number of steps.  R:dqn/replay_memory.py:38-39, R:dqn/agent.py:204-226."""
     from dqn import data_parallel as DP
+    for kv in filter(None, knobs.split(",")):
+        monkeypatch.setenv(*kv.split("="))
     E = _engine_mod()
     spec = E.mlp_spec(284, 8, "dueling")
     data = O.synth_transitions(cap, 284, 8, seed=3)
