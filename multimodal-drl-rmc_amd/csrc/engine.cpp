@@ -3292,9 +3292,14 @@ static int learn_step_inlaunch(dqnx_engine* e, int base, bool prefetch, hipStrea
 // of them) is self-contained, the draw hidden under the step's compute.  The blocked weight copies (no
 // sampler launch in the step to rebuild them) are rebuilt on the caller's stream when stale.  Bitwise
 // equal to sequential steps (test_gpu_side_prefetch_bit_identical).
+// Only for draws long enough to pay for the pipeline (a copy launch, a cross-queue wait and the draw's
+// workgroup slowing the forward beside it): rank 0's weak shard (4096 rows) replayed as GraphedDPStep
+// replays it measured 117.5 us drawn ahead vs 111.7 us with the draw as its own launch at k = 8192,
+// 116.9 vs 117.4 at 16384, 117.7 vs 145.2 at 32768.
 static bool side_fused_ok(const dqnx_engine* e, int base) {
     return e->bwd_plan == 2 && e->cfg.algo != DQNX_ALGO_PER_DOUBLE && !(base & DQNX_STEP_GIVEN_INDICES) &&
-           !inlaunch_prefetch_ok(e, base) && route_knob("DQNX_PF_SIDE_FUSED", 1) != 0;
+           !inlaunch_prefetch_ok(e, base) && route_knob("DQNX_PF_SIDE_FUSED", 1) != 0 &&
+           e->Bs > route_knob("DQNX_PF_SIDE_MIN_K", 8192);
 }
 
 // Side-stream prefetch (fused plan, k past the forward's sampler workgroup): the pending minibatch

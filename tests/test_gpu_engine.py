@@ -681,11 +681,12 @@ def test_gpu_apply_grads_tiles_bit_identical(monkeypatch, world, k):
 
 
 @pytest.mark.parametrize("batch,world,cap,graph_steps,knobs", [
-    (8192, 1, 30000, 0, ""), (32768, 8, 300000, 0, ""), (32768, 8, 300000, 3, ""),
+    (8192, 1, 30000, 0, "DQNX_PF_SIDE_MIN_K=0"), (32768, 8, 300000, 0, ""), (32768, 8, 300000, 3, ""),
     # the side pipeline's alternative routes: fork / draw-done as marker packets (+ the compute
     # launches eager), and the apply leaving the blocked copies to a relayout launch
     (32768, 8, 300000, 0, "DQNX_SIDE_EXTEV=0"), (32768, 8, 300000, 0, "DQNX_SIDE_EXTEV=0,DQNX_SIDE_GRAPH=0"),
-    (32768, 8, 300000, 0, "DQNX_SIDE_APPLY_KEEP=0"), (8192, 1, 30000, 0, "DQNX_SIDE_APPLY_KEEP=0")])
+    (32768, 8, 300000, 0, "DQNX_SIDE_APPLY_KEEP=0"), (8192, 1, 30000, 0, "DQNX_SIDE_APPLY_KEEP=0,DQNX_PF_SIDE_MIN_K=0"),
+    (16384, 4, 300000, 0, ""), (8192, 2, 300000, 0, "")])   # (k = 8192: the draw as its own launch)
 def test_gpu_side_prefetch_bit_identical(batch, world, cap, graph_steps, knobs, monkeypatch):
     """The fused plan's side-stream prefetch (k beyond the forward's sampler workgroup: step t+1's
     random.sample drawn on the engine's side stream beside step t, then copied over the compute slot):
