@@ -22,8 +22,9 @@ torch.cuda.set_device(dev)
 dist.init_process_group("nccl", device_id=dev)
 args = bench.parse()
 spec = bench.make_spec(args)
-eng = bench.make_engine(args, spec, 32768, 8, 0, dev)
-out = {}
+W = int(os.environ.get("PROBE_W", "8"))   # world size of the engine (4096 rows per rank)
+eng = bench.make_engine(args, spec, 4096 * W, W, 0, dev)
+out = {"world": W}
 for _ in range(10):
     dp_learn_step(eng, soft_update=True, prefetch=True)
 el = bench.timed_steps(lambda: dp_learn_step(eng, soft_update=True, prefetch=True), args.steps, dist, dev)
